@@ -1,0 +1,311 @@
+"""Benchmark: device-resident checksum + framing of Reliable-UDP packet batches.
+
+Contract (see DESIGN.md "Measurement"): `python bench.py --gpus N --steps K
+--warmup W`; for N > 1 launched by torch.distributed.run, one rank per GPU.
+A step is one rudp_encode launch over one batch of synthetic packets already
+resident in HBM (default: 1M x 1472 B per GPU, layout rudp7, the workload of
+BASELINE.json's 70%-of-roofline target).  Packet batches shard by slicing the
+packet array: each rank generates and frames its own slice,
+no collective touches the data path (scaling "weak": fixed work per GPU).
+Rank 0 prints one JSON line.
+
+Measured beside the headline (rank 0, N = 1 only): the other BASELINE
+shapes as "legs" (1M x 1024, 1M x 64, decode-verify, C4 encode->decode round
+trip, host-memory end to end), a device-to-device copy ceiling, and the
+reference algorithm's CPU path (the oracle's bit-string port of
+utils/packet.py) on a bounded sample on the host cores.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent
+sys.path.insert(0, str(REPO))
+sys.path.insert(0, str(REPO / "reliable-udp_amd"))
+
+HBM_PEAK_GBS = 8000.0      # MI355X HBM3E peak, MI355X_MICROARCH.md
+GIB = float(1 << 30)
+SEEDS = {1024: 0x5EED0002, 64: 0x5EED0003, 1472: 0x5EED0004}
+
+
+def algorithmic_bytes_encode(L: int) -> int:
+    """Per packet: read L payload + 5 header-table bytes, write L + 2 + 5."""
+    return 2 * L + 12
+
+
+def algorithmic_bytes_decode(L: int, H: int = 7) -> int:
+    """Per packet, zero-copy decode-verify: read L + H, write seq/ack/flags/ok = 6."""
+    return L + H + 6
+
+
+# ------------------------------------------------------------- CPU baseline
+def _cpu_worker(args):
+    seed, first, n, L = args
+    from oracle import bitstring_packet as bp
+    from oracle import codec_np, synth
+    seq, ack, flags, pay = synth.synth(seed, first, n, L)
+    _, csum = codec_np.encode(seq, ack, flags, pay, 5)
+    rows = [(int(seq[i]), int(ack[i]), int(flags[i]), pay[i].tobytes(), int(csum[i])) for i in range(n)]
+    t0 = time.perf_counter()
+    for s, a, f, p, c in rows:
+        bp.encode_like_reference(s, a, f, p, csum=c)
+    return n * L, time.perf_counter() - t0
+
+
+def cpu_baseline(L: int, per_worker: int, workers: int):
+    """Reference algorithm (bit-string port, rudp7 encode) on the host cores."""
+    import multiprocessing as mp
+    seed = SEEDS.get(L, 0x5EED0004)
+    ctx = mp.get_context("fork")  # before any HIP call in this process
+    tasks = [(seed, w * per_worker, per_worker, L) for w in range(workers)]
+    with ctx.Pool(workers) as pool:
+        res = pool.map(_cpu_worker, tasks)
+    single = _cpu_worker((seed, 0, max(per_worker // 4, 256), L))
+    total = sum(b for b, _ in res)
+    wall = max(t for _, t in res)
+    return {
+        "value": total / wall / GIB,
+        "unit": "GiB/s",
+        "cores": workers,
+        "kind": "port",
+        "sample": f"{workers} workers x {per_worker} packets x {L} B, rudp7 encode through "
+                  f"oracle/bitstring_packet.py (utils/packet.py algorithm), payload GiB/s",
+        "single_core_value": single[0] / single[1] / GIB,
+        "single_core_us_per_packet": single[1] / max(per_worker // 4, 256) * 1e6,
+        "cpu_model": _cpu_model(),
+        "os_cpu_count": os.cpu_count(),
+    }
+
+
+def _cpu_model() -> str:
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+# ------------------------------------------------------------- GPU helpers
+class Workload:
+    """Input/output buffer sets for one batch shape, rotated so the working
+    set exceeds the 256 MiB Infinity Cache (SURVEY.md §7 hard part 4)."""
+
+    def __init__(self, torch, batch, n, L, layout, first, seed, device, min_bytes=1 << 30):
+        H = batch.layout_header_len(layout)
+        set_bytes = n * (2 * L + H + 5)
+        self.sets = []
+        nsets = max(1, min(8, math.ceil(min_bytes / max(set_bytes, 1))))
+        for k in range(nsets):
+            tab, pay = batch.synth_batch(n, L, seed, first_index=first, device=device)
+            out = torch.empty((n, L + H), dtype=torch.uint8, device=device)
+            self.sets.append((tab, pay, out))
+        self.n, self.L, self.H, self.layout = n, L, H, layout
+
+    def encode(self, batch, i):
+        tab, pay, out = self.sets[i % len(self.sets)]
+        batch.pack_batch(tab, pay, self.layout, out=out, want_csum=False)
+
+    def decode(self, batch, i):
+        _, _, out = self.sets[i % len(self.sets)]
+        return batch.unpack_batch(out, self.layout)
+
+
+def time_loop(torch, fn, steps, warmup):
+    """HIP-event time of `steps` back-to-back calls on the current stream (ms)."""
+    for i in range(warmup):
+        fn(i)
+    torch.cuda.synchronize()
+    start = torch.cuda.Event(enable_timing=True)
+    stop = torch.cuda.Event(enable_timing=True)
+    start.record()
+    for i in range(steps):
+        fn(warmup + i)
+    stop.record()
+    stop.synchronize()
+    return start.elapsed_time(stop)
+
+
+def legs(torch, batch, device, steps):
+    out = {}
+    for L in (1024, 64):
+        w = Workload(torch, batch, 1 << 20, L, "rudp7", 0, SEEDS[L], device)
+        ms = time_loop(torch, lambda i: w.encode(batch, i), steps, 3) / steps
+        out[f"encode_1Mx{L}"] = {
+            "GiB_s": (1 << 20) * L / (ms / 1e3) / GIB, "ms": ms,
+            "roofline_frac": (1 << 20) * algorithmic_bytes_encode(L) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+            "buffer_sets": len(w.sets)}
+        del w
+    w = Workload(torch, batch, 1 << 20, 1472, "rudp7", 0, SEEDS[1472], device)
+    for i in range(len(w.sets)):
+        w.encode(batch, i)
+    ms = time_loop(torch, lambda i: w.decode(batch, i), steps, 3) / steps
+    out["decode_verify_1Mx1472"] = {
+        "GiB_s": (1 << 20) * 1472 / (ms / 1e3) / GIB, "ms": ms,
+        "roofline_frac": (1 << 20) * algorithmic_bytes_decode(1472) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS}
+
+    def rt(i):
+        w.encode(batch, i)
+        w.decode(batch, i)
+    ms = time_loop(torch, rt, steps, 3) / steps
+    out["roundtrip_1Mx1472"] = {
+        "GiB_s": (1 << 20) * 1472 / (ms / 1e3) / GIB, "ms": ms,
+        "roofline_frac": (1 << 20) * (algorithmic_bytes_encode(1472) + algorithmic_bytes_decode(1472))
+        / (ms / 1e3) / 1e9 / HBM_PEAK_GBS}
+    # device-to-device copy ceiling on the same byte count as one encode
+    a, b = w.sets[0][1], torch.empty_like(w.sets[0][1])
+    ms = time_loop(torch, lambda i: b.copy_(a), steps, 3) / steps
+    out["d2d_copy_ceiling_GBs"] = 2 * a.numel() / (ms / 1e3) / 1e9
+    del w, a, b
+    # end to end from pinned host memory (PCIe-bound)
+    n, L = 1 << 18, 1472
+    tab, pay = batch.synth_batch(n, L, SEEDS[L], device=device)
+    hp = torch.empty((n, L), dtype=torch.uint8, pin_memory=True)
+    hp.copy_(pay)
+    hs = torch.empty((n,), dtype=torch.uint16, pin_memory=True)
+    hs.copy_(tab.seq)
+    ha = torch.empty((n,), dtype=torch.uint16, pin_memory=True)
+    ha.copy_(tab.ack)
+    hf = torch.empty((n,), dtype=torch.uint8, pin_memory=True)
+    hf.copy_(tab.flags)
+    torch.cuda.synchronize()
+    args = ((hs.numpy(), ha.numpy(), hf.numpy()), hp.numpy())
+    batch.pack_batch(*args, "rudp7")
+    t0 = time.perf_counter()
+    reps = 3
+    for _ in range(reps):
+        batch.pack_batch(*args, "rudp7")
+    dt = (time.perf_counter() - t0) / reps
+    out["e2e_host_encode_256Kx1472"] = {"GiB_s": n * L / dt / GIB, "ms": dt * 1e3,
+                                        "note": "pageable numpy out, pinned in"}
+    return out
+
+
+def read_pmc_traffic(L, n):
+    """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
+    path = REPO / "profiles" / "pmc_encode.json"
+    if not path.exists():
+        return None, None
+    d = json.loads(path.read_text())
+    if d.get("L") != L or d.get("n") != n:
+        return None, None
+    return d.get("hbm_bytes_per_launch"), str(path.relative_to(REPO))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
+    ap.add_argument("--payload", type=int, default=1472)
+    ap.add_argument("--layout", default="rudp7", choices=["rudp5", "rudp7"])
+    ap.add_argument("--no-legs", action="store_true")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--cpu-packets", type=int, default=1 << 14, help="packets per CPU worker")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+
+    cpu = None
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        cpu = cpu_baseline(args.payload, args.cpu_packets, args.cpu_workers)
+
+    import torch
+    import torch.distributed as dist
+    from rudp import batch
+
+    torch.cuda.set_device(local_rank)
+    device = torch.device("cuda", local_rank)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=device)
+
+    n, L = args.packets, args.payload
+    seed = SEEDS.get(L, 0x5EED0004)
+    w = Workload(torch, batch, n, L, args.layout, rank * n, seed, device)
+    for i in range(args.warmup):
+        w.encode(batch, i)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    start = torch.cuda.Event(enable_timing=True)
+    stop = torch.cuda.Event(enable_timing=True)
+    t0 = time.perf_counter()
+    start.record()
+    for i in range(args.steps):
+        w.encode(batch, args.warmup + i)
+    stop.record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    wall = time.perf_counter() - t0
+    kernel_ms = start.elapsed_time(stop)
+    t = torch.tensor([wall], dtype=torch.float64, device=device)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall_max = float(t.item())
+
+    extra = legs(torch, batch, device, max(10, args.steps // 2)) if (
+        rank == 0 and world == 1 and not args.no_legs) else None
+
+    if rank == 0:
+        total_payload = world * n * L * args.steps
+        per_launch_s = kernel_ms / 1e3 / args.steps
+        achieved = n * algorithmic_bytes_encode(L) / per_launch_s / 1e9
+        traffic, traffic_src = read_pmc_traffic(L, n)
+        line = {
+            "metric": "GiB/s payload checksummed+framed (device-resident), 1/2/4/8 MI355X",
+            "value": total_payload / wall_max / GIB,
+            "unit": "GiB/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": wall_max / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak",
+            "vs_baseline": None,
+            "dtype": "u8",
+            "data": "synthetic (on-device splitmix64, ASCII payloads)",
+            "config": {
+                "workload": f"rudp_encode {args.layout}: checksum+frame {n} x {L} B packets per GPU "
+                            f"(BASELINE config 4/5 shape), device-resident",
+                "packets_per_gpu": n, "payload_bytes": L, "layout": args.layout,
+                "global_batch": world * n, "parallelism": f"packet-slice x{world}, no collective",
+                "buffer_sets": len(w.sets),
+            },
+            "roofline": {
+                "bound": "hbm",
+                "achieved": achieved,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved / HBM_PEAK_GBS,
+                "traffic": traffic,
+                "algorithmic_bytes_per_launch": n * algorithmic_bytes_encode(L),
+                "kernel_ms_per_launch": per_launch_s * 1e3,
+                "traffic_source": traffic_src,
+            },
+            "cpu_baseline": cpu,
+        }
+        if extra is not None:
+            line["legs"] = extra
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,149 @@
+/*
+ * rudp.h — C ABI of librudp: batched Reliable-UDP wire codec on MI355X (gfx950).
+ *
+ * The reference (reotam5/Reliable-UDP) has no FFI: its boundary is the Python
+ * class `Packet` in utils/packet.py:12-86 plus the module global
+ * `custom_header` (utils/packet.py:3-10), imported by utils/reliableUDP.py:4
+ * and proxy.py:10.  This header is the C boundary a maintainer binds (ctypes
+ * stub in INTEGRATION.md) to move the per-packet work of that class onto the
+ * GPU in batches.  Each entry point names the reference code it replaces.
+ *
+ * Wire format (utils/packet.py:3-10):
+ *   byte 0-1  seq_num, big-endian u16
+ *   byte 2-3  ack_num, big-endian u16
+ *   byte 4    flags: bit7 SYN, bit6 ACK, bit5 FIN, bits4-0 `offset`
+ *   RUDP_LAYOUT_RUDP7 only:
+ *   byte 5-6  checksum, big-endian u16
+ *   then the payload bytes.
+ * Checksum (build-defined; the reference has none): RFC 1071 one's-complement
+ * of the one's-complement sum of the frame taken as big-endian 16-bit words
+ * with the checksum field (rudp7) zero and an odd tail zero-padded.  In the
+ * rudp5 layout the frame carries no checksum field; the value is returned as
+ * a sideband u16 per packet.
+ *
+ * Conventions
+ *  - Buffers are caller-owned; the library never allocates or frees them.
+ *  - Device (d_*) pointers are HIP device memory on `device`; calls are
+ *    asynchronous on `hip_stream` (a hipStream_t, NULL = legacy default).
+ *  - The *_host variants take host pointers and are synchronous.
+ *  - Return 0 on success or a negative code (RUDP_E*); the message for the
+ *    calling thread is available from rudp_last_error().
+ *  - Reentrant and thread-safe: the only global state is a mutex-guarded
+ *    per-device cache of streams and staging buffers used by *_host calls.
+ */
+#ifndef RUDP_H_
+#define RUDP_H_
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RUDP_ABI_VERSION 1
+
+/* Frame layouts: the value is the header length in bytes. */
+#define RUDP_LAYOUT_RUDP5 5 /* reference-exact 5-byte header, checksum sideband */
+#define RUDP_LAYOUT_RUDP7 7 /* {**custom_header, "checksum": 2}, checksum in-band */
+
+/* Per-packet decode status written to d_ok. */
+#define RUDP_OK_BAD_CSUM 0   /* checksum mismatch */
+#define RUDP_OK_GOOD 1       /* checksum verified */
+#define RUDP_OK_SHORT 2      /* frame shorter than the header */
+#define RUDP_OK_UNVERIFIED 3 /* rudp5 decoded without a sideband checksum */
+
+/* Error codes (negative errno values, HIP errors offset by -1000). */
+#define RUDP_EINVAL (-22)
+#define RUDP_ENOMEM (-12)
+#define RUDP_ENOTSUP (-95)
+#define RUDP_EHIP_BASE (-1000) /* returned as RUDP_EHIP_BASE - hipError_t */
+
+/*
+ * A batch of packets to frame: the SoA header table plus payload bytes.
+ * Fixed-length batches: payload is n*payload_len contiguous bytes and
+ * len/payload_off are NULL.  (Variable-length batches are rejected with
+ * RUDP_ENOTSUP in ABI version 1.)
+ *   seq   -> custom_header["seq_num"]  (utils/packet.py:4)
+ *   ack   -> custom_header["ack_num"]  (utils/packet.py:5)
+ *   flags -> header byte 4 verbatim: syn/ack/fin/offset (utils/packet.py:6-9)
+ */
+typedef struct rudp_batch {
+  uint64_t n;
+  uint32_t payload_len;
+  uint32_t reserved;
+  const uint16_t* seq;
+  const uint16_t* ack;
+  const uint8_t* flags;
+  const uint8_t* payload;
+  const uint32_t* len;          /* reserved for variable-length batches */
+  const uint64_t* payload_off;  /* reserved for variable-length batches */
+} rudp_batch;
+
+/*
+ * Frame + checksum a device-resident batch.
+ * Replaces, per packet, the encode sequence of utils/reliableUDP.py:53-61
+ * (Packet(); set_header_field x2..4; set_payload; to_byte) i.e.
+ * utils/packet.py:13-16, :43-57, :60-65, :76-81.
+ * d_frames: n*(payload_len+layout) bytes.  d_csum_or_null: n u16 (rudp5
+ * sideband; for rudp7 it receives a copy of the in-band value).
+ * Fast path when payload_len % 16 == 0, payload_len <= 4096 and both
+ * d_frames and payload are 16-byte aligned; any other shape runs a
+ * byte-granular kernel with identical results.
+ */
+int rudp_encode(const rudp_batch* in, uint8_t* d_frames, uint16_t* d_csum_or_null,
+                int layout, int device, void* hip_stream);
+
+/*
+ * Parse + verify a device-resident batch of fixed-length frames.
+ * Replaces, per packet, utils/reliableUDP.py:118-123 / :67-73
+ * (Packet(data); get_header_field x N; get_payload), i.e.
+ * utils/packet.py:16, :29-40, :68-73.
+ * d_frame_off_or_null must be NULL in ABI version 1 (frames packed at
+ * stride frame_len).  d_csum_in_or_null: rudp5 sideband checksums to verify
+ * (NULL: d_ok = RUDP_OK_UNVERIFIED).  d_csum_out_or_null: the recomputed
+ * checksum per packet.  d_payload_out_or_null: n*(frame_len-layout) bytes,
+ * payloads copied out aligned; NULL = zero-copy (view at frame offset layout).
+ * Frames shorter than the header get d_ok = RUDP_OK_SHORT and the fields
+ * that are present (truncated as utils/packet.py:31 slices them), 0 otherwise.
+ */
+int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
+                uint32_t frame_len, uint64_t n, const uint16_t* d_csum_in_or_null,
+                uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags, uint8_t* d_ok,
+                uint16_t* d_csum_out_or_null, uint8_t* d_payload_out_or_null,
+                int layout, int device, void* hip_stream);
+
+/*
+ * Host-memory conveniences: same semantics, host pointers in and out.
+ * Staged through device buffers in chunks with H2D / kernel / D2H
+ * overlapped on two streams.  Synchronous.  These model the reference's
+ * real boundary, a UDP socket buffer in host memory (utils/reliableUDP.py:61,
+ * :67, :118).
+ */
+int rudp_encode_host(const rudp_batch* h_in, uint8_t* h_frames, uint16_t* h_csum_or_null,
+                     int layout, int device);
+int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
+                     const uint16_t* h_csum_in_or_null, uint16_t* h_seq, uint16_t* h_ack,
+                     uint8_t* h_flags, uint8_t* h_ok, uint16_t* h_csum_out_or_null,
+                     uint8_t* h_payload_out_or_null, int layout, int device);
+
+/*
+ * Deterministic synthetic batch, generated on the device:
+ * packet i (global index first_index + local index) gets
+ *   seq = (isn + i) mod 2^16, isn in [1, 5000]   (utils/reliableUDP.py:41, :54)
+ *   ack = splitmix u16, flags uniform over {00,80,20,A0,40,60}
+ *   payload bytes from splitmix64, masked to 0x00-0x7F when ascii != 0.
+ * The same definition is restated on the CPU in oracle/synth.py.
+ */
+int rudp_synth(uint64_t seed, uint64_t first_index, uint64_t n, uint32_t payload_len,
+               int ascii, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
+               uint8_t* d_payload, int device, void* hip_stream);
+
+int rudp_device_count(int* count);
+const char* rudp_last_error(void);
+int rudp_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RUDP_H_ */

@@ -1,0 +1,355 @@
+// C ABI of librudp (include/rudp.h): argument checking, path selection,
+// kernel launch, and the host-staged pipeline of the *_host variants.
+#include <errno.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <string.h>
+
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/rudp.h"
+#include "internal.hpp"
+
+namespace rudp {
+namespace {
+
+thread_local std::string g_last_error;
+
+int fail(int code, const char* fmt, ...) {
+  char buf[512];
+  va_list ap;
+  va_start(ap, fmt);
+  vsnprintf(buf, sizeof buf, fmt, ap);
+  va_end(ap);
+  g_last_error = buf;
+  return code;
+}
+
+int hip_fail(hipError_t e, const char* what) {
+  return fail(RUDP_EHIP_BASE - (int)e, "%s: %s (hipError %d)", what, hipGetErrorString(e), (int)e);
+}
+
+#define RUDP_HIP(call)                              \
+  do {                                              \
+    hipError_t e_ = (call);                         \
+    if (e_ != hipSuccess) return hip_fail(e_, #call); \
+  } while (0)
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+uint64_t mix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+uint64_t stream64(uint64_t key, uint64_t ctr) { return mix64(key + (ctr + 1ull) * 0x9E3779B97F4A7C15ull); }
+
+bool encode_tile_ok(uint32_t L, const void* payload, const void* frames) {
+  return L >= 16 && L % 16 == 0 && L <= kTileMaxPayload && aligned16(payload) && aligned16(frames);
+}
+
+bool decode_vec_ok(uint32_t F, int layout, const void* frames, const void* payload_out) {
+  if (F < (uint32_t)layout + 16) return false;
+  const uint32_t L = F - (uint32_t)layout;
+  return L % 16 == 0 && aligned16(frames) && (payload_out == nullptr || aligned16(payload_out));
+}
+
+int check_device(int device) {
+  int count = 0;
+  hipError_t e = hipGetDeviceCount(&count);
+  if (e != hipSuccess) return hip_fail(e, "hipGetDeviceCount");
+  if (device < 0 || device >= count)
+    return fail(RUDP_EINVAL, "device %d out of range (%d HIP devices)", device, count);
+  e = hipSetDevice(device);
+  if (e != hipSuccess) return hip_fail(e, "hipSetDevice");
+  return 0;
+}
+
+EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t* csum, int layout) {
+  EncodeTileArgs a{};
+  a.payload = in->payload;
+  a.seq = in->seq;
+  a.ack = in->ack;
+  a.flags = in->flags;
+  a.frames = frames;
+  a.csum = csum;
+  a.n = in->n;
+  a.L = in->payload_len;
+  const uint32_t F = a.L + (uint32_t)layout;
+  if (encode_tile_ok(a.L, in->payload, frames)) {
+    encode_tile_geometry(a.L, &a.T, &a.glog);
+    a.hdr_bytes = ((a.T + 1u) * 8u + 15u) & ~15u;
+    a.invF = ((1ull << 32) + F - 1ull) / F;
+  }
+  return a;
+}
+
+int validate_batch(const rudp_batch* in, const void* frames, int layout) {
+  if (!in) return fail(RUDP_EINVAL, "rudp_encode: batch is NULL");
+  if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
+    return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
+  if (in->len || in->payload_off)
+    return fail(RUDP_ENOTSUP, "variable-length batches are not supported by ABI version %d",
+                RUDP_ABI_VERSION);
+  if ((uint64_t)in->payload_len + (uint64_t)layout > 0xFFFFFFFFull)
+    return fail(RUDP_EINVAL, "payload_len %u too large", in->payload_len);
+  if (in->n == 0) return 0;
+  if (!in->seq || !in->ack || !in->flags || !frames || (in->payload_len && !in->payload))
+    return fail(RUDP_EINVAL, "rudp_encode: NULL buffer for a non-empty batch");
+  return 0;
+}
+
+int validate_decode(const void* frames, const void* frame_off, uint64_t n, const void* seq,
+                    const void* ack, const void* flags, const void* ok, int layout) {
+  if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
+    return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
+  if (frame_off)
+    return fail(RUDP_ENOTSUP, "per-frame offsets are not supported by ABI version %d",
+                RUDP_ABI_VERSION);
+  if (n == 0) return 0;
+  if (!frames || !seq || !ack || !flags || !ok)
+    return fail(RUDP_EINVAL, "rudp_decode: NULL buffer for a non-empty batch");
+  return 0;
+}
+
+// ---- per-device staging cache for the *_host variants ---------------------
+struct DeviceStage {
+  std::mutex mu;
+  bool init = false;
+  hipStream_t stream[2] = {nullptr, nullptr};
+  void* dbuf[2] = {nullptr, nullptr};
+  size_t bytes = 0;
+};
+
+std::mutex g_stage_mu;
+std::vector<DeviceStage*> g_stage;
+
+DeviceStage* stage_for(int device) {
+  std::lock_guard<std::mutex> lk(g_stage_mu);
+  if ((int)g_stage.size() <= device) g_stage.resize(device + 1, nullptr);
+  if (!g_stage[device]) g_stage[device] = new DeviceStage();  // lives for the process
+  return g_stage[device];
+}
+
+int stage_reserve(DeviceStage* st, size_t bytes) {
+  if (!st->init) {
+    for (int i = 0; i < 2; ++i) RUDP_HIP(hipStreamCreateWithFlags(&st->stream[i], hipStreamNonBlocking));
+    st->init = true;
+  }
+  if (st->bytes >= bytes) return 0;
+  for (int i = 0; i < 2; ++i) {
+    if (st->dbuf[i]) RUDP_HIP(hipFree(st->dbuf[i]));
+    st->dbuf[i] = nullptr;
+  }
+  st->bytes = 0;
+  for (int i = 0; i < 2; ++i) {
+    hipError_t e = hipMalloc(&st->dbuf[i], bytes);
+    if (e != hipSuccess) return fail(RUDP_ENOMEM, "staging hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+  }
+  st->bytes = bytes;
+  return 0;
+}
+
+size_t up256(size_t x) { return (x + 255u) & ~size_t(255); }
+
+constexpr uint64_t kStageBytes = 64ull << 20;  // per-slot input+output budget
+
+}  // namespace
+
+void encode_tile_geometry(uint32_t L, uint32_t* T, uint32_t* glog) {
+  uint32_t t = 16384u / L;
+  if (t > 256u) t = 256u;
+  uint32_t p = 16u;
+  while (p * 2u <= t) p *= 2u;  // power of two in [16, 256]
+  *T = p;
+  uint32_t g = 256u / p, lg = 0;
+  while ((1u << lg) < g) ++lg;
+  *glog = lg;
+}
+
+uint32_t decode_group_log2(uint32_t L) {
+  const uint32_t V = L / 16u;
+  uint32_t lg = 0;
+  while (lg < 4 && (2u << lg) <= V) ++lg;  // G = largest power of two <= min(V, 16)
+  return lg;
+}
+
+}  // namespace rudp
+
+using namespace rudp;
+
+extern "C" {
+
+int rudp_abi_version(void) { return RUDP_ABI_VERSION; }
+
+const char* rudp_last_error(void) { return g_last_error.c_str(); }
+
+int rudp_device_count(int* count) {
+  if (!count) return fail(RUDP_EINVAL, "rudp_device_count: NULL");
+  hipError_t e = hipGetDeviceCount(count);
+  if (e != hipSuccess) {
+    *count = 0;
+    return hip_fail(e, "hipGetDeviceCount");
+  }
+  return 0;
+}
+
+int rudp_encode(const rudp_batch* in, uint8_t* d_frames, uint16_t* d_csum_or_null, int layout,
+                int device, void* hip_stream) {
+  int rc = validate_batch(in, d_frames, layout);
+  if (rc || in->n == 0) return rc;
+  if ((rc = check_device(device))) return rc;
+  EncodeTileArgs a = make_encode_args(in, d_frames, d_csum_or_null, layout);
+  rc = launch_encode(a, layout, a.T != 0, (hipStream_t)hip_stream);
+  if (rc) return hip_fail((hipError_t)rc, "encode launch");
+  return 0;
+}
+
+int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, uint32_t frame_len,
+                uint64_t n, const uint16_t* d_csum_in_or_null, uint16_t* d_seq, uint16_t* d_ack,
+                uint8_t* d_flags, uint8_t* d_ok, uint16_t* d_csum_out_or_null,
+                uint8_t* d_payload_out_or_null, int layout, int device, void* hip_stream) {
+  int rc = validate_decode(d_frames, d_frame_off_or_null, n, d_seq, d_ack, d_flags, d_ok, layout);
+  if (rc || n == 0) return rc;
+  if ((rc = check_device(device))) return rc;
+  DecodeArgs a{};
+  a.frames = d_frames;
+  a.csum_in = d_csum_in_or_null;
+  a.seq = d_seq;
+  a.ack = d_ack;
+  a.flags = d_flags;
+  a.ok = d_ok;
+  a.csum_out = d_csum_out_or_null;
+  a.payload_out = frame_len > (uint32_t)layout ? d_payload_out_or_null : nullptr;
+  a.n = n;
+  a.F = frame_len;
+  const bool vec = decode_vec_ok(frame_len, layout, d_frames, a.payload_out);
+  a.glog = vec ? decode_group_log2(frame_len - (uint32_t)layout) : 0;
+  rc = launch_decode(a, layout, vec, (hipStream_t)hip_stream);
+  if (rc) return hip_fail((hipError_t)rc, "decode launch");
+  return 0;
+}
+
+int rudp_synth(uint64_t seed, uint64_t first_index, uint64_t n, uint32_t payload_len, int ascii,
+               uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags, uint8_t* d_payload, int device,
+               void* hip_stream) {
+  if (n == 0) return 0;
+  if (!d_seq || !d_ack || !d_flags || (payload_len && !d_payload))
+    return fail(RUDP_EINVAL, "rudp_synth: NULL buffer");
+  int rc = check_device(device);
+  if (rc) return rc;
+  SynthArgs a{};
+  const uint64_t k0 = stream64(seed, 0), k1 = stream64(seed, 1), k2 = stream64(seed, 2),
+                 k3 = stream64(seed, 3);
+  a.isn = (uint32_t)(1ull + stream64(k0, 0) % 5000ull);
+  a.key_ack = k1;
+  a.key_flags = k2;
+  a.key_payload = k3;
+  a.first = first_index;
+  a.n = n;
+  a.L = payload_len;
+  a.ascii = ascii ? 1u : 0u;
+  a.seq = d_seq;
+  a.ack = d_ack;
+  a.flags = d_flags;
+  a.payload = d_payload;
+  rc = launch_synth(a, (hipStream_t)hip_stream);
+  if (rc) return hip_fail((hipError_t)rc, "synth launch");
+  return 0;
+}
+
+int rudp_encode_host(const rudp_batch* h_in, uint8_t* h_frames, uint16_t* h_csum_or_null,
+                     int layout, int device) {
+  int rc = validate_batch(h_in, h_frames, layout);
+  if (rc || h_in->n == 0) return rc;
+  if ((rc = check_device(device))) return rc;
+  const uint64_t n = h_in->n;
+  const uint64_t L = h_in->payload_len;
+  const uint64_t F = L + (uint64_t)layout;
+  uint64_t cn = kStageBytes / (L + F + 8);
+  if (cn < 64) cn = 64;
+  if (cn > n) cn = n;
+  // Slot layout: payload | frames | seq | ack | flags | csum.
+  const size_t o_pay = 0, o_fr = up256(cn * L), o_seq = o_fr + up256(cn * F),
+               o_ack = o_seq + up256(cn * 2), o_fl = o_ack + up256(cn * 2),
+               o_cs = o_fl + up256(cn), slot = o_cs + up256(cn * 2);
+  DeviceStage* st = stage_for(device);
+  std::lock_guard<std::mutex> lk(st->mu);
+  if ((rc = stage_reserve(st, slot))) return rc;
+  for (uint64_t p0 = 0, k = 0; p0 < n; p0 += cn, ++k) {
+    const uint64_t m = (n - p0) < cn ? (n - p0) : cn;
+    const int b = (int)(k & 1);
+    hipStream_t s = st->stream[b];
+    char* base = (char*)st->dbuf[b];
+    if (L) RUDP_HIP(hipMemcpyAsync(base + o_pay, h_in->payload + p0 * L, m * L, hipMemcpyHostToDevice, s));
+    RUDP_HIP(hipMemcpyAsync(base + o_seq, h_in->seq + p0, m * 2, hipMemcpyHostToDevice, s));
+    RUDP_HIP(hipMemcpyAsync(base + o_ack, h_in->ack + p0, m * 2, hipMemcpyHostToDevice, s));
+    RUDP_HIP(hipMemcpyAsync(base + o_fl, h_in->flags + p0, m, hipMemcpyHostToDevice, s));
+    rudp_batch sub = *h_in;
+    sub.n = m;
+    sub.seq = (const uint16_t*)(base + o_seq);
+    sub.ack = (const uint16_t*)(base + o_ack);
+    sub.flags = (const uint8_t*)(base + o_fl);
+    sub.payload = (const uint8_t*)(base + o_pay);
+    uint16_t* dcs = h_csum_or_null ? (uint16_t*)(base + o_cs) : nullptr;
+    if ((rc = rudp_encode(&sub, (uint8_t*)(base + o_fr), dcs, layout, device, s))) return rc;
+    RUDP_HIP(hipMemcpyAsync(h_frames + p0 * F, base + o_fr, m * F, hipMemcpyDeviceToHost, s));
+    if (dcs) RUDP_HIP(hipMemcpyAsync(h_csum_or_null + p0, dcs, m * 2, hipMemcpyDeviceToHost, s));
+  }
+  for (int i = 0; i < 2; ++i) RUDP_HIP(hipStreamSynchronize(st->stream[i]));
+  return 0;
+}
+
+int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
+                     const uint16_t* h_csum_in_or_null, uint16_t* h_seq, uint16_t* h_ack,
+                     uint8_t* h_flags, uint8_t* h_ok, uint16_t* h_csum_out_or_null,
+                     uint8_t* h_payload_out_or_null, int layout, int device) {
+  int rc = validate_decode(h_frames, nullptr, n, h_seq, h_ack, h_flags, h_ok, layout);
+  if (rc || n == 0) return rc;
+  if ((rc = check_device(device))) return rc;
+  const uint64_t F = frame_len;
+  const uint64_t L = F > (uint64_t)layout ? F - (uint64_t)layout : 0;
+  uint8_t* h_pay = L ? h_payload_out_or_null : nullptr;
+  uint64_t cn = kStageBytes / (F + L + 16);
+  if (cn < 64) cn = 64;
+  if (cn > n) cn = n;
+  // Slot layout: frames | payload | seq | ack | flags | ok | csum_in | csum_out.
+  const size_t o_fr = 0, o_pay = up256(cn * F), o_seq = o_pay + up256(cn * L),
+               o_ack = o_seq + up256(cn * 2), o_fl = o_ack + up256(cn * 2),
+               o_ok = o_fl + up256(cn), o_ci = o_ok + up256(cn), o_co = o_ci + up256(cn * 2),
+               slot = o_co + up256(cn * 2);
+  DeviceStage* st = stage_for(device);
+  std::lock_guard<std::mutex> lk(st->mu);
+  if ((rc = stage_reserve(st, slot))) return rc;
+  for (uint64_t p0 = 0, k = 0; p0 < n; p0 += cn, ++k) {
+    const uint64_t m = (n - p0) < cn ? (n - p0) : cn;
+    const int b = (int)(k & 1);
+    hipStream_t s = st->stream[b];
+    char* base = (char*)st->dbuf[b];
+    if (F) RUDP_HIP(hipMemcpyAsync(base + o_fr, h_frames + p0 * F, m * F, hipMemcpyHostToDevice, s));
+    const uint16_t* dci = nullptr;
+    if (h_csum_in_or_null) {
+      RUDP_HIP(hipMemcpyAsync(base + o_ci, h_csum_in_or_null + p0, m * 2, hipMemcpyHostToDevice, s));
+      dci = (const uint16_t*)(base + o_ci);
+    }
+    uint16_t* dco = h_csum_out_or_null ? (uint16_t*)(base + o_co) : nullptr;
+    uint8_t* dpay = h_pay ? (uint8_t*)(base + o_pay) : nullptr;
+    if ((rc = rudp_decode((const uint8_t*)(base + o_fr), nullptr, frame_len, m, dci,
+                          (uint16_t*)(base + o_seq), (uint16_t*)(base + o_ack),
+                          (uint8_t*)(base + o_fl), (uint8_t*)(base + o_ok), dco, dpay, layout,
+                          device, s)))
+      return rc;
+    RUDP_HIP(hipMemcpyAsync(h_seq + p0, base + o_seq, m * 2, hipMemcpyDeviceToHost, s));
+    RUDP_HIP(hipMemcpyAsync(h_ack + p0, base + o_ack, m * 2, hipMemcpyDeviceToHost, s));
+    RUDP_HIP(hipMemcpyAsync(h_flags + p0, base + o_fl, m, hipMemcpyDeviceToHost, s));
+    RUDP_HIP(hipMemcpyAsync(h_ok + p0, base + o_ok, m, hipMemcpyDeviceToHost, s));
+    if (dco) RUDP_HIP(hipMemcpyAsync(h_csum_out_or_null + p0, dco, m * 2, hipMemcpyDeviceToHost, s));
+    if (dpay) RUDP_HIP(hipMemcpyAsync(h_pay + p0 * L, dpay, m * L, hipMemcpyDeviceToHost, s));
+  }
+  for (int i = 0; i < 2; ++i) RUDP_HIP(hipStreamSynchronize(st->stream[i]));
+  return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,108 @@
+// Device-side helpers shared by the gfx950 codec kernels.
+//
+// Checksum arithmetic (RFC 1071):
+//   S = seq + ack + (flags << 8) + sum_m LE16(payload[2m], payload[2m+1])
+// Both layouts put the payload at an ODD frame offset (5 or 7), so a payload
+// byte at even index j lands at an odd frame position and is the LOW byte of
+// its big-endian frame word: the frame-word sum of the payload equals the sum
+// of the payload read as little-endian u16 words — which is what a
+// little-endian dword load gives for free, no byte swap anywhere.  The
+// header words are seq, ack and flags<<8 (the checksum field counts as 0).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rudp {
+
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kBlock = 256;  // 4 waves of 64
+
+// End-around-carry fold of a 32-bit partial sum to 16 bits.
+__device__ __forceinline__ uint32_t fold16(uint32_t s) {
+  s = (s & 0xFFFFu) + (s >> 16);
+  s = (s & 0xFFFFu) + (s >> 16);
+  return s;
+}
+
+// Sum of the eight little-endian u16 halves of a 16-byte vector.
+__device__ __forceinline__ uint32_t le16_sum(u32x4 v) {
+  uint32_t lo = (v.x & 0xFFFFu) + (v.y & 0xFFFFu) + (v.z & 0xFFFFu) + (v.w & 0xFFFFu);
+  uint32_t hi = (v.x >> 16) + (v.y >> 16) + (v.z >> 16) + (v.w >> 16);
+  return lo + hi;
+}
+
+// RFC 1071 checksum of one packet from its payload word sum and header.
+__device__ __forceinline__ uint32_t packet_csum(uint32_t payload_sum, uint32_t seq, uint32_t ack,
+                                                uint32_t flags) {
+  return (~fold16(payload_sum + seq + ack + (flags << 8))) & 0xFFFFu;
+}
+
+// Header bytes in frame order packed little-endian into a u64 (byte p of the
+// frame at bits 8p).  H = 5 leaves the checksum out.
+template <int H>
+__device__ __forceinline__ uint64_t pack_header(uint32_t seq, uint32_t ack, uint32_t flags,
+                                                uint32_t csum) {
+  uint64_t h = (uint64_t)(seq >> 8) | ((uint64_t)(seq & 0xFFu) << 8) |
+               ((uint64_t)(ack >> 8) << 16) | ((uint64_t)(ack & 0xFFu) << 24) |
+               ((uint64_t)(flags & 0xFFu) << 32);
+  if (H == 7) h |= ((uint64_t)(csum >> 8) << 40) | ((uint64_t)(csum & 0xFFu) << 48);
+  return h;
+}
+
+// Mask of bytes [a, b) of an 8-byte word; a and b may lie outside [0, 8].
+__device__ __forceinline__ uint64_t byte_mask(int a, int b) {
+  a = a < 0 ? 0 : a;
+  b = b > 8 ? 8 : b;
+  if (b <= a) return 0ull;
+  uint64_t upto_b = (b >= 8) ? ~0ull : ((1ull << (8 * b)) - 1ull);
+  uint64_t below_a = (a == 0) ? 0ull : ((1ull << (8 * a)) - 1ull);
+  return upto_b & ~below_a;
+}
+
+__device__ __forceinline__ uint64_t lo64(u32x4 v) { return (uint64_t)v.x | ((uint64_t)v.y << 32); }
+__device__ __forceinline__ uint64_t hi64(u32x4 v) { return (uint64_t)v.z | ((uint64_t)v.w << 32); }
+__device__ __forceinline__ u32x4 make_u32x4(uint64_t lo, uint64_t hi) {
+  u32x4 r;
+  r.x = (uint32_t)lo;
+  r.y = (uint32_t)(lo >> 32);
+  r.z = (uint32_t)hi;
+  r.w = (uint32_t)(hi >> 32);
+  return r;
+}
+
+// 16 bytes starting at an arbitrary byte offset of a 4-byte-aligned region,
+// from five aligned dword reads and a byte funnel shift.
+__device__ __forceinline__ u32x4 window16_dw(const uint32_t* base_dw, uint32_t byte_off) {
+  const uint32_t* w = base_dw + (byte_off >> 2);
+  uint32_t sh = byte_off & 3u;
+  uint32_t w0 = w[0], w1 = w[1], w2 = w[2], w3 = w[3], w4 = w[4];
+  u32x4 r;
+  r.x = __builtin_amdgcn_alignbyte(w1, w0, sh);
+  r.y = __builtin_amdgcn_alignbyte(w2, w1, sh);
+  r.z = __builtin_amdgcn_alignbyte(w3, w2, sh);
+  r.w = __builtin_amdgcn_alignbyte(w4, w3, sh);
+  return r;
+}
+
+// 16 bytes from a 32-byte register pair (a = bytes 0-15, b = bytes 16-31)
+// starting at byte `sh` (0..15): dword select then byte funnel.
+__device__ __forceinline__ u32x4 funnel32(u32x4 a, u32x4 b, uint32_t sh) {
+  // s_i = dword (i + sh/4) of a:b as two select levels on plain scalars.  No
+  // array here on purpose: hipcc turns selects between elements of a private
+  // array back into a runtime index and demotes the array to LDS/scratch.
+  const bool two = (sh & 8u) != 0, one = (sh & 4u) != 0;
+  const uint32_t bs = sh & 3u;
+  const uint32_t e0 = two ? a.z : a.x, e1 = two ? a.w : a.y, e2 = two ? b.x : a.z,
+                 e3 = two ? b.y : a.w, e4 = two ? b.z : b.x, e5 = two ? b.w : b.y;
+  const uint32_t s0 = one ? e1 : e0, s1 = one ? e2 : e1, s2 = one ? e3 : e2, s3 = one ? e4 : e3,
+                 s4 = one ? e5 : e4;
+  u32x4 r;
+  r.x = __builtin_amdgcn_alignbyte(s1, s0, bs);
+  r.y = __builtin_amdgcn_alignbyte(s2, s1, bs);
+  r.z = __builtin_amdgcn_alignbyte(s3, s2, bs);
+  r.w = __builtin_amdgcn_alignbyte(s4, s3, bs);
+  return r;
+}
+
+}  // namespace rudp

@@ -1,0 +1,180 @@
+// Batched parse + verify (decode) kernels for gfx950.
+//
+// Replaces the per-packet decode of the reference, utils/reliableUDP.py:118-123
+// and :67-73: Packet(data) (utils/packet.py:16) -> get_header_field seq/ack/
+// syn/ack/fin (:29-40) -> get_payload (:68-73), plus verification of the
+// build-defined RFC 1071 checksum.
+//
+// Fast kernel (payload_len % 16 == 0): G lanes per packet, 256/G packets per
+// workgroup.  Lane g walks the packet's payload in 16-byte windows g, g+G, ...
+// Each window starts at the odd frame offset (p*F + H + 16j); it is read as
+// two aligned dwordx4 loads (the second one is the next lane's first, an L1
+// hit) and funnel-shifted into place in registers.  Every frame byte leaves
+// HBM once.  The window's LE u16 halves feed the packet sum (shfl_xor
+// butterfly over the G lanes); with a payload_out buffer the window is also
+// written out 16-byte aligned.  The group leader parses the header from the
+// frame's first window and writes seq/ack/flags/ok (+ checksum).
+#include "codec_device.hpp"
+#include "internal.hpp"
+
+namespace rudp {
+
+// 16 bytes at frames[off], off 16-byte aligned; bytes at or past `total`
+// read as zero (only the last packets of a batch take the byte path).
+__device__ __forceinline__ u32x4 load16_guarded(const unsigned char* frames, uint64_t off,
+                                                uint64_t total) {
+  if (off + 16 <= total)
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(frames + off));
+  uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+#pragma unroll
+  for (uint32_t b = 0; b < 16; ++b) {
+    const uint32_t v = (off + b < total) ? (uint32_t)frames[off + b] << (8 * (b & 3)) : 0u;
+    if (b < 4) d0 |= v;
+    else if (b < 8) d1 |= v;
+    else if (b < 12) d2 |= v;
+    else d3 |= v;
+  }
+  u32x4 r;
+  r.x = d0;
+  r.y = d1;
+  r.z = d2;
+  r.w = d3;
+  return r;
+}
+
+__device__ __forceinline__ u32x4 window16_global(const unsigned char* frames, uint64_t off,
+                                                 uint64_t total) {
+  const uint64_t al = off & ~15ull;
+  const u32x4 a = load16_guarded(frames, al, total);
+  const u32x4 b = load16_guarded(frames, al + 16, total);
+  return funnel32(a, b, (uint32_t)(off & 15u));
+}
+
+template <int H>
+__device__ __forceinline__ void finish_packet(const DecodeArgs& a, uint64_t p, uint32_t sum,
+                                              uint32_t seq, uint32_t ack, uint32_t flags,
+                                              uint32_t inband) {
+  const uint32_t c = packet_csum(sum, seq, ack, flags);
+  uint8_t ok;
+  if (H == 7)
+    ok = (c == inband) ? 1 : 0;
+  else if (a.csum_in)
+    ok = (c == a.csum_in[p]) ? 1 : 0;
+  else
+    ok = 3;
+  a.seq[p] = (uint16_t)seq;
+  a.ack[p] = (uint16_t)ack;
+  a.flags[p] = (uint8_t)flags;
+  a.ok[p] = ok;
+  if (a.csum_out) a.csum_out[p] = (uint16_t)c;
+}
+
+template <int H>
+__global__ void __launch_bounds__(kBlock) decode_vec_kernel(DecodeArgs a) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t glog = a.glog;
+  const uint32_t G = 1u << glog;
+  const uint32_t q = tid >> glog;
+  const uint32_t g = tid & (G - 1u);
+  const uint64_t p = (uint64_t)blockIdx.x * (kBlock >> glog) + q;
+  const bool valid = p < a.n;
+  const uint32_t F = a.F;
+  const uint32_t L = F - H;
+  const uint32_t V = L >> 4;
+  const uint64_t total = a.n * (uint64_t)F;
+  const uint64_t fbase = p * (uint64_t)F;
+
+  uint32_t sum = 0;
+  if (valid) {
+    for (uint32_t v0 = g; v0 < V; v0 += 4u * G) {
+      u32x4 w[4];
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t v = v0 + (uint32_t)u * G;
+        if (v < V) w[u] = window16_global(a.frames, fbase + H + 16ull * v, total);
+      }
+#pragma unroll
+      for (int u = 0; u < 4; ++u) {
+        const uint32_t v = v0 + (uint32_t)u * G;
+        if (v < V) {
+          sum += le16_sum(w[u]);
+          if (a.payload_out)
+            __builtin_nontemporal_store(
+                w[u], reinterpret_cast<u32x4*>(a.payload_out + p * (uint64_t)L + 16ull * v));
+        }
+      }
+    }
+  }
+  for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
+  if (g == 0 && valid) {
+    const u32x4 h = window16_global(a.frames, fbase, total);
+    const uint32_t seq = ((h.x & 0xFFu) << 8) | ((h.x >> 8) & 0xFFu);
+    const uint32_t ack = (((h.x >> 16) & 0xFFu) << 8) | (h.x >> 24);
+    const uint32_t flags = h.y & 0xFFu;
+    const uint32_t inband = (((h.y >> 8) & 0xFFu) << 8) | ((h.y >> 16) & 0xFFu);
+    finish_packet<H>(a, p, sum, seq, ack, flags, inband);
+  }
+}
+
+// Any frame length: one wave per packet, byte-granular.  Frames shorter
+// than the header report RUDP_OK_SHORT with the fields that are present,
+// truncated the way utils/packet.py:31 slices a short bit string.
+template <int H>
+__global__ void __launch_bounds__(kBlock) decode_bytes_kernel(DecodeArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t p = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (p >= a.n) return;  // wave-uniform
+  const uint32_t F = a.F;
+  const unsigned char* fr = a.frames + p * (uint64_t)F;
+  if (F < (uint32_t)H) {
+    if (lane == 0) {
+      uint32_t b[7] = {0, 0, 0, 0, 0, 0, 0};
+      for (uint32_t i = 0; i < F; ++i) b[i] = fr[i];
+      // A field cut short keeps only its present bytes (bit-string slice).
+      const uint32_t seq = F >= 2 ? (b[0] << 8) | b[1] : b[0];
+      const uint32_t ack = F >= 4 ? (b[2] << 8) | b[3] : b[2];
+      a.seq[p] = (uint16_t)seq;
+      a.ack[p] = (uint16_t)ack;
+      a.flags[p] = (uint8_t)b[4];
+      a.ok[p] = 2;
+      if (a.csum_out) a.csum_out[p] = 0;
+    }
+    return;
+  }
+  const uint32_t L = F - H;
+  uint32_t sum = 0;
+  for (uint32_t j = lane; j < L; j += 64) {
+    const uint32_t b = fr[H + j];
+    sum += (j & 1u) ? (b << 8) : b;
+    if (a.payload_out) a.payload_out[p * (uint64_t)L + j] = (unsigned char)b;
+  }
+  for (int m = 32; m > 0; m >>= 1) sum += __shfl_xor(sum, m, 64);
+  if (lane == 0) {
+    const uint32_t seq = ((uint32_t)fr[0] << 8) | fr[1];
+    const uint32_t ack = ((uint32_t)fr[2] << 8) | fr[3];
+    const uint32_t flags = fr[4];
+    const uint32_t inband = (H == 7) ? (((uint32_t)fr[5] << 8) | fr[6]) : 0u;
+    finish_packet<H>(a, p, sum, seq, ack, flags, inband);
+  }
+}
+
+int launch_decode(const DecodeArgs& args, int layout, bool vec_path, hipStream_t stream) {
+  if (args.n == 0) return 0;
+  if (vec_path) {
+    const uint32_t per_block = kBlock >> args.glog;
+    const uint64_t blocks = (args.n + per_block - 1) / per_block;
+    if (layout == 7)
+      hipLaunchKernelGGL(decode_vec_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+    else
+      hipLaunchKernelGGL(decode_vec_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+  } else {
+    const uint64_t blocks = (args.n + (kBlock / 64) - 1) / (kBlock / 64);
+    if (layout == 7)
+      hipLaunchKernelGGL(decode_bytes_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+    else
+      hipLaunchKernelGGL(decode_bytes_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace rudp

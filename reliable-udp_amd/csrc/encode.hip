@@ -1,0 +1,170 @@
+// Batched frame + checksum (encode) kernels for gfx950.
+//
+// Replaces the per-packet encode of the reference, utils/reliableUDP.py:53-61:
+//   Packet() (utils/packet.py:13-16) -> set_header_field seq/ack/syn/fin
+//   (:43-57) -> set_payload (:60-65) -> to_byte (:76-81)
+// plus the build-defined RFC 1071 checksum.
+//
+// Fast kernel (payload_len % 16 == 0): one workgroup per TILE of T packets,
+// T a multiple of 16 so that the tile's output range T*(L+H) starts and ends
+// 16-byte aligned even though the frame stride L+H is odd.
+//   phase 1  G = 256/T lanes per packet stream the packet's payload in 16 B
+//            vectors (coalesced dwordx4, non-temporal), sum LE u16 halves in
+//            registers, and write the vectors into an LDS tile.  The per
+//            packet sums meet in a shfl_xor butterfly over the G lanes; the
+//            group leader builds the 5/7-byte header (with checksum) in LDS.
+//   phase 2  output-stationary: each lane owns aligned 16 B output chunks,
+//            assembles them from two byte-shifted LDS windows (payload of
+//            packet q and of q+1, which sits H bytes further back) and the
+//            header words, and writes one dwordx4 non-temporal store.
+// HBM traffic = read L + 5 (payload + header table) and write L + H per
+// packet, each byte exactly once.
+#include "codec_device.hpp"
+#include "internal.hpp"
+
+namespace rudp {
+
+constexpr int kLdsGuard = 16;  // bytes before the payload tile (negative offsets)
+
+template <int H>
+__global__ void __launch_bounds__(kBlock) encode_tile_kernel(EncodeTileArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  uint64_t* lds_hdr = reinterpret_cast<uint64_t*>(lds);  // [T + 1]
+  unsigned char* lds_pay = lds + a.hdr_bytes;            // guard + T*L + tail guard
+
+  const uint32_t tid = threadIdx.x;
+  const uint32_t L = a.L;
+  const uint32_t T = a.T;
+  const uint32_t glog = a.glog;
+  const uint32_t G = 1u << glog;
+  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  const uint64_t left = a.n - p0;
+  const uint32_t Tv = left < T ? (uint32_t)left : T;
+
+  // ---- phase 1: payload -> LDS, per-packet LE16 sums --------------------
+  const uint32_t q = tid >> glog;
+  const uint32_t g = tid & (G - 1u);
+  const uint32_t V = L >> 4;  // 16 B vectors per packet
+  uint32_t sum = 0;
+  if (q < Tv) {
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + (p0 + q) * (uint64_t)L);
+    u32x4* dst = reinterpret_cast<u32x4*>(lds_pay + kLdsGuard + q * L);
+    for (uint32_t v0 = g; v0 < V; v0 += 8u * G) {
+      u32x4 r[8];
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        uint32_t v = v0 + (uint32_t)u * G;
+        if (v < V) r[u] = __builtin_nontemporal_load(src + v);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        uint32_t v = v0 + (uint32_t)u * G;
+        if (v < V) {
+          sum += le16_sum(r[u]);
+          dst[v] = r[u];
+        }
+      }
+    }
+  }
+  for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
+  if (g == 0 && q < Tv) {
+    const uint64_t p = p0 + q;
+    const uint32_t s = a.seq[p], k = a.ack[p], f = a.flags[p];
+    const uint32_t c = packet_csum(sum, s, k, f);
+    lds_hdr[q] = pack_header<H>(s, k, f, c);
+    if (a.csum) a.csum[p] = (uint16_t)c;
+  }
+  __syncthreads();
+
+  // ---- phase 2: aligned 16 B output chunks --------------------------------
+  const uint32_t F = L + H;
+  const uint32_t nbytes = Tv * F;
+  unsigned char* out = a.frames + p0 * (uint64_t)F;
+  const uint32_t* pay_dw = reinterpret_cast<const uint32_t*>(lds_pay);
+  for (uint32_t x = tid * 16u; x < nbytes; x += kBlock * 16u) {
+    const uint32_t qq = (uint32_t)(((uint64_t)x * a.invF) >> 32);  // x / F
+    const uint32_t r = x - qq * F;           // frame position of chunk byte 0
+    const int kA0 = r < (uint32_t)H ? H - (int)r : 0;  // first payload byte of qq
+    const int kend = (int)(F - r);           // first byte of packet qq+1
+    // LDS offset (from lds_pay) of byte 0 if it were payload of qq.
+    const uint32_t sA = kLdsGuard + qq * L + r - H;
+    const u32x4 A = window16_dw(pay_dw, sA);
+    uint64_t lo = lo64(A) & byte_mask(kA0, kend);
+    uint64_t hi = hi64(A) & byte_mask(kA0 - 8, kend - 8);
+    if (kA0 > 0) lo |= lds_hdr[qq] >> (8 * r);
+    if (kend < 16) {
+      const u32x4 B = window16_dw(pay_dw, sA - H);
+      lo |= lo64(B) & byte_mask(kend + H, 16);
+      hi |= hi64(B) & byte_mask(kend + H - 8, 8);
+      const uint64_t h1 = lds_hdr[qq + 1];
+      if (kend < 8) {
+        lo |= h1 << (8 * kend);
+        if (kend > 0) hi |= h1 >> (64 - 8 * kend);
+      } else {
+        hi |= h1 << (8 * (kend - 8));
+      }
+    }
+    const u32x4 v = make_u32x4(lo, hi);
+    if (x + 16u <= nbytes) {
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + x));
+    } else {
+      uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (uint32_t b = 0; b < 16; ++b)
+        if (x + b < nbytes) out[x + b] = (unsigned char)(d[b >> 2] >> (8 * (b & 3)));
+    }
+  }
+}
+
+// Any payload length / alignment: one wave per packet, byte-granular.
+// Same arithmetic as the tile kernel; used for reference-sized frames
+// (1-char payloads, utils/reliableUDP.py:11) and ragged shapes.
+template <int H>
+__global__ void __launch_bounds__(kBlock) encode_bytes_kernel(EncodeTileArgs a) {
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint64_t p = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
+  if (p >= a.n) return;  // wave-uniform
+  const uint32_t L = a.L;
+  const uint64_t F = (uint64_t)L + H;
+  const unsigned char* src = a.payload + p * (uint64_t)L;
+  unsigned char* dst = a.frames + p * F;
+  uint32_t sum = 0;
+  for (uint32_t j = lane; j < L; j += 64) {
+    const uint32_t b = src[j];
+    sum += (j & 1u) ? (b << 8) : b;
+    dst[H + j] = (unsigned char)b;
+  }
+  for (int m = 32; m > 0; m >>= 1) sum += __shfl_xor(sum, m, 64);
+  const uint32_t s = a.seq[p], k = a.ack[p], f = a.flags[p];
+  const uint32_t c = packet_csum(sum, s, k, f);
+  const uint64_t h = pack_header<H>(s, k, f, c);
+  if (lane < (uint32_t)H) dst[lane] = (unsigned char)(h >> (8 * lane));
+  if (lane == 0 && a.csum) a.csum[p] = (uint16_t)c;
+}
+
+int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStream_t stream) {
+  if (args.n == 0) return 0;
+  if (tile_path) {
+    const uint64_t blocks = (args.n + args.T - 1) / args.T;
+    const size_t lds = args.hdr_bytes + kLdsGuard + (size_t)args.T * args.L + 32;
+    const void* fn = layout == 7 ? reinterpret_cast<const void*>(&encode_tile_kernel<7>)
+                                 : reinterpret_cast<const void*>(&encode_tile_kernel<5>);
+    if (lds > 65536) {
+      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return (int)e;
+    }
+    if (layout == 7)
+      hipLaunchKernelGGL(encode_tile_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
+    else
+      hipLaunchKernelGGL(encode_tile_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
+  } else {
+    const uint64_t blocks = (args.n + (kBlock / 64) - 1) / (kBlock / 64);
+    if (layout == 7)
+      hipLaunchKernelGGL(encode_bytes_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+    else
+      hipLaunchKernelGGL(encode_bytes_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+  }
+  return (int)hipGetLastError();
+}
+
+}  // namespace rudp

@@ -1,0 +1,109 @@
+"""ctypes binding of librudp.so (C ABI declared in include/rudp.h).
+
+There is no CPU fallback behind this module: if the library is missing, or a
+compute entry point is called without a HIP device, the call raises.  The
+library is loaded after ``torch`` so that it binds to the HIP runtime torch
+already has in the process (same soname, libamdhip64.so.7) and device
+pointers / streams from torch are valid in it.
+"""
+from __future__ import annotations
+
+import ctypes
+import threading
+from pathlib import Path
+
+LIB_PATH = Path(__file__).resolve().parent / "librudp.so"
+
+LAYOUT_RUDP5 = 5
+LAYOUT_RUDP7 = 7
+OK_BAD_CSUM, OK_GOOD, OK_SHORT, OK_UNVERIFIED = 0, 1, 2, 3
+EINVAL, ENOMEM, ENOTSUP, EHIP_BASE = -22, -12, -95, -1000
+ABI_VERSION = 1
+
+# Every symbol include/rudp.h declares (checked by tests/test_abi.py).
+EXPORTS = (
+    "rudp_encode", "rudp_decode", "rudp_encode_host", "rudp_decode_host",
+    "rudp_synth", "rudp_device_count", "rudp_last_error", "rudp_abi_version",
+)
+
+
+class RudpBatch(ctypes.Structure):
+    """struct rudp_batch (include/rudp.h)."""
+    _fields_ = [
+        ("n", ctypes.c_uint64),
+        ("payload_len", ctypes.c_uint32),
+        ("reserved", ctypes.c_uint32),
+        ("seq", ctypes.c_void_p),
+        ("ack", ctypes.c_void_p),
+        ("flags", ctypes.c_void_p),
+        ("payload", ctypes.c_void_p),
+        ("len", ctypes.c_void_p),
+        ("payload_off", ctypes.c_void_p),
+    ]
+
+
+class RudpError(RuntimeError):
+    def __init__(self, code: int, message: str):
+        super().__init__(f"librudp error {code}: {message}")
+        self.code = code
+
+
+_lock = threading.Lock()
+_lib = None
+
+
+def _declare(lib: ctypes.CDLL) -> None:
+    P, U64, U32, I = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    sig = {
+        "rudp_encode": [ctypes.POINTER(RudpBatch), P, P, I, I, P],
+        "rudp_decode": [P, P, U32, U64, P, P, P, P, P, P, P, I, I, P],
+        "rudp_encode_host": [ctypes.POINTER(RudpBatch), P, P, I, I],
+        "rudp_decode_host": [P, U32, U64, P, P, P, P, P, P, P, I, I],
+        "rudp_synth": [U64, U64, U64, U32, I, P, P, P, P, I, P],
+        "rudp_device_count": [ctypes.POINTER(ctypes.c_int)],
+        "rudp_abi_version": [],
+    }
+    for name, args in sig.items():
+        fn = getattr(lib, name)
+        fn.argtypes = args
+        fn.restype = ctypes.c_int
+    lib.rudp_last_error.argtypes = []
+    lib.rudp_last_error.restype = ctypes.c_char_p
+
+
+def lib() -> ctypes.CDLL:
+    """Load librudp.so once per process (raises if it was not built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    with _lock:
+        if _lib is None:
+            if not LIB_PATH.exists():
+                raise RuntimeError(
+                    f"{LIB_PATH} is missing: build it with "
+                    "`python reliable-udp_amd/rudp/_build.py` (or __graft_entry__.build())")
+            import torch  # noqa: F401  -- bind to torch's HIP runtime first
+            handle = ctypes.CDLL(str(LIB_PATH))
+            _declare(handle)
+            if handle.rudp_abi_version() != ABI_VERSION:
+                raise RuntimeError("librudp.so ABI version mismatch; rebuild it")
+            _lib = handle
+    return _lib
+
+
+def check(rc: int) -> None:
+    """Map a librudp return code to a Python exception."""
+    if rc == 0:
+        return
+    msg = (lib().rudp_last_error() or b"").decode(errors="replace")
+    if rc in (EINVAL, ENOTSUP):
+        raise ValueError(f"librudp: {msg}")
+    if rc == ENOMEM:
+        raise MemoryError(f"librudp: {msg}")
+    raise RudpError(rc, msg)
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    rc = lib().rudp_device_count(ctypes.byref(n))
+    return n.value if rc == 0 else 0

@@ -1,0 +1,282 @@
+"""Batched encode / decode of Reliable-UDP frames on MI355X.
+
+The reference frames one packet per Python call (utils/reliableUDP.py:53-61
+encode, :118-123 decode, through utils/packet.py).  Here a whole batch is
+framed, checksummed, parsed and verified by HIP kernels in librudp.so:
+
+    frames, csum = pack_batch(headers, payloads, layout="rudp5")
+    dec = unpack_batch(frames, layout="rudp5", csum=csum)
+
+Inputs are either torch tensors on a HIP device (asynchronous, on the current
+stream; the device-resident path the benchmark measures) or numpy arrays in
+host memory (synchronous; staged through the GPU by rudp_encode_host /
+rudp_decode_host, the model of the reference's socket-buffer boundary).
+Nothing here computes on the CPU: without librudp.so or a HIP device the
+calls raise.
+
+Layouts:
+  "rudp5"  the reference's 5-byte header (utils/packet.py:3-10) byte for
+           byte; the RFC 1071 checksum comes back as a sideband u16 array.
+  "rudp7"  {**custom_header, "checksum": 2}: the checksum in-band at bytes
+           5-6, framed exactly as utils/packet.py frames that definition.
+"""
+from __future__ import annotations
+
+import ctypes
+from dataclasses import dataclass
+from typing import Any, NamedTuple, Optional, Tuple, Union
+
+import numpy as np
+
+from . import _native
+
+LAYOUTS = {"rudp5": 5, "rudp7": 7, 5: 5, 7: 7}
+
+# header byte 4 (utils/packet.py:6-9): SYN 0x80, ACK 0x40, FIN 0x20, offset 0x1F
+SYN, ACK, FIN, OFFSET_MASK = 0x80, 0x40, 0x20, 0x1F
+
+
+def layout_header_len(layout: Union[str, int]) -> int:
+    try:
+        return LAYOUTS[layout]
+    except (KeyError, TypeError):
+        raise ValueError(f"unknown layout {layout!r}: use 'rudp5' or 'rudp7'") from None
+
+
+def make_flags(syn=0, ack=0, fin=0, offset=0):
+    """Header byte 4 from the four custom_header bit fields (utils/packet.py:6-9)."""
+    return (syn & 1) << 7 | (ack & 1) << 6 | (fin & 1) << 5 | (offset & OFFSET_MASK)
+
+
+@dataclass
+class HeaderTable:
+    """SoA header table: seq_num u16[N], ack_num u16[N], flags u8[N]."""
+    seq: Any
+    ack: Any
+    flags: Any
+
+    def __len__(self) -> int:
+        return len(self.seq)
+
+
+class DecodedBatch(NamedTuple):
+    seq: Any
+    ack: Any
+    flags: Any
+    ok: Any          # 1 good, 0 bad checksum, 2 short frame, 3 unverified (rudp5, no csum)
+    csum: Any        # recomputed checksum per packet
+    payload: Any     # [N, L] view into frames (zero-copy) or a copy
+
+
+def _is_torch(x) -> bool:
+    try:
+        import torch
+    except ImportError:  # pragma: no cover
+        return False
+    return isinstance(x, torch.Tensor)
+
+
+def _as_table(headers) -> HeaderTable:
+    if isinstance(headers, HeaderTable):
+        return headers
+    if isinstance(headers, dict):
+        return HeaderTable(headers["seq_num"], headers["ack_num"], headers["flags"])
+    seq, ack, flags = headers
+    return HeaderTable(seq, ack, flags)
+
+
+# ---------------------------------------------------------------- device path
+def _dev_check(t, name, dtype, ndim, device):
+    import torch
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch.Tensor on the same device")
+    if t.device != device:
+        raise ValueError(f"{name} is on {t.device}, expected {device}")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if t.dim() != ndim:
+        raise ValueError(f"{name} must be {ndim}-D, got shape {tuple(t.shape)}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+
+
+def _stream_ptr(stream, device) -> int:
+    import torch
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return int(s.cuda_stream)
+
+
+def _pack_device(tab: HeaderTable, payloads, H: int, out, csum_out, want_csum, stream):
+    import torch
+    dev = payloads.device
+    if dev.type != "cuda":
+        raise ValueError("device path needs tensors on a HIP device")
+    _dev_check(payloads, "payloads", torch.uint8, 2, dev)
+    n, L = payloads.shape
+    for name, t, dt in (("seq", tab.seq, torch.uint16), ("ack", tab.ack, torch.uint16),
+                        ("flags", tab.flags, torch.uint8)):
+        _dev_check(t, name, dt, 1, dev)
+        if t.shape[0] != n:
+            raise ValueError(f"{name} has {t.shape[0]} entries for {n} payloads")
+    F = L + H
+    if out is None:
+        out = torch.empty((n, F), dtype=torch.uint8, device=dev)
+    else:
+        _dev_check(out, "out", torch.uint8, 2, dev)
+        if tuple(out.shape) != (n, F):
+            raise ValueError(f"out must have shape {(n, F)}, got {tuple(out.shape)}")
+    if csum_out is None and want_csum:
+        csum_out = torch.empty((n,), dtype=torch.uint16, device=dev)
+    elif csum_out is not None:
+        _dev_check(csum_out, "csum_out", torch.uint16, 1, dev)
+    b = _native.RudpBatch(n=n, payload_len=L, reserved=0, seq=tab.seq.data_ptr(),
+                          ack=tab.ack.data_ptr(), flags=tab.flags.data_ptr(),
+                          payload=payloads.data_ptr() if n * L else None, len=None,
+                          payload_off=None)
+    _native.check(_native.lib().rudp_encode(
+        ctypes.byref(b), out.data_ptr() if n else None,
+        csum_out.data_ptr() if (csum_out is not None and n) else None,
+        H, dev.index if dev.index is not None else torch.cuda.current_device(),
+        _stream_ptr(stream, dev)))
+    return out, csum_out
+
+
+def _unpack_device(frames, H: int, csum, copy_payload: bool, stream):
+    import torch
+    dev = frames.device
+    if dev.type != "cuda":
+        raise ValueError("device path needs tensors on a HIP device")
+    _dev_check(frames, "frames", torch.uint8, 2, dev)
+    n, F = frames.shape
+    L = max(F - H, 0)
+    seq = torch.empty((n,), dtype=torch.uint16, device=dev)
+    ack = torch.empty((n,), dtype=torch.uint16, device=dev)
+    flags = torch.empty((n,), dtype=torch.uint8, device=dev)
+    ok = torch.empty((n,), dtype=torch.uint8, device=dev)
+    cs = torch.empty((n,), dtype=torch.uint16, device=dev)
+    if csum is not None:
+        _dev_check(csum, "csum", torch.uint16, 1, dev)
+        if csum.shape[0] != n:
+            raise ValueError(f"csum has {csum.shape[0]} entries for {n} frames")
+    pay = torch.empty((n, L), dtype=torch.uint8, device=dev) if copy_payload else None
+    if n:
+        _native.check(_native.lib().rudp_decode(
+            frames.data_ptr(), None, F, n, csum.data_ptr() if csum is not None else None,
+            seq.data_ptr(), ack.data_ptr(), flags.data_ptr(), ok.data_ptr(), cs.data_ptr(),
+            pay.data_ptr() if (pay is not None and L) else None, H,
+            dev.index if dev.index is not None else torch.cuda.current_device(),
+            _stream_ptr(stream, dev)))
+    if pay is None:
+        pay = frames[:, H:] if F >= H else frames[:, :0]
+    return DecodedBatch(seq, ack, flags, ok, cs, pay)
+
+
+# ------------------------------------------------------------------ host path
+def _host_arr(a, name, dtype, ndim):
+    a = np.ascontiguousarray(a)
+    if a.dtype != dtype:
+        raise TypeError(f"{name} must be {np.dtype(dtype)}, got {a.dtype}")
+    if a.ndim != ndim:
+        raise ValueError(f"{name} must be {ndim}-D, got shape {a.shape}")
+    return a
+
+
+def _ptr(a) -> Optional[int]:
+    return a.ctypes.data if a.size else None
+
+
+def _pack_host(tab: HeaderTable, payloads, H, want_csum, device):
+    payloads = _host_arr(payloads, "payloads", np.uint8, 2)
+    n, L = payloads.shape
+    seq = _host_arr(tab.seq, "seq", np.uint16, 1)
+    ack = _host_arr(tab.ack, "ack", np.uint16, 1)
+    flags = _host_arr(tab.flags, "flags", np.uint8, 1)
+    for name, a in (("seq", seq), ("ack", ack), ("flags", flags)):
+        if a.shape[0] != n:
+            raise ValueError(f"{name} has {a.shape[0]} entries for {n} payloads")
+    frames = np.empty((n, L + H), dtype=np.uint8)
+    csum = np.empty((n,), dtype=np.uint16) if want_csum else None
+    b = _native.RudpBatch(n=n, payload_len=L, reserved=0, seq=_ptr(seq), ack=_ptr(ack),
+                          flags=_ptr(flags), payload=_ptr(payloads), len=None, payload_off=None)
+    _native.check(_native.lib().rudp_encode_host(
+        ctypes.byref(b), _ptr(frames), _ptr(csum) if csum is not None else None, H, device))
+    return frames, csum
+
+
+def _unpack_host(frames, H, csum, copy_payload, device):
+    frames = _host_arr(frames, "frames", np.uint8, 2)
+    n, F = frames.shape
+    L = max(F - H, 0)
+    seq = np.empty((n,), np.uint16)
+    ack = np.empty((n,), np.uint16)
+    flags = np.empty((n,), np.uint8)
+    ok = np.empty((n,), np.uint8)
+    cs = np.empty((n,), np.uint16)
+    if csum is not None:
+        csum = _host_arr(csum, "csum", np.uint16, 1)
+        if csum.shape[0] != n:
+            raise ValueError(f"csum has {csum.shape[0]} entries for {n} frames")
+    pay = np.empty((n, L), np.uint8) if copy_payload else None
+    if n:
+        _native.check(_native.lib().rudp_decode_host(
+            _ptr(frames), F, n, _ptr(csum) if csum is not None else None, _ptr(seq), _ptr(ack),
+            _ptr(flags), _ptr(ok), _ptr(cs), _ptr(pay) if pay is not None else None, H, device))
+    if pay is None:
+        pay = frames[:, H:] if F >= H else frames[:, :0]
+    return DecodedBatch(seq, ack, flags, ok, cs, pay)
+
+
+# ------------------------------------------------------------------ public API
+def pack_batch(headers, payloads, layout: Union[str, int] = "rudp7", *, out=None,
+               csum_out=None, want_csum: Optional[bool] = None, stream=None, device: int = 0
+               ) -> Tuple[Any, Any]:
+    """Frame + checksum a batch.  Returns ``(frames, csum)``.
+
+    ``headers``: HeaderTable, ``(seq, ack, flags)`` or a dict keyed like
+    custom_header (``seq_num``, ``ack_num``) plus ``flags``.  ``payloads``:
+    uint8 ``[N, L]``.  ``csum`` is the per-packet checksum (always for rudp5,
+    on request for rudp7; else None).  Torch tensors on a HIP device run
+    asynchronously on ``stream`` (default: current stream); numpy arrays run
+    synchronously through ``device``.
+    """
+    H = layout_header_len(layout)
+    tab = _as_table(headers)
+    if want_csum is None:
+        want_csum = H == 5
+    if _is_torch(payloads):
+        return _pack_device(tab, payloads, H, out, csum_out, want_csum, stream)
+    if out is not None or csum_out is not None:
+        raise ValueError("out=/csum_out= are only supported on the device path")
+    return _pack_host(tab, payloads, H, want_csum, device)
+
+
+def unpack_batch(frames, layout: Union[str, int] = "rudp7", *, csum=None,
+                 copy_payload: bool = False, stream=None, device: int = 0) -> DecodedBatch:
+    """Parse + verify a batch of fixed-length frames ``[N, F]``.
+
+    ``csum`` (rudp5 only): sideband checksums to verify against.  The payload
+    is returned as a zero-copy view ``frames[:, H:]`` unless ``copy_payload``.
+    """
+    H = layout_header_len(layout)
+    if H == 7 and csum is not None:
+        raise ValueError("rudp7 carries its checksum in-band; csum= is for rudp5")
+    if _is_torch(frames):
+        return _unpack_device(frames, H, csum, copy_payload, stream)
+    return _unpack_host(frames, H, csum, copy_payload, device)
+
+
+def synth_batch(n: int, payload_len: int, seed: int, *, first_index: int = 0, ascii: bool = True,
+                device=None, stream=None) -> Tuple[HeaderTable, Any]:
+    """Generate the deterministic synthetic batch on a HIP device (rudp_synth)."""
+    import torch
+    dev = torch.device(device) if device is not None else torch.device("cuda", torch.cuda.current_device())
+    seq = torch.empty((n,), dtype=torch.uint16, device=dev)
+    ack = torch.empty((n,), dtype=torch.uint16, device=dev)
+    flags = torch.empty((n,), dtype=torch.uint8, device=dev)
+    pay = torch.empty((n, payload_len), dtype=torch.uint8, device=dev)
+    if n:
+        _native.check(_native.lib().rudp_synth(
+            seed & (2**64 - 1), first_index, n, payload_len, 1 if ascii else 0, seq.data_ptr(),
+            ack.data_ptr(), flags.data_ptr(), pay.data_ptr() if payload_len else None,
+            dev.index if dev.index is not None else 0, _stream_ptr(stream, dev)))
+    return HeaderTable(seq, ack, flags), pay

@@ -1,0 +1,77 @@
+"""The C ABI library loads and exports what include/rudp.h declares.
+
+CPU-only: no compute call reaches a device here; only the argument checks
+that run before any HIP call are exercised.
+"""
+import ctypes
+import re
+
+import numpy as np
+import pytest
+
+from conftest import REPO
+from rudp import _native
+from rudp import batch
+
+
+def declared_functions():
+    text = (REPO / "include" / "rudp.h").read_text()
+    return set(re.findall(r"^(?:int|const char\*)\s+(rudp_\w+)\s*\(", text, flags=re.M))
+
+
+def test_header_and_binding_agree():
+    assert declared_functions() == set(_native.EXPORTS)
+
+
+def test_library_exports_every_declared_symbol():
+    lib = _native.lib()
+    for name in declared_functions():
+        assert hasattr(lib, name), name
+    assert lib.rudp_abi_version() == _native.ABI_VERSION
+
+
+def test_batch_struct_layout():
+    # struct rudp_batch: u64, u32, u32, then 6 pointers
+    assert ctypes.sizeof(_native.RudpBatch) == 8 + 4 + 4 + 6 * 8
+    assert _native.RudpBatch.seq.offset == 16
+
+
+def test_argument_errors_before_device():
+    lib = _native.lib()
+    assert lib.rudp_encode(None, None, None, 7, 0, None) == _native.EINVAL
+    assert b"NULL" in lib.rudp_last_error()
+    b = _native.RudpBatch(n=1, payload_len=4)
+    assert lib.rudp_encode(ctypes.byref(b), None, None, 6, 0, None) == _native.EINVAL
+    assert b"layout" in lib.rudp_last_error()
+    lens = (ctypes.c_uint32 * 1)(4)
+    b.len = ctypes.cast(lens, ctypes.c_void_p)
+    assert lib.rudp_encode(ctypes.byref(b), None, None, 7, 0, None) == _native.ENOTSUP
+    assert lib.rudp_decode(None, None, 10, 1, None, None, None, None, None, None, None, 9, 0,
+                           None) == _native.EINVAL
+    off = (ctypes.c_uint64 * 1)(0)
+    assert lib.rudp_decode(None, ctypes.cast(off, ctypes.c_void_p), 10, 1, None, None, None, None,
+                           None, None, None, 7, 0, None) == _native.ENOTSUP
+    # empty batches are a successful no-op, no device needed
+    assert lib.rudp_encode(ctypes.byref(_native.RudpBatch(n=0)), None, None, 5, 0, None) == 0
+    assert lib.rudp_synth(1, 0, 0, 16, 1, None, None, None, None, 0, None) == 0
+
+
+def test_error_mapping():
+    with pytest.raises(ValueError, match="layout"):
+        b = _native.RudpBatch(n=1, payload_len=4)
+        _native.check(_native.lib().rudp_encode(ctypes.byref(b), None, None, 6, 0, None))
+
+
+def test_python_api_validation():
+    seq = np.zeros(3, np.uint16)
+    with pytest.raises(ValueError, match="layout"):
+        batch.pack_batch((seq, seq, np.zeros(3, np.uint8)), np.zeros((3, 4), np.uint8), "rudp6")
+    with pytest.raises(TypeError, match="uint16"):
+        batch.pack_batch((seq.astype(np.int32), seq, np.zeros(3, np.uint8)),
+                         np.zeros((3, 4), np.uint8))
+    with pytest.raises(ValueError, match="entries"):
+        batch.pack_batch((seq[:2], seq, np.zeros(3, np.uint8)), np.zeros((3, 4), np.uint8))
+    with pytest.raises(ValueError, match="in-band"):
+        batch.unpack_batch(np.zeros((3, 20), np.uint8), "rudp7", csum=seq)
+    assert batch.make_flags(syn=1, fin=1) == 0xA0
+    assert batch.make_flags(ack=1, offset=0x3F) == 0x5F

@@ -1,0 +1,218 @@
+"""HIP kernels (through the C ABI) against the oracle and the reference goldens.
+
+Bit-exact everywhere: this is byte/integer work.  Small shapes are diffed
+element-wise against the committed golden vectors (produced by the reference
+utils/packet.py) and against oracle/codec_np.py; the BASELINE configs at full
+size are checked through SHA-256 digests of the reference-framed batches.
+"""
+import hashlib
+
+import numpy as np
+import pytest
+
+from conftest import small_lengths
+from oracle import codec_np, synth
+from rudp import batch
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a, cuda):
+    import torch
+    return torch.from_numpy(np.ascontiguousarray(a)).to(cuda)
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+def gpu_encode(cuda, seq, ack, flags, pay, layout, want_csum=True):
+    fr, cs = batch.pack_batch((dev(seq, cuda), dev(ack, cuda), dev(flags, cuda)), dev(pay, cuda),
+                              layout, want_csum=want_csum)
+    return host(fr), (host(cs) if cs is not None else None)
+
+
+# ------------------------------------------------------------------ synth
+@pytest.mark.parametrize("n,L,ascii", [(1000, 1472, True), (777, 65, False), (5000, 64, True),
+                                       (100, 0, True), (300, 7, False), (33, 1024, False)])
+def test_synth_matches_numpy(cuda, n, L, ascii):
+    tab, pay = batch.synth_batch(n, L, seed=0xABCDEF + L, first_index=12345, ascii=ascii,
+                                 device=cuda)
+    want = synth.synth(0xABCDEF + L, 12345, n, L, ascii=ascii)
+    for got, exp in zip((tab.seq, tab.ack, tab.flags, pay), want):
+        assert np.array_equal(host(got), exp)
+
+
+# --------------------------------------------------------------- goldens
+@pytest.mark.parametrize("layout", [5, 7])
+def test_encode_matches_reference_goldens(cuda, golden_small, layout):
+    for L in small_lengths(golden_small):
+        g = {k.split("_", 1)[1]: v for k, v in golden_small.items() if k.startswith(f"L{L}_")}
+        fr, cs = gpu_encode(cuda, g["seq"], g["ack"], g["flags"], g["payload"], layout)
+        assert np.array_equal(fr, g[f"frames{layout}"]), f"L={L}"
+        assert np.array_equal(cs, g["csum"]), f"L={L}"
+
+
+@pytest.mark.parametrize("layout", [5, 7])
+def test_decode_matches_reference_goldens(cuda, golden_small, layout):
+    for L in small_lengths(golden_small):
+        fr = golden_small[f"L{L}_full_frames{layout}"]
+        ref = golden_small[f"L{L}_full_fields{layout}"]
+        d = batch.unpack_batch(dev(fr, cuda), layout, copy_payload=True)
+        assert np.array_equal(host(d.seq), ref[:, 0]), f"L={L}"
+        assert np.array_equal(host(d.ack), ref[:, 1])
+        assert np.array_equal(host(d.flags), ref[:, 2])
+        assert np.array_equal(host(d.payload), fr[:, layout:])
+        if layout == 7:
+            assert np.array_equal(host(d.csum), ref[:, 3]) and (host(d.ok) == 1).all()
+        else:
+            assert (host(d.ok) == 3).all()
+            _, want = codec_np.encode(ref[:, 0], ref[:, 1], ref[:, 2], fr[:, 5:], 5)
+            assert np.array_equal(host(d.csum), want)
+            d2 = batch.unpack_batch(dev(fr, cuda), 5, csum=dev(want, cuda))
+            assert (host(d2.ok) == 1).all()
+
+
+# ------------------------------------------------------- shapes & edge cases
+LENGTHS = [16, 32, 48, 64, 80, 128, 256, 1008, 1024, 1472, 2048, 4096, 4112, 1, 5, 63, 1471]
+COUNTS = [1, 15, 16, 17, 255, 257, 4099]
+
+
+@pytest.mark.parametrize("L", LENGTHS)
+def test_roundtrip_vs_oracle(cuda, L):
+    for n in COUNTS:
+        seq, ack, flags, pay = synth.synth(0x1000 + L, 3 * n, n, L, ascii=False)
+        for layout in (5, 7):
+            fr, cs = gpu_encode(cuda, seq, ack, flags, pay, layout)
+            want_fr, want_cs = codec_np.encode(seq, ack, flags, pay, layout)
+            assert np.array_equal(fr, want_fr), (L, n, layout)
+            assert np.array_equal(cs, want_cs), (L, n, layout)
+            d = batch.unpack_batch(dev(fr, cuda), layout, copy_payload=True,
+                                   csum=dev(cs, cuda) if layout == 5 else None)
+            assert (host(d.ok) == 1).all(), (L, n, layout)
+            assert np.array_equal(host(d.seq), seq) and np.array_equal(host(d.ack), ack)
+            assert np.array_equal(host(d.flags), flags)
+            assert np.array_equal(host(d.payload), pay)
+
+
+def test_misaligned_buffers_take_byte_path(cuda):
+    import torch
+    n, L = 1000, 1024
+    seq, ack, flags, pay = synth.synth(77, 0, n, L, ascii=False)
+    raw = torch.zeros(n * L + 16, dtype=torch.uint8, device=cuda)
+    view = raw[3:3 + n * L].view(n, L)
+    view.copy_(dev(pay, cuda))
+    out_raw = torch.zeros(n * (L + 7) + 16, dtype=torch.uint8, device=cuda)
+    out = out_raw[5:5 + n * (L + 7)].view(n, L + 7)
+    fr, _ = batch.pack_batch((dev(seq, cuda), dev(ack, cuda), dev(flags, cuda)), view, 7, out=out)
+    want, _ = codec_np.encode(seq, ack, flags, pay, 7)
+    assert np.array_equal(host(fr), want)
+    d = batch.unpack_batch(out, 7, copy_payload=True)
+    assert (host(d.ok) == 1).all() and np.array_equal(host(d.payload), pay)
+
+
+@pytest.mark.parametrize("layout", [5, 7])
+def test_single_byte_corruption_detected(cuda, layout):
+    n, L = 4096, 1472
+    seq, ack, flags, pay = synth.synth(99, 0, n, L, ascii=False)
+    fr, cs = gpu_encode(cuda, seq, ack, flags, pay, layout)
+    rng = np.random.default_rng(5)
+    pos = rng.integers(0, L + layout, size=n)
+    delta = rng.integers(1, 256, size=n).astype(np.uint8)
+    bad = fr.copy()
+    bad[np.arange(n), pos] += delta
+    d = batch.unpack_batch(dev(bad, cuda), layout, csum=dev(cs, cuda) if layout == 5 else None)
+    assert (host(d.ok) == 0).all()
+    ok_np = codec_np.decode(bad, layout, cs if layout == 5 else None)[3]
+    assert np.array_equal(host(d.ok), ok_np)
+
+
+@pytest.mark.parametrize("layout", [5, 7])
+def test_short_frames(cuda, layout):
+    for F in range(0, layout):
+        fr = np.arange(37 * F, dtype=np.uint8).reshape(37, F) if F else np.zeros((37, 0), np.uint8)
+        d = batch.unpack_batch(dev(fr, cuda), layout)
+        seq, ack, flags, ok, cs, _ = codec_np.decode(fr, layout)
+        assert (host(d.ok) == 2).all()
+        assert np.array_equal(host(d.seq), seq) and np.array_equal(host(d.ack), ack)
+        assert np.array_equal(host(d.flags), flags)
+
+
+def test_header_only_frames(cuda):
+    # payload_len 0: the final ACK / FIN|ACK frames of utils/reliableUDP.py:88-92, :156-161
+    seq = np.array([0x0E21, 0, 0], np.uint16)
+    ack = np.array([1, 0x0E21, 0x0E1C], np.uint16)
+    flags = np.array([0x40, 0x60, 0x40], np.uint8)
+    fr, cs = gpu_encode(cuda, seq, ack, flags, np.zeros((3, 0), np.uint8), 5)
+    assert [bytes(r).hex() for r in fr] == ["0e21000140", "00000e2160", "00000e1c40"]
+    d = batch.unpack_batch(dev(fr, cuda), 5, csum=dev(cs, cuda))
+    assert (host(d.ok) == 1).all()
+
+
+def test_empty_batch(cuda):
+    fr, cs = gpu_encode(cuda, np.zeros(0, np.uint16), np.zeros(0, np.uint16), np.zeros(0, np.uint8),
+                        np.zeros((0, 64), np.uint8), 5)
+    assert fr.shape == (0, 69) and cs.shape == (0,)
+    d = batch.unpack_batch(dev(np.zeros((0, 71), np.uint8), cuda), 7)
+    assert host(d.ok).shape == (0,)
+
+
+def test_side_stream(cuda):
+    import torch
+    seq, ack, flags, pay = synth.synth(3, 0, 2048, 1472, ascii=False)
+    s = torch.cuda.Stream(cuda)
+    with torch.cuda.stream(s):
+        fr, _ = batch.pack_batch((dev(seq, cuda), dev(ack, cuda), dev(flags, cuda)), dev(pay, cuda), 7)
+    s.synchronize()
+    assert np.array_equal(host(fr), codec_np.encode(seq, ack, flags, pay, 7)[0])
+
+
+def test_host_staged_path(cuda):
+    seq, ack, flags, pay = synth.synth(11, 0, 70000, 1024, ascii=False)
+    for layout in (5, 7):
+        fr, cs = batch.pack_batch((seq, ack, flags), pay, layout)  # numpy in -> numpy out
+        want_fr, want_cs = codec_np.encode(seq, ack, flags, pay, layout)
+        assert np.array_equal(fr, want_fr) and np.array_equal(cs if cs is not None else want_cs, want_cs)
+        d = batch.unpack_batch(fr, layout, csum=cs if layout == 5 else None, copy_payload=True)
+        assert (d.ok == 1).all() and np.array_equal(d.payload, pay)
+        assert np.array_equal(d.seq, seq) and np.array_equal(d.flags, flags)
+
+
+# ------------------------------------------------- full-size BASELINE configs
+def _digest_run(cuda, cfg, layout, chunk_index):
+    import torch
+    n = min(cfg["chunk"], cfg["n"] - chunk_index * cfg["chunk"])
+    tab, pay = batch.synth_batch(n, cfg["L"], cfg["seed"], first_index=chunk_index * cfg["chunk"],
+                                 device=cuda)
+    fr, cs = batch.pack_batch(tab, pay, layout, want_csum=True)
+    torch.cuda.synchronize()
+    h_fr = hashlib.sha256(host(fr).tobytes()).hexdigest()
+    h_cs = hashlib.sha256(host(cs).astype("<u2").tobytes()).hexdigest()
+    return h_fr, h_cs, (tab, pay, fr, cs)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name,layout,chunk", [("C2", 5, 0), ("C3", 5, 0), ("C4", 5, 0), ("C4", 7, 0),
+                                               ("C5", 7, 0), ("C5", 7, 9), ("C5", 5, 15)])
+def test_full_size_digests(cuda, digests, name, layout, chunk):
+    cfg = digests[name]
+    h_fr, h_cs, _ = _digest_run(cuda, cfg, layout, chunk)
+    want = cfg["layouts"][str(layout)]
+    assert h_fr == want["frames"][chunk]
+    assert h_cs == want["csum"][chunk]
+
+
+@pytest.mark.slow
+def test_c4_roundtrip_full_size(cuda, digests):
+    """Config 4: 1M x 1472 B encode -> decode, bit-exact vs the reference digest."""
+    import torch
+    cfg = digests["C4"]
+    h_fr, _, (tab, pay, fr, cs) = _digest_run(cuda, cfg, 7, 0)
+    assert h_fr == cfg["layouts"]["7"]["frames"][0]
+    d = batch.unpack_batch(fr, 7, copy_payload=True)
+    assert bool((d.ok == 1).all())
+    assert torch.equal(d.payload, pay)
+    assert torch.equal(d.seq.view(torch.int16), tab.seq.view(torch.int16))
+    assert torch.equal(d.ack.view(torch.int16), tab.ack.view(torch.int16))
+    assert torch.equal(d.flags, tab.flags)
+    assert torch.equal(d.csum.view(torch.int16), cs.view(torch.int16))
