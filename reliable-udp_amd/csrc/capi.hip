@@ -101,15 +101,16 @@ int validate_batch(const rudp_batch* in, const void* frames, int layout) {
   return 0;
 }
 
-int validate_decode(const void* frames, const void* frame_off, uint64_t n, const void* seq,
-                    const void* ack, const void* flags, const void* ok, int layout) {
+int validate_decode(const void* frames, const void* frame_off, uint32_t frame_len, uint64_t n,
+                    const void* seq, const void* ack, const void* flags, const void* ok,
+                    int layout) {
   if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
     return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
   if (frame_off)
     return fail(RUDP_ENOTSUP, "per-frame offsets are not supported by ABI version %d",
                 RUDP_ABI_VERSION);
   if (n == 0) return 0;
-  if (!frames || !seq || !ack || !flags || !ok)
+  if ((frame_len && !frames) || !seq || !ack || !flags || !ok)
     return fail(RUDP_EINVAL, "rudp_decode: NULL buffer for a non-empty batch");
   return 0;
 }
@@ -211,7 +212,7 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, ui
                 uint64_t n, const uint16_t* d_csum_in_or_null, uint16_t* d_seq, uint16_t* d_ack,
                 uint8_t* d_flags, uint8_t* d_ok, uint16_t* d_csum_out_or_null,
                 uint8_t* d_payload_out_or_null, int layout, int device, void* hip_stream) {
-  int rc = validate_decode(d_frames, d_frame_off_or_null, n, d_seq, d_ack, d_flags, d_ok, layout);
+  int rc = validate_decode(d_frames, d_frame_off_or_null, frame_len, n, d_seq, d_ack, d_flags, d_ok, layout);
   if (rc || n == 0) return rc;
   if ((rc = check_device(device))) return rc;
   DecodeArgs a{};
@@ -306,7 +307,7 @@ int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
                      const uint16_t* h_csum_in_or_null, uint16_t* h_seq, uint16_t* h_ack,
                      uint8_t* h_flags, uint8_t* h_ok, uint16_t* h_csum_out_or_null,
                      uint8_t* h_payload_out_or_null, int layout, int device) {
-  int rc = validate_decode(h_frames, nullptr, n, h_seq, h_ack, h_flags, h_ok, layout);
+  int rc = validate_decode(h_frames, nullptr, frame_len, n, h_seq, h_ack, h_flags, h_ok, layout);
   if (rc || n == 0) return rc;
   if ((rc = check_device(device))) return rc;
   const uint64_t F = frame_len;

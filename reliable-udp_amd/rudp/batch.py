@@ -161,7 +161,7 @@ def _unpack_device(frames, H: int, csum, copy_payload: bool, stream):
     pay = torch.empty((n, L), dtype=torch.uint8, device=dev) if copy_payload else None
     if n:
         _native.check(_native.lib().rudp_decode(
-            frames.data_ptr(), None, F, n, csum.data_ptr() if csum is not None else None,
+            frames.data_ptr() if F else None, None, F, n, csum.data_ptr() if csum is not None else None,
             seq.data_ptr(), ack.data_ptr(), flags.data_ptr(), ok.data_ptr(), cs.data_ptr(),
             pay.data_ptr() if (pay is not None and L) else None, H,
             dev.index if dev.index is not None else torch.cuda.current_device(),

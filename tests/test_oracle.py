@@ -114,3 +114,17 @@ def test_c_restatement_matches_numpy_and_goldens(golden_small):
             want = codec_np.decode(fr, layout)
             for a, b in zip(got, want[:5]):
                 assert np.array_equal(a, b), (F, layout)
+
+
+@pytest.mark.slow
+@pytest.mark.parametrize("name,layout", [("C3", 5), ("C4", 7)])
+def test_c_oracle_reproduces_reference_digest(digests, name, layout):
+    """The C restatement frames BASELINE config chunk 0 exactly as utils/packet.py did."""
+    import hashlib
+
+    from oracle import codec_c
+    cfg = digests[name]
+    seq, ack, flags, pay = synth.synth(cfg["seed"], 0, cfg["chunk"], cfg["L"])
+    fr, cs = codec_c.encode(seq, ack, flags, pay, layout)
+    assert hashlib.sha256(fr.tobytes()).hexdigest() == cfg["layouts"][str(layout)]["frames"][0]
+    assert hashlib.sha256(cs.astype("<u2").tobytes()).hexdigest() == cfg["layouts"][str(layout)]["csum"][0]
