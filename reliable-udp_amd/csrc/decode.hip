@@ -116,6 +116,89 @@ __global__ void __launch_bounds__(kBlock) decode_vec_kernel(DecodeArgs a) {
   }
 }
 
+// Zero-copy verify (no payload_out): G lanes per packet load the ALIGNED
+// 16-byte chunks that overlap the packet's frame [p*F, p*F + F) exactly once
+// each (coalesced dwordx4 across the group; the two boundary chunks are
+// shared with the neighbour packets and come from L2).  No realignment: the
+// frame's big-endian word sum is a parity-weighted byte sum — a byte at
+// frame position k is the high byte of its word iff k is even, and since F
+// is odd, k = x - p*F has the parity of x + p for global offset x.  So each
+// lane sums bytes at even / odd global offsets (masked to the frame at the
+// two boundary chunks) and weights them by the packet's parity.  The header
+// comes from the group's first two chunks (lanes 0 and 1, one shuffle).  The
+// in-band checksum's own bytes are then taken back out of the exact integer
+// sum before the fold.
+template <int H>
+__global__ void __launch_bounds__(kBlock) decode_verify_kernel(DecodeArgs a) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t glog = a.glog;
+  const uint32_t G = 1u << glog;
+  const uint32_t q = tid >> glog;
+  const uint32_t g = tid & (G - 1u);
+  const uint64_t p = (uint64_t)blockIdx.x * (kBlock >> glog) + q;
+  const bool valid = p < a.n;
+  const uint64_t F = a.F;
+  const uint64_t total = a.n * F;
+  const uint64_t fstart = p * F;
+  const uint64_t fend = fstart + F;
+  const uint64_t c_lo = fstart >> 4;
+  const uint32_t nchunks = valid ? (uint32_t)(((fend - 1) >> 4) - c_lo + 1) : 0u;
+
+  uint32_t even_sum = 0, odd_sum = 0;  // byte sums at even / odd global offsets
+  u32x4 first = {0u, 0u, 0u, 0u};
+  for (uint32_t i0 = g; i0 < nchunks; i0 += 8u * G) {
+    // per round: at most 32 dwords, so the packed 2 x 16-bit lanes cannot overflow
+    uint32_t even = 0, odd = 0;
+    u32x4 v[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t i = i0 + (uint32_t)u * G;
+      if (i < nchunks) v[u] = load16_guarded(a.frames, (c_lo + i) << 4, total);
+    }
+    if (i0 == g) first = v[0];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t i = i0 + (uint32_t)u * G;
+      if (i < nchunks) {
+        u32x4 w = v[u];
+        if (i == 0 || i + 1 == nchunks) {  // boundary chunk: keep this frame's bytes only
+          const int64_t cb = (int64_t)((c_lo + i) << 4);
+          const int lo = (int)((int64_t)fstart - cb), hi = (int)((int64_t)fend - cb);
+          const uint64_t l = lo64(w) & byte_mask(lo, hi), h = hi64(w) & byte_mask(lo - 8, hi - 8);
+          w = make_u32x4(l, h);
+        }
+        even += (w.x & 0x00FF00FFu) + (w.y & 0x00FF00FFu) + (w.z & 0x00FF00FFu) + (w.w & 0x00FF00FFu);
+        odd += ((w.x >> 8) & 0x00FF00FFu) + ((w.y >> 8) & 0x00FF00FFu) +
+               ((w.z >> 8) & 0x00FF00FFu) + ((w.w >> 8) & 0x00FF00FFu);
+      }
+    }
+    even_sum += (even & 0xFFFFu) + (even >> 16);
+    odd_sum += (odd & 0xFFFFu) + (odd >> 16);
+  }
+  // frame position parity = parity(x + p): even-offset bytes are high bytes iff p is even
+  uint32_t sum = (p & 1u) ? (even_sum + (odd_sum << 8)) : ((even_sum << 8) + odd_sum);
+  for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
+  // header bytes: frame start lies in the group's first chunk, at most 6 bytes spill into the next
+  const int src = (int)((threadIdx.x & 63u) + 1u);
+  u32x4 next;
+  next.x = __shfl(first.x, src, 64);
+  next.y = __shfl(first.y, src, 64);
+  next.z = __shfl(first.z, src, 64);
+  next.w = __shfl(first.w, src, 64);
+  if (g == 0 && valid) {
+    const u32x4 h = funnel32(first, next, (uint32_t)(fstart & 15u));
+    const uint32_t seq = ((h.x & 0xFFu) << 8) | ((h.x >> 8) & 0xFFu);
+    const uint32_t ack = (((h.x >> 16) & 0xFFu) << 8) | (h.x >> 24);
+    const uint32_t flags = h.y & 0xFFu;
+    const uint32_t inband = (((h.y >> 8) & 0xFFu) << 8) | ((h.y >> 16) & 0xFFu);
+    // the sum above covered the whole frame; the checksum field (bytes 5, 6:
+    // odd then even position) contributed byte-swapped — take it back out
+    const uint32_t payload_and_rest =
+        sum - seq - ack - (flags << 8) - (H == 7 ? (((inband & 0xFFu) << 8) | (inband >> 8)) : 0u);
+    finish_packet<H>(a, p, payload_and_rest, seq, ack, flags, inband);
+  }
+}
+
 // Any frame length: one wave per packet, byte-granular.  Frames shorter
 // than the header report RUDP_OK_SHORT with the fields that are present,
 // truncated the way utils/packet.py:31 slices a short bit string.
@@ -158,15 +241,21 @@ __global__ void __launch_bounds__(kBlock) decode_bytes_kernel(DecodeArgs a) {
   }
 }
 
-int launch_decode(const DecodeArgs& args, int layout, bool vec_path, hipStream_t stream) {
+int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream_t stream) {
   if (args.n == 0) return 0;
-  if (vec_path) {
+  if (path != DecodePath::kBytes) {
     const uint32_t per_block = kBlock >> args.glog;
     const uint64_t blocks = (args.n + per_block - 1) / per_block;
-    if (layout == 7)
+    if (path == DecodePath::kVerify) {
+      if (layout == 7)
+        hipLaunchKernelGGL(decode_verify_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+      else
+        hipLaunchKernelGGL(decode_verify_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+    } else if (layout == 7) {
       hipLaunchKernelGGL(decode_vec_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
-    else
+    } else {
       hipLaunchKernelGGL(decode_vec_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+    }
   } else {
     const uint64_t blocks = (args.n + (kBlock / 64) - 1) / (kBlock / 64);
     if (layout == 7)

@@ -26,7 +26,21 @@ namespace rudp {
 
 constexpr int kLdsGuard = 16;  // bytes before the payload tile (negative offsets)
 
-template <int H>
+template <bool NT>
+__device__ __forceinline__ u32x4 load16(const u32x4* p) {
+  if (NT) return __builtin_nontemporal_load(p);
+  return *p;
+}
+
+template <bool NT>
+__device__ __forceinline__ void store16(u32x4 v, u32x4* p) {
+  if (NT)
+    __builtin_nontemporal_store(v, p);
+  else
+    *p = v;
+}
+
+template <int H, bool NTL, bool NTS, int UNROLL>
 __global__ void __launch_bounds__(kBlock) encode_tile_kernel(EncodeTileArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   uint64_t* lds_hdr = reinterpret_cast<uint64_t*>(lds);  // [T + 1]
@@ -37,7 +51,17 @@ __global__ void __launch_bounds__(kBlock) encode_tile_kernel(EncodeTileArgs a) {
   const uint32_t T = a.T;
   const uint32_t glog = a.glog;
   const uint32_t G = 1u << glog;
-  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  uint32_t tile = blockIdx.x;
+  if (a.xcd_swizzle) {
+    // Workgroups are dealt round-robin over the 8 XCDs (b, b+8, ... share
+    // one).  Give each XCD a contiguous run of tiles so neighbouring tiles'
+    // header-table lines and boundary output lines stay in one L2.  Bijective
+    // for any tile count; placement affects speed only.
+    const uint32_t nt = a.num_tiles, per = nt >> 3, rem = nt & 7u;
+    const uint32_t x = tile & 7u, k = tile >> 3;
+    tile = x * per + (x < rem ? x : rem) + k;
+  }
+  const uint64_t p0 = (uint64_t)tile * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
 
@@ -54,7 +78,7 @@ __global__ void __launch_bounds__(kBlock) encode_tile_kernel(EncodeTileArgs a) {
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
         uint32_t v = v0 + (uint32_t)u * G;
-        if (v < V) r[u] = __builtin_nontemporal_load(src + v);
+        if (v < V) r[u] = load16<NTL>(src + v);
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -81,6 +105,7 @@ __global__ void __launch_bounds__(kBlock) encode_tile_kernel(EncodeTileArgs a) {
   const uint32_t nbytes = Tv * F;
   unsigned char* out = a.frames + p0 * (uint64_t)F;
   const uint32_t* pay_dw = reinterpret_cast<const uint32_t*>(lds_pay);
+#pragma unroll UNROLL
   for (uint32_t x = tid * 16u; x < nbytes; x += kBlock * 16u) {
     const uint32_t qq = (uint32_t)(((uint64_t)x * a.invF) >> 32);  // x / F
     const uint32_t r = x - qq * F;           // frame position of chunk byte 0
@@ -106,7 +131,7 @@ __global__ void __launch_bounds__(kBlock) encode_tile_kernel(EncodeTileArgs a) {
     }
     const u32x4 v = make_u32x4(lo, hi);
     if (x + 16u <= nbytes) {
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + x));
+      store16<NTS>(v, reinterpret_cast<u32x4*>(out + x));
     } else {
       uint32_t d[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
@@ -142,28 +167,44 @@ __global__ void __launch_bounds__(kBlock) encode_bytes_kernel(EncodeTileArgs a) 
   if (lane == 0 && a.csum) a.csum[p] = (uint16_t)c;
 }
 
+template <int H, bool NTL, bool NTS, int UNROLL>
+int launch_tile(const EncodeTileArgs& args, hipStream_t stream) {
+  const uint64_t blocks = (args.n + args.T - 1) / args.T;
+  const size_t lds = args.hdr_bytes + kLdsGuard + (size_t)args.T * args.L + 32;
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_tile_kernel<H, NTL, NTS, UNROLL>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL((encode_tile_kernel<H, NTL, NTS, UNROLL>), dim3((uint32_t)blocks), dim3(kBlock), lds,
+                     stream, args);
+  return (int)hipGetLastError();
+}
+
+template <int H>
+int launch_tile_policy(const EncodeTileArgs& args, hipStream_t stream) {
+  const Tuning& t = tuning();
+  if (t.encode_unroll == 2) {
+    if (t.encode_nt_load && t.encode_nt_store) return launch_tile<H, true, true, 2>(args, stream);
+    if (t.encode_nt_load) return launch_tile<H, true, false, 2>(args, stream);
+    if (t.encode_nt_store) return launch_tile<H, false, true, 2>(args, stream);
+    return launch_tile<H, false, false, 2>(args, stream);
+  }
+  if (t.encode_nt_load && t.encode_nt_store) return launch_tile<H, true, true, 1>(args, stream);
+  if (t.encode_nt_load) return launch_tile<H, true, false, 1>(args, stream);
+  if (t.encode_nt_store) return launch_tile<H, false, true, 1>(args, stream);
+  return launch_tile<H, false, false, 1>(args, stream);
+}
+
 int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStream_t stream) {
   if (args.n == 0) return 0;
-  if (tile_path) {
-    const uint64_t blocks = (args.n + args.T - 1) / args.T;
-    const size_t lds = args.hdr_bytes + kLdsGuard + (size_t)args.T * args.L + 32;
-    const void* fn = layout == 7 ? reinterpret_cast<const void*>(&encode_tile_kernel<7>)
-                                 : reinterpret_cast<const void*>(&encode_tile_kernel<5>);
-    if (lds > 65536) {
-      hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e != hipSuccess) return (int)e;
-    }
-    if (layout == 7)
-      hipLaunchKernelGGL(encode_tile_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
-    else
-      hipLaunchKernelGGL(encode_tile_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
-  } else {
-    const uint64_t blocks = (args.n + (kBlock / 64) - 1) / (kBlock / 64);
-    if (layout == 7)
-      hipLaunchKernelGGL(encode_bytes_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
-    else
-      hipLaunchKernelGGL(encode_bytes_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
-  }
+  if (tile_path)
+    return layout == 7 ? launch_tile_policy<7>(args, stream) : launch_tile_policy<5>(args, stream);
+  const uint64_t blocks = (args.n + (kBlock / 64) - 1) / (kBlock / 64);
+  if (layout == 7)
+    hipLaunchKernelGGL(encode_bytes_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+  else
+    hipLaunchKernelGGL(encode_bytes_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
   return (int)hipGetLastError();
 }
 

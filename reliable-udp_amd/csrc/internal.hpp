@@ -18,6 +18,8 @@ struct EncodeTileArgs {
   uint32_t glog;        // log2(256 / T): lanes per packet
   uint32_t hdr_bytes;   // LDS bytes reserved for the tile's header words
   uint64_t invF;        // ceil(2^32 / (L + H)) for exact x / F, x < T*F
+  uint32_t xcd_swizzle; // 1: map blocks b, b+8, ... to consecutive tiles (one XCD each)
+  uint32_t num_tiles;
 };
 
 struct DecodeArgs {
@@ -48,13 +50,29 @@ struct SynthArgs {
 };
 
 constexpr uint32_t kTileMaxPayload = 4096;
+// Largest payload accepted: a UDP datagram's size field is 16 bits, and it
+// keeps every per-packet word sum exact in 32 bits (32768 words x 0xFFFF).
+constexpr uint32_t kMaxPayload = 65535;
+
+enum class DecodePath { kBytes, kCopy, kVerify };
+
+// Non-ABI tuning knobs (rudpx_tune in tuning.hip), read at launch.
+struct Tuning {
+  int encode_nt_load = 1;
+  int encode_nt_store = 1;
+  int encode_tile = 0;    // packets per tile; 0 = automatic
+  int encode_unroll = 1;  // phase-2 chunk loop unroll (1 or 2)
+  int decode_glog = -1;   // verify kernel lanes-per-packet log2; -1 = automatic
+  int encode_xcd_swizzle = 0;  // XCD-contiguous tile order (T1)
+};
+Tuning& tuning();
 
 // Tile geometry for a fast-path payload length (L % 16 == 0, 16 <= L <= 4096).
 void encode_tile_geometry(uint32_t L, uint32_t* T, uint32_t* glog);
 uint32_t decode_group_log2(uint32_t L);
 
 int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStream_t stream);
-int launch_decode(const DecodeArgs& args, int layout, bool vec_path, hipStream_t stream);
+int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream_t stream);
 int launch_synth(const SynthArgs& args, hipStream_t stream);
 
 }  // namespace rudp

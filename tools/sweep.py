@@ -1,0 +1,168 @@
+"""Kernel variant sweep on one GPU (interleaved A/B, median of repeats).
+
+Times encode launch-policy variants (rudpx_tune), decode paths, and the
+streaming-copy ceiling, on the BASELINE shapes.  Output: one JSON object.
+usage: python tools/sweep.py [--reps 15] [--only encode|decode|copy]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import statistics
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(REPO), str(REPO / "reliable-udp_amd")]
+
+import torch  # noqa: E402
+
+from rudp import _native, batch  # noqa: E402
+
+lib = _native.lib()
+lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+lib.rudpx_tune.restype = ctypes.c_int
+lib.rudpx_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                           ctypes.c_void_p]
+lib.rudpx_copy.restype = ctypes.c_int
+
+
+def event_ms(fn, reps=1):
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for _ in range(reps):
+        fn()
+    e.record()
+    e.synchronize()
+    return s.elapsed_time(e) / reps
+
+
+def interleaved(variants, reps):
+    """variants: name -> (setup, fn).  Returns name -> median ms."""
+    times = {k: [] for k in variants}
+    for _ in range(reps):
+        for k, (setup, fn) in variants.items():
+            setup()
+            fn()  # warm (and re-apply the setting's kernel)
+            times[k].append(event_ms(fn, 3))
+    return {k: statistics.median(v) for k, v in times.items()}
+
+
+def encode_sweep(reps):
+    out = {}
+    dev = torch.device("cuda", 0)
+    for L, tiles in ((1472, (0,)), (1024, (0,)), (64, (0,))):
+        n = 1 << 20
+        nsets = 1 if L > 512 else 7
+        sets = []
+        for _ in range(nsets):
+            tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
+            sets.append((tab, pay, torch.empty((n, L + 7), dtype=torch.uint8, device=dev)))
+        it = [0]
+
+        def run():
+            tab, pay, fr = sets[it[0] % nsets]
+            it[0] += 1
+            batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
+
+        variants = {}
+        for ntl, nts in ((1, 1), (0, 1), (0, 0)):
+            for tile in tiles:
+                for swz in (0, 1):
+                    def setup(ntl=ntl, nts=nts, tile=tile, swz=swz):
+                        lib.rudpx_tune(0, ntl)
+                        lib.rudpx_tune(1, nts)
+                        lib.rudpx_tune(2, tile)
+                        lib.rudpx_tune(5, swz)
+                    variants[f"L{L}_ntl{ntl}_nts{nts}_tile{tile}_swz{swz}"] = (setup, run)
+        res = interleaved(variants, reps)
+        alg = n * (2 * L + 12)
+        for k, ms in res.items():
+            out[k] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0}
+        del sets
+        torch.cuda.empty_cache()
+    lib.rudpx_tune(0, 1)
+    lib.rudpx_tune(1, 1)
+    lib.rudpx_tune(2, 0)
+    lib.rudpx_tune(3, 1)
+    lib.rudpx_tune(5, 0)
+    return out
+
+
+def decode_sweep(reps):
+    dev = torch.device("cuda", 0)
+    out = {}
+    for L in (1472, 64):
+        n = 1 << 20
+        nsets = 1 if L > 512 else 7
+        frs = []
+        for _ in range(nsets):
+            tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
+            fr, _ = batch.pack_batch(tab, pay, 7)
+            frs.append(fr)
+        pay_out = torch.empty((n, L), dtype=torch.uint8, device=dev)
+        it = [0]
+
+        def verify():
+            batch.unpack_batch(frs[it[0] % nsets], 7)
+            it[0] += 1
+
+        def copy():
+            f = frs[it[0] % nsets]
+            it[0] += 1
+            # copy-out path through the raw ABI with a preallocated output
+            seq = torch.empty(n, dtype=torch.uint16, device=dev)
+            ok = torch.empty(n, dtype=torch.uint8, device=dev)
+            _native.check(lib.rudp_decode(f.data_ptr(), None, L + 7, n, None, seq.data_ptr(),
+                                          seq.data_ptr(), ok.data_ptr(), ok.data_ptr(), None,
+                                          pay_out.data_ptr(), 7, 0,
+                                          torch.cuda.current_stream().cuda_stream))
+        variants = {f"L{L}_copyout": (lambda: None, copy)}
+        for glog in ((-1, 1, 2, 3, 4) if L > 256 else (-1, 1, 2)):
+            variants[f"L{L}_verify_glog{glog}"] = (lambda glog=glog: lib.rudpx_tune(4, glog), verify)
+        res = interleaved(variants, reps)
+        lib.rudpx_tune(4, -1)
+        for k, ms in res.items():
+            alg = n * (L + 13) if "verify" in k else n * (2 * L + 13)
+            out[k] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0}
+        del frs
+        torch.cuda.empty_cache()
+    return out
+
+
+def copy_sweep(reps):
+    dev = torch.device("cuda", 0)
+    nbytes = 1 << 20 << 10 >> 0  # placeholder, replaced below
+    nbytes = (1 << 20) * 1472
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(7)
+    stream = torch.cuda.current_stream().cuda_stream
+    variants = {}
+    for blocks in (1024, 2048, 4096, 16384, 65536):
+        variants[f"copy_blocks{blocks}"] = (
+            lambda: None,
+            lambda blocks=blocks: lib.rudpx_copy(a.data_ptr(), b.data_ptr(), nbytes // 16, blocks, stream))
+    variants["torch_copy_"] = (lambda: None, lambda: b.copy_(a))
+    res = interleaved(variants, reps)
+    return {k: {"ms": ms, "TBs": 2 * nbytes / ms / 1e9} for k, ms in res.items()}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--reps", type=int, default=15)
+    ap.add_argument("--only", choices=["encode", "decode", "copy"])
+    args = ap.parse_args()
+    result = {}
+    if args.only in (None, "copy"):
+        result["copy"] = copy_sweep(args.reps)
+    if args.only in (None, "decode"):
+        result["decode"] = decode_sweep(args.reps)
+    if args.only in (None, "encode"):
+        result["encode"] = encode_sweep(args.reps)
+    print(json.dumps(result, indent=1))
+
+
+if __name__ == "__main__":
+    main()
