@@ -40,7 +40,7 @@ __device__ __forceinline__ void store16(u32x4 v, u32x4* p) {
     *p = v;
 }
 
-template <int H, bool NTL, bool NTS, int UNROLL>
+template <int H, bool NTL, bool NTS, int P1, bool CONTIG>
 __global__ void __launch_bounds__(kBlock) encode_tile_kernel(EncodeTileArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   uint64_t* lds_hdr = reinterpret_cast<uint64_t*>(lds);  // [T + 1]
@@ -70,18 +70,44 @@ __global__ void __launch_bounds__(kBlock) encode_tile_kernel(EncodeTileArgs a) {
   const uint32_t g = tid & (G - 1u);
   const uint32_t V = L >> 4;  // 16 B vectors per packet
   uint32_t sum = 0;
-  if (q < Tv) {
+  if (CONTIG) {
+    // The tile's payload is one contiguous run: stream it like a copy (lane t
+    // takes vectors t, t+256, ...: every wave-instruction reads 1 KiB
+    // contiguous), then sum each packet back out of LDS.
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + p0 * (uint64_t)L);
+    u32x4* dst = reinterpret_cast<u32x4*>(lds_pay + kLdsGuard);
+    const uint32_t nvec = Tv * V;
+    for (uint32_t v0 = tid; v0 < nvec; v0 += (uint32_t)P1 * kBlock) {
+      u32x4 r[P1];
+#pragma unroll
+      for (int u = 0; u < P1; ++u) {
+        const uint32_t v = v0 + (uint32_t)u * kBlock;
+        if (v < nvec) r[u] = load16<NTL>(src + v);
+      }
+#pragma unroll
+      for (int u = 0; u < P1; ++u) {
+        const uint32_t v = v0 + (uint32_t)u * kBlock;
+        if (v < nvec) dst[v] = r[u];
+      }
+    }
+    __syncthreads();
+    if (q < Tv) {
+      const u32x4* mine = dst + q * V;
+      for (uint32_t v = g; v < V; v += G) sum += le16_sum(mine[v]);
+    }
+  } else if (q < Tv) {
     const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + (p0 + q) * (uint64_t)L);
     u32x4* dst = reinterpret_cast<u32x4*>(lds_pay + kLdsGuard + q * L);
-    for (uint32_t v0 = g; v0 < V; v0 += 8u * G) {
-      u32x4 r[8];
+    // P1 loads in flight per lane per round
+    for (uint32_t v0 = g; v0 < V; v0 += (uint32_t)P1 * G) {
+      u32x4 r[P1];
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < P1; ++u) {
         uint32_t v = v0 + (uint32_t)u * G;
         if (v < V) r[u] = load16<NTL>(src + v);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
+      for (int u = 0; u < P1; ++u) {
         uint32_t v = v0 + (uint32_t)u * G;
         if (v < V) {
           sum += le16_sum(r[u]);
@@ -105,7 +131,6 @@ __global__ void __launch_bounds__(kBlock) encode_tile_kernel(EncodeTileArgs a) {
   const uint32_t nbytes = Tv * F;
   unsigned char* out = a.frames + p0 * (uint64_t)F;
   const uint32_t* pay_dw = reinterpret_cast<const uint32_t*>(lds_pay);
-#pragma unroll UNROLL
   for (uint32_t x = tid * 16u; x < nbytes; x += kBlock * 16u) {
     const uint32_t qq = (uint32_t)(((uint64_t)x * a.invF) >> 32);  // x / F
     const uint32_t r = x - qq * F;           // frame position of chunk byte 0
@@ -167,33 +192,49 @@ __global__ void __launch_bounds__(kBlock) encode_bytes_kernel(EncodeTileArgs a) 
   if (lane == 0 && a.csum) a.csum[p] = (uint16_t)c;
 }
 
-template <int H, bool NTL, bool NTS, int UNROLL>
+template <int H, bool NTL, bool NTS, int P1, bool CONTIG>
 int launch_tile(const EncodeTileArgs& args, hipStream_t stream) {
   const uint64_t blocks = (args.n + args.T - 1) / args.T;
-  const size_t lds = args.hdr_bytes + kLdsGuard + (size_t)args.T * args.L + 32;
+  size_t lds = args.hdr_bytes + kLdsGuard + (size_t)args.T * args.L + 32;
+  int per_cu = tuning().encode_blocks_per_cu;
+  // Auto: at most 5 resident tiles per CU for big tiles (>= 16 KiB payload).
+  // Fewer tiles in flight keep the concurrent HBM footprint tighter: 1M x 1472 B
+  // 0.517 ms at 5 per CU vs 0.546 ms at the natural 6 (tools/sweep.py, r01).
+  if (per_cu < 0) per_cu = (size_t)args.T * args.L >= 16384 ? 5 : 0;
+  if (per_cu > 0) {  // reserve LDS to cap resident workgroups per CU
+    const size_t want = ((size_t)(160 * 1024) / (size_t)per_cu) & ~size_t(15);
+    if (want > lds) lds = want;
+  }
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_tile_kernel<H, NTL, NTS, UNROLL>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_tile_kernel<H, NTL, NTS, P1, CONTIG>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL((encode_tile_kernel<H, NTL, NTS, UNROLL>), dim3((uint32_t)blocks), dim3(kBlock), lds,
+  hipLaunchKernelGGL((encode_tile_kernel<H, NTL, NTS, P1, CONTIG>), dim3((uint32_t)blocks), dim3(kBlock), lds,
                      stream, args);
   return (int)hipGetLastError();
 }
 
+template <int H, int P1, bool CONTIG>
+int launch_tile_nt(const EncodeTileArgs& args, hipStream_t stream) {
+  const Tuning& t = tuning();
+  if (t.encode_nt_load && t.encode_nt_store) return launch_tile<H, true, true, P1, CONTIG>(args, stream);
+  if (t.encode_nt_load) return launch_tile<H, true, false, P1, CONTIG>(args, stream);
+  if (t.encode_nt_store) return launch_tile<H, false, true, P1, CONTIG>(args, stream);
+  return launch_tile<H, false, false, P1, CONTIG>(args, stream);
+}
+
 template <int H>
 int launch_tile_policy(const EncodeTileArgs& args, hipStream_t stream) {
-  const Tuning& t = tuning();
-  if (t.encode_unroll == 2) {
-    if (t.encode_nt_load && t.encode_nt_store) return launch_tile<H, true, true, 2>(args, stream);
-    if (t.encode_nt_load) return launch_tile<H, true, false, 2>(args, stream);
-    if (t.encode_nt_store) return launch_tile<H, false, true, 2>(args, stream);
-    return launch_tile<H, false, false, 2>(args, stream);
+  const int p1 = tuning().encode_p1;
+  if (tuning().encode_contig) {
+    if (p1 == 2) return launch_tile_nt<H, 2, true>(args, stream);
+    if (p1 == 4) return launch_tile_nt<H, 4, true>(args, stream);
+    return launch_tile_nt<H, 8, true>(args, stream);
   }
-  if (t.encode_nt_load && t.encode_nt_store) return launch_tile<H, true, true, 1>(args, stream);
-  if (t.encode_nt_load) return launch_tile<H, true, false, 1>(args, stream);
-  if (t.encode_nt_store) return launch_tile<H, false, true, 1>(args, stream);
-  return launch_tile<H, false, false, 1>(args, stream);
+  if (p1 == 2) return launch_tile_nt<H, 2, false>(args, stream);
+  if (p1 == 4) return launch_tile_nt<H, 4, false>(args, stream);
+  return launch_tile_nt<H, 8, false>(args, stream);
 }
 
 int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStream_t stream) {

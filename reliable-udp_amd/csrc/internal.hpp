@@ -61,9 +61,11 @@ struct Tuning {
   int encode_nt_load = 1;
   int encode_nt_store = 1;
   int encode_tile = 0;    // packets per tile; 0 = automatic
-  int encode_unroll = 1;  // phase-2 chunk loop unroll (1 or 2)
+  int encode_p1 = 8;      // phase-1 loads in flight per lane (2, 4, 8)
+  int encode_blocks_per_cu = -1;  // cap resident tiles per CU via LDS reservation; 0 = natural, -1 = auto
   int decode_glog = -1;   // verify kernel lanes-per-packet log2; -1 = automatic
   int encode_xcd_swizzle = 0;  // XCD-contiguous tile order (T1)
+  int encode_contig = 1;  // phase 1 streams the tile contiguously, sums from LDS
 };
 Tuning& tuning();
 

@@ -21,19 +21,71 @@ __global__ void __launch_bounds__(kBlock) copy_kernel(const u32x4* __restrict__ 
     __builtin_nontemporal_store(__builtin_nontemporal_load(src + i), dst + i);
 }
 
+// Each thread moves VPT vectors: all loads first, then all stores.
+template <int VPT, int POLICY>
+__global__ void __launch_bounds__(kBlock) copy_vpt_kernel(const u32x4* __restrict__ src,
+                                                          u32x4* __restrict__ dst, uint64_t n16) {
+  const uint64_t base = (uint64_t)blockIdx.x * kBlock * VPT + threadIdx.x;
+  u32x4 v[VPT];
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const uint64_t i = base + (uint64_t)k * kBlock;
+    if (i < n16) v[k] = POLICY ? __builtin_nontemporal_load(src + i) : src[i];
+  }
+#pragma unroll
+  for (int k = 0; k < VPT; ++k) {
+    const uint64_t i = base + (uint64_t)k * kBlock;
+    if (i < n16) {
+      if (POLICY) __builtin_nontemporal_store(v[k], dst + i);
+      else dst[i] = v[k];
+    }
+  }
+}
+
+template <int VPT, int POLICY>
+int launch_copy_vpt(const void* src, void* dst, uint64_t n16, hipStream_t s) {
+  const uint64_t blocks = (n16 + (uint64_t)kBlock * VPT - 1) / ((uint64_t)kBlock * VPT);
+  hipLaunchKernelGGL((copy_vpt_kernel<VPT, POLICY>), dim3((uint32_t)blocks), dim3(kBlock), 0, s,
+                     (const u32x4*)src, (u32x4*)dst, n16);
+  return (int)hipGetLastError();
+}
+
 }  // namespace rudp
 
 extern "C" {
 
+// Copy with VPT (1, 2, 4, 8, 16) vectors per thread, loads before stores;
+// policy 1 = non-temporal, 0 = default.
+int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy, void* stream) {
+  hipStream_t s = (hipStream_t)stream;
+  using namespace rudp;
+  switch (vpt * 2 + (policy ? 1 : 0)) {
+    case 2: return launch_copy_vpt<1, 0>(src, dst, n16, s);
+    case 3: return launch_copy_vpt<1, 1>(src, dst, n16, s);
+    case 4: return launch_copy_vpt<2, 0>(src, dst, n16, s);
+    case 5: return launch_copy_vpt<2, 1>(src, dst, n16, s);
+    case 8: return launch_copy_vpt<4, 0>(src, dst, n16, s);
+    case 9: return launch_copy_vpt<4, 1>(src, dst, n16, s);
+    case 16: return launch_copy_vpt<8, 0>(src, dst, n16, s);
+    case 17: return launch_copy_vpt<8, 1>(src, dst, n16, s);
+    case 32: return launch_copy_vpt<16, 0>(src, dst, n16, s);
+    case 33: return launch_copy_vpt<16, 1>(src, dst, n16, s);
+    default: return -22;
+  }
+}
+
 // key 0: encode non-temporal loads (0/1); 1: non-temporal stores (0/1);
-// 2: packets per encode tile (power of two 16..256, 0 = auto); 3: encode phase-2
-// unroll (1, 2); 4: decode-verify log2 lanes per packet (1..4, -1 = auto).
+// 2: packets per encode tile (power of two 16..256, 0 = auto); 3: encode phase-1
+// loads in flight per lane (2, 4, 8); 4: decode-verify log2 lanes per packet
+// (1..4, -1 = auto); 5: XCD-contiguous tile order; 6: encode tiles per CU cap;
+// 7: contiguous phase-1 stream with checksums summed from LDS.
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
   int* slot = key == 0 ? &t.encode_nt_load : key == 1 ? &t.encode_nt_store
-            : key == 2 ? &t.encode_tile : key == 3 ? &t.encode_unroll
-            : key == 4 ? &t.decode_glog : key == 5 ? &t.encode_xcd_swizzle : nullptr;
+            : key == 2 ? &t.encode_tile : key == 3 ? &t.encode_p1
+            : key == 4 ? &t.decode_glog : key == 5 ? &t.encode_xcd_swizzle
+            : key == 6 ? &t.encode_blocks_per_cu : key == 7 ? &t.encode_contig : nullptr;
   if (!slot) return -22;
   const int old = *slot;
   *slot = value;

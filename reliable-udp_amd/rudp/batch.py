@@ -185,7 +185,14 @@ def _ptr(a) -> Optional[int]:
     return a.ctypes.data if a.size else None
 
 
-def _pack_host(tab: HeaderTable, payloads, H, want_csum, device):
+def _host_out(a, name, dtype, shape):
+    if not isinstance(a, np.ndarray) or a.dtype != dtype or a.shape != shape \
+            or not a.flags["C_CONTIGUOUS"] or not a.flags["WRITEABLE"]:
+        raise ValueError(f"{name} must be a writeable C-contiguous {np.dtype(dtype)} array of shape {shape}")
+    return a
+
+
+def _pack_host(tab: HeaderTable, payloads, H, want_csum, device, out=None, csum_out=None):
     payloads = _host_arr(payloads, "payloads", np.uint8, 2)
     n, L = payloads.shape
     seq = _host_arr(tab.seq, "seq", np.uint16, 1)
@@ -194,8 +201,12 @@ def _pack_host(tab: HeaderTable, payloads, H, want_csum, device):
     for name, a in (("seq", seq), ("ack", ack), ("flags", flags)):
         if a.shape[0] != n:
             raise ValueError(f"{name} has {a.shape[0]} entries for {n} payloads")
-    frames = np.empty((n, L + H), dtype=np.uint8)
-    csum = np.empty((n,), dtype=np.uint16) if want_csum else None
+    frames = (_host_out(out, "out", np.uint8, (n, L + H)) if out is not None
+              else np.empty((n, L + H), dtype=np.uint8))
+    if csum_out is not None:
+        csum = _host_out(csum_out, "csum_out", np.uint16, (n,))
+    else:
+        csum = np.empty((n,), dtype=np.uint16) if want_csum else None
     b = _native.RudpBatch(n=n, payload_len=L, reserved=0, seq=_ptr(seq), ack=_ptr(ack),
                           flags=_ptr(flags), payload=_ptr(payloads), len=None, payload_off=None)
     _native.check(_native.lib().rudp_encode_host(
@@ -245,9 +256,7 @@ def pack_batch(headers, payloads, layout: Union[str, int] = "rudp7", *, out=None
         want_csum = H == 5
     if _is_torch(payloads):
         return _pack_device(tab, payloads, H, out, csum_out, want_csum, stream)
-    if out is not None or csum_out is not None:
-        raise ValueError("out=/csum_out= are only supported on the device path")
-    return _pack_host(tab, payloads, H, want_csum, device)
+    return _pack_host(tab, payloads, H, want_csum, device, out, csum_out)
 
 
 def unpack_batch(frames, layout: Union[str, int] = "rudp7", *, csum=None,

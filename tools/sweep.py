@@ -26,6 +26,9 @@ lib.rudpx_tune.restype = ctypes.c_int
 lib.rudpx_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                            ctypes.c_void_p]
 lib.rudpx_copy.restype = ctypes.c_int
+lib.rudpx_copy_vpt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                               ctypes.c_int, ctypes.c_void_p]
+lib.rudpx_copy_vpt.restype = ctypes.c_int
 
 
 def event_ms(fn, reps=1):
@@ -67,26 +70,35 @@ def encode_sweep(reps):
             batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
 
         variants = {}
-        for ntl, nts in ((1, 1), (0, 1), (0, 0)):
-            for tile in tiles:
-                for swz in (0, 1):
-                    def setup(ntl=ntl, nts=nts, tile=tile, swz=swz):
-                        lib.rudpx_tune(0, ntl)
-                        lib.rudpx_tune(1, nts)
-                        lib.rudpx_tune(2, tile)
-                        lib.rudpx_tune(5, swz)
-                    variants[f"L{L}_ntl{ntl}_nts{nts}_tile{tile}_swz{swz}"] = (setup, run)
+        for contig in (1,):
+            for p1 in (8, 4):
+                for per_cu in (-1, 0, 4, 6):
+                    def setup(contig=contig, p1=p1, per_cu=per_cu):
+                        lib.rudpx_tune(7, contig)
+                        lib.rudpx_tune(3, p1)
+                        lib.rudpx_tune(6, per_cu)
+                    variants[f"L{L}_contig{contig}_p1{p1}_percu{per_cu}"] = (setup, run)
         res = interleaved(variants, reps)
         alg = n * (2 * L + 12)
-        for k, ms in res.items():
-            out[k] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0}
+        # every variant must produce the default kernel's frames bit for bit
+        tab0, pay0, _ = sets[0]
+        lib.rudpx_tune(7, 0), lib.rudpx_tune(3, 8), lib.rudpx_tune(6, 0)
+        want, _ = batch.pack_batch(tab0, pay0, 7)  # the original per-packet phase 1
+        for k, (setup, _) in variants.items():
+            setup()
+            got, _ = batch.pack_batch(tab0, pay0, 7)
+            res[k] = (res[k], bool(torch.equal(got, want)))
+        for k, (ms, same) in res.items():
+            out[k] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0, "exact": same}
         del sets
         torch.cuda.empty_cache()
     lib.rudpx_tune(0, 1)
     lib.rudpx_tune(1, 1)
     lib.rudpx_tune(2, 0)
-    lib.rudpx_tune(3, 1)
+    lib.rudpx_tune(3, 8)
     lib.rudpx_tune(5, 0)
+    lib.rudpx_tune(6, -1)
+    lib.rudpx_tune(7, 1)
     return out
 
 
@@ -145,6 +157,12 @@ def copy_sweep(reps):
             lambda: None,
             lambda blocks=blocks: lib.rudpx_copy(a.data_ptr(), b.data_ptr(), nbytes // 16, blocks, stream))
     variants["torch_copy_"] = (lambda: None, lambda: b.copy_(a))
+    for vpt in (1, 2, 4, 8, 16):
+        for pol in (0, 1):
+            variants[f"copy_vpt{vpt}_nt{pol}"] = (
+                lambda: None,
+                lambda vpt=vpt, pol=pol: lib.rudpx_copy_vpt(a.data_ptr(), b.data_ptr(), nbytes // 16,
+                                                            vpt, pol, stream))
     res = interleaved(variants, reps)
     return {k: {"ms": ms, "TBs": 2 * nbytes / ms / 1e9} for k, ms in res.items()}
 
