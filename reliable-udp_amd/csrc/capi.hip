@@ -119,47 +119,99 @@ int validate_decode(const void* frames, const void* frame_off, uint32_t frame_le
   return 0;
 }
 
-// ---- per-device staging cache for the *_host variants ---------------------
-struct DeviceStage {
+// ---- host-staged pipeline for the *_host variants ---------------------------
+// Chunks of the batch cycle through S device slots.  Three streams, one per
+// engine: H2D copies, kernels, D2H copies; events chain chunk k's three steps
+// and hold a slot until its D2H has drained.  So the H2D of chunk k+1, the
+// kernel of chunk k and the D2H of chunk k-1 run at the same time.
+constexpr int kMaxSlots = 8;
+
+struct Pipeline {
   std::mutex mu;
   bool init = false;
-  hipStream_t stream[2] = {nullptr, nullptr};
-  void* dbuf[2] = {nullptr, nullptr};
+  hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
+  hipEvent_t in_ready[kMaxSlots], out_ready[kMaxSlots], slot_free[kMaxSlots];
+  void* dbuf[kMaxSlots] = {};
   size_t bytes = 0;
+  int slots = 0;
 };
 
-std::mutex g_stage_mu;
-std::vector<DeviceStage*> g_stage;
+std::mutex g_pipe_mu;
+std::vector<Pipeline*> g_pipe;
 
-DeviceStage* stage_for(int device) {
-  std::lock_guard<std::mutex> lk(g_stage_mu);
-  if ((int)g_stage.size() <= device) g_stage.resize(device + 1, nullptr);
-  if (!g_stage[device]) g_stage[device] = new DeviceStage();  // lives for the process
-  return g_stage[device];
+Pipeline* pipeline_for(int device) {
+  std::lock_guard<std::mutex> lk(g_pipe_mu);
+  if ((int)g_pipe.size() <= device) g_pipe.resize(device + 1, nullptr);
+  if (!g_pipe[device]) g_pipe[device] = new Pipeline();  // lives for the process
+  return g_pipe[device];
 }
 
-int stage_reserve(DeviceStage* st, size_t bytes) {
-  if (!st->init) {
-    for (int i = 0; i < 2; ++i) RUDP_HIP(hipStreamCreateWithFlags(&st->stream[i], hipStreamNonBlocking));
-    st->init = true;
+int pipeline_reserve(Pipeline* pp, int slots, size_t bytes) {
+  if (!pp->init) {
+    RUDP_HIP(hipStreamCreateWithFlags(&pp->h2d, hipStreamNonBlocking));
+    RUDP_HIP(hipStreamCreateWithFlags(&pp->comp, hipStreamNonBlocking));
+    RUDP_HIP(hipStreamCreateWithFlags(&pp->d2h, hipStreamNonBlocking));
+    for (int i = 0; i < kMaxSlots; ++i) {
+      RUDP_HIP(hipEventCreateWithFlags(&pp->in_ready[i], hipEventDisableTiming));
+      RUDP_HIP(hipEventCreateWithFlags(&pp->out_ready[i], hipEventDisableTiming));
+      RUDP_HIP(hipEventCreateWithFlags(&pp->slot_free[i], hipEventDisableTiming));
+    }
+    pp->init = true;
   }
-  if (st->bytes >= bytes) return 0;
-  for (int i = 0; i < 2; ++i) {
-    if (st->dbuf[i]) RUDP_HIP(hipFree(st->dbuf[i]));
-    st->dbuf[i] = nullptr;
+  if (pp->bytes >= bytes && pp->slots >= slots) return 0;
+  for (int i = 0; i < kMaxSlots; ++i) {
+    if (pp->dbuf[i]) RUDP_HIP(hipFree(pp->dbuf[i]));
+    pp->dbuf[i] = nullptr;
   }
-  st->bytes = 0;
-  for (int i = 0; i < 2; ++i) {
-    hipError_t e = hipMalloc(&st->dbuf[i], bytes);
+  pp->bytes = 0;
+  pp->slots = 0;
+  for (int i = 0; i < slots; ++i) {
+    hipError_t e = hipMalloc(&pp->dbuf[i], bytes);
     if (e != hipSuccess) return fail(RUDP_ENOMEM, "staging hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
   }
-  st->bytes = bytes;
+  pp->bytes = bytes;
+  pp->slots = slots;
   return 0;
 }
 
 size_t up256(size_t x) { return (x + 255u) & ~size_t(255); }
 
-constexpr uint64_t kStageBytes = 64ull << 20;  // per-slot input+output budget
+// Packets per chunk for a given per-packet staging footprint.
+uint64_t chunk_packets(uint64_t n, uint64_t bytes_per_packet) {
+  const int mb = tuning().host_stage_mb;
+  uint64_t cn = ((uint64_t)(mb > 0 ? mb : 32) << 20) / (bytes_per_packet ? bytes_per_packet : 1);
+  if (cn < 64) cn = 64;
+  return cn > n ? n : cn;
+}
+
+int pipeline_slots() {
+  const int s = tuning().host_slots;
+  return s < 2 ? 2 : s > kMaxSlots ? kMaxSlots : s;
+}
+
+// Drive chunks [0, n) in steps of cn through the pipeline.  The three
+// callbacks enqueue chunk work on the stream they are given.
+template <class H2D, class KERN, class D2H>
+int run_pipeline(Pipeline* pp, uint64_t n, uint64_t cn, H2D h2d, KERN kern, D2H d2h) {
+  const int S = pp->slots;
+  for (uint64_t p0 = 0, k = 0; p0 < n; p0 += cn, ++k) {
+    const uint64_t m = (n - p0) < cn ? (n - p0) : cn;
+    const int s = (int)(k % (uint64_t)S);
+    char* base = (char*)pp->dbuf[s];
+    if (k >= (uint64_t)S) RUDP_HIP(hipStreamWaitEvent(pp->h2d, pp->slot_free[s], 0));
+    int rc = h2d(base, p0, m, pp->h2d);
+    if (rc) return rc;
+    RUDP_HIP(hipEventRecord(pp->in_ready[s], pp->h2d));
+    RUDP_HIP(hipStreamWaitEvent(pp->comp, pp->in_ready[s], 0));
+    if ((rc = kern(base, p0, m, pp->comp))) return rc;
+    RUDP_HIP(hipEventRecord(pp->out_ready[s], pp->comp));
+    RUDP_HIP(hipStreamWaitEvent(pp->d2h, pp->out_ready[s], 0));
+    if ((rc = d2h(base, p0, m, pp->d2h))) return rc;
+    RUDP_HIP(hipEventRecord(pp->slot_free[s], pp->d2h));
+  }
+  RUDP_HIP(hipStreamSynchronize(pp->d2h));
+  return 0;
+}
 
 }  // namespace
 
@@ -296,38 +348,38 @@ int rudp_encode_host(const rudp_batch* h_in, uint8_t* h_frames, uint16_t* h_csum
   const uint64_t n = h_in->n;
   const uint64_t L = h_in->payload_len;
   const uint64_t F = L + (uint64_t)layout;
-  uint64_t cn = kStageBytes / (L + F + 8);
-  if (cn < 64) cn = 64;
-  if (cn > n) cn = n;
+  const uint64_t cn = chunk_packets(n, L + F + 7);
   // Slot layout: payload | frames | seq | ack | flags | csum.
   const size_t o_pay = 0, o_fr = up256(cn * L), o_seq = o_fr + up256(cn * F),
                o_ack = o_seq + up256(cn * 2), o_fl = o_ack + up256(cn * 2),
                o_cs = o_fl + up256(cn), slot = o_cs + up256(cn * 2);
-  DeviceStage* st = stage_for(device);
-  std::lock_guard<std::mutex> lk(st->mu);
-  if ((rc = stage_reserve(st, slot))) return rc;
-  for (uint64_t p0 = 0, k = 0; p0 < n; p0 += cn, ++k) {
-    const uint64_t m = (n - p0) < cn ? (n - p0) : cn;
-    const int b = (int)(k & 1);
-    hipStream_t s = st->stream[b];
-    char* base = (char*)st->dbuf[b];
+  Pipeline* pp = pipeline_for(device);
+  std::lock_guard<std::mutex> lk(pp->mu);
+  if ((rc = pipeline_reserve(pp, pipeline_slots(), slot))) return rc;
+  auto h2d = [&](char* base, uint64_t p0, uint64_t m, hipStream_t s) -> int {
     if (L) RUDP_HIP(hipMemcpyAsync(base + o_pay, h_in->payload + p0 * L, m * L, hipMemcpyHostToDevice, s));
     RUDP_HIP(hipMemcpyAsync(base + o_seq, h_in->seq + p0, m * 2, hipMemcpyHostToDevice, s));
     RUDP_HIP(hipMemcpyAsync(base + o_ack, h_in->ack + p0, m * 2, hipMemcpyHostToDevice, s));
     RUDP_HIP(hipMemcpyAsync(base + o_fl, h_in->flags + p0, m, hipMemcpyHostToDevice, s));
+    return 0;
+  };
+  auto kern = [&](char* base, uint64_t, uint64_t m, hipStream_t s) -> int {
     rudp_batch sub = *h_in;
     sub.n = m;
     sub.seq = (const uint16_t*)(base + o_seq);
     sub.ack = (const uint16_t*)(base + o_ack);
     sub.flags = (const uint8_t*)(base + o_fl);
     sub.payload = (const uint8_t*)(base + o_pay);
-    uint16_t* dcs = h_csum_or_null ? (uint16_t*)(base + o_cs) : nullptr;
-    if ((rc = rudp_encode(&sub, (uint8_t*)(base + o_fr), dcs, layout, device, s))) return rc;
+    return rudp_encode(&sub, (uint8_t*)(base + o_fr), h_csum_or_null ? (uint16_t*)(base + o_cs) : nullptr,
+                       layout, device, s);
+  };
+  auto d2h = [&](char* base, uint64_t p0, uint64_t m, hipStream_t s) -> int {
     RUDP_HIP(hipMemcpyAsync(h_frames + p0 * F, base + o_fr, m * F, hipMemcpyDeviceToHost, s));
-    if (dcs) RUDP_HIP(hipMemcpyAsync(h_csum_or_null + p0, dcs, m * 2, hipMemcpyDeviceToHost, s));
-  }
-  for (int i = 0; i < 2; ++i) RUDP_HIP(hipStreamSynchronize(st->stream[i]));
-  return 0;
+    if (h_csum_or_null)
+      RUDP_HIP(hipMemcpyAsync(h_csum_or_null + p0, base + o_cs, m * 2, hipMemcpyDeviceToHost, s));
+    return 0;
+  };
+  return run_pipeline(pp, n, cn, h2d, kern, d2h);
 }
 
 int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
@@ -340,44 +392,39 @@ int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
   const uint64_t F = frame_len;
   const uint64_t L = F > (uint64_t)layout ? F - (uint64_t)layout : 0;
   uint8_t* h_pay = L ? h_payload_out_or_null : nullptr;
-  uint64_t cn = kStageBytes / (F + L + 16);
-  if (cn < 64) cn = 64;
-  if (cn > n) cn = n;
+  const uint64_t cn = chunk_packets(n, F + (h_pay ? L : 0) + 10);
   // Slot layout: frames | payload | seq | ack | flags | ok | csum_in | csum_out.
-  const size_t o_fr = 0, o_pay = up256(cn * F), o_seq = o_pay + up256(cn * L),
+  const size_t o_fr = 0, o_pay = up256(cn * F), o_seq = o_pay + up256(h_pay ? cn * L : 0),
                o_ack = o_seq + up256(cn * 2), o_fl = o_ack + up256(cn * 2),
                o_ok = o_fl + up256(cn), o_ci = o_ok + up256(cn), o_co = o_ci + up256(cn * 2),
                slot = o_co + up256(cn * 2);
-  DeviceStage* st = stage_for(device);
-  std::lock_guard<std::mutex> lk(st->mu);
-  if ((rc = stage_reserve(st, slot))) return rc;
-  for (uint64_t p0 = 0, k = 0; p0 < n; p0 += cn, ++k) {
-    const uint64_t m = (n - p0) < cn ? (n - p0) : cn;
-    const int b = (int)(k & 1);
-    hipStream_t s = st->stream[b];
-    char* base = (char*)st->dbuf[b];
+  Pipeline* pp = pipeline_for(device);
+  std::lock_guard<std::mutex> lk(pp->mu);
+  if ((rc = pipeline_reserve(pp, pipeline_slots(), slot))) return rc;
+  auto h2d = [&](char* base, uint64_t p0, uint64_t m, hipStream_t s) -> int {
     if (F) RUDP_HIP(hipMemcpyAsync(base + o_fr, h_frames + p0 * F, m * F, hipMemcpyHostToDevice, s));
-    const uint16_t* dci = nullptr;
-    if (h_csum_in_or_null) {
+    if (h_csum_in_or_null)
       RUDP_HIP(hipMemcpyAsync(base + o_ci, h_csum_in_or_null + p0, m * 2, hipMemcpyHostToDevice, s));
-      dci = (const uint16_t*)(base + o_ci);
-    }
-    uint16_t* dco = h_csum_out_or_null ? (uint16_t*)(base + o_co) : nullptr;
-    uint8_t* dpay = h_pay ? (uint8_t*)(base + o_pay) : nullptr;
-    if ((rc = rudp_decode((const uint8_t*)(base + o_fr), nullptr, frame_len, m, dci,
-                          (uint16_t*)(base + o_seq), (uint16_t*)(base + o_ack),
-                          (uint8_t*)(base + o_fl), (uint8_t*)(base + o_ok), dco, dpay, layout,
-                          device, s)))
-      return rc;
+    return 0;
+  };
+  auto kern = [&](char* base, uint64_t, uint64_t m, hipStream_t s) -> int {
+    return rudp_decode((const uint8_t*)(base + o_fr), nullptr, frame_len, m,
+                       h_csum_in_or_null ? (const uint16_t*)(base + o_ci) : nullptr,
+                       (uint16_t*)(base + o_seq), (uint16_t*)(base + o_ack), (uint8_t*)(base + o_fl),
+                       (uint8_t*)(base + o_ok), h_csum_out_or_null ? (uint16_t*)(base + o_co) : nullptr,
+                       h_pay ? (uint8_t*)(base + o_pay) : nullptr, layout, device, s);
+  };
+  auto d2h = [&](char* base, uint64_t p0, uint64_t m, hipStream_t s) -> int {
     RUDP_HIP(hipMemcpyAsync(h_seq + p0, base + o_seq, m * 2, hipMemcpyDeviceToHost, s));
     RUDP_HIP(hipMemcpyAsync(h_ack + p0, base + o_ack, m * 2, hipMemcpyDeviceToHost, s));
     RUDP_HIP(hipMemcpyAsync(h_flags + p0, base + o_fl, m, hipMemcpyDeviceToHost, s));
     RUDP_HIP(hipMemcpyAsync(h_ok + p0, base + o_ok, m, hipMemcpyDeviceToHost, s));
-    if (dco) RUDP_HIP(hipMemcpyAsync(h_csum_out_or_null + p0, dco, m * 2, hipMemcpyDeviceToHost, s));
-    if (dpay) RUDP_HIP(hipMemcpyAsync(h_pay + p0 * L, dpay, m * L, hipMemcpyDeviceToHost, s));
-  }
-  for (int i = 0; i < 2; ++i) RUDP_HIP(hipStreamSynchronize(st->stream[i]));
-  return 0;
+    if (h_csum_out_or_null)
+      RUDP_HIP(hipMemcpyAsync(h_csum_out_or_null + p0, base + o_co, m * 2, hipMemcpyDeviceToHost, s));
+    if (h_pay) RUDP_HIP(hipMemcpyAsync(h_pay + p0 * L, base + o_pay, m * L, hipMemcpyDeviceToHost, s));
+    return 0;
+  };
+  return run_pipeline(pp, n, cn, h2d, kern, d2h);
 }
 
 }  // extern "C"
