@@ -201,6 +201,33 @@ def legs(torch, batch, device, steps):
     return out
 
 
+def config1_loopback():
+    """BASELINE config 1: client -> server over 127.0.0.1, stop-and-wait, 1 char per
+    datagram (rudp.transport over the drop-in Packet; no GPU).  Message = bin/input.txt
+    (recorded in tests/golden/wire_trace.json), plus a 2000-char message for a rate."""
+    import threading
+    from rudp.transport import ReliableUDP
+    msg = json.loads((REPO / "tests" / "golden" / "wire_trace.json").read_text())["message"]
+    out = {}
+    for name, m in (("input_txt", msg), ("2000_chars", "x" * 2000)):
+        server = ReliableUDP().create()
+        server.bind("127.0.0.1", 0)
+        port = server.socket.getsockname()[1]
+        got = {}
+        t = threading.Thread(target=lambda: got.setdefault("m", server.recv()), daemon=True)
+        t.start()
+        time.sleep(0.05)  # recv() flushes its socket first (reliableUDP.py:112): let it get there
+        client = ReliableUDP(timeout=1).create()
+        t0 = time.perf_counter()
+        client.send(m, "127.0.0.1", port)
+        t.join(timeout=60)
+        dt = time.perf_counter() - t0
+        client.close()
+        server.close()
+        out[name] = {"ok": got.get("m") == m, "wall_ms": dt * 1e3, "chars_per_s": len(m) / dt}
+    return out
+
+
 def read_pmc_traffic(L, n):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
     path = REPO / "profiles" / "pmc_encode.json"
@@ -235,6 +262,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(args.payload, args.cpu_packets, args.cpu_workers)
+        cpu["config1_loopback"] = config1_loopback()
 
     import torch
     import torch.distributed as dist
