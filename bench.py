@@ -251,6 +251,8 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1))
     ap.add_argument("--cpu-packets", type=int, default=1 << 14, help="packets per CPU worker")
+    ap.add_argument("--share-device", action="store_true",
+                    help="testing only: every rank uses cuda:0 and gloo (rehearse N>1 on one GPU)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -268,10 +270,14 @@ def main():
     import torch.distributed as dist
     from rudp import batch
 
-    torch.cuda.set_device(local_rank)
-    device = torch.device("cuda", local_rank)
+    dev_index = 0 if args.share_device else local_rank
+    torch.cuda.set_device(dev_index)
+    device = torch.device("cuda", dev_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=device)
+        if args.share_device:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=device)
 
     n, L = args.packets, args.payload
     seed = SEEDS.get(L, 0x5EED0004)
@@ -295,7 +301,8 @@ def main():
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
     kernel_ms = start.elapsed_time(stop)
-    t = torch.tensor([wall], dtype=torch.float64, device=device)
+    t = torch.tensor([wall], dtype=torch.float64,
+                     device="cpu" if args.share_device else device)
     if world > 1:
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())

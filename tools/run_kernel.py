@@ -1,0 +1,63 @@
+"""Run one codec op repeatedly on one shape, for rocprofv3 captures.
+
+usage: python tools/run_kernel.py --op encode|decode|roundtrip [--L 1472] [--n 1048576]
+          [--layout rudp7] [--steps 20]
+Prints the HIP-event time per launch so it can be set beside the profiler's
+kernel-trace average.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(REPO), str(REPO / "reliable-udp_amd")]
+
+import torch  # noqa: E402
+
+from rudp import batch  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--op", choices=["encode", "decode", "roundtrip"], default="encode")
+    ap.add_argument("--L", type=int, default=1472)
+    ap.add_argument("--n", type=int, default=1 << 20)
+    ap.add_argument("--layout", default="rudp7")
+    ap.add_argument("--steps", type=int, default=20)
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    H = batch.layout_header_len(args.layout)
+    per_set = args.n * (2 * args.L + H + 5)
+    nsets = max(1, min(8, math.ceil((1 << 30) / per_set)))
+    sets = []
+    for _ in range(nsets):
+        tab, pay = batch.synth_batch(args.n, args.L, 0x5EED0004, device=dev)
+        fr, _ = batch.pack_batch(tab, pay, args.layout)
+        sets.append((tab, pay, fr))
+
+    def step(i):
+        tab, pay, fr = sets[i % nsets]
+        if args.op in ("encode", "roundtrip"):
+            batch.pack_batch(tab, pay, args.layout, out=fr, want_csum=False)
+        if args.op in ("decode", "roundtrip"):
+            batch.unpack_batch(fr, args.layout)
+
+    for i in range(3):
+        step(i)
+    torch.cuda.synchronize()
+    s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    s.record()
+    for i in range(args.steps):
+        step(i)
+    e.record()
+    e.synchronize()
+    print(json.dumps({"op": args.op, "L": args.L, "n": args.n, "layout": args.layout,
+                      "buffer_sets": nsets, "ms_per_launch": s.elapsed_time(e) / args.steps}))
+
+
+if __name__ == "__main__":
+    main()
