@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RUDP_ABI_VERSION 1
+#define RUDP_ABI_VERSION 2
 
 /* Frame layouts: the value is the header length in bytes. */
 #define RUDP_LAYOUT_RUDP5 5 /* reference-exact 5-byte header, checksum sideband */
@@ -60,9 +60,11 @@ extern "C" {
 
 /*
  * A batch of packets to frame: the SoA header table plus payload bytes.
- * Fixed-length batches: payload is n*payload_len contiguous bytes and
- * len/payload_off are NULL.  (Variable-length batches are rejected with
- * RUDP_ENOTSUP in ABI version 1.)
+ * Fixed-length batches (rudp_encode): payload is n*payload_len contiguous
+ * bytes and len/payload_off are NULL.  Variable-length batches
+ * (rudp_encode_varlen): len[i] payload bytes of packet i (<= 65535) start at
+ * payload[payload_off[i]], or, with payload_off NULL, the payloads are packed
+ * back to back in packet order; payload_len is ignored.
  *   seq   -> custom_header["seq_num"]  (utils/packet.py:4)
  *   ack   -> custom_header["ack_num"]  (utils/packet.py:5)
  *   flags -> header byte 4 verbatim: syn/ack/fin/offset (utils/packet.py:6-9)
@@ -75,8 +77,8 @@ typedef struct rudp_batch {
   const uint16_t* ack;
   const uint8_t* flags;
   const uint8_t* payload;
-  const uint32_t* len;          /* reserved for variable-length batches */
-  const uint64_t* payload_off;  /* reserved for variable-length batches */
+  const uint32_t* len;          /* variable-length batches: payload bytes per packet */
+  const uint64_t* payload_off;  /* variable-length batches: payload start, or NULL = packed */
 } rudp_batch;
 
 /*
@@ -98,8 +100,11 @@ int rudp_encode(const rudp_batch* in, uint8_t* d_frames, uint16_t* d_csum_or_nul
  * Replaces, per packet, utils/reliableUDP.py:118-123 / :67-73
  * (Packet(data); get_header_field x N; get_payload), i.e.
  * utils/packet.py:16, :29-40, :68-73.
- * d_frame_off_or_null must be NULL in ABI version 1 (frames packed at
- * stride frame_len).  d_csum_in_or_null: rudp5 sideband checksums to verify
+ * Fixed-length frames: d_frame_off_or_null = NULL, frames at stride
+ * frame_len.  Variable-length frames: d_frame_off_or_null = n+1 offsets
+ * (frame i = d_frames[off[i], off[i+1]), as rudp_encode_varlen writes them),
+ * frame_len is ignored and the payload is zero-copy only
+ * (d_payload_out_or_null must be NULL).  d_csum_in_or_null: rudp5 sideband checksums to verify
  * (NULL: d_ok = RUDP_OK_UNVERIFIED).  d_csum_out_or_null: the recomputed
  * checksum per packet.  d_payload_out_or_null: n*(frame_len-layout) bytes,
  * payloads copied out aligned; NULL = zero-copy (view at frame offset layout).
@@ -113,9 +118,30 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
                 int layout, int device, void* hip_stream);
 
 /*
+ * Frame + checksum a device-resident VARIABLE-LENGTH batch (in->len set).
+ * The reference's own traffic: one UTF-8 character per datagram, 5-9 byte
+ * frames (utils/reliableUDP.py:11, :53-61).  d_frame_off receives n+1
+ * offsets, the exclusive scan of len[i] + layout (d_frame_off[n] = total
+ * bytes); d_frames must hold sum(len) + n*layout bytes.  The concatenated
+ * frames equal N calls of Packet(...).to_byte() back to back.
+ */
+int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_frame_off,
+                       uint16_t* d_csum_or_null, int layout, int device, void* hip_stream);
+
+/*
+ * Strict UTF-8 check of each frame's payload: d_valid[i] = 1 when
+ * Packet(frame).get_payload() would return (utils/packet.py:68-73: empty
+ * payload -> None; else bytes.decode(), strict UTF-8), 0 when it would raise
+ * UnicodeDecodeError.  Frames as in rudp_decode (fixed stride or offsets).
+ */
+int rudp_validate_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
+                       uint32_t frame_len, uint64_t n, int layout, uint8_t* d_valid, int device,
+                       void* hip_stream);
+
+/*
  * Host-memory conveniences: same semantics, host pointers in and out.
- * Staged through device buffers in chunks with H2D / kernel / D2H
- * overlapped on two streams.  Synchronous.  These model the reference's
+ * Staged through a ring of device slots in chunks, with H2D, kernel and D2H
+ * on three streams chained by events so the three overlap.  Synchronous.  These model the reference's
  * real boundary, a UDP socket buffer in host memory (utils/reliableUDP.py:61,
  * :67, :118).
  */

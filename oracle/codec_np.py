@@ -97,3 +97,49 @@ def decode(frames, layout: int, csum_in=None):
     ack = (b[:, 2] << 8) | b[:, 3] if F >= 4 else b[:, 2]
     return (seq.astype(np.uint16), ack.astype(np.uint16), b[:, 4].astype(np.uint8),
             np.full(n, 2, np.uint8), np.zeros(n, np.uint16), frames[:, :0])
+
+
+def encode_varlen(seq, ack, flags, payloads, layout: int):
+    """Frames for a list of payload byte strings, back to back, plus n+1 offsets."""
+    seq = np.asarray(seq, dtype=np.uint16)
+    ack = np.asarray(ack, dtype=np.uint16)
+    flags = np.asarray(flags, dtype=np.uint8)
+    out, off, cs = bytearray(), [0], []
+    for i, p in enumerate(payloads):
+        fr, c = encode(seq[i:i + 1], ack[i:i + 1], flags[i:i + 1],
+                       np.frombuffer(bytes(p), np.uint8).reshape(1, len(p)), layout)
+        out += fr.tobytes()
+        off.append(len(out))
+        cs.append(int(c[0]))
+    return (np.frombuffer(bytes(out), np.uint8), np.array(off, np.int64),
+            np.array(cs, np.uint16))
+
+
+def decode_varlen(frames, frame_off, layout: int, csum_in=None):
+    """(seq, ack, flags, ok, csum) for frames packed back to back."""
+    frames = np.asarray(frames, dtype=np.uint8)
+    n = len(frame_off) - 1
+    res = [np.zeros(n, np.uint16), np.zeros(n, np.uint16), np.zeros(n, np.uint8),
+           np.zeros(n, np.uint8), np.zeros(n, np.uint16)]
+    for i in range(n):
+        fr = frames[frame_off[i]:frame_off[i + 1]].reshape(1, -1)
+        ci = None if csum_in is None else np.asarray(csum_in)[i:i + 1]
+        out = decode(fr, layout, ci)
+        for k in range(5):
+            res[k][i] = out[k][0]
+    return tuple(res)
+
+
+def utf8_valid(frames, frame_off, layout: int):
+    """1 where Python's strict bytes.decode() accepts the payload (utils/packet.py:73)."""
+    n = len(frame_off) - 1
+    out = np.zeros(n, np.uint8)
+    for i in range(n):
+        body = bytes(frames[frame_off[i] + layout:frame_off[i + 1]]) \
+            if frame_off[i + 1] - frame_off[i] > layout else b""
+        try:
+            body.decode()
+            out[i] = 1
+        except UnicodeDecodeError:
+            out[i] = 0
+    return out

@@ -13,6 +13,10 @@
 #include "internal.hpp"
 
 namespace rudp {
+int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint64_t n,
+                  const uint16_t* d_csum_in, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
+                  uint8_t* d_ok, uint16_t* d_csum_out, uint8_t* d_payload_out, int layout,
+                  int device, void* hip_stream);
 namespace {
 
 thread_local std::string g_last_error;
@@ -93,8 +97,7 @@ int validate_batch(const rudp_batch* in, const void* frames, int layout) {
   if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
     return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
   if (in->len || in->payload_off)
-    return fail(RUDP_ENOTSUP, "variable-length batches are not supported by ABI version %d",
-                RUDP_ABI_VERSION);
+    return fail(RUDP_ENOTSUP, "variable-length batch: use rudp_encode_varlen");
   if (in->payload_len > kMaxPayload)
     return fail(RUDP_EINVAL, "payload_len %u exceeds %u", in->payload_len, kMaxPayload);
   if (in->n == 0) return 0;
@@ -109,8 +112,7 @@ int validate_decode(const void* frames, const void* frame_off, uint32_t frame_le
   if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
     return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
   if (frame_off)
-    return fail(RUDP_ENOTSUP, "per-frame offsets are not supported by ABI version %d",
-                RUDP_ABI_VERSION);
+    return fail(RUDP_ENOTSUP, "per-frame offsets are not supported by the host-staged decode");
   if (frame_len > kMaxPayload + (uint32_t)layout)
     return fail(RUDP_EINVAL, "frame_len %u exceeds %u", frame_len, kMaxPayload + (uint32_t)layout);
   if (n == 0) return 0;
@@ -245,6 +247,35 @@ uint32_t decode_group_log2(uint32_t L) {
   return lg;
 }
 
+int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint64_t n,
+                  const uint16_t* d_csum_in, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
+                  uint8_t* d_ok, uint16_t* d_csum_out, uint8_t* d_payload_out, int layout,
+                  int device, void* hip_stream) {
+  if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
+    return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
+  if (d_payload_out)
+    return fail(RUDP_ENOTSUP, "variable-length decode is zero-copy: payload i is "
+                "frames[frame_off[i] + layout, frame_off[i + 1])");
+  if (n == 0) return 0;
+  if (!d_seq || !d_ack || !d_flags || !d_ok)
+    return fail(RUDP_EINVAL, "rudp_decode: NULL buffer for a non-empty batch");
+  int rc = check_device(device);
+  if (rc) return rc;
+  VarlenArgs a{};
+  a.frames = const_cast<unsigned char*>(d_frames);
+  a.frame_off = d_frame_off;
+  a.csum_in = d_csum_in;
+  a.seq = d_seq;
+  a.ack = d_ack;
+  a.flags = d_flags;
+  a.ok = d_ok;
+  a.csum_out = d_csum_out;
+  a.n = n;
+  rc = launch_decode_varlen(a, layout, (hipStream_t)hip_stream);
+  if (rc) return hip_fail((hipError_t)rc, "varlen decode launch");
+  return 0;
+}
+
 }  // namespace rudp
 
 using namespace rudp;
@@ -280,7 +311,11 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, ui
                 uint64_t n, const uint16_t* d_csum_in_or_null, uint16_t* d_seq, uint16_t* d_ack,
                 uint8_t* d_flags, uint8_t* d_ok, uint16_t* d_csum_out_or_null,
                 uint8_t* d_payload_out_or_null, int layout, int device, void* hip_stream) {
-  int rc = validate_decode(d_frames, d_frame_off_or_null, frame_len, n, d_seq, d_ack, d_flags, d_ok, layout);
+  if (d_frame_off_or_null) {
+    return decode_varlen(d_frames, d_frame_off_or_null, n, d_csum_in_or_null, d_seq, d_ack, d_flags,
+                         d_ok, d_csum_out_or_null, d_payload_out_or_null, layout, device, hip_stream);
+  }
+  int rc = validate_decode(d_frames, nullptr, frame_len, n, d_seq, d_ack, d_flags, d_ok, layout);
   if (rc || n == 0) return rc;
   if ((rc = check_device(device))) return rc;
   DecodeArgs a{};
@@ -337,6 +372,61 @@ int rudp_synth(uint64_t seed, uint64_t first_index, uint64_t n, uint32_t payload
   a.payload = d_payload;
   rc = launch_synth(a, (hipStream_t)hip_stream);
   if (rc) return hip_fail((hipError_t)rc, "synth launch");
+  return 0;
+}
+
+int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_frame_off,
+                       uint16_t* d_csum_or_null, int layout, int device, void* hip_stream) {
+  if (!in) return fail(RUDP_EINVAL, "rudp_encode_varlen: batch is NULL");
+  if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
+    return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
+  if (in->n == 0) return 0;
+  if (!in->len || !d_frame_off)
+    return fail(RUDP_EINVAL, "rudp_encode_varlen: len[] and frame_off[] are required");
+  if (!in->seq || !in->ack || !in->flags || !d_frames || !in->payload)
+    return fail(RUDP_EINVAL, "rudp_encode_varlen: NULL buffer for a non-empty batch");
+  if (in->n > 0x7FFFFFFFull)
+    return fail(RUDP_EINVAL, "rudp_encode_varlen: at most 2^31-1 packets per call");
+  int rc = check_device(device);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)hip_stream;
+  rc = scan_frame_offsets(in->len, in->n, (uint32_t)layout, d_frame_off, s);
+  if (rc) return hip_fail((hipError_t)rc, "frame offset scan");
+  VarlenArgs a{};
+  a.payload = in->payload;
+  a.len = in->len;
+  a.payload_off = in->payload_off;
+  a.seq_in = in->seq;
+  a.ack_in = in->ack;
+  a.flags_in = in->flags;
+  a.frames = d_frames;
+  a.frame_off = d_frame_off;
+  a.csum = d_csum_or_null;
+  a.n = in->n;
+  rc = launch_encode_varlen(a, layout, s);
+  if (rc) return hip_fail((hipError_t)rc, "varlen encode launch");
+  return 0;
+}
+
+int rudp_validate_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
+                       uint32_t frame_len, uint64_t n, int layout, uint8_t* d_valid, int device,
+                       void* hip_stream) {
+  if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
+    return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
+  if (n == 0) return 0;
+  if (!d_valid || (!d_frames && (d_frame_off_or_null || frame_len)))
+    return fail(RUDP_EINVAL, "rudp_validate_utf8: NULL buffer for a non-empty batch");
+  int rc = check_device(device);
+  if (rc) return rc;
+  Utf8Args a{};
+  a.frames = d_frames;
+  a.frame_off = d_frame_off_or_null;
+  a.n = n;
+  a.F = frame_len;
+  a.H = (uint32_t)layout;
+  a.valid = d_valid;
+  rc = launch_validate_utf8(a, (hipStream_t)hip_stream);
+  if (rc) return hip_fail((hipError_t)rc, "utf8 validation launch");
   return 0;
 }
 

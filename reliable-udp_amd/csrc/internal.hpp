@@ -49,6 +49,35 @@ struct SynthArgs {
   unsigned char* payload;
 };
 
+struct VarlenArgs {
+  const unsigned char* payload;   // encode: payload buffer
+  const uint32_t* len;            // encode: payload bytes per packet
+  const uint64_t* payload_off;    // encode: may be null (packed in order)
+  const uint16_t* seq_in;
+  const uint16_t* ack_in;
+  const uint8_t* flags_in;
+  unsigned char* frames;          // encode: output; decode: input (as const)
+  const uint64_t* frame_off;      // [n + 1]
+  uint16_t* csum;                 // encode sideband, may be null
+  // decode outputs
+  const uint16_t* csum_in;
+  uint16_t* seq;
+  uint16_t* ack;
+  uint8_t* flags;
+  uint8_t* ok;
+  uint16_t* csum_out;
+  uint64_t n;
+};
+
+struct Utf8Args {
+  const unsigned char* frames;
+  const uint64_t* frame_off;  // [n + 1] or null (fixed stride F)
+  uint64_t n;
+  uint32_t F;
+  uint32_t H;
+  uint8_t* valid;
+};
+
 constexpr uint32_t kTileMaxPayload = 4096;
 // Largest payload accepted: a UDP datagram's size field is 16 bits, and it
 // keeps every per-packet word sum exact in 32 bits (32768 words x 0xFFFF).
@@ -78,5 +107,10 @@ uint32_t decode_group_log2(uint32_t L);
 int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStream_t stream);
 int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream_t stream);
 int launch_synth(const SynthArgs& args, hipStream_t stream);
+int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream);
+int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream);
+int launch_validate_utf8(const Utf8Args& args, hipStream_t stream);
+int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
+                       hipStream_t stream);
 
 }  // namespace rudp

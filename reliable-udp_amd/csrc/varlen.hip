@@ -1,0 +1,190 @@
+// Variable-length batches and strict UTF-8 validation.
+//
+// The reference's real traffic is 5-9 byte frames: one character of UTF-8
+// payload per datagram (utils/reliableUDP.py:11, :60).  A varlen batch is the
+// header table plus len[N] (+ optional payload_off[N]) over one payload
+// buffer.  Frame offsets are the exclusive scan of len[i] + H (hipcub), so the
+// frames come out packed back to back exactly as N calls of Packet.to_byte()
+// would be concatenated.
+//
+// Kernels are byte-granular with G = 8 lanes per packet: right for the tiny
+// frames this path exists for; the fixed-length tile kernels stay the path
+// for MTU-sized batches.
+#include <hipcub/hipcub.hpp>
+
+#include "codec_device.hpp"
+#include "internal.hpp"
+
+namespace rudp {
+
+constexpr uint32_t kVarLanes = 8;
+
+struct FrameLen {
+  const uint32_t* len;
+  uint32_t H;
+  __host__ __device__ uint64_t operator()(uint64_t i) const { return (uint64_t)len[i] + H; }
+};
+
+template <int H>
+__global__ void __launch_bounds__(kBlock) encode_varlen_kernel(VarlenArgs a) {
+  const uint32_t g = threadIdx.x & (kVarLanes - 1u);
+  const uint64_t p = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / kVarLanes;
+  const bool valid = p < a.n;
+  uint32_t sum = 0;
+  uint64_t fo = 0;
+  if (valid) {
+    const uint32_t L = a.len[p];
+    fo = a.frame_off[p];
+    const uint64_t po = a.payload_off ? a.payload_off[p] : fo - p * (uint64_t)H;
+    for (uint32_t j = g; j < L; j += kVarLanes) {
+      const uint32_t b = a.payload[po + j];
+      sum += (j & 1u) ? (b << 8) : b;  // LE u16 word sum (payload at an odd frame offset)
+      a.frames[fo + H + j] = (unsigned char)b;
+    }
+  }
+  for (uint32_t m = kVarLanes >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
+  if (valid) {
+    const uint32_t s = a.seq_in[p], k = a.ack_in[p], f = a.flags_in[p];
+    const uint32_t c = packet_csum(sum, s, k, f);
+    const uint64_t h = pack_header<H>(s, k, f, c);
+    for (uint32_t i = g; i < (uint32_t)H; i += kVarLanes) a.frames[fo + i] = (unsigned char)(h >> (8 * i));
+    if (g == 0 && a.csum) a.csum[p] = (uint16_t)c;
+  }
+}
+
+template <int H>
+__global__ void __launch_bounds__(kBlock) decode_varlen_kernel(VarlenArgs a) {
+  const uint32_t g = threadIdx.x & (kVarLanes - 1u);
+  const uint64_t p = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / kVarLanes;
+  const bool valid = p < a.n;
+  uint32_t sum = 0, F = 0;
+  uint64_t fo = 0;
+  if (valid) {
+    fo = a.frame_off[p];
+    F = (uint32_t)(a.frame_off[p + 1] - fo);
+    for (uint32_t j = (uint32_t)H + g; j < F; j += kVarLanes) {
+      const uint32_t b = a.frames[fo + j];
+      sum += ((j - H) & 1u) ? (b << 8) : b;
+    }
+  }
+  for (uint32_t m = kVarLanes >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
+  if (valid && g == 0) {
+    uint32_t b[7] = {0, 0, 0, 0, 0, 0, 0};
+#pragma unroll
+    for (uint32_t i = 0; i < 7; ++i)
+      if (i < F) b[i] = a.frames[fo + i];
+    uint32_t seq = (b[0] << 8) | b[1], ack = (b[2] << 8) | b[3];
+    if (F < (uint32_t)H) {  // short frame: fields truncated as utils/packet.py:31 slices them
+      if (F < 2) seq = b[0];
+      if (F < 4) ack = b[2];
+      a.seq[p] = (uint16_t)seq;
+      a.ack[p] = (uint16_t)ack;
+      a.flags[p] = (uint8_t)b[4];
+      a.ok[p] = 2;
+      if (a.csum_out) a.csum_out[p] = 0;
+      return;
+    }
+    const uint32_t c = packet_csum(sum, seq, ack, b[4]);
+    uint8_t ok;
+    if (H == 7) ok = c == ((b[5] << 8) | b[6]) ? 1 : 0;
+    else ok = a.csum_in ? (c == a.csum_in[p] ? 1 : 0) : 3;
+    a.seq[p] = (uint16_t)seq;
+    a.ack[p] = (uint16_t)ack;
+    a.flags[p] = (uint8_t)b[4];
+    a.ok[p] = ok;
+    if (a.csum_out) a.csum_out[p] = (uint16_t)c;
+  }
+}
+
+// Strict UTF-8 (RFC 3629, as CPython's bytes.decode() accepts it): no
+// overlongs (C0, C1, E0 80-9F, F0 80-8F), no surrogates (ED A0-BF), nothing
+// above U+10FFFF (F4 90+, F5-FF), no stray or missing continuation bytes.
+// One thread per packet, a 3-variable state machine over the payload bytes.
+__global__ void __launch_bounds__(kBlock) validate_utf8_kernel(Utf8Args a) {
+  const uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (p >= a.n) return;
+  uint64_t fo, fe;
+  if (a.frame_off) {
+    fo = a.frame_off[p];
+    fe = a.frame_off[p + 1];
+  } else {
+    fo = p * (uint64_t)a.F;
+    fe = fo + a.F;
+  }
+  uint8_t valid = 1;
+  uint32_t need = 0, lo = 0x80, hi = 0xBF;
+  for (uint64_t x = fo + a.H; x < fe; ++x) {
+    const uint32_t b = a.frames[x];
+    if (need) {
+      if (b < lo || b > hi) { valid = 0; break; }
+      --need;
+      lo = 0x80;
+      hi = 0xBF;
+    } else if (b < 0x80) {
+      continue;
+    } else if (b >= 0xC2 && b <= 0xDF) {
+      need = 1;
+    } else if (b >= 0xE0 && b <= 0xEF) {
+      need = 2;
+      if (b == 0xE0) lo = 0xA0;
+      if (b == 0xED) hi = 0x9F;
+    } else if (b >= 0xF0 && b <= 0xF4) {
+      need = 3;
+      if (b == 0xF0) lo = 0x90;
+      if (b == 0xF4) hi = 0x8F;
+    } else {
+      valid = 0;
+      break;
+    }
+  }
+  if (need) valid = 0;
+  a.valid[p] = valid;
+}
+
+int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream) {
+  if (args.n == 0) return 0;
+  const uint64_t blocks = (args.n * kVarLanes + kBlock - 1) / kBlock;
+  if (layout == 7)
+    hipLaunchKernelGGL(encode_varlen_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+  else
+    hipLaunchKernelGGL(encode_varlen_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+  return (int)hipGetLastError();
+}
+
+int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream) {
+  if (args.n == 0) return 0;
+  const uint64_t blocks = (args.n * kVarLanes + kBlock - 1) / kBlock;
+  if (layout == 7)
+    hipLaunchKernelGGL(decode_varlen_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+  else
+    hipLaunchKernelGGL(decode_varlen_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+  return (int)hipGetLastError();
+}
+
+int launch_validate_utf8(const Utf8Args& args, hipStream_t stream) {
+  if (args.n == 0) return 0;
+  const uint64_t blocks = (args.n + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(validate_utf8_kernel, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+  return (int)hipGetLastError();
+}
+
+// frame_off[0..n] = exclusive scan of len[i] + H, frame_off[n] = total bytes.
+int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
+                       hipStream_t stream) {
+  hipcub::CountingInputIterator<uint64_t> idx(0);
+  hipcub::TransformInputIterator<uint64_t, FrameLen, hipcub::CountingInputIterator<uint64_t>> it(
+      idx, FrameLen{d_len, H});
+  size_t temp = 0;
+  hipError_t e = hipcub::DeviceScan::InclusiveSum(nullptr, temp, it, d_frame_off + 1, (int)n, stream);
+  if (e != hipSuccess) return (int)e;
+  void* d_temp = nullptr;
+  if ((e = hipMallocAsync(&d_temp, temp ? temp : 1, stream)) != hipSuccess) return (int)e;
+  e = hipcub::DeviceScan::InclusiveSum(d_temp, temp, it, d_frame_off + 1, (int)n, stream);
+  hipError_t e2 = hipMemsetAsync(d_frame_off, 0, sizeof(uint64_t), stream);
+  hipError_t e3 = hipFreeAsync(d_temp, stream);
+  if (e != hipSuccess) return (int)e;
+  if (e2 != hipSuccess) return (int)e2;
+  return (int)e3;
+}
+
+}  // namespace rudp

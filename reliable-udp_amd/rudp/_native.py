@@ -18,12 +18,13 @@ LAYOUT_RUDP5 = 5
 LAYOUT_RUDP7 = 7
 OK_BAD_CSUM, OK_GOOD, OK_SHORT, OK_UNVERIFIED = 0, 1, 2, 3
 EINVAL, ENOMEM, ENOTSUP, EHIP_BASE = -22, -12, -95, -1000
-ABI_VERSION = 1
+ABI_VERSION = 2
 
 # Every symbol include/rudp.h declares (checked by tests/test_abi.py).
 EXPORTS = (
     "rudp_encode", "rudp_decode", "rudp_encode_host", "rudp_decode_host",
     "rudp_synth", "rudp_device_count", "rudp_last_error", "rudp_abi_version",
+    "rudp_encode_varlen", "rudp_validate_utf8",
 )
 
 
@@ -60,6 +61,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rudp_encode_host": [ctypes.POINTER(RudpBatch), P, P, I, I],
         "rudp_decode_host": [P, U32, U64, P, P, P, P, P, P, P, I, I],
         "rudp_synth": [U64, U64, U64, U32, I, P, P, P, P, I, P],
+        "rudp_encode_varlen": [ctypes.POINTER(RudpBatch), P, P, P, I, I, P],
+        "rudp_validate_utf8": [P, P, U32, U64, I, P, I, P],
         "rudp_device_count": [ctypes.POINTER(ctypes.c_int)],
         "rudp_abi_version": [],
     }

@@ -289,3 +289,149 @@ def synth_batch(n: int, payload_len: int, seed: int, *, first_index: int = 0, as
             ack.data_ptr(), flags.data_ptr(), pay.data_ptr() if payload_len else None,
             dev.index if dev.index is not None else 0, _stream_ptr(stream, dev)))
     return HeaderTable(seq, ack, flags), pay
+
+
+# ------------------------------------------------------- variable-length batches
+class VarlenFrames(NamedTuple):
+    frames: Any      # u8 [frame_off[-1]] — frames back to back
+    frame_off: Any   # int64 [N + 1] — frame i = frames[frame_off[i]:frame_off[i + 1]]
+    csum: Any        # u16 [N] or None
+
+
+def _int_tensor(t, name, device, n=None, dtypes=None):
+    import torch
+    dtypes = dtypes or (torch.int32,)
+    if not isinstance(t, torch.Tensor) or t.device != device or t.dtype not in dtypes \
+            or t.dim() != 1 or not t.is_contiguous():
+        raise TypeError(f"{name} must be a contiguous 1-D {'/'.join(map(str, dtypes))} tensor on {device}")
+    if n is not None and t.shape[0] != n:
+        raise ValueError(f"{name} has {t.shape[0]} entries, expected {n}")
+
+
+def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp7", *,
+                      payload_off=None, want_csum: Optional[bool] = None, stream=None
+                      ) -> VarlenFrames:
+    """Frame + checksum a variable-length batch on a HIP device.
+
+    ``payload``: u8 1-D tensor holding the payload bytes; ``lengths``: int32
+    [N] bytes per packet (<= 65535); ``payload_off``: int64 [N] start of each
+    payload in ``payload``, or None when the payloads are packed back to back
+    in packet order.  Returns frames packed back to back plus their offsets:
+    frame i is byte-identical to Packet(...).to_byte() of that packet
+    (utils/reliableUDP.py:53-61 builds one per character).
+    """
+    import torch
+    H = layout_header_len(layout)
+    tab = _as_table(headers)
+    dev = payload.device
+    if dev.type != "cuda":
+        raise ValueError("varlen batches run on a HIP device")
+    _dev_check(payload, "payload", torch.uint8, 1, dev)
+    _int_tensor(lengths, "lengths", dev, dtypes=(torch.int32, torch.uint32))
+    n = lengths.shape[0]
+    for name, t, dt in (("seq", tab.seq, torch.uint16), ("ack", tab.ack, torch.uint16),
+                        ("flags", tab.flags, torch.uint8)):
+        _dev_check(t, name, dt, 1, dev)
+        if t.shape[0] != n:
+            raise ValueError(f"{name} has {t.shape[0]} entries for {n} packets")
+    lens64 = lengths.to(torch.int64)
+    if n and (int(lens64.min().item()) < 0 or int(lens64.max().item()) > 65535):
+        raise ValueError("lengths must lie in [0, 65535]")
+    if payload_off is None:
+        if int(lens64.sum().item()) != payload.numel():
+            raise ValueError("packed payloads: sum(lengths) must equal payload.numel()")
+        total = payload.numel() + n * H
+    else:
+        _int_tensor(payload_off, "payload_off", dev, n, dtypes=(torch.int64,))
+        if n and (int(payload_off.min().item()) < 0
+                  or int((payload_off + lens64).max().item()) > payload.numel()):
+            raise ValueError("payload_off + lengths must stay inside payload")
+        total = int(lens64.sum().item()) + n * H
+    if want_csum is None:
+        want_csum = H == 5
+    frames = torch.empty((total,), dtype=torch.uint8, device=dev)
+    frame_off = torch.empty((n + 1,), dtype=torch.int64, device=dev)
+    csum = torch.empty((n,), dtype=torch.uint16, device=dev) if want_csum else None
+    if n == 0:
+        frame_off.zero_()
+        return VarlenFrames(frames, frame_off, csum)
+    b = _native.RudpBatch(n=n, payload_len=0, reserved=0, seq=tab.seq.data_ptr(),
+                          ack=tab.ack.data_ptr(), flags=tab.flags.data_ptr(),
+                          payload=payload.data_ptr() if payload.numel() else 16,  # never read: all lengths 0
+                          len=lengths.data_ptr(),
+                          payload_off=payload_off.data_ptr() if payload_off is not None else None)
+    _native.check(_native.lib().rudp_encode_varlen(
+        ctypes.byref(b), frames.data_ptr(), frame_off.data_ptr(),
+        csum.data_ptr() if csum is not None else None, H, dev.index or 0, _stream_ptr(stream, dev)))
+    return VarlenFrames(frames, frame_off, csum)
+
+
+def _check_offsets(frames, frame_off):
+    if frame_off.shape[0] > 1:
+        d = frame_off[1:] - frame_off[:-1]
+        if int(frame_off[0].item()) < 0 or bool((d < 0).any()) \
+                or int(frame_off[-1].item()) > frames.numel():
+            raise ValueError("frame_off must be non-decreasing offsets inside frames")
+
+
+def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *, csum=None,
+                        stream=None) -> DecodedBatch:
+    """Parse + verify frames packed back to back (offsets as pack_batch_varlen returns).
+
+    The payload is zero-copy: ``payload`` is the pair ``(start, end)`` of int64
+    [N] tensors indexing ``frames`` (empty for frames shorter than the header).
+    """
+    import torch
+    H = layout_header_len(layout)
+    if H == 7 and csum is not None:
+        raise ValueError("rudp7 carries its checksum in-band; csum= is for rudp5")
+    dev = frames.device
+    _dev_check(frames, "frames", torch.uint8, 1, dev)
+    _int_tensor(frame_off, "frame_off", dev, dtypes=(torch.int64,))
+    n = frame_off.shape[0] - 1
+    if n < 0:
+        raise ValueError("frame_off needs N + 1 entries")
+    _check_offsets(frames, frame_off)
+    if csum is not None:
+        _dev_check(csum, "csum", torch.uint16, 1, dev)
+        if csum.shape[0] != n:
+            raise ValueError(f"csum has {csum.shape[0]} entries for {n} frames")
+    seq = torch.empty((n,), dtype=torch.uint16, device=dev)
+    ack = torch.empty((n,), dtype=torch.uint16, device=dev)
+    flags = torch.empty((n,), dtype=torch.uint8, device=dev)
+    ok = torch.empty((n,), dtype=torch.uint8, device=dev)
+    cs = torch.empty((n,), dtype=torch.uint16, device=dev)
+    if n:
+        _native.check(_native.lib().rudp_decode(
+            frames.data_ptr() if frames.numel() else 16, frame_off.data_ptr(), 0, n,
+            csum.data_ptr() if csum is not None else None, seq.data_ptr(), ack.data_ptr(),
+            flags.data_ptr(), ok.data_ptr(), cs.data_ptr(), None, H, dev.index or 0,
+            _stream_ptr(stream, dev)))
+    end = frame_off[1:]
+    start = torch.minimum(frame_off[:-1] + H, end)
+    return DecodedBatch(seq, ack, flags, ok, cs, (start, end))
+
+
+def validate_utf8(frames, layout: Union[str, int] = "rudp7", *, frame_off=None, stream=None):
+    """u8 [N]: 1 where Packet(frame).get_payload() would succeed (utils/packet.py:68-73),
+    0 where it would raise UnicodeDecodeError.  ``frames``: [N, F] fixed-length,
+    or 1-D with ``frame_off`` (N + 1 offsets)."""
+    import torch
+    H = layout_header_len(layout)
+    dev = frames.device
+    if frame_off is None:
+        _dev_check(frames, "frames", torch.uint8, 2, dev)
+        n, F = frames.shape
+        off_ptr = None
+    else:
+        _dev_check(frames, "frames", torch.uint8, 1, dev)
+        _int_tensor(frame_off, "frame_off", dev, dtypes=(torch.int64,))
+        n, F = frame_off.shape[0] - 1, 0
+        _check_offsets(frames, frame_off)
+        off_ptr = frame_off.data_ptr()
+    valid = torch.empty((n,), dtype=torch.uint8, device=dev)
+    if n:
+        _native.check(_native.lib().rudp_validate_utf8(
+            frames.data_ptr() if frames.numel() else None, off_ptr, F, n, H, valid.data_ptr(),
+            dev.index or 0, _stream_ptr(stream, dev)))
+    return valid

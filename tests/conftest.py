@@ -52,3 +52,14 @@ def cuda():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
     return torch.device("cuda", 0)
+
+
+@pytest.fixture(scope="session")
+def golden_varlen():
+    with np.load(GOLDEN / "varlen.npz") as z:
+        return {k: z[k] for k in z.files}
+
+
+def split_by_lengths(buf, lengths):
+    off = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
+    return [bytes(buf[off[i]:off[i + 1]]) for i in range(len(lengths))], off

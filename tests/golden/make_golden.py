@@ -215,6 +215,62 @@ def make_small(mod):
     return arrays
 
 
+# ------------------------------------------------------------ varlen batches
+UTF8_CASES = [
+    b"", b"a", b"\x00", b"\x7f", b"\xc2\x80", b"\xdf\xbf", b"\xe0\xa0\x80", b"\xef\xbf\xbf",
+    b"\xf0\x90\x80\x80", b"\xf4\x8f\xbf\xbf", b"\xf0\x9f\x98\x80", b"\xed\x9f\xbf",
+    b"\x80", b"\xbf", b"\xc0\x80", b"\xc1\xbf", b"\xc2", b"\xe0\x80\x80", b"\xe0\x9f\xbf",
+    b"\xed\xa0\x80", b"\xed\xbf\xbf", b"\xe2\x82", b"\xf0\x80\x80\x80", b"\xf0\x8f\xbf\xbf",
+    b"\xf4\x90\x80\x80", b"\xf5\x80\x80\x80", b"\xff", b"\xfe", b"a\xc3\xa9b", b"a\xc3b",
+    b"\xe2\x82\xac\xe2\x82", b"\xf0\x9f\x98", b"\xc3\xa9\xc3\xa9\xc3\xa9\xc3",
+]
+
+
+def make_varlen(mod):
+    import random
+    rng = random.Random(0x5EED2000)
+    alphabet = "abcxyz019 \n\t~" + "éßñ" + "€中文字" + "😀🚀" + "\u0000\u007f\u0080\u07ff\u0800\uffff"
+    texts = [""] + ["".join(rng.choice(alphabet) for _ in range(rng.randint(0, 40))) for _ in range(399)]
+    pays = [t.encode() for t in texts]
+    n = len(pays)
+    seq, ack, flags, _ = synth.synth(0x5EED3000, 0, n, 0)
+    fr5, off5, cs = codec_np.encode_varlen(seq, ack, flags, pays, 5)
+    ref5, ref7 = bytearray(), bytearray()
+    for i, t in enumerate(texts):
+        for layout, buf in ((5, ref5), (7, ref7)):
+            p = mod.Packet(header_definition=rudp7_definition(mod)) if layout == 7 else mod.Packet()
+            p.set_header_field("seq_num", str(int(seq[i])), base=10)
+            p.set_header_field("ack_num", str(int(ack[i])), base=10)
+            for bit, name in ((0x80, "syn"), (0x40, "ack"), (0x20, "fin")):
+                if flags[i] & bit:
+                    p.set_header_field(name, "1", base=2)
+            if layout == 7:
+                p.set_header_field("checksum", format(int(cs[i]), "x"), base=16)
+            p.set_payload(t)
+            buf += p.to_byte()
+    # payload validity exactly as the reference's get_payload reports it
+    rnd = [bytes(rng.randrange(256) for _ in range(rng.randint(0, 12))) for _ in range(300)]
+    cases = UTF8_CASES + rnd
+    valid = []
+    for body in cases:
+        q = mod.Packet(b"\x00\x01\x00\x02\x40" + body)
+        try:
+            q.get_payload()
+            valid.append(1)
+        except UnicodeDecodeError:
+            valid.append(0)
+    return {
+        "seq": seq, "ack": ack, "flags": flags,
+        "payload": np.frombuffer(b"".join(pays), np.uint8),
+        "lengths": np.array([len(p) for p in pays], np.int32),
+        "frames5": np.frombuffer(bytes(ref5), np.uint8), "frames7": np.frombuffer(bytes(ref7), np.uint8),
+        "csum": cs,
+        "utf8_bodies": np.frombuffer(b"".join(cases), np.uint8),
+        "utf8_lengths": np.array([len(c) for c in cases], np.int32),
+        "utf8_valid": np.array(valid, np.uint8),
+    }
+
+
 # -------------------------------------------------------------------- digests
 def _digest_task(args):
     cfg, layout, chunk_index = args
@@ -311,7 +367,8 @@ def main():
         (HERE / "edge_cases.json").write_text(json.dumps(make_edge_cases(mod), indent=1) + "\n")
         np.savez_compressed(HERE / "frames_small.npz", **make_small(mod))
         (HERE / "wire_trace.json").write_text(json.dumps(make_wire_trace(mod), indent=1) + "\n")
-        print("wrote edge_cases.json, frames_small.npz, wire_trace.json")
+        np.savez_compressed(HERE / "varlen.npz", **make_varlen(mod))
+        print("wrote edge_cases.json, frames_small.npz, wire_trace.json, varlen.npz")
     if not args.skip_digests:
         (HERE / "digests.json").write_text(json.dumps(make_digests(args.jobs), indent=1) + "\n")
         print("wrote digests.json")

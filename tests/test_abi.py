@@ -49,8 +49,16 @@ def test_argument_errors_before_device():
     assert lib.rudp_decode(None, None, 10, 1, None, None, None, None, None, None, None, 9, 0,
                            None) == _native.EINVAL
     off = (ctypes.c_uint64 * 1)(0)
-    assert lib.rudp_decode(None, ctypes.cast(off, ctypes.c_void_p), 10, 1, None, None, None, None,
-                           None, None, None, 7, 0, None) == _native.ENOTSUP
+    offp = ctypes.cast(off, ctypes.c_void_p)
+    # variable-length decode is zero-copy: a payload_out buffer is refused
+    assert lib.rudp_decode(None, offp, 10, 1, None, None, None, None, None, None, offp, 7, 0,
+                           None) == _native.ENOTSUP
+    assert lib.rudp_decode(None, offp, 10, 1, None, None, None, None, None, None, None, 7, 0,
+                           None) == _native.EINVAL
+    assert lib.rudp_encode_varlen(ctypes.byref(_native.RudpBatch(n=1)), None, None, None, 7, 0,
+                                  None) == _native.EINVAL
+    assert b"len" in lib.rudp_last_error()
+    assert lib.rudp_validate_utf8(None, None, 10, 1, 7, None, 0, None) == _native.EINVAL
     # empty batches are a successful no-op, no device needed
     assert lib.rudp_encode(ctypes.byref(_native.RudpBatch(n=0)), None, None, 5, 0, None) == 0
     assert lib.rudp_synth(1, 0, 0, 16, 1, None, None, None, None, 0, None) == 0

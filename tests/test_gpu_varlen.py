@@ -1,0 +1,127 @@
+"""Variable-length batches and strict UTF-8 validation on the GPU.
+
+Pinned by tests/golden/varlen.npz: mixed-width UTF-8 strings framed one per
+packet by the reference utils/packet.py, and the reference get_payload()
+outcome (value or UnicodeDecodeError) on hand-picked and random byte bodies.
+"""
+import numpy as np
+import pytest
+
+from conftest import split_by_lengths
+from oracle import codec_np, synth
+from rudp import batch
+
+pytestmark = pytest.mark.gpu
+
+
+def dev(a, cuda):
+    import torch
+    return torch.from_numpy(np.array(a, copy=True)).to(cuda)
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+@pytest.mark.parametrize("layout", [5, 7])
+def test_varlen_encode_matches_reference(cuda, golden_varlen, layout):
+    g = golden_varlen
+    res = batch.pack_batch_varlen((dev(g["seq"], cuda), dev(g["ack"], cuda), dev(g["flags"], cuda)),
+                                  dev(g["payload"], cuda), dev(g["lengths"], cuda), layout,
+                                  want_csum=True)
+    assert np.array_equal(host(res.frames), g[f"frames{layout}"])
+    assert np.array_equal(host(res.csum), g["csum"])
+    off = host(res.frame_off)
+    assert off[0] == 0 and np.array_equal(np.diff(off), g["lengths"] + layout)
+    d = batch.unpack_batch_varlen(res.frames, res.frame_off, layout,
+                                  csum=res.csum if layout == 5 else None)
+    assert (host(d.ok) == 1).all()
+    assert np.array_equal(host(d.seq), g["seq"]) and np.array_equal(host(d.ack), g["ack"])
+    assert np.array_equal(host(d.flags), g["flags"]) and np.array_equal(host(d.csum), g["csum"])
+    start, end = host(d.payload[0]), host(d.payload[1])
+    fr = g[f"frames{layout}"]
+    pays, _ = split_by_lengths(g["payload"], g["lengths"])
+    assert all(bytes(fr[start[i]:end[i]]) == pays[i] for i in range(len(pays)))
+
+
+def test_varlen_gather_offsets(cuda):
+    rng = np.random.default_rng(3)
+    n = 5000
+    lens = rng.integers(0, 40, n).astype(np.int32)
+    buf = rng.integers(0, 256, int(lens.sum()) + 100, dtype=np.uint8)
+    # payloads taken from arbitrary places of the buffer (not packed, not in order)
+    starts = rng.integers(0, len(buf) - 40, n).astype(np.int64)
+    seq, ack, flags, _ = synth.synth(9, 0, n, 0)
+    res = batch.pack_batch_varlen((dev(seq, cuda), dev(ack, cuda), dev(flags, cuda)), dev(buf, cuda),
+                                  dev(lens, cuda), 7, payload_off=dev(starts, cuda))
+    pays = [bytes(buf[s:s + l]) for s, l in zip(starts, lens)]
+    want, off, cs = codec_np.encode_varlen(seq, ack, flags, pays, 7)
+    assert np.array_equal(host(res.frames), want) and np.array_equal(host(res.frame_off), off)
+
+
+def test_varlen_reference_traffic_roundtrip(cuda):
+    """1M one-character datagrams (utils/reliableUDP.py:11): encode -> decode on device."""
+    import torch
+    n = 1 << 20
+    rng = np.random.default_rng(11)
+    chars = np.array(list("test\n"), dtype="<U1")
+    text = "".join(rng.choice(chars, n))
+    pay = np.frombuffer(text.encode(), np.uint8)
+    lens = np.ones(n, np.int32)
+    seq, ack, flags, _ = synth.synth(0x5EED0001, 0, n, 0)
+    res = batch.pack_batch_varlen((dev(seq, cuda), dev(ack, cuda), dev(flags, cuda)), dev(pay, cuda),
+                                  dev(lens, cuda), 5, want_csum=True)
+    assert res.frames.numel() == 6 * n
+    # spot-check against the oracle on a prefix, then a full device round trip
+    pref = 4096
+    want, _, cs = codec_np.encode_varlen(seq[:pref], ack[:pref], flags[:pref],
+                                         [bytes([b]) for b in pay[:pref]], 5)
+    assert np.array_equal(host(res.frames[:6 * pref]), want)
+    d = batch.unpack_batch_varlen(res.frames, res.frame_off, 5, csum=res.csum)
+    assert bool((d.ok == 1).all())
+    assert torch.equal(d.flags, dev(flags, cuda))
+    assert torch.equal(res.frames.view(n, 6)[:, 5], dev(pay, cuda))
+    assert bool((batch.validate_utf8(res.frames, 5, frame_off=res.frame_off) == 1).all())
+
+
+def test_varlen_short_and_empty_frames(cuda):
+    # hand-built frames of every length 0..9, decoded with offsets
+    frames = [bytes(range(1, 1 + k)) for k in range(10)]
+    flat = np.frombuffer(b"".join(frames), np.uint8)
+    off = np.concatenate([[0], np.cumsum([len(f) for f in frames])]).astype(np.int64)
+    for layout in (5, 7):
+        d = batch.unpack_batch_varlen(dev(flat, cuda), dev(off, cuda), layout)
+        want = codec_np.decode_varlen(flat, off, layout)
+        for got, exp in zip((d.seq, d.ack, d.flags, d.ok, d.csum), want):
+            assert np.array_equal(host(got), exp), layout
+
+
+def test_utf8_matches_reference_get_payload(cuda, golden_varlen):
+    g = golden_varlen
+    bodies, _ = split_by_lengths(g["utf8_bodies"], g["utf8_lengths"])
+    frames = [b"\x00\x01\x00\x02\x40" + b for b in bodies]
+    off = np.concatenate([[0], np.cumsum([len(f) for f in frames])]).astype(np.int64)
+    flat = np.frombuffer(b"".join(frames), np.uint8)
+    v = batch.validate_utf8(dev(flat, cuda), 5, frame_off=dev(off, cuda))
+    assert np.array_equal(host(v), g["utf8_valid"])
+
+
+def test_utf8_fixed_length(cuda, golden_small):
+    for L in (1, 16, 64, 1472):
+        fr = golden_small[f"L{L}_full_frames7"]
+        off = np.arange(fr.shape[0] + 1, dtype=np.int64) * fr.shape[1]
+        want = codec_np.utf8_valid(fr.reshape(-1), off, 7)
+        assert np.array_equal(host(batch.validate_utf8(dev(fr, cuda), 7)), want)
+        ascii_fr = golden_small[f"L{L}_frames7"]
+        assert (host(batch.validate_utf8(dev(ascii_fr, cuda), 7)) == 1).all()
+
+
+def test_varlen_rejects_out_of_bounds(cuda):
+    z16 = dev(np.zeros(2, np.uint16), cuda)
+    z8 = dev(np.zeros(2, np.uint8), cuda)
+    with pytest.raises(ValueError, match="sum"):
+        batch.pack_batch_varlen((z16, z16, z8), dev(np.zeros(3, np.uint8), cuda),
+                                dev(np.array([2, 2], np.int32), cuda))
+    with pytest.raises(ValueError, match="inside"):
+        batch.unpack_batch_varlen(dev(np.zeros(8, np.uint8), cuda),
+                                  dev(np.array([0, 5, 12], np.int64), cuda))

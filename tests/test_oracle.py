@@ -128,3 +128,27 @@ def test_c_oracle_reproduces_reference_digest(digests, name, layout):
     fr, cs = codec_c.encode(seq, ack, flags, pay, layout)
     assert hashlib.sha256(fr.tobytes()).hexdigest() == cfg["layouts"][str(layout)]["frames"][0]
     assert hashlib.sha256(cs.astype("<u2").tobytes()).hexdigest() == cfg["layouts"][str(layout)]["csum"][0]
+
+
+def test_varlen_oracle_matches_reference(golden_varlen):
+    from conftest import split_by_lengths
+    g = golden_varlen
+    pays, _ = split_by_lengths(g["payload"], g["lengths"])
+    for layout in (5, 7):
+        fr, off, cs = codec_np.encode_varlen(g["seq"], g["ack"], g["flags"], pays, layout)
+        assert np.array_equal(fr, g[f"frames{layout}"]) and np.array_equal(cs, g["csum"])
+        assert off[-1] == len(fr) and np.array_equal(np.diff(off), g["lengths"] + layout)
+        seq, ack, flags, ok, cs2 = codec_np.decode_varlen(fr, off, layout,
+                                                           g["csum"] if layout == 5 else None)
+        assert np.array_equal(seq, g["seq"]) and np.array_equal(flags, g["flags"])
+        assert (ok == 1).all() and np.array_equal(cs2, g["csum"])
+
+
+def test_utf8_oracle_matches_reference_get_payload(golden_varlen):
+    from conftest import split_by_lengths
+    g = golden_varlen
+    bodies, _ = split_by_lengths(g["utf8_bodies"], g["utf8_lengths"])
+    frames = [b"\x00\x01\x00\x02\x40" + b for b in bodies]
+    off = np.concatenate([[0], np.cumsum([len(f) for f in frames])]).astype(np.int64)
+    flat = np.frombuffer(b"".join(frames), np.uint8)
+    assert np.array_equal(codec_np.utf8_valid(flat, off, 5), g["utf8_valid"])
