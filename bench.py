@@ -159,6 +159,25 @@ def legs(torch, batch, device, steps):
         "GiB_s": (1 << 20) * 1472 / (ms / 1e3) / GIB, "ms": ms,
         "roofline_frac": (1 << 20) * (algorithmic_bytes_encode(1472) + algorithmic_bytes_decode(1472))
         / (ms / 1e3) / 1e9 / HBM_PEAK_GBS}
+    # strict UTF-8 validation of the 1M x 1472 frames (get_payload strictness)
+    fr = w.sets[0][2]
+    ms = time_loop(torch, lambda i: batch.validate_utf8(fr, "rudp7"), steps, 3) / steps
+    out["utf8_validate_1Mx1472"] = {"GiB_s": (1 << 20) * 1472 / (ms / 1e3) / GIB, "ms": ms}
+    # reference-shaped traffic: 1M one-character datagrams (utils/reliableUDP.py:11),
+    # variable-length encode (scan + frame) and decode-verify, in packets/s
+    n1 = 1 << 20
+    tab1, pay1 = batch.synth_batch(n1, 1, SEEDS[1472], device=device)
+    lens1 = torch.ones(n1, dtype=torch.int32, device=device)
+    flat1 = pay1.view(-1)
+    enc = batch.pack_batch_varlen(tab1, flat1, lens1, "rudp5", want_csum=True)
+    ms_e = time_loop(torch, lambda i: batch.pack_batch_varlen(tab1, flat1, lens1, "rudp5",
+                                                              want_csum=True), steps, 3) / steps
+    ms_d = time_loop(torch, lambda i: batch.unpack_batch_varlen(enc.frames, enc.frame_off, "rudp5",
+                                                                csum=enc.csum), steps, 3) / steps
+    out["varlen_1M_x_1char"] = {"encode_Mpkt_s": n1 / ms_e / 1e3, "encode_ms": ms_e,
+                                "decode_verify_Mpkt_s": n1 / ms_d / 1e3, "decode_ms": ms_d,
+                                "note": "includes the host-side bounds checks (one sync) per call"}
+    del tab1, pay1, lens1, flat1, enc
     # device-to-device streaming-copy ceiling (dwordx4 nt copy kernel, rudpx_copy),
     # same byte count as one encode's payload
     import ctypes

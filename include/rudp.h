@@ -139,6 +139,20 @@ int rudp_validate_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_n
                        void* hip_stream);
 
 /*
+ * Retransmission detection of the reference proxy (proxy.py:90: `packet in
+ * self.packets`, a list of the last Proxy.MAX_MEMORY = 500 packets,
+ * proxy.py:17, :92-94) over a batch of frames in arrival order:
+ * d_dup[i] = 1 iff frame i equals (Packet.__eq__, utils/packet.py:83-86: same
+ * get_hex(), so an empty datagram equals 00 00 00 00 00) one of frames
+ * max(0, i - window) .. i-1.  window <= 4096 (the proxy uses 500).  To carry
+ * history across batches, prepend the previous batch's last `window` frames.
+ * Frames as in rudp_decode (fixed stride or n+1 offsets).
+ */
+int rudp_dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
+                      uint32_t frame_len, uint64_t n, uint32_t window, uint8_t* d_dup, int device,
+                      void* hip_stream);
+
+/*
  * Host-memory conveniences: same semantics, host pointers in and out.
  * Staged through a ring of device slots in chunks, with H2D, kernel and D2H
  * on three streams chained by events so the three overlap.  Synchronous.  These model the reference's

@@ -129,3 +129,15 @@ def decode_like_reference(frame: bytes, rudp7: bool = False):
              int(p.get_header_field("offset", base=2), 2))
     csum = int(p.get_header_field("checksum", base=16), 16) if rudp7 else None
     return seq, ack, flags, csum, p.get_payload()
+
+
+def proxy_retransmitted(frames, window=500):
+    """proxy.py:79-94 restated: per datagram, is it `in` the last `window` packets?"""
+    history, out = [], []
+    for data in frames:
+        pkt = BitstringPacket(bytes(data))
+        out.append(1 if pkt in history else 0)   # proxy.py:90 (list `in` -> __eq__)
+        history.append(pkt)                      # :92
+        if len(history) > window:                # :93-94
+            history.pop(0)
+    return out

@@ -430,6 +430,34 @@ int rudp_validate_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_n
   return 0;
 }
 
+int rudp_dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
+                      uint32_t frame_len, uint64_t n, uint32_t window, uint8_t* d_dup, int device,
+                      void* hip_stream) {
+  if (window > dedup_max_window())
+    return fail(RUDP_EINVAL, "window %u exceeds %u", window, dedup_max_window());
+  if (n == 0) return 0;
+  if (!d_dup || (!d_frames && (d_frame_off_or_null || frame_len)))
+    return fail(RUDP_EINVAL, "rudp_dedup_window: NULL buffer for a non-empty batch");
+  int rc = check_device(device);
+  if (rc) return rc;
+  hipStream_t s = (hipStream_t)hip_stream;
+  DedupArgs a{};
+  a.frames = d_frames;
+  a.frame_off = d_frame_off_or_null;
+  a.n = n;
+  a.F = frame_len;
+  a.window = window;
+  a.dup = d_dup;
+  void* scratch = nullptr;
+  RUDP_HIP(hipMallocAsync(&scratch, n * sizeof(uint64_t), s));
+  a.hash = (uint64_t*)scratch;
+  rc = launch_dedup(a, s);
+  hipError_t e = hipFreeAsync(scratch, s);
+  if (rc) return hip_fail((hipError_t)rc, "dedup launch");
+  if (e != hipSuccess) return hip_fail(e, "hipFreeAsync");
+  return 0;
+}
+
 int rudp_encode_host(const rudp_batch* h_in, uint8_t* h_frames, uint16_t* h_csum_or_null,
                      int layout, int device) {
   int rc = validate_batch(h_in, h_frames, layout);

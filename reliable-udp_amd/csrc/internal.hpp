@@ -78,6 +78,16 @@ struct Utf8Args {
   uint8_t* valid;
 };
 
+struct DedupArgs {
+  const unsigned char* frames;
+  const uint64_t* frame_off;  // [n + 1] or null (fixed stride F)
+  uint64_t n;
+  uint32_t F;
+  uint32_t window;
+  uint64_t* hash;             // scratch [n]
+  uint8_t* dup;
+};
+
 constexpr uint32_t kTileMaxPayload = 4096;
 // Largest payload accepted: a UDP datagram's size field is 16 bits, and it
 // keeps every per-packet word sum exact in 32 bits (32768 words x 0xFFFF).
@@ -110,6 +120,8 @@ int launch_synth(const SynthArgs& args, hipStream_t stream);
 int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream);
 int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream);
 int launch_validate_utf8(const Utf8Args& args, hipStream_t stream);
+int launch_dedup(const DedupArgs& args, hipStream_t stream);
+uint32_t dedup_max_window();
 int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
                        hipStream_t stream);
 

@@ -96,49 +96,71 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_kernel(VarlenArgs a) {
   }
 }
 
-// Strict UTF-8 (RFC 3629, as CPython's bytes.decode() accepts it): no
-// overlongs (C0, C1, E0 80-9F, F0 80-8F), no surrogates (ED A0-BF), nothing
-// above U+10FFFF (F4 90+, F5-FF), no stray or missing continuation bytes.
-// One thread per packet, a 3-variable state machine over the payload bytes.
-__global__ void __launch_bounds__(kBlock) validate_utf8_kernel(Utf8Args a) {
-  const uint64_t p = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (p >= a.n) return;
-  uint64_t fo, fe;
-  if (a.frame_off) {
-    fo = a.frame_off[p];
-    fe = a.frame_off[p + 1];
-  } else {
-    fo = p * (uint64_t)a.F;
-    fe = fo + a.F;
-  }
-  uint8_t valid = 1;
-  uint32_t need = 0, lo = 0x80, hi = 0xBF;
-  for (uint64_t x = fo + a.H; x < fe; ++x) {
-    const uint32_t b = a.frames[x];
-    if (need) {
-      if (b < lo || b > hi) { valid = 0; break; }
-      --need;
-      lo = 0x80;
-      hi = 0xBF;
-    } else if (b < 0x80) {
-      continue;
-    } else if (b >= 0xC2 && b <= 0xDF) {
-      need = 1;
-    } else if (b >= 0xE0 && b <= 0xEF) {
-      need = 2;
-      if (b == 0xE0) lo = 0xA0;
-      if (b == 0xED) hi = 0x9F;
-    } else if (b >= 0xF0 && b <= 0xF4) {
-      need = 3;
-      if (b == 0xF0) lo = 0x90;
-      if (b == 0xF4) hi = 0x8F;
+// Strict UTF-8 (RFC 3629, as CPython's bytes.decode() accepts it, i.e. what
+// utils/packet.py:73 enforces): no overlongs (C0, C1, E0 80-9F, F0 80-8F), no
+// surrogates (ED A0-BF), nothing above U+10FFFF (F4 90+, F5-FF), no stray or
+// missing continuation bytes.  Byte-parallel: every byte is judged from itself and the three bytes before it, so the
+// payload splits over G lanes with no carried state (the approach of SIMD
+// UTF-8 validators): byte c at payload index i, with p1 p2 p3 the bytes at
+// i-1, i-2, i-3 (0 before the payload start):
+//   c is a continuation byte  <=>  p1 is a 2/3/4-byte lead, or p2 a 3/4-byte
+//                                  lead, or p3 a 4-byte lead ("expected")
+//   C0 C1 F5..FF never appear; after E0 / ED / F0 / F4 the next byte lies in
+//   A0-BF / 80-9F / 90-BF / 80-8F; and nothing is still expected at the end.
+__device__ __forceinline__ uint32_t utf8_need(uint32_t b) {  // continuation bytes a lead asks for
+  return b >= 0xF0 ? 3u : b >= 0xE0 ? 2u : b >= 0xC0 ? 1u : 0u;
+}
+
+__device__ __forceinline__ bool utf8_byte_ok(uint32_t c, uint32_t p1, uint32_t p2, uint32_t p3) {
+  const bool cont = (c & 0xC0u) == 0x80u;
+  const bool expected = utf8_need(p1) >= 1 || utf8_need(p2) >= 2 || utf8_need(p3) >= 3;
+  // p1..p3 that are themselves continuation bytes ask for nothing (need() of 80-BF is 0)
+  if (cont != expected) return false;
+  if (c == 0xC0 || c == 0xC1 || c >= 0xF5) return false;
+  if (p1 == 0xE0 && c < 0xA0) return false;
+  if (p1 == 0xED && c > 0x9F) return false;
+  if (p1 == 0xF0 && c < 0x90) return false;
+  if (p1 == 0xF4 && c > 0x8F) return false;
+  return true;
+}
+
+__global__ void __launch_bounds__(kBlock) validate_utf8_par_kernel(Utf8Args a) {
+  const uint32_t g = threadIdx.x & (kVarLanes - 1u);
+  const uint64_t p = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / kVarLanes;
+  const bool valid_p = p < a.n;
+  uint32_t bad = 0;
+  uint64_t fo = 0, fe = 0;
+  if (valid_p) {
+    if (a.frame_off) {
+      fo = a.frame_off[p];
+      fe = a.frame_off[p + 1];
     } else {
-      valid = 0;
-      break;
+      fo = p * (uint64_t)a.F;
+      fe = fo + a.F;
+    }
+    const uint64_t s = fo + a.H;  // payload start
+    if (s < fe) {
+      const uint64_t len = fe - s;
+      // lane g judges a contiguous slice of ceil(len / G) bytes
+      const uint64_t per = (len + kVarLanes - 1) / kVarLanes;
+      const uint64_t b0 = g * per, b1 = b0 + per < len ? b0 + per : len;
+      uint32_t p3 = b0 >= 3 ? a.frames[s + b0 - 3] : 0u;
+      uint32_t p2 = b0 >= 2 ? a.frames[s + b0 - 2] : 0u;
+      uint32_t p1 = b0 >= 1 ? a.frames[s + b0 - 1] : 0u;
+      for (uint64_t i = b0; i < b1; ++i) {
+        const uint32_t c = a.frames[s + i];
+        bad |= utf8_byte_ok(c, p1, p2, p3) ? 0u : 1u;
+        p3 = p2;
+        p2 = p1;
+        p1 = c;
+      }
+      if (b1 == len && b0 < b1) {  // last slice: nothing may still be expected
+        bad |= (utf8_need(p1) >= 1 || utf8_need(p2) >= 2 || utf8_need(p3) >= 3) ? 1u : 0u;
+      }
     }
   }
-  if (need) valid = 0;
-  a.valid[p] = valid;
+  for (uint32_t m = kVarLanes >> 1; m > 0; m >>= 1) bad |= __shfl_xor(bad, (int)m, 64);
+  if (valid_p && g == 0) a.valid[p] = bad ? 0 : 1;
 }
 
 int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream) {
@@ -163,8 +185,8 @@ int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream)
 
 int launch_validate_utf8(const Utf8Args& args, hipStream_t stream) {
   if (args.n == 0) return 0;
-  const uint64_t blocks = (args.n + kBlock - 1) / kBlock;
-  hipLaunchKernelGGL(validate_utf8_kernel, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+  const uint64_t blocks = (args.n * kVarLanes + kBlock - 1) / kBlock;
+  hipLaunchKernelGGL(validate_utf8_par_kernel, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
   return (int)hipGetLastError();
 }
 

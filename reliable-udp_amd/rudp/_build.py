@@ -20,7 +20,7 @@ CSRC = ROOT / "csrc"
 INCLUDE = ROOT.parent / "include"
 BUILD = ROOT / "build"
 LIB = PKG_DIR / "librudp.so"
-SOURCES = ("encode.hip", "decode.hip", "synth.hip", "varlen.hip", "capi.hip", "tuning.hip")
+SOURCES = ("encode.hip", "decode.hip", "synth.hip", "varlen.hip", "dedup.hip", "capi.hip", "tuning.hip")
 ARCH = "gfx950"
 
 

@@ -24,7 +24,7 @@ ABI_VERSION = 2
 EXPORTS = (
     "rudp_encode", "rudp_decode", "rudp_encode_host", "rudp_decode_host",
     "rudp_synth", "rudp_device_count", "rudp_last_error", "rudp_abi_version",
-    "rudp_encode_varlen", "rudp_validate_utf8",
+    "rudp_encode_varlen", "rudp_validate_utf8", "rudp_dedup_window",
 )
 
 
@@ -63,6 +63,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rudp_synth": [U64, U64, U64, U32, I, P, P, P, P, I, P],
         "rudp_encode_varlen": [ctypes.POINTER(RudpBatch), P, P, P, I, I, P],
         "rudp_validate_utf8": [P, P, U32, U64, I, P, I, P],
+        "rudp_dedup_window": [P, P, U32, U64, U32, P, I, P],
         "rudp_device_count": [ctypes.POINTER(ctypes.c_int)],
         "rudp_abi_version": [],
     }

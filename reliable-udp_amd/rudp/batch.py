@@ -435,3 +435,34 @@ def validate_utf8(frames, layout: Union[str, int] = "rudp7", *, frame_off=None, 
             frames.data_ptr() if frames.numel() else None, off_ptr, F, n, H, valid.data_ptr(),
             dev.index or 0, _stream_ptr(stream, dev)))
     return valid
+
+
+PROXY_MAX_MEMORY = 500  # proxy.py:17
+
+
+def detect_retransmissions(frames, *, frame_off=None, window: int = PROXY_MAX_MEMORY, stream=None):
+    """u8 [N]: 1 where frame i equals one of the `window` frames before it.
+
+    Batched form of the reference proxy's `packet in self.packets` check
+    (proxy.py:90, with the 500-packet history of proxy.py:17, :92-94) and
+    Packet.__eq__ semantics (utils/packet.py:83-86).  ``frames``: [N, F]
+    fixed-length, or 1-D with ``frame_off`` (N + 1 offsets).
+    """
+    import torch
+    dev = frames.device
+    if frame_off is None:
+        _dev_check(frames, "frames", torch.uint8, 2, dev)
+        n, F = frames.shape
+        off_ptr = None
+    else:
+        _dev_check(frames, "frames", torch.uint8, 1, dev)
+        _int_tensor(frame_off, "frame_off", dev, dtypes=(torch.int64,))
+        _check_offsets(frames, frame_off)
+        n, F = frame_off.shape[0] - 1, 0
+        off_ptr = frame_off.data_ptr()
+    dup = torch.empty((n,), dtype=torch.uint8, device=dev)
+    if n:
+        _native.check(_native.lib().rudp_dedup_window(
+            frames.data_ptr() if frames.numel() else None, off_ptr, F, n, window, dup.data_ptr(),
+            dev.index or 0, _stream_ptr(stream, dev)))
+    return dup

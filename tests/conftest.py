@@ -63,3 +63,9 @@ def golden_varlen():
 def split_by_lengths(buf, lengths):
     off = np.concatenate([[0], np.cumsum(lengths)]).astype(np.int64)
     return [bytes(buf[off[i]:off[i + 1]]) for i in range(len(lengths))], off
+
+
+@pytest.fixture(scope="session")
+def golden_dedup():
+    with np.load(GOLDEN / "dedup.npz") as z:
+        return {k: z[k] for k in z.files}

@@ -271,6 +271,36 @@ def make_varlen(mod):
     }
 
 
+# ------------------------------------------------------- proxy retransmission
+def make_dedup(mod):
+    """Datagram sequence with retransmissions; dup flags from the reference
+    Packet.__eq__ under the proxy's list logic (proxy.py:90-94, window 500)."""
+    import random
+    rng = random.Random(0x5EED4000)
+    pool = [b"", b"\x00" * 5, b"\x00" * 4, b"\x00" * 6, b"\x01", b"\x00\x01",
+            bytes.fromhex("0e1b00008074"), bytes.fromhex("0e1c00000065"), bytes.fromhex("00000e1c40")]
+    pool += [bytes(rng.randrange(256) for _ in range(rng.randint(1, 30))) for _ in range(150)]
+    seq = []
+    for _ in range(3000):
+        r = rng.random()
+        if r < 0.3 and seq:        # retransmit something recent (inside or just outside the window)
+            seq.append(seq[-rng.randint(1, min(len(seq), 700))])
+        elif r < 0.4:              # the edge cases: empty vs zero header, short frames
+            seq.append(rng.choice(pool[:9]))
+        else:                      # a fresh datagram
+            seq.append(bytes(rng.randrange(256) for _ in range(rng.randint(1, 30))))
+    history, dup = [], []
+    for data in seq:
+        pkt = mod.Packet(data)
+        dup.append(1 if pkt in history else 0)
+        history.append(pkt)
+        if len(history) > 500:
+            history.pop(0)
+    return {"frames": np.frombuffer(b"".join(seq), np.uint8),
+            "lengths": np.array([len(d) for d in seq], np.int32),
+            "dup": np.array(dup, np.uint8)}
+
+
 # -------------------------------------------------------------------- digests
 def _digest_task(args):
     cfg, layout, chunk_index = args
@@ -368,7 +398,8 @@ def main():
         np.savez_compressed(HERE / "frames_small.npz", **make_small(mod))
         (HERE / "wire_trace.json").write_text(json.dumps(make_wire_trace(mod), indent=1) + "\n")
         np.savez_compressed(HERE / "varlen.npz", **make_varlen(mod))
-        print("wrote edge_cases.json, frames_small.npz, wire_trace.json, varlen.npz")
+        np.savez_compressed(HERE / "dedup.npz", **make_dedup(mod))
+        print("wrote edge_cases.json, frames_small.npz, wire_trace.json, varlen.npz, dedup.npz")
     if not args.skip_digests:
         (HERE / "digests.json").write_text(json.dumps(make_digests(args.jobs), indent=1) + "\n")
         print("wrote digests.json")

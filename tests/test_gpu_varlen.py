@@ -125,3 +125,61 @@ def test_varlen_rejects_out_of_bounds(cuda):
     with pytest.raises(ValueError, match="inside"):
         batch.unpack_batch_varlen(dev(np.zeros(8, np.uint8), cuda),
                                   dev(np.array([0, 5, 12], np.int64), cuda))
+
+
+def _near_utf8(rng, n):
+    """Mostly-valid UTF-8 strings with a few random byte edits (hits every DFA edge)."""
+    chars = [chr(c) for c in (0x41, 0x7F, 0x80, 0x7FF, 0x800, 0xD7FF, 0xE000, 0xFFFD, 0xFFFF,
+                               0x10000, 0x1F600, 0x10FFFF, 0xE9, 0x4E2D)]
+    out = []
+    for _ in range(n):
+        s = "".join(chars[i] for i in rng.integers(0, len(chars), rng.integers(0, 12))).encode()
+        b = bytearray(s)
+        for _ in range(rng.integers(0, 3)):
+            if b and rng.random() < 0.7:
+                b[rng.integers(0, len(b))] = int(rng.integers(0, 256))
+            elif rng.random() < 0.5 and b:
+                del b[rng.integers(0, len(b))]
+            else:
+                b.insert(int(rng.integers(0, len(b) + 1)), int(rng.choice([0x80, 0xBF, 0xC0, 0xE0, 0xED, 0xF0, 0xF4, 0xF5])))
+        out.append(bytes(b))
+    return out
+
+
+def test_utf8_random_vs_python_decoder(cuda):
+    rng = np.random.default_rng(1234)
+    bodies = _near_utf8(rng, 20000)
+    frames = [b"\x12\x34\x00\x00\x80" + b for b in bodies]
+    off = np.concatenate([[0], np.cumsum([len(f) for f in frames])]).astype(np.int64)
+    flat = np.frombuffer(b"".join(frames), np.uint8)
+    want = codec_np.utf8_valid(flat, off, 5)
+    assert 0.2 < want.mean() < 0.9  # both outcomes well represented
+    got = host(batch.validate_utf8(dev(flat, cuda), 5, frame_off=dev(off, cuda)))
+    assert np.array_equal(got, want)
+
+
+def test_dedup_matches_reference_proxy(cuda, golden_dedup):
+    g = golden_dedup
+    off = np.concatenate([[0], np.cumsum(g["lengths"])]).astype(np.int64)
+    dup = batch.detect_retransmissions(dev(g["frames"], cuda), frame_off=dev(off, cuda), window=500)
+    assert np.array_equal(host(dup), g["dup"])
+
+
+@pytest.mark.parametrize("window", [1, 7, 500, 4096])
+def test_dedup_fixed_length_vs_oracle(cuda, window):
+    from oracle.bitstring_packet import proxy_retransmitted
+    rng = np.random.default_rng(window)
+    base = rng.integers(0, 256, (300, 40), dtype=np.uint8)
+    idx = rng.integers(0, 300, 2500)
+    fr = np.ascontiguousarray(base[idx])
+    want = proxy_retransmitted([r.tobytes() for r in fr], window) if window < 4096 else None
+    got = host(batch.detect_retransmissions(dev(fr, cuda), window=window))
+    last, ref = {}, []  # last occurrence of each frame: dup iff it lies inside the window
+    for i, r in enumerate(fr):
+        k = r.tobytes()
+        ref.append(int(k in last and last[k] >= i - window))
+        last[k] = i
+    if want is None:
+        want = ref
+    assert list(want) == ref
+    assert got.tolist() == list(want)

@@ -152,3 +152,24 @@ def test_utf8_oracle_matches_reference_get_payload(golden_varlen):
     off = np.concatenate([[0], np.cumsum([len(f) for f in frames])]).astype(np.int64)
     flat = np.frombuffer(b"".join(frames), np.uint8)
     assert np.array_equal(codec_np.utf8_valid(flat, off, 5), g["utf8_valid"])
+
+
+def test_proxy_dedup_oracle_matches_reference(golden_dedup):
+    from conftest import split_by_lengths
+    frames, _ = split_by_lengths(golden_dedup["frames"], golden_dedup["lengths"])
+    assert bp.proxy_retransmitted(frames, 500) == golden_dedup["dup"].tolist()
+
+
+def test_proxy_dedup_with_dropin_packet(golden_dedup):
+    """The proxy's own loop (proxy.py:90-94) over the drop-in Packet gives the same flags."""
+    from conftest import split_by_lengths
+    from rudp.packet import Packet
+    frames, _ = split_by_lengths(golden_dedup["frames"], golden_dedup["lengths"])
+    history, dup = [], []
+    for data in frames:
+        pkt = Packet(data)
+        dup.append(1 if pkt in history else 0)
+        history.append(pkt)
+        if len(history) > 500:
+            history.pop(0)
+    assert dup == golden_dedup["dup"].tolist()
