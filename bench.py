@@ -177,6 +177,10 @@ def legs(torch, batch, device, steps):
     out["varlen_1M_x_1char"] = {"encode_Mpkt_s": n1 / ms_e / 1e3, "encode_ms": ms_e,
                                 "decode_verify_Mpkt_s": n1 / ms_d / 1e3, "decode_ms": ms_d,
                                 "note": "includes the host-side bounds checks (one sync) per call"}
+    # the proxy's retransmission check (proxy.py:90, 500-deep history) over the same 1M datagrams
+    ms_x = time_loop(torch, lambda i: batch.detect_retransmissions(enc.frames, frame_off=enc.frame_off,
+                                                                   window=500), steps, 3) / steps
+    out["proxy_dedup_1M_window500"] = {"Mpkt_s": n1 / ms_x / 1e3, "ms": ms_x}
     del tab1, pay1, lens1, flat1, enc
     # device-to-device streaming-copy ceiling (dwordx4 nt copy kernel, rudpx_copy),
     # same byte count as one encode's payload

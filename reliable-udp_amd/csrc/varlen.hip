@@ -163,6 +163,80 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_par_kernel(Utf8Args a) {
   if (valid_p && g == 0) a.valid[p] = bad ? 0 : 1;
 }
 
+// Vector form of the same check for 16-byte-aligned frame buffers: G = 16
+// lanes per frame walk the ALIGNED 16-byte chunks that overlap the payload
+// (one dwordx4 each, plus the dword before the chunk for the three
+// predecessor bytes), bytes outside [payload start, frame end) count as
+// absent (0).  An all-ASCII chunk whose predecessors hold no lead byte is
+// valid without the per-byte walk: the common case for text payloads.
+constexpr uint32_t kUtf8Lanes = 16;
+
+__device__ __forceinline__ uint32_t byte_of(u32x4 v, int k) {
+  const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
+  return (w >> (8 * (k & 3))) & 0xFFu;
+}
+
+__global__ void __launch_bounds__(kBlock) validate_utf8_vec_kernel(Utf8Args a) {
+  const uint32_t g = threadIdx.x & (kUtf8Lanes - 1u);
+  const uint64_t p = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / kUtf8Lanes;
+  const bool valid_p = p < a.n;
+  uint32_t bad = 0;
+  if (valid_p) {
+    uint64_t fo, fe;
+    if (a.frame_off) {
+      fo = a.frame_off[p];
+      fe = a.frame_off[p + 1];
+    } else {
+      fo = p * (uint64_t)a.F;
+      fe = fo + a.F;
+    }
+    const uint64_t s = fo + a.H;
+    const uint64_t total = a.frame_off ? a.frame_off[a.n] : a.n * (uint64_t)a.F;
+    if (s < fe) {
+      const uint64_t c_lo = s >> 4, c_hi = (fe - 1) >> 4;
+      for (uint64_t c = c_lo + g; c <= c_hi; c += kUtf8Lanes) {
+        const uint64_t base = c << 4;
+        u32x4 v;
+        if (base + 16 <= total) {
+          v = *reinterpret_cast<const u32x4*>(a.frames + base);
+        } else {  // the batch's last chunk: never read past the buffer
+          uint32_t d[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+          for (int k = 0; k < 16; ++k)
+            if (base + k < total) d[k >> 2] |= (uint32_t)a.frames[base + k] << (8 * (k & 3));
+          v.x = d[0];
+          v.y = d[1];
+          v.z = d[2];
+          v.w = d[3];
+        }
+        const uint32_t prev = base >= 4 && base > s ? *reinterpret_cast<const uint32_t*>(a.frames + base - 4) : 0u;
+        // predecessor bytes, zeroed where they fall before the payload start
+        uint32_t p3 = (base >= s + 3) ? (prev >> 8) & 0xFFu : 0u;
+        uint32_t p2 = (base >= s + 2) ? (prev >> 16) & 0xFFu : 0u;
+        uint32_t p1 = (base >= s + 1) ? (prev >> 24) : 0u;
+        const bool interior = base >= s && base + 16 <= fe;
+        if (interior && ((v.x | v.y | v.z | v.w) & 0x80808080u) == 0 && p1 < 0xC0 && p2 < 0xC0 &&
+            p3 < 0xC0)
+          continue;  // plain ASCII, nothing pending from before
+#pragma unroll
+        for (int k = 0; k < 16; ++k) {
+          const uint64_t x = base + (uint64_t)k;
+          if (x < s || x >= fe) continue;
+          const uint32_t cb = byte_of(v, k);
+          bad |= utf8_byte_ok(cb, p1, p2, p3) ? 0u : 1u;
+          p3 = p2;
+          p2 = p1;
+          p1 = cb;
+        }
+        if (c == c_hi)  // the frame's last chunk: nothing may still be expected
+          bad |= (utf8_need(p1) >= 1 || utf8_need(p2) >= 2 || utf8_need(p3) >= 3) ? 1u : 0u;
+      }
+    }
+  }
+  for (uint32_t m = kUtf8Lanes >> 1; m > 0; m >>= 1) bad |= __shfl_xor(bad, (int)m, 64);
+  if (valid_p && g == 0) a.valid[p] = bad ? 0 : 1;
+}
+
 int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream) {
   if (args.n == 0) return 0;
   const uint64_t blocks = (args.n * kVarLanes + kBlock - 1) / kBlock;
@@ -185,6 +259,11 @@ int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream)
 
 int launch_validate_utf8(const Utf8Args& args, hipStream_t stream) {
   if (args.n == 0) return 0;
+  if ((reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0) {
+    const uint64_t blocks = (args.n * kUtf8Lanes + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(validate_utf8_vec_kernel, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+    return (int)hipGetLastError();
+  }
   const uint64_t blocks = (args.n * kVarLanes + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(validate_utf8_par_kernel, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
   return (int)hipGetLastError();

@@ -183,3 +183,17 @@ def test_dedup_fixed_length_vs_oracle(cuda, window):
         want = ref
     assert list(want) == ref
     assert got.tolist() == list(want)
+
+
+def test_utf8_misaligned_buffer_uses_fallback(cuda):
+    import torch
+    rng = np.random.default_rng(77)
+    bodies = _near_utf8(rng, 3000)
+    frames = [b"\x12\x34\x00\x00\x80" + b for b in bodies]
+    off = np.concatenate([[0], np.cumsum([len(f) for f in frames])]).astype(np.int64)
+    flat = np.frombuffer(b"".join(frames), np.uint8)
+    raw = torch.zeros(len(flat) + 16, dtype=torch.uint8, device=cuda)
+    view = raw[3:3 + len(flat)]
+    view.copy_(dev(flat, cuda))
+    got = host(batch.validate_utf8(view, 5, frame_off=dev(off, cuda)))
+    assert np.array_equal(got, codec_np.utf8_valid(flat, off, 5))
