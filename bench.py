@@ -182,6 +182,9 @@ def legs(torch, batch, device, steps):
                                                                    window=500), steps, 3) / steps
     out["proxy_dedup_1M_window500"] = {"Mpkt_s": n1 / ms_x / 1e3, "ms": ms_x}
     del tab1, pay1, lens1, flat1, enc
+    # socket boundary: 1M one-character frames sendmmsg'd over loopback, recvmmsg'd into a
+    # pinned ring and decoded on the GPU per received batch (rudp.netio)
+    out["socket_e2e_1M_x_1char"] = socket_leg(torch, batch, device)
     # device-to-device streaming-copy ceiling (dwordx4 nt copy kernel, rudpx_copy),
     # same byte count as one encode's payload
     import ctypes
@@ -222,6 +225,41 @@ def legs(torch, batch, device, steps):
         "pcie_GBs_each_way": n * (L + 6) / dt / 1e9,
         "note": "pinned host in/out, rudp_encode_host (H2D, kernel, D2H on two streams)"}
     return out
+
+
+def socket_leg(torch, batch, device, n=1 << 20):
+    import socket
+    import threading
+    from rudp import netio
+    tab, pay = batch.synth_batch(n, 1, SEEDS[1472], device=device)
+    enc = batch.pack_batch_varlen(tab, pay.view(-1), torch.ones(n, dtype=torch.int32, device=device),
+                                  "rudp7")
+    frames, off = enc.frames.cpu().numpy(), enc.frame_off.cpu().numpy()
+    rx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    rx.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 27)
+    rx.bind(("127.0.0.1", 0))
+    tx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    recv = netio.BatchReceiver(rx, max_msgs=1 << 16, slot_bytes=64)
+    port = rx.getsockname()[1]
+    got = good = batches = 0
+    sender = threading.Thread(target=lambda: netio.send_batch(tx, frames, off, "127.0.0.1", port))
+    t0 = time.perf_counter()
+    sender.start()
+    while True:
+        k = recv.recv(timeout_ms=300)
+        if k == 0:
+            break
+        dec, _, _ = recv.decode("rudp7", device)
+        good += int((dec.ok == 1).sum().item())
+        got += k
+        batches += 1
+    dt = time.perf_counter() - t0 - 0.3  # minus the final idle timeout
+    sender.join()
+    rx.close()
+    tx.close()
+    return {"received": got, "verified": good, "batches": batches, "wall_s": dt,
+            "Mpkt_s": got / dt / 1e6,
+            "note": "loopback kernel UDP stack bound; sendmmsg/recvmmsg 1024 per call"}
 
 
 def config1_loopback():

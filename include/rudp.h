@@ -153,6 +153,27 @@ int rudp_dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_nu
                       void* hip_stream);
 
 /*
+ * Batched UDP socket I/O (host only, no device work): the reference moves one
+ * datagram per system call (sendto, utils/reliableUDP.py:61; recvfrom(1024),
+ * :67, :118; proxy.py:129).  These move up to 1024 per call (sendmmsg /
+ * recvmmsg) between a socket and caller-owned host buffers, in the packed
+ * frames + offsets layout of rudp_encode_varlen / variable-length rudp_decode.
+ *
+ * rudp_udp_recv_batch: waits up to timeout_ms (-1 forever, 0 not at all) for
+ * a first datagram, then drains up to min(max_msgs, cap_bytes / slot_bytes)
+ * without blocking.  A datagram longer than slot_bytes is truncated (as the
+ * reference's recvfrom(1024) truncates).  Frames are packed from h_frames[0];
+ * h_frame_off receives count+1 offsets.  Returns the count (0 on timeout) or
+ * a negative errno.
+ * rudp_udp_send_batch: sends frames [h_frame_off[i], h_frame_off[i+1]) for
+ * i < n to ip:port.  Returns the count sent or a negative errno.
+ */
+int rudp_udp_recv_batch(int fd, uint8_t* h_frames, uint64_t cap_bytes, uint32_t slot_bytes,
+                        uint32_t max_msgs, uint64_t* h_frame_off, int timeout_ms);
+int rudp_udp_send_batch(int fd, const uint8_t* h_frames, const uint64_t* h_frame_off, uint64_t n,
+                        const char* ip, uint16_t port);
+
+/*
  * Host-memory conveniences: same semantics, host pointers in and out.
  * Staged through a ring of device slots in chunks, with H2D, kernel and D2H
  * on three streams chained by events so the three overlap.  Synchronous.  These model the reference's

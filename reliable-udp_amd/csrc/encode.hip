@@ -40,8 +40,8 @@ __device__ __forceinline__ void store16(u32x4 v, u32x4* p) {
     *p = v;
 }
 
-template <int H, bool NTL, bool NTS, int P1, bool CONTIG>
-__global__ void __launch_bounds__(kBlock) encode_tile_kernel(EncodeTileArgs a) {
+template <int H, bool NTL, bool NTS, int P1, bool CONTIG, int BLOCK = kBlock>
+__global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   uint64_t* lds_hdr = reinterpret_cast<uint64_t*>(lds);  // [T + 1]
   unsigned char* lds_pay = lds + a.hdr_bytes;            // guard + T*L + tail guard
@@ -49,7 +49,8 @@ __global__ void __launch_bounds__(kBlock) encode_tile_kernel(EncodeTileArgs a) {
   const uint32_t tid = threadIdx.x;
   const uint32_t L = a.L;
   const uint32_t T = a.T;
-  const uint32_t glog = a.glog;
+  // a.glog is lanes-per-packet for 256-thread groups; wider groups give each packet more lanes
+  const uint32_t glog = a.glog + (BLOCK == 1024 ? 2u : BLOCK == 512 ? 1u : 0u);
   const uint32_t G = 1u << glog;
   uint32_t tile = blockIdx.x;
   if (a.xcd_swizzle) {
@@ -77,16 +78,16 @@ __global__ void __launch_bounds__(kBlock) encode_tile_kernel(EncodeTileArgs a) {
     const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + p0 * (uint64_t)L);
     u32x4* dst = reinterpret_cast<u32x4*>(lds_pay + kLdsGuard);
     const uint32_t nvec = Tv * V;
-    for (uint32_t v0 = tid; v0 < nvec; v0 += (uint32_t)P1 * kBlock) {
+    for (uint32_t v0 = tid; v0 < nvec; v0 += (uint32_t)P1 * BLOCK) {
       u32x4 r[P1];
 #pragma unroll
       for (int u = 0; u < P1; ++u) {
-        const uint32_t v = v0 + (uint32_t)u * kBlock;
+        const uint32_t v = v0 + (uint32_t)u * BLOCK;
         if (v < nvec) r[u] = load16<NTL>(src + v);
       }
 #pragma unroll
       for (int u = 0; u < P1; ++u) {
-        const uint32_t v = v0 + (uint32_t)u * kBlock;
+        const uint32_t v = v0 + (uint32_t)u * BLOCK;
         if (v < nvec) dst[v] = r[u];
       }
     }
@@ -131,7 +132,7 @@ __global__ void __launch_bounds__(kBlock) encode_tile_kernel(EncodeTileArgs a) {
   const uint32_t nbytes = Tv * F;
   unsigned char* out = a.frames + p0 * (uint64_t)F;
   const uint32_t* pay_dw = reinterpret_cast<const uint32_t*>(lds_pay);
-  for (uint32_t x = tid * 16u; x < nbytes; x += kBlock * 16u) {
+  for (uint32_t x = tid * 16u; x < nbytes; x += BLOCK * 16u) {
     const uint32_t qq = (uint32_t)(((uint64_t)x * a.invF) >> 32);  // x / F
     const uint32_t r = x - qq * F;           // frame position of chunk byte 0
     const int kA0 = r < (uint32_t)H ? H - (int)r : 0;  // first payload byte of qq
@@ -192,7 +193,7 @@ __global__ void __launch_bounds__(kBlock) encode_bytes_kernel(EncodeTileArgs a) 
   if (lane == 0 && a.csum) a.csum[p] = (uint16_t)c;
 }
 
-template <int H, bool NTL, bool NTS, int P1, bool CONTIG>
+template <int H, bool NTL, bool NTS, int P1, bool CONTIG, int BLOCK = kBlock>
 int launch_tile(const EncodeTileArgs& args, hipStream_t stream) {
   const uint64_t blocks = (args.n + args.T - 1) / args.T;
   size_t lds = args.hdr_bytes + kLdsGuard + (size_t)args.T * args.L + 32;
@@ -206,11 +207,11 @@ int launch_tile(const EncodeTileArgs& args, hipStream_t stream) {
     if (want > lds) lds = want;
   }
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_tile_kernel<H, NTL, NTS, P1, CONTIG>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_tile_kernel<H, NTL, NTS, P1, CONTIG, BLOCK>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL((encode_tile_kernel<H, NTL, NTS, P1, CONTIG>), dim3((uint32_t)blocks), dim3(kBlock), lds,
+  hipLaunchKernelGGL((encode_tile_kernel<H, NTL, NTS, P1, CONTIG, BLOCK>), dim3((uint32_t)blocks), dim3(BLOCK), lds,
                      stream, args);
   return (int)hipGetLastError();
 }
@@ -227,6 +228,9 @@ int launch_tile_nt(const EncodeTileArgs& args, hipStream_t stream) {
 template <int H>
 int launch_tile_policy(const EncodeTileArgs& args, hipStream_t stream) {
   const int p1 = tuning().encode_p1;
+  const int block = tuning().encode_block;
+  if (block == 512) return launch_tile<H, true, true, 8, true, 512>(args, stream);
+  if (block == 1024) return launch_tile<H, true, true, 8, true, 1024>(args, stream);
   if (tuning().encode_contig) {
     if (p1 == 2) return launch_tile_nt<H, 2, true>(args, stream);
     if (p1 == 4) return launch_tile_nt<H, 4, true>(args, stream);

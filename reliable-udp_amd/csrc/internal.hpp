@@ -105,6 +105,7 @@ struct Tuning {
   int decode_glog = -1;   // verify kernel lanes-per-packet log2; -1 = automatic
   int encode_xcd_swizzle = 0;  // XCD-contiguous tile order (T1)
   int encode_contig = 1;  // phase 1 streams the tile contiguously, sums from LDS
+  int encode_block = 256;  // tile workgroup size (256, 512, 1024)
   int host_slots = 3;     // *_host pipeline: device staging slots (2..8)
   int host_stage_mb = 128;  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
 };

@@ -20,7 +20,8 @@ CSRC = ROOT / "csrc"
 INCLUDE = ROOT.parent / "include"
 BUILD = ROOT / "build"
 LIB = PKG_DIR / "librudp.so"
-SOURCES = ("encode.hip", "decode.hip", "synth.hip", "varlen.hip", "dedup.hip", "capi.hip", "tuning.hip")
+SOURCES = ("encode.hip", "decode.hip", "synth.hip", "varlen.hip", "dedup.hip", "capi.hip", "tuning.hip",
+           "netio.cpp")
 ARCH = "gfx950"
 
 
@@ -48,7 +49,11 @@ def build(force: bool = False, verbose: bool = False) -> Path:
         s = CSRC / src
         o = BUILD / (Path(src).stem + ".o")
         if force or not o.exists() or o.stat().st_mtime < max(s.stat().st_mtime, hdr_time):
-            cmd = [hipcc, *flags, "-c", str(s), "-o", str(o)]
+            if s.suffix == ".cpp":  # host-only C++ (no HIP): plain g++
+                cmd = [shutil.which("g++") or "g++", "-O2", "-std=c++17", "-fPIC", "-Wall",
+                       f"-I{INCLUDE}", "-c", str(s), "-o", str(o)]
+            else:
+                cmd = [hipcc, *flags, "-c", str(s), "-o", str(o)]
             if verbose:
                 print(" ".join(cmd), file=sys.stderr)
             r = subprocess.run(cmd, capture_output=True, text=True)

@@ -25,6 +25,7 @@ EXPORTS = (
     "rudp_encode", "rudp_decode", "rudp_encode_host", "rudp_decode_host",
     "rudp_synth", "rudp_device_count", "rudp_last_error", "rudp_abi_version",
     "rudp_encode_varlen", "rudp_validate_utf8", "rudp_dedup_window",
+    "rudp_udp_recv_batch", "rudp_udp_send_batch",
 )
 
 
@@ -64,6 +65,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rudp_encode_varlen": [ctypes.POINTER(RudpBatch), P, P, P, I, I, P],
         "rudp_validate_utf8": [P, P, U32, U64, I, P, I, P],
         "rudp_dedup_window": [P, P, U32, U64, U32, P, I, P],
+        "rudp_udp_recv_batch": [I, P, U64, U32, U32, P, I],
+        "rudp_udp_send_batch": [I, P, P, U64, ctypes.c_char_p, ctypes.c_uint16],
         "rudp_device_count": [ctypes.POINTER(ctypes.c_int)],
         "rudp_abi_version": [],
     }

@@ -1,0 +1,96 @@
+"""Batched UDP socket I/O at the codec's host boundary.
+
+The reference does one system call per datagram: sendto (utils/
+reliableUDP.py:61) and recvfrom(1024) (:67, :118; proxy.py:129).  Here up to
+1024 datagrams move per call (recvmmsg / sendmmsg in librudp.so) directly
+into / out of pinned host buffers, in the packed-frames + offsets layout the
+variable-length GPU codec consumes and produces:
+
+    rx = BatchReceiver(sock, max_msgs=65536)
+    n = rx.recv(timeout_ms=100)              # socket -> pinned ring
+    dec = rx.decode("rudp5", device)         # pinned ring -> HBM -> unpack_batch_varlen
+
+    send_batch(sock, frames, frame_off, ip, port)   # pack_batch_varlen output -> wire
+"""
+from __future__ import annotations
+
+import ctypes
+import socket as _socket
+
+import numpy as np
+
+from . import _native
+from . import batch as _batch
+
+
+def _np_ptr(a) -> int:
+    return a.ctypes.data
+
+
+def recv_batch(sock: _socket.socket, frames: np.ndarray, frame_off: np.ndarray, *,
+               slot_bytes: int = 1024, max_msgs: int | None = None, timeout_ms: int = -1) -> int:
+    """Receive up to ``max_msgs`` datagrams into ``frames`` (u8, packed) and
+    ``frame_off`` (int64, count + 1).  Datagrams longer than ``slot_bytes`` are
+    truncated, as recvfrom(1024) truncates in the reference.  Returns the count
+    (0 on timeout)."""
+    if frames.dtype != np.uint8 or frames.ndim != 1 or not frames.flags["C_CONTIGUOUS"]:
+        raise TypeError("frames must be a contiguous 1-D uint8 array")
+    if frame_off.dtype != np.int64 or frame_off.ndim != 1 or not frame_off.flags["C_CONTIGUOUS"]:
+        raise TypeError("frame_off must be a contiguous 1-D int64 array")
+    cap_msgs = frame_off.shape[0] - 1
+    max_msgs = cap_msgs if max_msgs is None else min(max_msgs, cap_msgs)
+    if max_msgs < 0:
+        raise ValueError("frame_off needs at least one entry")
+    rc = _native.lib().rudp_udp_recv_batch(sock.fileno(), _np_ptr(frames), frames.nbytes,
+                                           slot_bytes, max_msgs, _np_ptr(frame_off), timeout_ms)
+    if rc < 0:
+        raise OSError(-rc, f"recvmmsg: {rc}")
+    return rc
+
+
+def send_batch(sock: _socket.socket, frames: np.ndarray, frame_off: np.ndarray, ip: str,
+               port: int) -> int:
+    """Send frames [frame_off[i], frame_off[i+1]) to ip:port; returns the count sent."""
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    frame_off = np.ascontiguousarray(frame_off, dtype=np.int64)
+    n = frame_off.shape[0] - 1
+    if n > 0 and (frame_off[0] < 0 or frame_off[-1] > frames.nbytes or (np.diff(frame_off) < 0).any()):
+        raise ValueError("frame_off must be non-decreasing offsets inside frames")
+    rc = _native.lib().rudp_udp_send_batch(sock.fileno(), _np_ptr(frames) if frames.size else None,
+                                           _np_ptr(frame_off), max(n, 0), ip.encode(), port)
+    if rc < 0:
+        raise OSError(-rc, f"sendmmsg: {rc}")
+    return rc
+
+
+class BatchReceiver:
+    """A pinned receive ring for one socket, decoded on the GPU in one launch."""
+
+    def __init__(self, sock: _socket.socket, max_msgs: int = 65536, slot_bytes: int = 1024):
+        import torch
+        self.sock = sock
+        self.slot_bytes = slot_bytes
+        self.max_msgs = max_msgs
+        self._frames_t = torch.empty((max_msgs * slot_bytes,), dtype=torch.uint8, pin_memory=True)
+        self._off_t = torch.empty((max_msgs + 1,), dtype=torch.int64, pin_memory=True)
+        self.frames = self._frames_t.numpy()
+        self.frame_off = self._off_t.numpy()
+        self.count = 0
+
+    def recv(self, timeout_ms: int = -1) -> int:
+        self.count = recv_batch(self.sock, self.frames, self.frame_off, slot_bytes=self.slot_bytes,
+                                max_msgs=self.max_msgs, timeout_ms=timeout_ms)
+        return self.count
+
+    def frame(self, i: int) -> bytes:
+        return bytes(self.frames[self.frame_off[i]:self.frame_off[i + 1]])
+
+    def decode(self, layout="rudp5", device=None, csum=None, stream=None):
+        """H2D of the received frames, then parse + verify them on the device."""
+        import torch
+        dev = torch.device(device) if device is not None else torch.device("cuda", 0)
+        n = self.count
+        total = int(self.frame_off[n])
+        d_frames = self._frames_t[:total].to(dev, non_blocking=True)
+        d_off = self._off_t[:n + 1].to(dev, non_blocking=True)
+        return _batch.unpack_batch_varlen(d_frames, d_off, layout, csum=csum, stream=stream), d_frames, d_off

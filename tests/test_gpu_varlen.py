@@ -197,3 +197,34 @@ def test_utf8_misaligned_buffer_uses_fallback(cuda):
     view.copy_(dev(flat, cuda))
     got = host(batch.validate_utf8(view, 5, frame_off=dev(off, cuda)))
     assert np.array_equal(got, codec_np.utf8_valid(flat, off, 5))
+
+
+def test_socket_ring_to_gpu_decode(cuda):
+    """Datagrams from a UDP socket (recvmmsg into a pinned ring) decoded on the GPU."""
+    import socket
+    import threading
+
+    from rudp import netio
+    n = 30000
+    rng = np.random.default_rng(21)
+    seq, ack, flags, _ = synth.synth(21, 0, n, 0)
+    pays = [bytes([int(c)]) for c in rng.integers(32, 127, n)]  # one character each (reliableUDP.py:11)
+    fr, off, cs = codec_np.encode_varlen(seq, ack, flags, pays, 7)
+    rx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    rx.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 25)
+    rx.bind(("127.0.0.1", 0))
+    tx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    t = threading.Thread(target=lambda: netio.send_batch(tx, fr, off, "127.0.0.1", rx.getsockname()[1]))
+    t.start()
+    recv = netio.BatchReceiver(rx, max_msgs=n, slot_bytes=64)
+    seen = []
+    while len(seen) < n:
+        k = recv.recv(timeout_ms=2000)
+        assert k > 0
+        dec, _, _ = recv.decode("rudp7", cuda)
+        seen += list(zip(host(dec.seq), host(dec.ok)))
+    t.join()
+    assert [s for s, _ in seen] == seq.tolist()
+    assert all(o == 1 for _, o in seen)
+    rx.close()
+    tx.close()

@@ -70,19 +70,17 @@ def encode_sweep(reps):
             batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
 
         variants = {}
-        for contig in (1,):
-            for p1 in (8, 4):
-                for per_cu in (-1, 0, 4, 6):
-                    def setup(contig=contig, p1=p1, per_cu=per_cu):
-                        lib.rudpx_tune(7, contig)
-                        lib.rudpx_tune(3, p1)
-                        lib.rudpx_tune(6, per_cu)
-                    variants[f"L{L}_contig{contig}_p1{p1}_percu{per_cu}"] = (setup, run)
+        for block in (256, 512, 1024):
+            for per_cu in ((-1, 0) if block == 256 else (0, 1, 2, 3)):
+                def setup(block=block, per_cu=per_cu):
+                    lib.rudpx_tune(10, block)
+                    lib.rudpx_tune(6, per_cu)
+                variants[f"L{L}_block{block}_percu{per_cu}"] = (setup, run)
         res = interleaved(variants, reps)
         alg = n * (2 * L + 12)
         # every variant must produce the default kernel's frames bit for bit
         tab0, pay0, _ = sets[0]
-        lib.rudpx_tune(7, 0), lib.rudpx_tune(3, 8), lib.rudpx_tune(6, 0)
+        lib.rudpx_tune(7, 0), lib.rudpx_tune(3, 8), lib.rudpx_tune(6, 0), lib.rudpx_tune(10, 256)
         want, _ = batch.pack_batch(tab0, pay0, 7)  # the original per-packet phase 1
         for k, (setup, _) in variants.items():
             setup()
@@ -99,6 +97,7 @@ def encode_sweep(reps):
     lib.rudpx_tune(5, 0)
     lib.rudpx_tune(6, -1)
     lib.rudpx_tune(7, 1)
+    lib.rudpx_tune(10, 256)
     return out
 
 
