@@ -337,6 +337,14 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, ui
     path = a.payload_out ? DecodePath::kCopy : DecodePath::kVerify;
     // the verify kernel reads the header from the group's first two lanes
     a.glog = (path == DecodePath::kVerify && lg == 0) ? 1 : lg;
+    // stage whole tiles in LDS when a tile fits in 64 KiB
+    const bool tile_fits = (size_t)(256u >> lg) * frame_len + 48 <= 65536;
+    if (path == DecodePath::kCopy && tile_fits && tuning().decode_copy_tile)
+      path = DecodePath::kCopyTile;
+    if (path == DecodePath::kVerify && tile_fits && tuning().decode_verify_tile) {
+      path = DecodePath::kVerifyTile;
+      a.glog = lg;
+    }
     const int forced = tuning().decode_glog;  // experiments only (rudpx_tune)
     if (path == DecodePath::kVerify && forced >= 1 && forced <= 4 &&
         (1u << forced) <= (frame_len - (uint32_t)layout) / 16u)

@@ -199,6 +199,70 @@ __global__ void __launch_bounds__(kBlock) decode_verify_kernel(DecodeArgs a) {
   }
 }
 
+// Copy-out decode through LDS (payload_out != null): the mirror of the encode
+// tile kernel.  A workgroup owns T = 256/G frames; T is a multiple of 16, so
+// the tile's frames start 16-byte aligned.  Phase 1 streams them into LDS like
+// a copy (lane t: vectors t, t+256, ...).  Phase 2: G lanes per frame read the
+// payload back as byte-shifted LDS windows (5 ds_read_b32 + v_alignbyte), sum
+// the LE u16 halves and store the windows to payload_out 16-byte aligned; the
+// group leader parses the header out of LDS.
+template <int H, bool COPY>
+__global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t glog = a.glog;
+  const uint32_t G = 1u << glog;
+  const uint32_t T = kBlock >> glog;
+  const uint32_t q = tid >> glog;
+  const uint32_t g = tid & (G - 1u);
+  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  const uint64_t left = a.n - p0;
+  const uint32_t Tv = left < T ? (uint32_t)left : T;
+  const uint32_t F = a.F;
+  const uint32_t L = F - H;
+  const uint64_t total = a.n * (uint64_t)F;
+  const uint64_t base = p0 * (uint64_t)F;  // 16-byte aligned: T % 16 == 0
+  const uint32_t nbytes = Tv * F;
+  const uint32_t nvec = (nbytes + 15u) >> 4;
+  u32x4* tile = reinterpret_cast<u32x4*>(lds);
+  for (uint32_t v0 = tid; v0 < nvec; v0 += 8u * kBlock) {
+    u32x4 r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t v = v0 + (uint32_t)u * kBlock;
+      if (v < nvec) r[u] = load16_guarded(a.frames, base + 16ull * v, total);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t v = v0 + (uint32_t)u * kBlock;
+      if (v < nvec) tile[v] = r[u];
+    }
+  }
+  __syncthreads();
+  const uint32_t* dw = reinterpret_cast<const uint32_t*>(lds);
+  uint32_t sum = 0;
+  const uint64_t p = p0 + q;
+  if (q < Tv) {
+    const uint32_t V = L >> 4;
+    const uint32_t pay = q * F + H;  // LDS byte offset of the payload
+    for (uint32_t v = g; v < V; v += G) {
+      const u32x4 w = window16_dw(dw, pay + 16u * v);
+      sum += le16_sum(w);
+      if (COPY)
+        __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(a.payload_out + p * (uint64_t)L + 16ull * v));
+    }
+  }
+  for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
+  if (g == 0 && q < Tv) {
+    const u32x4 h = window16_dw(dw, q * F);
+    const uint32_t seq = ((h.x & 0xFFu) << 8) | ((h.x >> 8) & 0xFFu);
+    const uint32_t ack = (((h.x >> 16) & 0xFFu) << 8) | (h.x >> 24);
+    const uint32_t flags = h.y & 0xFFu;
+    const uint32_t inband = (((h.y >> 8) & 0xFFu) << 8) | ((h.y >> 16) & 0xFFu);
+    finish_packet<H>(a, p, sum, seq, ack, flags, inband);
+  }
+}
+
 // Any frame length: one wave per packet, byte-granular.  Frames shorter
 // than the header report RUDP_OK_SHORT with the fields that are present,
 // truncated the way utils/packet.py:31 slices a short bit string.
@@ -246,7 +310,17 @@ int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream
   if (path != DecodePath::kBytes) {
     const uint32_t per_block = kBlock >> args.glog;
     const uint64_t blocks = (args.n + per_block - 1) / per_block;
-    if (path == DecodePath::kVerify) {
+    if (path == DecodePath::kCopyTile || path == DecodePath::kVerifyTile) {
+      const size_t lds = ((size_t)per_block * args.F + 32 + 15) & ~size_t(15);
+      const dim3 grid((uint32_t)blocks), block(kBlock);
+      if (path == DecodePath::kCopyTile) {
+        if (layout == 7) hipLaunchKernelGGL((decode_tile_kernel<7, true>), grid, block, lds, stream, args);
+        else hipLaunchKernelGGL((decode_tile_kernel<5, true>), grid, block, lds, stream, args);
+      } else {
+        if (layout == 7) hipLaunchKernelGGL((decode_tile_kernel<7, false>), grid, block, lds, stream, args);
+        else hipLaunchKernelGGL((decode_tile_kernel<5, false>), grid, block, lds, stream, args);
+      }
+    } else if (path == DecodePath::kVerify) {
       if (layout == 7)
         hipLaunchKernelGGL(decode_verify_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
       else

@@ -93,7 +93,7 @@ constexpr uint32_t kTileMaxPayload = 4096;
 // keeps every per-packet word sum exact in 32 bits (32768 words x 0xFFFF).
 constexpr uint32_t kMaxPayload = 65535;
 
-enum class DecodePath { kBytes, kCopy, kVerify };
+enum class DecodePath { kBytes, kCopy, kCopyTile, kVerify, kVerifyTile };
 
 // Non-ABI tuning knobs (rudpx_tune in tuning.hip), read at launch.
 struct Tuning {
@@ -106,6 +106,8 @@ struct Tuning {
   int encode_xcd_swizzle = 0;  // XCD-contiguous tile order (T1)
   int encode_contig = 1;  // phase 1 streams the tile contiguously, sums from LDS
   int encode_block = 256;  // tile workgroup size (256, 512, 1024)
+  int decode_copy_tile = 1;  // copy-out decode through an LDS tile (0: register windows)
+  int decode_verify_tile = 1;  // verify-only decode through an LDS tile (0: aligned-chunk kernel)
   int host_slots = 3;     // *_host pipeline: device staging slots (2..8)
   int host_stage_mb = 128;  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
 };

@@ -79,7 +79,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // loads in flight per lane (2, 4, 8); 4: decode-verify log2 lanes per packet
 // (1..4, -1 = auto); 5: XCD-contiguous tile order; 6: encode tiles per CU cap;
 // 7: contiguous phase-1 stream with checksums summed from LDS; 8: host pipeline
-// slots; 9: host pipeline MiB per slot; 10: encode tile workgroup size.
+// slots; 9: host pipeline MiB per slot; 10: encode tile workgroup size;
+// 11: copy-out decode through an LDS tile; 12: verify-only decode through an LDS tile.
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
@@ -88,7 +89,8 @@ int rudpx_tune(int key, int value) {
             : key == 4 ? &t.decode_glog : key == 5 ? &t.encode_xcd_swizzle
             : key == 6 ? &t.encode_blocks_per_cu : key == 7 ? &t.encode_contig
             : key == 8 ? &t.host_slots : key == 9 ? &t.host_stage_mb
-            : key == 10 ? &t.encode_block : nullptr;
+            : key == 10 ? &t.encode_block : key == 11 ? &t.decode_copy_tile
+            : key == 12 ? &t.decode_verify_tile : nullptr;
   if (!slot) return -22;
   const int old = *slot;
   *slot = value;

@@ -216,3 +216,34 @@ def test_c4_roundtrip_full_size(cuda, digests):
     assert torch.equal(d.ack.view(torch.int16), tab.ack.view(torch.int16))
     assert torch.equal(d.flags, tab.flags)
     assert torch.equal(d.csum.view(torch.int16), cs.view(torch.int16))
+
+
+@pytest.mark.parametrize("L", [16, 64, 256, 1472, 4096, 8192])
+def test_decode_paths_agree(cuda, L):
+    """Every decode kernel (LDS tile, aligned chunks, register windows) gives the same answer."""
+    import ctypes
+    from rudp import _native
+    lib = _native.lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    n = 3001
+    seq, ack, flags, pay = synth.synth(0x77 + L, 0, n, L, ascii=False)
+    fr, cs = gpu_encode(cuda, seq, ack, flags, pay, 7)
+    fr[17, 9] ^= 0x40  # one corrupted frame
+    want = codec_np.decode(fr, 7)
+    results = []
+    for verify_tile, copy_tile in ((1, 1), (0, 0)):
+        lib.rudpx_tune(12, verify_tile)
+        lib.rudpx_tune(11, copy_tile)
+        try:
+            for copy in (False, True):
+                d = batch.unpack_batch(dev(fr, cuda), 7, copy_payload=copy)
+                got = [host(x) for x in (d.seq, d.ack, d.flags, d.ok, d.csum)]
+                for g, w in zip(got, want[:5]):
+                    assert np.array_equal(g, w), (L, verify_tile, copy)
+                if copy:
+                    assert np.array_equal(host(d.payload), fr[:, 7:])
+                results.append(got)
+        finally:
+            lib.rudpx_tune(12, 1)
+            lib.rudpx_tune(11, 1)
+    assert host(d.ok)[17] == 0

@@ -104,7 +104,7 @@ def encode_sweep(reps):
 def decode_sweep(reps):
     dev = torch.device("cuda", 0)
     out = {}
-    for L in (1472, 64):
+    for L in (1472, 1024, 256, 64):
         n = 1 << 20
         nsets = 1 if L > 512 else 7
         frs = []
@@ -129,11 +129,14 @@ def decode_sweep(reps):
                                           seq.data_ptr(), ok.data_ptr(), ok.data_ptr(), None,
                                           pay_out.data_ptr(), 7, 0,
                                           torch.cuda.current_stream().cuda_stream))
-        variants = {f"L{L}_copyout": (lambda: None, copy)}
-        for glog in ((-1, 1, 2, 3, 4) if L > 256 else (-1, 1, 2)):
-            variants[f"L{L}_verify_glog{glog}"] = (lambda glog=glog: lib.rudpx_tune(4, glog), verify)
+        variants = {f"L{L}_copyout_tile": (lambda: lib.rudpx_tune(11, 1), copy),
+                    f"L{L}_copyout_regs": (lambda: lib.rudpx_tune(11, 0), copy)}
+        variants[f"L{L}_verify_chunks"] = (lambda: lib.rudpx_tune(12, 0), verify)
+        variants[f"L{L}_verify_tile"] = (lambda: lib.rudpx_tune(12, 1), verify)
         res = interleaved(variants, reps)
         lib.rudpx_tune(4, -1)
+        lib.rudpx_tune(11, 1)
+        lib.rudpx_tune(12, 1)
         for k, ms in res.items():
             alg = n * (L + 13) if "verify" in k else n * (2 * L + 13)
             out[k] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0}
