@@ -23,7 +23,7 @@ from rudp import batch  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--op", choices=["encode", "decode", "roundtrip"], default="encode")
+    ap.add_argument("--op", choices=["encode", "decode", "decode_copy", "roundtrip"], default="encode")
     ap.add_argument("--L", type=int, default=1472)
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--layout", default="rudp7")
@@ -38,6 +38,19 @@ def main():
         tab, pay = batch.synth_batch(args.n, args.L, 0x5EED0004, device=dev)
         fr, _ = batch.pack_batch(tab, pay, args.layout)
         sets.append((tab, pay, fr))
+    import ctypes
+    from rudp import _native
+    lib = _native.lib()
+    scratch = [torch.empty(args.n, dtype=torch.uint16, device=dev) for _ in range(2)] + \
+              [torch.empty(args.n, dtype=torch.uint8, device=dev) for _ in range(2)]
+
+    def decode_copy(tab, pay, fr):
+        # copy-out decode into the payload buffer (aligned), preallocated outputs
+        _native.check(lib.rudp_decode(fr.data_ptr(), None, args.L + H, args.n, None,
+                                      scratch[0].data_ptr(), scratch[1].data_ptr(),
+                                      scratch[2].data_ptr(), scratch[3].data_ptr(), None,
+                                      pay.data_ptr(), H, 0, torch.cuda.current_stream().cuda_stream))
+    del ctypes
 
     def step(i):
         tab, pay, fr = sets[i % nsets]
@@ -45,6 +58,8 @@ def main():
             batch.pack_batch(tab, pay, args.layout, out=fr, want_csum=False)
         if args.op in ("decode", "roundtrip"):
             batch.unpack_batch(fr, args.layout)
+        if args.op == "decode_copy":
+            decode_copy(tab, pay, fr)
 
     for i in range(3):
         step(i)
