@@ -159,6 +159,19 @@ def legs(torch, batch, device, steps):
         "GiB_s": (1 << 20) * 1472 / (ms / 1e3) / GIB, "ms": ms,
         "roofline_frac": (1 << 20) * (algorithmic_bytes_encode(1472) + algorithmic_bytes_decode(1472))
         / (ms / 1e3) / 1e9 / HBM_PEAK_GBS}
+    # BASELINE config 5's shape on one GPU: 16M x 1472 B (23.6 GB in, 23.7 GB out)
+    del w
+    torch.cuda.empty_cache()
+    w16 = Workload(torch, batch, 1 << 24, 1472, "rudp7", 0, 0x5EED0005, device, min_bytes=0)
+    ms = time_loop(torch, lambda i: w16.encode(batch, i), max(3, steps // 5), 1) / max(3, steps // 5)
+    out["encode_16Mx1472_C5_1gpu"] = {
+        "GiB_s": (1 << 24) * 1472 / (ms / 1e3) / GIB, "ms": ms,
+        "roofline_frac": (1 << 24) * algorithmic_bytes_encode(1472) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS}
+    del w16
+    torch.cuda.empty_cache()
+    w = Workload(torch, batch, 1 << 20, 1472, "rudp7", 0, SEEDS[1472], device)
+    for i in range(len(w.sets)):
+        w.encode(batch, i)
     # strict UTF-8 validation of the 1M x 1472 frames (get_payload strictness)
     fr = w.sets[0][2]
     ms = time_loop(torch, lambda i: batch.validate_utf8(fr, "rudp7"), steps, 3) / steps
@@ -305,7 +318,9 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU")
+    ap.add_argument("--packets", type=int, default=1 << 20, help="packets per GPU (weak scaling)")
+    ap.add_argument("--total-packets", type=int, default=0,
+                    help="strong scaling: split this many packets over the ranks (C5: 16777216)")
     ap.add_argument("--payload", type=int, default=1472)
     ap.add_argument("--layout", default="rudp7", choices=["rudp5", "rudp7"])
     ap.add_argument("--no-legs", action="store_true")
@@ -341,6 +356,10 @@ def main():
             dist.init_process_group("nccl", device_id=device)
 
     n, L = args.packets, args.payload
+    if args.total_packets:
+        if args.total_packets % world:
+            raise SystemExit("--total-packets must divide evenly over the ranks")
+        n = args.total_packets // world
     seed = SEEDS.get(L, 0x5EED0004)
     w = Workload(torch, batch, n, L, args.layout, rank * n, seed, device)
     for i in range(args.warmup):
@@ -385,7 +404,7 @@ def main():
             "warmup": args.warmup,
             "ms_per_step": wall_max / args.steps * 1e3,
             "higher_is_better": True,
-            "scaling": "weak",
+            "scaling": "strong" if args.total_packets else "weak",
             "vs_baseline": None,
             "dtype": "u8",
             "data": "synthetic (on-device splitmix64, ASCII payloads)",

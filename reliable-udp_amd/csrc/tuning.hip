@@ -50,9 +50,52 @@ int launch_copy_vpt(const void* src, void* dst, uint64_t n16, hipStream_t s) {
   return (int)hipGetLastError();
 }
 
+// Diagnostic: the encode kernel's memory pattern with no compute.  A block
+// streams a contiguous tile of `tile16` vectors into LDS (lane t: t, t+256,
+// ...), barriers, and streams it back out contiguously from LDS.
+__global__ void __launch_bounds__(kBlock) copy_tile_kernel(const u32x4* __restrict__ src,
+                                                           u32x4* __restrict__ dst, uint64_t n16,
+                                                           uint32_t tile16) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  u32x4* t = reinterpret_cast<u32x4*>(lds);
+  const uint64_t base = (uint64_t)blockIdx.x * tile16;
+  const uint32_t m = (uint32_t)((n16 - base) < tile16 ? (n16 - base) : tile16);
+  for (uint32_t v0 = threadIdx.x; v0 < m; v0 += 8u * kBlock) {
+    u32x4 r[8];
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t v = v0 + (uint32_t)u * kBlock;
+      if (v < m) r[u] = __builtin_nontemporal_load(src + base + v);
+    }
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t v = v0 + (uint32_t)u * kBlock;
+      if (v < m) t[v] = r[u];
+    }
+  }
+  __syncthreads();
+  for (uint32_t v = threadIdx.x; v < m; v += kBlock) __builtin_nontemporal_store(t[v], dst + base + v);
+}
+
 }  // namespace rudp
 
 extern "C" {
+
+// LDS-staged tile copy (diagnostic); lds_bytes >= tile16*16 sets occupancy.
+int rudpx_copy_tile(const void* src, void* dst, uint64_t n16, uint32_t tile16, uint32_t lds_bytes,
+                    void* stream) {
+  const uint64_t blocks = (n16 + tile16 - 1) / tile16;
+  size_t lds = (size_t)tile16 * 16;
+  if (lds_bytes > lds) lds = lds_bytes;
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&rudp::copy_tile_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(rudp::copy_tile_kernel, dim3((uint32_t)blocks), dim3(rudp::kBlock), lds,
+                     (hipStream_t)stream, (const rudp::u32x4*)src, (rudp::u32x4*)dst, n16, tile16);
+  return (int)hipGetLastError();
+}
 
 // Copy with VPT (1, 2, 4, 8, 16) vectors per thread, loads before stores;
 // policy 1 = non-temporal, 0 = default.

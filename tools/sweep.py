@@ -29,6 +29,9 @@ lib.rudpx_copy.restype = ctypes.c_int
 lib.rudpx_copy_vpt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
                                ctypes.c_int, ctypes.c_void_p]
 lib.rudpx_copy_vpt.restype = ctypes.c_int
+lib.rudpx_copy_tile.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                ctypes.c_uint32, ctypes.c_void_p]
+lib.rudpx_copy_tile.restype = ctypes.c_int
 
 
 def event_ms(fn, reps=1):
@@ -165,6 +168,13 @@ def copy_sweep(reps):
                 lambda: None,
                 lambda vpt=vpt, pol=pol: lib.rudpx_copy_vpt(a.data_ptr(), b.data_ptr(), nbytes // 16,
                                                             vpt, pol, stream))
+    for kb in (4, 8, 16, 24, 32):
+        for per_cu in (0, 5, 3):
+            lds = (160 * 1024 // per_cu) & ~15 if per_cu else 0
+            variants[f"copy_tile{kb}k_percu{per_cu}"] = (
+                lambda: None,
+                lambda kb=kb, lds=lds: lib.rudpx_copy_tile(a.data_ptr(), b.data_ptr(), nbytes // 16,
+                                                           kb * 64, lds, stream))
     res = interleaved(variants, reps)
     return {k: {"ms": ms, "TBs": 2 * nbytes / ms / 1e9} for k, ms in res.items()}
 
