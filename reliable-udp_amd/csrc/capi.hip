@@ -88,6 +88,7 @@ EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t*
     a.invF = ((1ull << 32) + F - 1ull) / F;
     a.num_tiles = (uint32_t)((a.n + a.T - 1) / a.T);
     a.xcd_swizzle = tuning().encode_xcd_swizzle ? 1u : 0u;
+    a.ablate = (uint32_t)tuning().encode_ablate;
   }
   return a;
 }
@@ -227,8 +228,9 @@ void encode_tile_geometry(uint32_t L, uint32_t* T, uint32_t* glog) {
   while (tile * 2u <= t) tile *= 2u;
   uint32_t lg = 0;
   while ((256u >> lg) > tile) ++lg;
-  const int forced = tuning().encode_tile;  // experiments only (rudpx_tune)
-  if (forced >= 16 && forced <= 256 && (forced & (forced - 1)) == 0) {
+  int forced = tuning().encode_tile;  // experiments only (rudpx_tune)
+  while (forced > 4 && (uint32_t)forced * L > 65536u) forced >>= 1;  // LDS tile <= 64 KiB
+  if (forced >= 4 && forced <= 256 && (forced & (forced - 1)) == 0) {
     uint32_t g = 256u / (uint32_t)forced, l2 = 0;
     while ((1u << l2) < g) ++l2;
     lg = l2;

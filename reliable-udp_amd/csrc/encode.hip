@@ -5,9 +5,10 @@
 //   (:43-57) -> set_payload (:60-65) -> to_byte (:76-81)
 // plus the build-defined RFC 1071 checksum.
 //
-// Fast kernel (payload_len % 16 == 0): one workgroup per TILE of T packets,
-// T a multiple of 16 so that the tile's output range T*(L+H) starts and ends
-// 16-byte aligned even though the frame stride L+H is odd.
+// Fast kernel (payload_len % 16 == 0): one workgroup per TILE of T packets
+// (a power of two, 4..256).  The frame stride L+H is odd, so for T < 16 a
+// tile's output range starts and ends mid-chunk; the two shared chunks are
+// written bytewise by their owners.
 //   phase 1  G = 256/T lanes per packet stream the packet's payload in 16 B
 //            vectors (coalesced dwordx4, non-temporal), sum LE u16 halves in
 //            registers, and write the vectors into an LDS tile.  The per
@@ -49,8 +50,10 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   const uint32_t tid = threadIdx.x;
   const uint32_t L = a.L;
   const uint32_t T = a.T;
-  // a.glog is lanes-per-packet for 256-thread groups; wider groups give each packet more lanes
-  const uint32_t glog = a.glog + (BLOCK == 1024 ? 2u : BLOCK == 512 ? 1u : 0u);
+  // a.glog is lanes-per-packet for 256-thread groups; wider (narrower) groups
+  // give each packet more (fewer) lanes.  The launcher keeps T <= BLOCK.
+  constexpr int kLogBlock = BLOCK == 64 ? 6 : BLOCK == 128 ? 7 : BLOCK == 512 ? 9 : BLOCK == 1024 ? 10 : 8;
+  const uint32_t glog = (uint32_t)((int)a.glog + kLogBlock - 8);
   const uint32_t G = 1u << glog;
   uint32_t tile = blockIdx.x;
   if (a.xcd_swizzle) {
@@ -92,7 +95,7 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
       }
     }
     __syncthreads();
-    if (q < Tv) {
+    if (q < Tv && !(a.ablate & 1u)) {
       const u32x4* mine = dst + q * V;
       for (uint32_t v = g; v < V; v += G) sum += le16_sum(mine[v]);
     }
@@ -120,7 +123,8 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
   if (g == 0 && q < Tv) {
     const uint64_t p = p0 + q;
-    const uint32_t s = a.seq[p], k = a.ack[p], f = a.flags[p];
+    const bool tab = !(a.ablate & 4u);
+    const uint32_t s = tab ? a.seq[p] : 1u, k = tab ? a.ack[p] : 2u, f = tab ? a.flags[p] : 3u;
     const uint32_t c = packet_csum(sum, s, k, f);
     lds_hdr[q] = pack_header<H>(s, k, f, c);
     if (a.csum) a.csum[p] = (uint16_t)c;
@@ -128,11 +132,33 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   __syncthreads();
 
   // ---- phase 2: aligned 16 B output chunks --------------------------------
+  // The tile owns output bytes [p0*F, (p0+Tv)*F).  Chunks are aligned to the
+  // global address; when T*F is not a multiple of 16 (T < 16) the tile's first
+  // and last chunk are shared with its neighbours and only the owned bytes
+  // are written (bytewise, two partial chunks per tile).
   const uint32_t F = L + H;
   const uint32_t nbytes = Tv * F;
   unsigned char* out = a.frames + p0 * (uint64_t)F;
+  const uint32_t lead = (uint32_t)(-(uintptr_t)out) & 15u;  // bytes before the first aligned chunk
+  const uint32_t nfull = nbytes > lead ? (nbytes - lead) >> 4 : 0u;
   const uint32_t* pay_dw = reinterpret_cast<const uint32_t*>(lds_pay);
-  for (uint32_t x = tid * 16u; x < nbytes; x += BLOCK * 16u) {
+  // unit k < nfull: full chunk at tile offset lead + 16k; the two units after
+  // that are the partial head [0, lead) and tail [lead + 16*nfull, nbytes).
+  for (uint32_t k = tid; k < nfull + 2u; k += BLOCK) {
+    uint32_t x, lo_b, hi_b;  // tile offset of chunk byte 0; owned byte range [lo_b, hi_b)
+    if (k < nfull) {
+      x = lead + 16u * k; lo_b = 0; hi_b = 16;
+    } else if (k == nfull) {
+      x = 0; lo_b = 0; hi_b = lead < nbytes ? lead : nbytes;
+    } else {
+      x = lead + 16u * nfull; lo_b = 0; hi_b = nbytes > x ? nbytes - x : 0u;
+    }
+    if (hi_b <= lo_b) continue;
+    if (a.ablate & 2u) {  // diagnostic: aligned LDS read in place of the window assembly
+      const u32x4 v = reinterpret_cast<const u32x4*>(lds_pay + kLdsGuard)[k < nfull ? k : 0u];
+      if (hi_b == 16u) store16<NTS>(v, reinterpret_cast<u32x4*>(out + x));
+      continue;
+    }
     const uint32_t qq = (uint32_t)(((uint64_t)x * a.invF) >> 32);  // x / F
     const uint32_t r = x - qq * F;           // frame position of chunk byte 0
     const int kA0 = r < (uint32_t)H ? H - (int)r : 0;  // first payload byte of qq
@@ -156,13 +182,13 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
       }
     }
     const u32x4 v = make_u32x4(lo, hi);
-    if (x + 16u <= nbytes) {
+    if (hi_b == 16u) {
       store16<NTS>(v, reinterpret_cast<u32x4*>(out + x));
     } else {
       uint32_t d[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (uint32_t b = 0; b < 16; ++b)
-        if (x + b < nbytes) out[x + b] = (unsigned char)(d[b >> 2] >> (8 * (b & 3)));
+        if (b < hi_b) out[x + b] = (unsigned char)(d[b >> 2] >> (8 * (b & 3)));
     }
   }
 }
@@ -198,10 +224,12 @@ int launch_tile(const EncodeTileArgs& args, hipStream_t stream) {
   const uint64_t blocks = (args.n + args.T - 1) / args.T;
   size_t lds = args.hdr_bytes + kLdsGuard + (size_t)args.T * args.L + 32;
   int per_cu = tuning().encode_blocks_per_cu;
-  // Auto: at most 5 resident tiles per CU for big tiles (>= 16 KiB payload).
+  // Auto: at most 5 resident tiles per CU for big tiles (> 16 KiB payload).
   // Fewer tiles in flight keep the concurrent HBM footprint tighter: 1M x 1472 B
-  // 0.517 ms at 5 per CU vs 0.546 ms at the natural 6 (tools/sweep.py, r01).
-  if (per_cu < 0) per_cu = (size_t)args.T * args.L >= 16384 ? 5 : 0;
+  // 0.510 ms at 5 per CU vs 0.540 ms at the natural 6; 1M x 1024 B (16 KiB
+  // tiles) is the other way round, 0.363 ms natural vs 0.383 ms at 5
+  // (tools/sweep.py, r01).
+  if (per_cu < 0) per_cu = (size_t)args.T * args.L > 16384 ? 5 : 0;
   if (per_cu > 0) {  // reserve LDS to cap resident workgroups per CU
     const size_t want = ((size_t)(160 * 1024) / (size_t)per_cu) & ~size_t(15);
     if (want > lds) lds = want;
@@ -229,6 +257,8 @@ template <int H>
 int launch_tile_policy(const EncodeTileArgs& args, hipStream_t stream) {
   const int p1 = tuning().encode_p1;
   const int block = tuning().encode_block;
+  if (block == 64 && args.T <= 64) return launch_tile<H, true, true, 8, true, 64>(args, stream);
+  if (block == 128 && args.T <= 128) return launch_tile<H, true, true, 8, true, 128>(args, stream);
   if (block == 512) return launch_tile<H, true, true, 8, true, 512>(args, stream);
   if (block == 1024) return launch_tile<H, true, true, 8, true, 1024>(args, stream);
   if (tuning().encode_contig) {

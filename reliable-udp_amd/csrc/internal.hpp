@@ -14,12 +14,14 @@ struct EncodeTileArgs {
   uint16_t* csum;       // may be null
   uint64_t n;
   uint32_t L;           // payload bytes per packet
-  uint32_t T;           // packets per tile (multiple of 16, power of 2)
+  uint32_t T;           // packets per tile (power of 2, 4..256)
   uint32_t glog;        // log2(256 / T): lanes per packet
   uint32_t hdr_bytes;   // LDS bytes reserved for the tile's header words
   uint64_t invF;        // ceil(2^32 / (L + H)) for exact x / F, x < T*F
   uint32_t xcd_swizzle; // 1: map blocks b, b+8, ... to consecutive tiles (one XCD each)
   uint32_t num_tiles;
+  uint32_t ablate;      // diagnostics only (wrong output): 1 no LDS sum pass, 2 plain phase-2
+                        // LDS reads, 4 no header-table loads
 };
 
 struct DecodeArgs {
@@ -105,9 +107,10 @@ struct Tuning {
   int decode_glog = -1;   // verify kernel lanes-per-packet log2; -1 = automatic
   int encode_xcd_swizzle = 0;  // XCD-contiguous tile order (T1)
   int encode_contig = 1;  // phase 1 streams the tile contiguously, sums from LDS
-  int encode_block = 256;  // tile workgroup size (256, 512, 1024)
+  int encode_block = 256;  // tile workgroup size (64, 128 when T <= block; 256, 512, 1024)
   int decode_copy_tile = 1;  // copy-out decode through an LDS tile (0: register windows)
   int decode_verify_tile = 1;  // verify-only decode through an LDS tile (0: aligned-chunk kernel)
+  int encode_ablate = 0;  // EncodeTileArgs::ablate (sweeps only)
   int host_slots = 3;     // *_host pipeline: device staging slots (2..8)
   int host_stage_mb = 128;  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
 };

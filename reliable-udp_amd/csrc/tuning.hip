@@ -77,9 +77,62 @@ __global__ void __launch_bounds__(kBlock) copy_tile_kernel(const u32x4* __restri
   for (uint32_t v = threadIdx.x; v < m; v += kBlock) __builtin_nontemporal_store(t[v], dst + base + v);
 }
 
+// Diagnostic: persistent tiled copy with the next tile's loads in flight
+// while the current tile drains from LDS (tile16 <= 8 * 256).
+__global__ void __launch_bounds__(kBlock) copy_tile_pipe_kernel(const u32x4* __restrict__ src,
+                                                                u32x4* __restrict__ dst,
+                                                                uint64_t n16, uint32_t tile16) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  u32x4* t = reinterpret_cast<u32x4*>(lds);
+  const uint64_t ntiles = (n16 + tile16 - 1) / tile16;
+  uint64_t tile = blockIdx.x;
+  u32x4 r[8];
+  auto fetch = [&](uint64_t tl) {
+    const uint64_t base = tl * tile16;
+    const uint32_t m = (uint32_t)((n16 - base) < tile16 ? (n16 - base) : tile16);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t v = threadIdx.x + (uint32_t)u * kBlock;
+      if (v < m) r[u] = __builtin_nontemporal_load(src + base + v);
+    }
+  };
+  if (tile < ntiles) fetch(tile);
+  while (tile < ntiles) {
+    const uint64_t base = tile * tile16;
+    const uint32_t m = (uint32_t)((n16 - base) < tile16 ? (n16 - base) : tile16);
+#pragma unroll
+    for (int u = 0; u < 8; ++u) {
+      const uint32_t v = threadIdx.x + (uint32_t)u * kBlock;
+      if (v < m) t[v] = r[u];
+    }
+    __syncthreads();
+    const uint64_t next = tile + gridDim.x;
+    if (next < ntiles) fetch(next);
+    for (uint32_t v = threadIdx.x; v < m; v += kBlock) __builtin_nontemporal_store(t[v], dst + base + v);
+    __syncthreads();
+    tile = next;
+  }
+}
+
 }  // namespace rudp
 
 extern "C" {
+
+// Persistent pipelined tiled copy (diagnostic): `blocks` workgroups.
+int rudpx_copy_tile_pipe(const void* src, void* dst, uint64_t n16, uint32_t tile16, uint32_t blocks,
+                         uint32_t lds_bytes, void* stream) {
+  if (tile16 == 0 || tile16 > 8u * rudp::kBlock || blocks == 0) return -22;
+  size_t lds = (size_t)tile16 * 16;
+  if (lds_bytes > lds) lds = lds_bytes;
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&rudp::copy_tile_pipe_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL(rudp::copy_tile_pipe_kernel, dim3(blocks), dim3(rudp::kBlock), lds,
+                     (hipStream_t)stream, (const rudp::u32x4*)src, (rudp::u32x4*)dst, n16, tile16);
+  return (int)hipGetLastError();
+}
 
 // LDS-staged tile copy (diagnostic); lds_bytes >= tile16*16 sets occupancy.
 int rudpx_copy_tile(const void* src, void* dst, uint64_t n16, uint32_t tile16, uint32_t lds_bytes,
@@ -133,7 +186,7 @@ int rudpx_tune(int key, int value) {
             : key == 6 ? &t.encode_blocks_per_cu : key == 7 ? &t.encode_contig
             : key == 8 ? &t.host_slots : key == 9 ? &t.host_stage_mb
             : key == 10 ? &t.encode_block : key == 11 ? &t.decode_copy_tile
-            : key == 12 ? &t.decode_verify_tile : nullptr;
+            : key == 12 ? &t.decode_verify_tile : key == 13 ? &t.encode_ablate : nullptr;
   if (!slot) return -22;
   const int old = *slot;
   *slot = value;

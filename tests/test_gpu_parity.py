@@ -247,3 +247,30 @@ def test_decode_paths_agree(cuda, L):
             lib.rudpx_tune(12, 1)
             lib.rudpx_tune(11, 1)
     assert host(d.ok)[17] == 0
+
+
+@pytest.mark.parametrize("L", [16, 64, 1024, 1472, 4096])
+def test_encode_tile_sizes_agree(cuda, L):
+    """Every encode tile size gives the oracle's frames (T < 16: tiles share boundary chunks)."""
+    import ctypes
+    from rudp import _native
+    lib = _native.lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    for n in (1, 3, 4, 5, 9, 33, 1027):
+        seq, ack, flags, pay = synth.synth(0x99 + L, n, n, L, ascii=False)
+        for layout in (5, 7):
+            want_fr, want_cs = codec_np.encode(seq, ack, flags, pay, layout)
+            combos = [(256, t, pc) for t in (4, 8, 16, 32, 256) for pc in (-1, 0, 5)]
+            combos += [(64, t, 0) for t in (4, 8, 16, 32)] + [(128, t, 16) for t in (8, 64)]
+            for block, tile, per_cu in combos:
+                lib.rudpx_tune(10, block)
+                lib.rudpx_tune(2, tile)
+                lib.rudpx_tune(6, per_cu)
+                try:
+                    fr, cs = gpu_encode(cuda, seq, ack, flags, pay, layout)
+                finally:
+                    lib.rudpx_tune(10, 256)
+                    lib.rudpx_tune(2, 0)
+                    lib.rudpx_tune(6, -1)
+                assert np.array_equal(fr, want_fr), (L, n, layout, block, tile, per_cu)
+                assert np.array_equal(cs, want_cs), (L, n, layout, block, tile, per_cu)

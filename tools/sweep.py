@@ -32,6 +32,9 @@ lib.rudpx_copy_vpt.restype = ctypes.c_int
 lib.rudpx_copy_tile.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                 ctypes.c_uint32, ctypes.c_void_p]
 lib.rudpx_copy_tile.restype = ctypes.c_int
+lib.rudpx_copy_tile_pipe.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                     ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
+lib.rudpx_copy_tile_pipe.restype = ctypes.c_int
 
 
 def event_ms(fn, reps=1):
@@ -58,7 +61,7 @@ def interleaved(variants, reps):
 def encode_sweep(reps):
     out = {}
     dev = torch.device("cuda", 0)
-    for L, tiles in ((1472, (0,)), (1024, (0,)), (64, (0,))):
+    for L, tiles in ((1472, (0, 4, 8, 16)), (1024, (0, 4, 8, 16)), (64, (0, 16, 32, 64, 128))):
         n = 1 << 20
         nsets = 1 if L > 512 else 7
         sets = []
@@ -73,17 +76,22 @@ def encode_sweep(reps):
             batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
 
         variants = {}
-        for block in (256, 512, 1024):
-            for per_cu in ((-1, 0) if block == 256 else (0, 1, 2, 3)):
-                def setup(block=block, per_cu=per_cu):
-                    lib.rudpx_tune(10, block)
-                    lib.rudpx_tune(6, per_cu)
-                variants[f"L{L}_block{block}_percu{per_cu}"] = (setup, run)
+        for block in (64, 128, 256):
+            for tile in tiles:
+                if tile > block:
+                    continue
+                for per_cu in ((-1, 0, 5) if block == 256 else (0, 16, 24)):
+                    def setup(tile=tile, per_cu=per_cu, block=block):
+                        lib.rudpx_tune(10, block)
+                        lib.rudpx_tune(2, tile)
+                        lib.rudpx_tune(6, per_cu)
+                    variants[f"L{L}_b{block}_tile{tile}_percu{per_cu}"] = (setup, run)
         res = interleaved(variants, reps)
         alg = n * (2 * L + 12)
         # every variant must produce the default kernel's frames bit for bit
         tab0, pay0, _ = sets[0]
         lib.rudpx_tune(7, 0), lib.rudpx_tune(3, 8), lib.rudpx_tune(6, 0), lib.rudpx_tune(10, 256)
+        lib.rudpx_tune(2, 16 if L > 256 else 128)
         want, _ = batch.pack_batch(tab0, pay0, 7)  # the original per-packet phase 1
         for k, (setup, _) in variants.items():
             setup()
@@ -157,38 +165,75 @@ def copy_sweep(reps):
     a.fill_(7)
     stream = torch.cuda.current_stream().cuda_stream
     variants = {}
-    for blocks in (1024, 2048, 4096, 16384, 65536):
+    for blocks in (65536,):
         variants[f"copy_blocks{blocks}"] = (
             lambda: None,
             lambda blocks=blocks: lib.rudpx_copy(a.data_ptr(), b.data_ptr(), nbytes // 16, blocks, stream))
     variants["torch_copy_"] = (lambda: None, lambda: b.copy_(a))
-    for vpt in (1, 2, 4, 8, 16):
+    for vpt in (1, 4):
         for pol in (0, 1):
             variants[f"copy_vpt{vpt}_nt{pol}"] = (
                 lambda: None,
                 lambda vpt=vpt, pol=pol: lib.rudpx_copy_vpt(a.data_ptr(), b.data_ptr(), nbytes // 16,
                                                             vpt, pol, stream))
-    for kb in (4, 8, 16, 24, 32):
-        for per_cu in (0, 5, 3):
+    for kb in (4, 8, 12, 24):
+        for per_cu in (0, 5):
             lds = (160 * 1024 // per_cu) & ~15 if per_cu else 0
             variants[f"copy_tile{kb}k_percu{per_cu}"] = (
                 lambda: None,
                 lambda kb=kb, lds=lds: lib.rudpx_copy_tile(a.data_ptr(), b.data_ptr(), nbytes // 16,
                                                            kb * 64, lds, stream))
+    for kb in (8, 12, 24):
+        for per_cu in (2, 4, 6, 8):
+            variants[f"copy_pipe{kb}k_blocks{per_cu}x256"] = (
+                lambda: None,
+                lambda kb=kb, per_cu=per_cu: lib.rudpx_copy_tile_pipe(
+                    a.data_ptr(), b.data_ptr(), nbytes // 16, kb * 64, per_cu * 256, 0, stream))
     res = interleaved(variants, reps)
     return {k: {"ms": ms, "TBs": 2 * nbytes / ms / 1e9} for k, ms in res.items()}
+
+
+def ablate_sweep(reps):
+    """Encode with stages switched off (inexact on purpose) beside LDS-tiled copies."""
+    dev = torch.device("cuda", 0)
+    n, L = 1 << 20, 1472
+    tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
+    fr = torch.empty((n, L + 7), dtype=torch.uint8, device=dev)
+    stream = torch.cuda.current_stream().cuda_stream
+    variants = {}
+    for tile in (8, 16):
+        for abl in range(8):
+            def setup(tile=tile, abl=abl):
+                lib.rudpx_tune(2, tile)
+                lib.rudpx_tune(13, abl)
+            variants[f"tile{tile}_ablate{abl}"] = (
+                setup, lambda: batch.pack_batch(tab, pay, 7, out=fr, want_csum=False))
+    a = pay.view(-1)
+    b = fr.view(-1)[: a.numel()]
+    for kb in (12, 24):
+        t16 = (kb * 1024 * 23 // 24) // 16 if kb == 24 else (11776 // 16)
+        variants[f"copy_tile{kb}k"] = (lambda: None, lambda t16=t16: lib.rudpx_copy_tile(
+            a.data_ptr(), b.data_ptr(), a.numel() // 16, t16, 0, stream))
+    res = interleaved(variants, reps)
+    lib.rudpx_tune(2, 0)
+    lib.rudpx_tune(13, 0)
+    alg = n * (2 * L + 12)
+    return {k: {"ms": ms, "TBs": (alg if "tile" in k and "copy" not in k else 2 * a.numel()) / ms / 1e9}
+            for k, ms in res.items()}
 
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
-    ap.add_argument("--only", choices=["encode", "decode", "copy"])
+    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate"])
     args = ap.parse_args()
     result = {}
     if args.only in (None, "copy"):
         result["copy"] = copy_sweep(args.reps)
     if args.only in (None, "decode"):
         result["decode"] = decode_sweep(args.reps)
+    if args.only == "ablate":
+        result["ablate"] = ablate_sweep(args.reps)
     if args.only in (None, "encode"):
         result["encode"] = encode_sweep(args.reps)
     print(json.dumps(result, indent=1))
