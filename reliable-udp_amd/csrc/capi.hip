@@ -351,6 +351,9 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, ui
     if (path == DecodePath::kVerify && forced >= 1 && forced <= 4 &&
         (1u << forced) <= (frame_len - (uint32_t)layout) / 16u)
       a.glog = (uint32_t)forced;
+    if ((path == DecodePath::kVerifyTile || path == DecodePath::kCopyTile) && forced >= 0 &&
+        forced <= 4 && (size_t)(256u >> forced) * frame_len + 48 <= 65536)
+      a.glog = (uint32_t)forced;
   }
   rc = launch_decode(a, layout, path, (hipStream_t)hip_stream);
   if (rc) return hip_fail((hipError_t)rc, "decode launch");

@@ -199,13 +199,14 @@ __global__ void __launch_bounds__(kBlock) decode_verify_kernel(DecodeArgs a) {
   }
 }
 
-// Copy-out decode through LDS (payload_out != null): the mirror of the encode
-// tile kernel.  A workgroup owns T = 256/G frames; T is a multiple of 16, so
-// the tile's frames start 16-byte aligned.  Phase 1 streams them into LDS like
-// a copy (lane t: vectors t, t+256, ...).  Phase 2: G lanes per frame read the
-// payload back as byte-shifted LDS windows (5 ds_read_b32 + v_alignbyte), sum
-// the LE u16 halves and store the windows to payload_out 16-byte aligned; the
-// group leader parses the header out of LDS.
+// Decode through LDS, verify-only or with payload copy-out: the mirror of the
+// encode tile kernel.  A workgroup owns T = 256/G frames; T is a multiple of
+// 16, so the tile's frames start 16-byte aligned.  Phase 1 streams them into
+// LDS like a copy (lane t: vectors t, t+256, ...).  Phase 2: G lanes per frame
+// read the payload back as byte-shifted LDS windows (5 ds_read_b32 +
+// v_alignbyte) and sum the LE u16 halves; the group leader parses the header
+// out of LDS.  Copy-out streams the same windows to payload_out as one
+// contiguous run per tile.
 template <int H, bool COPY>
 __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -242,14 +243,25 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
   const uint32_t* dw = reinterpret_cast<const uint32_t*>(lds);
   uint32_t sum = 0;
   const uint64_t p = p0 + q;
+  const uint32_t V = L >> 4;
   if (q < Tv) {
-    const uint32_t V = L >> 4;
     const uint32_t pay = q * F + H;  // LDS byte offset of the payload
-    for (uint32_t v = g; v < V; v += G) {
-      const u32x4 w = window16_dw(dw, pay + 16u * v);
-      sum += le16_sum(w);
-      if (COPY)
-        __builtin_nontemporal_store(w, reinterpret_cast<u32x4*>(a.payload_out + p * (uint64_t)L + 16ull * v));
+    for (uint32_t v = g; v < V; v += G) sum += le16_sum(window16_dw(dw, pay + 16u * v));
+  }
+  if (COPY) {
+    // The tile's payload_out range is contiguous (Tv*L bytes, 16-B aligned):
+    // store it as one stream, lane t taking vectors t, t+256, ... so every
+    // wave-instruction writes 1 KiB contiguous.  Vector j is vector j % V of
+    // packet j / V, tracked incrementally (no per-vector division).
+    const uint32_t nv = Tv * V;
+    const uint32_t dq = kBlock / V, dv = kBlock % V;
+    uint32_t qj = tid / V, vj = tid - qj * V;
+    u32x4* dst = reinterpret_cast<u32x4*>(a.payload_out + p0 * (uint64_t)L);
+    for (uint32_t j = tid; j < nv; j += kBlock) {
+      __builtin_nontemporal_store(window16_dw(dw, qj * F + H + 16u * vj), dst + j);
+      qj += dq;
+      vj += dv;
+      if (vj >= V) { vj -= V; ++qj; }
     }
   }
   for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);

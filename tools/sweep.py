@@ -140,10 +140,16 @@ def decode_sweep(reps):
                                           seq.data_ptr(), ok.data_ptr(), ok.data_ptr(), None,
                                           pay_out.data_ptr(), 7, 0,
                                           torch.cuda.current_stream().cuda_stream))
-        variants = {f"L{L}_copyout_tile": (lambda: lib.rudpx_tune(11, 1), copy),
-                    f"L{L}_copyout_regs": (lambda: lib.rudpx_tune(11, 0), copy)}
-        variants[f"L{L}_verify_chunks"] = (lambda: lib.rudpx_tune(12, 0), verify)
-        variants[f"L{L}_verify_tile"] = (lambda: lib.rudpx_tune(12, 1), verify)
+        variants = {f"L{L}_copyout_tile": (lambda: (lib.rudpx_tune(4, -1), lib.rudpx_tune(11, 1)), copy),
+                    f"L{L}_copyout_regs": (lambda: (lib.rudpx_tune(4, -1), lib.rudpx_tune(11, 0)), copy)}
+        variants[f"L{L}_verify_chunks"] = (lambda: (lib.rudpx_tune(4, -1), lib.rudpx_tune(12, 0)), verify)
+        variants[f"L{L}_verify_tile"] = (lambda: (lib.rudpx_tune(4, -1), lib.rudpx_tune(12, 1)), verify)
+        if L <= 256:
+            for lg in (0, 1, 2):
+                variants[f"L{L}_verify_tile_glog{lg}"] = (
+                    lambda lg=lg: (lib.rudpx_tune(12, 1), lib.rudpx_tune(4, lg)), verify)
+                variants[f"L{L}_copyout_tile_glog{lg}"] = (
+                    lambda lg=lg: (lib.rudpx_tune(11, 1), lib.rudpx_tune(4, lg)), copy)
         res = interleaved(variants, reps)
         lib.rudpx_tune(4, -1)
         lib.rudpx_tune(11, 1)
