@@ -64,7 +64,9 @@ extern "C" {
  * bytes and len/payload_off are NULL.  Variable-length batches
  * (rudp_encode_varlen): len[i] payload bytes of packet i (<= 65535) start at
  * payload[payload_off[i]], or, with payload_off NULL, the payloads are packed
- * back to back in packet order; payload_len is ignored.
+ * back to back in packet order; payload_len is then a hint of the typical
+ * payload length (0 = unknown/tiny) that picks lanes per packet, never the
+ * result.
  *   seq   -> custom_header["seq_num"]  (utils/packet.py:4)
  *   ack   -> custom_header["ack_num"]  (utils/packet.py:5)
  *   flags -> header byte 4 verbatim: syn/ack/fin/offset (utils/packet.py:6-9)
@@ -103,7 +105,8 @@ int rudp_encode(const rudp_batch* in, uint8_t* d_frames, uint16_t* d_csum_or_nul
  * Fixed-length frames: d_frame_off_or_null = NULL, frames at stride
  * frame_len.  Variable-length frames: d_frame_off_or_null = n+1 offsets
  * (frame i = d_frames[off[i], off[i+1]), as rudp_encode_varlen writes them),
- * frame_len is ignored and the payload is zero-copy only
+ * frame_len is a hint of the typical frame length (0 = unknown/tiny; it
+ * picks lanes per frame, never the result) and the payload is zero-copy only
  * (d_payload_out_or_null must be NULL).  d_csum_in_or_null: rudp5 sideband checksums to verify
  * (NULL: d_ok = RUDP_OK_UNVERIFIED).  d_csum_out_or_null: the recomputed
  * checksum per packet.  d_payload_out_or_null: n*(frame_len-layout) bytes,

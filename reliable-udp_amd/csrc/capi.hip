@@ -13,7 +13,7 @@
 #include "internal.hpp"
 
 namespace rudp {
-int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint64_t n,
+int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t len_hint, uint64_t n,
                   const uint16_t* d_csum_in, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
                   uint8_t* d_ok, uint16_t* d_csum_out, uint8_t* d_payload_out, int layout,
                   int device, void* hip_stream);
@@ -249,7 +249,7 @@ uint32_t decode_group_log2(uint32_t L) {
   return lg;
 }
 
-int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint64_t n,
+int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t len_hint, uint64_t n,
                   const uint16_t* d_csum_in, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
                   uint8_t* d_ok, uint16_t* d_csum_out, uint8_t* d_payload_out, int layout,
                   int device, void* hip_stream) {
@@ -273,6 +273,13 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint64_t
   a.ok = d_ok;
   a.csum_out = d_csum_out;
   a.n = n;
+  // Lanes per frame from the caller's typical frame length (0 = unknown:
+  // tiny frames).  Two or more 16-byte chunks per lane, G in [2, 16].
+  const uint32_t chunks = len_hint / 16u + 1u;
+  uint32_t lg = 1;
+  while (lg < 4 && (4u << lg) <= chunks) ++lg;
+  if (tuning().varlen_glog >= 1 && tuning().varlen_glog <= 6) lg = (uint32_t)tuning().varlen_glog;
+  a.glog = tuning().varlen_vec ? lg : kNoVec;
   rc = launch_decode_varlen(a, layout, (hipStream_t)hip_stream);
   if (rc) return hip_fail((hipError_t)rc, "varlen decode launch");
   return 0;
@@ -314,7 +321,7 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, ui
                 uint8_t* d_flags, uint8_t* d_ok, uint16_t* d_csum_out_or_null,
                 uint8_t* d_payload_out_or_null, int layout, int device, void* hip_stream) {
   if (d_frame_off_or_null) {
-    return decode_varlen(d_frames, d_frame_off_or_null, n, d_csum_in_or_null, d_seq, d_ack, d_flags,
+    return decode_varlen(d_frames, d_frame_off_or_null, frame_len, n, d_csum_in_or_null, d_seq, d_ack, d_flags,
                          d_ok, d_csum_out_or_null, d_payload_out_or_null, layout, device, hip_stream);
   }
   int rc = validate_decode(d_frames, nullptr, frame_len, n, d_seq, d_ack, d_flags, d_ok, layout);
@@ -416,6 +423,13 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
   a.frame_off = d_frame_off;
   a.csum = d_csum_or_null;
   a.n = in->n;
+  // Lanes per packet from payload_len, the caller's typical payload length
+  // (a hint for varlen batches; 0 = unknown/tiny): two+ chunks per lane.
+  const uint32_t chunks = in->payload_len / 16u + 1u;
+  uint32_t lg = 0;
+  while (lg < 4 && (4u << lg) <= chunks) ++lg;
+  if (tuning().varlen_glog >= 0 && tuning().varlen_glog <= 6) lg = (uint32_t)tuning().varlen_glog;
+  a.glog = tuning().varlen_vec ? lg : kNoVec;
   rc = launch_encode_varlen(a, layout, s);
   if (rc) return hip_fail((hipError_t)rc, "varlen encode launch");
   return 0;

@@ -105,4 +105,27 @@ __device__ __forceinline__ u32x4 funnel32(u32x4 a, u32x4 b, uint32_t sh) {
   return r;
 }
 
+// 16 bytes at frames[off], off 16-byte aligned; bytes at or past `total`
+// read as zero (only the last packets of a batch take the byte path).
+__device__ __forceinline__ u32x4 load16_guarded(const unsigned char* frames, uint64_t off,
+                                                uint64_t total) {
+  if (off + 16 <= total)
+    return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(frames + off));
+  uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
+#pragma unroll
+  for (uint32_t b = 0; b < 16; ++b) {
+    const uint32_t v = (off + b < total) ? (uint32_t)frames[off + b] << (8 * (b & 3)) : 0u;
+    if (b < 4) d0 |= v;
+    else if (b < 8) d1 |= v;
+    else if (b < 12) d2 |= v;
+    else d3 |= v;
+  }
+  u32x4 r;
+  r.x = d0;
+  r.y = d1;
+  r.z = d2;
+  r.w = d3;
+  return r;
+}
+
 }  // namespace rudp

@@ -69,7 +69,9 @@ struct VarlenArgs {
   uint8_t* ok;
   uint16_t* csum_out;
   uint64_t n;
+  uint32_t glog;                  // log2 lanes per packet (vector kernels); kNoVec = byte kernels
 };
+constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
 struct Utf8Args {
   const unsigned char* frames;
@@ -110,6 +112,8 @@ struct Tuning {
   int encode_block = 256;  // tile workgroup size (64, 128 when T <= block; 256, 512, 1024)
   int decode_copy_tile = 1;  // copy-out decode through an LDS tile (0: register windows)
   int decode_verify_tile = 1;  // verify-only decode through an LDS tile (0: aligned-chunk kernel)
+  int varlen_vec = 1;     // varlen encode/decode: vector kernels (0: byte kernels)
+  int varlen_glog = -1;   // varlen lanes-per-packet log2 (0..6); -1 = from the length hint
   int encode_ablate = 0;  // EncodeTileArgs::ablate (sweeps only)
   int host_slots = 3;     // *_host pipeline: device staging slots (2..8)
   int host_stage_mb = 128;  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)

@@ -186,7 +186,7 @@ int rudpx_tune(int key, int value) {
             : key == 6 ? &t.encode_blocks_per_cu : key == 7 ? &t.encode_contig
             : key == 8 ? &t.host_slots : key == 9 ? &t.host_stage_mb
             : key == 10 ? &t.encode_block : key == 11 ? &t.decode_copy_tile
-            : key == 12 ? &t.decode_verify_tile : key == 13 ? &t.encode_ablate : nullptr;
+            : key == 12 ? &t.decode_verify_tile : key == 13 ? &t.encode_ablate : key == 14 ? &t.varlen_vec : key == 15 ? &t.varlen_glog : nullptr;
   if (!slot) return -22;
   const int old = *slot;
   *slot = value;

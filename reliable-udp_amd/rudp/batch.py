@@ -335,18 +335,26 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
         if t.shape[0] != n:
             raise ValueError(f"{name} has {t.shape[0]} entries for {n} packets")
     lens64 = lengths.to(torch.int64)
-    if n and (int(lens64.min().item()) < 0 or int(lens64.max().item()) > 65535):
+    if payload_off is not None:
+        _int_tensor(payload_off, "payload_off", dev, n, dtypes=(torch.int64,))
+    # one device->host read for every bound
+    lmin = lmax = lsum = omin = oend = 0
+    if n:
+        stats = [lens64.min(), lens64.max(), lens64.sum()]
+        if payload_off is not None:
+            stats += [payload_off.min(), (payload_off + lens64).max()]
+        vals = torch.stack(stats).tolist()
+        lmin, lmax, lsum = vals[:3]
+        if payload_off is not None:
+            omin, oend = vals[3:]
+    if lmin < 0 or lmax > 65535:
         raise ValueError("lengths must lie in [0, 65535]")
     if payload_off is None:
-        if int(lens64.sum().item()) != payload.numel():
+        if lsum != payload.numel():
             raise ValueError("packed payloads: sum(lengths) must equal payload.numel()")
-        total = payload.numel() + n * H
-    else:
-        _int_tensor(payload_off, "payload_off", dev, n, dtypes=(torch.int64,))
-        if n and (int(payload_off.min().item()) < 0
-                  or int((payload_off + lens64).max().item()) > payload.numel()):
-            raise ValueError("payload_off + lengths must stay inside payload")
-        total = int(lens64.sum().item()) + n * H
+    elif omin < 0 or oend > payload.numel():
+        raise ValueError("payload_off + lengths must stay inside payload")
+    total = lsum + n * H
     if want_csum is None:
         want_csum = H == 5
     frames = torch.empty((total,), dtype=torch.uint8, device=dev)
@@ -355,7 +363,8 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
     if n == 0:
         frame_off.zero_()
         return VarlenFrames(frames, frame_off, csum)
-    b = _native.RudpBatch(n=n, payload_len=0, reserved=0, seq=tab.seq.data_ptr(),
+    # payload_len carries the mean payload length: a hint that picks lanes per packet
+    b = _native.RudpBatch(n=n, payload_len=min(lsum // n, 65535), reserved=0, seq=tab.seq.data_ptr(),
                           ack=tab.ack.data_ptr(), flags=tab.flags.data_ptr(),
                           payload=payload.data_ptr() if payload.numel() else 16,  # never read: all lengths 0
                           len=lengths.data_ptr(),
@@ -366,12 +375,17 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
     return VarlenFrames(frames, frame_off, csum)
 
 
-def _check_offsets(frames, frame_off):
-    if frame_off.shape[0] > 1:
-        d = frame_off[1:] - frame_off[:-1]
-        if int(frame_off[0].item()) < 0 or bool((d < 0).any()) \
-                or int(frame_off[-1].item()) > frames.numel():
-            raise ValueError("frame_off must be non-decreasing offsets inside frames")
+def _check_offsets(frames, frame_off) -> int:
+    """Validate offsets (one device->host read); returns the mean frame length."""
+    import torch
+    n = frame_off.shape[0] - 1
+    if n < 1:
+        return 0
+    bad = (frame_off[1:] < frame_off[:-1]).any().to(torch.int64)
+    first, last, nbad = torch.stack([frame_off[0], frame_off[-1], bad]).tolist()
+    if first < 0 or nbad or last > frames.numel():
+        raise ValueError("frame_off must be non-decreasing offsets inside frames")
+    return min((last - first) // n, 0xFFFFFFFF)
 
 
 def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *, csum=None,
@@ -391,7 +405,7 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
     n = frame_off.shape[0] - 1
     if n < 0:
         raise ValueError("frame_off needs N + 1 entries")
-    _check_offsets(frames, frame_off)
+    mean_len = _check_offsets(frames, frame_off)
     if csum is not None:
         _dev_check(csum, "csum", torch.uint16, 1, dev)
         if csum.shape[0] != n:
@@ -403,7 +417,7 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
     cs = torch.empty((n,), dtype=torch.uint16, device=dev)
     if n:
         _native.check(_native.lib().rudp_decode(
-            frames.data_ptr() if frames.numel() else 16, frame_off.data_ptr(), 0, n,
+            frames.data_ptr() if frames.numel() else 16, frame_off.data_ptr(), mean_len, n,
             csum.data_ptr() if csum is not None else None, seq.data_ptr(), ack.data_ptr(),
             flags.data_ptr(), ok.data_ptr(), cs.data_ptr(), None, H, dev.index or 0,
             _stream_ptr(stream, dev)))

@@ -228,3 +228,116 @@ def test_socket_ring_to_gpu_decode(cuda):
     assert all(o == 1 for _, o in seen)
     rx.close()
     tx.close()
+
+
+def _varlen_frames(rng, n, lo, hi, layout):
+    """Frames of payload length in [lo, hi], some short / corrupted, after a ragged prefix."""
+    lens = rng.integers(lo, hi + 1, n)
+    pays = [rng.integers(0, 256, int(k), dtype=np.uint8).tobytes() for k in lens]
+    seq, ack, flags, _ = synth.synth(int(rng.integers(1 << 30)), 0, n, 0)
+    frames, off, cs = codec_np.encode_varlen(seq, ack, flags, pays, layout)
+    parts = [frames[off[i]:off[i + 1]].tobytes() for i in range(n)]
+    for i in rng.choice(n, n // 20, replace=False):   # short frames, header cut
+        parts[i] = parts[i][: int(rng.integers(0, layout))]
+    for i in rng.choice(n, n // 20, replace=False):   # one flipped byte
+        if parts[i]:
+            b = bytearray(parts[i])
+            b[int(rng.integers(len(b)))] ^= 1 << int(rng.integers(8))
+            parts[i] = bytes(b)
+    prefix = int(rng.integers(0, 16))
+    buf = bytes(prefix) + b"".join(parts)
+    off = np.cumsum([prefix] + [len(p) for p in parts]).astype(np.int64)
+    return np.frombuffer(buf, np.uint8), off, cs
+
+
+@pytest.mark.parametrize("lo,hi", [(0, 9), (0, 1500), (1400, 1472), (3000, 9000)])
+@pytest.mark.parametrize("layout", [5, 7])
+def test_varlen_decode_kernels_vs_oracle(cuda, lo, hi, layout):
+    """Vector varlen decode (any lanes-per-frame hint) == byte kernel == oracle."""
+    import ctypes
+    import torch
+    from rudp import _native
+    lib = _native.lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    rng = np.random.default_rng(lo * 7 + hi + layout)
+    n = 1500 if hi < 2000 else 300
+    buf, off, cs = _varlen_frames(rng, n, lo, hi, layout)
+    csum_in = cs if layout == 5 else None
+    want = codec_np.decode_varlen(buf, off, layout, csum_in)
+    d_buf, d_off = dev(buf, cuda), dev(off, cuda)
+    d_cs = dev(cs, cuda) if layout == 5 else None
+    outs = [torch.empty(n, dtype=dt, device=cuda)
+            for dt in (torch.uint16, torch.uint16, torch.uint8, torch.uint8, torch.uint16)]
+    runs = [("python", None, 1)] + [("abi", h, v) for v in (1, 0) for h in (0, 8, 1472, 65535)]
+    for kind, hint, vec in runs:
+        lib.rudpx_tune(14, vec)
+        try:
+            if kind == "python":
+                d = batch.unpack_batch_varlen(d_buf, d_off, layout, csum=d_cs)
+                got = [host(x) for x in (d.seq, d.ack, d.flags, d.ok, d.csum)]
+            else:
+                for o in outs:
+                    o.fill_(0xAB)
+                _native.check(lib.rudp_decode(
+                    d_buf.data_ptr(), d_off.data_ptr(), hint, n,
+                    d_cs.data_ptr() if d_cs is not None else None,
+                    *[o.data_ptr() for o in outs], None, layout, 0,
+                    torch.cuda.current_stream().cuda_stream))
+                got = [host(o) for o in outs]
+        finally:
+            lib.rudpx_tune(14, 1)
+        for name, g, w in zip(("seq", "ack", "flags", "ok", "csum"), got, want):
+            assert np.array_equal(g, w), (lo, hi, layout, kind, hint, vec, name)
+    assert (want[3] == 2).any() and (want[3] == 0).any() and (want[3] == 1).any()
+
+
+@pytest.mark.parametrize("lo,hi", [(0, 3), (0, 100), (1400, 1472), (5000, 20000)])
+@pytest.mark.parametrize("layout", [5, 7])
+def test_varlen_encode_kernels_vs_oracle(cuda, lo, hi, layout):
+    """Vector varlen encode (any lanes-per-packet hint, packed or gathered
+    payloads) == byte kernel == oracle, frames and offsets bit for bit."""
+    import ctypes
+    import torch
+    from rudp import _native
+    lib = _native.lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    rng = np.random.default_rng(lo + 3 * hi + layout)
+    n = 2000 if hi < 2000 else 120
+    lens = rng.integers(lo, hi + 1, n).astype(np.int32)
+    seq, ack, flags, _ = synth.synth(int(rng.integers(1 << 30)), 0, n, 0)
+    packed = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    pays, _ = split_by_lengths(packed, lens)
+    want_fr, want_off, want_cs = codec_np.encode_varlen(seq, ack, flags, pays, layout)
+    # the same payloads scattered through a bigger buffer at arbitrary offsets
+    gaps = rng.integers(0, 40, n)
+    starts = (np.cumsum(gaps + lens) - lens).astype(np.int64)  # disjoint, ragged alignment
+    big = rng.integers(0, 256, int(starts[-1] + lens[-1]) + 64, dtype=np.uint8)
+    for i in range(n):
+        big[starts[i]:starts[i] + lens[i]] = np.frombuffer(pays[i], np.uint8)
+    tab = (dev(seq, cuda), dev(ack, cuda), dev(flags, cuda))
+    d_lens = dev(lens, cuda)
+    for vec in (1, 0):
+        lib.rudpx_tune(14, vec)
+        try:
+            for payload, off in ((dev(packed, cuda), None), (dev(big, cuda), dev(starts, cuda))):
+                res = batch.pack_batch_varlen(tab, payload, d_lens, layout, payload_off=off,
+                                              want_csum=True)
+                assert np.array_equal(host(res.frames), want_fr), (lo, hi, layout, vec, off is None)
+                assert np.array_equal(host(res.frame_off), want_off)
+                assert np.array_equal(host(res.csum), want_cs)
+            # any hint gives the same frames (raw ABI)
+            frames = torch.empty(len(want_fr), dtype=torch.uint8, device=cuda)
+            frame_off = torch.empty(n + 1, dtype=torch.int64, device=cuda)
+            p = dev(packed, cuda)
+            for hint in (0, 7, 1472, 65535):
+                frames.fill_(0xCD)
+                b = _native.RudpBatch(n=n, payload_len=hint, reserved=0, seq=tab[0].data_ptr(),
+                                      ack=tab[1].data_ptr(), flags=tab[2].data_ptr(),
+                                      payload=p.data_ptr() if p.numel() else 16,
+                                      len=d_lens.data_ptr(), payload_off=None)
+                _native.check(lib.rudp_encode_varlen(ctypes.byref(b), frames.data_ptr(),
+                                                     frame_off.data_ptr(), None, layout, 0,
+                                                     torch.cuda.current_stream().cuda_stream))
+                assert np.array_equal(host(frames), want_fr), (lo, hi, layout, vec, hint)
+        finally:
+            lib.rudpx_tune(14, 1)

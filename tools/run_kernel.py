@@ -23,7 +23,8 @@ from rudp import batch  # noqa: E402
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--op", choices=["encode", "decode", "decode_copy", "roundtrip"], default="encode")
+    ap.add_argument("--op", choices=["encode", "decode", "decode_copy", "roundtrip", "encode_varlen",
+                                     "decode_varlen"], default="encode")
     ap.add_argument("--L", type=int, default=1472)
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--layout", default="rudp7")
@@ -52,7 +53,21 @@ def main():
                                       pay.data_ptr(), H, 0, torch.cuda.current_stream().cuda_stream))
     del ctypes
 
+    vsets = []
+    if args.op.endswith("varlen"):
+        for tab, pay, fr in sets:
+            lens = torch.full((args.n,), args.L, dtype=torch.int32, device=dev)
+            res = batch.pack_batch_varlen(tab, pay.view(-1), lens, args.layout)
+            vsets.append((tab, pay.view(-1), lens, res.frames, res.frame_off))
+
     def step(i):
+        if vsets:
+            tab, flat, lens, vfr, voff = vsets[i % nsets]
+            if args.op == "encode_varlen":
+                batch.pack_batch_varlen(tab, flat, lens, args.layout)
+            else:
+                batch.unpack_batch_varlen(vfr, voff, args.layout)
+            return
         tab, pay, fr = sets[i % nsets]
         if args.op in ("encode", "roundtrip"):
             batch.pack_batch(tab, pay, args.layout, out=fr, want_csum=False)

@@ -228,16 +228,72 @@ def ablate_sweep(reps):
             for k, ms in res.items()}
 
 
+def varlen_sweep(reps):
+    """Varlen decode (raw ABI, preallocated outputs): vector kernel vs byte kernel."""
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    out = {}
+    for L in (1, 64, 1024, 1472):
+        n = 1 << 20
+        tab, pay = batch.synth_batch(n, L, 0x5EED0007, device=dev)
+        lens = torch.full((n,), L, dtype=torch.int32, device=dev)
+        res = batch.pack_batch_varlen(tab, pay.view(-1), lens, 7)
+        frames, off = res.frames, res.frame_off
+        o16 = [torch.empty(n, dtype=torch.uint16, device=dev) for _ in range(3)]
+        o8 = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(2)]
+
+        def run(hint):
+            _native.check(lib.rudp_decode(frames.data_ptr(), off.data_ptr(), hint, n, None,
+                                          o16[0].data_ptr(), o16[1].data_ptr(), o8[0].data_ptr(),
+                                          o8[1].data_ptr(), o16[2].data_ptr(), None, 7, 0, stream))
+        fr2 = torch.empty_like(frames)
+        off2 = torch.empty_like(off)
+        flat = pay.view(-1)
+
+        def enc(hint):
+            b = _native.RudpBatch(n=n, payload_len=hint, reserved=0, seq=tab.seq.data_ptr(),
+                                  ack=tab.ack.data_ptr(), flags=tab.flags.data_ptr(),
+                                  payload=flat.data_ptr(), len=lens.data_ptr(), payload_off=None)
+            _native.check(lib.rudp_encode_varlen(ctypes.byref(b), fr2.data_ptr(), off2.data_ptr(),
+                                                 None, 7, 0, stream))
+        variants = {f"L{L}_bytes": (lambda: (lib.rudpx_tune(15, -1), lib.rudpx_tune(14, 0)), lambda: run(L + 7)),
+                    f"L{L}_enc_bytes": (lambda: (lib.rudpx_tune(15, -1), lib.rudpx_tune(14, 0)), lambda: enc(L))}
+        for lg in (range(2, 7) if L >= 1024 else ()):
+            variants[f"L{L}_vec_glog{lg}"] = (lambda lg=lg: (lib.rudpx_tune(14, 1), lib.rudpx_tune(15, lg)),
+                                              lambda: run(L + 7))
+            variants[f"L{L}_enc_vec_glog{lg}"] = (lambda lg=lg: (lib.rudpx_tune(14, 1), lib.rudpx_tune(15, lg)),
+                                                  lambda: enc(L))
+        for hint in sorted({0, L + 7, 64, 1479}):
+            variants[f"L{L}_vec_hint{hint}"] = (lambda: (lib.rudpx_tune(15, -1), lib.rudpx_tune(14, 1)),
+                                                lambda hint=hint: run(hint))
+            variants[f"L{L}_enc_vec_hint{hint}"] = (lambda: (lib.rudpx_tune(15, -1), lib.rudpx_tune(14, 1)),
+                                                    lambda hint=hint: enc(hint))
+        res_t = interleaved(variants, reps)
+        lib.rudpx_tune(14, 1)
+        lib.rudpx_tune(15, -1)
+        for k, ms in res_t.items():
+            # decode: frames + offsets read, seq/ack/flags/ok/csum written;
+            # encode: payload + len + header table read, frames + offsets written
+            alg = n * (2 * L + 7 + 9 + 8) if "_enc_" in k else n * (L + 7 + 8 + 8)
+            out[k] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0}
+        del fr2, off2, flat
+        del frames, off, res, tab, pay
+        torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
-    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate"])
+    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen"])
     args = ap.parse_args()
     result = {}
     if args.only in (None, "copy"):
         result["copy"] = copy_sweep(args.reps)
     if args.only in (None, "decode"):
         result["decode"] = decode_sweep(args.reps)
+    if args.only == "varlen":
+        result["varlen"] = varlen_sweep(args.reps)
     if args.only == "ablate":
         result["ablate"] = ablate_sweep(args.reps)
     if args.only in (None, "encode"):
