@@ -198,19 +198,25 @@ def legs(torch, batch, device, steps):
     # socket boundary: 1M one-character frames sendmmsg'd over loopback, recvmmsg'd into a
     # pinned ring and decoded on the GPU per received batch (rudp.netio)
     out["socket_e2e_1M_x_1char"] = socket_leg(torch, batch, device)
-    # device-to-device streaming-copy ceiling (dwordx4 nt copy kernel, rudpx_copy),
-    # same byte count as one encode's payload
+    # device-to-device streaming-copy ceiling, same byte count as one encode's payload:
+    # the fastest copy in tools/sweep.py (one dwordx4 per thread, nt loads and stores,
+    # rudpx_copy_vpt) and, for reference, the grid-stride copy (rudpx_copy, 65536 blocks)
     import ctypes
     from rudp import _native
     lib = _native.lib()
     lib.rudpx_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                ctypes.c_void_p]
+    lib.rudpx_copy_vpt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
+                                   ctypes.c_int, ctypes.c_void_p]
     a = w.sets[0][1]
     b = torch.empty_like(a)
     stream = torch.cuda.current_stream().cuda_stream
-    ms = time_loop(torch, lambda i: lib.rudpx_copy(a.data_ptr(), b.data_ptr(), a.numel() // 16,
-                                                   65536, stream), steps, 3) / steps
+    ms = time_loop(torch, lambda i: lib.rudpx_copy_vpt(a.data_ptr(), b.data_ptr(), a.numel() // 16,
+                                                       1, 1, stream), steps, 3) / steps
+    ms_gs = time_loop(torch, lambda i: lib.rudpx_copy(a.data_ptr(), b.data_ptr(), a.numel() // 16,
+                                                      65536, stream), steps, 3) / steps
     out["d2d_copy_ceiling_GBs"] = 2 * a.numel() / (ms / 1e3) / 1e9
+    out["d2d_copy_gridstride_GBs"] = 2 * a.numel() / (ms_gs / 1e3) / 1e9
     del w, a, b
     torch.cuda.empty_cache()
     # end to end from pinned host memory: H2D -> encode -> D2H, two-stream pipeline

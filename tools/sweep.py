@@ -199,15 +199,18 @@ def copy_sweep(reps):
     return {k: {"ms": ms, "TBs": 2 * nbytes / ms / 1e9} for k, ms in res.items()}
 
 
+ABLATE_L = 1472
+
+
 def ablate_sweep(reps):
     """Encode with stages switched off (inexact on purpose) beside LDS-tiled copies."""
     dev = torch.device("cuda", 0)
-    n, L = 1 << 20, 1472
+    n, L = 1 << 20, ABLATE_L
     tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
     fr = torch.empty((n, L + 7), dtype=torch.uint8, device=dev)
     stream = torch.cuda.current_stream().cuda_stream
     variants = {}
-    for tile in (8, 16):
+    for tile in ((8, 16) if L >= 1024 else (128, 256)):
         for abl in range(8):
             def setup(tile=tile, abl=abl):
                 lib.rudpx_tune(2, tile)
@@ -216,8 +219,8 @@ def ablate_sweep(reps):
                 setup, lambda: batch.pack_batch(tab, pay, 7, out=fr, want_csum=False))
     a = pay.view(-1)
     b = fr.view(-1)[: a.numel()]
-    for kb in (12, 24):
-        t16 = (kb * 1024 * 23 // 24) // 16 if kb == 24 else (11776 // 16)
+    for kb in ((12, 24) if L >= 1024 else (8, 16)):
+        t16 = (kb * 1024 * 23 // 24) // 16 if kb == 24 else (kb * 1024 // 16)
         variants[f"copy_tile{kb}k"] = (lambda: None, lambda t16=t16: lib.rudpx_copy_tile(
             a.data_ptr(), b.data_ptr(), a.numel() // 16, t16, 0, stream))
     res = interleaved(variants, reps)
@@ -285,6 +288,7 @@ def varlen_sweep(reps):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
+    ap.add_argument("--L", type=int, default=1472, help="payload length for --only ablate")
     ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen"])
     args = ap.parse_args()
     result = {}
@@ -295,6 +299,8 @@ def main():
     if args.only == "varlen":
         result["varlen"] = varlen_sweep(args.reps)
     if args.only == "ablate":
+        global ABLATE_L
+        ABLATE_L = args.L
         result["ablate"] = ablate_sweep(args.reps)
     if args.only in (None, "encode"):
         result["encode"] = encode_sweep(args.reps)
