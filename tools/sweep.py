@@ -285,69 +285,17 @@ def varlen_sweep(reps):
     return out
 
 
-def w128_sweep(reps):
-    """LDS windows: 2 x ds_read_b128 + register funnel vs 5 x ds_read_b32 (rudpx_tune 16).
-
-    r01 result: the b128 form lost at small L (1M x 64 encode 0.0315 vs 0.0295 ms,
-    L = 256 0.1025 vs 0.0965 ms) and tied at L >= 1024, so the kernels keep the
-    dword windows and key 16 was removed; this mode is kept for the record and
-    errors out on the current library."""
-    dev = torch.device("cuda", 0)
-    stream = torch.cuda.current_stream().cuda_stream
-    out = {}
-    for L in (1472, 1024, 256, 64):
-        n = 1 << 20
-        nsets = 1 if L > 512 else 7
-        sets = []
-        for _ in range(nsets):
-            tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
-            fr, _ = batch.pack_batch(tab, pay, 7)
-            sets.append((tab, pay, fr))
-        o16 = [torch.empty(n, dtype=torch.uint16, device=dev) for _ in range(3)]
-        o8 = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(2)]
-        pay_out = torch.empty((n, L), dtype=torch.uint8, device=dev)
-        it = [0]
-
-        def enc():
-            tab, pay, fr = sets[it[0] % nsets]
-            it[0] += 1
-            batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
-
-        def dec(copy):
-            _, _, fr = sets[it[0] % nsets]
-            it[0] += 1
-            _native.check(lib.rudp_decode(fr.data_ptr(), None, L + 7, n, None, o16[0].data_ptr(),
-                                          o16[1].data_ptr(), o8[0].data_ptr(), o8[1].data_ptr(),
-                                          o16[2].data_ptr(), pay_out.data_ptr() if copy else None,
-                                          7, 0, stream))
-        variants = {}
-        for w in (1, 0):
-            variants[f"L{L}_encode_w128_{w}"] = (lambda w=w: lib.rudpx_tune(16, w), enc)
-            variants[f"L{L}_verify_w128_{w}"] = (lambda w=w: lib.rudpx_tune(16, w), lambda: dec(False))
-            variants[f"L{L}_copy_w128_{w}"] = (lambda w=w: lib.rudpx_tune(16, w), lambda: dec(True))
-        res = interleaved(variants, reps)
-        lib.rudpx_tune(16, 1)
-        for k, ms in res.items():
-            alg = n * (2 * L + 12 if "encode" in k else L + 15 if "verify" in k else 2 * L + 15)
-            out[k] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0}
-        del sets, pay_out
-        torch.cuda.empty_cache()
-    return out
-
-
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--L", type=int, default=1472, help="payload length for --only ablate")
-    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "w128"])
+    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen"])
     args = ap.parse_args()
     result = {}
     if args.only in (None, "copy"):
         result["copy"] = copy_sweep(args.reps)
     if args.only in (None, "decode"):
         result["decode"] = decode_sweep(args.reps)
-    if args.only == "w128":
-        result["w128"] = w128_sweep(args.reps)
     if args.only == "varlen":
         result["varlen"] = varlen_sweep(args.reps)
     if args.only == "ablate":
