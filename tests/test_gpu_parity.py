@@ -274,3 +274,45 @@ def test_encode_tile_sizes_agree(cuda, L):
                     lib.rudpx_tune(6, -1)
                 assert np.array_equal(fr, want_fr), (L, n, layout, block, tile, per_cu)
                 assert np.array_equal(cs, want_cs), (L, n, layout, block, tile, per_cu)
+
+
+def test_concurrent_callers(cuda):
+    """The proxy calls the codec from ThreadPoolExecutor workers (proxy.py:127, :154):
+    host-staged and device-resident calls from 8 threads at once stay exact, and an
+    error in one thread leaves the others' calls and messages alone."""
+    from concurrent.futures import ThreadPoolExecutor
+    import torch
+    from rudp import _native
+
+    import threading
+    start = threading.Barrier(8)  # eight distinct threads, all inside the library together
+
+    def job(k):
+        start.wait(timeout=60)
+        L = (64, 1472, 100, 1024)[k % 4]
+        seq, ack, flags, pay = synth.synth(0x7000 + k, k * 1000, 3000, L, ascii=False)
+        want_fr, want_cs = codec_np.encode(seq, ack, flags, pay, 7)
+        for rep in range(3):
+            if k % 2:   # host-staged pipeline (shared, mutex-guarded staging)
+                fr, cs = batch.pack_batch((seq, ack, flags), pay, 7, want_csum=True)
+                d = batch.unpack_batch(fr, 7)
+                got_fr, got_cs, ok = fr, cs, d.ok
+            else:       # device path on this thread's own stream
+                s = torch.cuda.Stream(cuda)
+                with torch.cuda.stream(s):
+                    fr, cs = batch.pack_batch((dev(seq, cuda), dev(ack, cuda), dev(flags, cuda)),
+                                              dev(pay, cuda), 7, want_csum=True)
+                    d = batch.unpack_batch(fr, 7)
+                s.synchronize()
+                got_fr, got_cs, ok = host(fr), host(cs), host(d.ok)
+            assert np.array_equal(got_fr, want_fr), (k, rep)
+            assert np.array_equal(got_cs, want_cs), (k, rep)
+            assert (ok == 1).all(), (k, rep)
+            if k == 3 and rep == 1:  # a failing C call on this thread only
+                assert _native.lib().rudp_device_count(None) == -22
+        return _native.lib().rudp_last_error().decode()
+
+    with ThreadPoolExecutor(8) as ex:
+        msgs = list(ex.map(job, range(8)))
+    # rudp_last_error is per thread: only the thread that failed carries a message
+    assert "NULL" in msgs[3] and not any(m for i, m in enumerate(msgs) if i != 3), msgs
