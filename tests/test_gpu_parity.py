@@ -316,3 +316,58 @@ def test_concurrent_callers(cuda):
         msgs = list(ex.map(job, range(8)))
     # rudp_last_error is per thread: only the thread that failed carries a message
     assert "NULL" in msgs[3] and not any(m for i, m in enumerate(msgs) if i != 3), msgs
+
+
+@pytest.mark.parametrize("slots,stage_mb", [(2, 1), (3, 1), (8, 2)])
+def test_host_pipeline_many_chunks(cuda, slots, stage_mb):
+    """rudp_encode_host / rudp_decode_host with small staging slots: the batch cycles
+    through the slot ring in many chunks (ragged last chunk), H2D/kernel/D2H overlapped."""
+    import ctypes
+    from rudp import _native
+    lib = _native.lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    old_slots, old_mb = lib.rudpx_tune(8, slots), lib.rudpx_tune(9, stage_mb)
+    try:
+        n, L = 20011, 1472   # ~29 MiB of frames: 15-30 chunks
+        seq, ack, flags, pay = synth.synth(0x4321 + slots, 7, n, L, ascii=False)
+        for layout in (5, 7):
+            fr, cs = batch.pack_batch((seq, ack, flags), pay, layout, want_csum=True)
+            want_fr, want_cs = codec_np.encode(seq, ack, flags, pay, layout)
+            assert np.array_equal(fr, want_fr) and np.array_equal(cs, want_cs), layout
+            fr[n - 1, 9] ^= 0x10  # the last frame of the ragged last chunk
+            d = batch.unpack_batch(fr, layout, csum=cs if layout == 5 else None, copy_payload=True)
+            ok = d.ok.copy()
+            assert ok[n - 1] == 0 and (ok[:-1] == 1).all()
+            assert np.array_equal(d.seq, seq) and np.array_equal(d.ack, ack)
+            assert np.array_equal(d.payload[:-1], pay[:-1])
+    finally:
+        lib.rudpx_tune(8, old_slots)
+        lib.rudpx_tune(9, old_mb)
+
+
+@pytest.mark.parametrize("L", [65535, 65520, 4096 + 16])
+def test_maximum_payloads(cuda, L):
+    """The largest payload utils/packet.py frames here (kMaxPayload = 65535): byte and
+    vector paths, both layouts, round trip and a corrupted byte."""
+    n = 37
+    seq, ack, flags, pay = synth.synth(0x600D + L, 0, n, L, ascii=False)
+    for layout in (5, 7):
+        fr, cs = gpu_encode(cuda, seq, ack, flags, pay, layout)
+        want_fr, want_cs = codec_np.encode(seq, ack, flags, pay, layout)
+        assert np.array_equal(fr, want_fr) and np.array_equal(cs, want_cs), (L, layout)
+        fr[5, L // 2] ^= 0x01
+        for copy in (False, True):
+            d = batch.unpack_batch(dev(fr, cuda), layout, copy_payload=copy,
+                                   csum=dev(cs, cuda) if layout == 5 else None)
+            ok = host(d.ok)
+            assert ok[5] == 0 and ok.sum() == n - 1, (L, layout, copy)
+            if copy:
+                assert np.array_equal(host(d.payload), fr[:, layout:])
+
+
+def test_payload_over_maximum_rejected(cuda):
+    import torch
+    pay = torch.zeros((2, 65536), dtype=torch.uint8, device=cuda)
+    tab = batch.synth_batch(2, 0, 1, device=cuda)[0]
+    with pytest.raises(ValueError, match="exceeds"):
+        batch.pack_batch(tab, pay, 7)
