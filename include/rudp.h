@@ -135,7 +135,8 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
  * Strict UTF-8 check of each frame's payload: d_valid[i] = 1 when
  * Packet(frame).get_payload() would return (utils/packet.py:68-73: empty
  * payload -> None; else bytes.decode(), strict UTF-8), 0 when it would raise
- * UnicodeDecodeError.  Frames as in rudp_decode (fixed stride or offsets).
+ * UnicodeDecodeError.  Frames as in rudp_decode (fixed stride or offsets;
+ * with offsets frame_len is a typical-length hint, as there).
  */
 int rudp_validate_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
                        uint32_t frame_len, uint64_t n, int layout, uint8_t* d_valid, int device,

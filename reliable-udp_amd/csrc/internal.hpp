@@ -77,9 +77,10 @@ struct Utf8Args {
   const unsigned char* frames;
   const uint64_t* frame_off;  // [n + 1] or null (fixed stride F)
   uint64_t n;
-  uint32_t F;
+  uint32_t F;                 // fixed stride; with frame_off a mean-length hint
   uint32_t H;
   uint8_t* valid;
+  uint32_t glog;              // log2 lanes per frame (vector kernel)
 };
 
 struct DedupArgs {

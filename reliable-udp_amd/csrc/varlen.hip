@@ -410,7 +410,6 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_par_kernel(Utf8Args a) {
 // predecessor bytes), bytes outside [payload start, frame end) count as
 // absent (0).  An all-ASCII chunk whose predecessors hold no lead byte is
 // valid without the per-byte walk: the common case for text payloads.
-constexpr uint32_t kUtf8Lanes = 16;
 
 __device__ __forceinline__ uint32_t byte_of(u32x4 v, int k) {
   const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
@@ -418,12 +417,14 @@ __device__ __forceinline__ uint32_t byte_of(u32x4 v, int k) {
 }
 
 __global__ void __launch_bounds__(kBlock) validate_utf8_vec_kernel(Utf8Args a) {
-  const uint32_t g = threadIdx.x & (kUtf8Lanes - 1u);
-  const uint64_t p = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / kUtf8Lanes;
+  constexpr uint32_t U = 4;  // chunks per lane per round (2 and 8, nt loads: no better)
+  const uint32_t G = 1u << a.glog;
+  const uint32_t lane = threadIdx.x & 63u;
+  const uint32_t g = threadIdx.x & (G - 1u);
+  const uint64_t p = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> a.glog;
   const bool valid_p = p < a.n;
-  uint32_t bad = 0;
+  uint64_t fo = 0, fe = 0;
   if (valid_p) {
-    uint64_t fo, fe;
     if (a.frame_off) {
       fo = a.frame_off[p];
       fe = a.frame_off[p + 1];
@@ -431,50 +432,85 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_vec_kernel(Utf8Args a) {
       fo = p * (uint64_t)a.F;
       fe = fo + a.F;
     }
-    const uint64_t s = fo + a.H;
-    const uint64_t total = a.frame_off ? a.frame_off[a.n] : a.n * (uint64_t)a.F;
-    if (s < fe) {
-      const uint64_t c_lo = s >> 4, c_hi = (fe - 1) >> 4;
-      for (uint64_t c = c_lo + g; c <= c_hi; c += kUtf8Lanes) {
-        const uint64_t base = c << 4;
-        u32x4 v;
+  }
+  const uint64_t s = fo + a.H;
+  const uint64_t total = a.frame_off ? a.frame_off[a.n] : a.n * (uint64_t)a.F;
+  const uint64_t c_lo = s >> 4;
+  const uint64_t c_hi = s < fe ? (fe - 1) >> 4 : 0;
+  const uint32_t nch = s < fe ? (uint32_t)(c_hi - c_lo + 1) : 0u;
+  // the group's round count is uniform across the wave's groups only up to
+  // their own nch: every lane runs the shuffles of the longest group's rounds
+  uint32_t rounds = (nch + G * U - 1u) / (G * U);
+  for (uint32_t m = 32; m > 0; m >>= 1) rounds = max(rounds, (uint32_t)__shfl_xor((int)rounds, (int)m, 64));
+  // Rounds of U chunks per lane, all loads issued first.  Lane g takes chunks
+  // c_lo + g + G*(u + U*r).  The three bytes before a chunk (the end of chunk
+  // c-1) come by shuffle: from lane g-1 in the same round slot, or for g = 0
+  // from lane G-1 one slot earlier (the previous round's last slot: `carry`).
+  const int src_same = (int)(g > 0 ? lane - 1u : lane);
+  const int src_prev = (int)(g == 0 ? lane + G - 1u : lane);
+  uint32_t bad = 0, carry = 0;
+  for (uint32_t r = 0; r < rounds; ++r) {
+    u32x4 vv[U];
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t i = g + G * (u + U * r);
+      const uint64_t base = (c_lo + i) << 4;
+      vv[u] = make_u32x4(0ull, 0ull);
+      if (i < nch) {
         if (base + 16 <= total) {
-          v = *reinterpret_cast<const u32x4*>(a.frames + base);
+          vv[u] = *reinterpret_cast<const u32x4*>(a.frames + base);
         } else {  // the batch's last chunk: never read past the buffer
-          uint32_t d[4] = {0u, 0u, 0u, 0u};
+          uint32_t d0 = 0, d1 = 0, d2 = 0, d3 = 0;
 #pragma unroll
-          for (int k = 0; k < 16; ++k)
-            if (base + k < total) d[k >> 2] |= (uint32_t)a.frames[base + k] << (8 * (k & 3));
-          v.x = d[0];
-          v.y = d[1];
-          v.z = d[2];
-          v.w = d[3];
+          for (int k = 0; k < 16; ++k) {
+            const uint32_t b = base + k < total ? (uint32_t)a.frames[base + k] << (8 * (k & 3)) : 0u;
+            if (k < 4) d0 |= b;
+            else if (k < 8) d1 |= b;
+            else if (k < 12) d2 |= b;
+            else d3 |= b;
+          }
+          vv[u].x = d0;
+          vv[u].y = d1;
+          vv[u].z = d2;
+          vv[u].w = d3;
         }
-        const uint32_t prev = base >= 4 && base > s ? *reinterpret_cast<const uint32_t*>(a.frames + base - 4) : 0u;
-        // predecessor bytes, zeroed where they fall before the payload start
-        uint32_t p3 = (base >= s + 3) ? (prev >> 8) & 0xFFu : 0u;
-        uint32_t p2 = (base >= s + 2) ? (prev >> 16) & 0xFFu : 0u;
-        uint32_t p1 = (base >= s + 1) ? (prev >> 24) : 0u;
-        const bool interior = base >= s && base + 16 <= fe;
-        if (interior && ((v.x | v.y | v.z | v.w) & 0x80808080u) == 0 && p1 < 0xC0 && p2 < 0xC0 &&
-            p3 < 0xC0)
-          continue;  // plain ASCII, nothing pending from before
-#pragma unroll
-        for (int k = 0; k < 16; ++k) {
-          const uint64_t x = base + (uint64_t)k;
-          if (x < s || x >= fe) continue;
-          const uint32_t cb = byte_of(v, k);
-          bad |= utf8_byte_ok(cb, p1, p2, p3) ? 0u : 1u;
-          p3 = p2;
-          p2 = p1;
-          p1 = cb;
-        }
-        if (c == c_hi)  // the frame's last chunk: nothing may still be expected
-          bad |= (utf8_need(p1) >= 1 || utf8_need(p2) >= 2 || utf8_need(p3) >= 3) ? 1u : 0u;
       }
     }
+#pragma unroll
+    for (uint32_t u = 0; u < U; ++u) {
+      const uint32_t same = (uint32_t)__shfl((int)vv[u].w, src_same, 64);
+      const uint32_t prev_slot = (uint32_t)__shfl((int)(u > 0 ? vv[u - 1].w : carry), src_prev, 64);
+      const uint32_t prev = g > 0 ? same : prev_slot;
+      const uint32_t i = g + G * (u + U * r);
+      if (i >= nch) continue;
+      const uint64_t base = (c_lo + i) << 4;
+      const u32x4 v = vv[u];
+      // predecessor bytes, zeroed where they fall before the payload start
+      uint32_t p3 = (base >= s + 3) ? (prev >> 8) & 0xFFu : 0u;
+      uint32_t p2 = (base >= s + 2) ? (prev >> 16) & 0xFFu : 0u;
+      uint32_t p1 = (base >= s + 1) ? (prev >> 24) : 0u;
+      // the payload's bytes of this chunk (others zeroed: ASCII by construction)
+      const int lo_b = (int)((int64_t)s - (int64_t)base), hi_b = (int)((int64_t)fe - (int64_t)base);
+      const uint64_t pl = lo64(v) & byte_mask(lo_b, hi_b), ph = hi64(v) & byte_mask(lo_b - 8, hi_b - 8);
+      if (((pl | ph) & 0x8080808080808080ull) == 0 && p1 < 0xC0 && p2 < 0xC0 && p3 < 0xC0)
+        continue;  // plain ASCII, nothing pending from before (and so nothing at the end)
+      if (bad) continue;  // this lane already found an invalid byte
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const uint64_t x = base + (uint64_t)k;
+        if (x < s || x >= fe) continue;
+        const uint32_t cb = byte_of(v, k);
+        bad |= utf8_byte_ok(cb, p1, p2, p3) ? 0u : 1u;
+        p3 = p2;
+        p2 = p1;
+        p1 = cb;
+      }
+      if (i + 1 == nch)  // the frame's last chunk: nothing may still be expected
+        bad |= (utf8_need(p1) >= 1 || utf8_need(p2) >= 2 || utf8_need(p3) >= 3) ? 1u : 0u;
+    }
+    carry = vv[U - 1].w;
   }
-  for (uint32_t m = kUtf8Lanes >> 1; m > 0; m >>= 1) bad |= __shfl_xor(bad, (int)m, 64);
+  for (uint32_t m = G >> 1; m > 0; m >>= 1) bad |= __shfl_xor(bad, (int)m, 64);
   if (valid_p && g == 0) a.valid[p] = bad ? 0 : 1;
 }
 
@@ -518,8 +554,14 @@ int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream)
 int launch_validate_utf8(const Utf8Args& args, hipStream_t stream) {
   if (args.n == 0) return 0;
   if ((reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0) {
-    const uint64_t blocks = (args.n * kUtf8Lanes + kBlock - 1) / kBlock;
-    hipLaunchKernelGGL(validate_utf8_vec_kernel, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+    // lanes per frame from the (typical) frame length: two+ 16-byte chunks per lane
+    Utf8Args a = args;
+    const uint32_t chunks = args.F / 16u + 1u;
+    uint32_t lg = 0;
+    while (lg < 4 && (4u << lg) <= chunks) ++lg;
+    a.glog = lg;
+    const uint64_t blocks = ((args.n << lg) + kBlock - 1) / kBlock;
+    hipLaunchKernelGGL(validate_utf8_vec_kernel, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, a);
     return (int)hipGetLastError();
   }
   const uint64_t blocks = (args.n * kVarLanes + kBlock - 1) / kBlock;

@@ -440,8 +440,8 @@ def validate_utf8(frames, layout: Union[str, int] = "rudp7", *, frame_off=None, 
     else:
         _dev_check(frames, "frames", torch.uint8, 1, dev)
         _int_tensor(frame_off, "frame_off", dev, dtypes=(torch.int64,))
-        n, F = frame_off.shape[0] - 1, 0
-        _check_offsets(frames, frame_off)
+        n = frame_off.shape[0] - 1
+        F = _check_offsets(frames, frame_off)  # mean frame length: a lanes-per-frame hint
         off_ptr = frame_off.data_ptr()
     valid = torch.empty((n,), dtype=torch.uint8, device=dev)
     if n:

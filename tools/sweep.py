@@ -285,17 +285,40 @@ def varlen_sweep(reps):
     return out
 
 
+def utf8_sweep(reps):
+    """Strict UTF-8 validation over fixed-length frames (ASCII and random payloads)."""
+    dev = torch.device("cuda", 0)
+    out = {}
+    for L in (1472, 64):
+        n = 1 << 20
+        variants = {}
+        for ascii in (True, False):
+            tab, pay = batch.synth_batch(n, L, 0x5EED0009, ascii=ascii, device=dev)
+            fr, _ = batch.pack_batch(tab, pay, 7)
+            variants[f"L{L}_{'ascii' if ascii else 'random'}"] = (
+                lambda: None, lambda fr=fr: batch.validate_utf8(fr, 7))
+        res = interleaved(variants, reps)
+        for k, ms in res.items():
+            alg = n * (L + 7 + 1)
+            out[k] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0}
+        del variants
+        torch.cuda.empty_cache()
+    return out
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--L", type=int, default=1472, help="payload length for --only ablate")
-    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen"])
+    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "utf8"])
     args = ap.parse_args()
     result = {}
     if args.only in (None, "copy"):
         result["copy"] = copy_sweep(args.reps)
     if args.only in (None, "decode"):
         result["decode"] = decode_sweep(args.reps)
+    if args.only == "utf8":
+        result["utf8"] = utf8_sweep(args.reps)
     if args.only == "varlen":
         result["varlen"] = varlen_sweep(args.reps)
     if args.only == "ablate":
