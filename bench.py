@@ -133,6 +133,37 @@ def time_loop(torch, fn, steps, warmup):
     return start.elapsed_time(stop)
 
 
+C5_PACKETS = 1 << 24
+
+
+def c5_strong_leg(torch, dist, batch, device, world, rank, layout, share_device, steps=10):
+    """BASELINE config 5: 16M x 1472 B packets sharded over the ranks by slicing
+    (rank r frames packets [r*16M/N, (r+1)*16M/N)); whole-job payload GiB/s."""
+    n = C5_PACKETS // world
+    w = Workload(torch, batch, n, 1472, layout, rank * n, SEEDS[1472], device, min_bytes=0)
+    for i in range(2):
+        w.encode(batch, i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for i in range(steps):
+        w.encode(batch, i)
+    torch.cuda.synchronize()
+    dist.barrier()
+    torch.cuda.synchronize()
+    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
+                     device="cpu" if share_device else device)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    wall = float(t.item())
+    del w
+    torch.cuda.empty_cache()
+    return {"GiB_s": C5_PACKETS * 1472 * steps / wall / GIB, "ms": wall / steps * 1e3,
+            "packets_total": C5_PACKETS, "packets_per_gpu": n, "n_gpus": world, "steps": steps,
+            "per_gpu_roofline_frac": n * algorithmic_bytes_encode(1472) / (wall / steps) / 1e9 / HBM_PEAK_GBS,
+            "scaling": "strong"}
+
+
 def legs(torch, batch, device, steps):
     out = {}
     for L in (1024, 64):
@@ -395,6 +426,11 @@ def main():
 
     extra = legs(torch, batch, device, max(10, args.steps // 2)) if (
         rank == 0 and world == 1 and not args.no_legs) else None
+    if world > 1 and not args.no_legs and not args.total_packets:
+        # BASELINE config 5 beside the weak-scaling headline: 16M x 1472 B split
+        # over the ranks (strong scaling), same barrier + max-over-ranks clock.
+        extra = {"c5_16Mx1472_strong": c5_strong_leg(torch, dist, batch, device, world, rank,
+                                                      args.layout, args.share_device)}
 
     if rank == 0:
         total_payload = world * n * L * args.steps
@@ -436,9 +472,10 @@ def main():
         }
         if extra is not None:
             line["legs"] = extra
-            ceiling = extra["d2d_copy_ceiling_GBs"]
-            line["roofline"]["measured_copy_ceiling_GBs"] = ceiling
-            line["roofline"]["frac_of_copy_ceiling"] = achieved / ceiling
+            ceiling = extra.get("d2d_copy_ceiling_GBs")
+            if ceiling:
+                line["roofline"]["measured_copy_ceiling_GBs"] = ceiling
+                line["roofline"]["frac_of_copy_ceiling"] = achieved / ceiling
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()

@@ -430,6 +430,8 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
   while (lg < 4 && (4u << lg) <= chunks) ++lg;
   if (tuning().varlen_glog >= 0 && tuning().varlen_glog <= 6) lg = (uint32_t)tuning().varlen_glog;
   a.glog = tuning().varlen_vec ? lg : kNoVec;
+  if (tuning().varlen_vec && tuning().varlen_tile)
+    varlen_tile_geometry(in->payload_len, &a.tile_T, &a.tile_glog, &a.tile_cap);
   rc = launch_encode_varlen(a, layout, s);
   if (rc) return hip_fail((hipError_t)rc, "varlen encode launch");
   return 0;

@@ -70,6 +70,12 @@ struct VarlenArgs {
   uint16_t* csum_out;
   uint64_t n;
   uint32_t glog;                  // log2 lanes per packet (vector kernels); kNoVec = byte kernels
+  // encode tile kernel (packed payload): packets per tile (power of two, 4..256),
+  // log2(256 / tile_T), and the LDS payload bytes a tile may use (larger tiles
+  // take the per-packet path inside the kernel).  tile_T = 0: no tile kernel.
+  uint32_t tile_T;
+  uint32_t tile_glog;
+  uint32_t tile_cap;
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -115,6 +121,9 @@ struct Tuning {
   int decode_verify_tile = 1;  // verify-only decode through an LDS tile (0: aligned-chunk kernel)
   int varlen_vec = 1;     // varlen encode/decode: vector kernels (0: byte kernels)
   int varlen_glog = -1;   // varlen lanes-per-packet log2 (0..6); -1 = from the length hint
+  int varlen_tile = 1;    // varlen encode of packed payloads through LDS tiles (0: vector kernel)
+  int varlen_tile_maxT = 256;     // varlen encode tile: most packets per tile
+  int varlen_tile_bytes = 24576;  // varlen encode tile: payload bytes per tile (at the hint)
   int encode_ablate = 0;  // EncodeTileArgs::ablate (sweeps only)
   int host_slots = 3;     // *_host pipeline: device staging slots (2..8)
   int host_stage_mb = 128;  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
@@ -128,6 +137,7 @@ uint32_t decode_group_log2(uint32_t L);
 int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStream_t stream);
 int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream_t stream);
 int launch_synth(const SynthArgs& args, hipStream_t stream);
+void varlen_tile_geometry(uint32_t len_hint, uint32_t* T, uint32_t* glog, uint32_t* cap);
 int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream);
 int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream);
 int launch_validate_utf8(const Utf8Args& args, hipStream_t stream);

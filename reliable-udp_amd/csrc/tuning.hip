@@ -176,7 +176,10 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // (1..4, -1 = auto); 5: XCD-contiguous tile order; 6: encode tiles per CU cap;
 // 7: contiguous phase-1 stream with checksums summed from LDS; 8: host pipeline
 // slots; 9: host pipeline MiB per slot; 10: encode tile workgroup size;
-// 11: copy-out decode through an LDS tile; 12: verify-only decode through an LDS tile.
+// 11: copy-out decode through an LDS tile; 12: verify-only decode through an LDS tile;
+// 13: encode stage ablation; 14: varlen vector kernels; 15: varlen lanes log2;
+// 16: varlen encode through LDS tiles (packed payloads); 17: most packets per
+// varlen tile; 18: varlen tile payload bytes at the hint.
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
@@ -186,7 +189,9 @@ int rudpx_tune(int key, int value) {
             : key == 6 ? &t.encode_blocks_per_cu : key == 7 ? &t.encode_contig
             : key == 8 ? &t.host_slots : key == 9 ? &t.host_stage_mb
             : key == 10 ? &t.encode_block : key == 11 ? &t.decode_copy_tile
-            : key == 12 ? &t.decode_verify_tile : key == 13 ? &t.encode_ablate : key == 14 ? &t.varlen_vec : key == 15 ? &t.varlen_glog : nullptr;
+            : key == 12 ? &t.decode_verify_tile : key == 13 ? &t.encode_ablate : key == 14 ? &t.varlen_vec : key == 15 ? &t.varlen_glog
+            : key == 16 ? &t.varlen_tile : key == 17 ? &t.varlen_tile_maxT
+            : key == 18 ? &t.varlen_tile_bytes : nullptr;
   if (!slot) return -22;
   const int old = *slot;
   *slot = value;

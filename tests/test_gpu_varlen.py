@@ -341,3 +341,58 @@ def test_varlen_encode_kernels_vs_oracle(cuda, lo, hi, layout):
                 assert np.array_equal(host(frames), want_fr), (lo, hi, layout, vec, hint)
         finally:
             lib.rudpx_tune(14, 1)
+
+
+@pytest.mark.parametrize("dist", ["uniform2944", "bursty", "empty", "tiny", "mtu"])
+@pytest.mark.parametrize("layout", [5, 7])
+def test_varlen_encode_tile_kernel_vs_oracle(cuda, dist, layout):
+    """The LDS-tile varlen encode (packed payloads) == per-packet vector kernel
+    == oracle, at every tile size the hint can pick, including tiles whose run
+    overflows the LDS budget (bursts far above the hint: per-packet path)."""
+    import ctypes
+    import torch
+    from rudp import _native
+    lib = _native.lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    rng = np.random.default_rng(sum(map(ord, dist)) * 10 + layout)
+    n = 20011
+    if dist == "uniform2944":
+        lens = rng.integers(0, 2945, n)
+    elif dist == "bursty":   # mostly one character, runs of MTU payloads
+        lens = np.where(rng.random(n) < 0.9, 1, 1472)
+        lens[5000:5300] = 4000
+    elif dist == "empty":
+        lens = np.zeros(n, np.int64)
+    elif dist == "tiny":
+        lens = rng.integers(0, 4, n)
+    else:
+        lens = np.full(n, 1472)
+    lens = lens.astype(np.int32)
+    seq, ack, flags, _ = synth.synth(int(rng.integers(1 << 30)), 0, n, 0)
+    packed = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    pays, _ = split_by_lengths(packed, lens)
+    want_fr, want_off, want_cs = codec_np.encode_varlen(seq, ack, flags, pays, layout)
+    tab = (dev(seq, cuda), dev(ack, cuda), dev(flags, cuda))
+    d_lens = dev(lens, cuda)
+    p = dev(packed, cuda)
+    frames = torch.empty(len(want_fr), dtype=torch.uint8, device=cuda)
+    frame_off = torch.empty(n + 1, dtype=torch.int64, device=cuda)
+    csum = torch.empty(n, dtype=torch.uint16, device=cuda)
+    try:
+        for tile in (1, 0):
+            lib.rudpx_tune(16, tile)
+            for hint in (0, 1, 16, 100, 1472, 3000, 6144):
+                frames.fill_(0xCD)
+                csum.fill_(0)
+                b = _native.RudpBatch(n=n, payload_len=hint, reserved=0, seq=tab[0].data_ptr(),
+                                      ack=tab[1].data_ptr(), flags=tab[2].data_ptr(),
+                                      payload=p.data_ptr() if p.numel() else 16,
+                                      len=d_lens.data_ptr(), payload_off=None)
+                _native.check(lib.rudp_encode_varlen(ctypes.byref(b), frames.data_ptr(),
+                                                     frame_off.data_ptr(), csum.data_ptr(), layout, 0,
+                                                     torch.cuda.current_stream().cuda_stream))
+                assert np.array_equal(host(frames), want_fr), (dist, layout, tile, hint)
+                assert np.array_equal(host(frame_off), want_off), (dist, layout, tile, hint)
+                assert np.array_equal(host(csum), want_cs), (dist, layout, tile, hint)
+    finally:
+        lib.rudpx_tune(16, 1)

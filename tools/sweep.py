@@ -285,6 +285,50 @@ def varlen_sweep(reps):
     return out
 
 
+def varlen_enc_sweep(reps):
+    """Varlen encode of packed payloads: LDS-tile kernel vs per-packet vector kernel."""
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    out = {}
+    n = 1 << 20
+    for name in ("L1", "L64", "L1024", "L1472", "U0-2944"):
+        if name.startswith("U"):
+            g = torch.Generator(device=dev)
+            g.manual_seed(7)
+            lens = torch.randint(0, 2945, (n,), device=dev, generator=g, dtype=torch.int32)
+        else:
+            lens = torch.full((n,), int(name[1:]), dtype=torch.int32, device=dev)
+        total = int(lens.sum().item())
+        flat = torch.randint(0, 128, (total,), dtype=torch.uint8, device=dev)
+        tab, _ = batch.synth_batch(n, 0, 0x5EED0007, device=dev)
+        hint = total // n
+        fr = torch.empty(total + 7 * n, dtype=torch.uint8, device=dev)
+        off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+
+        def enc(hint=hint, flat=flat, lens=lens, fr=fr, off=off, tab=tab):
+            b = _native.RudpBatch(n=n, payload_len=hint, reserved=0, seq=tab.seq.data_ptr(),
+                                  ack=tab.ack.data_ptr(), flags=tab.flags.data_ptr(),
+                                  payload=flat.data_ptr(), len=lens.data_ptr(), payload_off=None)
+            _native.check(lib.rudp_encode_varlen(ctypes.byref(b), fr.data_ptr(), off.data_ptr(),
+                                                 None, 7, 0, stream))
+        def cfg(tile, maxT=256, nbytes=24576):
+            return lambda: (lib.rudpx_tune(16, tile), lib.rudpx_tune(17, maxT), lib.rudpx_tune(18, nbytes))
+        variants = {f"{name}_tile": (cfg(1), enc), f"{name}_vec": (cfg(0), enc)}
+        for maxT in (64, 128):
+            variants[f"{name}_tile_maxT{maxT}"] = (cfg(1, maxT), enc)
+        for nbytes in (8192, 12288, 16384, 32768):
+            variants[f"{name}_tile_bytes{nbytes}"] = (cfg(1, 256, nbytes), enc)
+        res = interleaved(variants, reps)
+        cfg(1)()
+        # payload + len + header table read; frames + offsets written (scan included)
+        alg = 2 * total + n * (7 + 9 + 8)
+        for k, ms in res.items():
+            out[k] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0}
+        del flat, fr, off, lens, tab
+        torch.cuda.empty_cache()
+    return out
+
+
 def utf8_sweep(reps):
     """Strict UTF-8 validation over fixed-length frames (ASCII and random payloads)."""
     dev = torch.device("cuda", 0)
@@ -310,7 +354,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--L", type=int, default=1472, help="payload length for --only ablate")
-    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "utf8"])
+    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8"])
     args = ap.parse_args()
     result = {}
     if args.only in (None, "copy"):
@@ -321,6 +365,8 @@ def main():
         result["utf8"] = utf8_sweep(args.reps)
     if args.only == "varlen":
         result["varlen"] = varlen_sweep(args.reps)
+    if args.only == "varlen_enc":
+        result["varlen_enc"] = varlen_enc_sweep(args.reps)
     if args.only == "ablate":
         global ABLATE_L
         ABLATE_L = args.L
