@@ -256,7 +256,10 @@ int launch_tile_nt(const EncodeTileArgs& args, hipStream_t stream) {
 template <int H>
 int launch_tile_policy(const EncodeTileArgs& args, hipStream_t stream) {
   const int p1 = tuning().encode_p1;
-  const int block = tuning().encode_block;
+  int block = tuning().encode_block;
+  // A packet's lanes must sit in one wave (the shfl_xor reduction): wider
+  // blocks give each packet (256/T)*(block/256) lanes, so keep that <= 64.
+  if (block > 256 && (uint64_t)(256u / args.T) * (uint32_t)(block / 256) > 64u) block = 256;
   if (block == 64 && args.T <= 64) return launch_tile<H, true, true, 8, true, 64>(args, stream);
   if (block == 128 && args.T <= 128) return launch_tile<H, true, true, 8, true, 128>(args, stream);
   if (block == 512) return launch_tile<H, true, true, 8, true, 512>(args, stream);

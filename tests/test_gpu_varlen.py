@@ -388,6 +388,7 @@ def test_varlen_encode_tile_kernel_vs_oracle(cuda, dist, layout):
                                       ack=tab[1].data_ptr(), flags=tab[2].data_ptr(),
                                       payload=p.data_ptr() if p.numel() else 16,
                                       len=d_lens.data_ptr(), payload_off=None)
+                frame_off.fill_(-1)
                 _native.check(lib.rudp_encode_varlen(ctypes.byref(b), frames.data_ptr(),
                                                      frame_off.data_ptr(), csum.data_ptr(), layout, 0,
                                                      torch.cuda.current_stream().cuda_stream))

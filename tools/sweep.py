@@ -58,10 +58,16 @@ def interleaved(variants, reps):
     return {k: statistics.median(v) for k, v in times.items()}
 
 
+BLOCKS_OVERRIDE = None
+ENCODE_LS = None
+GEOMETRY_VARIANTS = False  # varlen_enc: also sweep tile size knobs (keys 17, 18)
+
+
 def encode_sweep(reps):
     out = {}
     dev = torch.device("cuda", 0)
-    for L, tiles in ((1472, (0, 4, 8, 16)), (1024, (0, 4, 8, 16)), (64, (0, 16, 32, 64, 128))):
+    shapes = ((1472, (0, 4, 8, 16)), (1024, (0, 4, 8, 16)), (64, (0, 16, 32, 64, 128)))
+    for L, tiles in (s for s in shapes if not ENCODE_LS or s[0] in ENCODE_LS):
         n = 1 << 20
         nsets = 1 if L > 512 else 7
         sets = []
@@ -76,11 +82,12 @@ def encode_sweep(reps):
             batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
 
         variants = {}
-        for block in (64, 128, 256):
+        blocks = BLOCKS_OVERRIDE or (64, 128, 256)
+        for block in blocks:
             for tile in tiles:
                 if tile > block:
                     continue
-                for per_cu in ((-1, 0, 5) if block == 256 else (0, 16, 24)):
+                for per_cu in ((-1, 0, 5) if block == 256 else (0, 16, 24) if block < 256 else (0, 2, 3)):
                     def setup(tile=tile, per_cu=per_cu, block=block):
                         lib.rudpx_tune(10, block)
                         lib.rudpx_tune(2, tile)
@@ -314,10 +321,11 @@ def varlen_enc_sweep(reps):
         def cfg(tile, maxT=256, nbytes=24576):
             return lambda: (lib.rudpx_tune(16, tile), lib.rudpx_tune(17, maxT), lib.rudpx_tune(18, nbytes))
         variants = {f"{name}_tile": (cfg(1), enc), f"{name}_vec": (cfg(0), enc)}
-        for maxT in (64, 128):
-            variants[f"{name}_tile_maxT{maxT}"] = (cfg(1, maxT), enc)
-        for nbytes in (8192, 12288, 16384, 32768):
-            variants[f"{name}_tile_bytes{nbytes}"] = (cfg(1, 256, nbytes), enc)
+        if GEOMETRY_VARIANTS:
+            for maxT in (64, 128):
+                variants[f"{name}_tile_maxT{maxT}"] = (cfg(1, maxT), enc)
+            for nbytes in (8192, 12288, 16384, 32768):
+                variants[f"{name}_tile_bytes{nbytes}"] = (cfg(1, 256, nbytes), enc)
         res = interleaved(variants, reps)
         cfg(1)()
         # payload + len + header table read; frames + offsets written (scan included)
@@ -355,7 +363,14 @@ def main():
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--L", type=int, default=1472, help="payload length for --only ablate")
     ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8"])
+    ap.add_argument("--blocks", type=str, default="", help="encode sweep: workgroup sizes, e.g. 256,512,1024")
+    ap.add_argument("--encode-L", type=str, default="", help="encode sweep: payload lengths, e.g. 1472")
     args = ap.parse_args()
+    global BLOCKS_OVERRIDE, ENCODE_LS
+    if args.blocks:
+        BLOCKS_OVERRIDE = tuple(int(b) for b in args.blocks.split(","))
+    if args.encode_L:
+        ENCODE_LS = tuple(int(x) for x in args.encode_L.split(","))
     result = {}
     if args.only in (None, "copy"):
         result["copy"] = copy_sweep(args.reps)
