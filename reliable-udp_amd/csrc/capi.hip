@@ -89,6 +89,8 @@ EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t*
     a.num_tiles = (uint32_t)((a.n + a.T - 1) / a.T);
     a.xcd_swizzle = tuning().encode_xcd_swizzle ? 1u : 0u;
     a.ablate = (uint32_t)tuning().encode_ablate;
+    const uint32_t V = a.L / 16u;
+    a.invV = ((1ull << 32) + V - 1ull) / V;
   }
   return a;
 }

@@ -274,8 +274,168 @@ int launch_tile_policy(const EncodeTileArgs& args, hipStream_t stream) {
   return launch_tile_nt<H, 8, false>(args, stream);
 }
 
+
+// Register-streamed encode (payload_len % 16 == 0, both buffers 16-B aligned);
+// opt-in (rudpx_tune 20), bit-exact, and SLOWER than the LDS tile kernel: 1M x
+// 1472 B 0.588 ms at best (T = 4) vs 0.530 ms, and 0.558 ms even with the sums
+// and header chunks ablated, so the LDS staging is not what bounds encode
+// (profiles/r01/sweeps/stream_encode*.json).
+// No LDS tile: the payload's 16-B vectors go load -> register -> store, one
+// vector per lane per round with consecutive lanes on consecutive vectors, so
+// every wave-instruction reads and writes 1 KiB contiguous, like a copy.
+// Packet q's payload starts at output byte P = q*F + H, s = (-P) mod 16 bytes
+// before the next 16-B boundary.  Output chunk k of q's payload run (all
+// payload bytes) is bytes [s + 16k, s + 16k + 16) of the payload: vector k
+// alone when s == 0, else the tail of vector k and the head of vector k+1,
+// which the lane holding vector k+1 takes from its left neighbour by a shuffle
+// (lane 0 of a wave loads it).  What the stream leaves out is, per packet, the
+// one or two aligned chunks [floor16(P - H), ceil16(P)) holding the header:
+// after one barrier, the packet's thread builds them from the header (its
+// checksum now complete), the previous packet's last vector and its own first
+// vector (both kept in LDS by the lanes that loaded them).  Per-packet sums
+// come from a segmented shuffle reduction per round and LDS atomics.
+template <int H, int R>
+__global__ void __launch_bounds__(kBlock) encode_stream_kernel(EncodeTileArgs a) {
+  __shared__ uint32_t s_sum[kBlock];
+  __shared__ u32x4 s_head[kBlock], s_tail[kBlock];
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t T = a.T, L = a.L, V = L >> 4, F = L + H;
+  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  const uint64_t left = a.n - p0;
+  const uint32_t Tv = left < T ? (uint32_t)left : T;
+  const uint32_t nvec = Tv * V;
+  const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + p0 * (uint64_t)L);
+  unsigned char* out = a.frames;
+  for (uint32_t i = tid; i < Tv; i += kBlock) s_sum[i] = 0;
+  __syncthreads();
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  for (uint32_t v0 = 0; v0 < nvec; v0 += (uint32_t)R * kBlock) {
+    u32x4 cur[R], lft[R];
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const uint32_t v = v0 + (uint32_t)u * kBlock + tid;
+      cur[u] = zero;
+      lft[u] = zero;
+      if (v < nvec) {
+        cur[u] = __builtin_nontemporal_load(src + v);
+        if (lane == 0 && v > 0) lft[u] = src[v - 1];
+      }
+    }
+#pragma unroll
+    for (int u = 0; u < R; ++u) {
+      const uint32_t v = v0 + (uint32_t)u * kBlock + tid;
+      u32x4 l;
+      l.x = __shfl_up(cur[u].x, 1, 64);
+      l.y = __shfl_up(cur[u].y, 1, 64);
+      l.z = __shfl_up(cur[u].z, 1, 64);
+      l.w = __shfl_up(cur[u].w, 1, 64);
+      if (lane == 0) l = lft[u];
+      const bool valid = v < nvec;
+      const uint32_t q = valid ? (uint32_t)(((uint64_t)v * a.invV) >> 32) : 0xFFFFFFFFu;
+      uint32_t x = valid ? le16_sum(cur[u]) : 0u;
+      if (valid) {
+        const uint32_t j = v - q * V;
+        const uint64_t P = (p0 + q) * (uint64_t)F + H;
+        const uint32_t sh = (uint32_t)(-P) & 15u;
+        if (sh == 0) {
+          __builtin_nontemporal_store(cur[u], reinterpret_cast<u32x4*>(out + P + 16ull * j));
+        } else if (j > 0) {
+          __builtin_nontemporal_store(funnel32(l, cur[u], sh),
+                                      reinterpret_cast<u32x4*>(out + P + sh + 16ull * (j - 1)));
+        }
+        if (j == 0) s_head[q] = cur[u];
+        if (j == V - 1) s_tail[q] = cur[u];
+      }
+      if (a.ablate & 8u) continue;  // diagnostic: no sums
+      // segmented inclusive sum over lanes of the same packet
+      for (uint32_t d = 1; d < 64; d <<= 1) {
+        const uint32_t y = __shfl_up(x, d, 64);
+        const uint32_t qy = __shfl_up(q, d, 64);
+        if (lane >= d && qy == q) x += y;
+      }
+      const uint32_t qn = __shfl_down(q, 1, 64);
+      if (valid && (lane == 63 || qn != q)) atomicAdd(&s_sum[q], x);
+    }
+  }
+  __syncthreads();
+
+  // header chunks [floor16(P - H), ceil16(P)) of packet q = tid
+  if (tid < Tv && !(a.ablate & 16u)) {
+    const uint32_t q = tid;
+    const uint64_t p = p0 + q;
+    const uint64_t P = p * (uint64_t)F + H;
+    const uint32_t s = a.seq[p], k = a.ack[p], f = a.flags[p];
+    const uint32_t c = packet_csum(s_sum[q], s, k, f);
+    if (a.csum) a.csum[p] = (uint16_t)c;
+    const uint64_t h = pack_header<H>(s, k, f, c);
+    const u32x4 head = s_head[q];
+    const u32x4 tail = q > 0 ? s_tail[q - 1] : (p > 0 ? src[-1] : zero);
+    const uint64_t X0 = (P - H) & ~15ull, X1 = (P + 15u) & ~15ull;
+    for (uint64_t X = X0; X < X1; X += 16) {
+      const int k0 = (int)(int64_t)(X - (P - H));  // frame position of chunk byte 0 (> -16)
+      u32x4 w = zero;
+      if (k0 < 0) w = funnel32(tail, zero, (uint32_t)(k0 + 16));  // previous payload's last bytes
+      const uint32_t d = (uint32_t)(P - X);                        // payload starts d bytes in
+      if (d < 16) {
+        const u32x4 hp = funnel32(zero, head, 16u - d);
+        w.x |= hp.x; w.y |= hp.y; w.z |= hp.z; w.w |= hp.w;
+      }
+      uint64_t lo = lo64(w), hi = hi64(w);
+      if (k0 >= 0) {
+        lo |= h >> (8 * k0);
+      } else {
+        const int sh = -k0;
+        if (sh < 8) {
+          lo |= h << (8 * sh);
+          hi |= h >> (64 - 8 * sh);
+        } else {
+          hi |= h << (8 * (sh - 8));
+        }
+      }
+      __builtin_nontemporal_store(make_u32x4(lo, hi), reinterpret_cast<u32x4*>(out + X));
+    }
+    if (p == a.n - 1) {  // the batch's last bytes: a partial chunk, bytewise
+      const uint64_t E = P + L, XE = E & ~15ull;
+      const u32x4 t = s_tail[q];
+      const uint32_t dw[4] = {t.x, t.y, t.z, t.w};
+      for (uint64_t y = XE; y < E; ++y) {
+        const uint32_t b = 16u - (uint32_t)(E - y);
+        out[y] = (unsigned char)(dw[b >> 2] >> (8 * (b & 3)));
+      }
+    }
+  }
+}
+
+template <int H>
+int launch_stream(const EncodeTileArgs& args, hipStream_t stream) {
+  const uint64_t blocks = (args.n + args.T - 1) / args.T;
+  const int R = tuning().encode_stream_R;
+  if (R == 1)
+    hipLaunchKernelGGL((encode_stream_kernel<H, 1>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+  else if (R == 4)
+    hipLaunchKernelGGL((encode_stream_kernel<H, 4>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+  else
+    hipLaunchKernelGGL((encode_stream_kernel<H, 2>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+  return (int)hipGetLastError();
+}
+
+// Packets per stream workgroup: about 1.5K vectors (T = 16 at 1472 B), <= 256.
+uint32_t stream_tile(uint32_t L) {
+  const int forced = tuning().encode_stream_T;
+  if (forced >= 1 && forced <= (int)kBlock) return (uint32_t)forced;
+  const uint32_t V = L / 16u;
+  uint32_t t = 1;
+  while (t * 2u <= kBlock && t * 2u * V <= 1536u) t *= 2u;
+  return t;
+}
+
 int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStream_t stream) {
   if (args.n == 0) return 0;
+  if (tile_path && tuning().encode_stream) {
+    EncodeTileArgs s = args;
+    s.T = stream_tile(args.L);
+    return layout == 7 ? launch_stream<7>(s, stream) : launch_stream<5>(s, stream);
+  }
   if (tile_path)
     return layout == 7 ? launch_tile_policy<7>(args, stream) : launch_tile_policy<5>(args, stream);
   const uint64_t blocks = (args.n + (kBlock / 64) - 1) / (kBlock / 64);

@@ -22,6 +22,7 @@ struct EncodeTileArgs {
   uint32_t num_tiles;
   uint32_t ablate;      // diagnostics only (wrong output): 1 no LDS sum pass, 2 plain phase-2
                         // LDS reads, 4 no header-table loads
+  uint64_t invV;        // ceil(2^32 / (L / 16)) for exact v / V (stream kernel)
 };
 
 struct DecodeArgs {
@@ -125,6 +126,9 @@ struct Tuning {
   int varlen_tile_maxT = 256;     // varlen encode tile: most packets per tile
   int varlen_tile_bytes = 24576;  // varlen encode tile: payload bytes per tile (at the hint)
   int encode_ablate = 0;  // EncodeTileArgs::ablate (sweeps only)
+  int encode_stream = 0;  // register-streamed encode (no LDS tile); 0 = LDS tile kernel
+  int encode_stream_T = 0;  // stream kernel packets per workgroup; 0 = automatic
+  int encode_stream_R = 2;  // stream kernel rounds of loads in flight per lane (1, 2, 4)
   int host_slots = 3;     // *_host pipeline: device staging slots (2..8)
   int host_stage_mb = 128;  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
 };

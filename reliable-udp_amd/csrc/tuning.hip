@@ -179,7 +179,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // 11: copy-out decode through an LDS tile; 12: verify-only decode through an LDS tile;
 // 13: encode stage ablation; 14: varlen vector kernels; 15: varlen lanes log2;
 // 16: varlen encode through LDS tiles (packed payloads); 17: most packets per
-// varlen tile; 18: varlen tile payload bytes at the hint.
+// varlen tile; 18: varlen tile payload bytes at the hint; 20: register-streamed
+// encode; 21: its packets per workgroup (0 auto); 22: its load rounds in flight.
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
@@ -191,7 +192,8 @@ int rudpx_tune(int key, int value) {
             : key == 10 ? &t.encode_block : key == 11 ? &t.decode_copy_tile
             : key == 12 ? &t.decode_verify_tile : key == 13 ? &t.encode_ablate : key == 14 ? &t.varlen_vec : key == 15 ? &t.varlen_glog
             : key == 16 ? &t.varlen_tile : key == 17 ? &t.varlen_tile_maxT
-            : key == 18 ? &t.varlen_tile_bytes : nullptr;
+            : key == 18 ? &t.varlen_tile_bytes : key == 20 ? &t.encode_stream
+            : key == 21 ? &t.encode_stream_T : key == 22 ? &t.encode_stream_R : nullptr;
   if (!slot) return -22;
   const int old = *slot;
   *slot = value;

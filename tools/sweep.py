@@ -60,7 +60,8 @@ def interleaved(variants, reps):
 
 BLOCKS_OVERRIDE = None
 ENCODE_LS = None
-GEOMETRY_VARIANTS = False  # varlen_enc: also sweep tile size knobs (keys 17, 18)
+GEOMETRY_VARIANTS = False
+STREAM_ABLATE = False      # stream: also time stage ablations (wrong output; key 13 bits 8/16)  # varlen_enc: also sweep tile size knobs (keys 17, 18)
 
 
 def encode_sweep(reps):
@@ -116,6 +117,55 @@ def encode_sweep(reps):
     lib.rudpx_tune(6, -1)
     lib.rudpx_tune(7, 1)
     lib.rudpx_tune(10, 256)
+    return out
+
+
+def stream_sweep(reps):
+    """Register-streamed encode (rudpx_tune 20-22) against the LDS-tile encode."""
+    out = {}
+    dev = torch.device("cuda", 0)
+    for L, tiles in ((1472, (4, 8, 16, 32)), (1024, (4, 8, 16, 32)), (64, (32, 64, 128, 256))):
+        n = 1 << 20
+        nsets = 1 if L > 512 else 7
+        sets = []
+        for _ in range(nsets):
+            tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
+            sets.append((tab, pay, torch.empty((n, L + 7), dtype=torch.uint8, device=dev)))
+        it = [0]
+
+        def run():
+            tab, pay, fr = sets[it[0] % nsets]
+            it[0] += 1
+            batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
+
+        def cfg(stream, tile=0, rounds=2):
+            return lambda: (lib.rudpx_tune(20, stream), lib.rudpx_tune(21, tile), lib.rudpx_tune(22, rounds))
+        variants = {f"L{L}_tile": (cfg(0), run)}
+        for tile in tiles:
+            for rounds in (1, 2, 4):
+                variants[f"L{L}_stream_T{tile}_R{rounds}"] = (cfg(1, tile, rounds), run)
+        if STREAM_ABLATE:
+            for abl in (8, 16, 24):
+                for tile in tiles[:2]:
+                    variants[f"L{L}_stream_T{tile}_R2_ablate{abl}"] = (
+                        lambda tile=tile, abl=abl: (cfg(1, tile, 2)(), lib.rudpx_tune(13, abl)), run)
+                    variants[f"L{L}_tile_ablate{abl}"] = (lambda: (cfg(0)(), lib.rudpx_tune(13, 0)), run)
+            variants[f"L{L}_tile"] = (lambda: (cfg(0)(), lib.rudpx_tune(13, 0)), run)
+        res = interleaved(variants, reps)
+        lib.rudpx_tune(13, 0)
+        alg = n * (2 * L + 12)
+        tab0, pay0, _ = sets[0]
+        cfg(0)()
+        want, _ = batch.pack_batch(tab0, pay0, 7)
+        for k, (setup, _) in variants.items():
+            setup()
+            got, _ = batch.pack_batch(tab0, pay0, 7)
+            lib.rudpx_tune(13, 0)
+            out[k] = {"ms": res[k], "TBs": alg / res[k] / 1e9, "frac": alg / res[k] / 1e9 / 8.0,
+                      "exact": bool(torch.equal(got, want))}
+        cfg(0)()
+        del sets
+        torch.cuda.empty_cache()
     return out
 
 
@@ -362,11 +412,13 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--L", type=int, default=1472, help="payload length for --only ablate")
-    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8"])
+    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "stream"])
     ap.add_argument("--blocks", type=str, default="", help="encode sweep: workgroup sizes, e.g. 256,512,1024")
     ap.add_argument("--encode-L", type=str, default="", help="encode sweep: payload lengths, e.g. 1472")
+    ap.add_argument("--ablate", action="store_true", help="stream sweep: add stage ablations")
     args = ap.parse_args()
-    global BLOCKS_OVERRIDE, ENCODE_LS
+    global BLOCKS_OVERRIDE, ENCODE_LS, STREAM_ABLATE
+    STREAM_ABLATE = args.ablate
     if args.blocks:
         BLOCKS_OVERRIDE = tuple(int(b) for b in args.blocks.split(","))
     if args.encode_L:
@@ -380,6 +432,8 @@ def main():
         result["utf8"] = utf8_sweep(args.reps)
     if args.only == "varlen":
         result["varlen"] = varlen_sweep(args.reps)
+    if args.only == "stream":
+        result["stream"] = stream_sweep(args.reps)
     if args.only == "varlen_enc":
         result["varlen_enc"] = varlen_enc_sweep(args.reps)
     if args.only == "ablate":
