@@ -91,6 +91,8 @@ EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t*
     a.ablate = (uint32_t)tuning().encode_ablate;
     const uint32_t V = a.L / 16u;
     a.invV = ((1ull << 32) + V - 1ull) / V;
+    const int al = tuning().out_align64;
+    a.out_align64 = (al == 1 || (al < 0 && a.T * a.L > 16384u)) ? 1u : 0u;
   }
   return a;
 }
@@ -330,6 +332,7 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, ui
   if (rc || n == 0) return rc;
   if ((rc = check_device(device))) return rc;
   DecodeArgs a{};
+  a.align64 = tuning().out_align64 == 1 ? 1u : 0u;
   a.frames = d_frames;
   a.csum_in = d_csum_in_or_null;
   a.seq = d_seq;
@@ -434,6 +437,7 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
   a.glog = tuning().varlen_vec ? lg : kNoVec;
   if (tuning().varlen_vec && tuning().varlen_tile)
     varlen_tile_geometry(in->payload_len, &a.tile_T, &a.tile_glog, &a.tile_cap);
+  a.align64 = tuning().out_align64 == 1 ? 1u : 0u;
   rc = launch_encode_varlen(a, layout, s);
   if (rc) return hip_fail((hipError_t)rc, "varlen encode launch");
   return 0;

@@ -203,17 +203,23 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
   const uint32_t nbytes = Tv * F;
   const uint32_t nvec = (nbytes + 15u) >> 4;
   u32x4* tile = reinterpret_cast<u32x4*>(lds);
+  // Lanes are dealt vectors from the tile's first 64-B boundary on (the 0-3
+  // vectors before it go last): every wave's 1 KiB load covers whole sectors.
+  uint32_t npre = a.align64 ? (uint32_t)((-reinterpret_cast<uintptr_t>(a.frames + base)) & 63u) >> 4 : 0u;
+  if (npre > nvec) npre = nvec;
   for (uint32_t v0 = tid; v0 < nvec; v0 += 8u * kBlock) {
     u32x4 r[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const uint32_t v = v0 + (uint32_t)u * kBlock;
-      if (v < nvec) r[u] = load16_guarded(a.frames, base + 16ull * v, total);
+      uint32_t v = v0 + (uint32_t)u * kBlock + npre;
+      v = v < nvec ? v : v - nvec;
+      if (v0 + (uint32_t)u * kBlock < nvec) r[u] = load16_guarded(a.frames, base + 16ull * v, total);
     }
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
-      const uint32_t v = v0 + (uint32_t)u * kBlock;
-      if (v < nvec) tile[v] = r[u];
+      uint32_t v = v0 + (uint32_t)u * kBlock + npre;
+      v = v < nvec ? v : v - nvec;
+      if (v0 + (uint32_t)u * kBlock < nvec) tile[v] = r[u];
     }
   }
   __syncthreads();
@@ -230,15 +236,28 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
     // store it as one stream, lane t taking vectors t, t+256, ... so every
     // wave-instruction writes 1 KiB contiguous.  Vector j is vector j % V of
     // packet j / V, tracked incrementally (no per-vector division).
+    // From the first 64-B boundary on, as phase 1 (the wrapped tail is
+    // re-derived by one division).
     const uint32_t nv = Tv * V;
     const uint32_t dq = kBlock / V, dv = kBlock % V;
-    uint32_t qj = tid / V, vj = tid - qj * V;
     u32x4* dst = reinterpret_cast<u32x4*>(a.payload_out + p0 * (uint64_t)L);
-    for (uint32_t j = tid; j < nv; j += kBlock) {
+    uint32_t jpre = a.align64 ? (uint32_t)((-(reinterpret_cast<uintptr_t>(dst))) & 63u) >> 4 : 0u;
+    if (jpre > nv) jpre = nv;
+    uint32_t j = tid + jpre;
+    if (j >= nv) j -= nv;
+    uint32_t qj = j / V, vj = j - qj * V;
+    for (uint32_t k = tid; k < nv; k += kBlock) {
       __builtin_nontemporal_store(window16_dw(dw, qj * F + H + 16u * vj), dst + j);
-      qj += dq;
-      vj += dv;
-      if (vj >= V) { vj -= V; ++qj; }
+      j += kBlock;
+      if (j >= nv) {
+        j -= nv;
+        qj = j / V;
+        vj = j - qj * V;
+      } else {
+        qj += dq;
+        vj += dv;
+        if (vj >= V) { vj -= V; ++qj; }
+      }
     }
   }
   for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);

@@ -141,13 +141,20 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   unsigned char* out = a.frames + p0 * (uint64_t)F;
   const uint32_t lead = (uint32_t)(-(uintptr_t)out) & 15u;  // bytes before the first aligned chunk
   const uint32_t nfull = nbytes > lead ? (nbytes - lead) >> 4 : 0u;
+  // Full chunks are dealt from the first 64-B boundary on (the 0-3 chunks
+  // before it go last), so each wave's 1 KiB store covers whole 64-B sectors
+  // instead of splitting one at each end with the next wave.
+  uint32_t npre = a.out_align64 ? ((uint32_t)(-(uintptr_t)out) & 63u) >> 4 : 0u;
+  if (npre > nfull) npre = nfull;
   const uint32_t* pay_dw = reinterpret_cast<const uint32_t*>(lds_pay);
-  // unit k < nfull: full chunk at tile offset lead + 16k; the two units after
-  // that are the partial head [0, lead) and tail [lead + 16*nfull, nbytes).
+  // unit k < nfull: full chunk i = (k + npre) mod nfull at tile offset
+  // lead + 16i; the two units after that are the partial head [0, lead) and
+  // tail [lead + 16*nfull, nbytes).
   for (uint32_t k = tid; k < nfull + 2u; k += BLOCK) {
     uint32_t x, lo_b, hi_b;  // tile offset of chunk byte 0; owned byte range [lo_b, hi_b)
     if (k < nfull) {
-      x = lead + 16u * k; lo_b = 0; hi_b = 16;
+      const uint32_t i = k + npre < nfull ? k + npre : k + npre - nfull;
+      x = lead + 16u * i; lo_b = 0; hi_b = 16;
     } else if (k == nfull) {
       x = 0; lo_b = 0; hi_b = lead < nbytes ? lead : nbytes;
     } else {

@@ -23,6 +23,7 @@ struct EncodeTileArgs {
   uint32_t ablate;      // diagnostics only (wrong output): 1 no LDS sum pass, 2 plain phase-2
                         // LDS reads, 4 no header-table loads
   uint64_t invV;        // ceil(2^32 / (L / 16)) for exact v / V (stream kernel)
+  uint32_t out_align64; // phase 2 deals full chunks from the tile's first 64-B boundary
 };
 
 struct DecodeArgs {
@@ -37,6 +38,7 @@ struct DecodeArgs {
   uint64_t n;
   uint32_t F;               // frame bytes
   uint32_t glog;            // log2(lanes per packet)
+  uint32_t align64;         // tile kernel: wave loads/stores start on 64-B sector boundaries
 };
 
 struct SynthArgs {
@@ -77,6 +79,7 @@ struct VarlenArgs {
   uint32_t tile_T;
   uint32_t tile_glog;
   uint32_t tile_cap;
+  uint32_t align64;               // tile kernel: wave stores start on 64-B sector boundaries
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -129,6 +132,12 @@ struct Tuning {
   int encode_stream = 0;  // register-streamed encode (no LDS tile); 0 = LDS tile kernel
   int encode_stream_T = 0;  // stream kernel packets per workgroup; 0 = automatic
   int encode_stream_R = 2;  // stream kernel rounds of loads in flight per lane (1, 2, 4)
+  // Wave loads/stores of the tile kernels start on a 64-B sector boundary
+  // (1) or on the first 16-B one (0).  -1 = automatic: on for encode tiles
+  // over 16 KiB of payload (1M x 1472 B: 0.516 vs 0.533 ms), off elsewhere,
+  // where it measured 1-3% slower (decode, L = 1024 encode, varlen;
+  // profiles/r01/sweeps/align64.json).
+  int out_align64 = -1;
   int host_slots = 3;     // *_host pipeline: device staging slots (2..8)
   int host_stage_mb = 128;  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
 };

@@ -320,13 +320,18 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_tile_kernel(VarlenArgs a
   // ---- phase 2: aligned 16-B output chunks ---------------------------------
   unsigned char* out = a.frames + fo0;
   const uint32_t nfull = nbytes > lead ? (nbytes - lead) >> 4 : 0u;
+  // full chunks dealt from the first 64-B boundary on (whole sectors per wave store)
+  uint32_t npre = a.align64 ? ((uint32_t)(-reinterpret_cast<uintptr_t>(out)) & 63u) >> 4 : 0u;
+  if (npre > nfull) npre = nfull;
   const uint32_t* pay_dw = reinterpret_cast<const uint32_t*>(lds_pay);
-  // unit k < nfull: full chunk at tile offset lead + 16k; then the partial head
-  // [0, lead) and tail [lead + 16*nfull, nbytes), written bytewise.
+  // unit k < nfull: full chunk i = (k + npre) mod nfull at tile offset
+  // lead + 16i; then the partial head [0, lead) and tail [lead + 16*nfull,
+  // nbytes), written bytewise.
   for (uint32_t k = tid; k < nfull + 2u; k += kBlock) {
     uint32_t x, hi_b, r;
     if (k < nfull) {
-      x = lead + 16u * k; hi_b = 16u; r = lds_map[k];
+      const uint32_t i = k + npre < nfull ? k + npre : k + npre - nfull;
+      x = lead + 16u * i; hi_b = 16u; r = lds_map[i];
     } else if (k == nfull) {
       x = 0; hi_b = lead < nbytes ? lead : nbytes; r = 0;
     } else {

@@ -231,21 +231,23 @@ def test_decode_paths_agree(cuda, L):
     fr[17, 9] ^= 0x40  # one corrupted frame
     want = codec_np.decode(fr, 7)
     results = []
-    for verify_tile, copy_tile in ((1, 1), (0, 0)):
+    for verify_tile, copy_tile, align in ((1, 1, -1), (1, 1, 1), (0, 0, -1)):
         lib.rudpx_tune(12, verify_tile)
         lib.rudpx_tune(11, copy_tile)
+        lib.rudpx_tune(23, align)  # tile loads/stores from a 64-B boundary
         try:
             for copy in (False, True):
                 d = batch.unpack_batch(dev(fr, cuda), 7, copy_payload=copy)
                 got = [host(x) for x in (d.seq, d.ack, d.flags, d.ok, d.csum)]
                 for g, w in zip(got, want[:5]):
-                    assert np.array_equal(g, w), (L, verify_tile, copy)
+                    assert np.array_equal(g, w), (L, verify_tile, copy, align)
                 if copy:
                     assert np.array_equal(host(d.payload), fr[:, 7:])
                 results.append(got)
         finally:
             lib.rudpx_tune(12, 1)
             lib.rudpx_tune(11, 1)
+            lib.rudpx_tune(23, -1)
     assert host(d.ok)[17] == 0
 
 
@@ -274,6 +276,38 @@ def test_encode_tile_sizes_agree(cuda, L):
                     lib.rudpx_tune(6, -1)
                 assert np.array_equal(fr, want_fr), (L, n, layout, block, tile, per_cu)
                 assert np.array_equal(cs, want_cs), (L, n, layout, block, tile, per_cu)
+
+
+@pytest.mark.parametrize("L", [16, 48, 64, 1024, 1472, 4096])
+def test_encode_align64_vs_oracle(cuda, L):
+    """Encode tile kernels dealing wave stores from the first 64-B boundary
+    (rudpx_tune 23 = 1) or the first 16-B one (0) give the oracle's frames,
+    fixed-length and varlen, every tile size."""
+    import ctypes
+    import torch
+    from rudp import _native
+    lib = _native.lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    for n in (1, 5, 16, 17, 257, 1031):
+        seq, ack, flags, pay = synth.synth(0x55 + L, n, n, L, ascii=False)
+        for layout in (5, 7):
+            want_fr, want_cs = codec_np.encode(seq, ack, flags, pay, layout)
+            tab = (dev(seq, cuda), dev(ack, cuda), dev(flags, cuda))
+            lens = torch.full((n,), L, dtype=torch.int32, device=cuda)
+            for align in (1, 0):
+                for tile in (0, 4, 8, 32):
+                    old = (lib.rudpx_tune(23, align), lib.rudpx_tune(2, tile))
+                    try:
+                        fr, cs = gpu_encode(cuda, seq, ack, flags, pay, layout)
+                        v = batch.pack_batch_varlen(tab, dev(pay.reshape(-1), cuda), lens, layout,
+                                                    want_csum=True)
+                    finally:
+                        lib.rudpx_tune(23, old[0])
+                        lib.rudpx_tune(2, old[1])
+                    assert np.array_equal(fr, want_fr), (L, n, layout, align, tile)
+                    assert np.array_equal(cs, want_cs), (L, n, layout, align, tile)
+                    assert np.array_equal(host(v.frames), want_fr.reshape(-1)), (L, n, layout, align)
+                    assert np.array_equal(host(v.csum), want_cs), (L, n, layout, align)
 
 
 @pytest.mark.parametrize("L", [16, 32, 48, 64, 80, 128, 1008, 1024, 1472, 2048, 4096])

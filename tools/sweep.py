@@ -120,6 +120,62 @@ def encode_sweep(reps):
     return out
 
 
+def align_sweep(reps):
+    """Encode tile kernel with phase-2 wave stores on 64-B sector boundaries (key 23) or not."""
+    out = {}
+    dev = torch.device("cuda", 0)
+    for L in (1472, 1024, 64):
+        n = 1 << 20
+        nsets = 1 if L > 512 else 7
+        sets = []
+        for _ in range(nsets):
+            tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
+            sets.append((tab, pay, torch.empty((n, L + 7), dtype=torch.uint8, device=dev)))
+        it = [0]
+
+        def run():
+            tab, pay, fr = sets[it[0] % nsets]
+            it[0] += 1
+            batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
+        pay_out = torch.empty((n, L), dtype=torch.uint8, device=dev)
+        o16 = torch.empty(n, dtype=torch.uint16, device=dev)
+        o8 = torch.empty(n, dtype=torch.uint8, device=dev)
+        for tab, pay, fr in sets:
+            batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
+
+        def verify():
+            fr = sets[it[0] % nsets][2]
+            it[0] += 1
+            batch.unpack_batch(fr, 7)
+
+        def copyout():
+            fr = sets[it[0] % nsets][2]
+            it[0] += 1
+            _native.check(lib.rudp_decode(fr.data_ptr(), None, L + 7, n, None, o16.data_ptr(),
+                                          o16.data_ptr(), o8.data_ptr(), o8.data_ptr(), None,
+                                          pay_out.data_ptr(), 7, 0, torch.cuda.current_stream().cuda_stream))
+        lens = torch.full((n,), L, dtype=torch.int32, device=dev)
+
+        def venc():
+            tab, pay, _ = sets[it[0] % nsets]
+            it[0] += 1
+            batch.pack_batch_varlen(tab, pay.view(-1), lens, 7)
+        algs = {"encode": n * (2 * L + 12), "verify": n * (L + 13), "copyout": n * (2 * L + 13),
+                "varlen_encode": n * (2 * L + 24)}
+        variants = {}
+        for op, fn in (("encode", run), ("verify", verify), ("copyout", copyout), ("varlen_encode", venc)):
+            variants[f"L{L}_{op}_align64"] = (lambda: lib.rudpx_tune(23, 1), fn)
+            variants[f"L{L}_{op}_align16"] = (lambda: lib.rudpx_tune(23, 0), fn)
+        res = interleaved(variants, reps)
+        lib.rudpx_tune(23, -1)
+        for k, ms in res.items():
+            alg = algs[k.split("_", 1)[1].rsplit("_", 1)[0]]
+            out[k] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0}
+        del sets
+        torch.cuda.empty_cache()
+    return out
+
+
 def stream_sweep(reps):
     """Register-streamed encode (rudpx_tune 20-22) against the LDS-tile encode."""
     out = {}
@@ -412,7 +468,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--L", type=int, default=1472, help="payload length for --only ablate")
-    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "stream"])
+    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "stream", "align"])
     ap.add_argument("--blocks", type=str, default="", help="encode sweep: workgroup sizes, e.g. 256,512,1024")
     ap.add_argument("--encode-L", type=str, default="", help="encode sweep: payload lengths, e.g. 1472")
     ap.add_argument("--ablate", action="store_true", help="stream sweep: add stage ablations")
@@ -432,6 +488,8 @@ def main():
         result["utf8"] = utf8_sweep(args.reps)
     if args.only == "varlen":
         result["varlen"] = varlen_sweep(args.reps)
+    if args.only == "align":
+        result["align"] = align_sweep(args.reps)
     if args.only == "stream":
         result["stream"] = stream_sweep(args.reps)
     if args.only == "varlen_enc":
