@@ -4,8 +4,8 @@ Counterpart of the reference's utils/reliableUDP.py (class ReliableUDP,
 :8-202), which is the only production caller of utils/packet.py.  It is
 rewritten here because the reference file does not parse below Python 3.12
 (PEP 701 f-string at :50).  It stays scalar Python, like the reference: one
-character per datagram (:11), so every frame is 5-6 bytes and goes through
-the host-side drop-in rudp.packet.Packet, never the GPU.
+character per datagram (:11), so every frame is 5-9 bytes and by default goes
+through the host-side drop-in rudp.packet.Packet.
 
 Same public surface: ReliableUDP(timeout).create() / bind(ip, port) /
 send(message, ip, port) / recv() / close() / flush_recv_buffer().  Same
@@ -13,6 +13,14 @@ protocol and wire bytes: the states of the reference's FSM tables (:96-107 and
 :186-199) are the methods below, with the same transitions, retry counts,
 timeouts and header values.  The config-1 wire trace (tests/golden/
 wire_trace.json, captured from the reference) is reproduced byte for byte.
+
+``ReliableUDP(codec_device="cuda:0")`` moves the sender's data frames
+(:53-61) onto the GPU codec: every frame send() can emit is known once the
+ISN is drawn (pointer p: seq = ISN + p, ack 0, SYN at p = 0, FIN from the last
+character on, payload message[p]), so send() frames the whole message in one
+pack_batch_varlen launch (rudp5, the reference's 5-byte layout) and each
+SEND_DATA step, retransmissions included, sends row p of that table.  The
+bytes on the wire are the same.
 """
 from __future__ import annotations
 
@@ -29,7 +37,8 @@ class ReliableUDP:
     RETRIES = 20            # :10
     PAYLOAD_SIZE = 1        # :11
 
-    def __init__(self, timeout=1, isn_source: Optional[Callable[[], int]] = None):
+    def __init__(self, timeout=1, isn_source: Optional[Callable[[], int]] = None,
+                 codec_device: Optional[str] = None):
         self.socket: socket
         self.message_pointer = 0
         self.random_number = 0
@@ -38,6 +47,8 @@ class ReliableUDP:
         self.retransmission_timeout = timeout
         # the ISN draw of :41; injectable so a test can pin the wire trace
         self._isn = isn_source or (lambda: random.randint(1, 5000))
+        self._codec_device = codec_device
+        self._frames: Optional[tuple] = None  # (bytes, offsets) of the pre-framed message
 
     def create(self):
         self.socket = socket(AF_INET, SOCK_DGRAM)
@@ -65,6 +76,7 @@ class ReliableUDP:
         self.flush_recv_buffer()
         self.message_pointer = 0
         self.random_number = self._isn()
+        self._frames = self._frame_message(message) if self._codec_device else None
         dest = (str(ip), port)
         state, args = "SEND_DATA", (ReliableUDP.RETRIES,)
         while True:
@@ -80,6 +92,23 @@ class ReliableUDP:
             state, args = step[0], step[1:]
         self.flush_recv_buffer()
 
+    def _frame_message(self, message):
+        """Frames for pointer values 0..len(message), in one GPU launch."""
+        import numpy as np
+        import torch
+        from . import batch
+        dev = torch.device(self._codec_device)
+        n = len(message) + 1  # p = len(message): the header-only FIN frame (empty payload)
+        p = np.arange(n, dtype=np.int64)
+        seq = ((self.random_number + p) & 0xFFFF).astype(np.uint16)
+        flags = np.where(p == 0, 0x80, 0) | np.where(p >= len(message) - 1, 0x20, 0)
+        lens = np.array([len(c.encode()) for c in message] + [0], dtype=np.int32)
+        payload = np.frombuffer(bytearray(message.encode()), dtype=np.uint8)
+        t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
+        res = batch.pack_batch_varlen((t(seq), t(np.zeros(n, np.uint16)), t(flags.astype(np.uint8))),
+                                      t(payload), t(lens), "rudp5", want_csum=False)
+        return res.frames.cpu().numpy().tobytes(), res.frame_off.cpu().tolist()
+
     def _send_data(self, message, dest, retries):
         # :43-62
         end = min(self.message_pointer + ReliableUDP.PAYLOAD_SIZE, len(message))
@@ -93,15 +122,20 @@ class ReliableUDP:
                       f"seconds ({ReliableUDP.RETRIES} retries * {self.retransmission_timeout} "
                       f"second timeout) {tail} \033[0m")
             return None
-        p = Packet()
-        p.set_header_field("seq_num", str(self.message_pointer + self.random_number), base=10)
-        p.set_header_field("ack_num", "0", base=10)
-        if is_first:
-            p.set_header_field("syn", "1", base=2)
-        if is_last:
-            p.set_header_field("fin", "1", base=2)
-        p.set_payload(message[self.message_pointer:end])
-        self.socket.sendto(p.to_byte(), dest)
+        if self._frames is not None:
+            data, off = self._frames
+            frame = data[off[self.message_pointer]:off[self.message_pointer + 1]]
+        else:
+            p = Packet()
+            p.set_header_field("seq_num", str(self.message_pointer + self.random_number), base=10)
+            p.set_header_field("ack_num", "0", base=10)
+            if is_first:
+                p.set_header_field("syn", "1", base=2)
+            if is_last:
+                p.set_header_field("fin", "1", base=2)
+            p.set_payload(message[self.message_pointer:end])
+            frame = p.to_byte()
+        self.socket.sendto(frame, dest)
         return ("WAIT_ACK", is_last, end - self.message_pointer, retries - 1)
 
     def _wait_ack(self, message, is_last, payload_length, retries):

@@ -54,7 +54,7 @@ class Relay(threading.Thread):
             self.sock.sendto(data, self.server if direction == "c2s" else self.client)
 
 
-def run_transfer(message, isn, drop=None, client_timeout=1):
+def run_transfer(message, isn, drop=None, client_timeout=1, codec_device=None):
     server = ReliableUDP().create()
     server.bind("127.0.0.1", 0)
     sport = server.socket.getsockname()[1]
@@ -64,7 +64,8 @@ def run_transfer(message, isn, drop=None, client_timeout=1):
     t = threading.Thread(target=lambda: got.setdefault("msg", server.recv()), daemon=True)
     t.start()
     time.sleep(0.05)  # recv() flushes its socket on entry (reliableUDP.py:112)
-    client = ReliableUDP(timeout=client_timeout, isn_source=lambda: isn).create()
+    client = ReliableUDP(timeout=client_timeout, isn_source=lambda: isn,
+                         codec_device=codec_device).create()
     t0 = time.perf_counter()
     client.send(message, "127.0.0.1", relay.port)
     t.join(timeout=30)
@@ -107,3 +108,70 @@ def test_config1_messages(message):
     msg, _, _ = run_transfer(message, isn=4999, client_timeout=0.2)
     # the reference server returns what it assembled; an empty message carries no payload
     assert msg == message
+
+
+@pytest.mark.gpu
+def test_config1_gpu_framed_sender_matches_reference_trace(wire_trace):
+    """The sender's data frames come from one GPU varlen launch; the wire
+    trace is still the reference's, byte for byte."""
+    msg, relay, _ = run_transfer(wire_trace["message"], wire_trace["isn"], codec_device="cuda:0")
+    assert msg == wire_trace["message"]
+    assert [d.hex() for d in relay.log["c2s"]] == wire_trace["client_to_server"]
+    assert [d.hex() for d in relay.log["s2c"]] == wire_trace["server_to_client"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("message", ["", "x", "héllo ✓ 𝄞", "a" * 300])
+def test_config1_gpu_framed_sender_messages(message):
+    """Multi-byte UTF-8 and the empty message, with drops forcing
+    retransmissions of GPU-framed rows."""
+    for isn in (1, 4999):
+        dropped = set()
+
+        def drop(direction, index):
+            if index % 7 == 3 and (direction, index) not in dropped:
+                dropped.add((direction, index))
+                return True
+            return False
+        msg, relay, _ = run_transfer(message, isn=isn, drop=drop, client_timeout=0.1,
+                                     codec_device="cuda:0")
+        assert msg == message
+        # every data frame on the wire equals the scalar drop-in's frame for its pointer
+        from rudp.packet import Packet
+        for frame in relay.log["c2s"]:
+            p = Packet(frame)
+            seq = int(p.get_header_field("seq_num", base=10))
+            ptr = (seq - isn) % 65536
+            if p.get_header_field("ack", base=2) == "1":
+                continue  # the final ACK (:87-93) is scalar
+            q = Packet()
+            q.set_header_field("seq_num", str(isn + ptr), base=10)
+            q.set_header_field("ack_num", "0", base=10)
+            if ptr == 0:
+                q.set_header_field("syn", "1", base=2)
+            if ptr >= len(message) - 1:
+                q.set_header_field("fin", "1", base=2)
+            q.set_payload(message[ptr:ptr + 1])
+            assert frame == q.to_byte(), (message, isn, ptr)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("isn", [1, 5000, 65500])
+def test_gpu_frame_table_rows_equal_scalar_packets(isn):
+    """Row p of the GPU frame table == the scalar Packet the reference builds
+    for pointer p (utils/reliableUDP.py:53-61), seq wrapping past 2^16."""
+    message = "ab✓𝄞" + "z" * 100
+    r = ReliableUDP(isn_source=lambda: isn, codec_device="cuda:0")
+    r.random_number = isn
+    data, off = r._frame_message(message)
+    assert len(off) == len(message) + 2
+    for ptr in range(len(message) + 1):
+        q = Packet()
+        q.set_header_field("seq_num", str(isn + ptr), base=10)
+        q.set_header_field("ack_num", "0", base=10)
+        if ptr == 0:
+            q.set_header_field("syn", "1", base=2)
+        if ptr >= len(message) - 1:
+            q.set_header_field("fin", "1", base=2)
+        q.set_payload(message[ptr:ptr + 1])
+        assert data[off[ptr]:off[ptr + 1]] == q.to_byte(), ptr
