@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RUDP_ABI_VERSION 2
+#define RUDP_ABI_VERSION 3
 
 /* Frame layouts: the value is the header length in bytes. */
 #define RUDP_LAYOUT_RUDP5 5 /* reference-exact 5-byte header, checksum sideband */
@@ -130,6 +130,22 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
  */
 int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_frame_off,
                        uint16_t* d_csum_or_null, int layout, int device, void* hip_stream);
+
+/*
+ * Bounds of a variable-length batch, computed on the device (argument checks
+ * the varlen entry points need before they can size or trust a buffer; the
+ * reference has no batch and so no counterpart).  Synchronous on hip_stream.
+ * rudp_varlen_bounds: h_out[0..4] = min len, max len, sum of len, min
+ * payload_off, max(payload_off + len); without offsets [3] = 0, [4] = sum.
+ * len[] is read as u32 (a negative int32 length shows as > 65535).
+ * rudp_frame_off_bounds: over d_frame_off[0..n], h_out[0..2] = min, max and
+ * the number of i < n with d_frame_off[i+1] < d_frame_off[i] (0 = valid
+ * offsets for rudp_decode; min and max are then the first and last).
+ */
+int rudp_varlen_bounds(const uint32_t* d_len, const int64_t* d_payload_off_or_null, uint64_t n,
+                       int64_t* h_out, int device, void* hip_stream);
+int rudp_frame_off_bounds(const int64_t* d_frame_off, uint64_t n, int64_t* h_out, int device,
+                          void* hip_stream);
 
 /*
  * Strict UTF-8 check of each frame's payload: d_valid[i] = 1 when

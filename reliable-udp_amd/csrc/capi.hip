@@ -443,6 +443,40 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
   return 0;
 }
 
+int rudp_varlen_bounds(const uint32_t* d_len, const int64_t* d_payload_off_or_null, uint64_t n,
+                       int64_t* h_out, int device, void* hip_stream) {
+  if (!h_out) return fail(RUDP_EINVAL, "rudp_varlen_bounds: h_out is NULL");
+  for (int i = 0; i < 5; ++i) h_out[i] = 0;
+  if (n == 0) return 0;
+  if (!d_len) return fail(RUDP_EINVAL, "rudp_varlen_bounds: len is NULL");
+  int rc = check_device(device);
+  if (rc) return rc;
+  Bounds b{};
+  rc = compute_bounds(d_len, d_payload_off_or_null, n, false, &b, (hipStream_t)hip_stream);
+  if (rc) return hip_fail((hipError_t)rc, "varlen bounds");
+  h_out[0] = (int64_t)b.min_len;
+  h_out[1] = (int64_t)b.max_len;
+  h_out[2] = (int64_t)b.sum_len;
+  h_out[3] = d_payload_off_or_null ? b.min_off : 0;
+  h_out[4] = d_payload_off_or_null ? b.max_end : (int64_t)b.sum_len;
+  return 0;
+}
+
+int rudp_frame_off_bounds(const int64_t* d_frame_off, uint64_t n, int64_t* h_out, int device,
+                          void* hip_stream) {
+  if (!h_out) return fail(RUDP_EINVAL, "rudp_frame_off_bounds: h_out is NULL");
+  if (!d_frame_off) return fail(RUDP_EINVAL, "rudp_frame_off_bounds: frame_off is NULL");
+  int rc = check_device(device);
+  if (rc) return rc;
+  Bounds b{};
+  rc = compute_bounds(nullptr, d_frame_off, n, true, &b, (hipStream_t)hip_stream);
+  if (rc) return hip_fail((hipError_t)rc, "frame offset bounds");
+  h_out[0] = b.min_off;
+  h_out[1] = b.max_end;
+  h_out[2] = (int64_t)b.n_decreasing;
+  return 0;
+}
+
 int rudp_validate_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
                        uint32_t frame_len, uint64_t n, int layout, uint8_t* d_valid, int device,
                        void* hip_stream) {

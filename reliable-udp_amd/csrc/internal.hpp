@@ -156,6 +156,15 @@ int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream)
 int launch_validate_utf8(const Utf8Args& args, hipStream_t stream);
 int launch_dedup(const DedupArgs& args, hipStream_t stream);
 uint32_t dedup_max_window();
+struct Bounds {
+  uint64_t min_len, max_len, sum_len;
+  int64_t min_off, max_end;
+  uint64_t n_decreasing;
+};
+// Bounds of len[] / payload_off[] (or, offsets_only, of frame_off[0..n]) on
+// `stream`, copied to *host; synchronous (bounds.hip).
+int compute_bounds(const uint32_t* len, const int64_t* off, uint64_t n, bool offsets_only,
+                   Bounds* host, hipStream_t stream);
 int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
                        hipStream_t stream);
 

@@ -20,8 +20,8 @@ CSRC = ROOT / "csrc"
 INCLUDE = ROOT.parent / "include"
 BUILD = ROOT / "build"
 LIB = PKG_DIR / "librudp.so"
-SOURCES = ("encode.hip", "decode.hip", "synth.hip", "varlen.hip", "dedup.hip", "capi.hip", "tuning.hip",
-           "netio.cpp")
+SOURCES = ("encode.hip", "decode.hip", "synth.hip", "varlen.hip", "dedup.hip", "bounds.hip", "capi.hip",
+           "tuning.hip", "netio.cpp")
 ARCH = "gfx950"
 
 

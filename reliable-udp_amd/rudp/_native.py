@@ -18,14 +18,14 @@ LAYOUT_RUDP5 = 5
 LAYOUT_RUDP7 = 7
 OK_BAD_CSUM, OK_GOOD, OK_SHORT, OK_UNVERIFIED = 0, 1, 2, 3
 EINVAL, ENOMEM, ENOTSUP, EHIP_BASE = -22, -12, -95, -1000
-ABI_VERSION = 2
+ABI_VERSION = 3
 
 # Every symbol include/rudp.h declares (checked by tests/test_abi.py).
 EXPORTS = (
     "rudp_encode", "rudp_decode", "rudp_encode_host", "rudp_decode_host",
     "rudp_synth", "rudp_device_count", "rudp_last_error", "rudp_abi_version",
     "rudp_encode_varlen", "rudp_validate_utf8", "rudp_dedup_window",
-    "rudp_udp_recv_batch", "rudp_udp_send_batch",
+    "rudp_udp_recv_batch", "rudp_udp_send_batch", "rudp_varlen_bounds", "rudp_frame_off_bounds",
 )
 
 
@@ -67,6 +67,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rudp_dedup_window": [P, P, U32, U64, U32, P, I, P],
         "rudp_udp_recv_batch": [I, P, U64, U32, U32, P, I],
         "rudp_udp_send_batch": [I, P, P, U64, ctypes.c_char_p, ctypes.c_uint16],
+        "rudp_varlen_bounds": [P, P, U64, P, I, P],
+        "rudp_frame_off_bounds": [P, U64, P, I, P],
         "rudp_device_count": [ctypes.POINTER(ctypes.c_int)],
         "rudp_abi_version": [],
     }

@@ -334,19 +334,17 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
         _dev_check(t, name, dt, 1, dev)
         if t.shape[0] != n:
             raise ValueError(f"{name} has {t.shape[0]} entries for {n} packets")
-    lens64 = lengths.to(torch.int64)
     if payload_off is not None:
         _int_tensor(payload_off, "payload_off", dev, n, dtypes=(torch.int64,))
-    # one device->host read for every bound
+    # every bound in one device pass and one 40-byte read (rudp_varlen_bounds);
+    # lengths are read as u32, so a negative int32 shows up as > 65535
     lmin = lmax = lsum = omin = oend = 0
     if n:
-        stats = [lens64.min(), lens64.max(), lens64.sum()]
-        if payload_off is not None:
-            stats += [payload_off.min(), (payload_off + lens64).max()]
-        vals = torch.stack(stats).tolist()
-        lmin, lmax, lsum = vals[:3]
-        if payload_off is not None:
-            omin, oend = vals[3:]
+        out = (ctypes.c_int64 * 5)()
+        _native.check(_native.lib().rudp_varlen_bounds(
+            lengths.data_ptr(), payload_off.data_ptr() if payload_off is not None else None, n, out,
+            dev.index or 0, _stream_ptr(stream, dev)))
+        lmin, lmax, lsum, omin, oend = list(out)
     if lmin < 0 or lmax > 65535:
         raise ValueError("lengths must lie in [0, 65535]")
     if payload_off is None:
@@ -375,14 +373,15 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
     return VarlenFrames(frames, frame_off, csum)
 
 
-def _check_offsets(frames, frame_off) -> int:
+def _check_offsets(frames, frame_off, stream=None) -> int:
     """Validate offsets (one device->host read); returns the mean frame length."""
-    import torch
     n = frame_off.shape[0] - 1
     if n < 1:
         return 0
-    bad = (frame_off[1:] < frame_off[:-1]).any().to(torch.int64)
-    first, last, nbad = torch.stack([frame_off[0], frame_off[-1], bad]).tolist()
+    out = (ctypes.c_int64 * 3)()  # min, max, decreasing pairs (rudp_frame_off_bounds)
+    _native.check(_native.lib().rudp_frame_off_bounds(
+        frame_off.data_ptr(), n, out, frame_off.device.index or 0, _stream_ptr(stream, frame_off.device)))
+    first, last, nbad = list(out)
     if first < 0 or nbad or last > frames.numel():
         raise ValueError("frame_off must be non-decreasing offsets inside frames")
     return min((last - first) // n, 0xFFFFFFFF)
@@ -405,7 +404,7 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
     n = frame_off.shape[0] - 1
     if n < 0:
         raise ValueError("frame_off needs N + 1 entries")
-    mean_len = _check_offsets(frames, frame_off)
+    mean_len = _check_offsets(frames, frame_off, stream)
     if csum is not None:
         _dev_check(csum, "csum", torch.uint16, 1, dev)
         if csum.shape[0] != n:
@@ -441,7 +440,7 @@ def validate_utf8(frames, layout: Union[str, int] = "rudp7", *, frame_off=None, 
         _dev_check(frames, "frames", torch.uint8, 1, dev)
         _int_tensor(frame_off, "frame_off", dev, dtypes=(torch.int64,))
         n = frame_off.shape[0] - 1
-        F = _check_offsets(frames, frame_off)  # mean frame length: a lanes-per-frame hint
+        F = _check_offsets(frames, frame_off, stream)  # mean frame length: a lanes-per-frame hint
         off_ptr = frame_off.data_ptr()
     valid = torch.empty((n,), dtype=torch.uint8, device=dev)
     if n:
@@ -471,7 +470,7 @@ def detect_retransmissions(frames, *, frame_off=None, window: int = PROXY_MAX_ME
     else:
         _dev_check(frames, "frames", torch.uint8, 1, dev)
         _int_tensor(frame_off, "frame_off", dev, dtypes=(torch.int64,))
-        _check_offsets(frames, frame_off)
+        _check_offsets(frames, frame_off, stream)
         n, F = frame_off.shape[0] - 1, 0
         off_ptr = frame_off.data_ptr()
     dup = torch.empty((n,), dtype=torch.uint8, device=dev)

@@ -59,6 +59,11 @@ def test_argument_errors_before_device():
                                   None) == _native.EINVAL
     assert b"len" in lib.rudp_last_error()
     assert lib.rudp_validate_utf8(None, None, 10, 1, 7, None, 0, None) == _native.EINVAL
+    out5 = (ctypes.c_int64 * 5)(9, 9, 9, 9, 9)
+    assert lib.rudp_varlen_bounds(None, None, 0, out5, 0, None) == 0 and list(out5) == [0] * 5
+    assert lib.rudp_varlen_bounds(None, None, 4, out5, 0, None) == _native.EINVAL
+    assert lib.rudp_varlen_bounds(None, None, 4, None, 0, None) == _native.EINVAL
+    assert lib.rudp_frame_off_bounds(None, 4, out5, 0, None) == _native.EINVAL
     # empty batches are a successful no-op, no device needed
     assert lib.rudp_encode(ctypes.byref(_native.RudpBatch(n=0)), None, None, 5, 0, None) == 0
     assert lib.rudp_synth(1, 0, 0, 16, 1, None, None, None, None, 0, None) == 0

@@ -397,3 +397,37 @@ def test_varlen_encode_tile_kernel_vs_oracle(cuda, dist, layout):
                 assert np.array_equal(host(csum), want_cs), (dist, layout, tile, hint)
     finally:
         lib.rudpx_tune(16, 1)
+
+
+@pytest.mark.parametrize("n", [1, 2, 255, 256, 257, 4099, 1 << 20])
+def test_device_bounds_match_numpy(cuda, n):
+    """rudp_varlen_bounds / rudp_frame_off_bounds == numpy on the same arrays
+    (negative int32 lengths show as > 65535; decreasing offsets counted)."""
+    import ctypes
+    import torch
+    from rudp import _native
+    lib = _native.lib()
+    rng = np.random.default_rng(n)
+    lens = rng.integers(0, 70000, n).astype(np.int32)
+    lens[rng.integers(n)] = -3
+    off = rng.integers(-5, 1 << 40, n).astype(np.int64)
+    stream = torch.cuda.current_stream().cuda_stream
+    out = (ctypes.c_int64 * 5)()
+    d_lens, d_off = dev(lens, cuda), dev(off, cuda)  # keep them alive across the calls
+    _native.check(lib.rudp_varlen_bounds(d_lens.data_ptr(), d_off.data_ptr(), n, out, 0, stream))
+    u = lens.astype(np.uint32).astype(np.int64)
+    assert list(out) == [u.min(), u.max(), u.sum(), off.min(), (off + u).max()]
+    _native.check(lib.rudp_varlen_bounds(d_lens.data_ptr(), None, n, out, 0, stream))
+    assert list(out) == [u.min(), u.max(), u.sum(), 0, u.sum()]
+    fo = np.concatenate([[0], np.cumsum(rng.integers(0, 9, n))]).astype(np.int64)
+    out3 = (ctypes.c_int64 * 3)()
+    d_fo = dev(fo, cuda)
+    _native.check(lib.rudp_frame_off_bounds(d_fo.data_ptr(), n, out3, 0, stream))
+    assert list(out3) == [fo[0], fo[-1], 0]
+    bad = fo.copy()
+    k = rng.integers(1, n + 1, 3)
+    bad[k] -= 1000
+    want_bad = int((bad[1:] < bad[:-1]).sum())
+    d_bad = dev(bad, cuda)
+    _native.check(lib.rudp_frame_off_bounds(d_bad.data_ptr(), n, out3, 0, stream))
+    assert list(out3) == [bad.min(), bad.max(), want_bad]
