@@ -71,6 +71,28 @@ int check_device(int device) {
   return 0;
 }
 
+// Makes `device` the calling thread's HIP device for one entry point and
+// gives the caller its own device back on return: a caller such as torch
+// keeps its current device, whatever device a batch names.
+class DeviceScope {
+ public:
+  DeviceScope() = default;
+  DeviceScope(const DeviceScope&) = delete;
+  DeviceScope& operator=(const DeviceScope&) = delete;
+  ~DeviceScope() {
+    if (prev_ >= 0 && prev_ != cur_) (void)hipSetDevice(prev_);
+  }
+  int set(int device) {
+    if (hipGetDevice(&prev_) != hipSuccess) prev_ = -1;
+    const int rc = check_device(device);
+    if (rc == 0) cur_ = device;
+    return rc;
+  }
+
+ private:
+  int prev_ = -1, cur_ = -1;
+};
+
 EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t* csum, int layout) {
   EncodeTileArgs a{};
   a.payload = in->payload;
@@ -265,7 +287,8 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
   if (n == 0) return 0;
   if (!d_seq || !d_ack || !d_flags || !d_ok)
     return fail(RUDP_EINVAL, "rudp_decode: NULL buffer for a non-empty batch");
-  int rc = check_device(device);
+  DeviceScope dev_scope;
+  int rc = dev_scope.set(device);
   if (rc) return rc;
   VarlenArgs a{};
   a.frames = const_cast<unsigned char*>(d_frames);
@@ -313,7 +336,8 @@ int rudp_encode(const rudp_batch* in, uint8_t* d_frames, uint16_t* d_csum_or_nul
                 int device, void* hip_stream) {
   int rc = validate_batch(in, d_frames, layout);
   if (rc || in->n == 0) return rc;
-  if ((rc = check_device(device))) return rc;
+  DeviceScope dev_scope;
+  if ((rc = dev_scope.set(device))) return rc;
   EncodeTileArgs a = make_encode_args(in, d_frames, d_csum_or_null, layout);
   rc = launch_encode(a, layout, a.T != 0, (hipStream_t)hip_stream);
   if (rc) return hip_fail((hipError_t)rc, "encode launch");
@@ -330,7 +354,8 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, ui
   }
   int rc = validate_decode(d_frames, nullptr, frame_len, n, d_seq, d_ack, d_flags, d_ok, layout);
   if (rc || n == 0) return rc;
-  if ((rc = check_device(device))) return rc;
+  DeviceScope dev_scope;
+  if ((rc = dev_scope.set(device))) return rc;
   DecodeArgs a{};
   a.align64 = tuning().out_align64 == 1 ? 1u : 0u;
   a.frames = d_frames;
@@ -378,7 +403,8 @@ int rudp_synth(uint64_t seed, uint64_t first_index, uint64_t n, uint32_t payload
   if (n == 0) return 0;
   if (!d_seq || !d_ack || !d_flags || (payload_len && !d_payload))
     return fail(RUDP_EINVAL, "rudp_synth: NULL buffer");
-  int rc = check_device(device);
+  DeviceScope dev_scope;
+  int rc = dev_scope.set(device);
   if (rc) return rc;
   SynthArgs a{};
   const uint64_t k0 = stream64(seed, 0), k1 = stream64(seed, 1), k2 = stream64(seed, 2),
@@ -412,7 +438,8 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
     return fail(RUDP_EINVAL, "rudp_encode_varlen: NULL buffer for a non-empty batch");
   if (in->n > 0x7FFFFFFFull)
     return fail(RUDP_EINVAL, "rudp_encode_varlen: at most 2^31-1 packets per call");
-  int rc = check_device(device);
+  DeviceScope dev_scope;
+  int rc = dev_scope.set(device);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)hip_stream;
   rc = scan_frame_offsets(in->len, in->n, (uint32_t)layout, d_frame_off, s);
@@ -449,7 +476,8 @@ int rudp_varlen_bounds(const uint32_t* d_len, const int64_t* d_payload_off_or_nu
   for (int i = 0; i < 5; ++i) h_out[i] = 0;
   if (n == 0) return 0;
   if (!d_len) return fail(RUDP_EINVAL, "rudp_varlen_bounds: len is NULL");
-  int rc = check_device(device);
+  DeviceScope dev_scope;
+  int rc = dev_scope.set(device);
   if (rc) return rc;
   Bounds b{};
   rc = compute_bounds(d_len, d_payload_off_or_null, n, false, &b, (hipStream_t)hip_stream);
@@ -466,7 +494,8 @@ int rudp_frame_off_bounds(const int64_t* d_frame_off, uint64_t n, int64_t* h_out
                           void* hip_stream) {
   if (!h_out) return fail(RUDP_EINVAL, "rudp_frame_off_bounds: h_out is NULL");
   if (!d_frame_off) return fail(RUDP_EINVAL, "rudp_frame_off_bounds: frame_off is NULL");
-  int rc = check_device(device);
+  DeviceScope dev_scope;
+  int rc = dev_scope.set(device);
   if (rc) return rc;
   Bounds b{};
   rc = compute_bounds(nullptr, d_frame_off, n, true, &b, (hipStream_t)hip_stream);
@@ -485,7 +514,8 @@ int rudp_validate_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_n
   if (n == 0) return 0;
   if (!d_valid || (!d_frames && (d_frame_off_or_null || frame_len)))
     return fail(RUDP_EINVAL, "rudp_validate_utf8: NULL buffer for a non-empty batch");
-  int rc = check_device(device);
+  DeviceScope dev_scope;
+  int rc = dev_scope.set(device);
   if (rc) return rc;
   Utf8Args a{};
   a.frames = d_frames;
@@ -507,7 +537,8 @@ int rudp_dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_nu
   if (n == 0) return 0;
   if (!d_dup || (!d_frames && (d_frame_off_or_null || frame_len)))
     return fail(RUDP_EINVAL, "rudp_dedup_window: NULL buffer for a non-empty batch");
-  int rc = check_device(device);
+  DeviceScope dev_scope;
+  int rc = dev_scope.set(device);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)hip_stream;
   DedupArgs a{};
@@ -531,7 +562,8 @@ int rudp_encode_host(const rudp_batch* h_in, uint8_t* h_frames, uint16_t* h_csum
                      int layout, int device) {
   int rc = validate_batch(h_in, h_frames, layout);
   if (rc || h_in->n == 0) return rc;
-  if ((rc = check_device(device))) return rc;
+  DeviceScope dev_scope;
+  if ((rc = dev_scope.set(device))) return rc;
   const uint64_t n = h_in->n;
   const uint64_t L = h_in->payload_len;
   const uint64_t F = L + (uint64_t)layout;
@@ -575,7 +607,8 @@ int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
                      uint8_t* h_payload_out_or_null, int layout, int device) {
   int rc = validate_decode(h_frames, nullptr, frame_len, n, h_seq, h_ack, h_flags, h_ok, layout);
   if (rc || n == 0) return rc;
-  if ((rc = check_device(device))) return rc;
+  DeviceScope dev_scope;
+  if ((rc = dev_scope.set(device))) return rc;
   const uint64_t F = frame_len;
   const uint64_t L = F > (uint64_t)layout ? F - (uint64_t)layout : 0;
   uint8_t* h_pay = L ? h_payload_out_or_null : nullptr;
