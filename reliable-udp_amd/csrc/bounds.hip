@@ -8,6 +8,9 @@
 // it is a grid-stride pass with per-block partials and one combining block
 // that writes the result straight to pinned host memory: 20 us per call with
 // the sync (a single launch whose last block combines measured 34 us).
+#include <mutex>
+#include <vector>
+
 #include "codec_device.hpp"
 #include "internal.hpp"
 
@@ -134,31 +137,49 @@ __global__ void __launch_bounds__(kBlock) bounds_final_kernel(const Bounds* part
   block_combine(b, out);
 }
 
-// Per-thread, per-device scratch: the block partials on the device and the
-// result in pinned host memory the final kernel writes directly (no copy
-// call).  compute_bounds is synchronous, so a thread's scratch is idle again
-// when it returns; other threads have their own.
+// Scratch for one call: the block partials on the device and the result in
+// mapped pinned memory the combining block writes (no copy call).  Kept in a
+// mutex-guarded per-device free list: a call takes a slot and gives it back
+// when it returns (it is synchronous), so slots are bounded by the peak number
+// of concurrent callers and are reused, never freed.
 struct BoundsScratch {
   Bounds* d_partial = nullptr;   // [kBoundsBlocks] block partials
   Bounds* h_result = nullptr;
+  int device = 0;
 };
 
-BoundsScratch* bounds_scratch(int device) {
-  constexpr int kMaxDev = 64;
-  thread_local BoundsScratch s[kMaxDev];
-  if (device < 0 || device >= kMaxDev) return nullptr;
-  BoundsScratch& b = s[device];
-  if (!b.d_partial) {
-    if (hipMalloc(reinterpret_cast<void**>(&b.d_partial), sizeof(Bounds) * kBoundsBlocks) != hipSuccess)
-      return nullptr;
-    if (hipHostMalloc(reinterpret_cast<void**>(&b.h_result), sizeof(Bounds), hipHostMallocMapped) !=
-        hipSuccess) {
-      (void)hipFree(b.d_partial);
-      b.d_partial = nullptr;
-      return nullptr;
+std::mutex g_bounds_mu;
+std::vector<std::vector<BoundsScratch*>> g_bounds_free;
+
+BoundsScratch* bounds_acquire(int device) {
+  {
+    std::lock_guard<std::mutex> lk(g_bounds_mu);
+    if ((int)g_bounds_free.size() <= device) g_bounds_free.resize(device + 1);
+    auto& fl = g_bounds_free[device];
+    if (!fl.empty()) {
+      BoundsScratch* s = fl.back();
+      fl.pop_back();
+      return s;
     }
   }
-  return &b;
+  BoundsScratch* s = new BoundsScratch();
+  s->device = device;
+  if (hipMalloc(reinterpret_cast<void**>(&s->d_partial), sizeof(Bounds) * kBoundsBlocks) != hipSuccess) {
+    delete s;
+    return nullptr;
+  }
+  if (hipHostMalloc(reinterpret_cast<void**>(&s->h_result), sizeof(Bounds), hipHostMallocMapped) !=
+      hipSuccess) {
+    (void)hipFree(s->d_partial);
+    delete s;
+    return nullptr;
+  }
+  return s;
+}
+
+void bounds_release(BoundsScratch* s) {
+  std::lock_guard<std::mutex> lk(g_bounds_mu);
+  g_bounds_free[s->device].push_back(s);
 }
 
 // Runs the pass on `stream` (the current device's) and returns the result in
@@ -168,8 +189,12 @@ int compute_bounds(const uint32_t* len, const int64_t* off, uint64_t n, bool off
   int device = 0;
   hipError_t e = hipGetDevice(&device);
   if (e != hipSuccess) return (int)e;
-  BoundsScratch* s = bounds_scratch(device);
+  BoundsScratch* s = bounds_acquire(device);
   if (!s) return (int)hipErrorOutOfMemory;
+  struct Release {
+    BoundsScratch* s;
+    ~Release() { bounds_release(s); }
+  } release{s};
   const uint64_t items = offsets_only ? n + 1 : n;
   uint64_t want = (items + kBlock * 8 - 1) / (kBlock * 8);  // >= 8 items per thread
   const uint32_t blocks = (uint32_t)(want < 1 ? 1 : want > kBoundsBlocks ? kBoundsBlocks : want);

@@ -431,3 +431,36 @@ def test_device_bounds_match_numpy(cuda, n):
     d_bad = dev(bad, cuda)
     _native.check(lib.rudp_frame_off_bounds(d_bad.data_ptr(), n, out3, 0, stream))
     assert list(out3) == [bad.min(), bad.max(), want_bad]
+
+
+def test_device_bounds_concurrent_callers(cuda):
+    """Eight threads, each on its own stream, take bounds of their own arrays
+    at once (the scratch free list hands each call its own slot)."""
+    import ctypes
+    import threading
+    import torch
+    from rudp import _native
+    lib = _native.lib()
+    rng = np.random.default_rng(11)
+    arrays = [rng.integers(0, 60000, 50000 + 977 * k).astype(np.int32) for k in range(8)]
+    errors = []
+
+    def work(k):
+        try:
+            s = torch.cuda.Stream(device=cuda)
+            with torch.cuda.stream(s):
+                d = dev(arrays[k], cuda)
+                for _ in range(20):
+                    out = (ctypes.c_int64 * 5)()
+                    _native.check(lib.rudp_varlen_bounds(d.data_ptr(), None, d.numel(), out, 0,
+                                                         s.cuda_stream))
+                    a = arrays[k].astype(np.int64)
+                    assert list(out) == [a.min(), a.max(), a.sum(), 0, a.sum()], k
+        except Exception as e:  # noqa: BLE001
+            errors.append(e)
+    threads = [threading.Thread(target=work, args=(k,)) for k in range(8)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors, errors
