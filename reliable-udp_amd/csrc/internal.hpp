@@ -138,6 +138,7 @@ struct Tuning {
   // where it measured 1-3% slower (decode, L = 1024 encode, varlen;
   // profiles/r01/sweeps/align64.json).
   int out_align64 = -1;
+  int varlen_scan = 1;    // frame offsets: 1 = reduce-then-scan (scan.hip), 0 = hipcub
   int host_slots = 3;     // *_host pipeline: device staging slots (2..8)
   int host_stage_mb = 128;  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
 };
@@ -165,6 +166,8 @@ struct Bounds {
 // `stream`, copied to *host; synchronous (bounds.hip).
 int compute_bounds(const uint32_t* len, const int64_t* off, uint64_t n, bool offsets_only,
                    Bounds* host, hipStream_t stream);
+int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
+                             hipStream_t stream);
 int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
                        hipStream_t stream);
 

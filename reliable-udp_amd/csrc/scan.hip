@@ -1,0 +1,128 @@
+// Frame offsets of a variable-length batch: frame_off[i] = sum_{j<i} (len[j] + H),
+// frame_off[n] = total bytes (the varlen layout).
+//
+// Reduce-then-scan in three launches, no temporary allocation beyond one u64
+// per 2048 packets:
+//   1. block sums of len + H over 2048-packet blocks (coalesced loads);
+//   2. one workgroup turns the block sums into exclusive block bases in place
+//      and writes frame_off[n];
+//   3. each block rescans its lengths through LDS from its base and writes
+//      frame_off[] with coalesced stores.
+// Replaces hipcub::DeviceScan (17 us for 1M lengths including its state
+// init; this form: see DESIGN.md §3 varlen).
+#include "codec_device.hpp"
+#include "internal.hpp"
+
+namespace rudp {
+
+constexpr uint32_t kScanItems = 8;                     // per thread
+constexpr uint32_t kScanBlockItems = kBlock * kScanItems;  // 2048 per block
+
+__global__ void __launch_bounds__(kBlock) scan_block_sums_kernel(const uint32_t* len, uint64_t n,
+                                                                 uint32_t H, uint64_t* sums) {
+  __shared__ uint64_t s_wave[kBlock / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanBlockItems;
+  uint64_t acc = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanItems; ++j) {
+    const uint64_t i = base + j * kBlock + threadIdx.x;
+    if (i < n) acc += (uint64_t)len[i] + H;
+  }
+  for (int m = 32; m > 0; m >>= 1) acc += __shfl_xor(acc, m, 64);
+  if ((threadIdx.x & 63u) == 0) s_wave[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    uint64_t t = 0;
+    for (uint32_t w = 0; w < kBlock / 64; ++w) t += s_wave[w];
+    sums[blockIdx.x] = t;
+  }
+}
+
+// Exclusive scan of one u64 per thread over the block (all threads call it).
+__device__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* total, uint64_t* s_wave) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  uint64_t incl = x;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) s_wave[wave] = incl;
+  __syncthreads();
+  uint64_t before = 0, all = 0;
+  for (uint32_t w = 0; w < nwaves; ++w) {
+    const uint64_t v = s_wave[w];
+    before += w < wave ? v : 0;
+    all += v;
+  }
+  __syncthreads();  // s_wave may be reused by the caller
+  *total = all;
+  return before + incl - x;
+}
+
+// One workgroup of 1024 threads: sums[b] <- sum_{c<b} sums[c]; frame_off[n] <- total.
+__global__ void __launch_bounds__(1024) scan_block_bases_kernel(uint64_t* sums, uint64_t nb,
+                                                               uint64_t* frame_off, uint64_t n) {
+  __shared__ uint64_t s_wave[1024 / 64];
+  const uint64_t per = (nb + 1023) / 1024;
+  const uint64_t lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
+  uint64_t mine = 0;
+  for (uint64_t i = lo; i < hi; ++i) mine += sums[i];
+  uint64_t total = 0;
+  uint64_t run = block_exclusive_scan(mine, &total, s_wave);
+  for (uint64_t i = lo; i < hi; ++i) {
+    const uint64_t v = sums[i];
+    sums[i] = run;
+    run += v;
+  }
+  if (threadIdx.x == 0) frame_off[n] = total;
+}
+
+__global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len, uint64_t n, uint32_t H,
+                                                            const uint64_t* bases, uint64_t* frame_off) {
+  __shared__ uint32_t s_len[kScanBlockItems];
+  __shared__ uint64_t s_off[kScanBlockItems];
+  __shared__ uint64_t s_wave[kBlock / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanBlockItems;
+  // coalesced load of the block's lengths, then each thread takes 8 in a row
+#pragma unroll
+  for (uint32_t j = 0; j < kScanItems; ++j) {
+    const uint32_t k = j * kBlock + threadIdx.x;
+    s_len[k] = base + k < n ? len[base + k] + H : 0u;
+  }
+  __syncthreads();
+  uint64_t mine = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kScanItems; ++j) mine += s_len[threadIdx.x * kScanItems + j];
+  uint64_t total = 0;
+  uint64_t run = bases[blockIdx.x] + block_exclusive_scan(mine, &total, s_wave);
+#pragma unroll
+  for (uint32_t j = 0; j < kScanItems; ++j) {
+    const uint32_t k = threadIdx.x * kScanItems + j;
+    s_off[k] = run;
+    run += s_len[k];
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < kScanItems; ++j) {
+    const uint32_t k = j * kBlock + threadIdx.x;
+    if (base + k < n) frame_off[base + k] = s_off[k];
+  }
+}
+
+int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
+                             hipStream_t stream) {
+  const uint64_t nb = (n + kScanBlockItems - 1) / kScanBlockItems;
+  uint64_t* sums = nullptr;
+  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&sums), nb * sizeof(uint64_t), stream);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(scan_block_sums_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, stream, d_len, n, H, sums);
+  hipLaunchKernelGGL(scan_block_bases_kernel, dim3(1), dim3(1024), 0, stream, sums, nb, d_frame_off, n);
+  hipLaunchKernelGGL(scan_apply_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, stream, d_len, n, H, sums,
+                     d_frame_off);
+  e = hipGetLastError();
+  hipError_t e2 = hipFreeAsync(sums, stream);
+  if (e != hipSuccess) return (int)e;
+  return (int)e2;
+}
+
+}  // namespace rudp

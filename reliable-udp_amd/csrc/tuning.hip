@@ -181,7 +181,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // 16: varlen encode through LDS tiles (packed payloads); 17: most packets per
 // varlen tile; 18: varlen tile payload bytes at the hint; 20: register-streamed
 // encode; 21: its packets per workgroup (0 auto); 22: its load rounds in flight;
-// 23: output wave stores start on 64-B sector boundaries.
+// 23: output wave stores start on 64-B sector boundaries; 24: varlen frame
+// offsets by the three-pass scan (1) or hipcub (0).
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
@@ -194,7 +195,7 @@ int rudpx_tune(int key, int value) {
             : key == 12 ? &t.decode_verify_tile : key == 13 ? &t.encode_ablate : key == 14 ? &t.varlen_vec : key == 15 ? &t.varlen_glog
             : key == 16 ? &t.varlen_tile : key == 17 ? &t.varlen_tile_maxT
             : key == 18 ? &t.varlen_tile_bytes : key == 20 ? &t.encode_stream
-            : key == 21 ? &t.encode_stream_T : key == 22 ? &t.encode_stream_R : key == 23 ? &t.out_align64 : nullptr;
+            : key == 21 ? &t.encode_stream_T : key == 22 ? &t.encode_stream_R : key == 23 ? &t.out_align64 : key == 24 ? &t.varlen_scan : nullptr;
   if (!slot) return -22;
   const int old = *slot;
   *slot = value;

@@ -785,6 +785,7 @@ int launch_validate_utf8(const Utf8Args& args, hipStream_t stream) {
 // frame_off[0..n] = exclusive scan of len[i] + H, frame_off[n] = total bytes.
 int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
                        hipStream_t stream) {
+  if (tuning().varlen_scan == 1) return scan_frame_offsets_3pass(d_len, n, H, d_frame_off, stream);
   hipcub::CountingInputIterator<uint64_t> idx(0);
   hipcub::TransformInputIterator<uint64_t, FrameLen, hipcub::CountingInputIterator<uint64_t>> it(
       idx, FrameLen{d_len, H});

@@ -464,3 +464,28 @@ def test_device_bounds_concurrent_callers(cuda):
     for t in threads:
         t.join()
     assert not errors, errors
+
+
+@pytest.mark.parametrize("n", [1, 2047, 2048, 2049, 4096 * 1024 + 5])
+def test_frame_offset_scans_agree(cuda, n):
+    """The three-pass frame-offset scan (default) == hipcub == numpy cumsum."""
+    import ctypes
+    import torch
+    from rudp import _native
+    lib = _native.lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    rng = np.random.default_rng(n)
+    lens = rng.integers(0, 65536, n).astype(np.int32) if n < 10000 else \
+        rng.integers(0, 3, n).astype(np.int32)
+    want = np.concatenate([[0], np.cumsum(lens.astype(np.int64) + 7)])
+    d_lens = dev(lens, cuda)
+    tab = (torch.zeros(n, dtype=torch.uint16, device=cuda), torch.zeros(n, dtype=torch.uint16, device=cuda),
+           torch.zeros(n, dtype=torch.uint8, device=cuda))
+    pay = torch.zeros(int(lens.sum()), dtype=torch.uint8, device=cuda)
+    try:
+        for scan in (1, 0):
+            lib.rudpx_tune(24, scan)
+            res = batch.pack_batch_varlen(tab, pay, d_lens, 7)
+            assert np.array_equal(host(res.frame_off), want), (n, scan)
+    finally:
+        lib.rudpx_tune(24, 1)

@@ -426,7 +426,10 @@ def varlen_enc_sweep(reps):
                                                  None, 7, 0, stream))
         def cfg(tile, maxT=256, nbytes=24576):
             return lambda: (lib.rudpx_tune(16, tile), lib.rudpx_tune(17, maxT), lib.rudpx_tune(18, nbytes))
-        variants = {f"{name}_tile": (cfg(1), enc), f"{name}_vec": (cfg(0), enc)}
+        variants = {f"{name}_tile": (cfg(1), enc), f"{name}_vec": (cfg(0), enc),
+                    f"{name}_tile_hipcub": (lambda: (cfg(1)(), lib.rudpx_tune(24, 0)), enc)}
+        variants[f"{name}_tile"] = (lambda: (cfg(1)(), lib.rudpx_tune(24, 1)), enc)
+        variants[f"{name}_vec"] = (lambda: (cfg(0)(), lib.rudpx_tune(24, 1)), enc)
         if GEOMETRY_VARIANTS:
             for maxT in (64, 128):
                 variants[f"{name}_tile_maxT{maxT}"] = (cfg(1, maxT), enc)
@@ -434,6 +437,7 @@ def varlen_enc_sweep(reps):
                 variants[f"{name}_tile_bytes{nbytes}"] = (cfg(1, 256, nbytes), enc)
         res = interleaved(variants, reps)
         cfg(1)()
+        lib.rudpx_tune(24, 1)
         # payload + len + header table read; frames + offsets written (scan included)
         alg = 2 * total + n * (7 + 9 + 8)
         for k, ms in res.items():
