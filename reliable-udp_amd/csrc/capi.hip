@@ -549,10 +549,10 @@ int rudp_dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_nu
   a.window = window;
   a.dup = d_dup;
   void* scratch = nullptr;
-  RUDP_HIP(hipMallocAsync(&scratch, n * sizeof(uint64_t), s));
+  RUDP_HIP(stream_alloc(&scratch, n * sizeof(uint64_t), s));
   a.hash = (uint64_t*)scratch;
   rc = launch_dedup(a, s);
-  hipError_t e = hipFreeAsync(scratch, s);
+  hipError_t e = stream_free(scratch, s);
   if (rc) return hip_fail((hipError_t)rc, "dedup launch");
   if (e != hipSuccess) return hip_fail(e, "hipFreeAsync");
   return 0;

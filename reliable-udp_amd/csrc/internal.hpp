@@ -157,6 +157,11 @@ int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream)
 int launch_validate_utf8(const Utf8Args& args, hipStream_t stream);
 int launch_dedup(const DedupArgs& args, hipStream_t stream);
 uint32_t dedup_max_window();
+// Stream-ordered temporaries from a library-owned pool of the current device
+// that keeps its memory across synchronizes (device_pool.hip).
+hipError_t stream_alloc(void** ptr, size_t bytes, hipStream_t stream);
+hipError_t stream_free(void* ptr, hipStream_t stream);
+
 struct Bounds {
   uint64_t min_len, max_len, sum_len;
   int64_t min_off, max_end;

@@ -113,14 +113,14 @@ int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint
                              hipStream_t stream) {
   const uint64_t nb = (n + kScanBlockItems - 1) / kScanBlockItems;
   uint64_t* sums = nullptr;
-  hipError_t e = hipMallocAsync(reinterpret_cast<void**>(&sums), nb * sizeof(uint64_t), stream);
+  hipError_t e = stream_alloc(reinterpret_cast<void**>(&sums), nb * sizeof(uint64_t), stream);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(scan_block_sums_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, stream, d_len, n, H, sums);
   hipLaunchKernelGGL(scan_block_bases_kernel, dim3(1), dim3(1024), 0, stream, sums, nb, d_frame_off, n);
   hipLaunchKernelGGL(scan_apply_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, stream, d_len, n, H, sums,
                      d_frame_off);
   e = hipGetLastError();
-  hipError_t e2 = hipFreeAsync(sums, stream);
+  hipError_t e2 = stream_free(sums, stream);
   if (e != hipSuccess) return (int)e;
   return (int)e2;
 }

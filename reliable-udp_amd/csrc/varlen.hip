@@ -793,10 +793,10 @@ int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* 
   hipError_t e = hipcub::DeviceScan::InclusiveSum(nullptr, temp, it, d_frame_off + 1, (int)n, stream);
   if (e != hipSuccess) return (int)e;
   void* d_temp = nullptr;
-  if ((e = hipMallocAsync(&d_temp, temp ? temp : 1, stream)) != hipSuccess) return (int)e;
+  if ((e = stream_alloc(&d_temp, temp ? temp : 1, stream)) != hipSuccess) return (int)e;
   e = hipcub::DeviceScan::InclusiveSum(d_temp, temp, it, d_frame_off + 1, (int)n, stream);
   hipError_t e2 = hipMemsetAsync(d_frame_off, 0, sizeof(uint64_t), stream);
-  hipError_t e3 = hipFreeAsync(d_temp, stream);
+  hipError_t e3 = stream_free(d_temp, stream);
   if (e != hipSuccess) return (int)e;
   if (e2 != hipSuccess) return (int)e2;
   return (int)e3;

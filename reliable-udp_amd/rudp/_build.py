@@ -20,7 +20,7 @@ CSRC = ROOT / "csrc"
 INCLUDE = ROOT.parent / "include"
 BUILD = ROOT / "build"
 LIB = PKG_DIR / "librudp.so"
-SOURCES = ("encode.hip", "decode.hip", "synth.hip", "varlen.hip", "dedup.hip", "bounds.hip", "scan.hip", "capi.hip",
+SOURCES = ("encode.hip", "decode.hip", "synth.hip", "varlen.hip", "dedup.hip", "bounds.hip", "scan.hip", "device_pool.hip", "capi.hip",
            "tuning.hip", "netio.cpp")
 ARCH = "gfx950"
 
