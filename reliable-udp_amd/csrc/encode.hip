@@ -41,6 +41,82 @@ __device__ __forceinline__ void store16(u32x4 v, u32x4* p) {
     *p = v;
 }
 
+// Phase 2 of the encode tile:
+// output-stationary aligned 16 B chunks assembled from the LDS payload tile
+// and header words.
+template <int H, bool NTS, int BLOCK>
+__device__ __forceinline__ void encode_phase2(const EncodeTileArgs& a, const unsigned char* lds_pay,
+                                              const uint64_t* lds_hdr, uint64_t p0, uint32_t Tv,
+                                              uint32_t tid) {
+  const uint32_t L = a.L;
+  // The tile owns output bytes [p0*F, (p0+Tv)*F).  Chunks are aligned to the
+  // global address; when T*F is not a multiple of 16 (T < 16) the tile's first
+  // and last chunk are shared with its neighbours and only the owned bytes
+  // are written (bytewise, two partial chunks per tile).
+  const uint32_t F = L + H;
+  const uint32_t nbytes = Tv * F;
+  unsigned char* out = a.frames + p0 * (uint64_t)F;
+  const uint32_t lead = (uint32_t)(-(uintptr_t)out) & 15u;  // bytes before the first aligned chunk
+  const uint32_t nfull = nbytes > lead ? (nbytes - lead) >> 4 : 0u;
+  // Full chunks are dealt from the first 64-B boundary on (the 0-3 chunks
+  // before it go last), so each wave's 1 KiB store covers whole 64-B sectors
+  // instead of splitting one at each end with the next wave.
+  uint32_t npre = a.out_align64 ? ((uint32_t)(-(uintptr_t)out) & 63u) >> 4 : 0u;
+  if (npre > nfull) npre = nfull;
+  const uint32_t* pay_dw = reinterpret_cast<const uint32_t*>(lds_pay);
+  // unit k < nfull: full chunk i = (k + npre) mod nfull at tile offset
+  // lead + 16i; the two units after that are the partial head [0, lead) and
+  // tail [lead + 16*nfull, nbytes).
+  for (uint32_t k = tid; k < nfull + 2u; k += BLOCK) {
+    uint32_t x, lo_b, hi_b;  // tile offset of chunk byte 0; owned byte range [lo_b, hi_b)
+    if (k < nfull) {
+      const uint32_t i = k + npre < nfull ? k + npre : k + npre - nfull;
+      x = lead + 16u * i; lo_b = 0; hi_b = 16;
+    } else if (k == nfull) {
+      x = 0; lo_b = 0; hi_b = lead < nbytes ? lead : nbytes;
+    } else {
+      x = lead + 16u * nfull; lo_b = 0; hi_b = nbytes > x ? nbytes - x : 0u;
+    }
+    if (hi_b <= lo_b) continue;
+    if (a.ablate & 2u) {  // diagnostic: aligned LDS read in place of the window assembly
+      const u32x4 v = reinterpret_cast<const u32x4*>(lds_pay + kLdsGuard)[k < nfull ? k : 0u];
+      if (hi_b == 16u) store16<NTS>(v, reinterpret_cast<u32x4*>(out + x));
+      continue;
+    }
+    const uint32_t qq = (uint32_t)(((uint64_t)x * a.invF) >> 32);  // x / F
+    const uint32_t r = x - qq * F;           // frame position of chunk byte 0
+    const int kA0 = r < (uint32_t)H ? H - (int)r : 0;  // first payload byte of qq
+    const int kend = (int)(F - r);           // first byte of packet qq+1
+    // LDS offset (from lds_pay) of byte 0 if it were payload of qq.
+    const uint32_t sA = kLdsGuard + qq * L + r - H;
+    const u32x4 A = window16_dw(pay_dw, sA);
+    uint64_t lo = lo64(A) & byte_mask(kA0, kend);
+    uint64_t hi = hi64(A) & byte_mask(kA0 - 8, kend - 8);
+    if (kA0 > 0) lo |= lds_hdr[qq] >> (8 * r);
+    if (kend < 16) {
+      const u32x4 B = window16_dw(pay_dw, sA - H);
+      lo |= lo64(B) & byte_mask(kend + H, 16);
+      hi |= hi64(B) & byte_mask(kend + H - 8, 8);
+      const uint64_t h1 = lds_hdr[qq + 1];
+      if (kend < 8) {
+        lo |= h1 << (8 * kend);
+        if (kend > 0) hi |= h1 >> (64 - 8 * kend);
+      } else {
+        hi |= h1 << (8 * (kend - 8));
+      }
+    }
+    const u32x4 v = make_u32x4(lo, hi);
+    if (hi_b == 16u) {
+      store16<NTS>(v, reinterpret_cast<u32x4*>(out + x));
+    } else {
+      uint32_t d[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (uint32_t b = 0; b < 16; ++b)
+        if (b < hi_b) out[x + b] = (unsigned char)(d[b >> 2] >> (8 * (b & 3)));
+    }
+  }
+}
+
 template <int H, bool NTL, bool NTS, int P1, bool CONTIG, int BLOCK = kBlock>
 __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -131,73 +207,7 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   }
   __syncthreads();
 
-  // ---- phase 2: aligned 16 B output chunks --------------------------------
-  // The tile owns output bytes [p0*F, (p0+Tv)*F).  Chunks are aligned to the
-  // global address; when T*F is not a multiple of 16 (T < 16) the tile's first
-  // and last chunk are shared with its neighbours and only the owned bytes
-  // are written (bytewise, two partial chunks per tile).
-  const uint32_t F = L + H;
-  const uint32_t nbytes = Tv * F;
-  unsigned char* out = a.frames + p0 * (uint64_t)F;
-  const uint32_t lead = (uint32_t)(-(uintptr_t)out) & 15u;  // bytes before the first aligned chunk
-  const uint32_t nfull = nbytes > lead ? (nbytes - lead) >> 4 : 0u;
-  // Full chunks are dealt from the first 64-B boundary on (the 0-3 chunks
-  // before it go last), so each wave's 1 KiB store covers whole 64-B sectors
-  // instead of splitting one at each end with the next wave.
-  uint32_t npre = a.out_align64 ? ((uint32_t)(-(uintptr_t)out) & 63u) >> 4 : 0u;
-  if (npre > nfull) npre = nfull;
-  const uint32_t* pay_dw = reinterpret_cast<const uint32_t*>(lds_pay);
-  // unit k < nfull: full chunk i = (k + npre) mod nfull at tile offset
-  // lead + 16i; the two units after that are the partial head [0, lead) and
-  // tail [lead + 16*nfull, nbytes).
-  for (uint32_t k = tid; k < nfull + 2u; k += BLOCK) {
-    uint32_t x, lo_b, hi_b;  // tile offset of chunk byte 0; owned byte range [lo_b, hi_b)
-    if (k < nfull) {
-      const uint32_t i = k + npre < nfull ? k + npre : k + npre - nfull;
-      x = lead + 16u * i; lo_b = 0; hi_b = 16;
-    } else if (k == nfull) {
-      x = 0; lo_b = 0; hi_b = lead < nbytes ? lead : nbytes;
-    } else {
-      x = lead + 16u * nfull; lo_b = 0; hi_b = nbytes > x ? nbytes - x : 0u;
-    }
-    if (hi_b <= lo_b) continue;
-    if (a.ablate & 2u) {  // diagnostic: aligned LDS read in place of the window assembly
-      const u32x4 v = reinterpret_cast<const u32x4*>(lds_pay + kLdsGuard)[k < nfull ? k : 0u];
-      if (hi_b == 16u) store16<NTS>(v, reinterpret_cast<u32x4*>(out + x));
-      continue;
-    }
-    const uint32_t qq = (uint32_t)(((uint64_t)x * a.invF) >> 32);  // x / F
-    const uint32_t r = x - qq * F;           // frame position of chunk byte 0
-    const int kA0 = r < (uint32_t)H ? H - (int)r : 0;  // first payload byte of qq
-    const int kend = (int)(F - r);           // first byte of packet qq+1
-    // LDS offset (from lds_pay) of byte 0 if it were payload of qq.
-    const uint32_t sA = kLdsGuard + qq * L + r - H;
-    const u32x4 A = window16_dw(pay_dw, sA);
-    uint64_t lo = lo64(A) & byte_mask(kA0, kend);
-    uint64_t hi = hi64(A) & byte_mask(kA0 - 8, kend - 8);
-    if (kA0 > 0) lo |= lds_hdr[qq] >> (8 * r);
-    if (kend < 16) {
-      const u32x4 B = window16_dw(pay_dw, sA - H);
-      lo |= lo64(B) & byte_mask(kend + H, 16);
-      hi |= hi64(B) & byte_mask(kend + H - 8, 8);
-      const uint64_t h1 = lds_hdr[qq + 1];
-      if (kend < 8) {
-        lo |= h1 << (8 * kend);
-        if (kend > 0) hi |= h1 >> (64 - 8 * kend);
-      } else {
-        hi |= h1 << (8 * (kend - 8));
-      }
-    }
-    const u32x4 v = make_u32x4(lo, hi);
-    if (hi_b == 16u) {
-      store16<NTS>(v, reinterpret_cast<u32x4*>(out + x));
-    } else {
-      uint32_t d[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (uint32_t b = 0; b < 16; ++b)
-        if (b < hi_b) out[x + b] = (unsigned char)(d[b >> 2] >> (8 * (b & 3)));
-    }
-  }
+  encode_phase2<H, NTS, BLOCK>(a, lds_pay, lds_hdr, p0, Tv, tid);
 }
 
 // Any payload length / alignment: one wave per packet, byte-granular.
@@ -225,6 +235,7 @@ __global__ void __launch_bounds__(kBlock) encode_bytes_kernel(EncodeTileArgs a) 
   if (lane < (uint32_t)H) dst[lane] = (unsigned char)(h >> (8 * lane));
   if (lane == 0 && a.csum) a.csum[p] = (uint16_t)c;
 }
+
 
 template <int H, bool NTL, bool NTS, int P1, bool CONTIG, int BLOCK = kBlock>
 int launch_tile(const EncodeTileArgs& args, hipStream_t stream) {
