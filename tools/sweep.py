@@ -60,6 +60,8 @@ def interleaved(variants, reps):
 
 BLOCKS_OVERRIDE = None
 ENCODE_LS = None
+PERCU_OVERRIDE = None      # encode: tiles-per-CU caps to try (256-thread blocks)
+TILES_OVERRIDE = None      # encode: packets per tile to try
 GEOMETRY_VARIANTS = False
 STREAM_ABLATE = False      # stream: also time stage ablations (wrong output; key 13 bits 8/16)  # varlen_enc: also sweep tile size knobs (keys 17, 18)
 
@@ -85,10 +87,10 @@ def encode_sweep(reps):
         variants = {}
         blocks = BLOCKS_OVERRIDE or (64, 128, 256)
         for block in blocks:
-            for tile in tiles:
+            for tile in (TILES_OVERRIDE or tiles):
                 if tile > block:
                     continue
-                for per_cu in ((-1, 0, 5) if block == 256 else (0, 16, 24) if block < 256 else (0, 2, 3)):
+                for per_cu in ((PERCU_OVERRIDE or (-1, 0, 5)) if block == 256 else (0, 16, 24) if block < 256 else (0, 2, 3)):
                     def setup(tile=tile, per_cu=per_cu, block=block):
                         lib.rudpx_tune(10, block)
                         lib.rudpx_tune(2, tile)
@@ -476,8 +478,14 @@ def main():
     ap.add_argument("--blocks", type=str, default="", help="encode sweep: workgroup sizes, e.g. 256,512,1024")
     ap.add_argument("--encode-L", type=str, default="", help="encode sweep: payload lengths, e.g. 1472")
     ap.add_argument("--ablate", action="store_true", help="stream sweep: add stage ablations")
+    ap.add_argument("--percu", type=str, default="", help="encode sweep: tiles-per-CU caps, e.g. 3,4,5")
+    ap.add_argument("--tiles", type=str, default="", help="encode sweep: packets per tile, e.g. 8,16")
     args = ap.parse_args()
-    global BLOCKS_OVERRIDE, ENCODE_LS, STREAM_ABLATE
+    global BLOCKS_OVERRIDE, ENCODE_LS, STREAM_ABLATE, PERCU_OVERRIDE, TILES_OVERRIDE
+    if args.percu:
+        PERCU_OVERRIDE = tuple(int(x) for x in args.percu.split(","))
+    if args.tiles:
+        TILES_OVERRIDE = tuple(int(x) for x in args.tiles.split(","))
     STREAM_ABLATE = args.ablate
     if args.blocks:
         BLOCKS_OVERRIDE = tuple(int(b) for b in args.blocks.split(","))
