@@ -115,6 +115,13 @@ EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t*
     a.invV = ((1ull << 32) + V - 1ull) / V;
     const int al = tuning().out_align64;
     a.out_align64 = (al == 1 || (al < 0 && a.T * a.L > 16384u)) ? 1u : 0u;
+    const uint32_t S = (uint32_t)tuning().encode_span_bytes;
+    if (tuning().encode_span && a.L >= 256u && S >= 1024u && S <= 32768u && S % 64u == 0 && F < S) {
+      a.span = S;
+      a.rcpF = 1.0 / (double)F;
+      a.invF = ((1ull << 32) + F - 1ull) / F;
+      encode_span_geometry(a.L, (uint32_t)layout, S, &a.span_glog, &a.hdr_bytes);
+    }
   }
   return a;
 }

@@ -117,7 +117,7 @@ __device__ __forceinline__ void encode_phase2(const EncodeTileArgs& a, const uns
   }
 }
 
-template <int H, bool NTL, bool NTS, int P1, bool CONTIG, int BLOCK = kBlock>
+template <int H, bool NTL, bool NTS, int P1, bool CONTIG, int BLOCK = kBlock, bool DMA = false>
 __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   uint64_t* lds_hdr = reinterpret_cast<uint64_t*>(lds);  // [T + 1]
@@ -157,7 +157,18 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
     const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + p0 * (uint64_t)L);
     u32x4* dst = reinterpret_cast<u32x4*>(lds_pay + kLdsGuard);
     const uint32_t nvec = Tv * V;
-    for (uint32_t v0 = tid; v0 < nvec; v0 += (uint32_t)P1 * BLOCK) {
+    if (DMA) {
+      // LDS-DMA (global_load_lds_dwordx4): each wave-instruction moves 1 KiB
+      // from HBM straight into the tile, lane-linear, no VGPR round trip.
+      const uint32_t wbase = tid & ~63u;
+      for (uint32_t v0 = wbase; v0 < nvec; v0 += BLOCK) {
+        if (v0 + (tid & 63u) < nvec)
+          __builtin_amdgcn_global_load_lds(
+              (const void __attribute__((address_space(1)))*)(src + v0 + (tid & 63u)),
+              (void __attribute__((address_space(3)))*)(dst + v0), 16, 0, NTL ? 2 : 0);
+      }
+    }
+    for (uint32_t v0 = tid; !DMA && v0 < nvec; v0 += (uint32_t)P1 * BLOCK) {
       u32x4 r[P1];
 #pragma unroll
       for (int u = 0; u < P1; ++u) {
@@ -210,6 +221,265 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   encode_phase2<H, NTS, BLOCK>(a, lds_pay, lds_hdr, p0, Tv, tid);
 }
 
+// The one or two aligned 16-B chunks [floor16(P - H), ceil16(P)) that hold a
+// packet's header, P = the output offset of its payload: the previous
+// packet's last payload bytes (`tail`: its last 16), the header bytes `h`
+// (frame order, packed little-endian) and the first payload bytes (`head`).
+template <int H>
+__device__ __forceinline__ void store_header_chunks(unsigned char* out, uint64_t P, uint64_t h,
+                                                    u32x4 tail, u32x4 head) {
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  const uint64_t X0 = (P - H) & ~15ull, X1 = (P + 15u) & ~15ull;
+  for (uint64_t X = X0; X < X1; X += 16) {
+    const int k0 = (int)(int64_t)(X - (P - H));  // frame position of chunk byte 0 (> -16)
+    u32x4 w = zero;
+    if (k0 < 0) w = funnel32(tail, zero, (uint32_t)(k0 + 16));  // previous payload's last bytes
+    const uint32_t d = (uint32_t)(P - X);                        // payload starts d bytes in
+    if (d < 16) {
+      const u32x4 hp = funnel32(zero, head, 16u - d);
+      w.x |= hp.x; w.y |= hp.y; w.z |= hp.z; w.w |= hp.w;
+    }
+    uint64_t lo = lo64(w), hi = hi64(w);
+    if (k0 >= 0) {
+      lo |= h >> (8 * k0);
+    } else {
+      const int sh = -k0;
+      if (sh < 8) {
+        lo |= h << (8 * sh);
+        hi |= h >> (64 - 8 * sh);
+      } else {
+        hi |= h << (8 * (sh - 8));
+      }
+    }
+    __builtin_nontemporal_store(make_u32x4(lo, hi), reinterpret_cast<u32x4*>(out + X));
+  }
+}
+
+// floor(x / F) for x < 2^52 from a double reciprocal and one correction
+// step (an inline 64-bit integer division costs ~130 instructions per wave).
+__device__ __forceinline__ uint64_t div_by_frame(uint64_t x, uint32_t F, double rcpF) {
+  uint64_t q = (uint64_t)((double)x * rcpF);
+  const int64_t r = (int64_t)(x - q * F);
+  if (r < 0) --q;
+  else if (r >= (int64_t)F) ++q;
+  return q;
+}
+
+// Span encode (L % 16 == 0, 256 <= L <= 4096, both buffers 16-B aligned).
+// The tile kernel's workgroup owns T whole packets, ~24 KiB of payload at
+// MTU size; LDS-staged copies of that footprint top out near 5.9 TB/s while
+// ~8 KiB footprints in short-lived workgroups reach the streaming-copy rate
+// (profiles/r01/sweeps/copy_dma.json).  Here a workgroup owns a fixed span of
+// S OUTPUT bytes [b*S, (b+1)*S) instead, whatever packets it cuts:
+//   phase 1  the payload bytes behind the span (one contiguous input run:
+//            packet boundaries in the input are 16-B aligned) go to LDS by
+//            LDS-DMA.
+//   sums     G lanes per packet sum each packet's bytes inside the span.  A
+//            packet wholly inside gets its header word in LDS.  A packet
+//            crossing a span boundary ("straddler") has two partial sums, one
+//            per workgroup, stored to the boundary's two slots.
+//   phase 2  every other aligned 16-B chunk of the span, output-stationary as
+//            in the tile kernel (encode_phase2's window assembly).
+// encode_straddle_kernel (a second launch, one lane per boundary) adds the
+// two parts and writes each straddler's header chunks (the 1-2 aligned
+// chunks over its header bytes) from the header table and the 32 input bytes
+// around its payload start.  A first form finished straddlers inside the span
+// kernel (an agent-scope atomic add, the second workgroup finishing): the
+// atomic's round trip on every workgroup's critical path made it 2.2x slower.
+// Every output chunk is written once, whole, by one workgroup: no bytewise
+// boundary chunks and no sector shared between two workgroups' stores.
+template <int H>
+__global__ void __launch_bounds__(kBlock) encode_span_kernel(EncodeTileArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  uint64_t* lds_hdr = reinterpret_cast<uint64_t*>(lds);  // slot s: packet qa + s
+  unsigned char* lds_pay = lds + a.hdr_bytes;
+  const uint32_t tid = threadIdx.x, lane = tid & 63u;
+  const uint32_t L = a.L, F = L + H, S = a.span;
+  const uint64_t Z = a.n * (uint64_t)F;
+  const uint64_t b = blockIdx.x;
+  const uint64_t X0 = b * S;
+  const uint64_t X1 = (X0 + S < Z) ? X0 + S : Z;
+  const uint64_t qa = div_by_frame(X0, F, a.rcpF), qb = div_by_frame(X1 - 1, F, a.rcpF);
+  const uint32_t ra = (uint32_t)(X0 - qa * F);   // frame position of X0 in packet qa
+  const uint32_t rb = (uint32_t)(X1 - qb * F);   // bytes of frame qb before X1 (1..F)
+  const bool start_str = ra != 0;                // qa began in span b-1
+  const bool end_str = rb != F;                  // qb goes on in span b+1
+  const uint64_t in0 = qa * L + (ra > (uint32_t)H ? ra - H : 0u);
+  const uint64_t in1 = qb * L + (rb > (uint32_t)H ? rb - H : 0u);
+  const uint64_t A0 = in0 & ~15ull;
+  const uint32_t nvec = (uint32_t)((((in1 + 15) & ~15ull) - A0) >> 4);
+
+  // Header-table loads for the packets wholly inside the span go out first,
+  // so their latency overlaps the payload DMA (one round trip per workgroup).
+  const uint32_t np = (uint32_t)(qb - qa + 1);
+  const uint32_t glog = a.span_glog, G = 1u << glog;
+  const uint32_t s = tid >> glog, g = tid & (G - 1u);
+  const bool lead = g == 0 && s < np;
+  const bool first = s == 0 && start_str, last = s == np - 1 && end_str;
+  uint32_t t_seq = 0, t_ack = 0, t_flags = 0;
+  if (lead && !first && !last) {
+    t_seq = a.seq[qa + s];
+    t_ack = a.ack[qa + s];
+    t_flags = a.flags[qa + s];
+  }
+  // ---- phase 1: input run -> LDS (LDS-DMA, 1 KiB per wave-instruction) ----
+  {
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + A0);
+    u32x4* dst = reinterpret_cast<u32x4*>(lds_pay + kLdsGuard);
+    for (uint32_t v0 = tid & ~63u; v0 < nvec; v0 += kBlock)
+      if (v0 + lane < nvec)
+        __builtin_amdgcn_global_load_lds(
+            (const void __attribute__((address_space(1)))*)(src + v0 + lane),
+            (void __attribute__((address_space(3)))*)(dst + v0), 16, 0, 2);
+  }
+  __syncthreads();
+
+  // ---- per-packet sums of the bytes inside the span ----------------------
+  uint32_t sum = 0;
+  if (s < np) {
+    const u32x4* img = reinterpret_cast<const u32x4*>(lds_pay + kLdsGuard);
+    const uint64_t q = qa + s;
+    const uint64_t lo = q * L > in0 ? q * L : in0;
+    const uint64_t hi = (q + 1) * L < in1 ? (q + 1) * L : in1;
+    if (hi > lo) {
+      const uint32_t blo = (uint32_t)(lo - A0), bhi = (uint32_t)(hi - A0);
+      const uint32_t c0 = blo >> 4, c1 = (bhi + 15u) >> 4;
+      for (uint32_t c = c0 + g; c < c1; c += G) {
+        u32x4 w = img[c];
+        if (c == c0 || c + 1 == c1) {  // keep bytes [blo, bhi) only
+          const int l = (int)blo - (int)(16u * c), h = (int)bhi - (int)(16u * c);
+          w = make_u32x4(lo64(w) & byte_mask(l, h), hi64(w) & byte_mask(l - 8, h - 8));
+        }
+        sum += le16_sum(w);  // input offsets and payload indices share parity (L even)
+      }
+    }
+  }
+  for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
+  if (lead) {
+    const uint64_t q = qa + s;
+    if (!first && !last) {
+      const uint32_t c = packet_csum(sum, t_seq, t_ack, t_flags);
+      lds_hdr[s] = pack_header<H>(t_seq, t_ack, t_flags, c);
+      if (a.csum) a.csum[q] = (uint16_t)c;
+    } else {
+      a.straddle[first ? 2 * b - 1 : 2 * b] = sum;
+    }
+  }
+  __syncthreads();
+
+  // ---- phase 2: the span's chunks, header chunks of straddlers excepted --
+  const uint32_t nbytes = (uint32_t)(X1 - X0);
+  const uint32_t nchunks = (nbytes + 15u) >> 4;
+  const uint64_t qaF = qa * F, qbF = qb * F;
+  const uint32_t* pay_dw = reinterpret_cast<const uint32_t*>(lds_pay);
+  const int64_t img_base = (int64_t)kLdsGuard + (int64_t)(qa * L) - (int64_t)A0;  // LDS offset of qa's payload byte 0
+  for (uint32_t k = tid; k < nchunks; k += kBlock) {
+    const uint64_t X = X0 + 16ull * k;
+    if (start_str && X + 16 > qaF && X < qaF + H) continue;
+    if (end_str && X + 16 > qbF && X < qbF + H) continue;
+    const uint32_t x = ra + 16u * k;  // offset from qa's frame start
+    const uint32_t qq = (uint32_t)(((uint64_t)x * a.invF) >> 32);  // x / F
+    const uint32_t r = x - qq * F;
+    const int kA0 = r < (uint32_t)H ? H - (int)r : 0;
+    const int kend = (int)(F - r);
+    const uint32_t sA = (uint32_t)(img_base + (int64_t)qq * L + (int64_t)r - H);
+    const u32x4 Aw = window16_dw(pay_dw, sA);
+    uint64_t lo = lo64(Aw) & byte_mask(kA0, kend);
+    uint64_t hi = hi64(Aw) & byte_mask(kA0 - 8, kend - 8);
+    if (kA0 > 0) lo |= lds_hdr[qq] >> (8 * r);
+    if (kend < 16) {
+      const u32x4 Bw = window16_dw(pay_dw, sA - H);
+      lo |= lo64(Bw) & byte_mask(kend + H, 16);
+      hi |= hi64(Bw) & byte_mask(kend + H - 8, 8);
+      const uint64_t h1 = lds_hdr[qq + 1];
+      if (kend < 8) {
+        lo |= h1 << (8 * kend);
+        if (kend > 0) hi |= h1 >> (64 - 8 * kend);
+      } else {
+        hi |= h1 << (8 * (kend - 8));
+      }
+    }
+    const u32x4 v = make_u32x4(lo, hi);
+    unsigned char* out = a.frames + X;
+    if (16u * k + 16u <= nbytes) {
+      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out));
+    } else {  // the batch's last bytes
+      const uint32_t nb = nbytes - 16u * k;
+      const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+      for (uint32_t i = 0; i < nb; ++i) out[i] = (unsigned char)(d[i >> 2] >> (8 * (i & 3)));
+    }
+  }
+}
+
+// Finishes the packets that cross span boundaries: lane b takes the boundary
+// after span b (no packet crosses it when it falls on a frame start).
+template <int H>
+__global__ void __launch_bounds__(kBlock) encode_straddle_kernel(EncodeTileArgs a, uint64_t nbound) {
+  const uint64_t b = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (b >= nbound) return;
+  const uint32_t L = a.L, F = L + H;
+  const uint64_t X = (b + 1) * (uint64_t)a.span;
+  const uint64_t q = div_by_frame(X, F, a.rcpF);
+  if (X == q * F) return;
+  const uint32_t sq = a.seq[q], k = a.ack[q], f = a.flags[q];
+  const uint32_t c = packet_csum(a.straddle[2 * b] + a.straddle[2 * b + 1], sq, k, f);
+  if (a.csum) a.csum[q] = (uint16_t)c;
+  const u32x4* in = reinterpret_cast<const u32x4*>(a.payload + q * L);
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  store_header_chunks<H>(a.frames, q * F + H, pack_header<H>(sq, k, f, c), q > 0 ? in[-1] : zero,
+                         in[0]);
+}
+
+// Span geometry: lanes per packet for the sum pass and LDS header slots.
+void encode_span_geometry(uint32_t L, uint32_t H, uint32_t S, uint32_t* glog, uint32_t* hdr_bytes) {
+  const uint32_t slots = S / (L + H) + 2u;
+  uint32_t lg = 0;
+  while (lg < 6 && (2u << lg) * slots <= (uint32_t)kBlock) ++lg;
+  *glog = lg;
+  *hdr_bytes = ((slots + 1u) * 8u + 15u) & ~15u;
+}
+
+int launch_span(const EncodeTileArgs& args, int layout, hipStream_t stream) {
+  const uint64_t Z = args.n * (uint64_t)(args.L + (uint32_t)layout);
+  const uint64_t spans = (Z + args.span - 1) / args.span;
+  const uint64_t nbound = spans - 1;
+  void* scratch = nullptr;
+  if (nbound) {
+    hipError_t e = stream_alloc(&scratch, nbound * 8, stream);
+    if (e != hipSuccess) return (int)e;
+  }
+  EncodeTileArgs a = args;
+  a.straddle = static_cast<uint32_t*>(scratch);
+  size_t lds = a.hdr_bytes + kLdsGuard + (size_t)a.span + 16 + 32;
+  int per_cu = tuning().encode_blocks_per_cu;
+  if (per_cu < 0) per_cu = 5;  // short-lived 8 KiB workgroups: 5 per CU measured best for LDS-staged copies
+  if (per_cu > 0) {
+    const size_t want = ((size_t)(160 * 1024) / (size_t)per_cu) & ~size_t(15);
+    if (want > lds) lds = want;
+  }
+  const void* fn = layout == 7 ? reinterpret_cast<const void*>(&encode_span_kernel<7>)
+                               : reinterpret_cast<const void*>(&encode_span_kernel<5>);
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  if (layout == 7)
+    hipLaunchKernelGGL(encode_span_kernel<7>, dim3((uint32_t)spans), dim3(kBlock), lds, stream, a);
+  else
+    hipLaunchKernelGGL(encode_span_kernel<5>, dim3((uint32_t)spans), dim3(kBlock), lds, stream, a);
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  if (!nbound) return 0;
+  const dim3 g2((uint32_t)((nbound + kBlock - 1) / kBlock));
+  if (layout == 7)
+    hipLaunchKernelGGL(encode_straddle_kernel<7>, g2, dim3(kBlock), 0, stream, a, nbound);
+  else
+    hipLaunchKernelGGL(encode_straddle_kernel<5>, g2, dim3(kBlock), 0, stream, a, nbound);
+  e = hipGetLastError();
+  if (e != hipSuccess) return (int)e;
+  return (int)stream_free(scratch, stream);
+}
+
 // Any payload length / alignment: one wave per packet, byte-granular.
 // Same arithmetic as the tile kernel; used for reference-sized frames
 // (1-char payloads, utils/reliableUDP.py:11) and ragged shapes.
@@ -237,7 +507,7 @@ __global__ void __launch_bounds__(kBlock) encode_bytes_kernel(EncodeTileArgs a) 
 }
 
 
-template <int H, bool NTL, bool NTS, int P1, bool CONTIG, int BLOCK = kBlock>
+template <int H, bool NTL, bool NTS, int P1, bool CONTIG, int BLOCK = kBlock, bool DMA = false>
 int launch_tile(const EncodeTileArgs& args, hipStream_t stream) {
   const uint64_t blocks = (args.n + args.T - 1) / args.T;
   size_t lds = args.hdr_bytes + kLdsGuard + (size_t)args.T * args.L + 32;
@@ -253,11 +523,11 @@ int launch_tile(const EncodeTileArgs& args, hipStream_t stream) {
     if (want > lds) lds = want;
   }
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_tile_kernel<H, NTL, NTS, P1, CONTIG, BLOCK>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_tile_kernel<H, NTL, NTS, P1, CONTIG, BLOCK, DMA>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL((encode_tile_kernel<H, NTL, NTS, P1, CONTIG, BLOCK>), dim3((uint32_t)blocks), dim3(BLOCK), lds,
+  hipLaunchKernelGGL((encode_tile_kernel<H, NTL, NTS, P1, CONTIG, BLOCK, DMA>), dim3((uint32_t)blocks), dim3(BLOCK), lds,
                      stream, args);
   return (int)hipGetLastError();
 }
@@ -278,6 +548,9 @@ int launch_tile_policy(const EncodeTileArgs& args, hipStream_t stream) {
   // A packet's lanes must sit in one wave (the shfl_xor reduction): wider
   // blocks give each packet (256/T)*(block/256) lanes, so keep that <= 64.
   if (block > 256 && (uint64_t)(256u / args.T) * (uint32_t)(block / 256) > 64u) block = 256;
+  const Tuning& t = tuning();
+  if (t.encode_dma && block == 256 && t.encode_contig && t.encode_nt_load && t.encode_nt_store)
+    return launch_tile<H, true, true, 8, true, kBlock, true>(args, stream);
   if (block == 64 && args.T <= 64) return launch_tile<H, true, true, 8, true, 64>(args, stream);
   if (block == 128 && args.T <= 128) return launch_tile<H, true, true, 8, true, 128>(args, stream);
   if (block == 512) return launch_tile<H, true, true, 8, true, 512>(args, stream);
@@ -454,6 +727,7 @@ int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStr
     s.T = stream_tile(args.L);
     return layout == 7 ? launch_stream<7>(s, stream) : launch_stream<5>(s, stream);
   }
+  if (tile_path && args.span) return launch_span(args, layout, stream);
   if (tile_path)
     return layout == 7 ? launch_tile_policy<7>(args, stream) : launch_tile_policy<5>(args, stream);
   const uint64_t blocks = (args.n + (kBlock / 64) - 1) / (kBlock / 64);

@@ -24,6 +24,14 @@ struct EncodeTileArgs {
                         // LDS reads, 4 no header-table loads
   uint64_t invV;        // ceil(2^32 / (L / 16)) for exact v / V (stream kernel)
   uint32_t out_align64; // phase 2 deals full chunks from the tile's first 64-B boundary
+  // span kernel: each workgroup owns `span` output bytes (a multiple of 64);
+  // a packet crossing the boundary after span b leaves its two partial
+  // payload sums in straddle[2b] (span b's part) and straddle[2b + 1]
+  // (span b+1's), and a second launch finishes it
+  uint32_t span;
+  uint32_t span_glog;       // log2 lanes per packet in the span sum pass
+  double rcpF;              // 1.0 / (L + H)
+  uint32_t* straddle;
 };
 
 struct DecodeArgs {
@@ -138,6 +146,15 @@ struct Tuning {
   // where it measured 1-3% slower (decode, L = 1024 encode, varlen;
   // profiles/r01/sweeps/align64.json).
   int out_align64 = -1;
+  // Encode tile phase 1 by LDS-DMA (global_load_lds_dwordx4) in place of
+  // register staging (256-thread contiguous tiles, nt loads and stores):
+  // 1M x 256 B 0.0967 -> 0.0946 ms, x 512 B 0.1884 -> 0.1854, x 64 B 0.0301
+  // -> 0.0292; x 1024 B and x 1472 B unchanged (profiles/r01/sweeps/span_vs_tile.json).
+  int encode_dma = 1;
+  // Encode by fixed output spans (encode_span_kernel; opt-in, bit-exact, not
+  // faster at MTU size: 1M x 1472 B 0.530 vs 0.518 ms, x 1024 B 0.352 vs 0.363).
+  int encode_span = 0;
+  int encode_span_bytes = 8192;  // span kernel: output bytes per workgroup (multiple of 64)
   int varlen_scan = 1;    // frame offsets: 1 = reduce-then-scan (scan.hip), 0 = hipcub
   int host_slots = 3;     // *_host pipeline: device staging slots (2..8)
   int host_stage_mb = 128;  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
@@ -146,6 +163,7 @@ Tuning& tuning();
 
 // Tile geometry for a fast-path payload length (L % 16 == 0, 16 <= L <= 4096).
 void encode_tile_geometry(uint32_t L, uint32_t* T, uint32_t* glog);
+void encode_span_geometry(uint32_t L, uint32_t H, uint32_t S, uint32_t* glog, uint32_t* hdr_bytes);
 uint32_t decode_group_log2(uint32_t L);
 
 int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStream_t stream);

@@ -114,6 +114,46 @@ __global__ void __launch_bounds__(kBlock) copy_tile_pipe_kernel(const u32x4* __r
   }
 }
 
+
+// Diagnostic: tiled copy staged by LDS-DMA (global_load_lds_dwordx4).  PIPE:
+// persistent blocks with two LDS buffers; the next tile's DMA is in flight
+// while the current tile drains from LDS to HBM.
+__device__ __forceinline__ void dma_tile(const u32x4* src, u32x4* buf, uint32_t m) {
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint32_t v0 = threadIdx.x & ~63u; v0 < m; v0 += kBlock)
+    if (v0 + lane < m)
+      __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)(src + v0 + lane),
+                                       (void __attribute__((address_space(3)))*)(buf + v0), 16, 0, 2);
+}
+
+template <bool PIPE>
+__global__ void __launch_bounds__(kBlock) copy_tile_dma_kernel(const u32x4* __restrict__ src,
+                                                               u32x4* __restrict__ dst, uint64_t n16,
+                                                               uint32_t tile16) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  u32x4* t = reinterpret_cast<u32x4*>(lds);
+  const uint64_t ntiles = (n16 + tile16 - 1) / tile16;
+  uint64_t tile = blockIdx.x;
+  const uint64_t stride = PIPE ? gridDim.x : ntiles;
+  uint32_t buf = 0;
+  auto count = [&](uint64_t tl) {
+    const uint64_t base = tl * tile16;
+    return (uint32_t)((n16 - base) < tile16 ? (n16 - base) : tile16);
+  };
+  if (tile < ntiles) dma_tile(src + tile * tile16, t, count(tile));
+  while (tile < ntiles) {
+    __syncthreads();  // vmcnt(0): this tile's DMA has landed; the other buffer is free
+    const uint64_t next = tile + stride;
+    if (next < ntiles) dma_tile(src + next * tile16, t + (buf ^ 1u) * tile16, count(next));
+    const uint32_t m = count(tile);
+    const u32x4* b = t + buf * tile16;
+    for (uint32_t v = threadIdx.x; v < m; v += kBlock)
+      __builtin_nontemporal_store(b[v], dst + tile * tile16 + v);
+    tile = next;
+    buf ^= 1u;
+  }
+}
+
 }  // namespace rudp
 
 extern "C" {
@@ -131,6 +171,30 @@ int rudpx_copy_tile_pipe(const void* src, void* dst, uint64_t n16, uint32_t tile
   }
   hipLaunchKernelGGL(rudp::copy_tile_pipe_kernel, dim3(blocks), dim3(rudp::kBlock), lds,
                      (hipStream_t)stream, (const rudp::u32x4*)src, (rudp::u32x4*)dst, n16, tile16);
+  return (int)hipGetLastError();
+}
+
+// LDS-DMA tiled copy (diagnostic).  pipe = 0: one tile per block; pipe = 1:
+// `blocks` persistent blocks, double-buffered.  lds_bytes >= 2*tile16*16 sets occupancy.
+int rudpx_copy_tile_dma(const void* src, void* dst, uint64_t n16, uint32_t tile16, uint32_t blocks,
+                        uint32_t lds_bytes, int pipe, void* stream) {
+  if (tile16 == 0 || tile16 > 4096u) return -22;
+  const uint64_t ntiles = (n16 + tile16 - 1) / tile16;
+  size_t lds = (size_t)tile16 * 16 * (pipe ? 2 : 1);
+  if (lds_bytes > lds) lds = lds_bytes;
+  const void* fn = pipe ? reinterpret_cast<const void*>(&rudp::copy_tile_dma_kernel<true>)
+                        : reinterpret_cast<const void*>(&rudp::copy_tile_dma_kernel<false>);
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  const uint32_t grid = pipe ? (uint32_t)(blocks < ntiles ? blocks : ntiles) : (uint32_t)ntiles;
+  if (pipe)
+    hipLaunchKernelGGL(rudp::copy_tile_dma_kernel<true>, dim3(grid), dim3(rudp::kBlock), lds,
+                       (hipStream_t)stream, (const rudp::u32x4*)src, (rudp::u32x4*)dst, n16, tile16);
+  else
+    hipLaunchKernelGGL(rudp::copy_tile_dma_kernel<false>, dim3(grid), dim3(rudp::kBlock), lds,
+                       (hipStream_t)stream, (const rudp::u32x4*)src, (rudp::u32x4*)dst, n16, tile16);
   return (int)hipGetLastError();
 }
 
@@ -182,7 +246,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // varlen tile; 18: varlen tile payload bytes at the hint; 20: register-streamed
 // encode; 21: its packets per workgroup (0 auto); 22: its load rounds in flight;
 // 23: output wave stores start on 64-B sector boundaries; 24: varlen frame
-// offsets by the three-pass scan (1) or hipcub (0).
+// offsets by the three-pass scan (1) or hipcub (0); 25: encode phase 1 by LDS-DMA;
+// 26: encode by fixed output spans; 27: span bytes per workgroup.
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
@@ -195,7 +260,8 @@ int rudpx_tune(int key, int value) {
             : key == 12 ? &t.decode_verify_tile : key == 13 ? &t.encode_ablate : key == 14 ? &t.varlen_vec : key == 15 ? &t.varlen_glog
             : key == 16 ? &t.varlen_tile : key == 17 ? &t.varlen_tile_maxT
             : key == 18 ? &t.varlen_tile_bytes : key == 20 ? &t.encode_stream
-            : key == 21 ? &t.encode_stream_T : key == 22 ? &t.encode_stream_R : key == 23 ? &t.out_align64 : key == 24 ? &t.varlen_scan : nullptr;
+            : key == 21 ? &t.encode_stream_T : key == 22 ? &t.encode_stream_R : key == 23 ? &t.out_align64 : key == 24 ? &t.varlen_scan : key == 25 ? &t.encode_dma
+            : key == 26 ? &t.encode_span : key == 27 ? &t.encode_span_bytes : nullptr;
   if (!slot) return -22;
   const int old = *slot;
   *slot = value;

@@ -1,0 +1,86 @@
+"""Span encode kernel (workgroups own fixed output byte spans; packets that
+cross a span boundary are finished by a second launch from the two partial
+sums) and the LDS-DMA phase 1 of the tile kernel, against the oracle.
+
+Bit-exact: frames and checksum sideband equal oracle/codec_np.encode (the
+restatement pinned to the reference utils/packet.py by tests/golden).
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+from oracle import codec_np, synth
+from rudp import _native, batch
+
+pytestmark = pytest.mark.gpu
+
+
+def _lib():
+    lib = _native.lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.rudpx_tune.restype = ctypes.c_int
+    return lib
+
+
+def _encode(cuda, seq, ack, flags, pay, layout):
+    import torch
+    tab = tuple(torch.from_numpy(np.ascontiguousarray(x)).to(cuda) for x in (seq, ack, flags))
+    fr, cs = batch.pack_batch(tab, torch.from_numpy(pay).to(cuda), layout, want_csum=True)
+    return fr.cpu().numpy(), cs.cpu().numpy()
+
+
+def _with(lib, settings, fn):
+    old = [(k, lib.rudpx_tune(k, v)) for k, v in settings]
+    try:
+        return fn()
+    finally:
+        for k, v in reversed(old):
+            lib.rudpx_tune(k, v)
+
+
+@pytest.mark.parametrize("L", [256, 272, 1024, 1472, 4096])
+def test_span_encode_vs_oracle(cuda, L):
+    lib = _lib()
+    for n in (1, 2, 3, 7, 64, 1001, 4099):
+        seq, ack, flags, pay = synth.synth(0x5A + L, n, n, L, ascii=False)
+        for layout in (5, 7):
+            want_fr, want_cs = codec_np.encode(seq, ack, flags, pay, layout)
+            for span in (1024, 8192, 32768):
+                if L + layout >= span:
+                    continue
+                fr, cs = _with(lib, [(26, 1), (27, span)],
+                               lambda: _encode(cuda, seq, ack, flags, pay, layout))
+                assert np.array_equal(fr, want_fr), (L, n, layout, span)
+                assert np.array_equal(cs, want_cs), (L, n, layout, span)
+
+
+def test_span_encode_repeated_launches_reuse_scratch(cuda):
+    """The straddle slots come from the stream-ordered pool (every slot is
+    written before the finishing launch reads it): back-to-back launches on
+    one stream stay exact."""
+    import torch
+    lib = _lib()
+    n, L = 20000, 1472
+    seq, ack, flags, pay = synth.synth(0x5B, 0, n, L, ascii=True)
+    want_fr, _ = codec_np.encode(seq, ack, flags, pay, 7)
+    tab = tuple(torch.from_numpy(x).to(cuda) for x in (seq, ack, flags))
+    p = torch.from_numpy(pay).to(cuda)
+
+    def run():
+        outs = [batch.pack_batch(tab, p, 7)[0] for _ in range(6)]
+        return [o.cpu().numpy() for o in outs]
+    for fr in _with(lib, [(26, 1), (27, 8192)], run):
+        assert np.array_equal(fr, want_fr)
+
+
+@pytest.mark.parametrize("L", [16, 64, 256, 1472])
+def test_dma_phase1_vs_oracle(cuda, L):
+    lib = _lib()
+    for n in (1, 17, 1031):
+        seq, ack, flags, pay = synth.synth(0x5C + L, n, n, L, ascii=False)
+        for layout in (5, 7):
+            want_fr, want_cs = codec_np.encode(seq, ack, flags, pay, layout)
+            fr, cs = _with(lib, [(25, 1)], lambda: _encode(cuda, seq, ack, flags, pay, layout))
+            assert np.array_equal(fr, want_fr), (L, n, layout)
+            assert np.array_equal(cs, want_cs), (L, n, layout)

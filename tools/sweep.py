@@ -35,6 +35,9 @@ lib.rudpx_copy_tile.restype = ctypes.c_int
 lib.rudpx_copy_tile_pipe.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
                                      ctypes.c_uint32, ctypes.c_uint32, ctypes.c_void_p]
 lib.rudpx_copy_tile_pipe.restype = ctypes.c_int
+lib.rudpx_copy_tile_dma.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
+                                    ctypes.c_uint32, ctypes.c_uint32, ctypes.c_int, ctypes.c_void_p]
+lib.rudpx_copy_tile_dma.restype = ctypes.c_int
 
 
 def event_ms(fn, reps=1):
@@ -178,6 +181,94 @@ def align_sweep(reps):
     return out
 
 
+def knob_sweep(reps, key, values, pre=()):
+    """Encode with one rudpx_tune knob at each of `values` (bit-exact check against the first);
+    `pre`: (key, value) settings held for the whole sweep."""
+    out = {}
+    for k, v in pre:
+        lib.rudpx_tune(k, v)
+    dev = torch.device("cuda", 0)
+    for L in (ENCODE_LS or (1472, 1024, 64)):
+        n = 1 << 20
+        nsets = 1 if L > 512 else 7
+        sets = []
+        for _ in range(nsets):
+            tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
+            sets.append((tab, pay, torch.empty((n, L + 7), dtype=torch.uint8, device=dev)))
+        it = [0]
+
+        def run():
+            tab, pay, fr = sets[it[0] % nsets]
+            it[0] += 1
+            batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
+        old = lib.rudpx_tune(key, values[0])
+        lib.rudpx_tune(key, old)
+        variants = {f"L{L}_key{key}_{v}": ((lambda v=v: lib.rudpx_tune(key, v)), run) for v in values}
+        res = interleaved(variants, reps)
+        tab0, pay0, _ = sets[0]
+        lib.rudpx_tune(key, values[0])
+        want, _ = batch.pack_batch(tab0, pay0, 7)
+        alg = n * (2 * L + 12)
+        for v in values:
+            lib.rudpx_tune(key, v)
+            got, _ = batch.pack_batch(tab0, pay0, 7)
+            k = f"L{L}_key{key}_{v}"
+            ms = res[k]
+            out[k] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0,
+                      "exact": bool(torch.equal(got, want))}
+        lib.rudpx_tune(key, old)
+        del sets
+        torch.cuda.empty_cache()
+    return out
+
+
+def multi_sweep(reps, specs):
+    """Encode under named settings: specs = [(name, [(key, value), ...])]; the
+    first is the reference for the bit-exact check.  Knobs are restored after."""
+    out = {}
+    dev = torch.device("cuda", 0)
+    keys = sorted({k for _, kv in specs for k, _ in kv})
+    for L in (ENCODE_LS or (1472, 1024, 64)):
+        n = 1 << 20
+        nsets = 1 if L > 512 else 7
+        sets = []
+        for _ in range(nsets):
+            tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
+            sets.append((tab, pay, torch.empty((n, L + 7), dtype=torch.uint8, device=dev)))
+        it = [0]
+
+        def run():
+            tab, pay, fr = sets[it[0] % nsets]
+            it[0] += 1
+            batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
+        defaults = {}
+        for k in keys:  # read each knob's default (set returns the old value)
+            defaults[k] = lib.rudpx_tune(k, 0)
+            lib.rudpx_tune(k, defaults[k])
+
+        def apply(kv):
+            for k in keys:
+                lib.rudpx_tune(k, defaults[k])
+            for k, v in kv:
+                lib.rudpx_tune(k, v)
+        variants = {f"L{L}_{name}": ((lambda kv=kv: apply(kv)), run) for name, kv in specs}
+        res = interleaved(variants, reps)
+        tab0, pay0, _ = sets[0]
+        alg = n * (2 * L + 12)
+        want = None
+        for name, kv in specs:
+            apply(kv)
+            got, _ = batch.pack_batch(tab0, pay0, 7)
+            want = got if want is None else want
+            ms = res[f"L{L}_{name}"]
+            out[f"L{L}_{name}"] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0,
+                                   "exact": bool(torch.equal(got, want))}
+        apply([])
+        del sets
+        torch.cuda.empty_cache()
+    return out
+
+
 def stream_sweep(reps):
     """Register-streamed encode (rudpx_tune 20-22) against the LDS-tile encode."""
     out = {}
@@ -311,6 +402,36 @@ def copy_sweep(reps):
                 lambda kb=kb, per_cu=per_cu: lib.rudpx_copy_tile_pipe(
                     a.data_ptr(), b.data_ptr(), nbytes // 16, kb * 64, per_cu * 256, 0, stream))
     res = interleaved(variants, reps)
+    return {k: {"ms": ms, "TBs": 2 * nbytes / ms / 1e9} for k, ms in res.items()}
+
+
+def copydma_sweep(reps):
+    """Tiled copies staged by LDS-DMA, one tile per block or persistent double-buffered."""
+    dev = torch.device("cuda", 0)
+    nbytes = (1 << 20) * 1472
+    a = torch.empty(nbytes, dtype=torch.uint8, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(7)
+    stream = torch.cuda.current_stream().cuda_stream
+    n16 = nbytes // 16
+    variants = {"copy_vpt1_nt1": (lambda: None, lambda: lib.rudpx_copy_vpt(a.data_ptr(), b.data_ptr(), n16, 1, 1, stream))}
+    for kb in (8, 24):
+        for per_cu in (0, 5):
+            lds = (160 * 1024 // per_cu) & ~15 if per_cu else 0
+            variants[f"regs_tile{kb}k_percu{per_cu}"] = (
+                lambda: None, lambda kb=kb, lds=lds: lib.rudpx_copy_tile(a.data_ptr(), b.data_ptr(), n16, kb * 64, lds, stream))
+            variants[f"dma_tile{kb}k_percu{per_cu}"] = (
+                lambda: None, lambda kb=kb, lds=lds: lib.rudpx_copy_tile_dma(a.data_ptr(), b.data_ptr(), n16, kb * 64, 0, lds, 0, stream))
+    for kb in (8, 12, 24):
+        for per_cu in (1, 2, 3, 4, 6):
+            if 2 * kb * per_cu > 160:
+                continue
+            variants[f"dma_pipe{kb}k_blocks{per_cu}x256"] = (
+                lambda: None, lambda kb=kb, per_cu=per_cu: lib.rudpx_copy_tile_dma(
+                    a.data_ptr(), b.data_ptr(), n16, kb * 64, per_cu * 256, (160 * 1024 // per_cu) & ~15, 1, stream))
+    res = interleaved(variants, reps)
+    torch.cuda.synchronize()
+    assert torch.equal(a, b), "copy mismatch"
     return {k: {"ms": ms, "TBs": 2 * nbytes / ms / 1e9} for k, ms in res.items()}
 
 
@@ -474,11 +595,16 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--L", type=int, default=1472, help="payload length for --only ablate")
-    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "stream", "align"])
+    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "stream", "align", "knob", "copydma", "multi"])
     ap.add_argument("--blocks", type=str, default="", help="encode sweep: workgroup sizes, e.g. 256,512,1024")
     ap.add_argument("--encode-L", type=str, default="", help="encode sweep: payload lengths, e.g. 1472")
     ap.add_argument("--ablate", action="store_true", help="stream sweep: add stage ablations")
     ap.add_argument("--percu", type=str, default="", help="encode sweep: tiles-per-CU caps, e.g. 3,4,5")
+    ap.add_argument("--key", type=int, default=25, help="--only knob: rudpx_tune key")
+    ap.add_argument("--values", type=str, default="0,1", help="--only knob: values (first = reference)")
+    ap.add_argument("--pre", type=str, default="", help="--only knob: held settings, e.g. 26=1,6=4")
+    ap.add_argument("--specs", type=str, default="",
+                    help="--only multi: name:key=val,key=val;name2:... (first = reference)")
     ap.add_argument("--tiles", type=str, default="", help="encode sweep: packets per tile, e.g. 8,16")
     args = ap.parse_args()
     global BLOCKS_OVERRIDE, ENCODE_LS, STREAM_ABLATE, PERCU_OVERRIDE, TILES_OVERRIDE
@@ -500,6 +626,17 @@ def main():
         result["utf8"] = utf8_sweep(args.reps)
     if args.only == "varlen":
         result["varlen"] = varlen_sweep(args.reps)
+    if args.only == "copydma":
+        result["copydma"] = copydma_sweep(args.reps)
+    if args.only == "multi":
+        specs = []
+        for part in args.specs.split(";"):
+            name, _, kvs = part.partition(":")
+            specs.append((name, [tuple(int(y) for y in x.split("=")) for x in kvs.split(",") if x]))
+        result["multi"] = multi_sweep(args.reps, specs)
+    if args.only == "knob":
+        pre = [tuple(int(y) for y in x.split("=")) for x in args.pre.split(",") if x]
+        result["knob"] = knob_sweep(args.reps, args.key, [int(x) for x in args.values.split(",")], pre)
     if args.only == "align":
         result["align"] = align_sweep(args.reps)
     if args.only == "stream":
