@@ -365,6 +365,7 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, ui
   if ((rc = dev_scope.set(device))) return rc;
   DecodeArgs a{};
   a.align64 = tuning().out_align64 == 1 ? 1u : 0u;
+  a.dma = tuning().tile_dma ? 1u : 0u;
   a.frames = d_frames;
   a.csum_in = d_csum_in_or_null;
   a.seq = d_seq;
@@ -472,6 +473,7 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
   if (tuning().varlen_vec && tuning().varlen_tile)
     varlen_tile_geometry(in->payload_len, &a.tile_T, &a.tile_glog, &a.tile_cap);
   a.align64 = tuning().out_align64 == 1 ? 1u : 0u;
+  a.dma = tuning().tile_dma ? 1u : 0u;
   rc = launch_encode_varlen(a, layout, s);
   if (rc) return hip_fail((hipError_t)rc, "varlen encode launch");
   return 0;

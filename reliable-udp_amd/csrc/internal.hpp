@@ -47,6 +47,7 @@ struct DecodeArgs {
   uint32_t F;               // frame bytes
   uint32_t glog;            // log2(lanes per packet)
   uint32_t align64;         // tile kernel: wave loads/stores start on 64-B sector boundaries
+  uint32_t dma;             // tile kernel: phase 1 by LDS-DMA (when align64 is off)
 };
 
 struct SynthArgs {
@@ -88,6 +89,7 @@ struct VarlenArgs {
   uint32_t tile_glog;
   uint32_t tile_cap;
   uint32_t align64;               // tile kernel: wave stores start on 64-B sector boundaries
+  uint32_t dma;                   // tile kernel: phase 1 by LDS-DMA
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -153,6 +155,10 @@ struct Tuning {
   int encode_dma = 1;
   // Encode by fixed output spans (encode_span_kernel; opt-in, bit-exact, not
   // faster at MTU size: 1M x 1472 B 0.530 vs 0.518 ms, x 1024 B 0.352 vs 0.363).
+  // Decode and varlen-encode tile phase 1 by LDS-DMA: opt-in, measured no
+  // faster (1M x 64 B verify 0.0208 vs 0.0198 ms, copy-out 0.0263 vs 0.0253;
+  // 1472 B varlen encode 0.641 vs 0.632; profiles/r01/sweeps/tile_dma.json).
+  int tile_dma = 0;
   int encode_span = 0;
   int encode_span_bytes = 8192;  // span kernel: output bytes per workgroup (multiple of 64)
   int varlen_scan = 1;    // frame offsets: 1 = reduce-then-scan (scan.hip), 0 = hipcub

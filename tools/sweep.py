@@ -125,11 +125,12 @@ def encode_sweep(reps):
     return out
 
 
-def align_sweep(reps):
-    """Encode tile kernel with phase-2 wave stores on 64-B sector boundaries (key 23) or not."""
+def align_sweep(reps, key=23, values=(1, 0), names=("align64", "align16")):
+    """Encode / verify / copy-out decode / varlen encode under one rudpx_tune knob:
+    by default phase-2 wave stores on 64-B sector boundaries (key 23) or not."""
     out = {}
     dev = torch.device("cuda", 0)
-    for L in (1472, 1024, 64):
+    for L in (ENCODE_LS or (1472, 1024, 64)):
         n = 1 << 20
         nsets = 1 if L > 512 else 7
         sets = []
@@ -168,11 +169,13 @@ def align_sweep(reps):
         algs = {"encode": n * (2 * L + 12), "verify": n * (L + 13), "copyout": n * (2 * L + 13),
                 "varlen_encode": n * (2 * L + 24)}
         variants = {}
+        old = lib.rudpx_tune(key, values[0])
+        lib.rudpx_tune(key, old)
         for op, fn in (("encode", run), ("verify", verify), ("copyout", copyout), ("varlen_encode", venc)):
-            variants[f"L{L}_{op}_align64"] = (lambda: lib.rudpx_tune(23, 1), fn)
-            variants[f"L{L}_{op}_align16"] = (lambda: lib.rudpx_tune(23, 0), fn)
+            for v, nm in zip(values, names):
+                variants[f"L{L}_{op}_{nm}"] = (lambda v=v: lib.rudpx_tune(key, v), fn)
         res = interleaved(variants, reps)
-        lib.rudpx_tune(23, -1)
+        lib.rudpx_tune(key, old)
         for k, ms in res.items():
             alg = algs[k.split("_", 1)[1].rsplit("_", 1)[0]]
             out[k] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0}
@@ -595,7 +598,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--L", type=int, default=1472, help="payload length for --only ablate")
-    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "stream", "align", "knob", "copydma", "multi"])
+    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "stream", "align", "knob", "copydma", "multi", "opsknob"])
     ap.add_argument("--blocks", type=str, default="", help="encode sweep: workgroup sizes, e.g. 256,512,1024")
     ap.add_argument("--encode-L", type=str, default="", help="encode sweep: payload lengths, e.g. 1472")
     ap.add_argument("--ablate", action="store_true", help="stream sweep: add stage ablations")
@@ -639,6 +642,9 @@ def main():
         result["knob"] = knob_sweep(args.reps, args.key, [int(x) for x in args.values.split(",")], pre)
     if args.only == "align":
         result["align"] = align_sweep(args.reps)
+    if args.only == "opsknob":  # every tile op under --key at --values (names v<value>)
+        vals = tuple(int(x) for x in args.values.split(","))
+        result["opsknob"] = align_sweep(args.reps, args.key, vals, tuple(f"v{v}" for v in vals))
     if args.only == "stream":
         result["stream"] = stream_sweep(args.reps)
     if args.only == "varlen_enc":
