@@ -107,6 +107,13 @@ EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t*
   if (encode_tile_ok(a.L, in->payload, frames)) {
     encode_tile_geometry(a.L, &a.T, &a.glog);
     a.hdr_bytes = ((a.T + 1u) * 8u + 15u) & ~15u;
+    const int early = tuning().encode_early_table;
+    a.early_table = (early == 1 || (early < 0 && a.T * a.L <= 16384u)) ? 1u : 0u;
+    if (tuning().encode_hchunk && a.T % 16u == 0 && !tuning().encode_ablate) {
+      a.hchunk = 1;
+      a.hc_off = a.hdr_bytes;
+      a.hdr_bytes += (a.T + 1u) * 32u;
+    }
     a.invF = ((1ull << 32) + F - 1ull) / F;
     a.num_tiles = (uint32_t)((a.n + a.T - 1) / a.T);
     a.xcd_swizzle = tuning().encode_xcd_swizzle ? 1u : 0u;
@@ -474,6 +481,11 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
     varlen_tile_geometry(in->payload_len, &a.tile_T, &a.tile_glog, &a.tile_cap);
   a.align64 = tuning().out_align64 == 1 ? 1u : 0u;
   a.dma = tuning().tile_dma ? 1u : 0u;
+  // Header-table loads before phase 1 only when forced (rudpx_tune 30 = 1):
+  // unlike fixed-length encode, the varlen tile measured 0.5-2% slower with
+  // them at every length (1M x 64 B 0.0934 vs 0.0915 ms; its offset loads
+  // already precede phase 1; profiles/r01/sweeps/encode_early_table.json).
+  a.early_table = tuning().encode_early_table == 1 ? 1u : 0u;
   rc = launch_encode_varlen(a, layout, s);
   if (rc) return hip_fail((hipError_t)rc, "varlen encode launch");
   return 0;

@@ -41,6 +41,48 @@ __device__ __forceinline__ void store16(u32x4 v, u32x4* p) {
     *p = v;
 }
 
+// Aligned 16-B chunk X of the output around a packet's header, P = the
+// output offset of its payload: the previous packet's last payload bytes
+// (`tail`: its last 16), the header bytes `h` (frame order, packed
+// little-endian) and the first payload bytes (`head`).  X is one of the one
+// or two chunks [floor16(P - H), ceil16(P)).
+template <int H>
+__device__ __forceinline__ u32x4 header_chunk(uint64_t X, uint64_t P, uint64_t h, u32x4 tail,
+                                              u32x4 head) {
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  const int k0 = (int)(int64_t)(X - (P - H));  // frame position of chunk byte 0 (> -16)
+  u32x4 w = zero;
+  if (k0 < 0) w = funnel32(tail, zero, (uint32_t)(k0 + 16));  // previous payload's last bytes
+  const uint32_t d = (uint32_t)(P - X);                        // payload starts d bytes in
+  if (d < 16) {
+    const u32x4 hp = funnel32(zero, head, 16u - d);
+    w.x |= hp.x; w.y |= hp.y; w.z |= hp.z; w.w |= hp.w;
+  }
+  uint64_t lo = lo64(w), hi = hi64(w);
+  if (k0 >= 0) {
+    lo |= h >> (8 * k0);
+  } else {
+    const int sh = -k0;
+    if (sh < 8) {
+      lo |= h << (8 * sh);
+      hi |= h >> (64 - 8 * sh);
+    } else {
+      hi |= h << (8 * (sh - 8));
+    }
+  }
+  return make_u32x4(lo, hi);
+}
+
+// Writes the one or two header chunks of the packet whose payload starts at
+// output offset P.
+template <int H>
+__device__ __forceinline__ void store_header_chunks(unsigned char* out, uint64_t P, uint64_t h,
+                                                    u32x4 tail, u32x4 head) {
+  const uint64_t X0 = (P - H) & ~15ull, X1 = (P + 15u) & ~15ull;
+  for (uint64_t X = X0; X < X1; X += 16)
+    __builtin_nontemporal_store(header_chunk<H>(X, P, h, tail, head), reinterpret_cast<u32x4*>(out + X));
+}
+
 // Phase 2 of the encode tile:
 // output-stationary aligned 16 B chunks assembled from the LDS payload tile
 // and header words.
@@ -117,6 +159,44 @@ __device__ __forceinline__ void encode_phase2(const EncodeTileArgs& a, const uns
   }
 }
 
+// Phase 2 with prebuilt header chunks (T % 16 == 0, so the tile starts on a
+// 16-B boundary).  A chunk is either pure payload of one packet (frame
+// positions [r, r + 16) inside [H, F)) — one byte-shifted LDS window — or one
+// of the 1-2 chunks over a header, which the packet's leader built in the sum
+// pass (lds_hc[2q + slot]).  Stores stay one 1 KiB run per wave-instruction.
+template <int H, bool NTS, int BLOCK>
+__device__ __forceinline__ void encode_phase2_hc(const EncodeTileArgs& a, const unsigned char* lds_pay,
+                                                 const u32x4* lds_hc, uint64_t p0, uint32_t Tv,
+                                                 uint32_t tid) {
+  const uint32_t L = a.L, F = L + H;
+  const uint32_t nbytes = Tv * F;
+  unsigned char* out = a.frames + p0 * (uint64_t)F;
+  const uint32_t nfull = nbytes >> 4;
+  const uint32_t nall = (nbytes + 15u) >> 4;
+  uint32_t npre = a.out_align64 ? ((uint32_t)(-(uintptr_t)out) & 63u) >> 4 : 0u;
+  if (npre > nfull) npre = nfull;
+  const uint32_t* pay_dw = reinterpret_cast<const uint32_t*>(lds_pay);
+  for (uint32_t k = tid; k < nall; k += BLOCK) {
+    const uint32_t i = k < nfull ? (k + npre < nfull ? k + npre : k + npre - nfull) : k;
+    const uint32_t x = 16u * i;
+    const uint32_t qq = (uint32_t)(((uint64_t)x * a.invF) >> 32);  // x / F
+    const uint32_t r = x - qq * F;
+    const uint32_t ph = r < (uint32_t)H ? qq : qq + 1u;  // packet whose header the chunk holds
+    u32x4 v;
+    if ((r >= (uint32_t)H && r + 16u <= F) || ph >= Tv) {
+      v = window16_dw(pay_dw, kLdsGuard + qq * L + r - H);
+    } else {
+      v = lds_hc[2u * ph + ((x - ((ph * F) & ~15u)) >> 4)];
+    }
+    if (i < nfull) {
+      store16<NTS>(v, reinterpret_cast<u32x4*>(out + x));
+    } else {  // the batch's last bytes
+      const uint32_t d[4] = {v.x, v.y, v.z, v.w};
+      for (uint32_t b = 0; b < nbytes - x; ++b) out[x + b] = (unsigned char)(d[b >> 2] >> (8 * (b & 3)));
+    }
+  }
+}
+
 template <int H, bool NTL, bool NTS, int P1, bool CONTIG, int BLOCK = kBlock, bool DMA = false>
 __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -149,6 +229,15 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   const uint32_t q = tid >> glog;
   const uint32_t g = tid & (G - 1u);
   const uint32_t V = L >> 4;  // 16 B vectors per packet
+  // Header-table loads can go out before the payload stream, so their latency
+  // overlaps phase 1 instead of adding a round trip after the barrier.
+  const bool tab = !(a.ablate & 4u);
+  uint32_t t_seq = 1u, t_ack = 2u, t_flags = 3u;
+  if (a.early_table && tab && g == 0 && q < Tv) {
+    t_seq = a.seq[p0 + q];
+    t_ack = a.ack[p0 + q];
+    t_flags = a.flags[p0 + q];
+  }
   uint32_t sum = 0;
   if (CONTIG) {
     // The tile's payload is one contiguous run: stream it like a copy (lane t
@@ -210,49 +299,27 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
   if (g == 0 && q < Tv) {
     const uint64_t p = p0 + q;
-    const bool tab = !(a.ablate & 4u);
-    const uint32_t s = tab ? a.seq[p] : 1u, k = tab ? a.ack[p] : 2u, f = tab ? a.flags[p] : 3u;
+    const bool late = tab && !a.early_table;
+    const uint32_t s = late ? a.seq[p] : t_seq, k = late ? a.ack[p] : t_ack, f = late ? a.flags[p] : t_flags;
     const uint32_t c = packet_csum(sum, s, k, f);
-    lds_hdr[q] = pack_header<H>(s, k, f, c);
+    const uint64_t h = pack_header<H>(s, k, f, c);
+    lds_hdr[q] = h;
     if (a.csum) a.csum[p] = (uint16_t)c;
+    if (a.hchunk) {  // this packet's 1-2 header chunks, for encode_phase2_hc
+      const u32x4* img = reinterpret_cast<const u32x4*>(lds_pay + kLdsGuard);
+      const uint32_t P = q * (L + H) + H;
+      u32x4* hc = reinterpret_cast<u32x4*>(lds + a.hc_off) + 2u * q;
+      const uint32_t X0 = (P - H) & ~15u, X1 = (P + 15u) & ~15u;
+      for (uint32_t X = X0; X < X1; X += 16)
+        hc[(X - X0) >> 4] = header_chunk<H>(X, P, h, img[q * V - 1u], img[q * V]);
+    }
   }
   __syncthreads();
 
-  encode_phase2<H, NTS, BLOCK>(a, lds_pay, lds_hdr, p0, Tv, tid);
-}
-
-// The one or two aligned 16-B chunks [floor16(P - H), ceil16(P)) that hold a
-// packet's header, P = the output offset of its payload: the previous
-// packet's last payload bytes (`tail`: its last 16), the header bytes `h`
-// (frame order, packed little-endian) and the first payload bytes (`head`).
-template <int H>
-__device__ __forceinline__ void store_header_chunks(unsigned char* out, uint64_t P, uint64_t h,
-                                                    u32x4 tail, u32x4 head) {
-  const u32x4 zero = {0u, 0u, 0u, 0u};
-  const uint64_t X0 = (P - H) & ~15ull, X1 = (P + 15u) & ~15ull;
-  for (uint64_t X = X0; X < X1; X += 16) {
-    const int k0 = (int)(int64_t)(X - (P - H));  // frame position of chunk byte 0 (> -16)
-    u32x4 w = zero;
-    if (k0 < 0) w = funnel32(tail, zero, (uint32_t)(k0 + 16));  // previous payload's last bytes
-    const uint32_t d = (uint32_t)(P - X);                        // payload starts d bytes in
-    if (d < 16) {
-      const u32x4 hp = funnel32(zero, head, 16u - d);
-      w.x |= hp.x; w.y |= hp.y; w.z |= hp.z; w.w |= hp.w;
-    }
-    uint64_t lo = lo64(w), hi = hi64(w);
-    if (k0 >= 0) {
-      lo |= h >> (8 * k0);
-    } else {
-      const int sh = -k0;
-      if (sh < 8) {
-        lo |= h << (8 * sh);
-        hi |= h >> (64 - 8 * sh);
-      } else {
-        hi |= h << (8 * (sh - 8));
-      }
-    }
-    __builtin_nontemporal_store(make_u32x4(lo, hi), reinterpret_cast<u32x4*>(out + X));
-  }
+  if (a.hchunk)
+    encode_phase2_hc<H, NTS, BLOCK>(a, lds_pay, reinterpret_cast<const u32x4*>(lds + a.hc_off), p0, Tv, tid);
+  else
+    encode_phase2<H, NTS, BLOCK>(a, lds_pay, lds_hdr, p0, Tv, tid);
 }
 
 // floor(x / F) for x < 2^52 from a double reciprocal and one correction

@@ -28,6 +28,9 @@ struct EncodeTileArgs {
   // a packet crossing the boundary after span b leaves its two partial
   // payload sums in straddle[2b] (span b's part) and straddle[2b + 1]
   // (span b+1's), and a second launch finishes it
+  uint32_t early_table;     // tile kernel: header-table loads issued before phase 1
+  uint32_t hchunk;          // tile kernel (T % 16 == 0): leaders prebuild header chunks in LDS
+  uint32_t hc_off;          // LDS byte offset of the header-chunk array [T + 1][2] x 16 B
   uint32_t span;
   uint32_t span_glog;       // log2 lanes per packet in the span sum pass
   double rcpF;              // 1.0 / (L + H)
@@ -90,6 +93,7 @@ struct VarlenArgs {
   uint32_t tile_cap;
   uint32_t align64;               // tile kernel: wave stores start on 64-B sector boundaries
   uint32_t dma;                   // tile kernel: phase 1 by LDS-DMA
+  uint32_t early_table;           // tile kernel: header-table loads before phase 1
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -159,6 +163,15 @@ struct Tuning {
   // faster (1M x 64 B verify 0.0208 vs 0.0198 ms, copy-out 0.0263 vs 0.0253;
   // 1472 B varlen encode 0.641 vs 0.632; profiles/r01/sweeps/tile_dma.json).
   int tile_dma = 0;
+  // Encode tile phase 2 with header chunks prebuilt by the packet leaders
+  // (T % 16 == 0): 1M x 64 B 0.0295 -> 0.0287 ms, x 256 B 0.0962 -> 0.0938,
+  // x 1024 B 0.3712 -> 0.3683, x 1472 B equal (profiles/r01/sweeps/encode_hchunk.json).
+  int encode_hchunk = 1;
+  // Encode tile header-table loads before phase 1 (1), after it (0), or -1 =
+  // automatic: before for tiles of at most 16 KiB of payload (1M x 64 B
+  // 0.0287 -> 0.0267 ms, x 256 B 0.0934 -> 0.0892, x 1024 B 0.3606 ->
+  // 0.3557), after above (x 1472 B 0.5208 vs 0.5291 early).
+  int encode_early_table = -1;
   int encode_span = 0;
   int encode_span_bytes = 8192;  // span kernel: output bytes per workgroup (multiple of 64)
   int varlen_scan = 1;    // frame offsets: 1 = reduce-then-scan (scan.hip), 0 = hipcub

@@ -249,6 +249,14 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_tile_kernel(VarlenArgs a
   const uint64_t p0 = (uint64_t)blockIdx.x * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
+  // Header-table loads first (small tiles): their latency overlaps the
+  // offset loads and phase 1 instead of following the barrier.
+  uint32_t t_seq = 0, t_ack = 0, t_flags = 0;
+  if (a.early_table && g == 0 && q < Tv) {
+    t_seq = a.seq_in[p0 + q];
+    t_ack = a.ack_in[p0 + q];
+    t_flags = a.flags_in[p0 + q];
+  }
   const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
   const uint64_t po0 = fo0 - p0 * (uint64_t)H;
   const uint64_t po_end = fo_end - (p0 + Tv) * (uint64_t)H;
@@ -319,7 +327,9 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_tile_kernel(VarlenArgs a
   for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
   if (g == 0 && q < Tv) {
     const uint64_t p = p0 + q;
-    const uint32_t s = a.seq_in[p], k = a.ack_in[p], f = a.flags_in[p];
+    const bool late = !a.early_table;
+    const uint32_t s = late ? a.seq_in[p] : t_seq, k = late ? a.ack_in[p] : t_ack,
+                   f = late ? a.flags_in[p] : t_flags;
     const uint32_t c = packet_csum(sum, s, k, f);
     lds_hdr[q] = pack_header<H>(s, k, f, c);
     if (a.csum) a.csum[p] = (uint16_t)c;

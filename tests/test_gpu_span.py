@@ -84,3 +84,23 @@ def test_dma_phase1_vs_oracle(cuda, L):
             fr, cs = _with(lib, [(25, 1)], lambda: _encode(cuda, seq, ack, flags, pay, layout))
             assert np.array_equal(fr, want_fr), (L, n, layout)
             assert np.array_equal(cs, want_cs), (L, n, layout)
+
+
+@pytest.mark.parametrize("L", [16, 32, 48, 64, 256, 1024, 1472, 4096])
+def test_prebuilt_header_chunks_vs_oracle(cuda, L):
+    """Encode phase 2 with header chunks prebuilt by the packet leaders
+    (rudpx_tune 29), every tile size with T % 16 == 0, both store dealings,
+    header-table loads before or after phase 1 (rudpx_tune 30)."""
+    lib = _lib()
+    for n in (1, 2, 15, 16, 17, 257, 1031):
+        seq, ack, flags, pay = synth.synth(0x5D + L, n, n, L, ascii=False)
+        for layout in (5, 7):
+            want_fr, want_cs = codec_np.encode(seq, ack, flags, pay, layout)
+            for tile in (0, 16, 32, 256):
+                if tile and tile * L > 65536:
+                    continue
+                for align, early in ((0, 0), (1, 0), (0, 1), (-1, -1)):
+                    fr, cs = _with(lib, [(29, 1), (2, tile), (23, align), (30, early)],
+                                   lambda: _encode(cuda, seq, ack, flags, pay, layout))
+                    assert np.array_equal(fr, want_fr), (L, n, layout, tile, align, early)
+                    assert np.array_equal(cs, want_cs), (L, n, layout, tile, align, early)
