@@ -249,7 +249,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // offsets by the three-pass scan (1) or hipcub (0); 25: encode phase 1 by LDS-DMA;
 // 26: encode by fixed output spans; 27: span bytes per workgroup; 28: decode and
 // varlen-encode tile phase 1 by LDS-DMA; 29: encode phase 2 with prebuilt header chunks;
-// 30: encode header-table loads before phase 1.
+// 30: encode header-table loads before phase 1; 31: fixed-stride UTF-8 validation
+// through LDS tiles.
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
@@ -266,7 +267,8 @@ int rudpx_tune(int key, int value) {
             : key == 26 ? &t.encode_span : key == 27 ? &t.encode_span_bytes
             : key == 28 ? &t.tile_dma
             : key == 29 ? &t.encode_hchunk
-            : key == 30 ? &t.encode_early_table : nullptr;
+            : key == 30 ? &t.encode_early_table
+            : key == 31 ? &t.utf8_tile : nullptr;
   if (!slot) return -22;
   const int old = *slot;
   *slot = value;

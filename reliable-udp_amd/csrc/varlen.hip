@@ -710,6 +710,76 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_vec_kernel(Utf8Args a) {
   if (valid_p && g == 0) a.valid[p] = bad ? 0 : 1;
 }
 
+// Fixed-stride frames through an LDS tile (frames 16-B aligned, H < F,
+// T = 256 / G frames per workgroup with T % 16 == 0, so the tile starts on a
+// 16-B boundary): the decode tile kernel's shape.  Phase 1 streams the tile's
+// T*F bytes into LDS as one contiguous run (1 KiB per wave-instruction);
+// phase 2 gives G lanes to each frame, which read its payload as aligned LDS
+// chunks: a chunk whose payload bytes are ASCII with nothing pending from the
+// three bytes before it (an aligned LDS dword, no shuffles) is done; any other
+// runs the byte checks.  The per-lane, per-frame strided global loads of the
+// vector kernel gave 256-B runs per wave-instruction instead.
+__global__ void __launch_bounds__(kBlock) validate_utf8_tile_kernel(Utf8Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t glog = a.glog, G = 1u << glog, T = kBlock >> glog;
+  const uint32_t q = tid >> glog, g = tid & (G - 1u);
+  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  const uint64_t left = a.n - p0;
+  const uint32_t Tv = left < T ? (uint32_t)left : T;
+  const uint32_t F = a.F, H = a.H;
+  const uint64_t total = a.n * (uint64_t)F;
+  const uint64_t base = p0 * (uint64_t)F;  // 16-B aligned: T % 16 == 0
+  const uint32_t nbytes = Tv * F;
+  const uint32_t nvec = (nbytes + 15u) >> 4;
+  u32x4* tile = reinterpret_cast<u32x4*>(lds + 16);  // 16 B of guard before the tile
+  {
+    const uint64_t whole = (total - base) >> 4;
+    const uint32_t ndma = whole < nvec ? (uint32_t)whole : nvec;
+    const uint32_t lane = tid & 63u;
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.frames + base);
+    for (uint32_t v0 = tid & ~63u; v0 < ndma; v0 += kBlock)
+      if (v0 + lane < ndma)
+        __builtin_amdgcn_global_load_lds(
+            (const void __attribute__((address_space(1)))*)(src + v0 + lane),
+            (void __attribute__((address_space(3)))*)(tile + v0), 16, 0, 2);
+    if (ndma < nvec && tid == 0) tile[ndma] = load16_guarded(a.frames, base + 16ull * ndma, total);
+  }
+  __syncthreads();
+  uint32_t bad = 0;
+  if (q < Tv) {
+    const uint32_t s = q * F + H, fe = q * F + F;  // payload bytes [s, fe) of the tile
+    const uint32_t c_lo = s >> 4, c_hi = (fe - 1u) >> 4;
+    const uint32_t* dw = reinterpret_cast<const uint32_t*>(lds + 16);
+    for (uint32_t c = c_lo + g; c <= c_hi; c += G) {
+      const uint32_t x = c << 4;
+      const u32x4 v = tile[c];
+      const uint32_t prev = dw[(x >> 2) - 1u];  // bytes x-4 .. x-1 (the guard before x = 0)
+      uint32_t p3 = x >= s + 3 ? (prev >> 8) & 0xFFu : 0u;
+      uint32_t p2 = x >= s + 2 ? (prev >> 16) & 0xFFu : 0u;
+      uint32_t p1 = x >= s + 1 ? prev >> 24 : 0u;
+      const int lo_b = (int)s - (int)x, hi_b = (int)fe - (int)x;
+      const uint64_t pl = lo64(v) & byte_mask(lo_b, hi_b), ph = hi64(v) & byte_mask(lo_b - 8, hi_b - 8);
+      if (((pl | ph) & 0x8080808080808080ull) == 0 && p1 < 0xC0 && p2 < 0xC0 && p3 < 0xC0) continue;
+      if (bad) continue;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const uint32_t y = x + (uint32_t)k;
+        if (y < s || y >= fe) continue;
+        const uint32_t cb = byte_of(v, k);
+        bad |= utf8_byte_ok(cb, p1, p2, p3) ? 0u : 1u;
+        p3 = p2;
+        p2 = p1;
+        p1 = cb;
+      }
+      if (c == c_hi)  // the frame's last chunk: nothing may still be expected
+        bad |= (utf8_need(p1) >= 1 || utf8_need(p2) >= 2 || utf8_need(p3) >= 3) ? 1u : 0u;
+    }
+  }
+  for (uint32_t m = G >> 1; m > 0; m >>= 1) bad |= __shfl_xor(bad, (int)m, 64);
+  if (g == 0 && q < Tv) a.valid[p0 + q] = bad ? 0 : 1;
+}
+
 template <int H>
 int launch_varlen_tile(const VarlenArgs& args, hipStream_t stream) {
   const uint64_t blocks = (args.n + args.tile_T - 1) / args.tile_T;
@@ -785,7 +855,19 @@ int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream)
 
 int launch_validate_utf8(const Utf8Args& args, hipStream_t stream) {
   if (args.n == 0) return 0;
-  if ((reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0) {
+  const bool aligned = (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0;
+  if (aligned && !args.frame_off && args.F > args.H && tuning().utf8_tile) {
+    Utf8Args a = args;
+    a.glog = decode_group_log2(args.F - args.H);  // T = 256 / G frames, a multiple of 16
+    const uint32_t T = kBlock >> a.glog;
+    const size_t lds = (((size_t)T * args.F + 15u) & ~size_t(15)) + 32u;
+    if (lds <= 65536) {
+      const uint64_t blocks = (args.n + T - 1) / T;
+      hipLaunchKernelGGL(validate_utf8_tile_kernel, dim3((uint32_t)blocks), dim3(kBlock), lds, stream, a);
+      return (int)hipGetLastError();
+    }
+  }
+  if (aligned) {
     // lanes per frame from the (typical) frame length: two+ 16-byte chunks per lane
     Utf8Args a = args;
     const uint32_t chunks = args.F / 16u + 1u;

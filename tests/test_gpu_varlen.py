@@ -489,3 +489,36 @@ def test_frame_offset_scans_agree(cuda, n):
             assert np.array_equal(host(res.frame_off), want), (n, scan)
     finally:
         lib.rudpx_tune(24, 1)
+
+
+@pytest.mark.parametrize("L", [1, 5, 16, 17, 64, 100, 256, 1472, 4096])
+def test_utf8_fixed_stride_tile_and_vector_kernels(cuda, L):
+    """Fixed-stride frames: the LDS-tile validator (default) and the per-frame
+    vector kernel (rudpx_tune 31 = 0) both equal Python's strict decoder, on
+    near-UTF-8 bodies cut or padded to L bytes (multibyte characters cross
+    16-B chunk and tile boundaries; both outcomes well represented)."""
+    import ctypes
+    from rudp import _native
+    lib = _native.lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.rudpx_tune.restype = ctypes.c_int
+    rng = np.random.default_rng(4321 + L)
+    n = 3001
+    bodies = []
+    for b in _near_utf8(rng, n):
+        reps = b * (L // max(1, len(b)) + 1) if b else b"A" * L
+        bodies.append((reps + b"A" * L)[:L])
+    for H in (5, 7):
+        hdr = b"\x12\x34\x00\x00\x80" + (b"\xbe\xef" if H == 7 else b"")
+        fr = np.frombuffer(b"".join(hdr + x for x in bodies), np.uint8).reshape(n, L + H)
+        off = np.arange(n + 1, dtype=np.int64) * (L + H)
+        want = codec_np.utf8_valid(fr.reshape(-1), off, H)
+        if L >= 16:
+            assert 0.05 < want.mean() < 0.95, want.mean()
+        for tile in (1, 0):
+            old = lib.rudpx_tune(31, tile)
+            try:
+                got = host(batch.validate_utf8(dev(fr, cuda), H))
+            finally:
+                lib.rudpx_tune(31, old)
+            assert np.array_equal(got, want), (L, H, tile)

@@ -574,18 +574,30 @@ def varlen_enc_sweep(reps):
 
 
 def utf8_sweep(reps):
-    """Strict UTF-8 validation over fixed-length frames (ASCII and random payloads)."""
+    """Strict UTF-8 validation over fixed-length frames (ASCII and random payloads),
+    LDS-tile kernel (rudpx_tune 31 = 1) against the per-frame vector kernel (0);
+    buffer sets rotate so every launch streams from HBM."""
     dev = torch.device("cuda", 0)
     out = {}
-    for L in (1472, 64):
+    for L in (ENCODE_LS or (1472, 1024, 256, 64)):
         n = 1 << 20
+        nsets = max(1, min(8, -(-(1 << 30) // (n * (L + 7)))))
         variants = {}
         for ascii in (True, False):
-            tab, pay = batch.synth_batch(n, L, 0x5EED0009, ascii=ascii, device=dev)
-            fr, _ = batch.pack_batch(tab, pay, 7)
-            variants[f"L{L}_{'ascii' if ascii else 'random'}"] = (
-                lambda: None, lambda fr=fr: batch.validate_utf8(fr, 7))
+            frs = []
+            for i in range(nsets):
+                tab, pay = batch.synth_batch(n, L, 0x5EED0009 + i, ascii=ascii, device=dev)
+                frs.append(batch.pack_batch(tab, pay, 7)[0])
+            it = [0]
+
+            def run(frs=frs, it=it):
+                batch.validate_utf8(frs[it[0] % len(frs)], 7)
+                it[0] += 1
+            for tile in (1, 0):
+                variants[f"L{L}_{'ascii' if ascii else 'random'}_tile{tile}"] = (
+                    lambda tile=tile: lib.rudpx_tune(31, tile), run)
         res = interleaved(variants, reps)
+        lib.rudpx_tune(31, 1)
         for k, ms in res.items():
             alg = n * (L + 7 + 1)
             out[k] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0}
