@@ -13,9 +13,13 @@
 //           mix64(position << 8 | byte) (order-sensitive, associative, so the
 //           lanes can split the frame), plus the length.
 //   pass 2  window: each workgroup stages the hashes of its 256 frames and the
-//           `window` frames before them in LDS; each frame scans its window
-//           there and confirms a hash hit byte by byte (exact, never a
-//           probabilistic answer).
+//           `window` frames before them in LDS and chains them into an LDS
+//           hash table (bucket heads by atomic exchange); each frame walks its
+//           bucket's chain for an entry inside its window with an equal hash
+//           and confirms the hit byte by byte (exact, never a probabilistic
+//           answer).  Expected O(1) per frame instead of `window` compares.
+//           The scan form (every frame compares its whole window) stays
+//           behind rudpx_tune key 32 = 0.
 #include "codec_device.hpp"
 #include "internal.hpp"
 
@@ -74,8 +78,14 @@ __device__ bool frames_equal(const DedupArgs& a, uint64_t i, uint64_t j) {
   frame_span(a, j, &oj, &lj);
   const uint32_t ci = li ? li : 5u, cj = lj ? lj : 5u;
   if (ci != cj) return false;
-  for (uint32_t k = 0; k < ci; ++k)
-    if (canon_byte(a, oi, li, k) != canon_byte(a, oj, lj, k)) return false;
+  // 16 bytes of each frame per step, all loads issued before the compares
+  for (uint32_t k0 = 0; k0 < ci; k0 += 16) {
+    uint32_t diff = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 16; ++k)
+      if (k0 + k < ci) diff |= canon_byte(a, oi, li, k0 + k) ^ canon_byte(a, oj, lj, k0 + k);
+    if (diff) return false;
+  }
   return true;
 }
 
@@ -101,11 +111,60 @@ __global__ void __launch_bounds__(kBlock) dedup_window_kernel(DedupArgs a) {
   a.dup[i] = dup;
 }
 
+// Table form of pass 2: LDS = hashes [cnt] u64, chain links [cnt] i32, bucket
+// heads [nb] i32 (nb a power of two, about 2x cnt).
+__global__ void __launch_bounds__(kBlock) dedup_table_kernel(DedupArgs a, uint32_t nb) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  const uint64_t first = (uint64_t)blockIdx.x * kBlock;
+  const uint64_t lo = first > a.window ? first - a.window : 0;
+  const uint64_t hi = first + kBlock < a.n ? first + kBlock : a.n;
+  const uint32_t cnt = (uint32_t)(hi - lo);
+  const uint32_t cap = a.window + kBlock;
+  uint64_t* lh = reinterpret_cast<uint64_t*>(lds_raw);  // [cap]
+  int* nxt = reinterpret_cast<int*>(lh + cap);          // [cap]
+  int* head = nxt + cap;                                 // [nb]
+  for (uint32_t b = threadIdx.x; b < nb; b += kBlock) head[b] = -1;
+  for (uint32_t e = threadIdx.x; e < cnt; e += kBlock) lh[e] = a.hash[lo + e];
+  __syncthreads();
+  for (uint32_t e = threadIdx.x; e < cnt; e += kBlock) {
+    const uint64_t h = lh[e];
+    nxt[e] = atomicExch(&head[(uint32_t)(h ^ (h >> 32)) & (nb - 1u)], (int)e);
+  }
+  __syncthreads();
+  const uint64_t i = first + threadIdx.x;
+  if (i >= a.n) return;
+  const uint32_t ei = (uint32_t)(i - lo);
+  const uint32_t emin = (uint32_t)((i > a.window ? i - a.window : 0) - lo);
+  const uint64_t h = lh[ei];
+  uint8_t dup = 0;
+  for (int e = head[(uint32_t)(h ^ (h >> 32)) & (nb - 1u)]; e >= 0; e = nxt[e]) {
+    const uint32_t u = (uint32_t)e;
+    if (u >= emin && u < ei && lh[u] == h && frames_equal(a, i, lo + u)) {
+      dup = 1;
+      break;
+    }
+  }
+  a.dup[i] = dup;
+}
+
 int launch_dedup(const DedupArgs& args, hipStream_t stream) {
   if (args.n == 0) return 0;
   const uint64_t hblocks = (args.n * kDedupLanes + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(dedup_hash_kernel, dim3((uint32_t)hblocks), dim3(kBlock), 0, stream, args);
   const uint64_t wblocks = (args.n + kBlock - 1) / kBlock;
+  if (tuning().dedup_table) {
+    const uint32_t cap = args.window + kBlock;
+    uint32_t nb = 256;
+    while (nb < 2u * cap && nb < 4096u) nb <<= 1;
+    const size_t lds = (size_t)cap * (sizeof(uint64_t) + sizeof(int)) + (size_t)nb * sizeof(int);
+    if (lds > 65536) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dedup_table_kernel),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return (int)e;
+    }
+    hipLaunchKernelGGL(dedup_table_kernel, dim3((uint32_t)wblocks), dim3(kBlock), lds, stream, args, nb);
+    return (int)hipGetLastError();
+  }
   const size_t lds = (size_t)(args.window + kBlock) * sizeof(uint64_t);
   hipLaunchKernelGGL(dedup_window_kernel, dim3((uint32_t)wblocks), dim3(kBlock), lds, stream, args);
   return (int)hipGetLastError();

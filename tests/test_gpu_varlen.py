@@ -158,22 +158,45 @@ def test_utf8_random_vs_python_decoder(cuda):
     assert np.array_equal(got, want)
 
 
-def test_dedup_matches_reference_proxy(cuda, golden_dedup):
+def _dedup_form(table):
+    """Context: the dedup window pass by LDS hash table (1) or by window scan (0)."""
+    import contextlib
+    import ctypes
+    from rudp import _native
+    lib = _native.lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.rudpx_tune.restype = ctypes.c_int
+
+    @contextlib.contextmanager
+    def ctx():
+        old = lib.rudpx_tune(32, table)
+        try:
+            yield
+        finally:
+            lib.rudpx_tune(32, old)
+    return ctx()
+
+
+@pytest.mark.parametrize("table", [1, 0])
+def test_dedup_matches_reference_proxy(cuda, golden_dedup, table):
     g = golden_dedup
     off = np.concatenate([[0], np.cumsum(g["lengths"])]).astype(np.int64)
-    dup = batch.detect_retransmissions(dev(g["frames"], cuda), frame_off=dev(off, cuda), window=500)
+    with _dedup_form(table):
+        dup = batch.detect_retransmissions(dev(g["frames"], cuda), frame_off=dev(off, cuda), window=500)
     assert np.array_equal(host(dup), g["dup"])
 
 
+@pytest.mark.parametrize("table", [1, 0])
 @pytest.mark.parametrize("window", [1, 7, 500, 4096])
-def test_dedup_fixed_length_vs_oracle(cuda, window):
+def test_dedup_fixed_length_vs_oracle(cuda, window, table):
     from oracle.bitstring_packet import proxy_retransmitted
     rng = np.random.default_rng(window)
     base = rng.integers(0, 256, (300, 40), dtype=np.uint8)
     idx = rng.integers(0, 300, 2500)
     fr = np.ascontiguousarray(base[idx])
     want = proxy_retransmitted([r.tobytes() for r in fr], window) if window < 4096 else None
-    got = host(batch.detect_retransmissions(dev(fr, cuda), window=window))
+    with _dedup_form(table):
+        got = host(batch.detect_retransmissions(dev(fr, cuda), window=window))
     last, ref = {}, []  # last occurrence of each frame: dup iff it lies inside the window
     for i, r in enumerate(fr):
         k = r.tobytes()
@@ -522,3 +545,26 @@ def test_utf8_fixed_stride_tile_and_vector_kernels(cuda, L):
             finally:
                 lib.rudpx_tune(31, old)
             assert np.array_equal(got, want), (L, H, tile)
+
+
+@pytest.mark.parametrize("window", [1, 500, 4096])
+def test_dedup_table_heavy_repeats_and_collisions(cuda, window):
+    """Long chains: few distinct frames (every bucket chain holds many equal
+    hashes, most outside the window), empty datagrams (equal to the 40-bit zero
+    header), and 20K frames so windows cross many workgroups."""
+    rng = np.random.default_rng(99 + window)
+    pool = [b"", bytes(5), b"\x01", b"\x00\x00\x00\x00\x00\x00"] + \
+           [bytes(rng.integers(0, 256, int(rng.integers(1, 40)), dtype=np.uint8)) for _ in range(60)]
+    seq = [pool[int(k)] for k in rng.integers(0, len(pool), 20000)]
+    off = np.concatenate([[0], np.cumsum([len(f) for f in seq])]).astype(np.int64)
+    flat = np.frombuffer(b"".join(seq) + b"\x00", np.uint8)[:-1] if off[-1] else np.zeros(0, np.uint8)
+    canon = [f if f else bytes(5) for f in seq]  # Packet(b"") equals the zero header
+    last, want = {}, []
+    for i, k in enumerate(canon):
+        want.append(int(k in last and last[k] >= i - window))
+        last[k] = i
+    for table in (1, 0):
+        with _dedup_form(table):
+            got = host(batch.detect_retransmissions(dev(flat, cuda), frame_off=dev(off, cuda),
+                                                    window=window))
+        assert got.tolist() == want, table
