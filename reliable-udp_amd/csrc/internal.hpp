@@ -172,6 +172,7 @@ struct Tuning {
   // 0.0287 -> 0.0267 ms, x 256 B 0.0934 -> 0.0892, x 1024 B 0.3606 ->
   // 0.3557), after above (x 1472 B 0.5208 vs 0.5291 early).
   int encode_early_table = -1;
+  int varlen_decode_tile = 1;  // varlen decode through LDS tiles for hints >= 512 B (2: any hint; 0: never)
   int dedup_table = 1;    // dedup window pass by LDS hash table (0: every frame scans its window)
   int utf8_tile = 1;      // fixed-stride UTF-8 validation through LDS tiles (0: per-frame vector kernel)
   int encode_span = 0;

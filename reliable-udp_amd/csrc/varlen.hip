@@ -439,6 +439,40 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_kernel(VarlenArgs a) {
   }
 }
 
+// The group leader's part of a varlen decode: `sum` is the whole frame's
+// big-endian word sum, `h` its first 16 bytes (little-endian packed).
+template <int H>
+__device__ __forceinline__ void decode_varlen_finish(const VarlenArgs& a, uint64_t p, uint32_t F,
+                                                     uint32_t sum, u32x4 h) {
+  const uint32_t b0 = h.x & 0xFFu, b1 = (h.x >> 8) & 0xFFu, b2 = (h.x >> 16) & 0xFFu,
+                 b3 = h.x >> 24, b4 = h.y & 0xFFu, b5 = (h.y >> 8) & 0xFFu,
+                 b6 = (h.y >> 16) & 0xFFu;
+  if (F < (uint32_t)H) {  // short frame: fields truncated as utils/packet.py:31 slices them
+    const uint32_t c0 = F > 0 ? b0 : 0u, c1 = F > 1 ? b1 : 0u, c2 = F > 2 ? b2 : 0u,
+                   c3 = F > 3 ? b3 : 0u, c4 = F > 4 ? b4 : 0u;
+    a.seq[p] = (uint16_t)(F >= 2 ? (c0 << 8) | c1 : c0);
+    a.ack[p] = (uint16_t)(F >= 4 ? (c2 << 8) | c3 : c2);
+    a.flags[p] = (uint8_t)c4;
+    a.ok[p] = 2;
+    if (a.csum_out) a.csum_out[p] = 0;
+    return;
+  }
+  const uint32_t seq = (b0 << 8) | b1, ack = (b2 << 8) | b3, flags = b4;
+  const uint32_t inband = (b5 << 8) | b6;
+  // the whole-frame sum holds seq, ack, flags<<8 and (rudp7) the checksum
+  // bytes at positions 5 (low) and 6 (high): take them back out
+  const uint32_t payload_sum = sum - seq - ack - (flags << 8) - (H == 7 ? (b5 | (b6 << 8)) : 0u);
+  const uint32_t c = packet_csum(payload_sum, seq, ack, flags);
+  uint8_t ok;
+  if (H == 7) ok = c == inband ? 1 : 0;
+  else ok = a.csum_in ? (c == a.csum_in[p] ? 1 : 0) : 3;
+  a.seq[p] = (uint16_t)seq;
+  a.ack[p] = (uint16_t)ack;
+  a.flags[p] = (uint8_t)flags;
+  a.ok[p] = ok;
+  if (a.csum_out) a.csum_out[p] = (uint16_t)c;
+}
+
 // Vectorized varlen decode (frames buffer 16-byte aligned): G lanes per
 // frame load the ALIGNED 16-byte chunks overlapping [off[p], off[p+1]) once
 // each, mask the two boundary chunks to the frame, and sum bytes at even and
@@ -450,13 +484,10 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_kernel(VarlenArgs a) {
 // the exact integer sum is taken back out before the fold.  G is chosen on the
 // host from the batch's mean frame length; any G >= 2 gives the same answer.
 template <int H>
-__global__ void __launch_bounds__(kBlock) decode_varlen_vec_kernel(VarlenArgs a) {
+__device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_t p, bool valid, uint32_t g,
+                                                    uint32_t glog) {
   const uint32_t tid = threadIdx.x;
-  const uint32_t glog = a.glog;
   const uint32_t G = 1u << glog;
-  const uint32_t g = tid & (G - 1u);
-  const uint64_t p = (uint64_t)blockIdx.x * (kBlock >> glog) + (tid >> glog);
-  const bool valid = p < a.n;
   const uint64_t total = a.frame_off[a.n];
   const uint64_t fstart = valid ? a.frame_off[p] : 0;
   const uint64_t fend = valid ? a.frame_off[p + 1] : 0;
@@ -502,35 +533,89 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_vec_kernel(VarlenArgs a)
   next.z = __shfl(first.z, src, 64);
   next.w = __shfl(first.w, src, 64);
   if (g != 0 || !valid) return;
-  const uint32_t F = (uint32_t)(fend - fstart);
-  const u32x4 h = funnel32(first, next, (uint32_t)(fstart & 15u));
-  const uint32_t b0 = h.x & 0xFFu, b1 = (h.x >> 8) & 0xFFu, b2 = (h.x >> 16) & 0xFFu,
-                 b3 = h.x >> 24, b4 = h.y & 0xFFu, b5 = (h.y >> 8) & 0xFFu,
-                 b6 = (h.y >> 16) & 0xFFu;
-  if (F < (uint32_t)H) {  // short frame: fields truncated as utils/packet.py:31 slices them
-    const uint32_t c0 = F > 0 ? b0 : 0u, c1 = F > 1 ? b1 : 0u, c2 = F > 2 ? b2 : 0u,
-                   c3 = F > 3 ? b3 : 0u, c4 = F > 4 ? b4 : 0u;
-    a.seq[p] = (uint16_t)(F >= 2 ? (c0 << 8) | c1 : c0);
-    a.ack[p] = (uint16_t)(F >= 4 ? (c2 << 8) | c3 : c2);
-    a.flags[p] = (uint8_t)c4;
-    a.ok[p] = 2;
-    if (a.csum_out) a.csum_out[p] = 0;
+  decode_varlen_finish<H>(a, p, (uint32_t)(fend - fstart), sum, funnel32(first, next, (uint32_t)(fstart & 15u)));
+}
+
+template <int H>
+__global__ void __launch_bounds__(kBlock) decode_varlen_vec_kernel(VarlenArgs a) {
+  const uint32_t glog = a.glog;
+  const uint64_t p = (uint64_t)blockIdx.x * (kBlock >> glog) + (threadIdx.x >> glog);
+  decode_varlen_frame<H>(a, p, p < a.n, threadIdx.x & ((1u << glog) - 1u), glog);
+}
+
+// Varlen decode through an LDS tile (the fixed-length decode tile's shape):
+// a workgroup owns T = 256 / G consecutive frames, whose bytes are one
+// contiguous run [frame_off[p0], frame_off[p0 + T]).  Phase 1 streams the run
+// into LDS as a copy (every wave-instruction 1 KiB contiguous) and puts the
+// tile's frame offsets there; phase 2 gives G lanes to each frame, which sum
+// its aligned LDS chunks by address parity (as decode_varlen_vec_kernel does
+// from HBM), and the leader parses the header from LDS.  A tile whose run
+// exceeds tile_cap (lengths far above the hint) decodes its frames with the
+// per-frame vector path inside the same launch.
+template <int H>
+__global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t glog = a.glog, G = 1u << glog, T = kBlock >> glog;
+  const uint32_t q = tid >> glog, g = tid & (G - 1u);
+  uint32_t* lds_fo = reinterpret_cast<uint32_t*>(lds);                       // [T + 1]
+  unsigned char* img = lds + ((((T + 1u) * 4u) + 15u) & ~15u) + kVTGuard;   // the run
+  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  const uint64_t left = a.n - p0;
+  const uint32_t Tv = left < T ? (uint32_t)left : T;
+  const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
+  const uint64_t A = fo0 & ~15ull;
+  const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
+  if (run > a.tile_cap) {  // uniform over the workgroup
+    decode_varlen_frame<H>(a, p0 + q, q < Tv, g, glog);
     return;
   }
-  const uint32_t seq = (b0 << 8) | b1, ack = (b2 << 8) | b3, flags = b4;
-  const uint32_t inband = (b5 << 8) | b6;
-  // the whole-frame sum holds seq, ack, flags<<8 and (rudp7) the checksum
-  // bytes at positions 5 (low) and 6 (high): take them back out
-  const uint32_t payload_sum = sum - seq - ack - (flags << 8) - (H == 7 ? (b5 | (b6 << 8)) : 0u);
-  const uint32_t c = packet_csum(payload_sum, seq, ack, flags);
-  uint8_t ok;
-  if (H == 7) ok = c == inband ? 1 : 0;
-  else ok = a.csum_in ? (c == a.csum_in[p] ? 1 : 0) : 3;
-  a.seq[p] = (uint16_t)seq;
-  a.ack[p] = (uint16_t)ack;
-  a.flags[p] = (uint8_t)flags;
-  a.ok[p] = ok;
-  if (a.csum_out) a.csum_out[p] = (uint16_t)c;
+  {
+    const uint64_t total = a.frame_off[a.n];
+    const uint32_t nvec = (uint32_t)(run >> 4);
+    u32x4* dst = reinterpret_cast<u32x4*>(img);
+    constexpr uint32_t P = 8;
+    for (uint32_t v0 = tid; v0 < nvec; v0 += P * kBlock) {
+      u32x4 r[P];
+#pragma unroll
+      for (uint32_t u = 0; u < P; ++u) {
+        const uint32_t v = v0 + u * kBlock;
+        if (v < nvec) r[u] = load16_guarded(a.frames, A + 16ull * v, total);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < P; ++u) {
+        const uint32_t v = v0 + u * kBlock;
+        if (v < nvec) dst[v] = r[u];
+      }
+    }
+    for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = (uint32_t)(a.frame_off[p0 + i] - A);
+  }
+  __syncthreads();
+  if (q >= Tv) return;
+  const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
+  const u32x4* img16 = reinterpret_cast<const u32x4*>(img);
+  uint32_t even_sum = 0, odd_sum = 0;  // byte sums at even / odd offsets (A is even)
+  if (fe > fs) {
+    const uint32_t c0 = fs >> 4, c1 = (fe - 1u) >> 4;
+    for (uint32_t c = c0 + g; c <= c1; c += G) {
+      u32x4 w = img16[c];
+      if (c == c0 || c == c1) {  // keep this frame's bytes only
+        const int lo = (int)fs - (int)(c << 4), hi = (int)fe - (int)(c << 4);
+        w = make_u32x4(lo64(w) & byte_mask(lo, hi), hi64(w) & byte_mask(lo - 8, hi - 8));
+      }
+      const uint32_t e = (w.x & 0x00FF00FFu) + (w.y & 0x00FF00FFu) + (w.z & 0x00FF00FFu) + (w.w & 0x00FF00FFu);
+      const uint32_t o = ((w.x >> 8) & 0x00FF00FFu) + ((w.y >> 8) & 0x00FF00FFu) +
+                         ((w.z >> 8) & 0x00FF00FFu) + ((w.w >> 8) & 0x00FF00FFu);
+      even_sum += (e & 0xFFFFu) + (e >> 16);
+      odd_sum += (o & 0xFFFFu) + (o >> 16);
+    }
+  }
+  // even offsets are high bytes iff the frame starts at an even offset
+  uint32_t sum = (fs & 1u) ? (even_sum + (odd_sum << 8)) : ((even_sum << 8) + odd_sum);
+  for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
+  if (g == 0)
+    decode_varlen_finish<H>(a, p0 + q, fe - fs,
+                            sum, window16_dw(reinterpret_cast<const uint32_t*>(img), fs));
 }
 
 // Strict UTF-8 (RFC 3629, as CPython's bytes.decode() accepts it, i.e. what
@@ -837,6 +922,18 @@ int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream)
 
 int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream) {
   if (args.n == 0) return 0;
+  if (args.glog != kNoVec && args.tile_cap && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0) {
+    const uint32_t T = kBlock >> args.glog;
+    const size_t lds = ((((T + 1u) * 4u) + 15u) & ~15u) + kVTGuard + args.tile_cap + 32u;
+    if (lds <= 65536) {
+      const uint64_t blocks = (args.n + T - 1) / T;
+      if (layout == 7)
+        hipLaunchKernelGGL(decode_varlen_tile_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
+      else
+        hipLaunchKernelGGL(decode_varlen_tile_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
+      return (int)hipGetLastError();
+    }
+  }
   if (args.glog != kNoVec && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0) {
     const uint64_t blocks = (args.n + (kBlock >> args.glog) - 1) / (kBlock >> args.glog);
     if (layout == 7)

@@ -276,7 +276,8 @@ def _varlen_frames(rng, n, lo, hi, layout):
 @pytest.mark.parametrize("lo,hi", [(0, 9), (0, 1500), (1400, 1472), (3000, 9000)])
 @pytest.mark.parametrize("layout", [5, 7])
 def test_varlen_decode_kernels_vs_oracle(cuda, lo, hi, layout):
-    """Vector varlen decode (any lanes-per-frame hint) == byte kernel == oracle."""
+    """LDS-tile and vector varlen decode (any lanes-per-frame hint; tiles past
+    their budget take the per-frame path) == byte kernel == oracle."""
     import ctypes
     import torch
     from rudp import _native
@@ -291,9 +292,11 @@ def test_varlen_decode_kernels_vs_oracle(cuda, lo, hi, layout):
     d_cs = dev(cs, cuda) if layout == 5 else None
     outs = [torch.empty(n, dtype=dt, device=cuda)
             for dt in (torch.uint16, torch.uint16, torch.uint8, torch.uint8, torch.uint16)]
-    runs = [("python", None, 1)] + [("abi", h, v) for v in (1, 0) for h in (0, 8, 1472, 65535)]
-    for kind, hint, vec in runs:
+    runs = [("python", None, 1, 1)] + [("abi", h, v, t) for v in (1, 0) for h in (0, 8, 64, 1472, 65535)
+                                         for t in ((2, 0) if v else (1,))]
+    for kind, hint, vec, tile in runs:
         lib.rudpx_tune(14, vec)
+        lib.rudpx_tune(33, tile)
         try:
             if kind == "python":
                 d = batch.unpack_batch_varlen(d_buf, d_off, layout, csum=d_cs)
@@ -309,8 +312,9 @@ def test_varlen_decode_kernels_vs_oracle(cuda, lo, hi, layout):
                 got = [host(o) for o in outs]
         finally:
             lib.rudpx_tune(14, 1)
+            lib.rudpx_tune(33, 1)
         for name, g, w in zip(("seq", "ack", "flags", "ok", "csum"), got, want):
-            assert np.array_equal(g, w), (lo, hi, layout, kind, hint, vec, name)
+            assert np.array_equal(g, w), (lo, hi, layout, kind, hint, vec, tile, name)
     assert (want[3] == 2).any() and (want[3] == 0).any() and (want[3] == 1).any()
 
 

@@ -272,6 +272,49 @@ def multi_sweep(reps, specs):
     return out
 
 
+def vdec_sweep(reps):
+    """Varlen decode through the raw ABI (preallocated outputs, hint = mean frame
+    length): LDS-tile kernel (rudpx_tune 33 = 1) vs per-frame vector kernel (0)."""
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    out = {}
+    for L in (1, 64, 256, 1024, 1472, -1):  # -1: lengths uniform in [0, 2944]
+        n = 1 << 20
+        tab, pay = batch.synth_batch(n, max(L, 2944), 0x5EED0007, device=dev)
+        if L >= 0:
+            lens = torch.full((n,), L, dtype=torch.int32, device=dev)
+        else:
+            lens = torch.randint(0, 2945, (n,), dtype=torch.int32, device=dev)
+        mean = int(lens.double().mean().item()) + 7
+        flat = pay.view(-1)[: int(lens.sum().item())] if L < 0 else pay[:, :max(L, 0)].contiguous().view(-1)
+        nsets = max(1, min(8, -(-(1 << 30) // (n * mean))))
+        sets = []
+        for _ in range(nsets):
+            r = batch.pack_batch_varlen(tab, flat, lens, 7)
+            sets.append((r.frames, r.frame_off))
+        o16 = [torch.empty(n, dtype=torch.uint16, device=dev) for _ in range(3)]
+        o8 = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(2)]
+        it = [0]
+
+        def run():
+            frames, off = sets[it[0] % nsets]
+            it[0] += 1
+            _native.check(lib.rudp_decode(frames.data_ptr(), off.data_ptr(), mean, n, None,
+                                          o16[0].data_ptr(), o16[1].data_ptr(), o8[0].data_ptr(),
+                                          o8[1].data_ptr(), o16[2].data_ptr(), None, 7, 0, stream))
+        name = f"L{L}" if L >= 0 else "U0-2944"
+        variants = {f"{name}_tile": (lambda: lib.rudpx_tune(33, 2), run),
+                    f"{name}_vec": (lambda: lib.rudpx_tune(33, 0), run)}
+        res = interleaved(variants, reps)
+        lib.rudpx_tune(33, 1)
+        alg = n * (mean + 8 + 8)  # frames + offsets read, seq/ack/flags/ok/csum written
+        for k, ms in res.items():
+            out[k] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0}
+        del sets, tab, pay, flat, lens
+        torch.cuda.empty_cache()
+    return out
+
+
 def stream_sweep(reps):
     """Register-streamed encode (rudpx_tune 20-22) against the LDS-tile encode."""
     out = {}
@@ -610,7 +653,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--L", type=int, default=1472, help="payload length for --only ablate")
-    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "stream", "align", "knob", "copydma", "multi", "opsknob"])
+    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "stream", "align", "knob", "copydma", "multi", "opsknob", "vdec"])
     ap.add_argument("--blocks", type=str, default="", help="encode sweep: workgroup sizes, e.g. 256,512,1024")
     ap.add_argument("--encode-L", type=str, default="", help="encode sweep: payload lengths, e.g. 1472")
     ap.add_argument("--ablate", action="store_true", help="stream sweep: add stage ablations")
@@ -649,6 +692,8 @@ def main():
             name, _, kvs = part.partition(":")
             specs.append((name, [tuple(int(y) for y in x.split("=")) for x in kvs.split(",") if x]))
         result["multi"] = multi_sweep(args.reps, specs)
+    if args.only == "vdec":
+        result["vdec"] = vdec_sweep(args.reps)
     if args.only == "knob":
         pre = [tuple(int(y) for y in x.split("=")) for x in args.pre.split(",") if x]
         result["knob"] = knob_sweep(args.reps, args.key, [int(x) for x in args.values.split(",")], pre)
