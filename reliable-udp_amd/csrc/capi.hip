@@ -383,6 +383,10 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, ui
   DecodeArgs a{};
   a.align64 = tuning().out_align64 == 1 ? 1u : 0u;
   a.dma = tuning().tile_dma ? 1u : 0u;
+  a.stage_out = (tuning().decode_stage_out &&
+                 ((reinterpret_cast<uintptr_t>(d_seq) | reinterpret_cast<uintptr_t>(d_ack) |
+                   reinterpret_cast<uintptr_t>(d_flags) | reinterpret_cast<uintptr_t>(d_ok) |
+                   reinterpret_cast<uintptr_t>(d_csum_out_or_null)) & 3u) == 0) ? 1u : 0u;
   a.frames = d_frames;
   a.csum_in = d_csum_in_or_null;
   a.seq = d_seq;

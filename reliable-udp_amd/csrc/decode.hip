@@ -276,13 +276,68 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
     }
   }
   for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
+  if (!a.stage_out) {
+    if (g == 0 && q < Tv) {
+      const u32x4 h = window16_dw(dw, q * F);
+      const uint32_t seq = ((h.x & 0xFFu) << 8) | ((h.x >> 8) & 0xFFu);
+      const uint32_t ack = (((h.x >> 16) & 0xFFu) << 8) | (h.x >> 24);
+      const uint32_t flags = h.y & 0xFFu;
+      const uint32_t inband = (((h.y >> 8) & 0xFFu) << 8) | ((h.y >> 16) & 0xFFu);
+      finish_packet<H>(a, p, sum, seq, ack, flags, inband);
+    }
+    return;
+  }
+  // Outputs staged in LDS after the tile (seq, ack, csum u16 [T]; flags, ok
+  // u8 [T]), then written as whole dwords: one wave-instruction covers 256 B
+  // of an output array instead of each leader storing 1-2 bytes into five.
+  const uint32_t st = (nbytes + 32u + 15u) & ~15u;
+  uint16_t* s_seq = reinterpret_cast<uint16_t*>(lds + st);
+  uint16_t* s_ack = s_seq + T;
+  uint16_t* s_cs = s_ack + T;
+  uint8_t* s_flags = reinterpret_cast<uint8_t*>(s_cs + T);
+  uint8_t* s_ok = s_flags + T;
   if (g == 0 && q < Tv) {
     const u32x4 h = window16_dw(dw, q * F);
     const uint32_t seq = ((h.x & 0xFFu) << 8) | ((h.x >> 8) & 0xFFu);
     const uint32_t ack = (((h.x >> 16) & 0xFFu) << 8) | (h.x >> 24);
     const uint32_t flags = h.y & 0xFFu;
     const uint32_t inband = (((h.y >> 8) & 0xFFu) << 8) | ((h.y >> 16) & 0xFFu);
-    finish_packet<H>(a, p, sum, seq, ack, flags, inband);
+    const uint32_t c = packet_csum(sum, seq, ack, flags);
+    uint8_t ok;
+    if (H == 7) ok = (c == inband) ? 1 : 0;
+    else if (a.csum_in) ok = (c == a.csum_in[p]) ? 1 : 0;
+    else ok = 3;
+    s_seq[q] = (uint16_t)seq;
+    s_ack[q] = (uint16_t)ack;
+    s_cs[q] = (uint16_t)c;
+    s_flags[q] = (uint8_t)flags;
+    s_ok[q] = ok;
+  }
+  __syncthreads();
+  if (Tv == T) {  // T % 16 == 0 and p0 % 16 == 0: every array slice is dword aligned
+    const uint32_t w16 = T / 2u, w8 = T / 4u;
+    const uint32_t* l_seq = reinterpret_cast<const uint32_t*>(s_seq);
+    const uint32_t* l_ack = reinterpret_cast<const uint32_t*>(s_ack);
+    const uint32_t* l_cs = reinterpret_cast<const uint32_t*>(s_cs);
+    const uint32_t* l_fl = reinterpret_cast<const uint32_t*>(s_flags);
+    const uint32_t* l_ok = reinterpret_cast<const uint32_t*>(s_ok);
+    for (uint32_t i = tid; i < w16; i += kBlock) {
+      reinterpret_cast<uint32_t*>(a.seq + p0)[i] = l_seq[i];
+      reinterpret_cast<uint32_t*>(a.ack + p0)[i] = l_ack[i];
+      if (a.csum_out) reinterpret_cast<uint32_t*>(a.csum_out + p0)[i] = l_cs[i];
+    }
+    for (uint32_t i = tid; i < w8; i += kBlock) {
+      reinterpret_cast<uint32_t*>(a.flags + p0)[i] = l_fl[i];
+      reinterpret_cast<uint32_t*>(a.ok + p0)[i] = l_ok[i];
+    }
+  } else {
+    for (uint32_t i = tid; i < Tv; i += kBlock) {
+      a.seq[p0 + i] = s_seq[i];
+      a.ack[p0 + i] = s_ack[i];
+      if (a.csum_out) a.csum_out[p0 + i] = s_cs[i];
+      a.flags[p0 + i] = s_flags[i];
+      a.ok[p0 + i] = s_ok[i];
+    }
   }
 }
 
@@ -334,7 +389,8 @@ int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream
     const uint32_t per_block = kBlock >> args.glog;
     const uint64_t blocks = (args.n + per_block - 1) / per_block;
     if (path == DecodePath::kCopyTile || path == DecodePath::kVerifyTile) {
-      const size_t lds = ((size_t)per_block * args.F + 32 + 15) & ~size_t(15);
+      size_t lds = ((size_t)per_block * args.F + 32 + 15) & ~size_t(15);
+      if (args.stage_out) lds += 8u * per_block;  // staged outputs
       const dim3 grid((uint32_t)blocks), block(kBlock);
       if (path == DecodePath::kCopyTile) {
         if (layout == 7) hipLaunchKernelGGL((decode_tile_kernel<7, true>), grid, block, lds, stream, args);

@@ -51,6 +51,7 @@ struct DecodeArgs {
   uint32_t glog;            // log2(lanes per packet)
   uint32_t align64;         // tile kernel: wave loads/stores start on 64-B sector boundaries
   uint32_t dma;             // tile kernel: phase 1 by LDS-DMA (when align64 is off)
+  uint32_t stage_out;       // tile kernel: outputs staged in LDS, written as dwords (pointers 4-B aligned)
 };
 
 struct SynthArgs {
@@ -172,6 +173,11 @@ struct Tuning {
   // 0.0287 -> 0.0267 ms, x 256 B 0.0934 -> 0.0892, x 1024 B 0.3606 ->
   // 0.3557), after above (x 1472 B 0.5208 vs 0.5291 early).
   int encode_early_table = -1;
+  // Decode tile outputs staged in LDS and written as whole dwords (output
+  // pointers 4-B aligned): 1M x 256 B verify 0.0489 -> 0.0470 ms, x 64 B
+  // 0.0156 -> 0.0152, x 1472 B equal; copy-out equal to +1%
+  // (profiles/r01/sweeps/decode_stage_out.json).
+  int decode_stage_out = 1;
   int varlen_decode_tile = 1;  // varlen decode through LDS tiles for hints >= 512 B (2: any hint; 0: never)
   int dedup_table = 1;    // dedup window pass by LDS hash table (0: every frame scans its window)
   int utf8_tile = 1;      // fixed-stride UTF-8 validation through LDS tiles (0: per-frame vector kernel)

@@ -231,16 +231,18 @@ def test_decode_paths_agree(cuda, L):
     fr[17, 9] ^= 0x40  # one corrupted frame
     want = codec_np.decode(fr, 7)
     results = []
-    for verify_tile, copy_tile, align in ((1, 1, -1), (1, 1, 1), (0, 0, -1)):
+    for verify_tile, copy_tile, align, stage in ((1, 1, -1, 0), (1, 1, 1, 0), (0, 0, -1, 0),
+                                                 (1, 1, -1, 1), (1, 1, 1, 1)):
         lib.rudpx_tune(12, verify_tile)
         lib.rudpx_tune(11, copy_tile)
         lib.rudpx_tune(23, align)  # tile loads/stores from a 64-B boundary
+        lib.rudpx_tune(34, stage)  # tile outputs staged in LDS, written as dwords
         try:
             for copy in (False, True):
                 d = batch.unpack_batch(dev(fr, cuda), 7, copy_payload=copy)
                 got = [host(x) for x in (d.seq, d.ack, d.flags, d.ok, d.csum)]
                 for g, w in zip(got, want[:5]):
-                    assert np.array_equal(g, w), (L, verify_tile, copy, align)
+                    assert np.array_equal(g, w), (L, verify_tile, copy, align, stage)
                 if copy:
                     assert np.array_equal(host(d.payload), fr[:, 7:])
                 results.append(got)
@@ -248,6 +250,7 @@ def test_decode_paths_agree(cuda, L):
             lib.rudpx_tune(12, 1)
             lib.rudpx_tune(11, 1)
             lib.rudpx_tune(23, -1)
+            lib.rudpx_tune(34, 0)
     assert host(d.ok)[17] == 0
 
 
