@@ -59,6 +59,43 @@ class HeaderTable:
         return len(self.seq)
 
 
+class PayloadSpans:
+    """Payload i of a packed batch is frames[start[i]:end[i]] (zero-copy).
+
+    Behaves as the pair ``(start, end)`` of int64 [N] tensors; ``start``
+    (= min(frame_off[i] + H, frame_off[i + 1]), two device ops) is computed on
+    first use, so a decode whose caller reads only the header fields does
+    not pay for it.
+    """
+
+    __slots__ = ("_frame_off", "_H", "_start")
+
+    def __init__(self, frame_off, H: int):
+        self._frame_off = frame_off
+        self._H = H
+        self._start = None
+
+    @property
+    def start(self):
+        if self._start is None:
+            import torch
+            self._start = torch.minimum(self._frame_off[:-1] + self._H, self._frame_off[1:])
+        return self._start
+
+    @property
+    def end(self):
+        return self._frame_off[1:]
+
+    def __iter__(self):
+        return iter((self.start, self.end))
+
+    def __getitem__(self, i):
+        return (self.start, self.end)[i]
+
+    def __len__(self):
+        return 2
+
+
 class DecodedBatch(NamedTuple):
     seq: Any
     ack: Any
@@ -392,7 +429,8 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
     """Parse + verify frames packed back to back (offsets as pack_batch_varlen returns).
 
     The payload is zero-copy: ``payload`` is the pair ``(start, end)`` of int64
-    [N] tensors indexing ``frames`` (empty for frames shorter than the header).
+    [N] tensors indexing ``frames`` (empty for frames shorter than the header),
+    as a ``PayloadSpans`` that computes ``start`` on first use.
     """
     import torch
     H = layout_header_len(layout)
@@ -420,9 +458,7 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
             csum.data_ptr() if csum is not None else None, seq.data_ptr(), ack.data_ptr(),
             flags.data_ptr(), ok.data_ptr(), cs.data_ptr(), None, H, dev.index or 0,
             _stream_ptr(stream, dev)))
-    end = frame_off[1:]
-    start = torch.minimum(frame_off[:-1] + H, end)
-    return DecodedBatch(seq, ack, flags, ok, cs, (start, end))
+    return DecodedBatch(seq, ack, flags, ok, cs, PayloadSpans(frame_off, H))
 
 
 def validate_utf8(frames, layout: Union[str, int] = "rudp7", *, frame_off=None, stream=None):

@@ -69,3 +69,16 @@ def test_gloo_world2_shards_match_unsharded():
     per = N // 2
     for first, n, digest in gathered:
         assert digest == hashlib.sha256(full_fr[first:first + n].tobytes()).digest()
+
+
+def test_payload_spans_is_the_start_end_pair():
+    """unpack_batch_varlen's lazy payload spans behave as (start, end)."""
+    import torch
+    from rudp.batch import PayloadSpans
+    off = torch.tensor([0, 3, 10, 10, 17, 30], dtype=torch.int64)
+    sp = PayloadSpans(off, 7)
+    start, end = sp
+    assert torch.equal(start, torch.tensor([3, 10, 10, 17, 24]))
+    assert torch.equal(end, off[1:])
+    assert torch.equal(sp[0], start) and torch.equal(sp[1], end) and len(sp) == 2
+    assert sp.start is sp.start  # computed once
