@@ -500,6 +500,8 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
   // them at every length (1M x 64 B 0.0934 vs 0.0915 ms; its offset loads
   // already precede phase 1; profiles/r01/sweeps/encode_early_table.json).
   a.early_table = tuning().encode_early_table == 1 ? 1u : 0u;
+  a.ablate = (uint32_t)tuning().varlen_ablate;
+  a.vhc = tuning().varlen_hchunk ? 1u : 0u;
   rc = launch_encode_varlen(a, layout, s);
   if (rc) return hip_fail((hipError_t)rc, "varlen encode launch");
   return 0;

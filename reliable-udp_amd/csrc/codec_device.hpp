@@ -128,4 +128,36 @@ __device__ __forceinline__ u32x4 load16_guarded(const unsigned char* frames, uin
   return r;
 }
 
+// Aligned 16-B chunk X of the output around a packet's header, P = the
+// output offset of its payload: the previous packet's last payload bytes
+// (`tail`: its last 16), the header bytes `h` (frame order, packed
+// little-endian) and the first payload bytes (`head`).  X is one of the one
+// or two chunks [floor16(P - H), ceil16(P)).
+template <int H>
+__device__ __forceinline__ u32x4 header_chunk(uint64_t X, uint64_t P, uint64_t h, u32x4 tail,
+                                              u32x4 head) {
+  const u32x4 zero = {0u, 0u, 0u, 0u};
+  const int k0 = (int)(int64_t)(X - (P - H));  // frame position of chunk byte 0 (> -16)
+  u32x4 w = zero;
+  if (k0 < 0) w = funnel32(tail, zero, (uint32_t)(k0 + 16));  // previous payload's last bytes
+  const uint32_t d = (uint32_t)(P - X);                        // payload starts d bytes in
+  if (d < 16) {
+    const u32x4 hp = funnel32(zero, head, 16u - d);
+    w.x |= hp.x; w.y |= hp.y; w.z |= hp.z; w.w |= hp.w;
+  }
+  uint64_t lo = lo64(w), hi = hi64(w);
+  if (k0 >= 0) {
+    lo |= h >> (8 * k0);
+  } else {
+    const int sh = -k0;
+    if (sh < 8) {
+      lo |= h << (8 * sh);
+      hi |= h >> (64 - 8 * sh);
+    } else {
+      hi |= h << (8 * (sh - 8));
+    }
+  }
+  return make_u32x4(lo, hi);
+}
+
 }  // namespace rudp

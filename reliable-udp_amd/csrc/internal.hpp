@@ -95,6 +95,9 @@ struct VarlenArgs {
   uint32_t align64;               // tile kernel: wave stores start on 64-B sector boundaries
   uint32_t dma;                   // tile kernel: phase 1 by LDS-DMA
   uint32_t early_table;           // tile kernel: header-table loads before phase 1
+  uint32_t ablate;                // diagnostics only (wrong output): 1 = phase 2 without the frame walk
+  uint32_t vhc;                   // tile kernel: prebuilt header chunks + pure-chunk fast phase 2
+  uint32_t hc_off;                // LDS byte offset of the header-chunk array (set by the launcher)
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -178,6 +181,12 @@ struct Tuning {
   // 0.0156 -> 0.0152, x 1472 B equal; copy-out equal to +1%
   // (profiles/r01/sweeps/decode_stage_out.json).
   int decode_stage_out = 1;
+  int varlen_ablate = 0;  // VarlenArgs::ablate (sweeps only)
+  // Varlen encode tile: prebuilt header chunks and a one-window phase 2 for
+  // tiles whose frames are all >= 32 B: 1M x 1472 B 0.738 -> 0.631 ms, x 1024
+  // B 0.562 -> 0.477, x 256 B 0.196 -> 0.169 (Python entry, one box;
+  // profiles/r01/sweeps/varlen_encode_hchunk.json).
+  int varlen_hchunk = 1;
   int varlen_decode_tile = 1;  // varlen decode through LDS tiles for hints >= 512 B (2: any hint; 0: never)
   int dedup_table = 1;    // dedup window pass by LDS hash table (0: every frame scans its window)
   int utf8_tile = 1;      // fixed-stride UTF-8 validation through LDS tiles (0: per-frame vector kernel)

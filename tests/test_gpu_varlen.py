@@ -318,7 +318,7 @@ def test_varlen_decode_kernels_vs_oracle(cuda, lo, hi, layout):
     assert (want[3] == 2).any() and (want[3] == 0).any() and (want[3] == 1).any()
 
 
-@pytest.mark.parametrize("lo,hi", [(0, 3), (0, 100), (1400, 1472), (5000, 20000)])
+@pytest.mark.parametrize("lo,hi", [(0, 3), (0, 100), (20, 40), (1400, 1472), (5000, 20000)])
 @pytest.mark.parametrize("layout", [5, 7])
 def test_varlen_encode_kernels_vs_oracle(cuda, lo, hi, layout):
     """Vector varlen encode (any lanes-per-packet hint, packed or gathered
@@ -343,13 +343,14 @@ def test_varlen_encode_kernels_vs_oracle(cuda, lo, hi, layout):
         big[starts[i]:starts[i] + lens[i]] = np.frombuffer(pays[i], np.uint8)
     tab = (dev(seq, cuda), dev(ack, cuda), dev(flags, cuda))
     d_lens = dev(lens, cuda)
-    for vec in (1, 0):
+    for vec, vhc in ((1, 0), (1, 1), (0, 0)):
         lib.rudpx_tune(14, vec)
+        old_vhc = lib.rudpx_tune(36, vhc)  # varlen tile: prebuilt header chunks, fast phase 2
         try:
             for payload, off in ((dev(packed, cuda), None), (dev(big, cuda), dev(starts, cuda))):
                 res = batch.pack_batch_varlen(tab, payload, d_lens, layout, payload_off=off,
                                               want_csum=True)
-                assert np.array_equal(host(res.frames), want_fr), (lo, hi, layout, vec, off is None)
+                assert np.array_equal(host(res.frames), want_fr), (lo, hi, layout, vec, vhc, off is None)
                 assert np.array_equal(host(res.frame_off), want_off)
                 assert np.array_equal(host(res.csum), want_cs)
             # any hint gives the same frames (raw ABI)
@@ -365,9 +366,10 @@ def test_varlen_encode_kernels_vs_oracle(cuda, lo, hi, layout):
                 _native.check(lib.rudp_encode_varlen(ctypes.byref(b), frames.data_ptr(),
                                                      frame_off.data_ptr(), None, layout, 0,
                                                      torch.cuda.current_stream().cuda_stream))
-                assert np.array_equal(host(frames), want_fr), (lo, hi, layout, vec, hint)
+                assert np.array_equal(host(frames), want_fr), (lo, hi, layout, vec, vhc, hint)
         finally:
             lib.rudpx_tune(14, 1)
+            lib.rudpx_tune(36, old_vhc)
 
 
 @pytest.mark.parametrize("dist", ["uniform2944", "bursty", "empty", "tiny", "mtu"])
@@ -406,8 +408,9 @@ def test_varlen_encode_tile_kernel_vs_oracle(cuda, dist, layout):
     frame_off = torch.empty(n + 1, dtype=torch.int64, device=cuda)
     csum = torch.empty(n, dtype=torch.uint16, device=cuda)
     try:
-        for tile in (1, 0):
+        for tile, vhc in ((1, 0), (1, 1), (0, 0)):
             lib.rudpx_tune(16, tile)
+            lib.rudpx_tune(36, vhc)  # prebuilt header chunks, fast phase 2 (tiles of frames >= 32 B)
             for hint in (0, 1, 16, 100, 1472, 3000, 6144):
                 frames.fill_(0xCD)
                 csum.fill_(0)
@@ -424,6 +427,7 @@ def test_varlen_encode_tile_kernel_vs_oracle(cuda, dist, layout):
                 assert np.array_equal(host(csum), want_cs), (dist, layout, tile, hint)
     finally:
         lib.rudpx_tune(16, 1)
+        lib.rudpx_tune(36, 0)
 
 
 @pytest.mark.parametrize("n", [1, 2, 255, 256, 257, 4099, 1 << 20])
