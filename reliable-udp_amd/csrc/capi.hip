@@ -495,11 +495,15 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
     varlen_tile_geometry(in->payload_len, &a.tile_T, &a.tile_glog, &a.tile_cap);
   a.align64 = tuning().out_align64 == 1 ? 1u : 0u;
   a.dma = tuning().tile_dma ? 1u : 0u;
-  // Header-table loads before phase 1 only when forced (rudpx_tune 30 = 1):
-  // unlike fixed-length encode, the varlen tile measured 0.5-2% slower with
-  // them at every length (1M x 64 B 0.0934 vs 0.0915 ms; its offset loads
-  // already precede phase 1; profiles/r01/sweeps/encode_early_table.json).
-  a.early_table = tuning().encode_early_table == 1 ? 1u : 0u;
+  // Header-table loads before phase 1 for hints of 128 B and up: with the
+  // fast phase 2 (varlen_hchunk) they measured 1M x 1472 B 0.637 -> 0.603 ms,
+  // x 1024 B 0.489 -> 0.468, x 256 B 0.170 -> 0.164
+  // (profiles/r01/sweeps/encode_early_table_varlen.json); before it they were
+  // 0.5-2% slower everywhere, and small hints keep them after the barrier.
+  {
+    const int early = tuning().encode_early_table;
+    a.early_table = (early == 1 || (early < 0 && in->payload_len >= 128u)) ? 1u : 0u;
+  }
   a.ablate = (uint32_t)tuning().varlen_ablate;
   a.vhc = tuning().varlen_hchunk ? 1u : 0u;
   rc = launch_encode_varlen(a, layout, s);
