@@ -109,7 +109,7 @@ EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t*
     a.hdr_bytes = ((a.T + 1u) * 8u + 15u) & ~15u;
     const int early = tuning().encode_early_table;
     a.early_table = (early == 1 || (early < 0 && a.T * a.L <= 16384u)) ? 1u : 0u;
-    if (tuning().encode_hchunk && a.T % 16u == 0 && !tuning().encode_ablate) {
+    if (tuning().encode_hchunk && a.T % 16u == 0 && !(tuning().encode_ablate & ~32)) {
       a.hchunk = 1;
       a.hc_off = a.hdr_bytes;
       a.hdr_bytes += (a.T + 1u) * 32u;

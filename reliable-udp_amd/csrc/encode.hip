@@ -273,7 +273,7 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
     const uint64_t h = pack_header<H>(s, k, f, c);
     lds_hdr[q] = h;
     if (a.csum) a.csum[p] = (uint16_t)c;
-    if (a.hchunk) {  // this packet's 1-2 header chunks, for encode_phase2_hc
+    if (a.hchunk && !(a.ablate & 32u)) {  // this packet's 1-2 header chunks, for encode_phase2_hc
       const u32x4* img = reinterpret_cast<const u32x4*>(lds_pay + kLdsGuard);
       const uint32_t P = q * (L + H) + H;
       u32x4* hc = reinterpret_cast<u32x4*>(lds + a.hc_off) + 2u * q;

@@ -21,7 +21,7 @@ struct EncodeTileArgs {
   uint32_t xcd_swizzle; // 1: map blocks b, b+8, ... to consecutive tiles (one XCD each)
   uint32_t num_tiles;
   uint32_t ablate;      // diagnostics only (wrong output): 1 no LDS sum pass, 2 plain phase-2
-                        // LDS reads, 4 no header-table loads
+                        // LDS reads, 4 no header-table loads, 32 no header-chunk build
   uint64_t invV;        // ceil(2^32 / (L / 16)) for exact v / V (stream kernel)
   uint32_t out_align64; // phase 2 deals full chunks from the tile's first 64-B boundary
   // span kernel: each workgroup owns `span` output bytes (a multiple of 64);
