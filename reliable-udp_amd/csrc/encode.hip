@@ -584,8 +584,12 @@ int launch_tile_policy(const EncodeTileArgs& args, hipStream_t stream) {
   // blocks give each packet (256/T)*(block/256) lanes, so keep that <= 64.
   if (block > 256 && (uint64_t)(256u / args.T) * (uint32_t)(block / 256) > 64u) block = 256;
   const Tuning& t = tuning();
-  if (t.encode_dma && block == 256 && t.encode_contig && t.encode_nt_load && t.encode_nt_store)
-    return launch_tile<H, true, true, 8, true, kBlock, true>(args, stream);
+  if (t.encode_dma && block == 256 && t.encode_contig) {
+    if (t.encode_nt_load && t.encode_nt_store) return launch_tile<H, true, true, 8, true, kBlock, true>(args, stream);
+    if (t.encode_nt_load) return launch_tile<H, true, false, 8, true, kBlock, true>(args, stream);
+    if (t.encode_nt_store) return launch_tile<H, false, true, 8, true, kBlock, true>(args, stream);
+    return launch_tile<H, false, false, 8, true, kBlock, true>(args, stream);
+  }
   if (block == 64 && args.T <= 64) return launch_tile<H, true, true, 8, true, 64>(args, stream);
   if (block == 128 && args.T <= 128) return launch_tile<H, true, true, 8, true, 128>(args, stream);
   if (block == 512) return launch_tile<H, true, true, 8, true, 512>(args, stream);
