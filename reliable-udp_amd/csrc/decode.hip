@@ -27,7 +27,9 @@ __device__ __forceinline__ u32x4 window16_global(const unsigned char* frames, ui
   return funnel32(a, b, (uint32_t)(off & 15u));
 }
 
-template <int H>
+// PRELOADED (rudp5): `inband` carries the sideband checksum the caller
+// already loaded; otherwise it is read here.
+template <int H, bool PRELOADED = false>
 __device__ __forceinline__ void finish_packet(const DecodeArgs& a, uint64_t p, uint32_t sum,
                                               uint32_t seq, uint32_t ack, uint32_t flags,
                                               uint32_t inband) {
@@ -36,7 +38,7 @@ __device__ __forceinline__ void finish_packet(const DecodeArgs& a, uint64_t p, u
   if (H == 7)
     ok = (c == inband) ? 1 : 0;
   else if (a.csum_in)
-    ok = (c == a.csum_in[p]) ? 1 : 0;
+    ok = (c == (PRELOADED ? inband : (uint32_t)a.csum_in[p])) ? 1 : 0;  // rudp5: the sideband value
   else
     ok = 3;
   a.seq[p] = (uint16_t)seq;
@@ -203,6 +205,11 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
   const uint32_t nbytes = Tv * F;
   const uint32_t nvec = (nbytes + 15u) >> 4;
   u32x4* tile = reinterpret_cast<u32x4*>(lds);
+  // rudp5 sideband checksums: the leaders load theirs before phase 1, so the
+  // round trip overlaps the frame stream instead of following the sums.
+  uint32_t want_cs = 0;
+  if (H == 5 && a.csum_in && (tid & ((1u << a.glog) - 1u)) == 0 && (tid >> a.glog) < Tv)
+    want_cs = a.csum_in[p0 + (tid >> a.glog)];
   // Lanes are dealt vectors from the tile's first 64-B boundary on (the 0-3
   // vectors before it go last): every wave's 1 KiB load covers whole sectors.
   uint32_t npre = a.align64 ? (uint32_t)((-reinterpret_cast<uintptr_t>(a.frames + base)) & 63u) >> 4 : 0u;
@@ -283,7 +290,7 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
       const uint32_t ack = (((h.x >> 16) & 0xFFu) << 8) | (h.x >> 24);
       const uint32_t flags = h.y & 0xFFu;
       const uint32_t inband = (((h.y >> 8) & 0xFFu) << 8) | ((h.y >> 16) & 0xFFu);
-      finish_packet<H>(a, p, sum, seq, ack, flags, inband);
+      finish_packet<H, true>(a, p, sum, seq, ack, flags, H == 5 ? want_cs : inband);
     }
     return;
   }
@@ -305,7 +312,7 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
     const uint32_t c = packet_csum(sum, seq, ack, flags);
     uint8_t ok;
     if (H == 7) ok = (c == inband) ? 1 : 0;
-    else if (a.csum_in) ok = (c == a.csum_in[p]) ? 1 : 0;
+    else if (a.csum_in) ok = (c == want_cs) ? 1 : 0;
     else ok = 3;
     s_seq[q] = (uint16_t)seq;
     s_ack[q] = (uint16_t)ack;
