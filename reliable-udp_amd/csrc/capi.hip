@@ -113,6 +113,12 @@ EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t*
       a.hchunk = 1;
       a.hc_off = a.hdr_bytes;
       a.hdr_bytes += (a.T + 1u) * 32u;
+      const int scr = tuning().encode_hc_scratch;
+      if (scr == 1 || (scr < 0 && a.T * a.L <= 16384u)) {
+        a.hc_scratch = 1;
+        a.scr_off = a.hdr_bytes;
+        a.hdr_bytes += a.T * 48u;
+      }
     }
     a.invF = ((1ull << 32) + F - 1ull) / F;
     a.num_tiles = (uint32_t)((a.n + a.T - 1) / a.T);

@@ -278,8 +278,31 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
       const uint32_t P = q * (L + H) + H;
       u32x4* hc = reinterpret_cast<u32x4*>(lds + a.hc_off) + 2u * q;
       const uint32_t X0 = (P - H) & ~15u, X1 = (P + 15u) & ~15u;
-      for (uint32_t X = X0; X < X1; X += 16)
-        hc[(X - X0) >> 4] = header_chunk<H>(X, P, h, img[q * V - 1u], img[q * V]);
+      const u32x4 tail = img[q * V - 1u], head = img[q * V];
+      if (a.hc_scratch) {
+        // [previous payload's last 16 | header | first 16 payload bytes] laid
+        // out in 48 B of LDS with compile-time shifts; each chunk is then one
+        // byte-shifted window (no variable-shift funnels).
+        constexpr uint32_t b = (uint32_t)H & 3u, sl = 8u * b, sr = 32u - 8u * b;
+        uint32_t* scr = reinterpret_cast<uint32_t*>(lds + a.scr_off) + 12u * q;
+        reinterpret_cast<u32x4*>(scr)[0] = tail;
+        u32x4 w1, w2;
+        w1.x = (uint32_t)h;
+        w1.y = ((uint32_t)(h >> 32) & ((1u << sl) - 1u)) | (head.x << sl);
+        w1.z = (head.x >> sr) | (head.y << sl);
+        w1.w = (head.y >> sr) | (head.z << sl);
+        w2.x = (head.z >> sr) | (head.w << sl);
+        w2.y = head.w >> sr;
+        w2.z = 0u;
+        w2.w = 0u;
+        reinterpret_cast<u32x4*>(scr)[1] = w1;
+        reinterpret_cast<u32x4*>(scr)[2] = w2;
+        for (uint32_t X = X0; X < X1; X += 16)
+          hc[(X - X0) >> 4] = window16_dw(scr, 16u + X - (P - H));
+      } else {
+        for (uint32_t X = X0; X < X1; X += 16)
+          hc[(X - X0) >> 4] = header_chunk<H>(X, P, h, tail, head);
+      }
     }
   }
   __syncthreads();

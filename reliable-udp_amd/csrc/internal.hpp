@@ -31,6 +31,8 @@ struct EncodeTileArgs {
   uint32_t early_table;     // tile kernel: header-table loads issued before phase 1
   uint32_t hchunk;          // tile kernel (T % 16 == 0): leaders prebuild header chunks in LDS
   uint32_t hc_off;          // LDS byte offset of the header-chunk array [T + 1][2] x 16 B
+  uint32_t hc_scratch;      // leaders build header chunks through a 48-B LDS scratch per packet
+  uint32_t scr_off;         // LDS byte offset of that scratch [T][48 B]
   uint32_t span;
   uint32_t span_glog;       // log2 lanes per packet in the span sum pass
   double rcpF;              // 1.0 / (L + H)
@@ -176,6 +178,12 @@ struct Tuning {
   // 0.0287 -> 0.0267 ms, x 256 B 0.0934 -> 0.0892, x 1024 B 0.3606 ->
   // 0.3557), after above (x 1472 B 0.5208 vs 0.5291 early).
   int encode_early_table = -1;
+  // Leaders build header chunks through a 48-B LDS scratch per packet
+  // (constant shifts, one window per chunk) instead of variable-shift
+  // funnels: 1, 0, or -1 = automatic (tiles of at most 16 KiB: 1M x 64 B
+  // 0.0272 -> 0.0266 ms, x 256 B 0.0923 -> 0.0912; x 1472 B within noise;
+  // profiles/r01/sweeps/encode_hc_scratch.json).
+  int encode_hc_scratch = -1;
   // Decode tile outputs staged in LDS and written as whole dwords (output
   // pointers 4-B aligned): 1M x 256 B verify 0.0489 -> 0.0470 ms, x 64 B
   // 0.0156 -> 0.0152, x 1472 B equal; copy-out equal to +1%

@@ -99,8 +99,8 @@ def test_prebuilt_header_chunks_vs_oracle(cuda, L):
             for tile in (0, 16, 32, 256):
                 if tile and tile * L > 65536:
                     continue
-                for align, early in ((0, 0), (1, 0), (0, 1), (-1, -1)):
-                    fr, cs = _with(lib, [(29, 1), (2, tile), (23, align), (30, early)],
+                for align, early, scr in ((0, 0, 0), (1, 0, 0), (0, 1, 0), (-1, -1, 0), (0, 0, 1), (-1, -1, 1)):
+                    fr, cs = _with(lib, [(29, 1), (2, tile), (23, align), (30, early), (37, scr)],
                                    lambda: _encode(cuda, seq, ack, flags, pay, layout))
-                    assert np.array_equal(fr, want_fr), (L, n, layout, tile, align, early)
-                    assert np.array_equal(cs, want_cs), (L, n, layout, tile, align, early)
+                    assert np.array_equal(fr, want_fr), (L, n, layout, tile, align, early, scr)
+                    assert np.array_equal(cs, want_cs), (L, n, layout, tile, align, early, scr)
