@@ -388,7 +388,6 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, ui
   if ((rc = dev_scope.set(device))) return rc;
   DecodeArgs a{};
   a.align64 = tuning().out_align64 == 1 ? 1u : 0u;
-  a.dma = tuning().tile_dma ? 1u : 0u;
   a.stage_out = (tuning().decode_stage_out &&
                  ((reinterpret_cast<uintptr_t>(d_seq) | reinterpret_cast<uintptr_t>(d_ack) |
                    reinterpret_cast<uintptr_t>(d_flags) | reinterpret_cast<uintptr_t>(d_ok) |
@@ -500,7 +499,6 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
   if (tuning().varlen_vec && tuning().varlen_tile)
     varlen_tile_geometry(in->payload_len, &a.tile_T, &a.tile_glog, &a.tile_cap);
   a.align64 = tuning().out_align64 == 1 ? 1u : 0u;
-  a.dma = tuning().tile_dma ? 1u : 0u;
   // Header-table loads before phase 1 for hints of 128 B and up: with the
   // fast phase 2 (varlen_hchunk) they measured 1M x 1472 B 0.637 -> 0.603 ms,
   // x 1024 B 0.489 -> 0.468, x 256 B 0.170 -> 0.164

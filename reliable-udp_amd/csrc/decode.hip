@@ -214,22 +214,7 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
   // vectors before it go last): every wave's 1 KiB load covers whole sectors.
   uint32_t npre = a.align64 ? (uint32_t)((-reinterpret_cast<uintptr_t>(a.frames + base)) & 63u) >> 4 : 0u;
   if (npre > nvec) npre = nvec;
-  const bool dma = a.dma && !a.align64;
-  if (dma) {
-    // LDS-DMA for the whole vectors (1 KiB per wave-instruction, lane-linear);
-    // a partial last vector of the batch is read bytewise below.
-    const uint64_t whole = total > base ? (total - base) >> 4 : 0u;
-    const uint32_t ndma = whole < nvec ? (uint32_t)whole : nvec;
-    const uint32_t lane = tid & 63u;
-    const u32x4* src = reinterpret_cast<const u32x4*>(a.frames + base);
-    for (uint32_t v0 = tid & ~63u; v0 < ndma; v0 += kBlock)
-      if (v0 + lane < ndma)
-        __builtin_amdgcn_global_load_lds(
-            (const void __attribute__((address_space(1)))*)(src + v0 + lane),
-            (void __attribute__((address_space(3)))*)(tile + v0), 16, 0, 2);
-    if (ndma < nvec && tid == 0) tile[ndma] = load16_guarded(a.frames, base + 16ull * ndma, total);
-  }
-  for (uint32_t v0 = tid; !dma && v0 < nvec; v0 += 8u * kBlock) {
+  for (uint32_t v0 = tid; v0 < nvec; v0 += 8u * kBlock) {
     u32x4 r[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {

@@ -52,7 +52,6 @@ struct DecodeArgs {
   uint32_t F;               // frame bytes
   uint32_t glog;            // log2(lanes per packet)
   uint32_t align64;         // tile kernel: wave loads/stores start on 64-B sector boundaries
-  uint32_t dma;             // tile kernel: phase 1 by LDS-DMA (when align64 is off)
   uint32_t stage_out;       // tile kernel: outputs staged in LDS, written as dwords (pointers 4-B aligned)
 };
 
@@ -95,7 +94,6 @@ struct VarlenArgs {
   uint32_t tile_glog;
   uint32_t tile_cap;
   uint32_t align64;               // tile kernel: wave stores start on 64-B sector boundaries
-  uint32_t dma;                   // tile kernel: phase 1 by LDS-DMA
   uint32_t early_table;           // tile kernel: header-table loads before phase 1
   uint32_t ablate;                // diagnostics only (wrong output): 1 = phase 2 without the frame walk
   uint32_t vhc;                   // tile kernel: prebuilt header chunks + pure-chunk fast phase 2
@@ -165,10 +163,6 @@ struct Tuning {
   int encode_dma = 1;
   // Encode by fixed output spans (encode_span_kernel; opt-in, bit-exact, not
   // faster at MTU size: 1M x 1472 B 0.530 vs 0.518 ms, x 1024 B 0.352 vs 0.363).
-  // Decode and varlen-encode tile phase 1 by LDS-DMA: opt-in, measured no
-  // faster (1M x 64 B verify 0.0208 vs 0.0198 ms, copy-out 0.0263 vs 0.0253;
-  // 1472 B varlen encode 0.641 vs 0.632; profiles/r01/sweeps/tile_dma.json).
-  int tile_dma = 0;
   // Encode tile phase 2 with header chunks prebuilt by the packet leaders
   // (T % 16 == 0): 1M x 64 B 0.0295 -> 0.0287 ms, x 256 B 0.0962 -> 0.0938,
   // x 1024 B 0.3712 -> 0.3683, x 1472 B equal (profiles/r01/sweeps/encode_hchunk.json).

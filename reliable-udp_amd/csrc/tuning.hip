@@ -247,8 +247,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // encode; 21: its packets per workgroup (0 auto); 22: its load rounds in flight;
 // 23: output wave stores start on 64-B sector boundaries; 24: varlen frame
 // offsets by the three-pass scan (1) or hipcub (0); 25: encode phase 1 by LDS-DMA;
-// 26: encode by fixed output spans; 27: span bytes per workgroup; 28: decode and
-// varlen-encode tile phase 1 by LDS-DMA; 29: encode phase 2 with prebuilt header chunks;
+// 26: encode by fixed output spans; 27: span bytes per workgroup; (28: decode and
+// varlen-encode phase 1 by LDS-DMA, measured no faster and removed); 29: encode phase 2 with prebuilt header chunks;
 // 30: encode header-table loads before phase 1; 31: fixed-stride UTF-8 validation
 // through LDS tiles; 32: dedup window pass by LDS hash table; 33: varlen decode
 // through LDS tiles; 34: decode tile outputs staged in LDS; 35: varlen encode tile
@@ -268,7 +268,6 @@ int rudpx_tune(int key, int value) {
             : key == 18 ? &t.varlen_tile_bytes : key == 20 ? &t.encode_stream
             : key == 21 ? &t.encode_stream_T : key == 22 ? &t.encode_stream_R : key == 23 ? &t.out_align64 : key == 24 ? &t.varlen_scan : key == 25 ? &t.encode_dma
             : key == 26 ? &t.encode_span : key == 27 ? &t.encode_span_bytes
-            : key == 28 ? &t.tile_dma
             : key == 29 ? &t.encode_hchunk
             : key == 30 ? &t.encode_early_table
             : key == 31 ? &t.utf8_tile

@@ -277,17 +277,8 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_tile_kernel(VarlenArgs a
     const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + A);
     u32x4* dst = reinterpret_cast<u32x4*>(lds_pay + kVTGuard);
     const uint32_t nvec = (uint32_t)(run >> 4);
-    if (a.dma) {
-      // LDS-DMA: each wave-instruction moves 1 KiB of the run into the tile
-      const uint32_t lane = tid & 63u;
-      for (uint32_t v0 = tid & ~63u; v0 < nvec; v0 += kBlock)
-        if (v0 + lane < nvec)
-          __builtin_amdgcn_global_load_lds(
-              (const void __attribute__((address_space(1)))*)(src + v0 + lane),
-              (void __attribute__((address_space(3)))*)(dst + v0), 16, 0, 2);
-    }
     constexpr uint32_t P = 8;
-    for (uint32_t v0 = tid; !a.dma && v0 < nvec; v0 += P * kBlock) {
+    for (uint32_t v0 = tid; v0 < nvec; v0 += P * kBlock) {
       u32x4 r[P];
 #pragma unroll
       for (uint32_t u = 0; u < P; ++u) {
