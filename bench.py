@@ -221,6 +221,25 @@ def legs(torch, batch, device, steps):
     out["varlen_1M_x_1char"] = {"encode_Mpkt_s": n1 / ms_e / 1e3, "encode_ms": ms_e,
                                 "decode_verify_Mpkt_s": n1 / ms_d / 1e3, "decode_ms": ms_d,
                                 "note": "includes the host-side bounds checks (one sync) per call"}
+    # the varlen path at MTU size: 1M x 1472 B payloads packed back to back
+    # (frames at odd offsets), encode (scan + tile kernel) and decode-verify
+    # through the Python entry points, bounds checks included
+    tabm, paym = batch.synth_batch(n1, 1472, SEEDS[1472], device=device)
+    lensm = torch.full((n1,), 1472, dtype=torch.int32, device=device)
+    flatm = paym.view(-1)
+    encm = batch.pack_batch_varlen(tabm, flatm, lensm, "rudp7")
+    ms_em = time_loop(torch, lambda i: batch.pack_batch_varlen(tabm, flatm, lensm, "rudp7"), steps, 3) / steps
+    ms_dm = time_loop(torch, lambda i: batch.unpack_batch_varlen(encm.frames, encm.frame_off, "rudp7"),
+                      steps, 3) / steps
+    # algorithmic bytes: encode reads payload + len + table (1472 + 4 + 5), writes frame + offset
+    # (1479 + 8); decode reads frame + offset, writes seq/ack/flags/ok/csum (8)
+    out["varlen_1Mx1472"] = {
+        "encode_GiB_s": n1 * 1472 / (ms_em / 1e3) / GIB, "encode_ms": ms_em,
+        "encode_roofline_frac": n1 * (1472 + 9 + 1479 + 8) / (ms_em / 1e3) / 1e9 / HBM_PEAK_GBS,
+        "decode_GiB_s": n1 * 1472 / (ms_dm / 1e3) / GIB, "decode_ms": ms_dm,
+        "decode_roofline_frac": n1 * (1479 + 8 + 8) / (ms_dm / 1e3) / 1e9 / HBM_PEAK_GBS,
+        "note": "Python entry incl. the bounds check (one sync) and the offset scan"}
+    del tabm, paym, lensm, flatm, encm
     # the proxy's retransmission check (proxy.py:90, 500-deep history) over the same 1M datagrams
     ms_x = time_loop(torch, lambda i: batch.detect_retransmissions(enc.frames, frame_off=enc.frame_off,
                                                                    window=500), steps, 3) / steps
