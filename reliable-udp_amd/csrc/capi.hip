@@ -334,7 +334,8 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
   // the run can stream) made it 2-7% slower (profiles/r01/sweeps/varlen_decode_tile.json).
   if (tuning().varlen_decode_tile && (len_hint >= 512u || tuning().varlen_decode_tile == 2)) {
     const uint64_t hint = len_hint ? len_hint : 16u;
-    const uint64_t cap = (((256u >> lg) * hint * 5u / 4u + 256u) + 15u) & ~15ull;
+    const uint64_t pct = (uint64_t)tuning().varlen_decode_cap_pct;
+    const uint64_t cap = (((256u >> lg) * hint * pct / 100u + 256u) + 15u) & ~15ull;
     a.tile_cap = cap <= 49152u ? (uint32_t)cap : 0u;
   }
   rc = launch_decode_varlen(a, layout, (hipStream_t)hip_stream);

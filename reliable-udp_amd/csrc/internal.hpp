@@ -189,6 +189,11 @@ struct Tuning {
   // B 0.562 -> 0.477, x 256 B 0.196 -> 0.169 (Python entry, one box;
   // profiles/r01/sweeps/varlen_encode_hchunk.json).
   int varlen_hchunk = 1;
+  // Varlen decode tile: LDS budget in % of the hinted run.  110 lets six
+  // 1472-B tiles share a CU (125 held five): 1M x 1479 B 0.288 -> 0.277 ms,
+  // lengths uniform in [0, 2944] 0.315 -> 0.306 (overflowing tiles take the
+  // per-frame path in the launch; profiles/r01/sweeps/varlen_decode_cap.json).
+  int varlen_decode_cap_pct = 110;
   int varlen_decode_tile = 1;  // varlen decode through LDS tiles for hints >= 512 B (2: any hint; 0: never)
   int dedup_table = 1;    // dedup window pass by LDS hash table (0: every frame scans its window)
   int utf8_tile = 1;      // fixed-stride UTF-8 validation through LDS tiles (0: per-frame vector kernel)

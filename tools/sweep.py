@@ -65,6 +65,7 @@ BLOCKS_OVERRIDE = None
 ENCODE_LS = None
 PERCU_OVERRIDE = None      # encode: tiles-per-CU caps to try (256-thread blocks)
 TILES_OVERRIDE = None      # encode: packets per tile to try
+VDEC_CAP_PCTS = ()         # vdec: extra varlen-decode tile LDS budgets (% of the hinted run)
 GEOMETRY_VARIANTS = False
 STREAM_ABLATE = False      # stream: also time stage ablations (wrong output; key 13 bits 8/16)  # varlen_enc: also sweep tile size knobs (keys 17, 18)
 
@@ -305,10 +306,13 @@ def vdec_sweep(reps):
                                           o16[0].data_ptr(), o16[1].data_ptr(), o8[0].data_ptr(),
                                           o8[1].data_ptr(), o16[2].data_ptr(), None, 7, 0, stream))
         name = f"L{L}" if L >= 0 else "U0-2944"
-        variants = {f"{name}_tile": (lambda: lib.rudpx_tune(33, 2), run),
+        variants = {f"{name}_tile": (lambda: (lib.rudpx_tune(33, 2), lib.rudpx_tune(38, 110)), run),
                     f"{name}_vec": (lambda: lib.rudpx_tune(33, 0), run)}
+        for pct in VDEC_CAP_PCTS:
+            variants[f"{name}_tile_cap{pct}"] = (lambda pct=pct: (lib.rudpx_tune(33, 2), lib.rudpx_tune(38, pct)), run)
         res = interleaved(variants, reps)
         lib.rudpx_tune(33, 1)
+        lib.rudpx_tune(38, 110)
         alg = n * (mean + 8 + 8)  # frames + offsets read, seq/ack/flags/ok/csum written
         for k, ms in res.items():
             out[k] = {"ms": ms, "TBs": alg / ms / 1e9, "frac": alg / ms / 1e9 / 8.0}
@@ -695,6 +699,8 @@ def main():
             specs.append((name, [tuple(int(y) for y in x.split("=")) for x in kvs.split(",") if x]))
         result["multi"] = multi_sweep(args.reps, specs)
     if args.only == "vdec":
+        global VDEC_CAP_PCTS
+        VDEC_CAP_PCTS = (105, 125)
         result["vdec"] = vdec_sweep(args.reps)
     if args.only == "knob":
         pre = [tuple(int(y) for y in x.split("=")) for x in args.pre.split(",") if x]
