@@ -194,6 +194,10 @@ struct Tuning {
   // lengths uniform in [0, 2944] 0.315 -> 0.306 (overflowing tiles take the
   // per-frame path in the launch; profiles/r01/sweeps/varlen_decode_cap.json).
   int varlen_decode_cap_pct = 110;
+  // Varlen encode tile: LDS budget in % of the hinted run (110: 1M x 1472 B
+  // 0.619 -> 0.586 ms, x 1024 B 0.468 -> 0.463, x 256 B 0.167 -> 0.164 vs
+  // 125; profiles/r01/sweeps/varlen_encode_cap.json).
+  int varlen_encode_cap_pct = 110;
   int varlen_decode_tile = 1;  // varlen decode through LDS tiles for hints >= 512 B (2: any hint; 0: never)
   int dedup_table = 1;    // dedup window pass by LDS hash table (0: every frame scans its window)
   int utf8_tile = 1;      // fixed-stride UTF-8 validation through LDS tiles (0: per-frame vector kernel)

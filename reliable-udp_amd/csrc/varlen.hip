@@ -927,8 +927,8 @@ int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
 
 void varlen_tile_geometry(uint32_t len_hint, uint32_t* T, uint32_t* glog, uint32_t* cap) {
   // About 24 KiB of payload per tile (the fixed-length encode's T = 16 at
-  // 1472 B); room for 1.25x the hinted run before a tile takes the per-packet
-  // path.  Hints above 6 KiB use the per-packet vector kernel (T = 0).
+  // 1472 B); room for 1.1x the hinted run (varlen_encode_cap_pct) before a
+  // tile takes the per-packet path.  Hints above 6 KiB use the per-packet vector kernel (T = 0).
   // 1M x 1472 B with the scan: 0.63 vs 0.77 ms; lengths uniform in
   // [0, 2944]: 0.75 vs 1.04 ms (tools/sweep.py --only varlen_enc).
   const uint32_t h = len_hint;
@@ -941,7 +941,7 @@ void varlen_tile_geometry(uint32_t len_hint, uint32_t* T, uint32_t* glog, uint32
   while (t > 4 && (t > maxT || t * h > bytes)) { t >>= 1; ++lg; }
   *T = t;
   *glog = lg;
-  *cap = ((t * h + (t * h >> 2) + 256u) + 15u) & ~15u;
+  *cap = ((t * h * (uint32_t)tuning().varlen_encode_cap_pct / 100u + 256u) + 15u) & ~15u;
   if (*cap < 1024u) *cap = 1024u;
 }
 
