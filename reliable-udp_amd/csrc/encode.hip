@@ -570,12 +570,17 @@ int launch_tile(const EncodeTileArgs& args, hipStream_t stream) {
   const uint64_t blocks = (args.n + args.T - 1) / args.T;
   size_t lds = args.hdr_bytes + kLdsGuard + (size_t)args.T * args.L + 32;
   int per_cu = tuning().encode_blocks_per_cu;
-  // Auto: at most 5 resident tiles per CU for big tiles (> 16 KiB payload).
-  // Fewer tiles in flight keep the concurrent HBM footprint tighter: 1M x 1472 B
-  // 0.510 ms at 5 per CU vs 0.540 ms at the natural 6; 1M x 1024 B (16 KiB
-  // tiles) is the other way round, 0.363 ms natural vs 0.383 ms at 5
-  // (tools/sweep.py, r01).
-  if (per_cu < 0) per_cu = (size_t)args.T * args.L > 16384 ? 5 : 0;
+  // Auto: cap resident tiles per CU by tile payload, so the concurrent HBM
+  // footprint stays near 70-120 KiB per CU: 5 above 14 KiB (1M x 1472 B
+  // 0.504 vs 0.516 ms at 6; x 1024 B 0.357 vs 0.370 ms natural), 6 above
+  // 10 KiB (x 768 B 0.259 vs 0.270 ms natural), natural below (x 512 B
+  // 0.176 vs 0.181 at 7).  (profiles/r01/sweeps/encode_percu_lds_dma.json;
+  // before LDS-DMA phase 1 and early table loads, 16 KiB tiles preferred
+  // natural occupancy.)
+  if (per_cu < 0) {
+    const size_t bytes = (size_t)args.T * args.L;
+    per_cu = bytes > 14336 ? 5 : bytes > 10240 ? 6 : 0;
+  }
   if (per_cu > 0) {  // reserve LDS to cap resident workgroups per CU
     const size_t want = ((size_t)(160 * 1024) / (size_t)per_cu) & ~size_t(15);
     if (want > lds) lds = want;
