@@ -383,6 +383,25 @@ int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream
     if (path == DecodePath::kCopyTile || path == DecodePath::kVerifyTile) {
       size_t lds = ((size_t)per_block * args.F + 32 + 15) & ~size_t(15);
       if (args.stage_out) lds += 8u * per_block;  // staged outputs
+      // Resident tiles per CU: verify-only wants every tile it can get; the
+      // copy-out (read + write, like encode) runs best at 5 for tiles over
+      // 14 KiB (1M x 1024 B 0.348 -> 0.340 ms, x 1472 B 0.518 -> 0.515; verify
+      // at 5: 0.169 -> 0.209 ms; profiles/r01/sweeps/decode_percu.json).
+      int per_cu = tuning().decode_blocks_per_cu;
+      if (per_cu < 0) per_cu = (path == DecodePath::kCopyTile && (size_t)per_block * args.F > 14336u) ? 5 : 0;
+      if (per_cu > 0) {
+        const size_t want = ((size_t)(160 * 1024) / (size_t)per_cu) & ~size_t(15);
+        if (want > lds) lds = want;
+      }
+      if (lds > 65536) {
+        const void* fn = path == DecodePath::kCopyTile
+            ? (layout == 7 ? reinterpret_cast<const void*>(&decode_tile_kernel<7, true>)
+                           : reinterpret_cast<const void*>(&decode_tile_kernel<5, true>))
+            : (layout == 7 ? reinterpret_cast<const void*>(&decode_tile_kernel<7, false>)
+                           : reinterpret_cast<const void*>(&decode_tile_kernel<5, false>));
+        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return (int)e;
+      }
       const dim3 grid((uint32_t)blocks), block(kBlock);
       if (path == DecodePath::kCopyTile) {
         if (layout == 7) hipLaunchKernelGGL((decode_tile_kernel<7, true>), grid, block, lds, stream, args);

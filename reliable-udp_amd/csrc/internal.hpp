@@ -183,6 +183,7 @@ struct Tuning {
   // 0.0156 -> 0.0152, x 1472 B equal; copy-out equal to +1%
   // (profiles/r01/sweeps/decode_stage_out.json).
   int decode_stage_out = 1;
+  int decode_blocks_per_cu = -1;  // decode tile: cap resident tiles per CU (0 = natural, -1 = auto)
   int varlen_ablate = 0;  // VarlenArgs::ablate (sweeps only)
   // Varlen encode tile: prebuilt header chunks and a one-window phase 2 for
   // tiles whose frames are all >= 32 B: 1M x 1472 B 0.738 -> 0.631 ms, x 1024
