@@ -127,7 +127,11 @@ EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t*
     const uint32_t V = a.L / 16u;
     a.invV = ((1ull << 32) + V - 1ull) / V;
     const int al = tuning().out_align64;
-    a.out_align64 = (al == 1 || (al < 0 && a.T * a.L > 16384u)) ? 1u : 0u;
+    // Fixed-length encode deals wave stores from the first 64-B boundary at
+    // every tile size (since LDS-DMA phase 1 and the header-chunk phase 2 it
+    // measured equal or 0.4-1.3% faster from 64 to 1472 B;
+    // profiles/r01/sweeps/align64_after_dma.json).
+    a.out_align64 = al != 0 ? 1u : 0u;
     const uint32_t S = (uint32_t)tuning().encode_span_bytes;
     if (tuning().encode_span && a.L >= 256u && S >= 1024u && S <= 32768u && S % 64u == 0 && F < S) {
       a.span = S;

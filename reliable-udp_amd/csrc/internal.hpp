@@ -151,10 +151,11 @@ struct Tuning {
   int encode_stream_T = 0;  // stream kernel packets per workgroup; 0 = automatic
   int encode_stream_R = 2;  // stream kernel rounds of loads in flight per lane (1, 2, 4)
   // Wave loads/stores of the tile kernels start on a 64-B sector boundary
-  // (1) or on the first 16-B one (0).  -1 = automatic: on for encode tiles
-  // over 16 KiB of payload (1M x 1472 B: 0.516 vs 0.533 ms), off elsewhere,
-  // where it measured 1-3% slower (decode, L = 1024 encode, varlen;
-  // profiles/r01/sweeps/align64.json).
+  // (1) or on the first 16-B one (0).  -1 = automatic: on for fixed-length
+  // encode at every tile size (1M x 1472 B: 0.516 vs 0.533 ms; smaller
+  // tiles equal or up to 1.3% faster since LDS-DMA phase 1), off for decode
+  // and varlen, where it measured 1-3% slower
+  // (profiles/r01/sweeps/align64.json, align64_after_dma.json).
   int out_align64 = -1;
   // Encode tile phase 1 by LDS-DMA (global_load_lds_dwordx4) in place of
   // register staging (256-thread contiguous tiles, nt loads and stores):
