@@ -109,6 +109,7 @@ struct Utf8Args {
   uint32_t H;
   uint8_t* valid;
   uint32_t glog;              // log2 lanes per frame (vector kernel)
+  uint32_t tile_cap;          // varlen tile kernel: LDS bytes a tile's run may use
 };
 
 struct DedupArgs {
@@ -202,7 +203,14 @@ struct Tuning {
   int varlen_encode_cap_pct = 110;
   int varlen_decode_tile = 1;  // varlen decode through LDS tiles for hints >= 512 B (2: any hint; 0: never)
   int dedup_table = 1;    // dedup window pass by LDS hash table (0: every frame scans its window)
-  int utf8_tile = 1;      // fixed-stride UTF-8 validation through LDS tiles (0: per-frame vector kernel)
+  int utf8_tile = 1;
+  // Packed-frame UTF-8 validation through LDS tiles (hints >= 512 B) and its
+  // LDS budget in % of the hinted run: 1M x 1479 B ASCII frames 0.287 ->
+  // 0.279 ms, lengths uniform in [0, 2944] 0.373 -> 0.370 at 130% (110%:
+  // more tiles overflow to the HBM path on ragged lengths; 150%: fewer tiles
+  // per CU; tools/utf8_varlen_sweep.py, profiles/r01/sweeps/utf8_varlen_tile.json).
+  int utf8_vtile = 1;
+  int utf8_vtile_cap_pct = 130;      // fixed-stride UTF-8 validation through LDS tiles (0: per-frame vector kernel)
   int encode_span = 0;
   int encode_span_bytes = 8192;  // span kernel: output bytes per workgroup (multiple of 64)
   int varlen_scan = 1;    // frame offsets: 1 = reduce-then-scan (scan.hip), 0 = hipcub

@@ -254,7 +254,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // through LDS tiles; 34: decode tile outputs staged in LDS; 35: varlen encode tile
 // stage ablation (diagnostic); 36: varlen encode tile prebuilt header chunks;
 // 37: encode header chunks through an LDS scratch; 38: varlen decode tile LDS budget (%);
-// 39: varlen encode tile LDS budget (%); 40: decode tiles per CU cap.
+// 39: varlen encode tile LDS budget (%); 40: decode tiles per CU cap; 41: packed-frame
+// UTF-8 validation through LDS tiles; 42: its LDS budget (%).
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
@@ -280,7 +281,9 @@ int rudpx_tune(int key, int value) {
             : key == 37 ? &t.encode_hc_scratch
             : key == 38 ? &t.varlen_decode_cap_pct
             : key == 39 ? &t.varlen_encode_cap_pct
-            : key == 40 ? &t.decode_blocks_per_cu : nullptr;
+            : key == 40 ? &t.decode_blocks_per_cu
+            : key == 41 ? &t.utf8_vtile
+            : key == 42 ? &t.utf8_vtile_cap_pct : nullptr;
   if (!slot) return -22;
   const int old = *slot;
   *slot = value;

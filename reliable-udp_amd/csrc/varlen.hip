@@ -836,6 +836,43 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_vec_kernel(Utf8Args a) {
   if (valid_p && g == 0) a.valid[p] = bad ? 0 : 1;
 }
 
+// Strict UTF-8 check of one frame's payload bytes [s, fe) by G lanes (lane g
+// takes aligned chunks c_lo + g, + G, ...): `chunk(c)` returns aligned chunk c
+// and `prev(x)` the dword of bytes x-4 .. x-1 (x a multiple of 16; only bytes
+// at or past s are used).  Returns nonzero if this lane saw an invalid byte.
+template <class Chunk, class Prev>
+__device__ __forceinline__ uint32_t utf8_check_frame(uint64_t s, uint64_t fe, uint32_t g, uint32_t G,
+                                                     Chunk chunk, Prev prev_dw) {
+  uint32_t bad = 0;
+  if (fe <= s) return 0;
+  const uint64_t c_lo = s >> 4, c_hi = (fe - 1u) >> 4;
+  for (uint64_t c = c_lo + g; c <= c_hi; c += G) {
+    const uint64_t x = c << 4;
+    const u32x4 v = chunk(c);
+    const uint32_t prev = prev_dw(x);
+    uint32_t p3 = x >= s + 3 ? (prev >> 8) & 0xFFu : 0u;
+    uint32_t p2 = x >= s + 2 ? (prev >> 16) & 0xFFu : 0u;
+    uint32_t p1 = x >= s + 1 ? prev >> 24 : 0u;
+    const int lo_b = (int)((int64_t)s - (int64_t)x), hi_b = (int)((int64_t)fe - (int64_t)x);
+    const uint64_t pl = lo64(v) & byte_mask(lo_b, hi_b), ph = hi64(v) & byte_mask(lo_b - 8, hi_b - 8);
+    if (((pl | ph) & 0x8080808080808080ull) == 0 && p1 < 0xC0 && p2 < 0xC0 && p3 < 0xC0) continue;
+    if (bad) continue;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint64_t y = x + (uint64_t)k;
+      if (y < s || y >= fe) continue;
+      const uint32_t cb = byte_of(v, k);
+      bad |= utf8_byte_ok(cb, p1, p2, p3) ? 0u : 1u;
+      p3 = p2;
+      p2 = p1;
+      p1 = cb;
+    }
+    if (c == c_hi)  // the frame's last chunk: nothing may still be expected
+      bad |= (utf8_need(p1) >= 1 || utf8_need(p2) >= 2 || utf8_need(p3) >= 3) ? 1u : 0u;
+  }
+  return bad;
+}
+
 // Fixed-stride frames through an LDS tile (frames 16-B aligned, H < F,
 // T = 256 / G frames per workgroup with T % 16 == 0, so the tile starts on a
 // 16-B boundary): the decode tile kernel's shape.  Phase 1 streams the tile's
@@ -874,32 +911,62 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_tile_kernel(Utf8Args a) 
   __syncthreads();
   uint32_t bad = 0;
   if (q < Tv) {
-    const uint32_t s = q * F + H, fe = q * F + F;  // payload bytes [s, fe) of the tile
-    const uint32_t c_lo = s >> 4, c_hi = (fe - 1u) >> 4;
     const uint32_t* dw = reinterpret_cast<const uint32_t*>(lds + 16);
-    for (uint32_t c = c_lo + g; c <= c_hi; c += G) {
-      const uint32_t x = c << 4;
-      const u32x4 v = tile[c];
-      const uint32_t prev = dw[(x >> 2) - 1u];  // bytes x-4 .. x-1 (the guard before x = 0)
-      uint32_t p3 = x >= s + 3 ? (prev >> 8) & 0xFFu : 0u;
-      uint32_t p2 = x >= s + 2 ? (prev >> 16) & 0xFFu : 0u;
-      uint32_t p1 = x >= s + 1 ? prev >> 24 : 0u;
-      const int lo_b = (int)s - (int)x, hi_b = (int)fe - (int)x;
-      const uint64_t pl = lo64(v) & byte_mask(lo_b, hi_b), ph = hi64(v) & byte_mask(lo_b - 8, hi_b - 8);
-      if (((pl | ph) & 0x8080808080808080ull) == 0 && p1 < 0xC0 && p2 < 0xC0 && p3 < 0xC0) continue;
-      if (bad) continue;
-#pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const uint32_t y = x + (uint32_t)k;
-        if (y < s || y >= fe) continue;
-        const uint32_t cb = byte_of(v, k);
-        bad |= utf8_byte_ok(cb, p1, p2, p3) ? 0u : 1u;
-        p3 = p2;
-        p2 = p1;
-        p1 = cb;
-      }
-      if (c == c_hi)  // the frame's last chunk: nothing may still be expected
-        bad |= (utf8_need(p1) >= 1 || utf8_need(p2) >= 2 || utf8_need(p3) >= 3) ? 1u : 0u;
+    bad = utf8_check_frame(q * F + H, q * F + F, g, G,  // payload bytes [s, fe) of the tile
+                           [&](uint64_t c) { return tile[c]; },
+                           [&](uint64_t x) { return dw[(x >> 2) - 1u]; });  // x = 0 reads the guard
+  }
+  for (uint32_t m = G >> 1; m > 0; m >>= 1) bad |= __shfl_xor(bad, (int)m, 64);
+  if (g == 0 && q < Tv) a.valid[p0 + q] = bad ? 0 : 1;
+}
+
+// Packed variable-length frames through an LDS tile (frames 16-B aligned;
+// hints of 512 B and up): a workgroup owns T = 256 / G consecutive frames,
+// one contiguous run [frame_off[p0], frame_off[p0 + T]) streamed into LDS by
+// LDS-DMA; the frames' offsets come along.  A run over tile_cap (lengths far
+// above the hint) checks its frames straight from HBM instead.
+__global__ void __launch_bounds__(kBlock) validate_utf8_vtile_kernel(Utf8Args a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t glog = a.glog, G = 1u << glog, T = kBlock >> glog;
+  const uint32_t q = tid >> glog, g = tid & (G - 1u);
+  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  const uint64_t left = a.n - p0;
+  const uint32_t Tv = left < T ? (uint32_t)left : T;
+  const uint64_t total = a.frame_off[a.n];
+  const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
+  const uint64_t A = fo0 & ~15ull;
+  const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
+  uint32_t bad = 0;
+  if (run > a.tile_cap) {  // uniform over the workgroup: frames straight from HBM
+    if (q < Tv)
+      bad = utf8_check_frame(a.frame_off[p0 + q] + a.H, a.frame_off[p0 + q + 1], g, G,
+                             [&](uint64_t c) { return load16_guarded(a.frames, c << 4, total); },
+                             [&](uint64_t x) {
+                               return x >= 4 ? *reinterpret_cast<const uint32_t*>(a.frames + x - 4) : 0u;
+                             });
+  } else {
+    uint32_t* lds_fo = reinterpret_cast<uint32_t*>(lds);                    // [T + 1]
+    const uint32_t img_off = ((((T + 1u) * 4u) + 15u) & ~15u) + 16u;       // 16 B guard before the run
+    u32x4* img = reinterpret_cast<u32x4*>(lds + img_off);
+    const uint32_t nvec = (uint32_t)(run >> 4);
+    const uint64_t whole = total > A ? (total - A) >> 4 : 0u;
+    const uint32_t ndma = whole < nvec ? (uint32_t)whole : nvec;
+    const uint32_t lane = tid & 63u;
+    const u32x4* src = reinterpret_cast<const u32x4*>(a.frames + A);
+    for (uint32_t v0 = tid & ~63u; v0 < ndma; v0 += kBlock)
+      if (v0 + lane < ndma)
+        __builtin_amdgcn_global_load_lds(
+            (const void __attribute__((address_space(1)))*)(src + v0 + lane),
+            (void __attribute__((address_space(3)))*)(img + v0), 16, 0, 2);
+    if (ndma < nvec && tid == 0) img[ndma] = load16_guarded(a.frames, A + 16ull * ndma, total);
+    for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = (uint32_t)(a.frame_off[p0 + i] - A);
+    __syncthreads();
+    if (q < Tv) {
+      const uint32_t* dw = reinterpret_cast<const uint32_t*>(lds + img_off);
+      bad = utf8_check_frame((uint64_t)lds_fo[q] + a.H, lds_fo[q + 1], g, G,
+                             [&](uint64_t c) { return img[c]; },
+                             [&](uint64_t x) { return dw[(x >> 2) - 1u]; });  // x = 0 reads the guard
     }
   }
   for (uint32_t m = G >> 1; m > 0; m >>= 1) bad |= __shfl_xor(bad, (int)m, 64);
@@ -1008,6 +1075,23 @@ int launch_validate_utf8(const Utf8Args& args, hipStream_t stream) {
     if (lds <= 65536) {
       const uint64_t blocks = (args.n + T - 1) / T;
       hipLaunchKernelGGL(validate_utf8_tile_kernel, dim3((uint32_t)blocks), dim3(kBlock), lds, stream, a);
+      return (int)hipGetLastError();
+    }
+  }
+  if (aligned && args.frame_off && args.F >= 512u && tuning().utf8_vtile) {
+    // packed frames through LDS tiles of T = 256 / G frames, 1.1x the hinted run
+    Utf8Args a = args;
+    const uint32_t chunks = args.F / 16u + 1u;
+    uint32_t lg = 1;
+    while (lg < 4 && (4u << lg) <= chunks) ++lg;
+    a.glog = lg;
+    const uint32_t T = kBlock >> lg;
+    const uint64_t cap = (((uint64_t)T * args.F * (uint64_t)tuning().utf8_vtile_cap_pct / 100u + 256u) + 15u) & ~15ull;
+    if (cap <= 49152u) {
+      a.tile_cap = (uint32_t)cap;
+      const size_t lds = ((((T + 1u) * 4u) + 15u) & ~15u) + 16u + cap + 32u;
+      const uint64_t blocks = (args.n + T - 1) / T;
+      hipLaunchKernelGGL(validate_utf8_vtile_kernel, dim3((uint32_t)blocks), dim3(kBlock), lds, stream, a);
       return (int)hipGetLastError();
     }
   }

@@ -576,3 +576,40 @@ def test_dedup_table_heavy_repeats_and_collisions(cuda, window):
             got = host(batch.detect_retransmissions(dev(flat, cuda), frame_off=dev(off, cuda),
                                                     window=window))
         assert got.tolist() == want, table
+
+
+def test_utf8_packed_tile_vs_python_decoder(cuda):
+    """Packed frames of 0.3-3 KB (mean-length hint >= 512 B: the LDS-tile
+    validator; a low hint: every tile overflows its budget and checks its
+    frames from HBM) == per-frame vector kernel == Python's strict decoder."""
+    import ctypes
+    import torch
+    from rudp import _native
+    lib = _native.lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    lib.rudpx_tune.restype = ctypes.c_int
+    rng = np.random.default_rng(2468)
+    bodies = []
+    for b in _near_utf8(rng, 3000):
+        L = int(rng.integers(300, 3000))
+        bodies.append(((b or b"A") * (L // max(1, len(b)) + 1))[:L])
+    frames = [b"\x12\x34\x00\x00\x80" + b for b in bodies]
+    off = np.concatenate([[0], np.cumsum([len(f) for f in frames])]).astype(np.int64)
+    flat = np.frombuffer(b"".join(frames), np.uint8)
+    want = codec_np.utf8_valid(flat, off, 5)
+    assert 0.05 < want.mean() < 0.95
+    d_flat, d_off = dev(flat, cuda), dev(off, cuda)
+    out = torch.empty(len(frames), dtype=torch.uint8, device=cuda)
+    for vtile in (1, 0):
+        old = lib.rudpx_tune(41, vtile)
+        try:
+            got = host(batch.validate_utf8(d_flat, 5, frame_off=d_off))
+            assert np.array_equal(got, want), vtile
+            for hint in (512, 1600, 4000):  # 512: runs overflow the tile budget
+                out.fill_(7)
+                _native.check(lib.rudp_validate_utf8(d_flat.data_ptr(), d_off.data_ptr(), hint,
+                                                     len(frames), 5, out.data_ptr(), 0,
+                                                     torch.cuda.current_stream().cuda_stream))
+                assert np.array_equal(host(out), want), (vtile, hint)
+        finally:
+            lib.rudpx_tune(41, old)
