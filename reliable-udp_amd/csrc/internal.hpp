@@ -146,7 +146,7 @@ struct Tuning {
   int varlen_glog = -1;   // varlen lanes-per-packet log2 (0..6); -1 = from the length hint
   int varlen_tile = 1;    // varlen encode of packed payloads through LDS tiles (0: vector kernel)
   int varlen_tile_maxT = 256;     // varlen encode tile: most packets per tile
-  int varlen_tile_bytes = 24576;  // varlen encode tile: payload bytes per tile (at the hint)
+  int varlen_tile_bytes = 0;  // varlen encode tile: payload bytes per tile at the hint (0 = automatic)
   int encode_ablate = 0;  // EncodeTileArgs::ablate (sweeps only)
   int encode_stream = 0;  // register-streamed encode (no LDS tile); 0 = LDS tile kernel
   int encode_stream_T = 0;  // stream kernel packets per workgroup; 0 = automatic

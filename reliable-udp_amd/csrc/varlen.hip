@@ -1004,7 +1004,14 @@ void varlen_tile_geometry(uint32_t len_hint, uint32_t* T, uint32_t* glog, uint32
   // 0.037 vs 0.038 ms with the scan).
   if (h < 16 || h > 6144) return;
   uint32_t t = 256, lg = 0;
-  const uint32_t maxT = (uint32_t)tuning().varlen_tile_maxT, bytes = (uint32_t)tuning().varlen_tile_bytes;
+  // Payload bytes per tile at the hint: 32 KiB above 512-B hints (which only
+  // changes hints in (768, 1024]: 1M x 1024 B gets T = 32, 0.468-0.473 ->
+  // 0.429-0.431 ms; at 1472 B it still gives T = 16, and a 47 KiB tile ran
+  // 0.87 ms), 24 KiB up to 512 B (32 KiB tiles at 128-512 B measured up to
+  // 12% slower; profiles/r01/sweeps/varlen_tile_bytes.json).
+  const uint32_t maxT = (uint32_t)tuning().varlen_tile_maxT;
+  const uint32_t bytes = tuning().varlen_tile_bytes > 0 ? (uint32_t)tuning().varlen_tile_bytes
+                                                        : (h > 512u ? 32768u : 24576u);
   while (t > 4 && (t > maxT || t * h > bytes)) { t >>= 1; ++lg; }
   *T = t;
   *glog = lg;

@@ -599,7 +599,7 @@ def varlen_enc_sweep(reps):
                                   payload=flat.data_ptr(), len=lens.data_ptr(), payload_off=None)
             _native.check(lib.rudp_encode_varlen(ctypes.byref(b), fr.data_ptr(), off.data_ptr(),
                                                  None, 7, 0, stream))
-        def cfg(tile, maxT=256, nbytes=24576):
+        def cfg(tile, maxT=256, nbytes=0):  # nbytes 0: the automatic tile size
             return lambda: (lib.rudpx_tune(16, tile), lib.rudpx_tune(17, maxT), lib.rudpx_tune(18, nbytes))
         variants = {f"{name}_tile": (cfg(1), enc), f"{name}_vec": (cfg(0), enc),
                     f"{name}_tile_hipcub": (lambda: (cfg(1)(), lib.rudpx_tune(24, 0)), enc)}
