@@ -5,15 +5,16 @@
 // syn/ack/fin (:29-40) -> get_payload (:68-73), plus verification of the
 // build-defined RFC 1071 checksum.
 //
-// Fast kernel (payload_len % 16 == 0): G lanes per packet, 256/G packets per
-// workgroup.  Lane g walks the packet's payload in 16-byte windows g, g+G, ...
-// Each window starts at the odd frame offset (p*F + H + 16j); it is read as
-// two aligned dwordx4 loads (the second one is the next lane's first, an L1
-// hit) and funnel-shifted into place in registers.  Every frame byte leaves
-// HBM once.  The window's LE u16 halves feed the packet sum (shfl_xor
-// butterfly over the G lanes); with a payload_out buffer the window is also
-// written out 16-byte aligned.  The group leader parses the header from the
-// frame's first window and writes seq/ack/flags/ok (+ checksum).
+// Fast kernel (payload_len % 16 == 0, tile within 64 KiB of LDS):
+// decode_tile_kernel.  A workgroup owns T = 256/G frames (T % 16 == 0, so the
+// tile starts 16-B aligned); phase 1 streams the tile's T*F bytes into LDS as
+// one contiguous run; G lanes per frame sum its payload's LE u16 halves from
+// byte-shifted LDS windows; the leader parses the header (rudp5 sideband
+// checksums are loaded before phase 1) and the outputs go out as whole dwords
+// through LDS.  With payload_out, the tile's payloads stream out as one
+// contiguous run.  Every frame byte leaves HBM once.  Frames too large for an
+// LDS tile take decode_verify_kernel (aligned chunks, parity-weighted sums) or
+// decode_vec_kernel (register windows); any other shape the byte kernel.
 #include "codec_device.hpp"
 #include "internal.hpp"
 

@@ -6,20 +6,24 @@
 // plus the build-defined RFC 1071 checksum.
 //
 // Fast kernel (payload_len % 16 == 0): one workgroup per TILE of T packets
-// (a power of two, 4..256).  The frame stride L+H is odd, so for T < 16 a
-// tile's output range starts and ends mid-chunk; the two shared chunks are
-// written bytewise by their owners.
-//   phase 1  G = 256/T lanes per packet stream the packet's payload in 16 B
-//            vectors (coalesced dwordx4, non-temporal), sum LE u16 halves in
-//            registers, and write the vectors into an LDS tile.  The per
-//            packet sums meet in a shfl_xor butterfly over the G lanes; the
-//            group leader builds the 5/7-byte header (with checksum) in LDS.
-//   phase 2  output-stationary: each lane owns aligned 16 B output chunks,
-//            assembles them from two byte-shifted LDS windows (payload of
-//            packet q and of q+1, which sits H bytes further back) and the
-//            header words, and writes one dwordx4 non-temporal store.
+// (a power of two, 4..256; 16 at L >= 512).  The frame stride L+H is odd, so
+// for T < 16 a tile's output range starts and ends mid-chunk; the two shared
+// chunks are written bytewise by their owners.
+//   phase 1  the tile's payload is one contiguous run: it streams into an
+//            LDS tile by LDS-DMA (global_load_lds_dwordx4 nt, 1 KiB per
+//            wave-instruction; register staging behind a tuning knob).  For
+//            tiles up to 16 KiB the leaders' header-table loads go out first.
+//   sums     G = 256/T lanes per packet sum its LE u16 halves out of LDS; a
+//            shfl_xor butterfly combines them; the leader writes the 5/7-byte
+//            header word (with checksum) and, for T % 16 == 0, prebuilds the
+//            packet's 1-2 header chunks in LDS.
+//   phase 2  output-stationary: each lane owns aligned 16 B output chunks
+//            (dealt from the tile's first 64-B boundary): a pure-payload chunk
+//            is one byte-shifted LDS window, a header chunk one aligned LDS
+//            read of the prebuilt chunk (the general form assembles any chunk
+//            from two windows and the header words); one dwordx4 nt store.
 // HBM traffic = read L + 5 (payload + header table) and write L + H per
-// packet, each byte exactly once.
+// packet, each byte exactly once (PMC: 1.011x at L = 1472).
 #include "codec_device.hpp"
 #include "internal.hpp"
 

@@ -3,16 +3,18 @@
 // The reference's real traffic is 5-9 byte frames: one character of UTF-8
 // payload per datagram (utils/reliableUDP.py:11, :60).  A varlen batch is the
 // header table plus len[N] (+ optional payload_off[N]) over one payload
-// buffer.  Frame offsets are the exclusive scan of len[i] + H (hipcub), so the
-// frames come out packed back to back exactly as N calls of Packet.to_byte()
-// would be concatenated.
+// buffer.  Frame offsets are the exclusive scan of len[i] + H (scan.hip, a
+// three-pass reduce-then-scan; hipcub behind a tuning knob), so the frames
+// come out packed back to back exactly as N calls of Packet.to_byte() would
+// be concatenated.
 //
-// Encode and decode run vector kernels (16-byte aligned chunk loads, G lanes
-// per packet with G picked from the caller's mean-length hint) when both
-// buffers are 16-byte aligned, and byte-granular kernels (8 lanes per
-// packet) otherwise.  1M x 1472 B: decode 0.26-0.29 ms (0.74 of HBM peak),
-// encode 0.78 ms; 1M one-character datagrams: decode 0.015 ms, encode
-// 0.034 ms including the offset scan (tools/sweep.py --only varlen).
+// Packed payloads (the common case) encode through LDS tiles of T packets
+// (encode_varlen_tile_kernel; prebuilt header chunks and a one-window phase 2
+// when every frame of the tile is >= 32 B); hints of 512 B and up decode and
+// validate UTF-8 through LDS tiles of consecutive frames.  Otherwise vector
+// kernels (16-byte aligned chunks, G lanes per packet from the caller's
+// mean-length hint) when the buffers are 16-byte aligned, byte-granular
+// kernels (8 lanes per packet) when not.  Numbers: DESIGN.md §3.
 #include <hipcub/hipcub.hpp>
 
 #include "codec_device.hpp"
