@@ -357,7 +357,7 @@ def test_varlen_encode_kernels_vs_oracle(cuda, lo, hi, layout):
             frames = torch.empty(len(want_fr), dtype=torch.uint8, device=cuda)
             frame_off = torch.empty(n + 1, dtype=torch.int64, device=cuda)
             p = dev(packed, cuda)
-            for hint in (0, 7, 1472, 65535):
+            for hint in (0, 7, 1000, 1472, 65535):
                 frames.fill_(0xCD)
                 b = _native.RudpBatch(n=n, payload_len=hint, reserved=0, seq=tab[0].data_ptr(),
                                       ack=tab[1].data_ptr(), flags=tab[2].data_ptr(),
@@ -411,7 +411,7 @@ def test_varlen_encode_tile_kernel_vs_oracle(cuda, dist, layout):
         for tile, vhc in ((1, 0), (1, 1), (0, 0)):
             lib.rudpx_tune(16, tile)
             lib.rudpx_tune(36, vhc)  # prebuilt header chunks, fast phase 2 (tiles of frames >= 32 B)
-            for hint in (0, 1, 16, 100, 1472, 3000, 6144):
+            for hint in (0, 1, 16, 100, 800, 1024, 1472, 3000, 6144):
                 frames.fill_(0xCD)
                 csum.fill_(0)
                 b = _native.RudpBatch(n=n, payload_len=hint, reserved=0, seq=tab[0].data_ptr(),
