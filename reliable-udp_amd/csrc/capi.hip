@@ -342,6 +342,7 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
     const uint64_t cap = (((256u >> lg) * hint * pct / 100u + 256u) + 15u) & ~15ull;
     a.tile_cap = cap <= 49152u ? (uint32_t)cap : 0u;
   }
+  a.early_fo = tuning().varlen_early_fo ? 1u : 0u;
   rc = launch_decode_varlen(a, layout, (hipStream_t)hip_stream);
   if (rc) return hip_fail((hipError_t)rc, "varlen decode launch");
   return 0;
@@ -515,6 +516,7 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
   }
   a.ablate = (uint32_t)tuning().varlen_ablate;
   a.vhc = tuning().varlen_hchunk ? 1u : 0u;
+  a.early_fo = tuning().varlen_early_fo ? 1u : 0u;
   rc = launch_encode_varlen(a, layout, s);
   if (rc) return hip_fail((hipError_t)rc, "varlen encode launch");
   return 0;

@@ -98,6 +98,7 @@ struct VarlenArgs {
   uint32_t ablate;                // diagnostics only (wrong output): 1 = phase 2 without the frame walk
   uint32_t vhc;                   // tile kernel: prebuilt header chunks + pure-chunk fast phase 2
   uint32_t hc_off;                // LDS byte offset of the header-chunk array (set by the launcher)
+  uint32_t early_fo;              // tile kernels: the tile's frame offsets loaded before phase 1
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -211,6 +212,11 @@ struct Tuning {
   // per CU; tools/utf8_varlen_sweep.py, profiles/r01/sweeps/utf8_varlen_tile.json).
   int utf8_vtile = 1;
   int utf8_vtile_cap_pct = 130;      // fixed-stride UTF-8 validation through LDS tiles (0: per-frame vector kernel)
+  // Varlen tile kernels load the tile's frame offsets into registers before
+  // phase 1 (1) instead of after its payload loads (0): decode 1M x 1479 B
+  // 0.280 -> 0.265 ms, x 1031 B 0.222 -> 0.215; encode (Python entry) 1472 B
+  // 0.583 -> 0.579, 1024 B 0.433 -> 0.428 (profiles/r01/sweeps/varlen_early_fo.json).
+  int varlen_early_fo = 1;
   int encode_span = 0;
   int encode_span_bytes = 8192;  // span kernel: output bytes per workgroup (multiple of 64)
   int varlen_scan = 1;    // frame offsets: 1 = reduce-then-scan (scan.hip), 0 = hipcub

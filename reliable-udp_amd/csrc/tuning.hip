@@ -283,7 +283,8 @@ int rudpx_tune(int key, int value) {
             : key == 39 ? &t.varlen_encode_cap_pct
             : key == 40 ? &t.decode_blocks_per_cu
             : key == 41 ? &t.utf8_vtile
-            : key == 42 ? &t.utf8_vtile_cap_pct : nullptr;
+            : key == 42 ? &t.utf8_vtile_cap_pct
+            : key == 43 ? &t.varlen_early_fo : nullptr;
   if (!slot) return -22;
   const int old = *slot;
   *slot = value;

@@ -276,6 +276,13 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_tile_kernel(VarlenArgs a
 
   // ---- phase 1: payload run -> LDS, frame offsets ------------------------
   {
+    // The tile's T + 1 frame offsets (at most two per lane): issued before the
+    // payload stream so their round trip overlaps it (early_fo).
+    uint32_t fo_r0 = 0, fo_r1 = 0;
+    if (a.early_fo) {
+      if (tid <= Tv) fo_r0 = (uint32_t)(a.frame_off[p0 + tid] - fo0);
+      if (tid + kBlock <= Tv) fo_r1 = (uint32_t)(a.frame_off[p0 + tid + kBlock] - fo0);
+    }
     const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + A);
     u32x4* dst = reinterpret_cast<u32x4*>(lds_pay + kVTGuard);
     const uint32_t nvec = (uint32_t)(run >> 4);
@@ -293,7 +300,12 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_tile_kernel(VarlenArgs a
         if (v < nvec) dst[v] = r[u];
       }
     }
-    for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = (uint32_t)(a.frame_off[p0 + i] - fo0);
+    if (a.early_fo) {
+      if (tid <= Tv) lds_fo[tid] = fo_r0;
+      if (tid + kBlock <= Tv) lds_fo[tid + kBlock] = fo_r1;
+    } else {
+      for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = (uint32_t)(a.frame_off[p0 + i] - fo0);
+    }
   }
   __syncthreads();
 
@@ -614,6 +626,8 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
     return;
   }
   {
+    // T = 256 / G <= 128 frames: one offset per lane, loaded before the run (early_fo)
+    const uint32_t fo_r = a.early_fo && tid <= Tv ? (uint32_t)(a.frame_off[p0 + tid] - A) : 0u;
     const uint64_t total = a.frame_off[a.n];
     const uint32_t nvec = (uint32_t)(run >> 4);
     u32x4* dst = reinterpret_cast<u32x4*>(img);
@@ -631,7 +645,11 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
         if (v < nvec) dst[v] = r[u];
       }
     }
-    for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = (uint32_t)(a.frame_off[p0 + i] - A);
+    if (a.early_fo) {
+      if (tid <= Tv) lds_fo[tid] = fo_r;
+    } else {
+      for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = (uint32_t)(a.frame_off[p0 + i] - A);
+    }
   }
   __syncthreads();
   if (q >= Tv) return;

@@ -321,6 +321,60 @@ def vdec_sweep(reps):
     return out
 
 
+def vknob_sweep(reps, key, values):
+    """Varlen encode (Python entry: bounds check, offset scan, tile kernel) and
+    varlen decode-verify (raw ABI, preallocated outputs) with one rudpx_tune
+    knob at each of `values`; outputs checked bit-exact against the first."""
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    out = {}
+    old = lib.rudpx_tune(key, values[0])
+    lib.rudpx_tune(key, old)
+    for L in (1472, 1024, 512, 256, -1):  # -1: lengths uniform in [0, 2944]
+        n = 1 << 20
+        tab, pay = batch.synth_batch(n, max(L, 2944), 0x5EED0009, device=dev)
+        if L >= 0:
+            lens = torch.full((n,), L, dtype=torch.int32, device=dev)
+        else:
+            lens = torch.randint(0, 2945, (n,), dtype=torch.int32, device=dev)
+        flat = pay.view(-1)[: int(lens.sum().item())] if L < 0 else pay[:, :L].contiguous().view(-1)
+        del pay
+        mean = int(lens.double().mean().item()) + 7
+        ref = batch.pack_batch_varlen(tab, flat, lens, 7)
+        o16 = [torch.empty(n, dtype=torch.uint16, device=dev) for _ in range(3)]
+        o8 = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(2)]
+
+        def enc():
+            batch.pack_batch_varlen(tab, flat, lens, 7)
+
+        def dec():
+            _native.check(lib.rudp_decode(ref.frames.data_ptr(), ref.frame_off.data_ptr(), mean, n, None,
+                                          o16[0].data_ptr(), o16[1].data_ptr(), o8[0].data_ptr(),
+                                          o8[1].data_ptr(), o16[2].data_ptr(), None, 7, 0, stream))
+        name = f"L{L}" if L >= 0 else "U0-2944"
+        variants = {}
+        for v in values:
+            variants[f"{name}_enc_key{key}_{v}"] = ((lambda v=v: lib.rudpx_tune(key, v)), enc)
+            variants[f"{name}_dec_key{key}_{v}"] = ((lambda v=v: lib.rudpx_tune(key, v)), dec)
+        res = interleaved(variants, reps)
+        exact = {}
+        for v in values:
+            lib.rudpx_tune(key, v)
+            r = batch.pack_batch_varlen(tab, flat, lens, 7)
+            dec()
+            ok_all = bool((o8[1] == 1).all().item())
+            exact[v] = bool(torch.equal(r.frames, ref.frames)) and ok_all
+        lib.rudpx_tune(key, old)
+        alg_e = n * (2 * mean + 12)
+        alg_d = n * (mean + 8 + 8)
+        for k, ms in res.items():
+            alg = alg_e if "_enc_" in k else alg_d
+            out[k] = {"ms": ms, "frac": alg / ms / 1e9 / 8.0, "exact": exact[int(k.rsplit("_", 1)[1])]}
+        del ref, tab, flat, lens
+        torch.cuda.empty_cache()
+    return out
+
+
 def stream_sweep(reps):
     """Register-streamed encode (rudpx_tune 20-22) against the LDS-tile encode."""
     out = {}
@@ -659,7 +713,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--L", type=int, default=1472, help="payload length for --only ablate")
-    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "stream", "align", "knob", "copydma", "multi", "opsknob", "vdec"])
+    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "stream", "align", "knob", "copydma", "multi", "opsknob", "vdec", "vknob"])
     ap.add_argument("--blocks", type=str, default="", help="encode sweep: workgroup sizes, e.g. 256,512,1024")
     ap.add_argument("--encode-L", type=str, default="", help="encode sweep: payload lengths, e.g. 1472")
     ap.add_argument("--ablate", action="store_true", help="stream sweep: add stage ablations")
@@ -702,6 +756,8 @@ def main():
         global VDEC_CAP_PCTS
         VDEC_CAP_PCTS = (105, 125)
         result["vdec"] = vdec_sweep(args.reps)
+    if args.only == "vknob":
+        result["vknob"] = vknob_sweep(args.reps, args.key, [int(x) for x in args.values.split(",")])
     if args.only == "knob":
         pre = [tuple(int(y) for y in x.split("=")) for x in args.pre.split(",") if x]
         result["knob"] = knob_sweep(args.reps, args.key, [int(x) for x in args.values.split(",")], pre)
