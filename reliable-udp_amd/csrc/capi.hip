@@ -515,7 +515,7 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
     a.early_table = (early == 1 || (early < 0 && in->payload_len >= 128u)) ? 1u : 0u;
   }
   a.ablate = (uint32_t)tuning().varlen_ablate;
-  a.vhc = tuning().varlen_hchunk ? 1u : 0u;
+  a.vhc = (uint32_t)(tuning().varlen_hchunk < 0 ? 0 : tuning().varlen_hchunk > 2 ? 2 : tuning().varlen_hchunk);
   a.early_fo = tuning().varlen_early_fo ? 1u : 0u;
   rc = launch_encode_varlen(a, layout, s);
   if (rc) return hip_fail((hipError_t)rc, "varlen encode launch");

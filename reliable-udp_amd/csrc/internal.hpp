@@ -192,7 +192,11 @@ struct Tuning {
   // tiles whose frames are all >= 32 B: 1M x 1472 B 0.738 -> 0.631 ms, x 1024
   // B 0.562 -> 0.477, x 256 B 0.196 -> 0.169 (Python entry, one box;
   // profiles/r01/sweeps/varlen_encode_hchunk.json).
-  int varlen_hchunk = 1;
+  // 2 = the same with a coded u16 chunk map (owner frame + chunk class), so a
+  // phase-2 chunk needs no frame-offset reads: 1M x 1472 B 0.581 -> 0.569 ms,
+  // x 512 B 0.265 -> 0.256, x 256 B 0.165 -> 0.160, x 1024 B kept on the u8
+  // map by the occupancy rule (profiles/r01/sweeps/varlen_coded_map.json).
+  int varlen_hchunk = 2;
   // Varlen decode tile: LDS budget in % of the hinted run.  110 lets six
   // 1472-B tiles share a CU (125 held five): 1M x 1479 B 0.288 -> 0.277 ms,
   // lengths uniform in [0, 2944] 0.315 -> 0.306 (overflowing tiles take the

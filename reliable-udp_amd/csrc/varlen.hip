@@ -210,16 +210,19 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_vec_kernel(VarlenArgs a)
 // frame offsets u32[T + 1], the chunk -> frame map u8[], then the payload run
 // (guard, cap bytes, guard).  Shared by the launcher (LDS size) and the kernel.
 constexpr uint32_t kVTGuard = 32;
-__host__ __device__ inline uint32_t vt_map_bytes(uint32_t T, uint32_t cap, uint32_t H) {
-  return ((cap + T * H) >> 4) + 4u;
+// The map holds one u8 (owner frame) per output chunk, or with the coded map
+// (vhc == 2) one u16: owner frame in bits 0-7, bit 15 = pure payload chunk,
+// else bit 8 = header chunk of the next frame and bit 9 = its slot.
+__host__ __device__ inline uint32_t vt_map_bytes(uint32_t T, uint32_t cap, uint32_t H, uint32_t wide) {
+  return (((cap + T * H) >> 4) + 4u) << (wide ? 1 : 0);
 }
 // Frames of at least this many bytes: an aligned 16-B chunk overlaps at most
 // one header, and the 16 payload bytes before a frame's payload belong to the
 // previous frame (the varlen tile's fast phase 2).
 constexpr uint32_t kVHCMinFrame = 32;
 
-__host__ __device__ inline uint32_t vt_pay_off(uint32_t T, uint32_t cap, uint32_t H) {
-  return (8u * T + 4u * (T + 1u) + vt_map_bytes(T, cap, H) + 15u) & ~15u;
+__host__ __device__ inline uint32_t vt_pay_off(uint32_t T, uint32_t cap, uint32_t H, uint32_t wide) {
+  return (8u * T + 4u * (T + 1u) + vt_map_bytes(T, cap, H, wide) + 15u) & ~15u;
 }
 
 // Varlen encode of a PACKED payload buffer (payload_off == null) through an
@@ -248,8 +251,10 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_tile_kernel(VarlenArgs a
   const uint32_t T = a.tile_T, glog = a.tile_glog, G = 1u << glog, cap = a.tile_cap;
   uint64_t* lds_hdr = reinterpret_cast<uint64_t*>(lds);
   uint32_t* lds_fo = reinterpret_cast<uint32_t*>(lds + 8u * T);
+  const bool wide = a.vhc == 2u;  // coded chunk map (u16 entries)
   uint8_t* lds_map = reinterpret_cast<uint8_t*>(lds_fo + T + 1u);
-  unsigned char* lds_pay = lds + vt_pay_off(T, cap, H);
+  uint16_t* lds_map16 = reinterpret_cast<uint16_t*>(lds_map);
+  unsigned char* lds_pay = lds + vt_pay_off(T, cap, H, wide ? 1u : 0u);
 
   const uint32_t tid = threadIdx.x;
   const uint32_t q = tid >> glog, g = tid & (G - 1u);
@@ -332,7 +337,26 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_tile_kernel(VarlenArgs a
     // map[k] = q for the output units k whose first byte lead + 16k lies in [fs, fe)
     const uint32_t klo = fs > lead ? (fs - lead + 15u) >> 4 : 0u;
     const uint32_t khi = fe > lead ? (fe - lead + 15u) >> 4 : 0u;
-    for (uint32_t k = klo + g; k < khi; k += G) lds_map[k] = (uint8_t)q;
+    if (wide) {
+      // the chunk's class for the fast phase 2: pure payload of q, or one of
+      // the prebuilt header chunks of q (chunk starts in q's header) or q + 1
+      for (uint32_t k = klo + g; k < khi; k += G) {
+        const uint32_t x = lead + 16u * k;
+        const int k0 = (int)x - (int)fs;
+        uint32_t e = q;
+        if (k0 >= H && x + 16u <= fe) {
+          e |= 0x8000u;
+        } else {
+          const uint32_t nxt = k0 >= H ? 1u : 0u;
+          const uint32_t fsp = nxt ? fe : fs;
+          const int i0 = fsp >= lead ? (int)((fsp - lead) >> 4) : -1;
+          e |= (nxt << 8) | ((uint32_t)((int)k - i0) & 1u) << 9;
+        }
+        lds_map16[k] = (uint16_t)e;
+      }
+    } else {
+      for (uint32_t k = klo + g; k < khi; k += G) lds_map[k] = (uint8_t)q;
+    }
   }
   for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
   if (g == 0 && q < Tv) {
@@ -382,11 +406,30 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_tile_kernel(VarlenArgs a
     uint32_t x, hi_b, r;
     if (k < nfull) {
       const uint32_t i = k + npre < nfull ? k + npre : k + npre - nfull;
-      x = lead + 16u * i; hi_b = 16u; r = lds_map[i];
+      x = lead + 16u * i; hi_b = 16u;
+      if (wide) {
+        const uint32_t e = lds_map16[i];
+        if (vfast) {
+          // pure payload: one LDS window at shift + x - (r + 1) H; otherwise a
+          // prebuilt header chunk, no frame offsets needed
+          const uint32_t rr = e & 0xFFu;
+          u32x4 v;
+          if (e & 0x8000u)
+            v = window16_dw(pay_dw, shift + x - (rr + 1u) * (uint32_t)H);
+          else
+            v = reinterpret_cast<const u32x4*>(lds + a.hc_off)[2u * (rr + ((e >> 8) & 1u)) + ((e >> 9) & 1u)];
+          __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + x));
+          continue;
+        }
+        r = e & 0xFFu;
+      } else {
+        r = lds_map[i];
+      }
     } else if (k == nfull) {
       x = 0; hi_b = lead < nbytes ? lead : nbytes; r = 0;
     } else {
-      x = lead + 16u * nfull; hi_b = nbytes > x ? nbytes - x : 0u; r = hi_b ? lds_map[nfull] : 0u;
+      x = lead + 16u * nfull; hi_b = nbytes > x ? nbytes - x : 0u;
+      r = hi_b ? (wide ? (lds_map16[nfull] & 0xFFu) : lds_map[nfull]) : 0u;
     }
     if (hi_b == 0) continue;
     if (vfast && k < nfull) {
@@ -997,7 +1040,18 @@ template <int H>
 int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
   VarlenArgs args = in;
   const uint64_t blocks = (args.n + args.tile_T - 1) / args.tile_T;
-  size_t lds = vt_pay_off(args.tile_T, args.tile_cap, H) + 2u * kVTGuard + args.tile_cap;
+  const auto tile_lds = [&](uint32_t wide) {
+    size_t b = vt_pay_off(args.tile_T, args.tile_cap, H, wide) + 2u * kVTGuard + args.tile_cap;
+    if (args.vhc) b = ((b + 15u) & ~size_t(15)) + 32u * args.tile_T;
+    return b;
+  };
+  // The coded map costs 1 B more per output chunk.  Where that would leave
+  // fewer than 4 tiles per CU (1M x 1024 B: 4 -> 3, 9% slower) the u8 map is
+  // used instead; 7 -> 6 at 256 B still gains 3.4%
+  // (profiles/r01/sweeps/varlen_coded_map.json).
+  constexpr size_t kLdsPerCu = 160u * 1024u;
+  if (args.vhc == 2u && kLdsPerCu / tile_lds(1) < 4u && kLdsPerCu / tile_lds(0) >= 4u) args.vhc = 1u;
+  size_t lds = vt_pay_off(args.tile_T, args.tile_cap, H, args.vhc == 2u ? 1u : 0u) + 2u * kVTGuard + args.tile_cap;
   if (args.vhc) {  // prebuilt header chunks [T][2] x 16 B after the payload run
     lds = (lds + 15u) & ~size_t(15);
     args.hc_off = (uint32_t)lds;

@@ -343,7 +343,7 @@ def test_varlen_encode_kernels_vs_oracle(cuda, lo, hi, layout):
         big[starts[i]:starts[i] + lens[i]] = np.frombuffer(pays[i], np.uint8)
     tab = (dev(seq, cuda), dev(ack, cuda), dev(flags, cuda))
     d_lens = dev(lens, cuda)
-    for vec, vhc in ((1, 0), (1, 1), (0, 0)):
+    for vec, vhc in ((1, 0), (1, 1), (1, 2), (0, 0)):
         lib.rudpx_tune(14, vec)
         old_vhc = lib.rudpx_tune(36, vhc)  # varlen tile: prebuilt header chunks, fast phase 2
         try:
@@ -407,8 +407,9 @@ def test_varlen_encode_tile_kernel_vs_oracle(cuda, dist, layout):
     frames = torch.empty(len(want_fr), dtype=torch.uint8, device=cuda)
     frame_off = torch.empty(n + 1, dtype=torch.int64, device=cuda)
     csum = torch.empty(n, dtype=torch.uint16, device=cuda)
+    old_vhc = lib.rudpx_tune(36, 1)
     try:
-        for tile, vhc in ((1, 0), (1, 1), (0, 0)):
+        for tile, vhc in ((1, 0), (1, 1), (1, 2), (0, 0)):
             lib.rudpx_tune(16, tile)
             lib.rudpx_tune(36, vhc)  # prebuilt header chunks, fast phase 2 (tiles of frames >= 32 B)
             for hint in (0, 1, 16, 100, 800, 1024, 1472, 3000, 6144):
@@ -427,7 +428,7 @@ def test_varlen_encode_tile_kernel_vs_oracle(cuda, dist, layout):
                 assert np.array_equal(host(csum), want_cs), (dist, layout, tile, hint)
     finally:
         lib.rudpx_tune(16, 1)
-        lib.rudpx_tune(36, 0)
+        lib.rudpx_tune(36, old_vhc)
 
 
 @pytest.mark.parametrize("n", [1, 2, 255, 256, 257, 4099, 1 << 20])
