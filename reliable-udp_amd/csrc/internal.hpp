@@ -221,6 +221,10 @@ struct Tuning {
   // 0.280 -> 0.265 ms, x 1031 B 0.222 -> 0.215; encode (Python entry) 1472 B
   // 0.583 -> 0.579, 1024 B 0.433 -> 0.428 (profiles/r01/sweeps/varlen_early_fo.json).
   int varlen_early_fo = 1;
+  // Varlen encode tile: minimum waves per SIMD imposed on its register
+  // allocation (amdgpu_waves_per_eu: 6, 7, 8; 0 = none, 88 VGPRs = 5 waves;
+  // -1 = automatic from the tile's LDS occupancy, see launch_varlen_tile).
+  int varlen_waves = -1;
   int encode_span = 0;
   int encode_span_bytes = 8192;  // span kernel: output bytes per workgroup (multiple of 64)
   int varlen_scan = 1;    // frame offsets: 1 = reduce-then-scan (scan.hip), 0 = hipcub

@@ -284,7 +284,8 @@ int rudpx_tune(int key, int value) {
             : key == 40 ? &t.decode_blocks_per_cu
             : key == 41 ? &t.utf8_vtile
             : key == 42 ? &t.utf8_vtile_cap_pct
-            : key == 43 ? &t.varlen_early_fo : nullptr;
+            : key == 43 ? &t.varlen_early_fo
+            : key == 44 ? &t.varlen_waves : nullptr;
   if (!slot) return -22;
   const int old = *slot;
   *slot = value;

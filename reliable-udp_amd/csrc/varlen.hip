@@ -245,8 +245,9 @@ __host__ __device__ inline uint32_t vt_pay_off(uint32_t T, uint32_t cap, uint32_
 //            with the neighbour tiles are written bytewise.
 // A tile whose run exceeds tile_cap (lengths far above the caller's hint)
 // encodes its packets with the per-packet vector path instead.
-template <int H>
-__global__ void __launch_bounds__(kBlock) encode_varlen_tile_kernel(VarlenArgs a) {
+// W: minimum waves per SIMD the register allocation must allow (1 = none).
+template <int H, int W>
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))) encode_varlen_tile_kernel(VarlenArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const uint32_t T = a.tile_T, glog = a.tile_glog, G = 1u << glog, cap = a.tile_cap;
   uint64_t* lds_hdr = reinterpret_cast<uint64_t*>(lds);
@@ -1036,6 +1037,17 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_vtile_kernel(Utf8Args a)
   if (g == 0 && q < Tv) a.valid[p0 + q] = bad ? 0 : 1;
 }
 
+template <int H, int W>
+int launch_varlen_tile_w(const VarlenArgs& args, size_t lds, uint64_t blocks, hipStream_t stream) {
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_varlen_tile_kernel<H, W>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL((encode_varlen_tile_kernel<H, W>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
+  return (int)hipGetLastError();
+}
+
 template <int H>
 int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
   VarlenArgs args = in;
@@ -1047,8 +1059,7 @@ int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
   };
   // The coded map costs 1 B more per output chunk.  Where that would leave
   // fewer than 4 tiles per CU (1M x 1024 B: 4 -> 3, 9% slower) the u8 map is
-  // used instead; 7 -> 6 at 256 B still gains 3.4%
-  // (profiles/r01/sweeps/varlen_coded_map.json).
+  // used instead (profiles/r01/sweeps/varlen_coded_map.json).
   constexpr size_t kLdsPerCu = 160u * 1024u;
   if (args.vhc == 2u && kLdsPerCu / tile_lds(1) < 4u && kLdsPerCu / tile_lds(0) >= 4u) args.vhc = 1u;
   size_t lds = vt_pay_off(args.tile_T, args.tile_cap, H, args.vhc == 2u ? 1u : 0u) + 2u * kVTGuard + args.tile_cap;
@@ -1057,13 +1068,22 @@ int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
     args.hc_off = (uint32_t)lds;
     lds += 32u * args.tile_T;
   }
-  if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_varlen_tile_kernel<H>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
+  // Register budget to match the LDS occupancy: the kernel needs 88 VGPRs (5
+  // waves per SIMD) unconstrained, so tiles small enough for 6-7 per CU ask
+  // the allocator for that many waves (a few spills in the per-packet
+  // fallback): 1M x 512 B 0.259 -> 0.233 ms (W = 7), x 256 B 0.163 -> 0.153
+  // (W = 6).  At 5 tiles per CU and fewer it stays unconstrained: spills cost
+  // ragged batches whose tiles take the fallback (lengths uniform in
+  // [0, 2944] at W = 7: 0.80 -> 1.00 ms; profiles/r01/sweeps/varlen_waves.json).
+  int w = tuning().varlen_waves;
+  if (w < 0) {
+    const size_t per_cu = kLdsPerCu / lds;
+    w = per_cu >= 7 ? 7 : per_cu == 6 ? 6 : 1;
   }
-  hipLaunchKernelGGL(encode_varlen_tile_kernel<H>, dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
-  return (int)hipGetLastError();
+  return w == 6 ? launch_varlen_tile_w<H, 6>(args, lds, blocks, stream)
+       : w == 7 ? launch_varlen_tile_w<H, 7>(args, lds, blocks, stream)
+       : w == 8 ? launch_varlen_tile_w<H, 8>(args, lds, blocks, stream)
+                : launch_varlen_tile_w<H, 1>(args, lds, blocks, stream);
 }
 
 void varlen_tile_geometry(uint32_t len_hint, uint32_t* T, uint32_t* glog, uint32_t* cap) {
@@ -1122,6 +1142,9 @@ int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream)
     const size_t lds = ((((T + 1u) * 4u) + 15u) & ~15u) + kVTGuard + args.tile_cap + 32u;
     if (lds <= 65536) {
       const uint64_t blocks = (args.n + T - 1) / T;
+      // 76 VGPRs (6 waves per SIMD).  Asking the allocator for 7 or 8 waves
+      // spills and was slower at every size (1M x 1479 B 0.265 -> 0.306 ms;
+      // profiles/r01/sweeps/varlen_decode_waves.json).
       if (layout == 7)
         hipLaunchKernelGGL(decode_varlen_tile_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
       else
