@@ -1098,14 +1098,14 @@ void varlen_tile_geometry(uint32_t len_hint, uint32_t* T, uint32_t* glog, uint32
   // 0.037 vs 0.038 ms with the scan).
   if (h < 16 || h > 6144) return;
   uint32_t t = 256, lg = 0;
-  // Payload bytes per tile at the hint: 32 KiB above 512-B hints (which only
-  // changes hints in (768, 1024]: 1M x 1024 B gets T = 32, 0.468-0.473 ->
-  // 0.429-0.431 ms; at 1472 B it still gives T = 16, and a 47 KiB tile ran
-  // 0.87 ms), 24 KiB up to 512 B (32 KiB tiles at 128-512 B measured up to
-  // 12% slower; profiles/r01/sweeps/varlen_tile_bytes.json).
+  // Payload bytes per tile at the hint: 24 KiB.  A 32 KiB target above
+  // 512-B hints (T = 32 at 1024 B) won while the kernel was VGPR-bound at 5
+  // waves (0.47 -> 0.43 ms); with the register budget matched to LDS
+  // occupancy, T = 16 (7 tiles per CU) is faster: 1M x 1024 B 0.440 -> 0.407
+  // ms (profiles/r01/sweeps/varlen_tile_bytes_r2.json; 32 KiB tiles at
+  // 128-512 B measured up to 12% slower, varlen_tile_bytes.json).
   const uint32_t maxT = (uint32_t)tuning().varlen_tile_maxT;
-  const uint32_t bytes = tuning().varlen_tile_bytes > 0 ? (uint32_t)tuning().varlen_tile_bytes
-                                                        : (h > 512u ? 32768u : 24576u);
+  const uint32_t bytes = tuning().varlen_tile_bytes > 0 ? (uint32_t)tuning().varlen_tile_bytes : 24576u;
   while (t > 4 && (t > maxT || t * h > bytes)) { t >>= 1; ++lg; }
   *T = t;
   *glog = lg;
