@@ -338,6 +338,18 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
   // the run can stream) made it 2-7% slower (profiles/r01/sweeps/varlen_decode_tile.json).
   if (tuning().varlen_decode_tile && (len_hint >= 512u || tuning().varlen_decode_tile == 2)) {
     const uint64_t hint = len_hint ? len_hint : 16u;
+    // Tile of T = 256 / G frames sized by bytes, not by chunks per lane: the
+    // most frames (fewest lanes each, G >= 2) whose run stays within 34 KiB.
+    // Four such tiles per CU keep ~130 KiB in flight; the chunks-per-lane
+    // rule gave 16-frame tiles (8 KiB at 519 B) and the kernel's 76 VGPRs cap
+    // a CU at 6 of them: 1M x 519 B 0.158 -> 0.103 ms, x 1031 B 0.213 ->
+    // 0.207, x 1479 B unchanged (profiles/r01/sweeps/varlen_decode_lanes.json).
+    if (tuning().varlen_glog < 1 && tuning().varlen_vec) {
+      uint32_t tlg = 1;
+      while (tlg < 4 && (256u >> tlg) * hint > 34816u) ++tlg;
+      lg = tlg;
+      a.glog = lg;
+    }
     const uint64_t pct = (uint64_t)tuning().varlen_decode_cap_pct;
     const uint64_t cap = (((256u >> lg) * hint * pct / 100u + 256u) + 15u) & ~15ull;
     a.tile_cap = cap <= 49152u ? (uint32_t)cap : 0u;

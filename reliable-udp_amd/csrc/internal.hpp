@@ -225,6 +225,11 @@ struct Tuning {
   // allocation (amdgpu_waves_per_eu: 6, 7, 8; 0 = none, 88 VGPRs = 5 waves;
   // -1 = automatic from the tile's LDS occupancy, see launch_varlen_tile).
   int varlen_waves = -1;
+  // Packed-frame UTF-8 tile: the most frames per tile whose LDS budget stays
+  // within these bytes (0: lanes from chunks per lane).  A 34 KiB raw run
+  // (T = 64 at 519 B) gave 0.164 -> 0.136 ms there but 0.228 -> 0.247 at
+  // 1031 B (3 tiles per CU at the 130% budget; varlen_decode_lanes.json).
+  int utf8_vtile_bytes = 34816;
   int encode_span = 0;
   int encode_span_bytes = 8192;  // span kernel: output bytes per workgroup (multiple of 64)
   int varlen_scan = 1;    // frame offsets: 1 = reduce-then-scan (scan.hip), 0 = hipcub

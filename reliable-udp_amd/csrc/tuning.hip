@@ -285,7 +285,8 @@ int rudpx_tune(int key, int value) {
             : key == 41 ? &t.utf8_vtile
             : key == 42 ? &t.utf8_vtile_cap_pct
             : key == 43 ? &t.varlen_early_fo
-            : key == 44 ? &t.varlen_waves : nullptr;
+            : key == 44 ? &t.varlen_waves
+            : key == 45 ? &t.utf8_vtile_bytes : nullptr;
   if (!slot) return -22;
   const int old = *slot;
   *slot = value;

@@ -1187,7 +1187,12 @@ int launch_validate_utf8(const Utf8Args& args, hipStream_t stream) {
     Utf8Args a = args;
     const uint32_t chunks = args.F / 16u + 1u;
     uint32_t lg = 1;
-    while (lg < 4 && (4u << lg) <= chunks) ++lg;
+    const uint32_t run = (uint32_t)tuning().utf8_vtile_bytes;
+    if (run) {  // the most frames (G >= 2) whose LDS budget stays within `run` bytes
+      while (lg < 4 && (uint64_t)(256u >> lg) * args.F * (uint64_t)tuning().utf8_vtile_cap_pct / 100u > run) ++lg;
+    } else {    // two+ 16-byte chunks per lane
+      while (lg < 4 && (4u << lg) <= chunks) ++lg;
+    }
     a.glog = lg;
     const uint32_t T = kBlock >> lg;
     const uint64_t cap = (((uint64_t)T * args.F * (uint64_t)tuning().utf8_vtile_cap_pct / 100u + 256u) + 15u) & ~15ull;

@@ -351,11 +351,14 @@ def vknob_sweep(reps, key, values):
             _native.check(lib.rudp_decode(ref.frames.data_ptr(), ref.frame_off.data_ptr(), mean, n, None,
                                           o16[0].data_ptr(), o16[1].data_ptr(), o8[0].data_ptr(),
                                           o8[1].data_ptr(), o16[2].data_ptr(), None, 7, 0, stream))
+        def utf():
+            batch.validate_utf8(ref.frames, "rudp7", frame_off=ref.frame_off)
         name = f"L{L}" if L >= 0 else "U0-2944"
         variants = {}
         for v in values:
             variants[f"{name}_enc_key{key}_{v}"] = ((lambda v=v: lib.rudpx_tune(key, v)), enc)
             variants[f"{name}_dec_key{key}_{v}"] = ((lambda v=v: lib.rudpx_tune(key, v)), dec)
+            variants[f"{name}_utf_key{key}_{v}"] = ((lambda v=v: lib.rudpx_tune(key, v)), utf)
         res = interleaved(variants, reps)
         exact = {}
         for v in values:
@@ -363,12 +366,15 @@ def vknob_sweep(reps, key, values):
             r = batch.pack_batch_varlen(tab, flat, lens, 7)
             dec()
             ok_all = bool((o8[1] == 1).all().item())
-            exact[v] = bool(torch.equal(r.frames, ref.frames)) and ok_all
+            u = batch.validate_utf8(ref.frames, "rudp7", frame_off=ref.frame_off)
+            if v == values[0]:
+                u0 = u.clone()
+            exact[v] = bool(torch.equal(r.frames, ref.frames)) and ok_all and bool(torch.equal(u, u0))
         lib.rudpx_tune(key, old)
         alg_e = n * (2 * mean + 12)
         alg_d = n * (mean + 8 + 8)
         for k, ms in res.items():
-            alg = alg_e if "_enc_" in k else alg_d
+            alg = alg_e if "_enc_" in k else alg_d  # utf: frames + offsets read, as decode
             out[k] = {"ms": ms, "frac": alg / ms / 1e9 / 8.0, "exact": exact[int(k.rsplit("_", 1)[1])]}
         del ref, tab, flat, lens
         torch.cuda.empty_cache()
