@@ -331,12 +331,13 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
   while (lg < 4 && (4u << lg) <= chunks) ++lg;
   if (tuning().varlen_glog >= 1 && tuning().varlen_glog <= 6) lg = (uint32_t)tuning().varlen_glog;
   a.glog = tuning().varlen_vec ? lg : kNoVec;
-  // LDS tile of T = 256 / G frames: room for 1.25x the hinted run (a tile
-  // past it takes the per-frame path inside the launch).  Frames of 512 B and
-  // up only: 1M x 1031 B 0.2299 -> 0.2190 ms, x 1479 B 0.2906 -> 0.2846; at
-  // 8-263 B the tile's extra dependent round trip (its frame offsets, before
-  // the run can stream) made it 2-7% slower (profiles/r01/sweeps/varlen_decode_tile.json).
-  if (tuning().varlen_decode_tile && (len_hint >= 512u || tuning().varlen_decode_tile == 2)) {
+  // LDS tile of T = 256 / G frames: room for 1.1x the hinted run (a tile
+  // past it takes the per-frame path inside the launch).  1M x 1031 B 0.2299
+  // -> 0.2190 ms, x 1479 B 0.2906 -> 0.2846 (varlen_decode_tile.json).  Hints
+  // of 128 B and up since the tiles are sized by bytes and load their offsets
+  // early: 1M x 263 B 0.080 -> 0.056 ms, 71 B equal, 8 B 0.0164 vs 0.0175
+  // slower (profiles/r01/sweeps/varlen_decode_small.json).
+  if (tuning().varlen_decode_tile && (len_hint >= 128u || tuning().varlen_decode_tile == 2)) {
     const uint64_t hint = len_hint ? len_hint : 16u;
     // Tile of T = 256 / G frames sized by bytes, not by chunks per lane: the
     // most frames (fewest lanes each, G >= 2) whose run stays within 34 KiB.

@@ -206,10 +206,10 @@ struct Tuning {
   // 0.619 -> 0.586 ms, x 1024 B 0.468 -> 0.463, x 256 B 0.167 -> 0.164 vs
   // 125; profiles/r01/sweeps/varlen_encode_cap.json).
   int varlen_encode_cap_pct = 110;
-  int varlen_decode_tile = 1;  // varlen decode through LDS tiles for hints >= 512 B (2: any hint; 0: never)
+  int varlen_decode_tile = 1;  // varlen decode through LDS tiles for hints >= 128 B (2: any hint; 0: never)
   int dedup_table = 1;    // dedup window pass by LDS hash table (0: every frame scans its window)
   int utf8_tile = 1;
-  // Packed-frame UTF-8 validation through LDS tiles (hints >= 512 B) and its
+  // Packed-frame UTF-8 validation through LDS tiles (hints >= 128 B) and its
   // LDS budget in % of the hinted run: 1M x 1479 B ASCII frames 0.287 ->
   // 0.279 ms, lengths uniform in [0, 2944] 0.373 -> 0.370 at 130% (110%:
   // more tiles overflow to the HBM path on ragged lengths; 150%: fewer tiles

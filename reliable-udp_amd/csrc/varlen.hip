@@ -10,7 +10,7 @@
 //
 // Packed payloads (the common case) encode through LDS tiles of T packets
 // (encode_varlen_tile_kernel; prebuilt header chunks and a one-window phase 2
-// when every frame of the tile is >= 32 B); hints of 512 B and up decode and
+// when every frame of the tile is >= 32 B); hints of 128 B and up decode and
 // validate UTF-8 through LDS tiles of consecutive frames.  Otherwise vector
 // kernels (16-byte aligned chunks, G lanes per packet from the caller's
 // mean-length hint) when the buffers are 16-byte aligned, byte-granular
@@ -985,7 +985,7 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_tile_kernel(Utf8Args a) 
 }
 
 // Packed variable-length frames through an LDS tile (frames 16-B aligned;
-// hints of 512 B and up): a workgroup owns T = 256 / G consecutive frames,
+// hints of 128 B and up): a workgroup owns T = 256 / G consecutive frames,
 // one contiguous run [frame_off[p0], frame_off[p0 + T]) streamed into LDS by
 // LDS-DMA; the frames' offsets come along.  A run over tile_cap (lengths far
 // above the hint) checks its frames straight from HBM instead.
@@ -1182,7 +1182,9 @@ int launch_validate_utf8(const Utf8Args& args, hipStream_t stream) {
       return (int)hipGetLastError();
     }
   }
-  if (aligned && args.frame_off && args.F >= 512u && tuning().utf8_vtile) {
+  // Hints of 128 B and up (1M x 263 B 0.102 -> 0.079 ms with the byte-sized
+  // tiles; profiles/r01/sweeps/varlen_decode_small.json).
+  if (aligned && args.frame_off && tuning().utf8_vtile && (args.F >= 128u || tuning().utf8_vtile == 2)) {
     // packed frames through LDS tiles of T = 256 / G frames, 1.1x the hinted run
     Utf8Args a = args;
     const uint32_t chunks = args.F / 16u + 1u;
