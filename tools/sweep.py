@@ -321,13 +321,14 @@ def vdec_sweep(reps):
     return out
 
 
-def vknob_sweep(reps, key, values):
+def vknob_sweep(reps, key, values, pre=()):
     """Varlen encode (Python entry: bounds check, offset scan, tile kernel) and
     varlen decode-verify (raw ABI, preallocated outputs) with one rudpx_tune
     knob at each of `values`; outputs checked bit-exact against the first."""
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream().cuda_stream
     out = {}
+    held = [(k, lib.rudpx_tune(k, v)) for k, v in pre]  # settings held for the whole sweep
     old = lib.rudpx_tune(key, values[0])
     lib.rudpx_tune(key, old)
     for L in (1472, 1024, 512, 256, -1):  # -1: lengths uniform in [0, 2944]
@@ -378,6 +379,8 @@ def vknob_sweep(reps, key, values):
             out[k] = {"ms": ms, "frac": alg / ms / 1e9 / 8.0, "exact": exact[int(k.rsplit("_", 1)[1])]}
         del ref, tab, flat, lens
         torch.cuda.empty_cache()
+    for k, v in reversed(held):
+        lib.rudpx_tune(k, v)
     return out
 
 
@@ -763,7 +766,8 @@ def main():
         VDEC_CAP_PCTS = (105, 125)
         result["vdec"] = vdec_sweep(args.reps)
     if args.only == "vknob":
-        result["vknob"] = vknob_sweep(args.reps, args.key, [int(x) for x in args.values.split(",")])
+        pre = [tuple(int(y) for y in x.split("=")) for x in args.pre.split(",") if x]
+        result["vknob"] = vknob_sweep(args.reps, args.key, [int(x) for x in args.values.split(",")], pre)
     if args.only == "knob":
         pre = [tuple(int(y) for y in x.split("=")) for x in args.pre.split(",") if x]
         result["knob"] = knob_sweep(args.reps, args.key, [int(x) for x in args.values.split(",")], pre)
