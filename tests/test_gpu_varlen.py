@@ -292,7 +292,7 @@ def test_varlen_decode_kernels_vs_oracle(cuda, lo, hi, layout):
     d_cs = dev(cs, cuda) if layout == 5 else None
     outs = [torch.empty(n, dtype=dt, device=cuda)
             for dt in (torch.uint16, torch.uint16, torch.uint8, torch.uint8, torch.uint16)]
-    runs = [("python", None, 1, 1)] + [("abi", h, v, t) for v in (1, 0) for h in (0, 8, 64, 1472, 65535)
+    runs = [("python", None, 1, 1)] + [("abi", h, v, t) for v in (1, 0) for h in (0, 8, 64, 263, 519, 1031, 1472, 65535)
                                          for t in ((2, 0) if v else (1,))]
     for kind, hint, vec, tile in runs:
         lib.rudpx_tune(14, vec)
@@ -580,7 +580,7 @@ def test_dedup_table_heavy_repeats_and_collisions(cuda, window):
 
 
 def test_utf8_packed_tile_vs_python_decoder(cuda):
-    """Packed frames of 0.3-3 KB (mean-length hint >= 512 B: the LDS-tile
+    """Packed frames of 0.3-3 KB (mean-length hint >= 128 B: the LDS-tile
     validator; a low hint: every tile overflows its budget and checks its
     frames from HBM) == per-frame vector kernel == Python's strict decoder."""
     import ctypes
@@ -606,7 +606,7 @@ def test_utf8_packed_tile_vs_python_decoder(cuda):
         try:
             got = host(batch.validate_utf8(d_flat, 5, frame_off=d_off))
             assert np.array_equal(got, want), vtile
-            for hint in (512, 1600, 4000):  # 512: runs overflow the tile budget
+            for hint in (200, 512, 1600, 4000):  # 200/512: runs overflow the tile budget
                 out.fill_(7)
                 _native.check(lib.rudp_validate_utf8(d_flat.data_ptr(), d_off.data_ptr(), hint,
                                                      len(frames), 5, out.data_ptr(), 0,
