@@ -118,6 +118,48 @@ class Workload:
         return batch.unpack_batch(out, self.layout)
 
 
+def time_events(torch, fn, steps, warmup):
+    """Per-launch HIP-event times (ms) of `steps` calls on the current stream,
+    after `warmup` untimed calls: a start/stop event pair around every call."""
+    for i in range(warmup):
+        fn(i)
+    torch.cuda.synchronize()
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for _ in range(steps)]
+    for i, (a, b) in enumerate(ev):
+        a.record()
+        fn(warmup + i)
+        b.record()
+    torch.cuda.synchronize()
+    return [a.elapsed_time(b) for a, b in ev]
+
+
+def rank_slice(rank: int, world: int, total: int):
+    """Packets rank r frames when `total` packets are split over `world` ranks:
+    [r*total/world, (r+1)*total/world) (no exchange step)."""
+    if total % world:
+        raise ValueError("the packet count must divide evenly over the ranks")
+    n = total // world
+    return rank * n, n
+
+
+def verify_c5(w, first, n):
+    """Hash this rank's C5 frames per 2^20-packet chunk and compare them with the
+    digests utils/packet.py produced (tests/golden/digests.json).  Returns
+    (chunks checked, chunks matching), or None when the fixture is absent."""
+    path = REPO / "tests" / "golden" / "digests.json"
+    if not path.exists():
+        return None
+    cfg = json.loads(path.read_text())["C5"]
+    want = cfg["layouts"].get(str(w.H))
+    if want is None or first % cfg["chunk"] or n % cfg["chunk"] or w.L != cfg["L"]:
+        return None
+    from rudp import digest
+    got = digest.chunk_sha256(w.sets[0][2], None, cfg["chunk"])
+    k0 = first // cfg["chunk"]
+    return len(got), sum(h == want["frames"][k0 + k] for k, (h, _) in enumerate(got))
+
+
 def time_loop(torch, fn, steps, warmup):
     """HIP-event time of `steps` back-to-back calls on the current stream (ms)."""
     for i in range(warmup):
@@ -134,13 +176,14 @@ def time_loop(torch, fn, steps, warmup):
 
 
 C5_PACKETS = 1 << 24
+C5_SEED = 0x5EED0005   # tests/golden/make_golden.py CONFIGS["C5"]
 
 
 def c5_strong_leg(torch, dist, batch, device, world, rank, layout, share_device, steps=10):
     """BASELINE config 5: 16M x 1472 B packets sharded over the ranks by slicing
     (rank r frames packets [r*16M/N, (r+1)*16M/N)); whole-job payload GiB/s."""
-    n = C5_PACKETS // world
-    w = Workload(torch, batch, n, 1472, layout, rank * n, SEEDS[1472], device, min_bytes=0)
+    first, n = rank_slice(rank, world, C5_PACKETS)
+    w = Workload(torch, batch, n, 1472, layout, first, C5_SEED, device, min_bytes=0)
     for i in range(2):
         w.encode(batch, i)
     torch.cuda.synchronize()
@@ -156,9 +199,16 @@ def c5_strong_leg(torch, dist, batch, device, world, rank, layout, share_device,
                      device="cpu" if share_device else device)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall = float(t.item())
+    # every rank's frames against the reference's chunk digests (outside the clock)
+    chk = verify_c5(w, first, n)
+    ok = torch.tensor([0 if chk is None else int(chk[0] == chk[1]), 0 if chk is None else chk[1]],
+                      dtype=torch.int64, device="cpu" if share_device else device)
+    dist.all_reduce(ok, op=dist.ReduceOp.SUM)
     del w
     torch.cuda.empty_cache()
     return {"GiB_s": C5_PACKETS * 1472 * steps / wall / GIB, "ms": wall / steps * 1e3,
+            "ranks_bit_exact_vs_reference": int(ok[0].item()),
+            "chunks_matching_reference_digests": int(ok[1].item()),
             "packets_total": C5_PACKETS, "packets_per_gpu": n, "n_gpus": world, "steps": steps,
             "per_gpu_roofline_frac": n * algorithmic_bytes_encode(1472) / (wall / steps) / 1e9 / HBM_PEAK_GBS,
             "scaling": "strong"}
@@ -193,11 +243,16 @@ def legs(torch, batch, device, steps):
     # BASELINE config 5's shape on one GPU: 16M x 1472 B (23.6 GB in, 23.7 GB out)
     del w
     torch.cuda.empty_cache()
-    w16 = Workload(torch, batch, 1 << 24, 1472, "rudp7", 0, 0x5EED0005, device, min_bytes=0)
-    ms = time_loop(torch, lambda i: w16.encode(batch, i), max(3, steps // 5), 1) / max(3, steps // 5)
+    w16 = Workload(torch, batch, C5_PACKETS, 1472, "rudp7", 0, C5_SEED, device, min_bytes=0)
+    ts = sorted(time_events(torch, lambda i: w16.encode(batch, i), max(10, steps // 2), 3))
+    ms = ts[len(ts) // 2]
+    chk = verify_c5(w16, 0, C5_PACKETS)
     out["encode_16Mx1472_C5_1gpu"] = {
-        "GiB_s": (1 << 24) * 1472 / (ms / 1e3) / GIB, "ms": ms,
-        "roofline_frac": (1 << 24) * algorithmic_bytes_encode(1472) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS}
+        "GiB_s": C5_PACKETS * 1472 / (ms / 1e3) / GIB, "ms": ms,
+        "roofline_frac": C5_PACKETS * algorithmic_bytes_encode(1472) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+        "timing": f"median of {len(ts)} per-launch HIP-event pairs after 3 warmups",
+        "ms_min_max": [ts[0], ts[-1]],
+        "chunks_matching_reference_digests": None if chk is None else f"{chk[1]}/{chk[0]}"}
     del w16
     torch.cuda.empty_cache()
     w = Workload(torch, batch, 1 << 20, 1472, "rudp7", 0, SEEDS[1472], device)
@@ -413,12 +468,13 @@ def main():
             dist.init_process_group("nccl", device_id=device)
 
     n, L = args.packets, args.payload
+    first = rank * n
     if args.total_packets:
         if args.total_packets % world:
             raise SystemExit("--total-packets must divide evenly over the ranks")
-        n = args.total_packets // world
+        first, n = rank_slice(rank, world, args.total_packets)
     seed = SEEDS.get(L, 0x5EED0004)
-    w = Workload(torch, batch, n, L, args.layout, rank * n, seed, device)
+    w = Workload(torch, batch, n, L, args.layout, first, seed, device)
     for i in range(args.warmup):
         w.encode(batch, i)
     torch.cuda.synchronize()

@@ -1,0 +1,126 @@
+"""BASELINE config 5 end to end on the HIP path (16M x 1472 B, both layouts).
+
+tests/golden/digests.json holds the SHA-256 of each of the 16 chunks of 2^20
+packets of the frames utils/packet.py produced for C5 (make_golden.py, from
+utils/packet.py:80-81 `to_byte`).  Here:
+
+* one 16M-packet launch per layout is hashed chunk by chunk and every chunk
+  must equal the reference's;
+* the rank-sliced launches bench.py runs for G = 2/4/8 (rank r frames
+  [r*16M/G, (r+1)*16M/G), its inputs synthesized from the global packet index)
+  must reproduce the single launch byte for byte, on the device;
+* two and four fresh processes over gloo, sharing cuda:0, frame their slices
+  through librudp exactly as bench.py's ranks do, hash their own chunks and
+  all-gather the digests: together they must give all 16 reference digests.
+"""
+import os
+import socket
+import sys
+from pathlib import Path
+
+import pytest
+import torch.multiprocessing as mp
+
+import bench
+from rudp import batch, digest
+
+pytestmark = [pytest.mark.gpu, pytest.mark.slow]
+
+LAYOUTS = (7, 5)
+
+
+def _want(digests, layout):
+    cfg = digests["C5"]
+    assert cfg["n"] == bench.C5_PACKETS and cfg["seed"] == bench.C5_SEED and cfg["L"] == 1472
+    return cfg, cfg["layouts"][str(layout)]
+
+
+@pytest.mark.parametrize("layout", LAYOUTS)
+def test_c5_single_launch_all_chunks(cuda, digests, layout):
+    import torch
+    cfg, want = _want(digests, layout)
+    n, L = cfg["n"], cfg["L"]
+    tab, pay = batch.synth_batch(n, L, cfg["seed"], device=cuda)
+    frames, cs = batch.pack_batch(tab, pay, layout, want_csum=True)
+    torch.cuda.synchronize()
+    got = digest.chunk_sha256(frames, cs, cfg["chunk"])
+    assert len(got) == 16
+    bad = [k for k, (hf, hc) in enumerate(got) if hf != want["frames"][k] or hc != want["csum"][k]]
+    assert not bad, f"chunks differing from the reference: {bad}"
+
+    # the rank slices of bench.py's C5 leg, each its own synth + launch
+    for world in (2, 4, 8):
+        for r in range(world):
+            first, m = bench.rank_slice(r, world, n)
+            t_r, p_r = batch.synth_batch(m, L, cfg["seed"], first_index=first, device=cuda)
+            f_r, c_r = batch.pack_batch(t_r, p_r, layout, want_csum=True)
+            assert torch.equal(f_r, frames[first:first + m]), (world, r)
+            assert torch.equal(c_r.view(torch.int16), cs[first:first + m].view(torch.int16)), (world, r)
+            del t_r, p_r, f_r, c_r
+    del tab, pay, frames, cs
+    torch.cuda.empty_cache()
+
+
+def _rank_worker(rank, world, port, q):
+    """One bench.py-style rank: its own process, gloo, cuda:0, its C5 slice."""
+    repo = Path(__file__).resolve().parent.parent
+    sys.path[:0] = [str(repo), str(repo / "reliable-udp_amd")]
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    import torch
+    import torch.distributed as dist
+
+    import bench as b
+    from rudp import batch as bt
+    from rudp import digest as dg
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        torch.cuda.set_device(0)
+        dev = torch.device("cuda", 0)
+        first, n = b.rank_slice(rank, world, b.C5_PACKETS)
+        res = {}
+        for layout in LAYOUTS:
+            w = b.Workload(torch, bt, n, 1472, layout, first, b.C5_SEED, dev, min_bytes=0)
+            w.encode(bt, 0)
+            torch.cuda.synchronize()
+            res[layout] = [h for h, _ in dg.chunk_sha256(w.sets[0][2], None, 1 << 20, workers=4)]
+            del w
+            torch.cuda.empty_cache()
+        gathered = [None] * world
+        dist.all_gather_object(gathered, (first, n, res))
+        if rank == 0:
+            q.put(gathered)
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_c5_multirank_processes_match_reference(digests, world):
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_rank_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    try:
+        gathered = q.get(timeout=100)
+    finally:
+        for p in procs:
+            p.join(timeout=60)
+            if p.exitcode is None:
+                p.kill()
+    assert all(p.exitcode == 0 for p in procs)
+    chunk = digests["C5"]["chunk"]
+    for layout in LAYOUTS:
+        _, want = _want(digests, layout)
+        seen = []
+        for first, n, res in sorted(gathered, key=lambda g: g[0]):
+            assert n == bench.C5_PACKETS // world
+            for k, h in enumerate(res[layout]):
+                seen.append(first // chunk + k)
+                assert h == want["frames"][first // chunk + k], (layout, first, k)
+        assert seen == list(range(16)), seen

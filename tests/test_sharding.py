@@ -12,14 +12,21 @@ import pytest
 import torch.distributed as dist
 import torch.multiprocessing as mp
 
+import bench
 from oracle import codec_c, synth
 
 SEED, N, L = 0x5EED0005, 4096, 1472
 
 
 def shard_range(rank, world, n_total):
-    per = n_total // world
-    return rank * per, per
+    """bench.py's slicing rule (the one its ranks use for C5)."""
+    return bench.rank_slice(rank, world, n_total)
+
+
+def test_rank_slice_rule():
+    assert [bench.rank_slice(r, 8, 1 << 24) for r in (0, 7)] == [(0, 1 << 21), (7 << 21, 1 << 21)]
+    with pytest.raises(ValueError):
+        bench.rank_slice(0, 3, 1 << 24)
 
 
 @pytest.mark.parametrize("world", [1, 2, 4, 8])

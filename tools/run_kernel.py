@@ -10,6 +10,7 @@ from __future__ import annotations
 import argparse
 import json
 import math
+import time
 import sys
 from pathlib import Path
 
@@ -29,6 +30,9 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--layout", default="rudp7")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--gap-ms", type=float, default=0.0,
+                    help="idle time between launches (synchronize, then sleep): separates a "
+                         "per-launch effect from one of sustained back-to-back HBM load")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     H = batch.layout_header_len(args.layout)
@@ -83,6 +87,9 @@ def main():
     s.record()
     for i in range(args.steps):
         step(i)
+        if args.gap_ms:
+            torch.cuda.synchronize()
+            time.sleep(args.gap_ms / 1e3)
     e.record()
     e.synchronize()
     print(json.dumps({"op": args.op, "L": args.L, "n": args.n, "layout": args.layout,
