@@ -263,29 +263,45 @@ def legs(torch, batch, device, steps):
     ms = time_loop(torch, lambda i: batch.validate_utf8(fr, "rudp7"), steps, 3) / steps
     out["utf8_validate_1Mx1472"] = {"GiB_s": (1 << 20) * 1472 / (ms / 1e3) / GIB, "ms": ms}
     # reference-shaped traffic: 1M one-character datagrams (utils/reliableUDP.py:11),
-    # variable-length encode (scan + frame) and decode-verify, in packets/s
+    # variable-length encode (scan + frame) and decode-verify, in packets/s, through the
+    # Python entry points in their sync-free form (argument checks on the device, the
+    # status read once after the loop) and, beside it, with the per-call eager check
     n1 = 1 << 20
     tab1, pay1 = batch.synth_batch(n1, 1, SEEDS[1472], device=device)
     lens1 = torch.ones(n1, dtype=torch.int32, device=device)
     flat1 = pay1.view(-1)
     enc = batch.pack_batch_varlen(tab1, flat1, lens1, "rudp5", want_csum=True)
-    ms_e = time_loop(torch, lambda i: batch.pack_batch_varlen(tab1, flat1, lens1, "rudp5",
-                                                              want_csum=True), steps, 3) / steps
-    ms_d = time_loop(torch, lambda i: batch.unpack_batch_varlen(enc.frames, enc.frame_off, "rudp5",
-                                                                csum=enc.csum), steps, 3) / steps
+
+    def varlen_pair(tab, flat, lens, layout, frames, off, csum):
+        last = {}
+
+        def e(i, check=False):
+            last["e"] = batch.pack_batch_varlen(tab, flat, lens, layout, want_csum=csum is not None,
+                                                check=check)
+
+        def d(i, check=False):
+            last["d"] = batch.unpack_batch_varlen(frames, off, layout, csum=csum, check=check)
+        ms_e = time_loop(torch, e, steps, 3) / steps
+        last["e"].check()
+        ms_d = time_loop(torch, d, steps, 3) / steps
+        last["d"].check()
+        ms_e_sync = time_loop(torch, lambda i: e(i, True), steps, 3) / steps
+        ms_d_sync = time_loop(torch, lambda i: d(i, True), steps, 3) / steps
+        return ms_e, ms_d, ms_e_sync, ms_d_sync
+
+    ms_e, ms_d, ms_es, ms_ds = varlen_pair(tab1, flat1, lens1, "rudp5", enc.frames, enc.frame_off, enc.csum)
     out["varlen_1M_x_1char"] = {"encode_Mpkt_s": n1 / ms_e / 1e3, "encode_ms": ms_e,
                                 "decode_verify_Mpkt_s": n1 / ms_d / 1e3, "decode_ms": ms_d,
-                                "note": "includes the host-side bounds checks (one sync) per call"}
+                                "encode_ms_eager_check": ms_es, "decode_ms_eager_check": ms_ds,
+                                "note": "Python entry, sync-free (device-side argument checks, status "
+                                        "read after the loop); *_eager_check: one sync per call"}
     # the varlen path at MTU size: 1M x 1472 B payloads packed back to back
     # (frames at odd offsets), encode (scan + tile kernel) and decode-verify
-    # through the Python entry points, bounds checks included
     tabm, paym = batch.synth_batch(n1, 1472, SEEDS[1472], device=device)
     lensm = torch.full((n1,), 1472, dtype=torch.int32, device=device)
     flatm = paym.view(-1)
     encm = batch.pack_batch_varlen(tabm, flatm, lensm, "rudp7")
-    ms_em = time_loop(torch, lambda i: batch.pack_batch_varlen(tabm, flatm, lensm, "rudp7"), steps, 3) / steps
-    ms_dm = time_loop(torch, lambda i: batch.unpack_batch_varlen(encm.frames, encm.frame_off, "rudp7"),
-                      steps, 3) / steps
+    ms_em, ms_dm, ms_ems, ms_dms = varlen_pair(tabm, flatm, lensm, "rudp7", encm.frames, encm.frame_off, None)
     # algorithmic bytes: encode reads payload + len + table (1472 + 4 + 5), writes frame + offset
     # (1479 + 8); decode reads frame + offset, writes seq/ack/flags/ok/csum (8)
     out["varlen_1Mx1472"] = {
@@ -293,7 +309,8 @@ def legs(torch, batch, device, steps):
         "encode_roofline_frac": n1 * (1472 + 9 + 1479 + 8) / (ms_em / 1e3) / 1e9 / HBM_PEAK_GBS,
         "decode_GiB_s": n1 * 1472 / (ms_dm / 1e3) / GIB, "decode_ms": ms_dm,
         "decode_roofline_frac": n1 * (1479 + 8 + 8) / (ms_dm / 1e3) / 1e9 / HBM_PEAK_GBS,
-        "note": "Python entry incl. the bounds check (one sync) and the offset scan"}
+        "encode_ms_eager_check": ms_ems, "decode_ms_eager_check": ms_dms,
+        "note": "Python entry, sync-free (offset scan and device-side checks included)"}
     del tabm, paym, lensm, flatm, encm
     # the proxy's retransmission check (proxy.py:90, 500-deep history) over the same 1M datagrams
     ms_x = time_loop(torch, lambda i: batch.detect_retransmissions(enc.frames, frame_off=enc.frame_off,

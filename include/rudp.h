@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define RUDP_ABI_VERSION 3
+#define RUDP_ABI_VERSION 4
 
 /* Frame layouts: the value is the header length in bytes. */
 #define RUDP_LAYOUT_RUDP5 5 /* reference-exact 5-byte header, checksum sideband */
@@ -51,6 +51,16 @@ extern "C" {
 #define RUDP_OK_GOOD 1       /* checksum verified */
 #define RUDP_OK_SHORT 2      /* frame shorter than the header */
 #define RUDP_OK_UNVERIFIED 3 /* rudp5 decoded without a sideband checksum */
+
+/*
+ * Status word of the sync-free variable-length calls (*_checked): written on
+ * the device by the call itself, 0 when the batch is valid, else these bits.
+ * A call whose status is non-zero writes none of its outputs past the offsets.
+ */
+#define RUDP_ST_LEN 1u        /* a len[i] > 65535 */
+#define RUDP_ST_PAYLOAD 2u    /* packed: sum(len) != payload_bytes; gathered: payload outside the buffer */
+#define RUDP_ST_FRAMES_CAP 4u /* sum(len) + n*layout > frames_cap */
+#define RUDP_ST_OFFSETS 8u    /* frame_off decreasing, or outside [0, frames_bytes] */
 
 /* Error codes (negative errno values, HIP errors offset by -1000). */
 #define RUDP_EINVAL (-22)
@@ -130,6 +140,33 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
  */
 int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_frame_off,
                        uint16_t* d_csum_or_null, int layout, int device, void* hip_stream);
+
+/*
+ * Sync-free forms of the two variable-length calls: the argument checks of
+ * rudp_varlen_bounds / rudp_frame_off_bounds run on the device inside the call
+ * (folded into the offset scan for encode; two small launches before the
+ * decode) and land in *d_status (RUDP_ST_*), so the host never waits.  The
+ * caller reads d_status whenever it next synchronizes (the Python layer:
+ * VarlenFrames.check() / DecodedBatch.check()).
+ * rudp_encode_varlen_checked: payload_bytes = size of in->payload; frames_cap =
+ *   capacity of d_frames.  Packed payloads (payload_off NULL) must satisfy
+ *   sum(len) == payload_bytes; gathered ones payload_off[i] + len[i] <=
+ *   payload_bytes.  d_frame_off is always written (n + 1 entries).
+ * rudp_decode_varlen_checked: rudp_decode with offsets (zero-copy payload);
+ *   frame_off[0..n] must be non-decreasing and <= frames_bytes.
+ * rudp_frame_off_check: only the offset check, for callers that run their own
+ *   kernels on the frames afterwards.
+ */
+int rudp_encode_varlen_checked(const rudp_batch* in, uint64_t payload_bytes, uint8_t* d_frames,
+                               uint64_t frames_cap, uint64_t* d_frame_off, uint16_t* d_csum_or_null,
+                               uint32_t* d_status, int layout, int device, void* hip_stream);
+int rudp_decode_varlen_checked(const uint8_t* d_frames, uint64_t frames_bytes, const uint64_t* d_frame_off,
+                               uint32_t len_hint, uint64_t n, const uint16_t* d_csum_in_or_null,
+                               uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags, uint8_t* d_ok,
+                               uint16_t* d_csum_out_or_null, uint32_t* d_status, int layout, int device,
+                               void* hip_stream);
+int rudp_frame_off_check(const uint64_t* d_frame_off, uint64_t n, uint64_t frames_bytes, uint32_t* d_status,
+                         int device, void* hip_stream);
 
 /*
  * Bounds of a variable-length batch, computed on the device (argument checks

@@ -214,4 +214,43 @@ int compute_bounds(const uint32_t* len, const int64_t* off, uint64_t n, bool off
   return 0;
 }
 
+// ---- sync-free offset check -------------------------------------------------
+// frame_off[0..n] non-decreasing and inside [0, frames_bytes] (read as u64, so
+// a negative offset is out of range).  Block partials, then one block writes
+// the status word: no zero-initialisation, no host round trip.
+__global__ void __launch_bounds__(kBlock) off_check_kernel(const uint64_t* off, uint64_t n,
+                                                           uint64_t frames_bytes, uint32_t* partial) {
+  uint32_t bad = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * kBlock;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i <= n; i += stride) {
+    const uint64_t o = off[i];
+    if (o > frames_bytes || (i < n && off[i + 1] < o)) bad = 1;
+  }
+  bad = (uint32_t)__syncthreads_or((int)bad);
+  if (threadIdx.x == 0) partial[blockIdx.x] = bad;
+}
+
+__global__ void __launch_bounds__(kBlock) off_check_final_kernel(const uint32_t* partial, uint32_t nparts,
+                                                                 uint32_t* status) {
+  uint32_t bad = 0;
+  for (uint32_t i = threadIdx.x; i < nparts; i += kBlock) bad |= partial[i];
+  bad = (uint32_t)__syncthreads_or((int)bad);
+  if (threadIdx.x == 0) *status = bad ? RUDP_ST_OFFSETS : 0u;
+}
+
+int check_frame_offsets(const uint64_t* d_frame_off, uint64_t n, uint64_t frames_bytes, uint32_t* d_status,
+                        hipStream_t stream) {
+  uint64_t want = (n + 1 + kBlock * 8 - 1) / (kBlock * 8);
+  const uint32_t blocks = (uint32_t)(want < 1 ? 1 : want > kBoundsBlocks ? kBoundsBlocks : want);
+  uint32_t* partial = nullptr;
+  hipError_t e = stream_alloc(reinterpret_cast<void**>(&partial), blocks * sizeof(uint32_t), stream);
+  if (e != hipSuccess) return (int)e;
+  hipLaunchKernelGGL(off_check_kernel, dim3(blocks), dim3(kBlock), 0, stream, d_frame_off, n, frames_bytes,
+                     partial);
+  hipLaunchKernelGGL(off_check_final_kernel, dim3(1), dim3(kBlock), 0, stream, partial, blocks, d_status);
+  e = hipGetLastError();
+  hipError_t e2 = stream_free(partial, stream);
+  return (int)(e != hipSuccess ? e : e2);
+}
+
 }  // namespace rudp

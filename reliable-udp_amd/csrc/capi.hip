@@ -16,7 +16,7 @@ namespace rudp {
 int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t len_hint, uint64_t n,
                   const uint16_t* d_csum_in, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
                   uint8_t* d_ok, uint16_t* d_csum_out, uint8_t* d_payload_out, int layout,
-                  int device, void* hip_stream);
+                  int device, void* hip_stream, const uint32_t* status = nullptr);
 namespace {
 
 thread_local std::string g_last_error;
@@ -124,21 +124,12 @@ EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t*
     a.num_tiles = (uint32_t)((a.n + a.T - 1) / a.T);
     a.xcd_swizzle = tuning().encode_xcd_swizzle ? 1u : 0u;
     a.ablate = (uint32_t)tuning().encode_ablate;
-    const uint32_t V = a.L / 16u;
-    a.invV = ((1ull << 32) + V - 1ull) / V;
     const int al = tuning().out_align64;
     // Fixed-length encode deals wave stores from the first 64-B boundary at
     // every tile size (since LDS-DMA phase 1 and the header-chunk phase 2 it
     // measured equal or 0.4-1.3% faster from 64 to 1472 B;
     // profiles/r01/sweeps/align64_after_dma.json).
     a.out_align64 = al != 0 ? 1u : 0u;
-    const uint32_t S = (uint32_t)tuning().encode_span_bytes;
-    if (tuning().encode_span && a.L >= 256u && S >= 1024u && S <= 32768u && S % 64u == 0 && F < S) {
-      a.span = S;
-      a.rcpF = 1.0 / (double)F;
-      a.invF = ((1ull << 32) + F - 1ull) / F;
-      encode_span_geometry(a.L, (uint32_t)layout, S, &a.span_glog, &a.hdr_bytes);
-    }
   }
   return a;
 }
@@ -243,26 +234,39 @@ int pipeline_slots() {
 }
 
 // Drive chunks [0, n) in steps of cn through the pipeline.  The three
-// callbacks enqueue chunk work on the stream they are given.
+// callbacks enqueue chunk work on the stream they are given.  Returns only
+// after all three streams have drained, on success and on every error path:
+// earlier chunks' copies into the caller's host arrays must not outlive the
+// call (the caller may free those arrays as soon as it returns).
 template <class H2D, class KERN, class D2H>
 int run_pipeline(Pipeline* pp, uint64_t n, uint64_t cn, H2D h2d, KERN kern, D2H d2h) {
   const int S = pp->slots;
-  for (uint64_t p0 = 0, k = 0; p0 < n; p0 += cn, ++k) {
-    const uint64_t m = (n - p0) < cn ? (n - p0) : cn;
-    const int s = (int)(k % (uint64_t)S);
-    char* base = (char*)pp->dbuf[s];
-    if (k >= (uint64_t)S) RUDP_HIP(hipStreamWaitEvent(pp->h2d, pp->slot_free[s], 0));
-    int rc = h2d(base, p0, m, pp->h2d);
-    if (rc) return rc;
-    RUDP_HIP(hipEventRecord(pp->in_ready[s], pp->h2d));
-    RUDP_HIP(hipStreamWaitEvent(pp->comp, pp->in_ready[s], 0));
-    if ((rc = kern(base, p0, m, pp->comp))) return rc;
-    RUDP_HIP(hipEventRecord(pp->out_ready[s], pp->comp));
-    RUDP_HIP(hipStreamWaitEvent(pp->d2h, pp->out_ready[s], 0));
-    if ((rc = d2h(base, p0, m, pp->d2h))) return rc;
-    RUDP_HIP(hipEventRecord(pp->slot_free[s], pp->d2h));
-  }
-  RUDP_HIP(hipStreamSynchronize(pp->d2h));
+  auto enqueue = [&]() -> int {
+    for (uint64_t p0 = 0, k = 0; p0 < n; p0 += cn, ++k) {
+      const uint64_t m = (n - p0) < cn ? (n - p0) : cn;
+      const int s = (int)(k % (uint64_t)S);
+      char* base = (char*)pp->dbuf[s];
+      if (k >= (uint64_t)S) RUDP_HIP(hipStreamWaitEvent(pp->h2d, pp->slot_free[s], 0));
+      int rc = h2d(base, p0, m, pp->h2d);
+      if (rc) return rc;
+      RUDP_HIP(hipEventRecord(pp->in_ready[s], pp->h2d));
+      RUDP_HIP(hipStreamWaitEvent(pp->comp, pp->in_ready[s], 0));
+      if ((rc = kern(base, p0, m, pp->comp))) return rc;
+      RUDP_HIP(hipEventRecord(pp->out_ready[s], pp->comp));
+      RUDP_HIP(hipStreamWaitEvent(pp->d2h, pp->out_ready[s], 0));
+      if ((rc = d2h(base, p0, m, pp->d2h))) return rc;
+      RUDP_HIP(hipEventRecord(pp->slot_free[s], pp->d2h));
+    }
+    return 0;
+  };
+  const int rc = enqueue();
+  const hipError_t e1 = hipStreamSynchronize(pp->h2d);
+  const hipError_t e2 = hipStreamSynchronize(pp->comp);
+  const hipError_t e3 = hipStreamSynchronize(pp->d2h);
+  if (rc) return rc;
+  if (e1 != hipSuccess) return hip_fail(e1, "pipeline H2D stream");
+  if (e2 != hipSuccess) return hip_fail(e2, "pipeline kernel stream");
+  if (e3 != hipSuccess) return hip_fail(e3, "pipeline D2H stream");
   return 0;
 }
 
@@ -302,7 +306,7 @@ uint32_t decode_group_log2(uint32_t L) {
 int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t len_hint, uint64_t n,
                   const uint16_t* d_csum_in, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
                   uint8_t* d_ok, uint16_t* d_csum_out, uint8_t* d_payload_out, int layout,
-                  int device, void* hip_stream) {
+                  int device, void* hip_stream, const uint32_t* status) {
   if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
     return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
   if (d_payload_out)
@@ -356,6 +360,7 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
     a.tile_cap = cap <= 49152u ? (uint32_t)cap : 0u;
   }
   a.early_fo = tuning().varlen_early_fo ? 1u : 0u;
+  a.status = status;
   rc = launch_decode_varlen(a, layout, (hipStream_t)hip_stream);
   if (rc) return hip_fail((hipError_t)rc, "varlen decode launch");
   return 0;
@@ -479,8 +484,9 @@ int rudp_synth(uint64_t seed, uint64_t first_index, uint64_t n, uint32_t payload
   return 0;
 }
 
-int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_frame_off,
-                       uint16_t* d_csum_or_null, int layout, int device, void* hip_stream) {
+static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_frame_off,
+                         uint16_t* d_csum_or_null, int layout, int device, void* hip_stream,
+                         const ScanCheck& chk) {
   if (!in) return fail(RUDP_EINVAL, "rudp_encode_varlen: batch is NULL");
   if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
     return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
@@ -495,7 +501,7 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
   int rc = dev_scope.set(device);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)hip_stream;
-  rc = scan_frame_offsets(in->len, in->n, (uint32_t)layout, d_frame_off, s);
+  rc = scan_frame_offsets(in->len, in->n, (uint32_t)layout, d_frame_off, chk, s);
   if (rc) return hip_fail((hipError_t)rc, "frame offset scan");
   VarlenArgs a{};
   a.payload = in->payload;
@@ -528,10 +534,71 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
     a.early_table = (early == 1 || (early < 0 && in->payload_len >= 128u)) ? 1u : 0u;
   }
   a.ablate = (uint32_t)tuning().varlen_ablate;
-  a.vhc = (uint32_t)(tuning().varlen_hchunk < 0 ? 0 : tuning().varlen_hchunk > 2 ? 2 : tuning().varlen_hchunk);
+  {
+    const int vhc = tuning().varlen_hchunk;
+    a.vhc = (uint32_t)(vhc < 0 ? 0 : vhc > 2 ? 2 : vhc);
+  }
   a.early_fo = tuning().varlen_early_fo ? 1u : 0u;
+  a.status = chk.status;
   rc = launch_encode_varlen(a, layout, s);
   if (rc) return hip_fail((hipError_t)rc, "varlen encode launch");
+  return 0;
+}
+
+int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_frame_off,
+                       uint16_t* d_csum_or_null, int layout, int device, void* hip_stream) {
+  return encode_varlen(in, d_frames, d_frame_off, d_csum_or_null, layout, device, hip_stream, ScanCheck{});
+}
+
+int rudp_encode_varlen_checked(const rudp_batch* in, uint64_t payload_bytes, uint8_t* d_frames,
+                               uint64_t frames_cap, uint64_t* d_frame_off, uint16_t* d_csum_or_null,
+                               uint32_t* d_status, int layout, int device, void* hip_stream) {
+  if (!d_status) return fail(RUDP_EINVAL, "rudp_encode_varlen_checked: d_status is NULL");
+  if (in && in->n == 0) {
+    // nothing to launch a check from: the status is written here, on the stream
+    DeviceScope dev_scope;
+    int rc = dev_scope.set(device);
+    if (rc) return rc;
+    RUDP_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), (hipStream_t)hip_stream));
+    if (d_frame_off) RUDP_HIP(hipMemsetAsync(d_frame_off, 0, sizeof(uint64_t), (hipStream_t)hip_stream));
+    return 0;
+  }
+  ScanCheck chk{};
+  chk.payload_off = in ? in->payload_off : nullptr;
+  chk.payload_bytes = payload_bytes;
+  chk.frames_cap = frames_cap;
+  chk.status = d_status;
+  return encode_varlen(in, d_frames, d_frame_off, d_csum_or_null, layout, device, hip_stream, chk);
+}
+
+int rudp_decode_varlen_checked(const uint8_t* d_frames, uint64_t frames_bytes, const uint64_t* d_frame_off,
+                               uint32_t len_hint, uint64_t n, const uint16_t* d_csum_in_or_null,
+                               uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags, uint8_t* d_ok,
+                               uint16_t* d_csum_out_or_null, uint32_t* d_status, int layout, int device,
+                               void* hip_stream) {
+  if (!d_frame_off || !d_status) return fail(RUDP_EINVAL, "rudp_decode_varlen_checked: NULL pointer");
+  if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
+    return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
+  {
+    DeviceScope dev_scope;
+    int rc = dev_scope.set(device);
+    if (rc) return rc;
+    rc = check_frame_offsets(d_frame_off, n, frames_bytes, d_status, (hipStream_t)hip_stream);
+    if (rc) return hip_fail((hipError_t)rc, "frame offset check");
+  }
+  if (n == 0) return 0;
+  return decode_varlen(d_frames, d_frame_off, len_hint, n, d_csum_in_or_null, d_seq, d_ack, d_flags, d_ok,
+                       d_csum_out_or_null, nullptr, layout, device, hip_stream, d_status);
+}
+
+int rudp_frame_off_check(const uint64_t* d_frame_off, uint64_t n, uint64_t frames_bytes, uint32_t* d_status,
+                         int device, void* hip_stream) {
+  if (!d_frame_off || !d_status) return fail(RUDP_EINVAL, "rudp_frame_off_check: NULL pointer");
+  DeviceScope dev_scope;
+  int rc = dev_scope.set(device);
+  if (rc) return rc;
+  rc = check_frame_offsets(d_frame_off, n, frames_bytes, d_status, (hipStream_t)hip_stream);
+  if (rc) return hip_fail((hipError_t)rc, "frame offset check");
   return 0;
 }
 

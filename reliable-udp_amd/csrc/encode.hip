@@ -317,231 +317,6 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
     encode_phase2<H, NTS, BLOCK>(a, lds_pay, lds_hdr, p0, Tv, tid);
 }
 
-// floor(x / F) for x < 2^52 from a double reciprocal and one correction
-// step (an inline 64-bit integer division costs ~130 instructions per wave).
-__device__ __forceinline__ uint64_t div_by_frame(uint64_t x, uint32_t F, double rcpF) {
-  uint64_t q = (uint64_t)((double)x * rcpF);
-  const int64_t r = (int64_t)(x - q * F);
-  if (r < 0) --q;
-  else if (r >= (int64_t)F) ++q;
-  return q;
-}
-
-// Span encode (L % 16 == 0, 256 <= L <= 4096, both buffers 16-B aligned).
-// The tile kernel's workgroup owns T whole packets, ~24 KiB of payload at
-// MTU size; LDS-staged copies of that footprint top out near 5.9 TB/s while
-// ~8 KiB footprints in short-lived workgroups reach the streaming-copy rate
-// (profiles/r01/sweeps/copy_dma.json).  Here a workgroup owns a fixed span of
-// S OUTPUT bytes [b*S, (b+1)*S) instead, whatever packets it cuts:
-//   phase 1  the payload bytes behind the span (one contiguous input run:
-//            packet boundaries in the input are 16-B aligned) go to LDS by
-//            LDS-DMA.
-//   sums     G lanes per packet sum each packet's bytes inside the span.  A
-//            packet wholly inside gets its header word in LDS.  A packet
-//            crossing a span boundary ("straddler") has two partial sums, one
-//            per workgroup, stored to the boundary's two slots.
-//   phase 2  every other aligned 16-B chunk of the span, output-stationary as
-//            in the tile kernel (encode_phase2's window assembly).
-// encode_straddle_kernel (a second launch, one lane per boundary) adds the
-// two parts and writes each straddler's header chunks (the 1-2 aligned
-// chunks over its header bytes) from the header table and the 32 input bytes
-// around its payload start.  A first form finished straddlers inside the span
-// kernel (an agent-scope atomic add, the second workgroup finishing): the
-// atomic's round trip on every workgroup's critical path made it 2.2x slower.
-// Every output chunk is written once, whole, by one workgroup: no bytewise
-// boundary chunks and no sector shared between two workgroups' stores.
-template <int H>
-__global__ void __launch_bounds__(kBlock) encode_span_kernel(EncodeTileArgs a) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  uint64_t* lds_hdr = reinterpret_cast<uint64_t*>(lds);  // slot s: packet qa + s
-  unsigned char* lds_pay = lds + a.hdr_bytes;
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t L = a.L, F = L + H, S = a.span;
-  const uint64_t Z = a.n * (uint64_t)F;
-  const uint64_t b = blockIdx.x;
-  const uint64_t X0 = b * S;
-  const uint64_t X1 = (X0 + S < Z) ? X0 + S : Z;
-  const uint64_t qa = div_by_frame(X0, F, a.rcpF), qb = div_by_frame(X1 - 1, F, a.rcpF);
-  const uint32_t ra = (uint32_t)(X0 - qa * F);   // frame position of X0 in packet qa
-  const uint32_t rb = (uint32_t)(X1 - qb * F);   // bytes of frame qb before X1 (1..F)
-  const bool start_str = ra != 0;                // qa began in span b-1
-  const bool end_str = rb != F;                  // qb goes on in span b+1
-  const uint64_t in0 = qa * L + (ra > (uint32_t)H ? ra - H : 0u);
-  const uint64_t in1 = qb * L + (rb > (uint32_t)H ? rb - H : 0u);
-  const uint64_t A0 = in0 & ~15ull;
-  const uint32_t nvec = (uint32_t)((((in1 + 15) & ~15ull) - A0) >> 4);
-
-  // Header-table loads for the packets wholly inside the span go out first,
-  // so their latency overlaps the payload DMA (one round trip per workgroup).
-  const uint32_t np = (uint32_t)(qb - qa + 1);
-  const uint32_t glog = a.span_glog, G = 1u << glog;
-  const uint32_t s = tid >> glog, g = tid & (G - 1u);
-  const bool lead = g == 0 && s < np;
-  const bool first = s == 0 && start_str, last = s == np - 1 && end_str;
-  uint32_t t_seq = 0, t_ack = 0, t_flags = 0;
-  if (lead && !first && !last) {
-    t_seq = a.seq[qa + s];
-    t_ack = a.ack[qa + s];
-    t_flags = a.flags[qa + s];
-  }
-  // ---- phase 1: input run -> LDS (LDS-DMA, 1 KiB per wave-instruction) ----
-  {
-    const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + A0);
-    u32x4* dst = reinterpret_cast<u32x4*>(lds_pay + kLdsGuard);
-    for (uint32_t v0 = tid & ~63u; v0 < nvec; v0 += kBlock)
-      if (v0 + lane < nvec)
-        __builtin_amdgcn_global_load_lds(
-            (const void __attribute__((address_space(1)))*)(src + v0 + lane),
-            (void __attribute__((address_space(3)))*)(dst + v0), 16, 0, 2);
-  }
-  __syncthreads();
-
-  // ---- per-packet sums of the bytes inside the span ----------------------
-  uint32_t sum = 0;
-  if (s < np) {
-    const u32x4* img = reinterpret_cast<const u32x4*>(lds_pay + kLdsGuard);
-    const uint64_t q = qa + s;
-    const uint64_t lo = q * L > in0 ? q * L : in0;
-    const uint64_t hi = (q + 1) * L < in1 ? (q + 1) * L : in1;
-    if (hi > lo) {
-      const uint32_t blo = (uint32_t)(lo - A0), bhi = (uint32_t)(hi - A0);
-      const uint32_t c0 = blo >> 4, c1 = (bhi + 15u) >> 4;
-      for (uint32_t c = c0 + g; c < c1; c += G) {
-        u32x4 w = img[c];
-        if (c == c0 || c + 1 == c1) {  // keep bytes [blo, bhi) only
-          const int l = (int)blo - (int)(16u * c), h = (int)bhi - (int)(16u * c);
-          w = make_u32x4(lo64(w) & byte_mask(l, h), hi64(w) & byte_mask(l - 8, h - 8));
-        }
-        sum += le16_sum(w);  // input offsets and payload indices share parity (L even)
-      }
-    }
-  }
-  for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
-  if (lead) {
-    const uint64_t q = qa + s;
-    if (!first && !last) {
-      const uint32_t c = packet_csum(sum, t_seq, t_ack, t_flags);
-      lds_hdr[s] = pack_header<H>(t_seq, t_ack, t_flags, c);
-      if (a.csum) a.csum[q] = (uint16_t)c;
-    } else {
-      a.straddle[first ? 2 * b - 1 : 2 * b] = sum;
-    }
-  }
-  __syncthreads();
-
-  // ---- phase 2: the span's chunks, header chunks of straddlers excepted --
-  const uint32_t nbytes = (uint32_t)(X1 - X0);
-  const uint32_t nchunks = (nbytes + 15u) >> 4;
-  const uint64_t qaF = qa * F, qbF = qb * F;
-  const uint32_t* pay_dw = reinterpret_cast<const uint32_t*>(lds_pay);
-  const int64_t img_base = (int64_t)kLdsGuard + (int64_t)(qa * L) - (int64_t)A0;  // LDS offset of qa's payload byte 0
-  for (uint32_t k = tid; k < nchunks; k += kBlock) {
-    const uint64_t X = X0 + 16ull * k;
-    if (start_str && X + 16 > qaF && X < qaF + H) continue;
-    if (end_str && X + 16 > qbF && X < qbF + H) continue;
-    const uint32_t x = ra + 16u * k;  // offset from qa's frame start
-    const uint32_t qq = (uint32_t)(((uint64_t)x * a.invF) >> 32);  // x / F
-    const uint32_t r = x - qq * F;
-    const int kA0 = r < (uint32_t)H ? H - (int)r : 0;
-    const int kend = (int)(F - r);
-    const uint32_t sA = (uint32_t)(img_base + (int64_t)qq * L + (int64_t)r - H);
-    const u32x4 Aw = window16_dw(pay_dw, sA);
-    uint64_t lo = lo64(Aw) & byte_mask(kA0, kend);
-    uint64_t hi = hi64(Aw) & byte_mask(kA0 - 8, kend - 8);
-    if (kA0 > 0) lo |= lds_hdr[qq] >> (8 * r);
-    if (kend < 16) {
-      const u32x4 Bw = window16_dw(pay_dw, sA - H);
-      lo |= lo64(Bw) & byte_mask(kend + H, 16);
-      hi |= hi64(Bw) & byte_mask(kend + H - 8, 8);
-      const uint64_t h1 = lds_hdr[qq + 1];
-      if (kend < 8) {
-        lo |= h1 << (8 * kend);
-        if (kend > 0) hi |= h1 >> (64 - 8 * kend);
-      } else {
-        hi |= h1 << (8 * (kend - 8));
-      }
-    }
-    const u32x4 v = make_u32x4(lo, hi);
-    unsigned char* out = a.frames + X;
-    if (16u * k + 16u <= nbytes) {
-      __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out));
-    } else {  // the batch's last bytes
-      const uint32_t nb = nbytes - 16u * k;
-      const uint32_t d[4] = {v.x, v.y, v.z, v.w};
-      for (uint32_t i = 0; i < nb; ++i) out[i] = (unsigned char)(d[i >> 2] >> (8 * (i & 3)));
-    }
-  }
-}
-
-// Finishes the packets that cross span boundaries: lane b takes the boundary
-// after span b (no packet crosses it when it falls on a frame start).
-template <int H>
-__global__ void __launch_bounds__(kBlock) encode_straddle_kernel(EncodeTileArgs a, uint64_t nbound) {
-  const uint64_t b = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
-  if (b >= nbound) return;
-  const uint32_t L = a.L, F = L + H;
-  const uint64_t X = (b + 1) * (uint64_t)a.span;
-  const uint64_t q = div_by_frame(X, F, a.rcpF);
-  if (X == q * F) return;
-  const uint32_t sq = a.seq[q], k = a.ack[q], f = a.flags[q];
-  const uint32_t c = packet_csum(a.straddle[2 * b] + a.straddle[2 * b + 1], sq, k, f);
-  if (a.csum) a.csum[q] = (uint16_t)c;
-  const u32x4* in = reinterpret_cast<const u32x4*>(a.payload + q * L);
-  const u32x4 zero = {0u, 0u, 0u, 0u};
-  store_header_chunks<H>(a.frames, q * F + H, pack_header<H>(sq, k, f, c), q > 0 ? in[-1] : zero,
-                         in[0]);
-}
-
-// Span geometry: lanes per packet for the sum pass and LDS header slots.
-void encode_span_geometry(uint32_t L, uint32_t H, uint32_t S, uint32_t* glog, uint32_t* hdr_bytes) {
-  const uint32_t slots = S / (L + H) + 2u;
-  uint32_t lg = 0;
-  while (lg < 6 && (2u << lg) * slots <= (uint32_t)kBlock) ++lg;
-  *glog = lg;
-  *hdr_bytes = ((slots + 1u) * 8u + 15u) & ~15u;
-}
-
-int launch_span(const EncodeTileArgs& args, int layout, hipStream_t stream) {
-  const uint64_t Z = args.n * (uint64_t)(args.L + (uint32_t)layout);
-  const uint64_t spans = (Z + args.span - 1) / args.span;
-  const uint64_t nbound = spans - 1;
-  void* scratch = nullptr;
-  if (nbound) {
-    hipError_t e = stream_alloc(&scratch, nbound * 8, stream);
-    if (e != hipSuccess) return (int)e;
-  }
-  EncodeTileArgs a = args;
-  a.straddle = static_cast<uint32_t*>(scratch);
-  size_t lds = a.hdr_bytes + kLdsGuard + (size_t)a.span + 16 + 32;
-  int per_cu = tuning().encode_blocks_per_cu;
-  if (per_cu < 0) per_cu = 5;  // short-lived 8 KiB workgroups: 5 per CU measured best for LDS-staged copies
-  if (per_cu > 0) {
-    const size_t want = ((size_t)(160 * 1024) / (size_t)per_cu) & ~size_t(15);
-    if (want > lds) lds = want;
-  }
-  const void* fn = layout == 7 ? reinterpret_cast<const void*>(&encode_span_kernel<7>)
-                               : reinterpret_cast<const void*>(&encode_span_kernel<5>);
-  if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e != hipSuccess) return (int)e;
-  }
-  if (layout == 7)
-    hipLaunchKernelGGL(encode_span_kernel<7>, dim3((uint32_t)spans), dim3(kBlock), lds, stream, a);
-  else
-    hipLaunchKernelGGL(encode_span_kernel<5>, dim3((uint32_t)spans), dim3(kBlock), lds, stream, a);
-  hipError_t e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  if (!nbound) return 0;
-  const dim3 g2((uint32_t)((nbound + kBlock - 1) / kBlock));
-  if (layout == 7)
-    hipLaunchKernelGGL(encode_straddle_kernel<7>, g2, dim3(kBlock), 0, stream, a, nbound);
-  else
-    hipLaunchKernelGGL(encode_straddle_kernel<5>, g2, dim3(kBlock), 0, stream, a, nbound);
-  e = hipGetLastError();
-  if (e != hipSuccess) return (int)e;
-  return (int)stream_free(scratch, stream);
-}
-
 // Any payload length / alignment: one wave per packet, byte-granular.
 // Same arithmetic as the tile kernel; used for reference-sized frames
 // (1-char payloads, utils/reliableUDP.py:11) and ragged shapes.
@@ -637,168 +412,8 @@ int launch_tile_policy(const EncodeTileArgs& args, hipStream_t stream) {
 }
 
 
-// Register-streamed encode (payload_len % 16 == 0, both buffers 16-B aligned);
-// opt-in (rudpx_tune 20), bit-exact, and SLOWER than the LDS tile kernel: 1M x
-// 1472 B 0.588 ms at best (T = 4) vs 0.530 ms, and 0.558 ms even with the sums
-// and header chunks ablated, so the LDS staging is not what bounds encode
-// (profiles/r01/sweeps/stream_encode*.json).
-// No LDS tile: the payload's 16-B vectors go load -> register -> store, one
-// vector per lane per round with consecutive lanes on consecutive vectors, so
-// every wave-instruction reads and writes 1 KiB contiguous, like a copy.
-// Packet q's payload starts at output byte P = q*F + H, s = (-P) mod 16 bytes
-// before the next 16-B boundary.  Output chunk k of q's payload run (all
-// payload bytes) is bytes [s + 16k, s + 16k + 16) of the payload: vector k
-// alone when s == 0, else the tail of vector k and the head of vector k+1,
-// which the lane holding vector k+1 takes from its left neighbour by a shuffle
-// (lane 0 of a wave loads it).  What the stream leaves out is, per packet, the
-// one or two aligned chunks [floor16(P - H), ceil16(P)) holding the header:
-// after one barrier, the packet's thread builds them from the header (its
-// checksum now complete), the previous packet's last vector and its own first
-// vector (both kept in LDS by the lanes that loaded them).  Per-packet sums
-// come from a segmented shuffle reduction per round and LDS atomics.
-template <int H, int R>
-__global__ void __launch_bounds__(kBlock) encode_stream_kernel(EncodeTileArgs a) {
-  __shared__ uint32_t s_sum[kBlock];
-  __shared__ u32x4 s_head[kBlock], s_tail[kBlock];
-  const uint32_t tid = threadIdx.x, lane = tid & 63u;
-  const uint32_t T = a.T, L = a.L, V = L >> 4, F = L + H;
-  const uint64_t p0 = (uint64_t)blockIdx.x * T;
-  const uint64_t left = a.n - p0;
-  const uint32_t Tv = left < T ? (uint32_t)left : T;
-  const uint32_t nvec = Tv * V;
-  const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + p0 * (uint64_t)L);
-  unsigned char* out = a.frames;
-  for (uint32_t i = tid; i < Tv; i += kBlock) s_sum[i] = 0;
-  __syncthreads();
-  const u32x4 zero = {0u, 0u, 0u, 0u};
-  for (uint32_t v0 = 0; v0 < nvec; v0 += (uint32_t)R * kBlock) {
-    u32x4 cur[R], lft[R];
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-      const uint32_t v = v0 + (uint32_t)u * kBlock + tid;
-      cur[u] = zero;
-      lft[u] = zero;
-      if (v < nvec) {
-        cur[u] = __builtin_nontemporal_load(src + v);
-        if (lane == 0 && v > 0) lft[u] = src[v - 1];
-      }
-    }
-#pragma unroll
-    for (int u = 0; u < R; ++u) {
-      const uint32_t v = v0 + (uint32_t)u * kBlock + tid;
-      u32x4 l;
-      l.x = __shfl_up(cur[u].x, 1, 64);
-      l.y = __shfl_up(cur[u].y, 1, 64);
-      l.z = __shfl_up(cur[u].z, 1, 64);
-      l.w = __shfl_up(cur[u].w, 1, 64);
-      if (lane == 0) l = lft[u];
-      const bool valid = v < nvec;
-      const uint32_t q = valid ? (uint32_t)(((uint64_t)v * a.invV) >> 32) : 0xFFFFFFFFu;
-      uint32_t x = valid ? le16_sum(cur[u]) : 0u;
-      if (valid) {
-        const uint32_t j = v - q * V;
-        const uint64_t P = (p0 + q) * (uint64_t)F + H;
-        const uint32_t sh = (uint32_t)(-P) & 15u;
-        if (sh == 0) {
-          __builtin_nontemporal_store(cur[u], reinterpret_cast<u32x4*>(out + P + 16ull * j));
-        } else if (j > 0) {
-          __builtin_nontemporal_store(funnel32(l, cur[u], sh),
-                                      reinterpret_cast<u32x4*>(out + P + sh + 16ull * (j - 1)));
-        }
-        if (j == 0) s_head[q] = cur[u];
-        if (j == V - 1) s_tail[q] = cur[u];
-      }
-      if (a.ablate & 8u) continue;  // diagnostic: no sums
-      // segmented inclusive sum over lanes of the same packet
-      for (uint32_t d = 1; d < 64; d <<= 1) {
-        const uint32_t y = __shfl_up(x, d, 64);
-        const uint32_t qy = __shfl_up(q, d, 64);
-        if (lane >= d && qy == q) x += y;
-      }
-      const uint32_t qn = __shfl_down(q, 1, 64);
-      if (valid && (lane == 63 || qn != q)) atomicAdd(&s_sum[q], x);
-    }
-  }
-  __syncthreads();
-
-  // header chunks [floor16(P - H), ceil16(P)) of packet q = tid
-  if (tid < Tv && !(a.ablate & 16u)) {
-    const uint32_t q = tid;
-    const uint64_t p = p0 + q;
-    const uint64_t P = p * (uint64_t)F + H;
-    const uint32_t s = a.seq[p], k = a.ack[p], f = a.flags[p];
-    const uint32_t c = packet_csum(s_sum[q], s, k, f);
-    if (a.csum) a.csum[p] = (uint16_t)c;
-    const uint64_t h = pack_header<H>(s, k, f, c);
-    const u32x4 head = s_head[q];
-    const u32x4 tail = q > 0 ? s_tail[q - 1] : (p > 0 ? src[-1] : zero);
-    const uint64_t X0 = (P - H) & ~15ull, X1 = (P + 15u) & ~15ull;
-    for (uint64_t X = X0; X < X1; X += 16) {
-      const int k0 = (int)(int64_t)(X - (P - H));  // frame position of chunk byte 0 (> -16)
-      u32x4 w = zero;
-      if (k0 < 0) w = funnel32(tail, zero, (uint32_t)(k0 + 16));  // previous payload's last bytes
-      const uint32_t d = (uint32_t)(P - X);                        // payload starts d bytes in
-      if (d < 16) {
-        const u32x4 hp = funnel32(zero, head, 16u - d);
-        w.x |= hp.x; w.y |= hp.y; w.z |= hp.z; w.w |= hp.w;
-      }
-      uint64_t lo = lo64(w), hi = hi64(w);
-      if (k0 >= 0) {
-        lo |= h >> (8 * k0);
-      } else {
-        const int sh = -k0;
-        if (sh < 8) {
-          lo |= h << (8 * sh);
-          hi |= h >> (64 - 8 * sh);
-        } else {
-          hi |= h << (8 * (sh - 8));
-        }
-      }
-      __builtin_nontemporal_store(make_u32x4(lo, hi), reinterpret_cast<u32x4*>(out + X));
-    }
-    if (p == a.n - 1) {  // the batch's last bytes: a partial chunk, bytewise
-      const uint64_t E = P + L, XE = E & ~15ull;
-      const u32x4 t = s_tail[q];
-      const uint32_t dw[4] = {t.x, t.y, t.z, t.w};
-      for (uint64_t y = XE; y < E; ++y) {
-        const uint32_t b = 16u - (uint32_t)(E - y);
-        out[y] = (unsigned char)(dw[b >> 2] >> (8 * (b & 3)));
-      }
-    }
-  }
-}
-
-template <int H>
-int launch_stream(const EncodeTileArgs& args, hipStream_t stream) {
-  const uint64_t blocks = (args.n + args.T - 1) / args.T;
-  const int R = tuning().encode_stream_R;
-  if (R == 1)
-    hipLaunchKernelGGL((encode_stream_kernel<H, 1>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
-  else if (R == 4)
-    hipLaunchKernelGGL((encode_stream_kernel<H, 4>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
-  else
-    hipLaunchKernelGGL((encode_stream_kernel<H, 2>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
-  return (int)hipGetLastError();
-}
-
-// Packets per stream workgroup: about 1.5K vectors (T = 16 at 1472 B), <= 256.
-uint32_t stream_tile(uint32_t L) {
-  const int forced = tuning().encode_stream_T;
-  if (forced >= 1 && forced <= (int)kBlock) return (uint32_t)forced;
-  const uint32_t V = L / 16u;
-  uint32_t t = 1;
-  while (t * 2u <= kBlock && t * 2u * V <= 1536u) t *= 2u;
-  return t;
-}
-
 int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStream_t stream) {
   if (args.n == 0) return 0;
-  if (tile_path && tuning().encode_stream) {
-    EncodeTileArgs s = args;
-    s.T = stream_tile(args.L);
-    return layout == 7 ? launch_stream<7>(s, stream) : launch_stream<5>(s, stream);
-  }
-  if (tile_path && args.span) return launch_span(args, layout, stream);
   if (tile_path)
     return layout == 7 ? launch_tile_policy<7>(args, stream) : launch_tile_policy<5>(args, stream);
   const uint64_t blocks = (args.n + (kBlock / 64) - 1) / (kBlock / 64);

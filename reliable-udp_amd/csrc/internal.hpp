@@ -3,6 +3,10 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <atomic>
+
+#include "../../include/rudp.h"
+
 namespace rudp {
 
 struct EncodeTileArgs {
@@ -22,21 +26,12 @@ struct EncodeTileArgs {
   uint32_t num_tiles;
   uint32_t ablate;      // diagnostics only (wrong output): 1 no LDS sum pass, 2 plain phase-2
                         // LDS reads, 4 no header-table loads, 32 no header-chunk build
-  uint64_t invV;        // ceil(2^32 / (L / 16)) for exact v / V (stream kernel)
   uint32_t out_align64; // phase 2 deals full chunks from the tile's first 64-B boundary
-  // span kernel: each workgroup owns `span` output bytes (a multiple of 64);
-  // a packet crossing the boundary after span b leaves its two partial
-  // payload sums in straddle[2b] (span b's part) and straddle[2b + 1]
-  // (span b+1's), and a second launch finishes it
   uint32_t early_table;     // tile kernel: header-table loads issued before phase 1
   uint32_t hchunk;          // tile kernel (T % 16 == 0): leaders prebuild header chunks in LDS
   uint32_t hc_off;          // LDS byte offset of the header-chunk array [T + 1][2] x 16 B
   uint32_t hc_scratch;      // leaders build header chunks through a 48-B LDS scratch per packet
   uint32_t scr_off;         // LDS byte offset of that scratch [T][48 B]
-  uint32_t span;
-  uint32_t span_glog;       // log2 lanes per packet in the span sum pass
-  double rcpF;              // 1.0 / (L + H)
-  uint32_t* straddle;
 };
 
 struct DecodeArgs {
@@ -99,6 +94,10 @@ struct VarlenArgs {
   uint32_t vhc;                   // tile kernel: prebuilt header chunks + pure-chunk fast phase 2
   uint32_t hc_off;                // LDS byte offset of the header-chunk array (set by the launcher)
   uint32_t early_fo;              // tile kernels: the tile's frame offsets loaded before phase 1
+  // Sync-free entry points: the call's device status word (RUDP_ST_*), written
+  // by an earlier kernel of the same call; every kernel returns without a
+  // memory access past its own offsets when it is non-zero.  Null: unchecked.
+  const uint32_t* status;
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -111,6 +110,7 @@ struct Utf8Args {
   uint8_t* valid;
   uint32_t glog;              // log2 lanes per frame (vector kernel)
   uint32_t tile_cap;          // varlen tile kernel: LDS bytes a tile's run may use
+  const uint32_t* status;     // sync-free call: RUDP_ST_* from check_frame_offsets, or null
 };
 
 struct DedupArgs {
@@ -130,64 +130,62 @@ constexpr uint32_t kMaxPayload = 65535;
 
 enum class DecodePath { kBytes, kCopy, kCopyTile, kVerify, kVerifyTile };
 
-// Non-ABI tuning knobs (rudpx_tune in tuning.hip), read at launch.
+// Non-ABI tuning knobs (rudpx_tune in tuning.hip), read at launch.  Each
+// knob is an atomic int, so a concurrent rudpx_tune is not a data race; a
+// launch that runs while knobs change may see some old and some new values
+// (the knobs are for sweeps, not for production callers).
 struct Tuning {
-  int encode_nt_load = 1;
-  int encode_nt_store = 1;
-  int encode_tile = 0;    // packets per tile; 0 = automatic
-  int encode_p1 = 8;      // phase-1 loads in flight per lane (2, 4, 8)
-  int encode_blocks_per_cu = -1;  // cap resident tiles per CU via LDS reservation; 0 = natural, -1 = auto
-  int decode_glog = -1;   // verify kernel lanes-per-packet log2; -1 = automatic
-  int encode_xcd_swizzle = 0;  // XCD-contiguous tile order (T1)
-  int encode_contig = 1;  // phase 1 streams the tile contiguously, sums from LDS
-  int encode_block = 256;  // tile workgroup size (64, 128 when T <= block; 256, 512, 1024)
-  int decode_copy_tile = 1;  // copy-out decode through an LDS tile (0: register windows)
-  int decode_verify_tile = 1;  // verify-only decode through an LDS tile (0: aligned-chunk kernel)
-  int varlen_vec = 1;     // varlen encode/decode: vector kernels (0: byte kernels)
-  int varlen_glog = -1;   // varlen lanes-per-packet log2 (0..6); -1 = from the length hint
-  int varlen_tile = 1;    // varlen encode of packed payloads through LDS tiles (0: vector kernel)
-  int varlen_tile_maxT = 256;     // varlen encode tile: most packets per tile
-  int varlen_tile_bytes = 0;  // varlen encode tile: payload bytes per tile at the hint (0 = automatic)
-  int encode_ablate = 0;  // EncodeTileArgs::ablate (sweeps only)
-  int encode_stream = 0;  // register-streamed encode (no LDS tile); 0 = LDS tile kernel
-  int encode_stream_T = 0;  // stream kernel packets per workgroup; 0 = automatic
-  int encode_stream_R = 2;  // stream kernel rounds of loads in flight per lane (1, 2, 4)
+  std::atomic<int> encode_nt_load{1};
+  std::atomic<int> encode_nt_store{1};
+  std::atomic<int> encode_tile{0};    // packets per tile; 0 = automatic
+  std::atomic<int> encode_p1{8};      // phase-1 loads in flight per lane (2, 4, 8)
+  std::atomic<int> encode_blocks_per_cu{-1};  // cap resident tiles per CU via LDS reservation; 0 = natural, -1 = auto
+  std::atomic<int> decode_glog{-1};   // verify kernel lanes-per-packet log2; -1 = automatic
+  std::atomic<int> encode_xcd_swizzle{0};  // XCD-contiguous tile order (T1)
+  std::atomic<int> encode_contig{1};  // phase 1 streams the tile contiguously, sums from LDS
+  std::atomic<int> encode_block{256};  // tile workgroup size (64, 128 when T <= block; 256, 512, 1024)
+  std::atomic<int> decode_copy_tile{1};  // copy-out decode through an LDS tile (0: register windows)
+  std::atomic<int> decode_verify_tile{1};  // verify-only decode through an LDS tile (0: aligned-chunk kernel)
+  std::atomic<int> varlen_vec{1};     // varlen encode/decode: vector kernels (0: byte kernels)
+  std::atomic<int> varlen_glog{-1};   // varlen lanes-per-packet log2 (0..6); -1 = from the length hint
+  std::atomic<int> varlen_tile{1};    // varlen encode of packed payloads through LDS tiles (0: vector kernel)
+  std::atomic<int> varlen_tile_maxT{256};     // varlen encode tile: most packets per tile
+  std::atomic<int> varlen_tile_bytes{0};  // varlen encode tile: payload bytes per tile at the hint (0 = automatic)
+  std::atomic<int> encode_ablate{0};  // EncodeTileArgs::ablate (sweeps only)
   // Wave loads/stores of the tile kernels start on a 64-B sector boundary
   // (1) or on the first 16-B one (0).  -1 = automatic: on for fixed-length
   // encode at every tile size (1M x 1472 B: 0.516 vs 0.533 ms; smaller
   // tiles equal or up to 1.3% faster since LDS-DMA phase 1), off for decode
   // and varlen, where it measured 1-3% slower
   // (profiles/r01/sweeps/align64.json, align64_after_dma.json).
-  int out_align64 = -1;
+  std::atomic<int> out_align64{-1};
   // Encode tile phase 1 by LDS-DMA (global_load_lds_dwordx4) in place of
   // register staging (256-thread contiguous tiles, nt loads and stores):
   // 1M x 256 B 0.0967 -> 0.0946 ms, x 512 B 0.1884 -> 0.1854, x 64 B 0.0301
   // -> 0.0292; x 1024 B and x 1472 B unchanged (profiles/r01/sweeps/span_vs_tile.json).
-  int encode_dma = 1;
-  // Encode by fixed output spans (encode_span_kernel; opt-in, bit-exact, not
-  // faster at MTU size: 1M x 1472 B 0.530 vs 0.518 ms, x 1024 B 0.352 vs 0.363).
+  std::atomic<int> encode_dma{1};
   // Encode tile phase 2 with header chunks prebuilt by the packet leaders
   // (T % 16 == 0): 1M x 64 B 0.0295 -> 0.0287 ms, x 256 B 0.0962 -> 0.0938,
   // x 1024 B 0.3712 -> 0.3683, x 1472 B equal (profiles/r01/sweeps/encode_hchunk.json).
-  int encode_hchunk = 1;
+  std::atomic<int> encode_hchunk{1};
   // Encode tile header-table loads before phase 1 (1), after it (0), or -1 =
   // automatic: before for tiles of at most 16 KiB of payload (1M x 64 B
   // 0.0287 -> 0.0267 ms, x 256 B 0.0934 -> 0.0892, x 1024 B 0.3606 ->
   // 0.3557), after above (x 1472 B 0.5208 vs 0.5291 early).
-  int encode_early_table = -1;
+  std::atomic<int> encode_early_table{-1};
   // Leaders build header chunks through a 48-B LDS scratch per packet
   // (constant shifts, one window per chunk) instead of variable-shift
   // funnels: 1, 0, or -1 = automatic (tiles of at most 16 KiB: 1M x 64 B
   // 0.0272 -> 0.0266 ms, x 256 B 0.0923 -> 0.0912; x 1472 B within noise;
   // profiles/r01/sweeps/encode_hc_scratch.json).
-  int encode_hc_scratch = -1;
+  std::atomic<int> encode_hc_scratch{-1};
   // Decode tile outputs staged in LDS and written as whole dwords (output
   // pointers 4-B aligned): 1M x 256 B verify 0.0489 -> 0.0470 ms, x 64 B
   // 0.0156 -> 0.0152, x 1472 B equal; copy-out equal to +1%
   // (profiles/r01/sweeps/decode_stage_out.json).
-  int decode_stage_out = 1;
-  int decode_blocks_per_cu = -1;  // decode tile: cap resident tiles per CU (0 = natural, -1 = auto)
-  int varlen_ablate = 0;  // VarlenArgs::ablate (sweeps only)
+  std::atomic<int> decode_stage_out{1};
+  std::atomic<int> decode_blocks_per_cu{-1};  // decode tile: cap resident tiles per CU (0 = natural, -1 = auto)
+  std::atomic<int> varlen_ablate{0};  // VarlenArgs::ablate (sweeps only)
   // Varlen encode tile: prebuilt header chunks and a one-window phase 2 for
   // tiles whose frames are all >= 32 B: 1M x 1472 B 0.738 -> 0.631 ms, x 1024
   // B 0.562 -> 0.477, x 256 B 0.196 -> 0.169 (Python entry, one box;
@@ -196,51 +194,48 @@ struct Tuning {
   // phase-2 chunk needs no frame-offset reads: 1M x 1472 B 0.581 -> 0.569 ms,
   // x 512 B 0.265 -> 0.256, x 256 B 0.165 -> 0.160, x 1024 B kept on the u8
   // map by the occupancy rule (profiles/r01/sweeps/varlen_coded_map.json).
-  int varlen_hchunk = 2;
+  std::atomic<int> varlen_hchunk{2};
   // Varlen decode tile: LDS budget in % of the hinted run.  110 lets six
   // 1472-B tiles share a CU (125 held five): 1M x 1479 B 0.288 -> 0.277 ms,
   // lengths uniform in [0, 2944] 0.315 -> 0.306 (overflowing tiles take the
   // per-frame path in the launch; profiles/r01/sweeps/varlen_decode_cap.json).
-  int varlen_decode_cap_pct = 110;
+  std::atomic<int> varlen_decode_cap_pct{110};
   // Varlen encode tile: LDS budget in % of the hinted run (110: 1M x 1472 B
   // 0.619 -> 0.586 ms, x 1024 B 0.468 -> 0.463, x 256 B 0.167 -> 0.164 vs
   // 125; profiles/r01/sweeps/varlen_encode_cap.json).
-  int varlen_encode_cap_pct = 110;
-  int varlen_decode_tile = 1;  // varlen decode through LDS tiles for hints >= 128 B (2: any hint; 0: never)
-  int dedup_table = 1;    // dedup window pass by LDS hash table (0: every frame scans its window)
-  int utf8_tile = 1;
+  std::atomic<int> varlen_encode_cap_pct{110};
+  std::atomic<int> varlen_decode_tile{1};  // varlen decode through LDS tiles for hints >= 128 B (2: any hint; 0: never)
+  std::atomic<int> dedup_table{1};    // dedup window pass by LDS hash table (0: every frame scans its window)
+  std::atomic<int> utf8_tile{1};
   // Packed-frame UTF-8 validation through LDS tiles (hints >= 128 B) and its
   // LDS budget in % of the hinted run: 1M x 1479 B ASCII frames 0.287 ->
   // 0.279 ms, lengths uniform in [0, 2944] 0.373 -> 0.370 at 130% (110%:
   // more tiles overflow to the HBM path on ragged lengths; 150%: fewer tiles
   // per CU; tools/utf8_varlen_sweep.py, profiles/r01/sweeps/utf8_varlen_tile.json).
-  int utf8_vtile = 1;
-  int utf8_vtile_cap_pct = 130;      // fixed-stride UTF-8 validation through LDS tiles (0: per-frame vector kernel)
+  std::atomic<int> utf8_vtile{1};
+  std::atomic<int> utf8_vtile_cap_pct{130};      // fixed-stride UTF-8 validation through LDS tiles (0: per-frame vector kernel)
   // Varlen tile kernels load the tile's frame offsets into registers before
   // phase 1 (1) instead of after its payload loads (0): decode 1M x 1479 B
   // 0.280 -> 0.265 ms, x 1031 B 0.222 -> 0.215; encode (Python entry) 1472 B
   // 0.583 -> 0.579, 1024 B 0.433 -> 0.428 (profiles/r01/sweeps/varlen_early_fo.json).
-  int varlen_early_fo = 1;
+  std::atomic<int> varlen_early_fo{1};
   // Varlen encode tile: minimum waves per SIMD imposed on its register
   // allocation (amdgpu_waves_per_eu: 6, 7, 8; 0 = none, 88 VGPRs = 5 waves;
   // -1 = automatic from the tile's LDS occupancy, see launch_varlen_tile).
-  int varlen_waves = -1;
+  std::atomic<int> varlen_waves{-1};
   // Packed-frame UTF-8 tile: the most frames per tile whose LDS budget stays
   // within these bytes (0: lanes from chunks per lane).  A 34 KiB raw run
   // (T = 64 at 519 B) gave 0.164 -> 0.136 ms there but 0.228 -> 0.247 at
   // 1031 B (3 tiles per CU at the 130% budget; varlen_decode_lanes.json).
-  int utf8_vtile_bytes = 34816;
-  int encode_span = 0;
-  int encode_span_bytes = 8192;  // span kernel: output bytes per workgroup (multiple of 64)
-  int varlen_scan = 1;    // frame offsets: 1 = reduce-then-scan (scan.hip), 0 = hipcub
-  int host_slots = 3;     // *_host pipeline: device staging slots (2..8)
-  int host_stage_mb = 128;  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
+  std::atomic<int> utf8_vtile_bytes{34816};
+  std::atomic<int> varlen_scan{1};    // frame offsets: 1 = reduce-then-scan (scan.hip), 0 = hipcub
+  std::atomic<int> host_slots{3};     // *_host pipeline: device staging slots (2..8)
+  std::atomic<int> host_stage_mb{128};  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
 };
 Tuning& tuning();
 
 // Tile geometry for a fast-path payload length (L % 16 == 0, 16 <= L <= 4096).
 void encode_tile_geometry(uint32_t L, uint32_t* T, uint32_t* glog);
-void encode_span_geometry(uint32_t L, uint32_t H, uint32_t S, uint32_t* glog, uint32_t* hdr_bytes);
 uint32_t decode_group_log2(uint32_t L);
 
 int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStream_t stream);
@@ -266,9 +261,21 @@ struct Bounds {
 // `stream`, copied to *host; synchronous (bounds.hip).
 int compute_bounds(const uint32_t* len, const int64_t* off, uint64_t n, bool offsets_only,
                    Bounds* host, hipStream_t stream);
+// Device-side validation folded into the offset scan (sync-free varlen
+// encode).  status == null: no checks.
+struct ScanCheck {
+  const uint64_t* payload_off;  // gathered payloads, or null (packed)
+  uint64_t payload_bytes;       // size of the payload buffer
+  uint64_t frames_cap;          // capacity of the frame buffer
+  uint32_t* status;             // written once: RUDP_ST_* bits, 0 = valid
+};
 int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
-                             hipStream_t stream);
+                             const ScanCheck& chk, hipStream_t stream);
 int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
-                       hipStream_t stream);
+                       const ScanCheck& chk, hipStream_t stream);
+// frame_off[0..n] non-decreasing and inside [0, frames_bytes]: writes
+// *d_status = 0 or RUDP_ST_OFFSETS, asynchronously (bounds.hip).
+int check_frame_offsets(const uint64_t* d_frame_off, uint64_t n, uint64_t frames_bytes, uint32_t* d_status,
+                        hipStream_t stream);
 
 }  // namespace rudp

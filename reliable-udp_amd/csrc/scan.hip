@@ -10,6 +10,12 @@
 //      frame_off[] with coalesced stores.
 // Replaces hipcub::DeviceScan (17 us for 1M lengths including its state
 // init; this form: see DESIGN.md §3 varlen).
+//
+// With a ScanCheck the same passes validate the batch on the device (the
+// sync-free entry points): pass 1 flags lengths over 65535 and gathered
+// payloads outside the payload buffer in the top bits of its block sum, pass 2
+// checks the packed payload size and the frame buffer's capacity against the
+// total and writes the status word every later kernel of the call reads.
 #include "codec_device.hpp"
 #include "internal.hpp"
 
@@ -18,23 +24,45 @@ namespace rudp {
 constexpr uint32_t kScanItems = 8;                     // per thread
 constexpr uint32_t kScanBlockItems = kBlock * kScanItems;  // 2048 per block
 
+// Status bits of a block live above bit 56 of its block sum (a sum of at
+// most 2048 x (2^32 - 1 + 7) fits in 44 bits).
+constexpr int kSumBitsShift = 56;
+constexpr uint64_t kSumMask = (1ull << kSumBitsShift) - 1ull;
+
 __global__ void __launch_bounds__(kBlock) scan_block_sums_kernel(const uint32_t* len, uint64_t n,
-                                                                 uint32_t H, uint64_t* sums) {
+                                                                 uint32_t H, uint64_t* sums,
+                                                                 ScanCheck chk) {
   __shared__ uint64_t s_wave[kBlock / 64];
+  __shared__ uint32_t s_bits;
+  if (threadIdx.x == 0) s_bits = 0;
   const uint64_t base = (uint64_t)blockIdx.x * kScanBlockItems;
   uint64_t acc = 0;
+  uint32_t bits = 0;
 #pragma unroll
   for (uint32_t j = 0; j < kScanItems; ++j) {
     const uint64_t i = base + j * kBlock + threadIdx.x;
-    if (i < n) acc += (uint64_t)len[i] + H;
+    if (i < n) {
+      const uint32_t l = len[i];
+      acc += (uint64_t)l + H;
+      if (chk.status) {
+        if (l > kMaxPayload) bits |= RUDP_ST_LEN;
+        if (chk.payload_off) {
+          const uint64_t o = chk.payload_off[i];
+          // o + l <= payload_bytes without overflow (o is read as u64: a negative int64 is huge)
+          if (o > chk.payload_bytes || (uint64_t)l > chk.payload_bytes - o) bits |= RUDP_ST_PAYLOAD;
+        }
+      }
+    }
   }
   for (int m = 32; m > 0; m >>= 1) acc += __shfl_xor(acc, m, 64);
+  __syncthreads();  // s_bits initialised
+  if (bits) atomicOr(&s_bits, bits);
   if ((threadIdx.x & 63u) == 0) s_wave[threadIdx.x >> 6] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t t = 0;
     for (uint32_t w = 0; w < kBlock / 64; ++w) t += s_wave[w];
-    sums[blockIdx.x] = t;
+    sums[blockIdx.x] = t | ((uint64_t)s_bits << kSumBitsShift);
   }
 }
 
@@ -59,22 +87,41 @@ __device__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* total, uint64_t* 
   return before + incl - x;
 }
 
-// One workgroup of 1024 threads: sums[b] <- sum_{c<b} sums[c]; frame_off[n] <- total.
+// One workgroup of 1024 threads: sums[b] <- sum_{c<b} sums[c]; frame_off[n] <- total;
+// with a ScanCheck, the call's status word.
 __global__ void __launch_bounds__(1024) scan_block_bases_kernel(uint64_t* sums, uint64_t nb,
-                                                               uint64_t* frame_off, uint64_t n) {
+                                                               uint64_t* frame_off, uint64_t n,
+                                                               uint32_t H, ScanCheck chk) {
   __shared__ uint64_t s_wave[1024 / 64];
+  __shared__ uint32_t s_bits;
+  if (threadIdx.x == 0) s_bits = 0;
   const uint64_t per = (nb + 1023) / 1024;
   const uint64_t lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
   uint64_t mine = 0;
-  for (uint64_t i = lo; i < hi; ++i) mine += sums[i];
-  uint64_t total = 0;
-  uint64_t run = block_exclusive_scan(mine, &total, s_wave);
+  uint32_t bits = 0;
   for (uint64_t i = lo; i < hi; ++i) {
     const uint64_t v = sums[i];
+    mine += v & kSumMask;
+    bits |= (uint32_t)(v >> kSumBitsShift);
+  }
+  uint64_t total = 0;
+  uint64_t run = block_exclusive_scan(mine, &total, s_wave);  // (its barriers order s_bits)
+  if (bits) atomicOr(&s_bits, bits);
+  for (uint64_t i = lo; i < hi; ++i) {
+    const uint64_t v = sums[i] & kSumMask;
     sums[i] = run;
     run += v;
   }
-  if (threadIdx.x == 0) frame_off[n] = total;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    frame_off[n] = total;
+    if (chk.status) {
+      uint32_t st = s_bits;
+      if (!chk.payload_off && total - n * (uint64_t)H != chk.payload_bytes) st |= RUDP_ST_PAYLOAD;
+      if (total > chk.frames_cap) st |= RUDP_ST_FRAMES_CAP;
+      *chk.status = st;
+    }
+  }
 }
 
 __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len, uint64_t n, uint32_t H,
@@ -110,13 +157,15 @@ __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len,
 }
 
 int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
-                             hipStream_t stream) {
+                             const ScanCheck& chk, hipStream_t stream) {
   const uint64_t nb = (n + kScanBlockItems - 1) / kScanBlockItems;
   uint64_t* sums = nullptr;
   hipError_t e = stream_alloc(reinterpret_cast<void**>(&sums), nb * sizeof(uint64_t), stream);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(scan_block_sums_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, stream, d_len, n, H, sums);
-  hipLaunchKernelGGL(scan_block_bases_kernel, dim3(1), dim3(1024), 0, stream, sums, nb, d_frame_off, n);
+  hipLaunchKernelGGL(scan_block_sums_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, stream, d_len, n, H, sums,
+                     chk);
+  hipLaunchKernelGGL(scan_block_bases_kernel, dim3(1), dim3(1024), 0, stream, sums, nb, d_frame_off, n, H,
+                     chk);
   hipLaunchKernelGGL(scan_apply_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, stream, d_len, n, H, sums,
                      d_frame_off);
   e = hipGetLastError();

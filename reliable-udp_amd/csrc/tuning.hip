@@ -259,7 +259,7 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
-  int* slot = key == 0 ? &t.encode_nt_load : key == 1 ? &t.encode_nt_store
+  std::atomic<int>* slot = key == 0 ? &t.encode_nt_load : key == 1 ? &t.encode_nt_store
             : key == 2 ? &t.encode_tile : key == 3 ? &t.encode_p1
             : key == 4 ? &t.decode_glog : key == 5 ? &t.encode_xcd_swizzle
             : key == 6 ? &t.encode_blocks_per_cu : key == 7 ? &t.encode_contig
@@ -267,9 +267,7 @@ int rudpx_tune(int key, int value) {
             : key == 10 ? &t.encode_block : key == 11 ? &t.decode_copy_tile
             : key == 12 ? &t.decode_verify_tile : key == 13 ? &t.encode_ablate : key == 14 ? &t.varlen_vec : key == 15 ? &t.varlen_glog
             : key == 16 ? &t.varlen_tile : key == 17 ? &t.varlen_tile_maxT
-            : key == 18 ? &t.varlen_tile_bytes : key == 20 ? &t.encode_stream
-            : key == 21 ? &t.encode_stream_T : key == 22 ? &t.encode_stream_R : key == 23 ? &t.out_align64 : key == 24 ? &t.varlen_scan : key == 25 ? &t.encode_dma
-            : key == 26 ? &t.encode_span : key == 27 ? &t.encode_span_bytes
+            : key == 18 ? &t.varlen_tile_bytes : key == 23 ? &t.out_align64 : key == 24 ? &t.varlen_scan : key == 25 ? &t.encode_dma
             : key == 29 ? &t.encode_hchunk
             : key == 30 ? &t.encode_early_table
             : key == 31 ? &t.utf8_tile
@@ -288,9 +286,7 @@ int rudpx_tune(int key, int value) {
             : key == 44 ? &t.varlen_waves
             : key == 45 ? &t.utf8_vtile_bytes : nullptr;
   if (!slot) return -22;
-  const int old = *slot;
-  *slot = value;
-  return old;
+  return slot->exchange(value);
 }
 
 // Copy n16 16-byte vectors (both pointers 16-byte aligned) with `blocks` workgroups.

@@ -24,6 +24,10 @@ namespace rudp {
 
 constexpr uint32_t kVarLanes = 8;
 
+// Sync-free calls: an earlier kernel of the call found the batch invalid.
+// Uniform (a kernel argument), so this is one scalar load per wave.
+__device__ __forceinline__ bool call_failed(const uint32_t* status) { return status && *status; }
+
 struct FrameLen {
   const uint32_t* len;
   uint32_t H;
@@ -32,6 +36,7 @@ struct FrameLen {
 
 template <int H>
 __global__ void __launch_bounds__(kBlock) encode_varlen_kernel(VarlenArgs a) {
+  if (call_failed(a.status)) return;
   const uint32_t g = threadIdx.x & (kVarLanes - 1u);
   const uint64_t p = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / kVarLanes;
   const bool valid = p < a.n;
@@ -200,6 +205,7 @@ __device__ __forceinline__ void encode_varlen_packet(const VarlenArgs& a, uint64
 
 template <int H>
 __global__ void __launch_bounds__(kBlock) encode_varlen_vec_kernel(VarlenArgs a) {
+  if (call_failed(a.status)) return;
   const uint32_t tid = threadIdx.x;
   const uint32_t glog = a.glog;
   const uint64_t p = (uint64_t)blockIdx.x * (kBlock >> glog) + (tid >> glog);
@@ -271,6 +277,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     t_flags = a.flags_in[p0 + q];
   }
   const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
+  if (call_failed(a.status)) return;  // issued with the offset loads: one round trip for both
   const uint64_t po0 = fo0 - p0 * (uint64_t)H;
   const uint64_t po_end = fo_end - (p0 + Tv) * (uint64_t)H;
   const uint64_t A = po0 & ~15ull;
@@ -496,6 +503,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
 
 template <int H>
 __global__ void __launch_bounds__(kBlock) decode_varlen_kernel(VarlenArgs a) {
+  if (call_failed(a.status)) return;
   const uint32_t g = threadIdx.x & (kVarLanes - 1u);
   const uint64_t p = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / kVarLanes;
   const bool valid = p < a.n;
@@ -637,6 +645,7 @@ __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_
 
 template <int H>
 __global__ void __launch_bounds__(kBlock) decode_varlen_vec_kernel(VarlenArgs a) {
+  if (call_failed(a.status)) return;
   const uint32_t glog = a.glog;
   const uint64_t p = (uint64_t)blockIdx.x * (kBlock >> glog) + (threadIdx.x >> glog);
   decode_varlen_frame<H>(a, p, p < a.n, threadIdx.x & ((1u << glog) - 1u), glog);
@@ -663,6 +672,7 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
   const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
+  if (call_failed(a.status)) return;
   const uint64_t A = fo0 & ~15ull;
   const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
   if (run > a.tile_cap) {  // uniform over the workgroup
@@ -752,6 +762,7 @@ __device__ __forceinline__ bool utf8_byte_ok(uint32_t c, uint32_t p1, uint32_t p
 }
 
 __global__ void __launch_bounds__(kBlock) validate_utf8_par_kernel(Utf8Args a) {
+  if (call_failed(a.status)) return;
   const uint32_t g = threadIdx.x & (kVarLanes - 1u);
   const uint64_t p = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / kVarLanes;
   const bool valid_p = p < a.n;
@@ -803,6 +814,7 @@ __device__ __forceinline__ uint32_t byte_of(u32x4 v, int k) {
 }
 
 __global__ void __launch_bounds__(kBlock) validate_utf8_vec_kernel(Utf8Args a) {
+  if (call_failed(a.status)) return;
   constexpr uint32_t U = 4;  // chunks per lane per round (2 and 8, nt loads: no better)
   const uint32_t G = 1u << a.glog;
   const uint32_t lane = threadIdx.x & 63u;
@@ -999,6 +1011,7 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_vtile_kernel(Utf8Args a)
   const uint32_t Tv = left < T ? (uint32_t)left : T;
   const uint64_t total = a.frame_off[a.n];
   const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
+  if (call_failed(a.status)) return;
   const uint64_t A = fo0 & ~15ull;
   const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
   uint32_t bad = 0;
@@ -1224,8 +1237,10 @@ int launch_validate_utf8(const Utf8Args& args, hipStream_t stream) {
 
 // frame_off[0..n] = exclusive scan of len[i] + H, frame_off[n] = total bytes.
 int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
-                       hipStream_t stream) {
-  if (tuning().varlen_scan == 1) return scan_frame_offsets_3pass(d_len, n, H, d_frame_off, stream);
+                       const ScanCheck& chk, hipStream_t stream) {
+  // the device-side checks live in the three-pass scan only
+  if (tuning().varlen_scan == 1 || chk.status)
+    return scan_frame_offsets_3pass(d_len, n, H, d_frame_off, chk, stream);
   hipcub::CountingInputIterator<uint64_t> idx(0);
   hipcub::TransformInputIterator<uint64_t, FrameLen, hipcub::CountingInputIterator<uint64_t>> it(
       idx, FrameLen{d_len, H});

@@ -18,7 +18,9 @@ LAYOUT_RUDP5 = 5
 LAYOUT_RUDP7 = 7
 OK_BAD_CSUM, OK_GOOD, OK_SHORT, OK_UNVERIFIED = 0, 1, 2, 3
 EINVAL, ENOMEM, ENOTSUP, EHIP_BASE = -22, -12, -95, -1000
-ABI_VERSION = 3
+ABI_VERSION = 4
+# status bits of the sync-free varlen calls (RUDP_ST_*)
+ST_LEN, ST_PAYLOAD, ST_FRAMES_CAP, ST_OFFSETS = 1, 2, 4, 8
 
 # Every symbol include/rudp.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -26,6 +28,7 @@ EXPORTS = (
     "rudp_synth", "rudp_device_count", "rudp_last_error", "rudp_abi_version",
     "rudp_encode_varlen", "rudp_validate_utf8", "rudp_dedup_window",
     "rudp_udp_recv_batch", "rudp_udp_send_batch", "rudp_varlen_bounds", "rudp_frame_off_bounds",
+    "rudp_encode_varlen_checked", "rudp_decode_varlen_checked", "rudp_frame_off_check",
 )
 
 
@@ -69,6 +72,9 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rudp_udp_send_batch": [I, P, P, U64, ctypes.c_char_p, ctypes.c_uint16],
         "rudp_varlen_bounds": [P, P, U64, P, I, P],
         "rudp_frame_off_bounds": [P, U64, P, I, P],
+        "rudp_encode_varlen_checked": [ctypes.POINTER(RudpBatch), U64, P, U64, P, P, P, I, I, P],
+        "rudp_decode_varlen_checked": [P, U64, P, U32, U64, P, P, P, P, P, P, P, I, I, P],
+        "rudp_frame_off_check": [P, U64, U64, P, I, P],
         "rudp_device_count": [ctypes.POINTER(ctypes.c_int)],
         "rudp_abi_version": [],
     }

@@ -96,6 +96,25 @@ class PayloadSpans:
         return 2
 
 
+_ST_MESSAGES = (
+    (_native.ST_LEN, "lengths must lie in [0, 65535]"),
+    (_native.ST_PAYLOAD, "packed payloads: sum(lengths) must equal payload.numel(); "
+                         "gathered payloads: payload_off + lengths must stay inside payload"),
+    (_native.ST_FRAMES_CAP, "out is too small for the frames (sum(lengths) + N * header bytes)"),
+    (_native.ST_OFFSETS, "frame_off must be non-decreasing offsets inside frames"),
+)
+
+
+def _raise_status(status) -> None:
+    """Read a sync-free call's device status word (synchronizes) and raise
+    ValueError with the reason when the device found the batch invalid."""
+    if status is None:
+        return
+    bits = int(status.item())
+    if bits:
+        raise ValueError("; ".join(m for b, m in _ST_MESSAGES if bits & b) or f"status {bits:#x}")
+
+
 class DecodedBatch(NamedTuple):
     seq: Any
     ack: Any
@@ -103,6 +122,13 @@ class DecodedBatch(NamedTuple):
     ok: Any          # 1 good, 0 bad checksum, 2 short frame, 3 unverified (rudp5, no csum)
     csum: Any        # recomputed checksum per packet
     payload: Any     # [N, L] view into frames (zero-copy) or a copy
+    status: Any = None  # sync-free varlen decode: device u32[1], RUDP_ST_* (0 = valid)
+
+    def check(self) -> "DecodedBatch":
+        """Raise ValueError if the device rejected the batch (reads ``status``:
+        one synchronization).  A no-op for calls that checked eagerly."""
+        _raise_status(self.status)
+        return self
 
 
 def _is_torch(x) -> bool:
@@ -330,9 +356,15 @@ def synth_batch(n: int, payload_len: int, seed: int, *, first_index: int = 0, as
 
 # ------------------------------------------------------- variable-length batches
 class VarlenFrames(NamedTuple):
-    frames: Any      # u8 [frame_off[-1]] — frames back to back
+    frames: Any      # u8 [frame_off[-1]] — frames back to back (or the caller's ``out``)
     frame_off: Any   # int64 [N + 1] — frame i = frames[frame_off[i]:frame_off[i + 1]]
     csum: Any        # u16 [N] or None
+    status: Any = None  # device u32[1], RUDP_ST_* of the call (0 = valid)
+
+    def check(self) -> "VarlenFrames":
+        """Raise ValueError if the device rejected the batch (one synchronization)."""
+        _raise_status(self.status)
+        return self
 
 
 def _int_tensor(t, name, device, n=None, dtypes=None):
@@ -346,8 +378,8 @@ def _int_tensor(t, name, device, n=None, dtypes=None):
 
 
 def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp7", *,
-                      payload_off=None, want_csum: Optional[bool] = None, stream=None
-                      ) -> VarlenFrames:
+                      payload_off=None, want_csum: Optional[bool] = None, stream=None, out=None,
+                      check: bool = True) -> VarlenFrames:
     """Frame + checksum a variable-length batch on a HIP device.
 
     ``payload``: u8 1-D tensor holding the payload bytes; ``lengths``: int32
@@ -356,6 +388,16 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
     in packet order.  Returns frames packed back to back plus their offsets:
     frame i is byte-identical to Packet(...).to_byte() of that packet
     (utils/reliableUDP.py:53-61 builds one per character).
+
+    The argument checks run on the device, inside the call (rudp_encode_varlen_checked):
+    ``check=True`` waits for them and raises ValueError on a bad batch, as the
+    reference's per-packet calls would fail; ``check=False`` never waits — the
+    host does not touch the device — and the result's ``check()`` raises later.
+    A rejected batch leaves ``frames`` unwritten.  ``out``: u8 1-D frame buffer
+    of at least sum(lengths) + N * header bytes (its first frame_off[-1] bytes
+    are the frames).  Without ``out`` the frame buffer is sized on the host for
+    packed payloads (payload.numel() + N * header bytes) and, for gathered
+    payloads, from one device read of the lengths' sum.
     """
     import torch
     H = layout_header_len(layout)
@@ -373,41 +415,44 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
             raise ValueError(f"{name} has {t.shape[0]} entries for {n} packets")
     if payload_off is not None:
         _int_tensor(payload_off, "payload_off", dev, n, dtypes=(torch.int64,))
-    # every bound in one device pass and one 40-byte read (rudp_varlen_bounds);
-    # lengths are read as u32, so a negative int32 shows up as > 65535
-    lmin = lmax = lsum = omin = oend = 0
-    if n:
-        out = (ctypes.c_int64 * 5)()
-        _native.check(_native.lib().rudp_varlen_bounds(
-            lengths.data_ptr(), payload_off.data_ptr() if payload_off is not None else None, n, out,
-            dev.index or 0, _stream_ptr(stream, dev)))
-        lmin, lmax, lsum, omin, oend = list(out)
-    if lmin < 0 or lmax > 65535:
-        raise ValueError("lengths must lie in [0, 65535]")
-    if payload_off is None:
-        if lsum != payload.numel():
-            raise ValueError("packed payloads: sum(lengths) must equal payload.numel()")
-    elif omin < 0 or oend > payload.numel():
-        raise ValueError("payload_off + lengths must stay inside payload")
-    total = lsum + n * H
+    if out is not None:
+        _dev_check(out, "out", torch.uint8, 1, dev)
+        frames = out
+        lsum = max(out.numel() - n * H, 0)  # at most; only the lanes hint reads it
+    elif payload_off is None:
+        lsum = payload.numel()  # exact for a valid packed batch; the device checks it
+        frames = torch.empty((lsum + n * H,), dtype=torch.uint8, device=dev)
+    else:
+        # gathered payloads: the frame bytes are unknown until the lengths are summed
+        # (rudp_varlen_bounds, one 40-byte device read); lengths are read as u32
+        lmin = lmax = lsum = omin = oend = 0
+        if n:
+            bnd = (ctypes.c_int64 * 5)()
+            _native.check(_native.lib().rudp_varlen_bounds(
+                lengths.data_ptr(), payload_off.data_ptr(), n, bnd, dev.index or 0, _stream_ptr(stream, dev)))
+            lmin, lmax, lsum, omin, oend = list(bnd)
+        if lmin < 0 or lmax > 65535:
+            raise ValueError("lengths must lie in [0, 65535]")
+        if omin < 0 or oend > payload.numel():
+            raise ValueError("payload_off + lengths must stay inside payload")
+        frames = torch.empty((lsum + n * H,), dtype=torch.uint8, device=dev)
     if want_csum is None:
         want_csum = H == 5
-    frames = torch.empty((total,), dtype=torch.uint8, device=dev)
     frame_off = torch.empty((n + 1,), dtype=torch.int64, device=dev)
     csum = torch.empty((n,), dtype=torch.uint16, device=dev) if want_csum else None
-    if n == 0:
-        frame_off.zero_()
-        return VarlenFrames(frames, frame_off, csum)
+    status = torch.empty((1,), dtype=torch.int32, device=dev)
     # payload_len carries the mean payload length: a hint that picks lanes per packet
-    b = _native.RudpBatch(n=n, payload_len=min(lsum // n, 65535), reserved=0, seq=tab.seq.data_ptr(),
-                          ack=tab.ack.data_ptr(), flags=tab.flags.data_ptr(),
+    b = _native.RudpBatch(n=n, payload_len=min(lsum // n, 65535) if n else 0, reserved=0,
+                          seq=tab.seq.data_ptr(), ack=tab.ack.data_ptr(), flags=tab.flags.data_ptr(),
                           payload=payload.data_ptr() if payload.numel() else 16,  # never read: all lengths 0
                           len=lengths.data_ptr(),
                           payload_off=payload_off.data_ptr() if payload_off is not None else None)
-    _native.check(_native.lib().rudp_encode_varlen(
-        ctypes.byref(b), frames.data_ptr(), frame_off.data_ptr(),
-        csum.data_ptr() if csum is not None else None, H, dev.index or 0, _stream_ptr(stream, dev)))
-    return VarlenFrames(frames, frame_off, csum)
+    _native.check(_native.lib().rudp_encode_varlen_checked(
+        ctypes.byref(b), payload.numel(), frames.data_ptr() if frames.numel() else 16, frames.numel(),
+        frame_off.data_ptr(), csum.data_ptr() if csum is not None else None, status.data_ptr(), H,
+        dev.index or 0, _stream_ptr(stream, dev)))
+    res = VarlenFrames(frames, frame_off, csum, status)
+    return res.check() if check else res
 
 
 def _check_offsets(frames, frame_off, stream=None) -> int:
@@ -425,12 +470,15 @@ def _check_offsets(frames, frame_off, stream=None) -> int:
 
 
 def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *, csum=None,
-                        stream=None) -> DecodedBatch:
+                        stream=None, check: bool = True) -> DecodedBatch:
     """Parse + verify frames packed back to back (offsets as pack_batch_varlen returns).
 
     The payload is zero-copy: ``payload`` is the pair ``(start, end)`` of int64
     [N] tensors indexing ``frames`` (empty for frames shorter than the header),
-    as a ``PayloadSpans`` that computes ``start`` on first use.
+    as a ``PayloadSpans`` that computes ``start`` on first use.  The offsets
+    are checked on the device inside the call (rudp_decode_varlen_checked):
+    ``check=True`` waits and raises ValueError on bad offsets; ``check=False``
+    never waits, and the result's ``check()`` raises later.
     """
     import torch
     H = layout_header_len(layout)
@@ -442,7 +490,6 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
     n = frame_off.shape[0] - 1
     if n < 0:
         raise ValueError("frame_off needs N + 1 entries")
-    mean_len = _check_offsets(frames, frame_off, stream)
     if csum is not None:
         _dev_check(csum, "csum", torch.uint16, 1, dev)
         if csum.shape[0] != n:
@@ -452,13 +499,16 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
     flags = torch.empty((n,), dtype=torch.uint8, device=dev)
     ok = torch.empty((n,), dtype=torch.uint8, device=dev)
     cs = torch.empty((n,), dtype=torch.uint16, device=dev)
-    if n:
-        _native.check(_native.lib().rudp_decode(
-            frames.data_ptr() if frames.numel() else 16, frame_off.data_ptr(), mean_len, n,
-            csum.data_ptr() if csum is not None else None, seq.data_ptr(), ack.data_ptr(),
-            flags.data_ptr(), ok.data_ptr(), cs.data_ptr(), None, H, dev.index or 0,
-            _stream_ptr(stream, dev)))
-    return DecodedBatch(seq, ack, flags, ok, cs, PayloadSpans(frame_off, H))
+    status = torch.empty((1,), dtype=torch.int32, device=dev)
+    # mean frame length from the buffer size: a hint that picks lanes / tiles per frame
+    hint = min(frames.numel() // n, 0xFFFFFFFF) if n else 0
+    _native.check(_native.lib().rudp_decode_varlen_checked(
+        frames.data_ptr() if frames.numel() else 16, frames.numel(), frame_off.data_ptr(), hint, n,
+        csum.data_ptr() if csum is not None else None, seq.data_ptr(), ack.data_ptr(),
+        flags.data_ptr(), ok.data_ptr(), cs.data_ptr(), status.data_ptr(), H, dev.index or 0,
+        _stream_ptr(stream, dev)))
+    res = DecodedBatch(seq, ack, flags, ok, cs, PayloadSpans(frame_off, H), status)
+    return res.check() if check else res
 
 
 def validate_utf8(frames, layout: Union[str, int] = "rudp7", *, frame_off=None, stream=None):

@@ -64,33 +64,90 @@ def send_batch(sock: _socket.socket, frames: np.ndarray, frame_off: np.ndarray, 
 
 
 class BatchReceiver:
-    """A pinned receive ring for one socket, decoded on the GPU in one launch."""
+    """A ring of pinned receive slots for one socket, decoded on the GPU.
 
-    def __init__(self, sock: _socket.socket, max_msgs: int = 65536, slot_bytes: int = 1024):
+    ``recv()`` fills the next slot with recvmmsg while the H2D copy and the
+    decode of the previous batches run on ``stream``: a slot is handed to the
+    socket again only after the event recorded behind its H2D copy has fired,
+    so a copy still in flight is never overwritten (no reliance on any other
+    synchronization).  ``decode()`` never waits for the device: it enqueues the
+    copy and the sync-free varlen decode on ``stream`` and makes the caller's
+    current stream wait for them, so ordinary torch work on the results is
+    ordered after the decode.
+
+        rx = BatchReceiver(sock, slots=3)
+        while (k := rx.recv(timeout_ms=100)):
+            dec, frames, off = rx.decode("rudp5", device)   # async
+    """
+
+    def __init__(self, sock: _socket.socket, max_msgs: int = 65536, slot_bytes: int = 1024,
+                 slots: int = 3, device=None, stream=None):
         import torch
+        if slots < 1:
+            raise ValueError("slots must be >= 1")
         self.sock = sock
         self.slot_bytes = slot_bytes
         self.max_msgs = max_msgs
-        self._frames_t = torch.empty((max_msgs * slot_bytes,), dtype=torch.uint8, pin_memory=True)
-        self._off_t = torch.empty((max_msgs + 1,), dtype=torch.int64, pin_memory=True)
-        self.frames = self._frames_t.numpy()
-        self.frame_off = self._off_t.numpy()
+        self.device = torch.device(device) if device is not None else torch.device("cuda", 0)
+        self.stream = stream if stream is not None else torch.cuda.Stream(self.device)
+        self._frames_t = [torch.empty((max_msgs * slot_bytes,), dtype=torch.uint8, pin_memory=True)
+                          for _ in range(slots)]
+        self._off_t = [torch.empty((max_msgs + 1,), dtype=torch.int64, pin_memory=True) for _ in range(slots)]
+        self._copied = [None] * slots   # event behind the last H2D copy out of each slot
+        self._slot = -1
         self.count = 0
 
+    @property
+    def frames(self) -> np.ndarray:
+        """Host view of the slot the last recv() filled."""
+        return self._frames_t[self._slot].numpy()
+
+    @property
+    def frame_off(self) -> np.ndarray:
+        return self._off_t[self._slot].numpy()
+
     def recv(self, timeout_ms: int = -1) -> int:
-        self.count = recv_batch(self.sock, self.frames, self.frame_off, slot_bytes=self.slot_bytes,
-                                max_msgs=self.max_msgs, timeout_ms=timeout_ms)
+        k = (self._slot + 1) % len(self._frames_t)
+        if self._copied[k] is not None:
+            self._copied[k].synchronize()  # that slot's H2D copy has left the pinned buffer
+            self._copied[k] = None
+        self._slot = k
+        self.count = recv_batch(self.sock, self._frames_t[k].numpy(), self._off_t[k].numpy(),
+                                slot_bytes=self.slot_bytes, max_msgs=self.max_msgs, timeout_ms=timeout_ms)
         return self.count
 
     def frame(self, i: int) -> bytes:
         return bytes(self.frames[self.frame_off[i]:self.frame_off[i + 1]])
 
-    def decode(self, layout="rudp5", device=None, csum=None, stream=None):
-        """H2D of the received frames, then parse + verify them on the device."""
+    def decode(self, layout="rudp5", device=None, csum=None, stream=None, check=False):
+        """H2D of the received frames, then parse + verify them on the device.
+
+        Returns ``(DecodedBatch, d_frames, d_frame_off)``; the device buffers are
+        fresh (the caller owns them; the payload spans index ``d_frames``).
+        ``check=True`` also waits for the device's offset check and raises on
+        bad offsets (recvmmsg writes valid ones, so the default is not to wait).
+        """
         import torch
-        dev = torch.device(device) if device is not None else torch.device("cuda", 0)
-        n = self.count
-        total = int(self.frame_off[n])
-        d_frames = self._frames_t[:total].to(dev, non_blocking=True)
-        d_off = self._off_t[:n + 1].to(dev, non_blocking=True)
-        return _batch.unpack_batch_varlen(d_frames, d_off, layout, csum=csum, stream=stream), d_frames, d_off
+        if device is not None and torch.device(device) != self.device:
+            raise ValueError(f"this receiver decodes on {self.device}")
+        s = stream if stream is not None else self.stream
+        k, n = self._slot, self.count
+        if k < 0:
+            raise RuntimeError("decode() before any recv()")
+        total = int(self._off_t[k][n])
+        s.wait_stream(torch.cuda.current_stream(self.device))  # e.g. csum written by the caller
+        with torch.cuda.stream(s):
+            d_frames = torch.empty((total,), dtype=torch.uint8, device=self.device)
+            d_off = torch.empty((n + 1,), dtype=torch.int64, device=self.device)
+            d_frames.copy_(self._frames_t[k][:total], non_blocking=True)
+            d_off.copy_(self._off_t[k][:n + 1], non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(s)
+            self._copied[k] = ev
+            dec = _batch.unpack_batch_varlen(d_frames, d_off, layout, csum=csum, stream=s, check=False)
+        cur = torch.cuda.current_stream(self.device)
+        cur.wait_stream(s)
+        # allocated on `s`, used on the caller's stream from here on
+        for t in (d_frames, d_off, dec.seq, dec.ack, dec.flags, dec.ok, dec.csum, dec.status):
+            t.record_stream(cur)
+        return (dec.check() if check else dec), d_frames, d_off

@@ -64,6 +64,13 @@ def test_argument_errors_before_device():
     assert lib.rudp_varlen_bounds(None, None, 4, out5, 0, None) == _native.EINVAL
     assert lib.rudp_varlen_bounds(None, None, 4, None, 0, None) == _native.EINVAL
     assert lib.rudp_frame_off_bounds(None, 4, out5, 0, None) == _native.EINVAL
+    # the sync-free varlen entries need their status word and offsets
+    b1 = ctypes.byref(_native.RudpBatch(n=1))
+    assert lib.rudp_encode_varlen_checked(b1, 0, None, 0, None, None, None, 7, 0, None) == _native.EINVAL
+    assert b"d_status" in lib.rudp_last_error()
+    assert lib.rudp_decode_varlen_checked(None, 0, None, 0, 1, None, None, None, None, None, None, None, 7, 0,
+                                          None) == _native.EINVAL
+    assert lib.rudp_frame_off_check(None, 1, 0, None, 0, None) == _native.EINVAL
     # empty batches are a successful no-op, no device needed
     assert lib.rudp_encode(ctypes.byref(_native.RudpBatch(n=0)), None, None, 5, 0, None) == 0
     assert lib.rudp_synth(1, 0, 0, 16, 1, None, None, None, None, 0, None) == 0

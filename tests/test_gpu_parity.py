@@ -313,48 +313,6 @@ def test_encode_align64_vs_oracle(cuda, L):
                     assert np.array_equal(host(v.csum), want_cs), (L, n, layout, align)
 
 
-@pytest.mark.parametrize("L", [16, 32, 48, 64, 80, 128, 1008, 1024, 1472, 2048, 4096])
-def test_encode_stream_kernel_vs_oracle(cuda, L):
-    """The register-streamed encode (rudpx_tune 20) gives the oracle's frames
-    and checksums for every workgroup size and load depth, including batches
-    whose last chunk is partial and workgroups of one packet."""
-    import ctypes
-    from rudp import _native
-    lib = _native.lib()
-    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
-    for n in (1, 2, 3, 15, 16, 17, 255, 257, 1027):
-        seq, ack, flags, pay = synth.synth(0x77 + L, n, n, L, ascii=False)
-        for layout in (5, 7):
-            want_fr, want_cs = codec_np.encode(seq, ack, flags, pay, layout)
-            for tile, rounds in ((0, 2), (1, 1), (3, 4), (16, 2), (256, 1), (0, 4)):
-                old = (lib.rudpx_tune(20, 1), lib.rudpx_tune(21, tile), lib.rudpx_tune(22, rounds))
-                try:
-                    fr, cs = gpu_encode(cuda, seq, ack, flags, pay, layout)
-                finally:
-                    for key, val in zip((20, 21, 22), old):
-                        lib.rudpx_tune(key, val)
-                assert np.array_equal(fr, want_fr), (L, n, layout, tile, rounds)
-                assert np.array_equal(cs, want_cs), (L, n, layout, tile, rounds)
-
-
-@pytest.mark.slow
-@pytest.mark.parametrize("name,layout", [("C2", 5), ("C3", 5), ("C4", 7), ("C4", 5)])
-def test_encode_stream_kernel_full_size_digests(cuda, digests, name, layout):
-    """Register-streamed encode reproduces the reference digests at full size."""
-    import ctypes
-    from rudp import _native
-    lib = _native.lib()
-    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
-    old = lib.rudpx_tune(20, 1)
-    try:
-        h_fr, h_cs, _ = _digest_run(cuda, digests[name], layout, 0)
-    finally:
-        lib.rudpx_tune(20, old)
-    want = digests[name]["layouts"][str(layout)]
-    assert h_fr == want["frames"][0]
-    assert h_cs == want["csum"][0]
-
-
 def test_concurrent_callers(cuda):
     """The proxy calls the codec from ThreadPoolExecutor workers (proxy.py:127, :154):
     host-staged and device-resident calls from 8 threads at once stay exact, and an

@@ -614,3 +614,148 @@ def test_utf8_packed_tile_vs_python_decoder(cuda):
                 assert np.array_equal(host(out), want), (vtile, hint)
         finally:
             lib.rudpx_tune(41, old)
+
+
+# ------------------------------------------------ sync-free (device-checked) entries
+def test_varlen_sync_free_matches_checked(cuda):
+    """check=False never waits for the device and gives the same frames / fields."""
+    import torch
+    rng = np.random.default_rng(41)
+    n = 20011
+    lens = rng.integers(0, 300, n).astype(np.int32)
+    pay = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    seq, ack, flags, _ = synth.synth(41, 0, n, 0)
+    tab = (dev(seq, cuda), dev(ack, cuda), dev(flags, cuda))
+    for layout in (5, 7):
+        a = batch.pack_batch_varlen(tab, dev(pay, cuda), dev(lens, cuda), layout, want_csum=True)
+        b = batch.pack_batch_varlen(tab, dev(pay, cuda), dev(lens, cuda), layout, want_csum=True, check=False)
+        b.check()
+        assert int(b.status.item()) == 0
+        assert torch.equal(a.frames, b.frames) and torch.equal(a.frame_off, b.frame_off)
+        want, off, cs = codec_np.encode_varlen(seq, ack, flags, split_by_lengths(pay, lens)[0], layout)
+        assert np.array_equal(host(b.frames), want) and np.array_equal(host(b.csum), cs)
+        d = batch.unpack_batch_varlen(b.frames, b.frame_off, layout, csum=b.csum if layout == 5 else None,
+                                      check=False)
+        assert int(d.status.item()) == 0 and bool((d.ok == 1).all())
+        assert np.array_equal(host(d.seq), seq)
+        # caller-provided frame buffer larger than needed: the frames are its prefix
+        big = torch.full((int(lens.sum()) + n * layout + 100,), 0xAA, dtype=torch.uint8, device=cuda)
+        c = batch.pack_batch_varlen(tab, dev(pay, cuda), dev(lens, cuda), layout, out=big, check=False).check()
+        assert c.frames is big and np.array_equal(host(big[:len(want)]), want)
+        assert (host(big[len(want):]) == 0xAA).all()
+
+
+def test_varlen_device_checks_reject_bad_batches(cuda):
+    """Every argument check runs on the device; a rejected batch writes no frames."""
+    import torch
+    n = 4096
+    seq, ack, flags, _ = synth.synth(5, 0, n, 0)
+    tab = (dev(seq, cuda), dev(ack, cuda), dev(flags, cuda))
+    lens = np.full(n, 3, np.int32)
+    pay = dev(np.zeros(3 * n, np.uint8), cuda)
+
+    def rejected(match, **kw):
+        kw.setdefault("payload", pay)
+        kw.setdefault("lengths", dev(lens, cuda))
+        for check in (True, False):
+            out = torch.full((4 * 70000 * 7 + 64,), 0x5C, dtype=torch.uint8, device=cuda) \
+                if "out" not in kw else kw["out"]
+            args = dict(kw, out=out)
+            with pytest.raises(ValueError, match=match):
+                r = batch.pack_batch_varlen(tab, args.pop("payload"), args.pop("lengths"), 7, check=check,
+                                            **args)
+                r.check()  # check=False: raises here, not inside the call
+            assert bool((out == 0x5C).all()), "a rejected batch must leave the frame buffer alone"
+
+    bad = lens.copy(); bad[777] = 70000
+    rejected("65535", lengths=dev(bad, cuda), payload=dev(np.zeros(int(bad.sum()), np.uint8), cuda))
+    rejected("sum", lengths=dev(lens + 1, cuda))
+    offs = (np.arange(n) * 3).astype(np.int64); offs[100] = 3 * n - 1
+    rejected("inside payload", payload_off=dev(offs, cuda))
+    offs2 = offs.copy(); offs2[5] = -4
+    rejected("inside payload", payload_off=dev(offs2, cuda))
+    small = torch.full((n * 10 - 1,), 0x5C, dtype=torch.uint8, device=cuda)
+    rejected("too small", out=small)
+    # without check the call returns at once; the status tells
+    r = batch.pack_batch_varlen(tab, pay, dev(lens + 1, cuda), 7, check=False)
+    assert int(r.status.item()) & 2
+    # decode: offsets decreasing, past the buffer, negative
+    fr = batch.pack_batch_varlen(tab, pay, dev(lens, cuda), 7)
+    for mut in ((7, 3), (n, 10 ** 9), (0, -8)):
+        off = fr.frame_off.clone()
+        off[mut[0]] = mut[1]
+        for check in (True, False):
+            with pytest.raises(ValueError, match="non-decreasing"):
+                batch.unpack_batch_varlen(fr.frames, off, 7, check=check).check()
+
+
+def test_varlen_empty_batches_sync_free(cuda):
+    import torch
+    z = torch.zeros(0, dtype=torch.uint16, device=cuda)
+    r = batch.pack_batch_varlen((z, z, z.to(torch.uint8)), torch.zeros(0, dtype=torch.uint8, device=cuda),
+                                torch.zeros(0, dtype=torch.int32, device=cuda), 5, check=False).check()
+    assert r.frames.numel() == 0 and host(r.frame_off).tolist() == [0]
+    d = batch.unpack_batch_varlen(r.frames, r.frame_off, 5, check=False).check()
+    assert d.ok.numel() == 0
+    # header-only frames (all lengths 0): frames exist, payload buffer is empty
+    n = 1000
+    seq, ack, flags, _ = synth.synth(8, 0, n, 0)
+    r = batch.pack_batch_varlen((dev(seq, cuda), dev(ack, cuda), dev(flags, cuda)),
+                                torch.zeros(0, dtype=torch.uint8, device=cuda),
+                                torch.zeros(n, dtype=torch.int32, device=cuda), 7, check=False).check()
+    want, _, _ = codec_np.encode_varlen(seq, ack, flags, [b""] * n, 7)
+    assert np.array_equal(host(r.frames), want)
+
+
+@pytest.mark.parametrize("slots", [1, 2, 4])
+def test_socket_ring_overlapped_decode_side_stream(cuda, slots):
+    """The receive ring (§8f row 1): recvmmsg into slot k+1 while slot k's H2D copy
+    and decode run on a side stream; every batch equals the oracle's decode."""
+    import socket
+    import threading
+
+    import torch
+    from rudp import netio
+    n = 30000
+    rng = np.random.default_rng(50 + slots)
+    seq, ack, flags, _ = synth.synth(50 + slots, 0, n, 0)
+    pays = [rng.integers(32, 127, int(k), dtype=np.uint8).tobytes() for k in rng.integers(1, 9, n)]
+    fr, off, cs = codec_np.encode_varlen(seq, ack, flags, pays, 7)
+    fr = fr.copy()
+    fr[off[999] + 3] ^= 0x20  # one corrupted datagram
+    rx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    rx.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 26)
+    rx.bind(("127.0.0.1", 0))
+    tx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    side = torch.cuda.Stream(cuda)
+    recv = netio.BatchReceiver(rx, max_msgs=4096, slot_bytes=64, slots=slots, device=cuda, stream=side)
+    t = threading.Thread(target=lambda: netio.send_batch(tx, fr, off, "127.0.0.1", rx.getsockname()[1]))
+    t.start()
+    pending, got = [], 0
+    while got < n:
+        k = recv.recv(timeout_ms=3000)
+        assert k > 0
+        # what the socket delivered into this slot (copied before the slot is reused)
+        snap = (recv.frames[:recv.frame_off[k]].copy(), recv.frame_off[:k + 1].copy())
+        dec, d_frames, d_off = recv.decode("rudp7")  # async: the next recv overlaps it
+        pending.append((snap, dec, d_frames, d_off))
+        got += k
+    t.join()
+    torch.cuda.synchronize()
+    i0 = 0
+    for (h_fr, h_off), dec, d_frames, d_off in pending:
+        dec.check()
+        k = len(h_off) - 1
+        host_frames = [bytes(h_fr[h_off[i]:h_off[i + 1]]) for i in range(k)]
+        want = [bytes(fr[off[i]:off[i + 1]]) for i in range(i0, i0 + k)]
+        assert host_frames == want
+        flat = np.frombuffer(b"".join(want), np.uint8)
+        w_off = np.concatenate([[0], np.cumsum([len(x) for x in want])]).astype(np.int64)
+        exp = codec_np.decode_varlen(flat, w_off, 7)
+        for g, e in zip((dec.seq, dec.ack, dec.flags, dec.ok, dec.csum), exp):
+            assert np.array_equal(host(g), e)
+        assert np.array_equal(host(d_frames), flat) and np.array_equal(host(d_off), w_off)
+        i0 += k
+    assert i0 == n
+    rx.close()
+    tx.close()

@@ -67,7 +67,6 @@ PERCU_OVERRIDE = None      # encode: tiles-per-CU caps to try (256-thread blocks
 TILES_OVERRIDE = None      # encode: packets per tile to try
 VDEC_CAP_PCTS = ()         # vdec: extra varlen-decode tile LDS budgets (% of the hinted run)
 GEOMETRY_VARIANTS = False
-STREAM_ABLATE = False      # stream: also time stage ablations (wrong output; key 13 bits 8/16)  # varlen_enc: also sweep tile size knobs (keys 17, 18)
 
 
 def encode_sweep(reps):
@@ -384,55 +383,6 @@ def vknob_sweep(reps, key, values, pre=()):
     return out
 
 
-def stream_sweep(reps):
-    """Register-streamed encode (rudpx_tune 20-22) against the LDS-tile encode."""
-    out = {}
-    dev = torch.device("cuda", 0)
-    for L, tiles in ((1472, (4, 8, 16, 32)), (1024, (4, 8, 16, 32)), (64, (32, 64, 128, 256))):
-        n = 1 << 20
-        nsets = 1 if L > 512 else 7
-        sets = []
-        for _ in range(nsets):
-            tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
-            sets.append((tab, pay, torch.empty((n, L + 7), dtype=torch.uint8, device=dev)))
-        it = [0]
-
-        def run():
-            tab, pay, fr = sets[it[0] % nsets]
-            it[0] += 1
-            batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
-
-        def cfg(stream, tile=0, rounds=2):
-            return lambda: (lib.rudpx_tune(20, stream), lib.rudpx_tune(21, tile), lib.rudpx_tune(22, rounds))
-        variants = {f"L{L}_tile": (cfg(0), run)}
-        for tile in tiles:
-            for rounds in (1, 2, 4):
-                variants[f"L{L}_stream_T{tile}_R{rounds}"] = (cfg(1, tile, rounds), run)
-        if STREAM_ABLATE:
-            for abl in (8, 16, 24):
-                for tile in tiles[:2]:
-                    variants[f"L{L}_stream_T{tile}_R2_ablate{abl}"] = (
-                        lambda tile=tile, abl=abl: (cfg(1, tile, 2)(), lib.rudpx_tune(13, abl)), run)
-                    variants[f"L{L}_tile_ablate{abl}"] = (lambda: (cfg(0)(), lib.rudpx_tune(13, 0)), run)
-            variants[f"L{L}_tile"] = (lambda: (cfg(0)(), lib.rudpx_tune(13, 0)), run)
-        res = interleaved(variants, reps)
-        lib.rudpx_tune(13, 0)
-        alg = n * (2 * L + 12)
-        tab0, pay0, _ = sets[0]
-        cfg(0)()
-        want, _ = batch.pack_batch(tab0, pay0, 7)
-        for k, (setup, _) in variants.items():
-            setup()
-            got, _ = batch.pack_batch(tab0, pay0, 7)
-            lib.rudpx_tune(13, 0)
-            out[k] = {"ms": res[k], "TBs": alg / res[k] / 1e9, "frac": alg / res[k] / 1e9 / 8.0,
-                      "exact": bool(torch.equal(got, want))}
-        cfg(0)()
-        del sets
-        torch.cuda.empty_cache()
-    return out
-
-
 def decode_sweep(reps):
     dev = torch.device("cuda", 0)
     out = {}
@@ -722,10 +672,9 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--L", type=int, default=1472, help="payload length for --only ablate")
-    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "stream", "align", "knob", "copydma", "multi", "opsknob", "vdec", "vknob"])
+    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "align", "knob", "copydma", "multi", "opsknob", "vdec", "vknob"])
     ap.add_argument("--blocks", type=str, default="", help="encode sweep: workgroup sizes, e.g. 256,512,1024")
     ap.add_argument("--encode-L", type=str, default="", help="encode sweep: payload lengths, e.g. 1472")
-    ap.add_argument("--ablate", action="store_true", help="stream sweep: add stage ablations")
     ap.add_argument("--percu", type=str, default="", help="encode sweep: tiles-per-CU caps, e.g. 3,4,5")
     ap.add_argument("--key", type=int, default=25, help="--only knob: rudpx_tune key")
     ap.add_argument("--values", type=str, default="0,1", help="--only knob: values (first = reference)")
@@ -734,12 +683,11 @@ def main():
                     help="--only multi: name:key=val,key=val;name2:... (first = reference)")
     ap.add_argument("--tiles", type=str, default="", help="encode sweep: packets per tile, e.g. 8,16")
     args = ap.parse_args()
-    global BLOCKS_OVERRIDE, ENCODE_LS, STREAM_ABLATE, PERCU_OVERRIDE, TILES_OVERRIDE
+    global BLOCKS_OVERRIDE, ENCODE_LS, PERCU_OVERRIDE, TILES_OVERRIDE
     if args.percu:
         PERCU_OVERRIDE = tuple(int(x) for x in args.percu.split(","))
     if args.tiles:
         TILES_OVERRIDE = tuple(int(x) for x in args.tiles.split(","))
-    STREAM_ABLATE = args.ablate
     if args.blocks:
         BLOCKS_OVERRIDE = tuple(int(b) for b in args.blocks.split(","))
     if args.encode_L:
@@ -776,8 +724,6 @@ def main():
     if args.only == "opsknob":  # every tile op under --key at --values (names v<value>)
         vals = tuple(int(x) for x in args.values.split(","))
         result["opsknob"] = align_sweep(args.reps, args.key, vals, tuple(f"v{v}" for v in vals))
-    if args.only == "stream":
-        result["stream"] = stream_sweep(args.reps)
     if args.only == "varlen_enc":
         result["varlen_enc"] = varlen_enc_sweep(args.reps)
     if args.only == "ablate":
