@@ -272,8 +272,27 @@ def legs(torch, batch, device, steps):
     flat1 = pay1.view(-1)
     enc = batch.pack_batch_varlen(tab1, flat1, lens1, "rudp5", want_csum=True)
 
-    def varlen_pair(tab, flat, lens, layout, frames, off, csum):
+    def varlen_pair(tab, flat, lens, layout, frames, off, csum, rounds=7):
+        """Sync-free and eager-check encode / decode through the Python entry, and the
+        raw C-ABI call chain beside them (preallocated outputs, no Python wrapper),
+        interleaved round by round so all four see the same box state; medians
+        of the per-round means (ms per call)."""
+        import ctypes
+        from rudp import _native
+        lib = _native.lib()
+        H = batch.layout_header_len(layout)
+        n = lens.shape[0]
         last = {}
+        f_out = torch.empty_like(frames)
+        o_out = torch.empty_like(off)
+        c_out = torch.empty((n,), dtype=torch.uint16, device=device) if csum is not None else None
+        st = torch.empty((1,), dtype=torch.int32, device=device)
+        d_out = [torch.empty((n,), dtype=dt, device=device)
+                 for dt in (torch.uint16, torch.uint16, torch.uint8, torch.uint8, torch.uint16)]
+        rb = _native.RudpBatch(n=n, payload_len=flat.numel() // n, reserved=0, seq=tab.seq.data_ptr(),
+                               ack=tab.ack.data_ptr(), flags=tab.flags.data_ptr(), payload=flat.data_ptr(),
+                               len=lens.data_ptr(), payload_off=None)
+        sp = torch.cuda.current_stream().cuda_stream
 
         def e(i, check=False):
             last["e"] = batch.pack_batch_varlen(tab, flat, lens, layout, want_csum=csum is not None,
@@ -281,27 +300,45 @@ def legs(torch, batch, device, steps):
 
         def d(i, check=False):
             last["d"] = batch.unpack_batch_varlen(frames, off, layout, csum=csum, check=check)
-        ms_e = time_loop(torch, e, steps, 3) / steps
-        last["e"].check()
-        ms_d = time_loop(torch, d, steps, 3) / steps
-        last["d"].check()
-        ms_e_sync = time_loop(torch, lambda i: e(i, True), steps, 3) / steps
-        ms_d_sync = time_loop(torch, lambda i: d(i, True), steps, 3) / steps
-        return ms_e, ms_d, ms_e_sync, ms_d_sync
 
-    ms_e, ms_d, ms_es, ms_ds = varlen_pair(tab1, flat1, lens1, "rudp5", enc.frames, enc.frame_off, enc.csum)
-    out["varlen_1M_x_1char"] = {"encode_Mpkt_s": n1 / ms_e / 1e3, "encode_ms": ms_e,
-                                "decode_verify_Mpkt_s": n1 / ms_d / 1e3, "decode_ms": ms_d,
-                                "encode_ms_eager_check": ms_es, "decode_ms_eager_check": ms_ds,
+        def e_abi(i):
+            lib.rudp_encode_varlen_checked(ctypes.byref(rb), flat.numel(), f_out.data_ptr(), f_out.numel(),
+                                           o_out.data_ptr(), c_out.data_ptr() if c_out is not None else None,
+                                           st.data_ptr(), H, device.index or 0, sp)
+
+        def d_abi(i):
+            lib.rudp_decode_varlen_checked(frames.data_ptr(), frames.numel(), off.data_ptr(),
+                                           frames.numel() // n, n,
+                                           csum.data_ptr() if csum is not None else None,
+                                           *[t.data_ptr() for t in d_out], st.data_ptr(), H,
+                                           device.index or 0, sp)
+        fns = {"encode": e, "decode": d, "encode_eager_check": lambda i: e(i, True),
+               "decode_eager_check": lambda i: d(i, True), "encode_abi": e_abi, "decode_abi": d_abi}
+        per = {k: [] for k in fns}
+        for r in range(rounds):
+            for k, fn in fns.items():
+                per[k].append(time_loop(torch, fn, steps, 2 if r == 0 else 1) / steps)
+        last["e"].check()
+        last["d"].check()
+        if int(st.item()):
+            raise RuntimeError("the raw C-ABI varlen calls rejected the bench batch")
+        return {k: sorted(v)[len(v) // 2] for k, v in per.items()}
+
+    t1 = varlen_pair(tab1, flat1, lens1, "rudp5", enc.frames, enc.frame_off, enc.csum)
+    out["varlen_1M_x_1char"] = {"encode_Mpkt_s": n1 / t1["encode"] / 1e3, "encode_ms": t1["encode"],
+                                "decode_verify_Mpkt_s": n1 / t1["decode"] / 1e3, "decode_ms": t1["decode"],
+                                "ms_by_form": t1,
                                 "note": "Python entry, sync-free (device-side argument checks, status "
-                                        "read after the loop); *_eager_check: one sync per call"}
+                                        "read after the loop); *_eager_check: one sync per call; *_abi: "
+                                        "the C-ABI calls alone; medians of 7 interleaved rounds"}
     # the varlen path at MTU size: 1M x 1472 B payloads packed back to back
     # (frames at odd offsets), encode (scan + tile kernel) and decode-verify
     tabm, paym = batch.synth_batch(n1, 1472, SEEDS[1472], device=device)
     lensm = torch.full((n1,), 1472, dtype=torch.int32, device=device)
     flatm = paym.view(-1)
     encm = batch.pack_batch_varlen(tabm, flatm, lensm, "rudp7")
-    ms_em, ms_dm, ms_ems, ms_dms = varlen_pair(tabm, flatm, lensm, "rudp7", encm.frames, encm.frame_off, None)
+    tm = varlen_pair(tabm, flatm, lensm, "rudp7", encm.frames, encm.frame_off, None)
+    ms_em, ms_dm = tm["encode"], tm["decode"]
     # algorithmic bytes: encode reads payload + len + table (1472 + 4 + 5), writes frame + offset
     # (1479 + 8); decode reads frame + offset, writes seq/ack/flags/ok/csum (8)
     out["varlen_1Mx1472"] = {
@@ -309,8 +346,9 @@ def legs(torch, batch, device, steps):
         "encode_roofline_frac": n1 * (1472 + 9 + 1479 + 8) / (ms_em / 1e3) / 1e9 / HBM_PEAK_GBS,
         "decode_GiB_s": n1 * 1472 / (ms_dm / 1e3) / GIB, "decode_ms": ms_dm,
         "decode_roofline_frac": n1 * (1479 + 8 + 8) / (ms_dm / 1e3) / 1e9 / HBM_PEAK_GBS,
-        "encode_ms_eager_check": ms_ems, "decode_ms_eager_check": ms_dms,
-        "note": "Python entry, sync-free (offset scan and device-side checks included)"}
+        "ms_by_form": tm,
+        "note": "Python entry, sync-free (offset scan and device-side checks included); medians of "
+                "7 interleaved rounds beside the eager-check and raw C-ABI forms"}
     del tabm, paym, lensm, flatm, encm
     # the proxy's retransmission check (proxy.py:90, 500-deep history) over the same 1M datagrams
     ms_x = time_loop(torch, lambda i: batch.detect_retransmissions(enc.frames, frame_off=enc.frame_off,
