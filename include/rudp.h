@@ -51,6 +51,7 @@ extern "C" {
 #define RUDP_OK_GOOD 1       /* checksum verified */
 #define RUDP_OK_SHORT 2      /* frame shorter than the header */
 #define RUDP_OK_UNVERIFIED 3 /* rudp5 decoded without a sideband checksum */
+#define RUDP_OK_BAD_OFFSETS 4 /* variable-length decode: frame_off[i] > frame_off[i+1] or past the buffer */
 
 /*
  * Status word of the sync-free variable-length calls (*_checked): written on
@@ -144,8 +145,10 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
 /*
  * Sync-free forms of the two variable-length calls: the argument checks of
  * rudp_varlen_bounds / rudp_frame_off_bounds run on the device inside the call
- * (folded into the offset scan for encode; two small launches before the
- * decode) and land in *d_status (RUDP_ST_*), so the host never waits.  The
+ * (folded into the offset scan for encode; inside the decode kernels, where
+ * every frame checks its own pair of offsets and a rejected frame gets
+ * d_ok = RUDP_OK_BAD_OFFSETS) and land in *d_status (RUDP_ST_*), so the host
+ * never waits.  The
  * caller reads d_status whenever it next synchronizes (the Python layer:
  * VarlenFrames.check() / DecodedBatch.check()).
  * rudp_encode_varlen_checked: payload_bytes = size of in->payload; frames_cap =

@@ -16,7 +16,7 @@ namespace rudp {
 int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t len_hint, uint64_t n,
                   const uint16_t* d_csum_in, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
                   uint8_t* d_ok, uint16_t* d_csum_out, uint8_t* d_payload_out, int layout,
-                  int device, void* hip_stream, const uint32_t* status = nullptr);
+                  int device, void* hip_stream, uint32_t* status_out = nullptr, uint64_t frames_lim = 0);
 namespace {
 
 thread_local std::string g_last_error;
@@ -306,7 +306,7 @@ uint32_t decode_group_log2(uint32_t L) {
 int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t len_hint, uint64_t n,
                   const uint16_t* d_csum_in, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
                   uint8_t* d_ok, uint16_t* d_csum_out, uint8_t* d_payload_out, int layout,
-                  int device, void* hip_stream, const uint32_t* status) {
+                  int device, void* hip_stream, uint32_t* status_out, uint64_t frames_lim) {
   if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
     return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
   if (d_payload_out)
@@ -360,7 +360,20 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
     a.tile_cap = cap <= 49152u ? (uint32_t)cap : 0u;
   }
   a.early_fo = tuning().varlen_early_fo ? 1u : 0u;
-  a.status = status;
+  // Small frames (payload hint under varlen_small bytes): tiles of 256 * fpt
+  // frames with the per-frame outputs lane-strided (decode_varlen_small_kernel).
+  {
+    const int small_hint = tuning().varlen_small;
+    if (small_hint > 0 && len_hint < (uint32_t)small_hint + (uint32_t)layout && tuning().varlen_vec) {
+      const int fpt = tuning().varlen_small_fpt;
+      a.small_fpt = (fpt == 1 || fpt == 2 || fpt == 8) ? (uint32_t)fpt : 4u;
+      const uint64_t T = (uint64_t)256u * a.small_fpt;
+      const uint64_t hint = len_hint ? len_hint : (uint64_t)layout + 1u;
+      a.small_cap = (uint32_t)((T * hint * 5u / 4u + 256u + 15u) & ~15ull);
+    }
+  }
+  a.status_out = status_out;
+  a.frames_lim = frames_lim;
   rc = launch_decode_varlen(a, layout, (hipStream_t)hip_stream);
   if (rc) return hip_fail((hipError_t)rc, "varlen decode launch");
   return 0;
@@ -501,8 +514,6 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
   int rc = dev_scope.set(device);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)hip_stream;
-  rc = scan_frame_offsets(in->len, in->n, (uint32_t)layout, d_frame_off, chk, s);
-  if (rc) return hip_fail((hipError_t)rc, "frame offset scan");
   VarlenArgs a{};
   a.payload = in->payload;
   a.len = in->len;
@@ -540,6 +551,22 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
   }
   a.early_fo = tuning().varlen_early_fo ? 1u : 0u;
   a.status = chk.status;
+  // Small frames (hints under varlen_small bytes, packed, aligned): the scan's
+  // last pass and the framing in one tile kernel (launch_encode_varlen_small).
+  const int small_hint = tuning().varlen_small;
+  if (small_hint > 0 && in->payload_len < (uint32_t)small_hint && !in->payload_off && tuning().varlen_vec &&
+      aligned16(in->payload) && aligned16(d_frames)) {
+    const int fpt = tuning().varlen_small_fpt;
+    a.small_fpt = (fpt == 1 || fpt == 2 || fpt == 8) ? (uint32_t)fpt : 4u;
+    const uint64_t T = (uint64_t)256u * a.small_fpt;
+    const uint64_t hint = in->payload_len ? in->payload_len : 1u;
+    a.small_cap = (uint32_t)((T * hint * 5u / 4u + 256u + 15u) & ~15ull);
+    rc = launch_encode_varlen_small(a, chk, layout, s);
+    if (rc) return hip_fail((hipError_t)rc, "small-frame varlen encode launch");
+    return 0;
+  }
+  rc = scan_frame_offsets(in->len, in->n, (uint32_t)layout, d_frame_off, chk, s);
+  if (rc) return hip_fail((hipError_t)rc, "frame offset scan");
   rc = launch_encode_varlen(a, layout, s);
   if (rc) return hip_fail((hipError_t)rc, "varlen encode launch");
   return 0;
@@ -580,15 +607,17 @@ int rudp_decode_varlen_checked(const uint8_t* d_frames, uint64_t frames_bytes, c
   if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
     return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
   {
+    // every frame checks its own pair of offsets inside the decode kernels
+    // (a valid batch is exactly one whose frames all pass); they or
+    // RUDP_ST_OFFSETS into the zeroed status word
     DeviceScope dev_scope;
     int rc = dev_scope.set(device);
     if (rc) return rc;
-    rc = check_frame_offsets(d_frame_off, n, frames_bytes, d_status, (hipStream_t)hip_stream);
-    if (rc) return hip_fail((hipError_t)rc, "frame offset check");
+    RUDP_HIP(hipMemsetAsync(d_status, 0, sizeof(uint32_t), (hipStream_t)hip_stream));
   }
   if (n == 0) return 0;
   return decode_varlen(d_frames, d_frame_off, len_hint, n, d_csum_in_or_null, d_seq, d_ack, d_flags, d_ok,
-                       d_csum_out_or_null, nullptr, layout, device, hip_stream, d_status);
+                       d_csum_out_or_null, nullptr, layout, device, hip_stream, d_status, frames_bytes);
 }
 
 int rudp_frame_off_check(const uint64_t* d_frame_off, uint64_t n, uint64_t frames_bytes, uint32_t* d_status,

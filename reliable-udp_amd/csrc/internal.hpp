@@ -98,6 +98,14 @@ struct VarlenArgs {
   // by an earlier kernel of the same call; every kernel returns without a
   // memory access past its own offsets when it is non-zero.  Null: unchecked.
   const uint32_t* status;
+  // Decode: frames reach at most frames_lim bytes into the buffer, and a frame
+  // whose offsets are decreasing or past it is rejected (ok = RUDP_OK_BAD_OFFSETS,
+  // RUDP_ST_OFFSETS or'ed into *status_out, nothing read).  status_out null:
+  // an unchecked caller, the limit is frame_off[n].
+  uint64_t frames_lim;
+  uint32_t* status_out;
+  uint32_t small_fpt;             // decode small-frame tile: frames per thread (0: not used)
+  uint32_t small_cap;             // its LDS run budget in bytes
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -229,6 +237,11 @@ struct Tuning {
   // 1031 B (3 tiles per CU at the 130% budget; varlen_decode_lanes.json).
   std::atomic<int> utf8_vtile_bytes{34816};
   std::atomic<int> varlen_scan{1};    // frame offsets: 1 = reduce-then-scan (scan.hip), 0 = hipcub
+  // Small-frame varlen encode (scan's last pass + framing in one tile kernel)
+  // for packed batches whose mean payload hint is under this many bytes (0: off),
+  // and its packets per thread (1, 2, 4, 8: tiles of 256 * fpt packets).
+  std::atomic<int> varlen_small{16};
+  std::atomic<int> varlen_small_fpt{4};
   std::atomic<int> host_slots{3};     // *_host pipeline: device staging slots (2..8)
   std::atomic<int> host_stage_mb{128};  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
 };
@@ -269,6 +282,17 @@ struct ScanCheck {
   uint64_t frames_cap;          // capacity of the frame buffer
   uint32_t* status;             // written once: RUDP_ST_* bits, 0 = valid
 };
+// The scan's first two passes alone (scan.hip): block sums of len + H over
+// blocks of kBlock * items packets (items 1, 2, 4 or 8; with the ScanCheck's
+// bits), then the exclusive block bases in place, frame_off[n] and the status.
+void scan_block_sums(const uint32_t* d_len, uint64_t n, uint32_t H, uint32_t items, uint64_t* sums,
+                     const ScanCheck& chk, hipStream_t stream);
+void scan_block_bases(uint64_t* sums, uint64_t nb, uint64_t* d_frame_off, uint64_t n, uint32_t H,
+                      const ScanCheck& chk, hipStream_t stream);
+// Small-frame varlen encode of packed payloads (varlen.hip): the scan's first
+// two passes, then one kernel per tile of kBlock * fpt packets that writes the
+// tile's offsets and assembles its frames in LDS.
+int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int layout, hipStream_t stream);
 int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
                              const ScanCheck& chk, hipStream_t stream);
 int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,

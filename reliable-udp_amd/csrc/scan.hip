@@ -18,6 +18,7 @@
 // total and writes the status word every later kernel of the call reads.
 #include "codec_device.hpp"
 #include "internal.hpp"
+#include "scan_device.hpp"
 
 namespace rudp {
 
@@ -29,17 +30,20 @@ constexpr uint32_t kScanBlockItems = kBlock * kScanItems;  // 2048 per block
 constexpr int kSumBitsShift = 56;
 constexpr uint64_t kSumMask = (1ull << kSumBitsShift) - 1ull;
 
+// ITEMS packets per thread: a block sums kBlock * ITEMS lengths (8 for the
+// offset scan; the small-frame encode uses its own tile size).
+template <uint32_t ITEMS>
 __global__ void __launch_bounds__(kBlock) scan_block_sums_kernel(const uint32_t* len, uint64_t n,
                                                                  uint32_t H, uint64_t* sums,
                                                                  ScanCheck chk) {
   __shared__ uint64_t s_wave[kBlock / 64];
   __shared__ uint32_t s_bits;
   if (threadIdx.x == 0) s_bits = 0;
-  const uint64_t base = (uint64_t)blockIdx.x * kScanBlockItems;
+  const uint64_t base = (uint64_t)blockIdx.x * (kBlock * ITEMS);
   uint64_t acc = 0;
   uint32_t bits = 0;
 #pragma unroll
-  for (uint32_t j = 0; j < kScanItems; ++j) {
+  for (uint32_t j = 0; j < ITEMS; ++j) {
     const uint64_t i = base + j * kBlock + threadIdx.x;
     if (i < n) {
       const uint32_t l = len[i];
@@ -64,27 +68,6 @@ __global__ void __launch_bounds__(kBlock) scan_block_sums_kernel(const uint32_t*
     for (uint32_t w = 0; w < kBlock / 64; ++w) t += s_wave[w];
     sums[blockIdx.x] = t | ((uint64_t)s_bits << kSumBitsShift);
   }
-}
-
-// Exclusive scan of one u64 per thread over the block (all threads call it).
-__device__ uint64_t block_exclusive_scan(uint64_t x, uint64_t* total, uint64_t* s_wave) {
-  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
-  uint64_t incl = x;
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint64_t y = __shfl_up(incl, d, 64);
-    if (lane >= d) incl += y;
-  }
-  if (lane == 63) s_wave[wave] = incl;
-  __syncthreads();
-  uint64_t before = 0, all = 0;
-  for (uint32_t w = 0; w < nwaves; ++w) {
-    const uint64_t v = s_wave[w];
-    before += w < wave ? v : 0;
-    all += v;
-  }
-  __syncthreads();  // s_wave may be reused by the caller
-  *total = all;
-  return before + incl - x;
 }
 
 // One workgroup of 1024 threads: sums[b] <- sum_{c<b} sums[c]; frame_off[n] <- total;
@@ -156,16 +139,31 @@ __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len,
   }
 }
 
+void scan_block_sums(const uint32_t* d_len, uint64_t n, uint32_t H, uint32_t items, uint64_t* sums,
+                     const ScanCheck& chk, hipStream_t stream) {
+  const uint64_t nb = (n + kBlock * items - 1) / (kBlock * items);
+  const dim3 grid((uint32_t)nb), block(kBlock);
+  switch (items) {
+    case 1: hipLaunchKernelGGL(scan_block_sums_kernel<1>, grid, block, 0, stream, d_len, n, H, sums, chk); break;
+    case 2: hipLaunchKernelGGL(scan_block_sums_kernel<2>, grid, block, 0, stream, d_len, n, H, sums, chk); break;
+    case 4: hipLaunchKernelGGL(scan_block_sums_kernel<4>, grid, block, 0, stream, d_len, n, H, sums, chk); break;
+    default: hipLaunchKernelGGL(scan_block_sums_kernel<8>, grid, block, 0, stream, d_len, n, H, sums, chk);
+  }
+}
+
+void scan_block_bases(uint64_t* sums, uint64_t nb, uint64_t* d_frame_off, uint64_t n, uint32_t H,
+                      const ScanCheck& chk, hipStream_t stream) {
+  hipLaunchKernelGGL(scan_block_bases_kernel, dim3(1), dim3(1024), 0, stream, sums, nb, d_frame_off, n, H, chk);
+}
+
 int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
                              const ScanCheck& chk, hipStream_t stream) {
   const uint64_t nb = (n + kScanBlockItems - 1) / kScanBlockItems;
   uint64_t* sums = nullptr;
   hipError_t e = stream_alloc(reinterpret_cast<void**>(&sums), nb * sizeof(uint64_t), stream);
   if (e != hipSuccess) return (int)e;
-  hipLaunchKernelGGL(scan_block_sums_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, stream, d_len, n, H, sums,
-                     chk);
-  hipLaunchKernelGGL(scan_block_bases_kernel, dim3(1), dim3(1024), 0, stream, sums, nb, d_frame_off, n, H,
-                     chk);
+  scan_block_sums(d_len, n, H, kScanItems, sums, chk, stream);
+  scan_block_bases(sums, nb, d_frame_off, n, H, chk, stream);
   hipLaunchKernelGGL(scan_apply_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, stream, d_len, n, H, sums,
                      d_frame_off);
   e = hipGetLastError();

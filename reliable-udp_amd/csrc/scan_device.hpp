@@ -1,0 +1,30 @@
+// Block-wide scan shared by the offset scan (scan.hip) and the small-frame
+// varlen encode, which folds the scan's last pass into its own tile (varlen.hip).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace rudp {
+
+// Exclusive scan of one u64 per thread over the block (all threads call it).
+__device__ inline uint64_t block_exclusive_scan(uint64_t x, uint64_t* total, uint64_t* s_wave) {
+  const uint32_t lane = threadIdx.x & 63u, wave = threadIdx.x >> 6, nwaves = blockDim.x >> 6;
+  uint64_t incl = x;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint64_t y = __shfl_up(incl, d, 64);
+    if (lane >= d) incl += y;
+  }
+  if (lane == 63) s_wave[wave] = incl;
+  __syncthreads();
+  uint64_t before = 0, all = 0;
+  for (uint32_t w = 0; w < nwaves; ++w) {
+    const uint64_t v = s_wave[w];
+    before += w < wave ? v : 0;
+    all += v;
+  }
+  __syncthreads();  // s_wave may be reused by the caller
+  *total = all;
+  return before + incl - x;
+}
+
+}  // namespace rudp

@@ -255,7 +255,10 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // stage ablation (diagnostic); 36: varlen encode tile prebuilt header chunks;
 // 37: encode header chunks through an LDS scratch; 38: varlen decode tile LDS budget (%);
 // 39: varlen encode tile LDS budget (%); 40: decode tiles per CU cap; 41: packed-frame
-// UTF-8 validation through LDS tiles; 42: its LDS budget (%).
+// UTF-8 validation through LDS tiles; 42: its LDS budget (%); 43: varlen tile
+// offsets before phase 1; 44: varlen encode tile waves per SIMD; 45: packed UTF-8
+// tile bytes; 46: small-frame varlen encode below this hint (0 = off); 47: its
+// packets per thread.
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
@@ -284,7 +287,9 @@ int rudpx_tune(int key, int value) {
             : key == 42 ? &t.utf8_vtile_cap_pct
             : key == 43 ? &t.varlen_early_fo
             : key == 44 ? &t.varlen_waves
-            : key == 45 ? &t.utf8_vtile_bytes : nullptr;
+            : key == 45 ? &t.utf8_vtile_bytes
+            : key == 46 ? &t.varlen_small
+            : key == 47 ? &t.varlen_small_fpt : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }

@@ -19,6 +19,7 @@
 
 #include "codec_device.hpp"
 #include "internal.hpp"
+#include "scan_device.hpp"
 
 namespace rudp {
 
@@ -117,12 +118,13 @@ __device__ __forceinline__ void store_owned(unsigned char* dst, int b_lo, int b_
 // holding header bytes wait for the group's sum; they are rebuilt and
 // written after the shfl reduction.
 // G = 2^glog lanes (g = 0..G-1, one aligned group of a wave) encode packet p.
+// fo_in: the frame's offset when the caller already has it (~0: read frame_off).
 template <int H>
 __device__ __forceinline__ void encode_varlen_packet(const VarlenArgs& a, uint64_t p, bool valid, uint32_t g,
-                                                     uint32_t glog) {
+                                                     uint32_t glog, uint64_t fo_in = ~0ull) {
   const uint32_t G = 1u << glog;
   const uint32_t L = valid ? a.len[p] : 0u;
-  const uint64_t fo = valid ? a.frame_off[p] : 0;
+  const uint64_t fo = valid ? (fo_in != ~0ull ? fo_in : a.frame_off[p]) : 0;
   const uint64_t po = valid ? (a.payload_off ? a.payload_off[p] : fo - p * (uint64_t)H) : 0;
   const uint64_t pend = po + L;
   const uint32_t F = L + H;
@@ -501,17 +503,35 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   }
 }
 
+// Byte limit of a decode's frames: the caller's buffer size for checked
+// calls, else (unchecked callers) the last offset.
+__device__ __forceinline__ uint64_t frames_limit(const VarlenArgs& a) {
+  return a.status_out ? a.frames_lim : a.frame_off[a.n];
+}
+
+// A frame whose offsets are invalid: no byte of it is read.
+__device__ __forceinline__ void decode_varlen_reject(const VarlenArgs& a, uint64_t p) {
+  a.seq[p] = 0;
+  a.ack[p] = 0;
+  a.flags[p] = 0;
+  a.ok[p] = RUDP_OK_BAD_OFFSETS;
+  if (a.csum_out) a.csum_out[p] = 0;
+  if (a.status_out) atomicOr(a.status_out, RUDP_ST_OFFSETS);
+}
+
 template <int H>
 __global__ void __launch_bounds__(kBlock) decode_varlen_kernel(VarlenArgs a) {
-  if (call_failed(a.status)) return;
   const uint32_t g = threadIdx.x & (kVarLanes - 1u);
   const uint64_t p = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / kVarLanes;
   const bool valid = p < a.n;
   uint32_t sum = 0, F = 0;
   uint64_t fo = 0;
+  bool bad = false;
   if (valid) {
     fo = a.frame_off[p];
-    F = (uint32_t)(a.frame_off[p + 1] - fo);
+    const uint64_t fe = a.frame_off[p + 1];
+    bad = fo > fe || fe > frames_limit(a);
+    F = bad ? 0u : (uint32_t)(fe - fo);
     for (uint32_t j = (uint32_t)H + g; j < F; j += kVarLanes) {
       const uint32_t b = a.frames[fo + j];
       sum += ((j - H) & 1u) ? (b << 8) : b;
@@ -519,6 +539,10 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_kernel(VarlenArgs a) {
   }
   for (uint32_t m = kVarLanes >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
   if (valid && g == 0) {
+    if (bad) {
+      decode_varlen_reject(a, p);
+      return;
+    }
     uint32_t b[7] = {0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (uint32_t i = 0; i < 7; ++i)
@@ -595,9 +619,11 @@ __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_
                                                     uint32_t glog) {
   const uint32_t tid = threadIdx.x;
   const uint32_t G = 1u << glog;
-  const uint64_t total = a.frame_off[a.n];
-  const uint64_t fstart = valid ? a.frame_off[p] : 0;
-  const uint64_t fend = valid ? a.frame_off[p + 1] : 0;
+  const uint64_t total = frames_limit(a);
+  uint64_t fstart = valid ? a.frame_off[p] : 0;
+  uint64_t fend = valid ? a.frame_off[p + 1] : 0;
+  const bool bad = valid && (fstart > fend || fend > total);
+  if (bad) fstart = fend = 0;  // nothing of it is read
   const uint64_t c_lo = fstart >> 4;
   const uint32_t nchunks = fend > fstart ? (uint32_t)(((fend - 1) >> 4) - c_lo + 1) : 0u;
 
@@ -640,12 +666,15 @@ __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_
   next.z = __shfl(first.z, src, 64);
   next.w = __shfl(first.w, src, 64);
   if (g != 0 || !valid) return;
+  if (bad) {
+    decode_varlen_reject(a, p);
+    return;
+  }
   decode_varlen_finish<H>(a, p, (uint32_t)(fend - fstart), sum, funnel32(first, next, (uint32_t)(fstart & 15u)));
 }
 
 template <int H>
 __global__ void __launch_bounds__(kBlock) decode_varlen_vec_kernel(VarlenArgs a) {
-  if (call_failed(a.status)) return;
   const uint32_t glog = a.glog;
   const uint64_t p = (uint64_t)blockIdx.x * (kBlock >> glog) + (threadIdx.x >> glog);
   decode_varlen_frame<H>(a, p, p < a.n, threadIdx.x & ((1u << glog) - 1u), glog);
@@ -672,17 +701,18 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
   const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
-  if (call_failed(a.status)) return;
+  const uint64_t total = frames_limit(a);
   const uint64_t A = fo0 & ~15ull;
-  const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
-  if (run > a.tile_cap) {  // uniform over the workgroup
+  const uint64_t run = ((fo_end + 15u) & ~15ull) - A;  // fo_end < fo0 wraps: far over the cap
+  if (run > a.tile_cap || fo_end > total) {  // uniform over the workgroup
     decode_varlen_frame<H>(a, p0 + q, q < Tv, g, glog);
     return;
   }
+  // tile-relative offsets; one outside the run reads as 0xFFFFFFFF (its frames are rejected)
+  auto rel = [&](uint64_t o) { return o - A <= run ? (uint32_t)(o - A) : 0xFFFFFFFFu; };
   {
     // T = 256 / G <= 128 frames: one offset per lane, loaded before the run (early_fo)
-    const uint32_t fo_r = a.early_fo && tid <= Tv ? (uint32_t)(a.frame_off[p0 + tid] - A) : 0u;
-    const uint64_t total = a.frame_off[a.n];
+    const uint32_t fo_r = a.early_fo && tid <= Tv ? rel(a.frame_off[p0 + tid]) : 0u;
     const uint32_t nvec = (uint32_t)(run >> 4);
     u32x4* dst = reinterpret_cast<u32x4*>(img);
     constexpr uint32_t P = 8;
@@ -702,11 +732,18 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
     if (a.early_fo) {
       if (tid <= Tv) lds_fo[tid] = fo_r;
     } else {
-      for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = (uint32_t)(a.frame_off[p0 + i] - A);
+      for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = rel(a.frame_off[p0 + i]);
     }
   }
   __syncthreads();
   if (q >= Tv) return;
+  {
+    const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
+    if (fs > fe || fe > (uint32_t)(fo_end - A)) {  // uniform over the frame's lanes
+      if (g == 0) decode_varlen_reject(a, p0 + q);
+      return;
+    }
+  }
   const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
   const u32x4* img16 = reinterpret_cast<const u32x4*>(img);
   uint32_t even_sum = 0, odd_sum = 0;  // byte sums at even / odd offsets (A is even)
@@ -1050,6 +1087,325 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_vtile_kernel(Utf8Args a)
   if (g == 0 && q < Tv) a.valid[p0 + q] = bad ? 0 : 1;
 }
 
+// ---- small frames (the reference's 1-character datagrams) ------------------
+// Packed payloads with a mean length hint under kSmallHint bytes: frames of
+// 5-20 bytes share every aligned 16-B chunk with their neighbours, so the
+// per-packet vector kernel writes them bytewise, and the offset scan's last
+// pass plus the encode launch re-read the offsets.  Here one kernel per tile
+// of T = 256 * FPT packets does the scan's last pass and the framing:
+//   loads    the tile's lengths and header table (coalesced), and its packed
+//            payload run [fo0 - p0*H, fo_end - (p0+T)*H) into LDS, where fo0 /
+//            fo_end are the scan's block bases (passes 1-2 ran over the same
+//            tiles);
+//   scan     lengths -> tile-relative frame offsets (block scan), written to
+//            frame_off with coalesced stores;
+//   frames   each thread builds its FPT consecutive frames in an LDS image of
+//            the tile's output run (header word + payload bytes, LE16 sums on
+//            the way), then the block stores the run as aligned 16-B vectors
+//            (only the two edge chunks, shared with the neighbour tiles, bytewise).
+// A tile whose run outgrows the LDS budget (a burst far above the hint)
+// encodes its packets with the per-packet vector path inside the launch.
+constexpr uint32_t kSmallHint = 16;
+
+__host__ __device__ inline uint32_t small_lds_off_seq(uint32_t T) { return ((8u * T + 4u + 15u) & ~15u); }
+__host__ __device__ inline uint32_t small_lds_off_pay(uint32_t T) {
+  return small_lds_off_seq(T) + ((7u * T + 15u) & ~15u);  // seq u16, ack u16, flags u8, csum u16
+}
+__host__ __device__ inline uint32_t small_lds_off_out(uint32_t T, uint32_t cap) {
+  return small_lds_off_pay(T) + cap + 32u;
+}
+__host__ __device__ inline uint32_t small_out_cap(uint32_t T, uint32_t cap, uint32_t H) { return cap + T * H + 16u; }
+
+template <int H, uint32_t FPT>
+__global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs a, const uint64_t* bases) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  constexpr uint32_t T = kBlock * FPT;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t cap = a.small_cap;
+  uint32_t* s_len = reinterpret_cast<uint32_t*>(lds);        // [T]
+  uint32_t* s_off = s_len + T;                               // [T + 1], tile-relative
+  uint16_t* s_seq = reinterpret_cast<uint16_t*>(lds + small_lds_off_seq(T));
+  uint16_t* s_ack = s_seq + T;
+  uint16_t* s_cs = s_ack + T;
+  uint8_t* s_flags = reinterpret_cast<uint8_t*>(s_cs + T);
+  unsigned char* pay = lds + small_lds_off_pay(T);
+  unsigned char* img = lds + small_lds_off_out(T, cap);
+
+  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  const uint32_t Tv = a.n - p0 < T ? (uint32_t)(a.n - p0) : T;
+  const uint64_t fo0 = bases[blockIdx.x];
+  const uint64_t fo_end = p0 + T < a.n ? bases[blockIdx.x + 1] : a.frame_off[a.n];
+  if (call_failed(a.status)) return;
+  const uint64_t po0 = fo0 - p0 * (uint64_t)H, po_end = fo_end - (p0 + Tv) * (uint64_t)H;
+  const uint64_t A = po0 & ~15ull, OA = fo0 & ~15ull;
+  const uint64_t prun = ((po_end + 15u) & ~15ull) - A;
+  const uint64_t orun = ((fo_end + 15u) & ~15ull) - OA;
+  const bool fits = prun <= cap && orun <= small_out_cap(T, cap, H);
+
+  // ---- loads: lengths, header table, payload run ---------------------------
+  {
+    uint32_t lv[FPT], sq[FPT], ak[FPT], fl[FPT];
+#pragma unroll
+    for (uint32_t j = 0; j < FPT; ++j) {
+      const uint32_t q = j * kBlock + tid;
+      lv[j] = sq[j] = ak[j] = fl[j] = 0;
+      if (q < Tv) {
+        lv[j] = a.len[p0 + q];
+        if (fits) {
+          sq[j] = a.seq_in[p0 + q];
+          ak[j] = a.ack_in[p0 + q];
+          fl[j] = a.flags_in[p0 + q];
+        }
+      }
+    }
+    if (fits) {
+      const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + A);
+      u32x4* dst = reinterpret_cast<u32x4*>(pay);
+      const uint32_t nvec = (uint32_t)(prun >> 4);
+      for (uint32_t v0 = tid; v0 < nvec; v0 += 4u * kBlock) {
+        u32x4 r[4];
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u)
+          if (v0 + u * kBlock < nvec) r[u] = __builtin_nontemporal_load(src + v0 + u * kBlock);
+#pragma unroll
+        for (uint32_t u = 0; u < 4; ++u)
+          if (v0 + u * kBlock < nvec) dst[v0 + u * kBlock] = r[u];
+      }
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < FPT; ++j) {
+      const uint32_t q = j * kBlock + tid;
+      s_len[q] = lv[j];
+      s_seq[q] = (uint16_t)sq[j];
+      s_ack[q] = (uint16_t)ak[j];
+      s_flags[q] = (uint8_t)fl[j];
+    }
+  }
+  __syncthreads();
+
+  // ---- the scan's last pass: tile-relative offsets, frame_off ---------------
+  __shared__ uint64_t s_wave[kBlock / 64];
+  {
+    uint32_t mine = 0;
+#pragma unroll
+    for (uint32_t i = 0; i < FPT; ++i) {
+      const uint32_t q = tid * FPT + i;
+      mine += q < Tv ? s_len[q] + (uint32_t)H : 0u;
+    }
+    uint64_t total = 0;
+    uint32_t run = (uint32_t)block_exclusive_scan(mine, &total, s_wave);
+#pragma unroll
+    for (uint32_t i = 0; i < FPT; ++i) {
+      const uint32_t q = tid * FPT + i;
+      s_off[q] = run;
+      run += q < Tv ? s_len[q] + (uint32_t)H : 0u;
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (uint32_t j = 0; j < FPT; ++j) {
+    const uint32_t q = j * kBlock + tid;
+    if (q < Tv) const_cast<uint64_t*>(a.frame_off)[p0 + q] = fo0 + s_off[q];
+  }
+  if (!fits) {  // uniform: per-packet vector path, offsets from LDS
+#pragma unroll
+    for (uint32_t j = 0; j < FPT; ++j) {
+      const uint32_t q = j * kBlock + tid;
+      encode_varlen_packet<H>(a, p0 + q, q < Tv, 0u, 0u, q < Tv ? fo0 + s_off[q] : 0ull);
+    }
+    return;
+  }
+
+  // ---- frames into the LDS image of the output run ---------------------------
+  const uint32_t lead = (uint32_t)(fo0 - OA);   // output bytes before fo0 in the first chunk
+  const uint32_t pshift = (uint32_t)(po0 - A);  // LDS offset of payload byte po0
+#pragma unroll
+  for (uint32_t i = 0; i < FPT; ++i) {
+    const uint32_t q = tid * FPT + i;
+    if (q < Tv) {
+      const uint32_t Lq = s_len[q], fs = s_off[q];
+      const unsigned char* src = pay + pshift + fs - q * (uint32_t)H;
+      unsigned char* dst = img + lead + fs;
+      uint32_t sum = 0;
+      for (uint32_t j = 0; j < Lq; ++j) {
+        const uint32_t b = src[j];
+        sum += (j & 1u) ? (b << 8) : b;  // LE16 words: payload sits at an odd frame offset
+        dst[H + j] = (unsigned char)b;
+      }
+      const uint32_t sq = s_seq[q], ak = s_ack[q], fl = s_flags[q];
+      const uint32_t c = packet_csum(sum, sq, ak, fl);
+      const uint64_t h = pack_header<H>(sq, ak, fl, c);
+#pragma unroll
+      for (int k = 0; k < H; ++k) dst[k] = (unsigned char)(h >> (8 * k));
+      s_cs[q] = (uint16_t)c;
+    }
+  }
+  __syncthreads();
+  if (a.csum) {
+#pragma unroll
+    for (uint32_t j = 0; j < FPT; ++j) {
+      const uint32_t q = j * kBlock + tid;
+      if (q < Tv) a.csum[p0 + q] = s_cs[q];
+    }
+  }
+  // ---- the output run: aligned 16-B vectors, edge chunks bytewise ------------
+  const uint32_t end = (uint32_t)(fo_end - OA);
+  const uint32_t nch = (uint32_t)(orun >> 4);
+  const u32x4* img16 = reinterpret_cast<const u32x4*>(img);
+  unsigned char* out = a.frames + OA;
+  for (uint32_t c = tid; c < nch; c += kBlock) {
+    const uint32_t X = c << 4;
+    if (X >= lead && X + 16u <= end) {
+      __builtin_nontemporal_store(img16[c], reinterpret_cast<u32x4*>(out + X));
+    } else {
+      const uint32_t lo = X > lead ? X : lead, hi = X + 16u < end ? X + 16u : end;
+      for (uint32_t b = lo; b < hi; ++b) out[b] = img[b];
+    }
+  }
+}
+
+template <int H, uint32_t FPT>
+int launch_small_fpt(const VarlenArgs& args, const uint64_t* bases, uint64_t nb, hipStream_t stream) {
+  constexpr uint32_t T = kBlock * FPT;
+  const size_t lds = small_lds_off_out(T, args.small_cap) + small_out_cap(T, args.small_cap, H) + 32u;
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL((encode_varlen_small_kernel<H, FPT>), dim3((uint32_t)nb), dim3(kBlock), lds, stream, args,
+                     bases);
+  return (int)hipGetLastError();
+}
+
+int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int layout, hipStream_t stream) {
+  if (args.n == 0) return 0;
+  const uint32_t fpt = args.small_fpt;
+  const uint64_t T = (uint64_t)kBlock * fpt;
+  const uint64_t nb = (args.n + T - 1) / T;
+  uint64_t* sums = nullptr;
+  hipError_t e = stream_alloc(reinterpret_cast<void**>(&sums), nb * sizeof(uint64_t), stream);
+  if (e != hipSuccess) return (int)e;
+  scan_block_sums(args.len, args.n, (uint32_t)layout, fpt, sums, chk, stream);
+  scan_block_bases(sums, nb, const_cast<uint64_t*>(args.frame_off), args.n, (uint32_t)layout, chk, stream);
+  int rc;
+  if (layout == 7)
+    rc = fpt == 1 ? launch_small_fpt<7, 1>(args, sums, nb, stream)
+       : fpt == 2 ? launch_small_fpt<7, 2>(args, sums, nb, stream)
+       : fpt == 4 ? launch_small_fpt<7, 4>(args, sums, nb, stream) : launch_small_fpt<7, 8>(args, sums, nb, stream);
+  else
+    rc = fpt == 1 ? launch_small_fpt<5, 1>(args, sums, nb, stream)
+       : fpt == 2 ? launch_small_fpt<5, 2>(args, sums, nb, stream)
+       : fpt == 4 ? launch_small_fpt<5, 4>(args, sums, nb, stream) : launch_small_fpt<5, 8>(args, sums, nb, stream);
+  e = stream_free(sums, stream);
+  return rc ? rc : (int)e;
+}
+
+// Small-frame decode: a tile of T = 256 * FPT consecutive frames (the
+// reference's 6-9 B datagrams) is one contiguous run; its offsets and the run
+// stream into LDS, then each lane parses FPT frames (lane-strided, so the
+// per-frame outputs leave as coalesced stores), summing a frame's LDS dwords
+// by address parity.  A run over the LDS budget decodes per frame (G = 1).
+template <int H, uint32_t FPT>
+__global__ void __launch_bounds__(kBlock) decode_varlen_small_kernel(VarlenArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  constexpr uint32_t T = kBlock * FPT;
+  const uint32_t tid = threadIdx.x;
+  uint32_t* s_fo = reinterpret_cast<uint32_t*>(lds);                    // [T + 1]
+  unsigned char* img = lds + ((4u * (T + 1u) + 15u) & ~15u);            // the run, then a guard
+  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  const uint32_t Tv = a.n - p0 < T ? (uint32_t)(a.n - p0) : T;
+  const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
+  const uint64_t total = frames_limit(a);
+  const uint64_t A = fo0 & ~15ull;
+  const uint64_t run = ((fo_end + 15u) & ~15ull) - A;  // fo_end < fo0 wraps: far over the cap
+  if (run > a.small_cap || fo_end > total) {  // uniform: per-frame path, one lane each
+#pragma unroll
+    for (uint32_t j = 0; j < FPT; ++j) {
+      const uint32_t q = j * kBlock + tid;
+      decode_varlen_frame<H>(a, p0 + q, q < Tv, 0u, 0u);
+    }
+    return;
+  }
+  {
+    uint32_t fo_r[FPT], fo_last = 0;
+#pragma unroll
+    for (uint32_t j = 0; j < FPT; ++j) {
+      const uint32_t q = j * kBlock + tid;
+      const uint64_t o = q <= Tv ? a.frame_off[p0 + q] : A;
+      fo_r[j] = o - A <= run ? (uint32_t)(o - A) : 0xFFFFFFFFu;  // outside the run: its frames are rejected
+    }
+    if (tid == 0) fo_last = (uint32_t)(fo_end - A);
+    const uint32_t nvec = (uint32_t)(run >> 4);
+    u32x4* dst = reinterpret_cast<u32x4*>(img);
+    for (uint32_t v0 = tid; v0 < nvec; v0 += 4u * kBlock) {
+      u32x4 r[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u)
+        if (v0 + u * kBlock < nvec) r[u] = load16_guarded(a.frames, A + 16ull * (v0 + u * kBlock), total);
+#pragma unroll
+      for (uint32_t u = 0; u < 4; ++u)
+        if (v0 + u * kBlock < nvec) dst[v0 + u * kBlock] = r[u];
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < FPT; ++j) s_fo[j * kBlock + tid] = fo_r[j];
+    if (tid == 0) s_fo[Tv] = fo_last;
+  }
+  __syncthreads();
+  const uint32_t* dw = reinterpret_cast<const uint32_t*>(img);
+  const uint32_t lim = (uint32_t)(fo_end - A);
+#pragma unroll
+  for (uint32_t j = 0; j < FPT; ++j) {
+    const uint32_t q = j * kBlock + tid;
+    if (q >= Tv) continue;
+    const uint32_t fs = s_fo[q], fe = s_fo[q + 1];
+    if (fs > fe || fe > lim) {
+      decode_varlen_reject(a, p0 + q);
+      continue;
+    }
+    uint32_t ev = 0, od = 0;  // byte sums at even / odd offsets (A is even)
+    if (fe > fs) {
+      const uint32_t w0 = fs >> 2, w1 = (fe - 1u) >> 2;
+      for (uint32_t w = w0; w <= w1; ++w) {
+        uint32_t v = dw[w];
+        if (w == w0 || w == w1) {  // keep this frame's bytes only
+          const int lo = (int)fs - (int)(4u * w), hi = (int)fe - (int)(4u * w);
+          v &= (uint32_t)byte_mask(lo, hi < 4 ? hi : 4);
+        }
+        ev += (v & 0xFFu) + ((v >> 16) & 0xFFu);
+        od += ((v >> 8) & 0xFFu) + (v >> 24);
+      }
+    }
+    const uint32_t sum = (fs & 1u) ? (ev + (od << 8)) : ((ev << 8) + od);
+    decode_varlen_finish<H>(a, p0 + q, fe - fs, sum, window16_dw(dw, fs));
+  }
+}
+
+template <int H, uint32_t FPT>
+int launch_decode_small_fpt(const VarlenArgs& args, hipStream_t stream) {
+  constexpr uint32_t T = kBlock * FPT;
+  const size_t lds = ((4u * (T + 1u) + 15u) & ~15u) + (size_t)args.small_cap + 32u;
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_varlen_small_kernel<H, FPT>),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  const uint64_t blocks = (args.n + T - 1) / T;
+  hipLaunchKernelGGL((decode_varlen_small_kernel<H, FPT>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream,
+                     args);
+  return (int)hipGetLastError();
+}
+
+template <int H>
+int launch_decode_small(const VarlenArgs& args, hipStream_t stream) {
+  switch (args.small_fpt) {
+    case 1: return launch_decode_small_fpt<H, 1>(args, stream);
+    case 2: return launch_decode_small_fpt<H, 2>(args, stream);
+    case 8: return launch_decode_small_fpt<H, 8>(args, stream);
+    default: return launch_decode_small_fpt<H, 4>(args, stream);
+  }
+}
+
 template <int H, int W>
 int launch_varlen_tile_w(const VarlenArgs& args, size_t lds, uint64_t blocks, hipStream_t stream) {
   if (lds > 65536) {
@@ -1150,6 +1506,8 @@ int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream)
 
 int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream) {
   if (args.n == 0) return 0;
+  if (args.small_fpt && args.glog != kNoVec && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0)
+    return layout == 7 ? launch_decode_small<7>(args, stream) : launch_decode_small<5>(args, stream);
   if (args.glog != kNoVec && args.tile_cap && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0) {
     const uint32_t T = kBlock >> args.glog;
     const size_t lds = ((((T + 1u) * 4u) + 15u) & ~15u) + kVTGuard + args.tile_cap + 32u;

@@ -759,3 +759,52 @@ def test_socket_ring_overlapped_decode_side_stream(cuda, slots):
     assert i0 == n
     rx.close()
     tx.close()
+
+
+@pytest.mark.parametrize("fpt", [1, 2, 4, 8])
+def test_small_frame_tiles_vs_oracle(cuda, fpt):
+    """Small-frame varlen encode (scan's last pass + framing in one tile kernel)
+    and decode tiles, every tile size: tiles that fit, tiles with a burst past
+    the LDS budget (per-packet path), ragged last tiles, both layouts."""
+    import ctypes
+    import torch
+    from rudp import _native
+    lib = _native.lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    rng = np.random.default_rng(70 + fpt)
+    for n, lo, hi, burst in ((1, 0, 3, False), (255, 1, 1, False), (256 * fpt + 3, 0, 9, False),
+                             (5 * 256 * fpt - 1, 1, 4, True), (40000, 0, 15, True)):
+        lens = rng.integers(lo, hi + 1, n).astype(np.int32)
+        if burst:
+            lens[n // 3] = 9000  # far past the tile's budget at these hints
+        pay = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+        seq, ack, flags, _ = synth.synth(fpt * 1000 + n, 0, n, 0)
+        pays = split_by_lengths(pay, lens)[0]
+        for layout in (5, 7):
+            want, off, cs = codec_np.encode_varlen(seq, ack, flags, pays, layout)
+            results = []
+            for small in (16, 0):  # the small-frame kernels, then the vector kernels
+                old = (lib.rudpx_tune(46, small), lib.rudpx_tune(47, fpt))
+                try:
+                    r = batch.pack_batch_varlen((dev(seq, cuda), dev(ack, cuda), dev(flags, cuda)), dev(pay, cuda),
+                                                dev(lens, cuda), layout, want_csum=True, check=False).check()
+                    d = batch.unpack_batch_varlen(r.frames, r.frame_off, layout,
+                                                  csum=r.csum if layout == 5 else None, check=False).check()
+                    bad_off = r.frame_off.clone()
+                    if n > 2:
+                        bad_off[n // 2] = bad_off[n // 2 + 1] + 1  # one decreasing pair
+                        db = batch.unpack_batch_varlen(r.frames, bad_off, layout, check=False)
+                        assert int(db.status.item()) == _native.ST_OFFSETS
+                        okb = host(db.ok)
+                        assert okb[n // 2 - 1] == 4 or okb[n // 2] == 4
+                finally:
+                    lib.rudpx_tune(46, old[0])
+                    lib.rudpx_tune(47, old[1])
+                ctx = (fpt, n, layout, small)
+                assert np.array_equal(host(r.frames), want), ctx
+                assert np.array_equal(host(r.frame_off), off) and np.array_equal(host(r.csum), cs), ctx
+                exp = codec_np.decode_varlen(want, off, layout, cs if layout == 5 else None)
+                for g, e in zip((d.seq, d.ack, d.flags, d.ok, d.csum), exp):
+                    assert np.array_equal(host(g), e), ctx
+                results.append(host(r.frames))
+            assert np.array_equal(results[0], results[1])
