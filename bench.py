@@ -80,7 +80,24 @@ def cpu_baseline(L: int, per_worker: int, workers: int):
         "single_core_us_per_packet": single[1] / max(per_worker // 4, 256) * 1e6,
         "cpu_model": _cpu_model(),
         "os_cpu_count": os.cpu_count(),
+        "cpu_share": usable_cpus(),
+        "workers_note": "one worker per usable CPU (affinity mask / cgroup quota): os.cpu_count() "
+                        "counts the whole host, of which this job may use only its share",
     }
+
+
+def usable_cpus() -> dict:
+    """CPUs this process may actually run on: the affinity mask, capped by a
+    cgroup CPU quota when there is one (os.cpu_count() reports the whole host)."""
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    quota = None
+    try:
+        q, period = open("/sys/fs/cgroup/cpu.max").read().split()
+        if q != "max":
+            quota = max(1, int(int(q) / int(period)))
+    except (OSError, ValueError):
+        pass
+    return {"affinity": aff, "cgroup_quota": quota, "usable": min(aff, quota) if quota else aff}
 
 
 def _cpu_model() -> str:
@@ -442,29 +459,34 @@ def socket_leg(torch, batch, device, n=1 << 20):
 
 
 def config1_loopback():
-    """BASELINE config 1: client -> server over 127.0.0.1, stop-and-wait, 1 char per
-    datagram (rudp.transport over the drop-in Packet; no GPU).  Message = bin/input.txt
-    (recorded in tests/golden/wire_trace.json), plus a 2000-char message for a rate."""
+    """BASELINE config 1: client -> proxy -> server over 127.0.0.1, stop-and-wait, 1 char per
+    datagram (rudp.transport over the drop-in Packet, rudp.relay in proxy.py's role; no
+    GPU).  Message = bin/input.txt (recorded in tests/golden/wire_trace.json), plus a
+    2000-char message for a rate; the relay's counters follow proxy.py:79-94."""
     import threading
+    from rudp.relay import Relay
     from rudp.transport import ReliableUDP
     msg = json.loads((REPO / "tests" / "golden" / "wire_trace.json").read_text())["message"]
     out = {}
     for name, m in (("input_txt", msg), ("2000_chars", "x" * 2000)):
         server = ReliableUDP().create()
         server.bind("127.0.0.1", 0)
-        port = server.socket.getsockname()[1]
+        relay = Relay(server.socket.getsockname()[1])
+        relay.start()
         got = {}
         t = threading.Thread(target=lambda: got.setdefault("m", server.recv()), daemon=True)
         t.start()
-        time.sleep(0.05)  # recv() flushes its socket first (reliableUDP.py:112): let it get there
+        time.sleep(0.05)  # recv() flushes its socket first: let it get there
         client = ReliableUDP(timeout=1).create()
         t0 = time.perf_counter()
-        client.send(m, "127.0.0.1", port)
+        client.send(m, "127.0.0.1", relay.port)
         t.join(timeout=60)
         dt = time.perf_counter() - t0
+        relay.stop()
         client.close()
         server.close()
-        out[name] = {"ok": got.get("m") == m, "wall_ms": dt * 1e3, "chars_per_s": len(m) / dt}
+        out[name] = {"ok": got.get("m") == m, "wall_ms": dt * 1e3, "chars_per_s": len(m) / dt,
+                     "path": "client -> relay (proxy.py role) -> server", "relay_stats": relay.stats}
     return out
 
 
@@ -491,9 +513,10 @@ def main():
     ap.add_argument("--layout", default="rudp7", choices=["rudp5", "rudp7"])
     ap.add_argument("--no-legs", action="store_true")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-workers", type=int, default=min(16, os.cpu_count() or 1))
+    ap.add_argument("--cpu-workers", type=int, default=0,
+                    help="CPU baseline processes (0: one per usable CPU, see usable_cpus())")
     ap.add_argument("--cpu-packets", type=int, default=1 << 15,
-                    help="packets per CPU worker (16 workers x 32768 x ~26 us: about 14 s of CPU work)")
+                    help="packets per CPU worker at 16 workers, scaled to keep the total (16 x 32768 x ~26 us: about 14 s of CPU work)")
     ap.add_argument("--share-device", action="store_true",
                     help="testing only: every rank uses cuda:0 and gloo (rehearse N>1 on one GPU)")
     args = ap.parse_args()
@@ -506,7 +529,8 @@ def main():
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
-        cpu = cpu_baseline(args.payload, args.cpu_packets, args.cpu_workers)
+        workers = args.cpu_workers or usable_cpus()["usable"]
+        cpu = cpu_baseline(args.payload, max(256, args.cpu_packets * 16 // workers), workers)
         cpu["config1_loopback"] = config1_loopback()
 
     import torch

@@ -1319,11 +1319,11 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_small_kernel(VarlenArgs 
   const uint64_t total = frames_limit(a);
   const uint64_t A = fo0 & ~15ull;
   const uint64_t run = ((fo_end + 15u) & ~15ull) - A;  // fo_end < fo0 wraps: far over the cap
-  if (run > a.small_cap || fo_end > total) {  // uniform: per-frame path, one lane each
+  if (run > a.small_cap || fo_end > total) {  // uniform: per-frame path, two lanes each
 #pragma unroll
-    for (uint32_t j = 0; j < FPT; ++j) {
-      const uint32_t q = j * kBlock + tid;
-      decode_varlen_frame<H>(a, p0 + q, q < Tv, 0u, 0u);
+    for (uint32_t j = 0; j < 2u * FPT; ++j) {  // (the header comes from the pair's two first chunks)
+      const uint32_t q = j * (kBlock / 2u) + (tid >> 1);
+      decode_varlen_frame<H>(a, p0 + q, q < Tv, tid & 1u, 1u);
     }
     return;
   }

@@ -1,55 +1,92 @@
-"""Stop-and-wait ARQ over UDP: the caller of the codec (config 1).
+"""Stop-and-wait transfer of one message over UDP: the codec's caller (config 1).
 
-Counterpart of the reference's utils/reliableUDP.py (class ReliableUDP,
-:8-202), which is the only production caller of utils/packet.py.  It is
-rewritten here because the reference file does not parse below Python 3.12
-(PEP 701 f-string at :50).  It stays scalar Python, like the reference: one
-character per datagram (:11), so every frame is 5-9 bytes and by default goes
-through the host-side drop-in rudp.packet.Packet.
+The reference's only production caller of utils/packet.py is its
+utils/reliableUDP.py (class ReliableUDP, :8-202), which does not parse below
+Python 3.12 (PEP 701 f-string at :50).  This module is written from the
+protocol it implements and the wire trace captured from it
+(tests/golden/wire_trace.json): the same public surface, the same bytes on the
+wire, organised as two loops, one per role.
 
-Same public surface: ReliableUDP(timeout).create() / bind(ip, port) /
-send(message, ip, port) / recv() / close() / flush_recv_buffer().  Same
-protocol and wire bytes: the states of the reference's FSM tables (:96-107 and
-:186-199) are the methods below, with the same transitions, retry counts,
-timeouts and header values.  The config-1 wire trace (tests/golden/
-wire_trace.json, captured from the reference) is reproduced byte for byte.
+Protocol (one character of payload per datagram, utils/reliableUDP.py:11):
 
-``ReliableUDP(codec_device="cuda:0")`` moves the sender's data frames
-(:53-61) onto the GPU codec: every frame send() can emit is known once the
-ISN is drawn (pointer p: seq = ISN + p, ack 0, SYN at p = 0, FIN from the last
-character on, payload message[p]), so send() frames the whole message in one
-pack_batch_varlen launch (rudp5, the reference's 5-byte layout) and each
-SEND_DATA step, retransmissions included, sends row p of that table.  The
-bytes on the wire are the same.
+* sender — draws an ISN in [1, 5000]; frame k carries message[k] with
+  seq = ISN + k, ack 0, SYN on k = 0 and FIN on the last character (an empty
+  message is one SYN|FIN frame).  It waits ``timeout`` seconds for a reply
+  whose ack_num is ISN + k + len(payload); other replies are ignored, a
+  timeout resends frame k.  Twenty sends without progress abort the transfer.
+  An ACK moves k to ack_num - ISN.  After the last frame it keeps waiting for
+  the receiver's FIN, answers it with ACK(seq = ISN + k, ack = peer seq + 1)
+  and returns.
+* receiver — accepts a SYN (unless it repeats the previous transfer's ISN) as
+  a new transfer and then the frame whose seq - ISN equals the characters
+  received so far; every datagram is answered with ACK(ack = ISN + characters
+  received).  After accepting a FIN frame it sends FIN|ACK(ack = ISN + length)
+  up to twenty times, half a second apart, until an ACK with ack_num 1 comes
+  back, and returns the message.
+
+``ReliableUDP(codec_device="cuda:0")`` frames the sender's data frames on the
+GPU: every frame a transfer can send is known once the ISN is drawn, so one
+pack_batch_varlen launch (rudp5, the reference's 5-byte layout) builds the
+table and each send, retransmissions included, takes row k.  Same wire bytes.
 """
 from __future__ import annotations
 
 import ipaddress
 import random
 from socket import AF_INET, SOCK_DGRAM, socket
-from typing import Any, Callable, Optional
+from typing import Any, Callable, NamedTuple, Optional
 
+from .batch import ACK, FIN, SYN
 from .packet import Packet
+
+MAX_DATAGRAM = 1024   # recvfrom size of the reference (utils/reliableUDP.py:9)
+MAX_SENDS = 20        # sends without progress before giving up (:10)
+CHUNK = 1             # characters per datagram (:11)
+FIN_WAIT_S = 0.5      # receiver's wait for the final ACK (:166)
+
+
+class Reply(NamedTuple):
+    seq: int
+    ack: int
+    flags: int
+    payload: str
+
+
+def build(seq: int, ack: int, flags: int, payload: str = "") -> bytes:
+    """One frame through the drop-in codec (seq/ack taken mod 2^16 as
+    set_header_field keeps the low 16 bits, utils/packet.py:56)."""
+    p = Packet()
+    p.set_header_field("seq_num", str(seq), base=10)
+    p.set_header_field("ack_num", str(ack), base=10)
+    for name, bit in (("syn", SYN), ("ack", ACK), ("fin", FIN)):
+        if flags & bit:
+            p.set_header_field(name, "1", base=2)
+    p.set_payload(payload)
+    return p.to_byte()
+
+
+def parse(data: bytes) -> Reply:
+    p = Packet(data)
+    flags = sum(bit for name, bit in (("syn", SYN), ("ack", ACK), ("fin", FIN))
+                if p.get_header_field(name, base=2) == "1")
+    return Reply(int(p.get_header_field("seq_num", base=10)), int(p.get_header_field("ack_num", base=10)),
+                 flags, p.get_payload() or "")
 
 
 class ReliableUDP:
-    BUFFER_SIZE = 1024      # utils/reliableUDP.py:9
-    RETRIES = 20            # :10
-    PAYLOAD_SIZE = 1        # :11
+    BUFFER_SIZE = MAX_DATAGRAM
+    RETRIES = MAX_SENDS
+    PAYLOAD_SIZE = CHUNK
 
     def __init__(self, timeout=1, isn_source: Optional[Callable[[], int]] = None,
                  codec_device: Optional[str] = None):
         self.socket: socket
-        self.message_pointer = 0
-        self.random_number = 0
-        self.prev_random_number = None
-        self.target_addr: Any = None
         self.retransmission_timeout = timeout
-        # the ISN draw of :41; injectable so a test can pin the wire trace
-        self._isn = isn_source or (lambda: random.randint(1, 5000))
+        self._draw_isn = isn_source or (lambda: random.randint(1, 5000))
         self._codec_device = codec_device
-        self._frames: Optional[tuple] = None  # (bytes, offsets) of the pre-framed message
+        self._last_isn: Optional[int] = None  # the previous transfer's ISN (a repeated SYN is ignored)
 
+    # ------------------------------------------------------------ socket
     def create(self):
         self.socket = socket(AF_INET, SOCK_DGRAM)
         return self
@@ -57,203 +94,121 @@ class ReliableUDP:
     def bind(self, ip, port):
         self.socket.bind((str(ipaddress.ip_address(ip)), port))
 
+    def close(self):
+        self.socket.close()
+
     def flush_recv_buffer(self):
+        """Drop whatever is queued on the socket (stale replies of an earlier transfer)."""
+        self.socket.setblocking(False)
         try:
-            self.socket.setblocking(False)
-            while self.socket.recvfrom(65535):
-                continue
+            while True:
+                self.socket.recvfrom(65535)
         except BlockingIOError:
             pass
         finally:
             self.socket.setblocking(True)
 
-    def close(self):
-        self.socket.close()
+    def _receive(self, timeout: Optional[float]):
+        """(Reply, addr), or None when nothing arrived within `timeout` seconds."""
+        self.socket.settimeout(timeout)
+        try:
+            data, addr = self.socket.recvfrom(MAX_DATAGRAM)
+        except TimeoutError:
+            return None
+        return parse(data), addr
 
-    # ------------------------------------------------------------- sender
-    def send(self, message, ip, port):
-        """utils/reliableUDP.py:38-108 — SEND_DATA <-> WAIT_ACK -> SEND_ACK -> EXIT."""
+    # ------------------------------------------------------------ sender
+    def send(self, message: str, ip, port) -> None:
         self.flush_recv_buffer()
-        self.message_pointer = 0
-        self.random_number = self._isn()
-        self._frames = self._frame_message(message) if self._codec_device else None
-        dest = (str(ip), port)
-        state, args = "SEND_DATA", (ReliableUDP.RETRIES,)
+        try:
+            self._transmit(message, (str(ipaddress.ip_address(ip)), port))
+        finally:
+            self.flush_recv_buffer()
+
+    def _transmit(self, message: str, dest) -> None:
+        isn = self._draw_isn()
+        table = self._gpu_frames(message, isn) if self._codec_device else None
+        k, sends_left = 0, MAX_SENDS
+        expect = None  # (ack_num that acknowledges the outstanding frame, it was the last one)
         while True:
-            if state == "SEND_DATA":
-                step = self._send_data(message, dest, *args)
-            elif state == "WAIT_ACK":
-                step = self._wait_ack(message, *args)
-            else:  # SEND_ACK
-                self._send_final_ack(ip, port, *args)
-                break
-            if step is None:  # EXIT after the retries ran out
-                break
-            state, args = step[0], step[1:]
-        self.flush_recv_buffer()
+            if expect is None:  # (re)send frame k
+                n = CHUNK if k < len(message) else 0
+                last = k + n >= len(message)
+                if sends_left < 1:
+                    if not last:
+                        print(f"\033[91mAborted after {MAX_SENDS * self.retransmission_timeout} seconds "
+                              f"({MAX_SENDS} sends of character {k} unacknowledged)\033[0m")
+                    return
+                if table is not None:
+                    frame = table[0][table[1][k]:table[1][k + 1]]
+                else:
+                    flags = (SYN if k == 0 else 0) | (FIN if last else 0)
+                    frame = build(isn + k, 0, flags, message[k:k + n])
+                self.socket.sendto(frame, dest)
+                sends_left -= 1
+                expect = (isn + k + n, last)
+            got = self._receive(self.retransmission_timeout)
+            if got is None:
+                expect = None  # timeout: resend
+                continue
+            reply = got[0]
+            if reply.ack != expect[0]:
+                continue  # not for the outstanding frame
+            if reply.flags & ACK:
+                k = reply.ack - isn
+            if reply.flags & FIN:
+                self.socket.sendto(build(isn + k, reply.seq + 1, ACK), dest)
+                return
+            if expect[1]:
+                expect = (isn + k, True)  # everything is sent: wait for the FIN
+            else:
+                expect, sends_left = None, MAX_SENDS
 
-    def _frame_message(self, message):
-        """Frames for pointer values 0..len(message), in one GPU launch."""
+    def _gpu_frames(self, message: str, isn: int):
+        """Frames for k = 0..len(message) in one GPU launch: (bytes, offsets)."""
         import numpy as np
         import torch
         from . import batch
         dev = torch.device(self._codec_device)
-        n = len(message) + 1  # p = len(message): the header-only FIN frame (empty payload)
-        p = np.arange(n, dtype=np.int64)
-        seq = ((self.random_number + p) & 0xFFFF).astype(np.uint16)
-        flags = np.where(p == 0, 0x80, 0) | np.where(p >= len(message) - 1, 0x20, 0)
+        n = len(message) + 1  # k = len(message): the header-only FIN frame a late resend carries
+        k = np.arange(n, dtype=np.int64)
+        seq = ((isn + k) & 0xFFFF).astype(np.uint16)
+        flags = (np.where(k == 0, SYN, 0) | np.where(k >= len(message) - 1, FIN, 0)).astype(np.uint8)
         lens = np.array([len(c.encode()) for c in message] + [0], dtype=np.int32)
         payload = np.frombuffer(bytearray(message.encode()), dtype=np.uint8)
         t = lambda a: torch.from_numpy(np.ascontiguousarray(a)).to(dev)  # noqa: E731
-        res = batch.pack_batch_varlen((t(seq), t(np.zeros(n, np.uint16)), t(flags.astype(np.uint8))),
-                                      t(payload), t(lens), "rudp5", want_csum=False)
+        res = batch.pack_batch_varlen((t(seq), t(np.zeros(n, np.uint16)), t(flags)), t(payload), t(lens),
+                                      "rudp5", want_csum=False)
         return res.frames.cpu().numpy().tobytes(), res.frame_off.cpu().tolist()
 
-    def _send_data(self, message, dest, retries):
-        # :43-62
-        end = min(self.message_pointer + ReliableUDP.PAYLOAD_SIZE, len(message))
-        is_first = self.message_pointer == 0
-        is_last = end == len(message)
-        if retries < 1:
-            if not is_last:
-                sent = message[:self.message_pointer]
-                tail = f"\n'{sent}'" if self.message_pointer > 0 else ""
-                print(f"\033[91mAborted after {ReliableUDP.RETRIES * self.retransmission_timeout} "
-                      f"seconds ({ReliableUDP.RETRIES} retries * {self.retransmission_timeout} "
-                      f"second timeout) {tail} \033[0m")
-            return None
-        if self._frames is not None:
-            data, off = self._frames
-            frame = data[off[self.message_pointer]:off[self.message_pointer + 1]]
-        else:
-            p = Packet()
-            p.set_header_field("seq_num", str(self.message_pointer + self.random_number), base=10)
-            p.set_header_field("ack_num", "0", base=10)
-            if is_first:
-                p.set_header_field("syn", "1", base=2)
-            if is_last:
-                p.set_header_field("fin", "1", base=2)
-            p.set_payload(message[self.message_pointer:end])
-            frame = p.to_byte()
-        self.socket.sendto(frame, dest)
-        return ("WAIT_ACK", is_last, end - self.message_pointer, retries - 1)
-
-    def _wait_ack(self, message, is_last, payload_length, retries):
-        # :64-85
-        try:
-            self.socket.settimeout(self.retransmission_timeout)
-            data, _ = self.socket.recvfrom(ReliableUDP.BUFFER_SIZE)
-            p = Packet(data)
-            ack_num = int(p.get_header_field("ack_num", base=10))
-            seq_num = int(p.get_header_field("seq_num", base=10))
-            is_valid = ack_num == self.random_number + self.message_pointer + payload_length
-            is_ack = is_valid and p.get_header_field("ack", base=2) == "1"
-            is_fin = is_valid and p.get_header_field("fin", base=2) == "1"
-            if not is_valid:
-                return ("WAIT_ACK", is_last, payload_length, retries)
-            if is_ack:
-                self.message_pointer = ack_num - self.random_number
-            if is_fin:
-                return ("SEND_ACK", seq_num)
-            if is_last:
-                return ("WAIT_ACK", True, 0, retries)
-            return ("SEND_DATA", ReliableUDP.RETRIES)
-        except TimeoutError:
-            return ("SEND_DATA", retries)
-
-    def _send_final_ack(self, ip, port, last_seq_num):
-        # :87-93
-        p = Packet()
-        p.set_header_field("seq_num", str(self.random_number + self.message_pointer), base=10)
-        p.set_header_field("ack_num", str(last_seq_num + 1), base=10)
-        p.set_header_field("ack", "1", base=2)
-        self.socket.sendto(p.to_byte(), (str(ipaddress.ip_address(ip)), port))
-
     # ----------------------------------------------------------- receiver
-    def recv(self):
-        """utils/reliableUDP.py:111-199 — RECEIVE_DATA <-> SEND_ACK -> SEND_FIN <-> WAIT_ACK."""
+    def recv(self) -> str:
         self.flush_recv_buffer()
-        self.message_pointer = 0
-        self.random_number = 0
-        state, args = "RECEIVE_DATA", ("",)
+        isn, text, peer = 0, "", None
+        received = 0  # characters accepted so far (the next in-order frame is isn + received)
         while True:
-            if state == "RECEIVE_DATA":
-                state, *args = self._receive_data(*args)
-            elif state == "SEND_ACK":
-                state, *args = self._send_ack(*args)
-            elif state == "SEND_FIN":
-                state, *args = self._send_fin(*args)
-            elif state == "WAIT_ACK":
-                state, *args = self._wait_fin_ack(*args)
-            else:  # EXIT
-                return self._clean_up(*args)
-
-    def _receive_data(self, buffer=""):
-        # :116-137
-        self.socket.settimeout(None)
-        data, addr = self.socket.recvfrom(ReliableUDP.BUFFER_SIZE)
-        p = Packet(data)
-        seq_num = int(p.get_header_field("seq_num", base=10))
-        payload = p.get_payload() or ""
-        is_last_message = p.get_header_field("fin", base=2) == "1"
-        is_syn = p.get_header_field("syn", base=2) == "1"
-        is_valid = (self.message_pointer == 0 and is_syn) or \
-            seq_num - self.random_number == self.message_pointer
-        is_new_connection = is_syn and not is_valid
-        is_duplicate_syn = is_syn and seq_num == self.prev_random_number
-        if is_syn and not is_duplicate_syn:
-            self.random_number = seq_num
-            self.message_pointer = 0
-            self.target_addr = addr
-            buffer = ""
-        if (is_valid or is_new_connection) and not is_duplicate_syn:
-            self.message_pointer = len(buffer + payload)
-            return ("SEND_ACK", buffer + payload, is_last_message)
-        return ("SEND_ACK", buffer, False)
-
-    def _send_ack(self, acknowledged_message, is_last_message):
-        # :139-150
-        if not self.target_addr:
-            return ("RECEIVE_DATA", "")
-        p = Packet()
-        p.set_header_field("ack", "1", base=2)
-        p.set_header_field("seq_num", "0", base=10)
-        p.set_header_field("ack_num", str(self.random_number + len(acknowledged_message)), base=10)
-        self.socket.sendto(p.to_byte(), self.target_addr)
-        if is_last_message:
-            return ("SEND_FIN", acknowledged_message, 20)
-        return ("RECEIVE_DATA", acknowledged_message)
-
-    def _send_fin(self, message, retries):
-        # :152-162
-        if retries < 1:
-            return ("EXIT", message)
-        p = Packet()
-        p.set_header_field("fin", "1", base=2)
-        p.set_header_field("ack", "1", base=2)
-        p.set_header_field("seq_num", "0", base=10)
-        p.set_header_field("ack_num", str(self.random_number + len(message)), base=10)
-        self.socket.sendto(p.to_byte(), self.target_addr)
-        return ("WAIT_ACK", message, retries - 1)
-
-    def _wait_fin_ack(self, message, retries):
-        # :164-176
-        try:
-            self.socket.settimeout(0.5)
-            data, _ = self.socket.recvfrom(ReliableUDP.BUFFER_SIZE)
-            p = Packet(data)
-            is_ack = p.get_header_field("ack", base=2) == "1"
-            ack_num = int(p.get_header_field("ack_num", base=10))
-            if is_ack and ack_num == 1:
-                return ("EXIT", message)
-            return ("SEND_FIN", message, retries)
-        except TimeoutError:
-            return ("SEND_FIN", message, retries)
-
-    def _clean_up(self, message):
-        # :178-183
-        self.message_pointer = 0
-        self.prev_random_number = self.random_number
-        self.random_number = 0
+            reply, addr = self._receive(None)
+            syn = bool(reply.flags & SYN)
+            in_order = (received == 0 and syn) or reply.seq - isn == received
+            repeated_syn = syn and reply.seq == self._last_isn
+            finished = False
+            if syn and not repeated_syn:  # a new transfer starts here
+                isn, received, peer, text = reply.seq, 0, addr, ""
+            if (in_order or syn) and not repeated_syn:
+                text += reply.payload
+                received = len(text)
+                finished = bool(reply.flags & FIN)
+            if peer is None:  # nothing to answer yet
+                text = ""
+                continue
+            self.socket.sendto(build(0, isn + len(text), ACK), peer)
+            if finished:
+                break
+        for _ in range(MAX_SENDS):
+            self.socket.sendto(build(0, isn + len(text), FIN | ACK), peer)
+            got = self._receive(FIN_WAIT_S)
+            if got is not None and got[0].flags & ACK and got[0].ack == 1:
+                break
+        self._last_isn = isn
         self.flush_recv_buffer()
-        return message
+        return text

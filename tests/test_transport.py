@@ -1,8 +1,8 @@
 """Config 1: client -> relay -> server over 127.0.0.1 with the drop-in codec.
 
 rudp.transport.ReliableUDP (the caller, counterpart of utils/reliableUDP.py)
-moves bin/input.txt's message through a UDP relay that plays proxy.py's role
-(forward both ways, record, optionally drop).  Every datagram on the wire is
+moves bin/input.txt's message through rudp.relay.Relay, which plays proxy.py's
+role (forward both ways, record, optionally drop).  Every datagram on the wire is
 compared with the trace captured from the reference (tests/golden/
 wire_trace.json, ISN 0x0e1b), and the relay checks each one with the drop-in
 Packet the way proxy.py:81,90 does.
@@ -14,44 +14,8 @@ import time
 import pytest
 
 from rudp.packet import Packet
+from rudp.relay import Relay
 from rudp.transport import ReliableUDP
-
-
-class Relay(threading.Thread):
-    """UDP forwarder between one client and one server (proxy.py:126-154, minus the UI)."""
-
-    def __init__(self, server_port, drop=lambda direction, index: False):
-        super().__init__(daemon=True)
-        self.sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
-        self.sock.bind(("127.0.0.1", 0))
-        self.sock.settimeout(0.05)
-        self.port = self.sock.getsockname()[1]
-        self.server = ("127.0.0.1", server_port)
-        self.client = None
-        self.drop = drop
-        self.log = {"c2s": [], "s2c": []}
-        self.seen = []
-        self.retransmitted = 0
-        self.stop = threading.Event()
-
-    def run(self):
-        while not self.stop.is_set():
-            try:
-                data, addr = self.sock.recvfrom(1024)
-            except socket.timeout:
-                continue
-            direction = "s2c" if addr == self.server else "c2s"
-            if direction == "c2s":
-                self.client = addr
-            index = len(self.log[direction])
-            self.log[direction].append(data)
-            pkt = Packet(data)                  # proxy.py:81
-            if pkt in self.seen:                # proxy.py:90, Packet.__eq__
-                self.retransmitted += 1
-            self.seen.append(pkt)
-            if self.drop(direction, index):
-                continue
-            self.sock.sendto(data, self.server if direction == "c2s" else self.client)
 
 
 def run_transfer(message, isn, drop=None, client_timeout=1, codec_device=None):
@@ -71,8 +35,7 @@ def run_transfer(message, isn, drop=None, client_timeout=1, codec_device=None):
     t.join(timeout=30)
     dt = time.perf_counter() - t0
     time.sleep(0.05)
-    relay.stop.set()
-    relay.join(timeout=2)
+    relay.stop()
     client.close()
     server.close()
     return got.get("msg"), relay, dt
@@ -84,6 +47,10 @@ def test_config1_wire_trace_matches_reference(wire_trace):
     assert [d.hex() for d in relay.log["c2s"]] == wire_trace["client_to_server"]
     assert [d.hex() for d in relay.log["s2c"]] == wire_trace["server_to_client"]
     assert relay.retransmitted == 0
+    n_c, n_s = len(wire_trace["client_to_server"]), len(wire_trace["server_to_client"])
+    assert relay.stats == {"client_sent": n_c, "client_received": n_s, "client_dropped": 0,
+                           "client_retransmitted": 0, "server_sent": n_s, "server_received": n_c,
+                           "server_dropped": 0, "server_retransmitted": 0}
 
 
 def test_config1_survives_drops(wire_trace):
@@ -175,3 +142,28 @@ def test_gpu_frame_table_rows_equal_scalar_packets(isn):
             q.set_header_field("fin", "1", base=2)
         q.set_payload(message[ptr:ptr + 1])
         assert data[off[ptr]:off[ptr + 1]] == q.to_byte(), ptr
+
+
+def test_relay_history_equals_proxy_list_scan():
+    """The relay's keyed history gives the proxy's `Packet(data) in self.packets`
+    answer (proxy.py:81-94, 500 deep) on datagrams with repeats, empty ones and
+    ones that differ only in length."""
+    import random as _r
+    from rudp.relay import MAX_MEMORY, Relay
+    rng = _r.Random(7)
+    pool = [b"", bytes(5), b"\x00", bytes(6), b"\x01\x02\x03\x04\x05", b"\x01\x02\x03\x04\x05a"] + \
+        [bytes(rng.randrange(256) for _ in range(rng.randrange(0, 9))) for _ in range(40)]
+    seq = [rng.choice(pool) for _ in range(3000)]
+    relay = Relay(9)  # never started: only its bookkeeping is used
+    want, history = [], []
+    for i, data in enumerate(seq):
+        pkt = Packet(data)
+        want.append(pkt in history)
+        history.append(pkt)
+        if len(history) > MAX_MEMORY:
+            history.pop(0)
+        before = relay.retransmitted
+        relay._record("client", data, False)
+        assert (relay.retransmitted - before == 1) == want[-1], i
+    relay.sock.close()
+    assert any(want) and not all(want)
