@@ -703,8 +703,8 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
   const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
   const uint64_t total = frames_limit(a);
   const uint64_t A = fo0 & ~15ull;
-  const uint64_t run = ((fo_end + 15u) & ~15ull) - A;  // fo_end < fo0 wraps: far over the cap
-  if (run > a.tile_cap || fo_end > total) {  // uniform over the workgroup
+  const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
+  if (fo0 > fo_end || fo_end > total || run > a.tile_cap) {  // uniform over the workgroup
     decode_varlen_frame<H>(a, p0 + q, q < Tv, g, glog);
     return;
   }
@@ -1318,8 +1318,8 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_small_kernel(VarlenArgs 
   const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
   const uint64_t total = frames_limit(a);
   const uint64_t A = fo0 & ~15ull;
-  const uint64_t run = ((fo_end + 15u) & ~15ull) - A;  // fo_end < fo0 wraps: far over the cap
-  if (run > a.small_cap || fo_end > total) {  // uniform: per-frame path, two lanes each
+  const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
+  if (fo0 > fo_end || fo_end > total || run > a.small_cap) {  // uniform: per-frame path, two lanes each
 #pragma unroll
     for (uint32_t j = 0; j < 2u * FPT; ++j) {  // (the header comes from the pair's two first chunks)
       const uint32_t q = j * (kBlock / 2u) + (tid >> 1);
