@@ -129,8 +129,7 @@ def test_gpu_frame_table_rows_equal_scalar_packets(isn):
     for pointer p (utils/reliableUDP.py:53-61), seq wrapping past 2^16."""
     message = "ab✓𝄞" + "z" * 100
     r = ReliableUDP(isn_source=lambda: isn, codec_device="cuda:0")
-    r.random_number = isn
-    data, off = r._frame_message(message)
+    data, off = r._gpu_frames(message, isn)
     assert len(off) == len(message) + 2
     for ptr in range(len(message) + 1):
         q = Packet()
