@@ -9,6 +9,9 @@ launch (median of HIP-event pairs), interleaved round by round:
   four_sets   four sets rotating
   flushed     one set, a 1 GiB scratch write between launches (outside the events)
   n16M        the C5 shape, one set, per 2^20 packets
+  n16M_split  the same 16M buffers encoded as 16 launches of 2^20 packets each
+              (launch size vs address-space size)
+  n4M         one 4M-packet launch (12.4 GB in + out)
 
 usage: python tools/cache_residency.py [--reps 20] [--rounds 5]
 """
@@ -70,6 +73,13 @@ def main():
     }
     if big is not None:
         forms["n16M"] = lambda: timed(lambda i: big, max(4, args.reps // 4), scale=16.0)
+        parts = [(type(big[0])(big[0].seq[k * n:(k + 1) * n], big[0].ack[k * n:(k + 1) * n],
+                               big[0].flags[k * n:(k + 1) * n]), big[1][k * n:(k + 1) * n],
+                  big[2][k * n:(k + 1) * n]) for k in range(16)]
+        forms["n16M_split"] = lambda: timed(lambda i: parts[i % 16], 16 * max(2, args.reps // 8))
+        forms["n4M"] = lambda: timed(lambda i: (type(big[0])(big[0].seq[:4 * n], big[0].ack[:4 * n],
+                                                             big[0].flags[:4 * n]), big[1][:4 * n],
+                                                big[2][:4 * n]), max(4, args.reps // 2), scale=4.0)
     for f in forms.values():  # warm every form once
         f()
     per = {k: [] for k in forms}

@@ -383,6 +383,84 @@ def vknob_sweep(reps, key, values, pre=()):
     return out
 
 
+def small_sweep(reps):
+    """Small frames (the reference's one-character datagrams and a few other
+    tiny shapes): varlen encode and decode-verify through the sync-free C ABI
+    (preallocated outputs), with the small-frame tile kernels at 1/2/4/8
+    packets per thread (keys 46/47) against the per-packet vector kernels.
+    Every variant is checked bit-exact against the vector kernels."""
+    import ctypes
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    out = {}
+    specs = {"vec": ((46, 0),), "fpt1": ((46, 16), (47, 1)), "fpt2": ((46, 16), (47, 2)),
+             "fpt4": ((46, 16), (47, 4)), "fpt8": ((46, 16), (47, 8))}
+    old = {k: lib.rudpx_tune(k, 0) for k in (46, 47)}
+    for k, v in old.items():
+        lib.rudpx_tune(k, v)
+    for shape in ("L1", "L4", "U1-4", "L9", "L15"):
+        n = 1 << 20
+        if shape.startswith("U"):
+            lens = torch.randint(1, 5, (n,), dtype=torch.int32, device=dev)
+        else:
+            lens = torch.full((n,), int(shape[1:]), dtype=torch.int32, device=dev)
+        total = int(lens.sum().item())
+        tab, pay = batch.synth_batch(n, 16, 0x5EED000B, device=dev)
+        flat = pay.view(-1)[:total].contiguous()
+        del pay
+        H = 7
+        hint = total // n
+        frames = torch.empty(total + n * H, dtype=torch.uint8, device=dev)
+        off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        st = torch.empty(1, dtype=torch.int32, device=dev)
+        o16 = [torch.empty(n, dtype=torch.uint16, device=dev) for _ in range(3)]
+        o8 = [torch.empty(n, dtype=torch.uint8, device=dev) for _ in range(2)]
+        b = _native.RudpBatch(n=n, payload_len=hint, reserved=0, seq=tab.seq.data_ptr(), ack=tab.ack.data_ptr(),
+                              flags=tab.flags.data_ptr(), payload=flat.data_ptr(), len=lens.data_ptr(),
+                              payload_off=None)
+
+        def enc():
+            _native.check(lib.rudp_encode_varlen_checked(ctypes.byref(b), total, frames.data_ptr(), frames.numel(),
+                                                         off.data_ptr(), None, st.data_ptr(), H, 0, stream))
+
+        def dec():
+            _native.check(lib.rudp_decode_varlen_checked(frames.data_ptr(), frames.numel(), off.data_ptr(),
+                                                         frames.numel() // n, n, None, o16[0].data_ptr(),
+                                                         o16[1].data_ptr(), o8[0].data_ptr(), o8[1].data_ptr(),
+                                                         o16[2].data_ptr(), st.data_ptr(), H, 0, stream))
+
+        def setter(kv):
+            return lambda: [lib.rudpx_tune(k, v) for k, v in kv]
+        variants = {}
+        for name, kv in specs.items():
+            variants[f"{shape}_enc_{name}"] = (setter(kv), enc)
+            variants[f"{shape}_dec_{name}"] = (setter(kv), dec)
+        res = interleaved(variants, reps)
+        ref = None
+        exact = {}
+        for name, kv in specs.items():
+            setter(kv)()
+            enc()
+            dec()
+            got = (frames.clone(), off.clone(), [o.clone() for o in o16 + o8])
+            if ref is None:
+                ref = got
+            exact[name] = (torch.equal(got[0], ref[0]) and torch.equal(got[1], ref[1])
+                           and all(torch.equal(x, y) for x, y in zip(got[2], ref[2]))
+                           and bool((o8[1] == 1).all().item()) and int(st.item()) == 0)
+        for k, v in old.items():
+            lib.rudpx_tune(k, v)
+        mean_f = (total + n * H) / n
+        alg_e = n * (4 + total / n + 5 + mean_f + 8)      # len, payload, table in; frames, offsets out
+        alg_d = n * (mean_f + 8 + 8)                      # frames, offsets in; seq/ack/flags/ok/csum out
+        for k, ms in res.items():
+            alg = alg_e if "_enc_" in k else alg_d
+            out[k] = {"ms": ms, "frac": alg / ms / 1e9 / 8.0, "exact": exact[k.rsplit("_", 1)[1]]}
+        del tab, flat, lens, frames, off
+        torch.cuda.empty_cache()
+    return out
+
+
 def decode_sweep(reps):
     dev = torch.device("cuda", 0)
     out = {}
@@ -672,7 +750,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--L", type=int, default=1472, help="payload length for --only ablate")
-    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "align", "knob", "copydma", "multi", "opsknob", "vdec", "vknob"])
+    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "small", "align", "knob", "copydma", "multi", "opsknob", "vdec", "vknob"])
     ap.add_argument("--blocks", type=str, default="", help="encode sweep: workgroup sizes, e.g. 256,512,1024")
     ap.add_argument("--encode-L", type=str, default="", help="encode sweep: payload lengths, e.g. 1472")
     ap.add_argument("--percu", type=str, default="", help="encode sweep: tiles-per-CU caps, e.g. 3,4,5")
@@ -697,6 +775,8 @@ def main():
         result["copy"] = copy_sweep(args.reps)
     if args.only in (None, "decode"):
         result["decode"] = decode_sweep(args.reps)
+    if args.only == "small":
+        result["small"] = small_sweep(args.reps)
     if args.only == "utf8":
         result["utf8"] = utf8_sweep(args.reps)
     if args.only == "varlen":
