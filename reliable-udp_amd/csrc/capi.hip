@@ -405,9 +405,23 @@ int rudp_encode(const rudp_batch* in, uint8_t* d_frames, uint16_t* d_csum_or_nul
   if (rc || in->n == 0) return rc;
   DeviceScope dev_scope;
   if ((rc = dev_scope.set(device))) return rc;
-  EncodeTileArgs a = make_encode_args(in, d_frames, d_csum_or_null, layout);
-  rc = launch_encode(a, layout, a.T != 0, (hipStream_t)hip_stream);
-  if (rc) return hip_fail((hipError_t)rc, "encode launch");
+  // Batches over `encode_launch_packets` go out as several launches on the
+  // stream, each over a contiguous slice (a multiple of every tile size).
+  const int lp = tuning().encode_launch_packets;
+  const uint64_t chunk = lp > 0 ? ((uint64_t)lp + 255u) & ~255ull : in->n;
+  const uint64_t F = (uint64_t)in->payload_len + (uint64_t)layout;
+  for (uint64_t p0 = 0; p0 < in->n; p0 += chunk) {
+    rudp_batch sub = *in;
+    sub.n = in->n - p0 < chunk ? in->n - p0 : chunk;
+    sub.seq = in->seq + p0;
+    sub.ack = in->ack + p0;
+    sub.flags = in->flags + p0;
+    sub.payload = in->payload ? in->payload + p0 * in->payload_len : nullptr;
+    EncodeTileArgs a = make_encode_args(&sub, d_frames + p0 * F, d_csum_or_null ? d_csum_or_null + p0 : nullptr,
+                                        layout);
+    rc = launch_encode(a, layout, a.T != 0, (hipStream_t)hip_stream);
+    if (rc) return hip_fail((hipError_t)rc, "encode launch");
+  }
   return 0;
 }
 

@@ -242,6 +242,9 @@ struct Tuning {
   // and its packets per thread (1, 2, 4, 8: tiles of 256 * fpt packets).
   std::atomic<int> varlen_small{16};
   std::atomic<int> varlen_small_fpt{4};
+  // Fixed-length encode: batches of more packets than this go out as several
+  // launches of at most this many (0: one launch).
+  std::atomic<int> encode_launch_packets{0};
   std::atomic<int> host_slots{3};     // *_host pipeline: device staging slots (2..8)
   std::atomic<int> host_stage_mb{128};  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
 };

@@ -258,7 +258,7 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // UTF-8 validation through LDS tiles; 42: its LDS budget (%); 43: varlen tile
 // offsets before phase 1; 44: varlen encode tile waves per SIMD; 45: packed UTF-8
 // tile bytes; 46: small-frame varlen encode below this hint (0 = off); 47: its
-// packets per thread.
+// packets per thread; 48: fixed-length encode packets per launch (0 = one launch).
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
@@ -289,7 +289,8 @@ int rudpx_tune(int key, int value) {
             : key == 44 ? &t.varlen_waves
             : key == 45 ? &t.utf8_vtile_bytes
             : key == 46 ? &t.varlen_small
-            : key == 47 ? &t.varlen_small_fpt : nullptr;
+            : key == 47 ? &t.varlen_small_fpt
+            : key == 48 ? &t.encode_launch_packets : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }
