@@ -360,6 +360,7 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
     a.tile_cap = cap <= 49152u ? (uint32_t)cap : 0u;
   }
   a.early_fo = tuning().varlen_early_fo ? 1u : 0u;
+  a.xcd = tuning().tile_xcd ? 1u : 0u;
   // Small frames (payload hint under varlen_small bytes): tiles of 256 * fpt
   // frames with the per-frame outputs lane-strided (decode_varlen_small_kernel).
   {
@@ -443,6 +444,7 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, ui
                  ((reinterpret_cast<uintptr_t>(d_seq) | reinterpret_cast<uintptr_t>(d_ack) |
                    reinterpret_cast<uintptr_t>(d_flags) | reinterpret_cast<uintptr_t>(d_ok) |
                    reinterpret_cast<uintptr_t>(d_csum_out_or_null)) & 3u) == 0) ? 1u : 0u;
+  a.xcd = tuning().tile_xcd ? 1u : 0u;
   a.frames = d_frames;
   a.csum_in = d_csum_in_or_null;
   a.seq = d_seq;
@@ -564,6 +566,7 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
     a.vhc = (uint32_t)(vhc < 0 ? 0 : vhc > 2 ? 2 : vhc);
   }
   a.early_fo = tuning().varlen_early_fo ? 1u : 0u;
+  a.xcd = tuning().tile_xcd ? 1u : 0u;
   a.status = chk.status;
   // Small frames (hints under varlen_small bytes, packed, aligned): the scan's
   // last pass and the framing in one tile kernel (launch_encode_varlen_small).
@@ -699,6 +702,7 @@ int rudp_validate_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_n
   a.F = frame_len;
   a.H = (uint32_t)layout;
   a.valid = d_valid;
+  a.xcd = tuning().tile_xcd ? 1u : 0u;
   rc = launch_validate_utf8(a, (hipStream_t)hip_stream);
   if (rc) return hip_fail((hipError_t)rc, "utf8 validation launch");
   return 0;

@@ -18,6 +18,18 @@ typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kBlock = 256;  // 4 waves of 64
 
+// An MI355X deals a launch's workgroups round-robin over its 8 XCDs (blocks
+// b, b + 8, ... run on one XCD, each XCD with its own L2).  xcd_tile(b, nt)
+// renumbers them so XCD x owns the contiguous run of tiles
+// [x*per + min(x, rem), ...) of nt = per*8 + rem: every XCD streams its own
+// slice of the batch front to back.  Bijective over [0, nt).
+constexpr uint32_t kXcds = 8;
+__device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nt) {
+  const uint32_t per = nt / kXcds, rem = nt % kXcds;
+  const uint32_t x = b % kXcds, k = b / kXcds;
+  return x * per + (x < rem ? x : rem) + k;
+}
+
 // End-around-carry fold of a 32-bit partial sum to 16 bits.
 __device__ __forceinline__ uint32_t fold16(uint32_t s) {
   s = (s & 0xFFFFu) + (s >> 16);

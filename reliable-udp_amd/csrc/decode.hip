@@ -196,7 +196,7 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
   const uint32_t T = kBlock >> glog;
   const uint32_t q = tid >> glog;
   const uint32_t g = tid & (G - 1u);
-  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
   const uint32_t F = a.F;

@@ -184,15 +184,7 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   const uint32_t glog = (uint32_t)((int)a.glog + kLogBlock - 8);
   const uint32_t G = 1u << glog;
   uint32_t tile = blockIdx.x;
-  if (a.xcd_swizzle) {
-    // Workgroups are dealt round-robin over the 8 XCDs (b, b+8, ... share
-    // one).  Give each XCD a contiguous run of tiles so neighbouring tiles'
-    // header-table lines and boundary output lines stay in one L2.  Bijective
-    // for any tile count; placement affects speed only.
-    const uint32_t nt = a.num_tiles, per = nt >> 3, rem = nt & 7u;
-    const uint32_t x = tile & 7u, k = tile >> 3;
-    tile = x * per + (x < rem ? x : rem) + k;
-  }
+  if (a.xcd_swizzle) tile = xcd_tile(tile, a.num_tiles);  // each XCD streams its own slice
   const uint64_t p0 = (uint64_t)tile * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;

@@ -48,6 +48,7 @@ struct DecodeArgs {
   uint32_t glog;            // log2(lanes per packet)
   uint32_t align64;         // tile kernel: wave loads/stores start on 64-B sector boundaries
   uint32_t stage_out;       // tile kernel: outputs staged in LDS, written as dwords (pointers 4-B aligned)
+  uint32_t xcd;             // tile kernel: XCD-contiguous tile order (xcd_tile)
 };
 
 struct SynthArgs {
@@ -106,6 +107,7 @@ struct VarlenArgs {
   uint32_t* status_out;
   uint32_t small_fpt;             // decode small-frame tile: frames per thread (0: not used)
   uint32_t small_cap;             // its LDS run budget in bytes
+  uint32_t xcd;                   // tile kernels: XCD-contiguous tile order (xcd_tile)
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -119,6 +121,7 @@ struct Utf8Args {
   uint32_t glog;              // log2 lanes per frame (vector kernel)
   uint32_t tile_cap;          // varlen tile kernel: LDS bytes a tile's run may use
   const uint32_t* status;     // sync-free call: RUDP_ST_* from check_frame_offsets, or null
+  uint32_t xcd;               // tile kernels: XCD-contiguous tile order (xcd_tile)
 };
 
 struct DedupArgs {
@@ -149,7 +152,12 @@ struct Tuning {
   std::atomic<int> encode_p1{8};      // phase-1 loads in flight per lane (2, 4, 8)
   std::atomic<int> encode_blocks_per_cu{-1};  // cap resident tiles per CU via LDS reservation; 0 = natural, -1 = auto
   std::atomic<int> decode_glog{-1};   // verify kernel lanes-per-packet log2; -1 = automatic
-  std::atomic<int> encode_xcd_swizzle{0};  // XCD-contiguous tile order (T1)
+  // XCD-contiguous tile order (xcd_tile) for the fixed-length encode tile:
+  // 16M x 1472 B 0.540 -> 0.481 ms per 2^20 packets, 1M x 1472 B 0.518 ->
+  // 0.513 ms (tools/launch_split.py, profiles/r02/sweeps/launch_split.json).
+  std::atomic<int> encode_xcd_swizzle{1};
+  // The same order for the decode, varlen and UTF-8 tile kernels.
+  std::atomic<int> tile_xcd{0};
   std::atomic<int> encode_contig{1};  // phase 1 streams the tile contiguously, sums from LDS
   std::atomic<int> encode_block{256};  // tile workgroup size (64, 128 when T <= block; 256, 512, 1024)
   std::atomic<int> decode_copy_tile{1};  // copy-out decode through an LDS tile (0: register windows)

@@ -258,7 +258,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // UTF-8 validation through LDS tiles; 42: its LDS budget (%); 43: varlen tile
 // offsets before phase 1; 44: varlen encode tile waves per SIMD; 45: packed UTF-8
 // tile bytes; 46: small-frame varlen encode below this hint (0 = off); 47: its
-// packets per thread; 48: fixed-length encode packets per launch (0 = one launch).
+// packets per thread; 48: fixed-length encode packets per launch (0 = one launch);
+// 49: XCD-contiguous tile order in the decode / varlen / UTF-8 tile kernels.
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
@@ -290,7 +291,8 @@ int rudpx_tune(int key, int value) {
             : key == 45 ? &t.utf8_vtile_bytes
             : key == 46 ? &t.varlen_small
             : key == 47 ? &t.varlen_small_fpt
-            : key == 48 ? &t.encode_launch_packets : nullptr;
+            : key == 48 ? &t.encode_launch_packets
+            : key == 49 ? &t.tile_xcd : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }

@@ -267,7 +267,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
 
   const uint32_t tid = threadIdx.x;
   const uint32_t q = tid >> glog, g = tid & (G - 1u);
-  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
   // Header-table loads first (small tiles): their latency overlaps the
@@ -697,7 +697,7 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
   const uint32_t q = tid >> glog, g = tid & (G - 1u);
   uint32_t* lds_fo = reinterpret_cast<uint32_t*>(lds);                       // [T + 1]
   unsigned char* img = lds + ((((T + 1u) * 4u) + 15u) & ~15u) + kVTGuard;   // the run
-  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
   const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
@@ -1000,7 +1000,7 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_tile_kernel(Utf8Args a) 
   const uint32_t tid = threadIdx.x;
   const uint32_t glog = a.glog, G = 1u << glog, T = kBlock >> glog;
   const uint32_t q = tid >> glog, g = tid & (G - 1u);
-  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
   const uint32_t F = a.F, H = a.H;
@@ -1043,7 +1043,7 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_vtile_kernel(Utf8Args a)
   const uint32_t tid = threadIdx.x;
   const uint32_t glog = a.glog, G = 1u << glog, T = kBlock >> glog;
   const uint32_t q = tid >> glog, g = tid & (G - 1u);
-  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
   const uint64_t total = a.frame_off[a.n];
@@ -1131,10 +1131,11 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
   unsigned char* pay = lds + small_lds_off_pay(T);
   unsigned char* img = lds + small_lds_off_out(T, cap);
 
-  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint32_t Tv = a.n - p0 < T ? (uint32_t)(a.n - p0) : T;
-  const uint64_t fo0 = bases[blockIdx.x];
-  const uint64_t fo_end = p0 + T < a.n ? bases[blockIdx.x + 1] : a.frame_off[a.n];
+  const uint64_t tile = p0 / T;
+  const uint64_t fo0 = bases[tile];
+  const uint64_t fo_end = p0 + T < a.n ? bases[tile + 1] : a.frame_off[a.n];
   if (call_failed(a.status)) return;
   const uint64_t po0 = fo0 - p0 * (uint64_t)H, po_end = fo_end - (p0 + Tv) * (uint64_t)H;
   const uint64_t A = po0 & ~15ull, OA = fo0 & ~15ull;
@@ -1313,7 +1314,7 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_small_kernel(VarlenArgs 
   const uint32_t tid = threadIdx.x;
   uint32_t* s_fo = reinterpret_cast<uint32_t*>(lds);                    // [T + 1]
   unsigned char* img = lds + ((4u * (T + 1u) + 15u) & ~15u);            // the run, then a guard
-  const uint64_t p0 = (uint64_t)blockIdx.x * T;
+  const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint32_t Tv = a.n - p0 < T ? (uint32_t)(a.n - p0) : T;
   const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
   const uint64_t total = frames_limit(a);
