@@ -249,7 +249,8 @@ struct Tuning {
   // for packed batches whose mean payload hint is under this many bytes (0: off),
   // and its packets per thread (1, 2, 4, 8: tiles of 256 * fpt packets).
   std::atomic<int> varlen_small{16};
-  std::atomic<int> varlen_small_fpt{4};
+  std::atomic<int> varlen_small_fpt{0};  // 0: 4 for hints up to 4 B, 2 above (profiles/r02/sweeps/small.json)
+  std::atomic<int> varlen_small_fused{1};  // the framing kernel finds its own base (no pass-2 launch)
   // Fixed-length encode: batches of more packets than this go out as several
   // launches of at most this many (0: one launch).
   std::atomic<int> encode_launch_packets{0};

@@ -25,10 +25,6 @@ namespace rudp {
 constexpr uint32_t kScanItems = 8;                     // per thread
 constexpr uint32_t kScanBlockItems = kBlock * kScanItems;  // 2048 per block
 
-// Status bits of a block live above bit 56 of its block sum (a sum of at
-// most 2048 x (2^32 - 1 + 7) fits in 44 bits).
-constexpr int kSumBitsShift = 56;
-constexpr uint64_t kSumMask = (1ull << kSumBitsShift) - 1ull;
 
 // ITEMS packets per thread: a block sums kBlock * ITEMS lengths (8 for the
 // offset scan; the small-frame encode uses its own tile size).

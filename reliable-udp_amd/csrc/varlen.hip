@@ -1116,8 +1116,16 @@ __host__ __device__ inline uint32_t small_lds_off_out(uint32_t T, uint32_t cap) 
 }
 __host__ __device__ inline uint32_t small_out_cap(uint32_t T, uint32_t cap, uint32_t H) { return cap + T * H + 16u; }
 
-template <int H, uint32_t FPT>
-__global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs a, const uint64_t* bases) {
+// FUSED: `sums` are the raw pass-1 block sums (with their status bits) and
+// every block finds its own base (the sum of the sums before it) and the
+// status from all of them -- nb <= kSmallFusedTiles, so that is a few KiB of
+// L2 reads per block -- instead of a one-workgroup pass between the two
+// launches.  Otherwise `sums` are pass 2's exclusive bases.
+constexpr uint64_t kSmallFusedTiles = 2048;
+
+template <int H, uint32_t FPT, bool FUSED>
+__global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs a, const uint64_t* sums,
+                                                                     uint64_t nb, ScanCheck chk) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   constexpr uint32_t T = kBlock * FPT;
   const uint32_t tid = threadIdx.x;
@@ -1130,13 +1138,58 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
   uint8_t* s_flags = reinterpret_cast<uint8_t*>(s_cs + T);
   unsigned char* pay = lds + small_lds_off_pay(T);
   unsigned char* img = lds + small_lds_off_out(T, cap);
+  __shared__ uint64_t s_wave[kBlock / 64];
 
-  const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
+  const uint64_t tile = a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+  const uint64_t p0 = tile * T;
   const uint32_t Tv = a.n - p0 < T ? (uint32_t)(a.n - p0) : T;
-  const uint64_t tile = p0 / T;
-  const uint64_t fo0 = bases[tile];
-  const uint64_t fo_end = p0 + T < a.n ? bases[tile + 1] : a.frame_off[a.n];
-  if (call_failed(a.status)) return;
+  uint64_t fo0, fo_end;
+  if (FUSED) {
+    __shared__ uint64_t s_pre[kBlock / 64], s_all[kBlock / 64];
+    __shared__ uint32_t s_bits;
+    if (tid == 0) s_bits = 0;
+    uint64_t pre = 0, all = 0;
+    uint32_t bits = 0;
+    for (uint64_t c = tid; c < nb; c += kBlock) {
+      const uint64_t v = sums[c];
+      all += v & kSumMask;
+      pre += c < tile ? (v & kSumMask) : 0u;
+      bits |= (uint32_t)(v >> kSumBitsShift);
+    }
+    for (int m = 32; m > 0; m >>= 1) {
+      pre += __shfl_xor(pre, m, 64);
+      all += __shfl_xor(all, m, 64);
+    }
+    __syncthreads();  // s_bits initialised
+    if (bits) atomicOr(&s_bits, bits);
+    if ((tid & 63u) == 0) {
+      s_pre[tid >> 6] = pre;
+      s_all[tid >> 6] = all;
+    }
+    __syncthreads();
+    pre = all = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < kBlock / 64; ++w) {
+      pre += s_pre[w];
+      all += s_all[w];
+    }
+    uint32_t st = s_bits;
+    if (chk.status) {
+      if (!chk.payload_off && all - a.n * (uint64_t)H != chk.payload_bytes) st |= RUDP_ST_PAYLOAD;
+      if (all > chk.frames_cap) st |= RUDP_ST_FRAMES_CAP;
+    }
+    if (tile == 0 && tid == 0) {
+      const_cast<uint64_t*>(a.frame_off)[a.n] = all;
+      if (chk.status) *chk.status = st;
+    }
+    if (chk.status && st) return;  // uniform: every block computes the same status
+    fo0 = pre;
+    fo_end = pre + (sums[tile] & kSumMask);
+  } else {
+    fo0 = sums[tile];
+    fo_end = p0 + T < a.n ? sums[tile + 1] : a.frame_off[a.n];
+    if (call_failed(a.status)) return;
+  }
   const uint64_t po0 = fo0 - p0 * (uint64_t)H, po_end = fo_end - (p0 + Tv) * (uint64_t)H;
   const uint64_t A = po0 & ~15ull, OA = fo0 & ~15ull;
   const uint64_t prun = ((po_end + 15u) & ~15ull) - A;
@@ -1185,7 +1238,6 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
   __syncthreads();
 
   // ---- the scan's last pass: tile-relative offsets, frame_off ---------------
-  __shared__ uint64_t s_wave[kBlock / 64];
   {
     uint32_t mine = 0;
 #pragma unroll
@@ -1266,16 +1318,22 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
 }
 
 template <int H, uint32_t FPT>
-int launch_small_fpt(const VarlenArgs& args, const uint64_t* bases, uint64_t nb, hipStream_t stream) {
+int launch_small_fpt(const VarlenArgs& args, const uint64_t* sums, uint64_t nb, const ScanCheck& chk,
+                     bool fused, hipStream_t stream) {
   constexpr uint32_t T = kBlock * FPT;
   const size_t lds = small_lds_off_out(T, args.small_cap) + small_out_cap(T, args.small_cap, H) + 32u;
+  const void* fn = fused ? reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT, true>)
+                         : reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT, false>);
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL((encode_varlen_small_kernel<H, FPT>), dim3((uint32_t)nb), dim3(kBlock), lds, stream, args,
-                     bases);
+  if (fused)
+    hipLaunchKernelGGL((encode_varlen_small_kernel<H, FPT, true>), dim3((uint32_t)nb), dim3(kBlock), lds, stream,
+                       args, sums, nb, chk);
+  else
+    hipLaunchKernelGGL((encode_varlen_small_kernel<H, FPT, false>), dim3((uint32_t)nb), dim3(kBlock), lds,
+                       stream, args, sums, nb, chk);
   return (int)hipGetLastError();
 }
 
@@ -1287,17 +1345,22 @@ int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int
   uint64_t* sums = nullptr;
   hipError_t e = stream_alloc(reinterpret_cast<void**>(&sums), nb * sizeof(uint64_t), stream);
   if (e != hipSuccess) return (int)e;
+  // pass 1, then either the framing kernel finds its own base (two launches)
+  // or pass 2 runs between them (three)
+  const bool fused = tuning().varlen_small_fused && nb <= kSmallFusedTiles;
   scan_block_sums(args.len, args.n, (uint32_t)layout, fpt, sums, chk, stream);
-  scan_block_bases(sums, nb, const_cast<uint64_t*>(args.frame_off), args.n, (uint32_t)layout, chk, stream);
+  if (!fused) scan_block_bases(sums, nb, const_cast<uint64_t*>(args.frame_off), args.n, (uint32_t)layout, chk, stream);
   int rc;
   if (layout == 7)
-    rc = fpt == 1 ? launch_small_fpt<7, 1>(args, sums, nb, stream)
-       : fpt == 2 ? launch_small_fpt<7, 2>(args, sums, nb, stream)
-       : fpt == 4 ? launch_small_fpt<7, 4>(args, sums, nb, stream) : launch_small_fpt<7, 8>(args, sums, nb, stream);
+    rc = fpt == 1 ? launch_small_fpt<7, 1>(args, sums, nb, chk, fused, stream)
+       : fpt == 2 ? launch_small_fpt<7, 2>(args, sums, nb, chk, fused, stream)
+       : fpt == 4 ? launch_small_fpt<7, 4>(args, sums, nb, chk, fused, stream)
+                  : launch_small_fpt<7, 8>(args, sums, nb, chk, fused, stream);
   else
-    rc = fpt == 1 ? launch_small_fpt<5, 1>(args, sums, nb, stream)
-       : fpt == 2 ? launch_small_fpt<5, 2>(args, sums, nb, stream)
-       : fpt == 4 ? launch_small_fpt<5, 4>(args, sums, nb, stream) : launch_small_fpt<5, 8>(args, sums, nb, stream);
+    rc = fpt == 1 ? launch_small_fpt<5, 1>(args, sums, nb, chk, fused, stream)
+       : fpt == 2 ? launch_small_fpt<5, 2>(args, sums, nb, chk, fused, stream)
+       : fpt == 4 ? launch_small_fpt<5, 4>(args, sums, nb, chk, fused, stream)
+                  : launch_small_fpt<5, 8>(args, sums, nb, chk, fused, stream);
   e = stream_free(sums, stream);
   return rc ? rc : (int)e;
 }

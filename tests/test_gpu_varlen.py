@@ -783,8 +783,9 @@ def test_small_frame_tiles_vs_oracle(cuda, fpt):
         for layout in (5, 7):
             want, off, cs = codec_np.encode_varlen(seq, ack, flags, pays, layout)
             results = []
-            for small in (16, 0):  # the small-frame kernels, then the vector kernels
-                old = (lib.rudpx_tune(46, small), lib.rudpx_tune(47, fpt))
+            # the small-frame kernels (own tile bases, then after the pass-2 launch), then the vector kernels
+            for small, fused in ((16, 1), (16, 0), (0, 1)):
+                old = (lib.rudpx_tune(46, small), lib.rudpx_tune(47, fpt), lib.rudpx_tune(50, fused))
                 try:
                     r = batch.pack_batch_varlen((dev(seq, cuda), dev(ack, cuda), dev(flags, cuda)), dev(pay, cuda),
                                                 dev(lens, cuda), layout, want_csum=True, check=False).check()
@@ -800,11 +801,12 @@ def test_small_frame_tiles_vs_oracle(cuda, fpt):
                 finally:
                     lib.rudpx_tune(46, old[0])
                     lib.rudpx_tune(47, old[1])
-                ctx = (fpt, n, layout, small)
+                    lib.rudpx_tune(50, old[2])
+                ctx = (fpt, n, layout, small, fused)
                 assert np.array_equal(host(r.frames), want), ctx
                 assert np.array_equal(host(r.frame_off), off) and np.array_equal(host(r.csum), cs), ctx
                 exp = codec_np.decode_varlen(want, off, layout, cs if layout == 5 else None)
                 for g, e in zip((d.seq, d.ack, d.flags, d.ok, d.csum), exp):
                     assert np.array_equal(host(g), e), ctx
                 results.append(host(r.frames))
-            assert np.array_equal(results[0], results[1])
+            assert np.array_equal(results[0], results[1]) and np.array_equal(results[0], results[2])
