@@ -446,7 +446,7 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, ui
                  ((reinterpret_cast<uintptr_t>(d_seq) | reinterpret_cast<uintptr_t>(d_ack) |
                    reinterpret_cast<uintptr_t>(d_flags) | reinterpret_cast<uintptr_t>(d_ok) |
                    reinterpret_cast<uintptr_t>(d_csum_out_or_null)) & 3u) == 0) ? 1u : 0u;
-  a.xcd = tuning().tile_xcd ? 1u : 0u;
+  a.xcd = (tuning().tile_xcd && frame_len >= 128u) ? 1u : 0u;
   a.frames = d_frames;
   a.csum_in = d_csum_in_or_null;
   a.seq = d_seq;

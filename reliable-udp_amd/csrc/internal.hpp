@@ -156,8 +156,13 @@ struct Tuning {
   // 16M x 1472 B 0.540 -> 0.481 ms per 2^20 packets, 1M x 1472 B 0.518 ->
   // 0.513 ms (tools/launch_split.py, profiles/r02/sweeps/launch_split.json).
   std::atomic<int> encode_xcd_swizzle{1};
-  // The same order for the decode, varlen and UTF-8 tile kernels.
-  std::atomic<int> tile_xcd{0};
+  // The same order for the decode, varlen and UTF-8 tile kernels: fixed decode
+  // verify 1M x 1472 B 0.240 -> 0.218 ms, x 1024 B 0.170 -> 0.154; copy-out
+  // 1472 B 0.523 -> 0.504; varlen decode 1479 B 0.266 -> 0.230, ragged [0, 2944]
+  // 0.306 -> 0.284; varlen encode 1472 B 0.587 -> 0.557; 256 B and below
+  // within noise, fixed copy-out at 64 B 5% slower, so the fixed decode keeps
+  // it off below 128-B frames (profiles/r02/sweeps/tile_xcd_*.json).
+  std::atomic<int> tile_xcd{1};
   std::atomic<int> encode_contig{1};  // phase 1 streams the tile contiguously, sums from LDS
   std::atomic<int> encode_block{256};  // tile workgroup size (64, 128 when T <= block; 256, 512, 1024)
   std::atomic<int> decode_copy_tile{1};  // copy-out decode through an LDS tile (0: register windows)
