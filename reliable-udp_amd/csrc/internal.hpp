@@ -91,7 +91,8 @@ struct VarlenArgs {
   uint32_t tile_cap;
   uint32_t align64;               // tile kernel: wave stores start on 64-B sector boundaries
   uint32_t early_table;           // tile kernel: header-table loads before phase 1
-  uint32_t ablate;                // diagnostics only (wrong output): 1 = phase 2 without the frame walk
+  uint32_t ablate;                // diagnostics only (wrong output): 1 = phase 2 without the frame walk,
+                                  // 2 = no sum pass, 4 = tiles over their LDS budget do nothing
   uint32_t vhc;                   // tile kernel: prebuilt header chunks + pure-chunk fast phase 2
   uint32_t hc_off;                // LDS byte offset of the header-chunk array (set by the launcher)
   uint32_t early_fo;              // tile kernels: the tile's frame offsets loaded before phase 1

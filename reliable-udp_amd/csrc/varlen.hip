@@ -285,6 +285,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   const uint64_t A = po0 & ~15ull;
   const uint64_t run = ((po_end + 15u) & ~15ull) - A;
   if (run > cap) {  // uniform over the workgroup
+    if (a.ablate & 4u) return;  // diagnostic (wrong output): overflowing tiles do nothing
     encode_varlen_packet<H>(a, p0 + q, q < Tv, g, glog);
     return;
   }
@@ -333,7 +334,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
     const uint32_t Lq = fe - fs - H;
     const uint32_t d = shift + fs - q * H;  // LDS offset of the packet's first payload byte
-    if (Lq) {
+    if (Lq && !(a.ablate & 2u)) {  // ablate bit 2 (diagnostic, wrong output): no sum pass
       const u32x4* pay16 = reinterpret_cast<const u32x4*>(lds_pay);
       const uint32_t c1 = (d + Lq - 1u) >> 4;
       for (uint32_t c = (d >> 4) + g; c <= c1; c += G) {

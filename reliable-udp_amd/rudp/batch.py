@@ -165,8 +165,12 @@ def _dev_check(t, name, dtype, ndim, device):
 
 def _stream_ptr(stream, device) -> int:
     import torch
-    s = stream if stream is not None else torch.cuda.current_stream(device)
-    return int(s.cuda_stream)
+    if stream is not None:
+        return int(stream.cuda_stream)
+    raw = getattr(torch._C, "_cuda_getCurrentRawStream", None)  # no Stream object per call
+    if raw is not None:
+        return int(raw(device.index if device.index is not None else torch.cuda.current_device()))
+    return int(torch.cuda.current_stream(device).cuda_stream)
 
 
 def _pack_device(tab: HeaderTable, payloads, H: int, out, csum_out, want_csum, stream):
@@ -438,9 +442,10 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
         frames = torch.empty((lsum + n * H,), dtype=torch.uint8, device=dev)
     if want_csum is None:
         want_csum = H == 5
-    frame_off = torch.empty((n + 1,), dtype=torch.int64, device=dev)
+    aux = torch.empty((n + 2,), dtype=torch.int64, device=dev)  # frame_off [n + 1] | status
+    frame_off = aux[:n + 1]
+    status = aux[n + 1:].view(torch.int32)[:1]
     csum = torch.empty((n,), dtype=torch.uint16, device=dev) if want_csum else None
-    status = torch.empty((1,), dtype=torch.int32, device=dev)
     # payload_len carries the mean payload length: a hint that picks lanes per packet
     b = _native.RudpBatch(n=n, payload_len=min(lsum // n, 65535) if n else 0, reserved=0,
                           seq=tab.seq.data_ptr(), ack=tab.ack.data_ptr(), flags=tab.flags.data_ptr(),
@@ -494,12 +499,11 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
         _dev_check(csum, "csum", torch.uint16, 1, dev)
         if csum.shape[0] != n:
             raise ValueError(f"csum has {csum.shape[0]} entries for {n} frames")
-    seq = torch.empty((n,), dtype=torch.uint16, device=dev)
-    ack = torch.empty((n,), dtype=torch.uint16, device=dev)
-    flags = torch.empty((n,), dtype=torch.uint8, device=dev)
-    ok = torch.empty((n,), dtype=torch.uint8, device=dev)
-    cs = torch.empty((n,), dtype=torch.uint16, device=dev)
-    status = torch.empty((1,), dtype=torch.int32, device=dev)
+    # one allocation for every output: seq | ack | csum (u16) | flags | ok (u8) | status (i32)
+    out = torch.empty((8 * n + 8,), dtype=torch.uint8, device=dev)
+    seq, ack, cs = (out[k * 2 * n:(k + 1) * 2 * n].view(torch.uint16) for k in range(3))
+    flags, ok = out[6 * n:7 * n], out[7 * n:8 * n]
+    status = out[8 * n:8 * n + 4].view(torch.int32)
     # mean frame length from the buffer size: a hint that picks lanes / tiles per frame
     hint = min(frames.numel() // n, 0xFFFFFFFF) if n else 0
     _native.check(_native.lib().rudp_decode_varlen_checked(

@@ -461,6 +461,62 @@ def small_sweep(reps):
     return out
 
 
+def ragged_sweep(reps):
+    """Where ragged varlen encode loses (lengths uniform in [0, 2944], mean
+    1472, against equal 1472-B lengths): stage ablations of the tile kernel
+    (key 35: 2 = no sum pass, 4 = overflowing tiles skipped; wrong output, so
+    not checked) and LDS budgets (key 39), through the sync-free C ABI.
+    Also counts the tiles whose payload run exceeds the default budget."""
+    import ctypes
+    dev = torch.device("cuda", 0)
+    stream = torch.cuda.current_stream().cuda_stream
+    n, H = 1 << 20, 7
+    out = {}
+    torch.manual_seed(11)
+    for shape in ("U0-2944", "L1472"):
+        lens = (torch.randint(0, 2945, (n,), dtype=torch.int32, device=dev) if shape[0] == "U"
+                else torch.full((n,), 1472, dtype=torch.int32, device=dev))
+        total = int(lens.sum().item())
+        tab, pay = batch.synth_batch(n, 2944, 0x5EED000C, device=dev)
+        flat = pay.view(-1)[:total].contiguous()
+        del pay
+        frames = torch.empty(total + n * H, dtype=torch.uint8, device=dev)
+        off = torch.empty(n + 1, dtype=torch.int64, device=dev)
+        st = torch.empty(1, dtype=torch.int32, device=dev)
+        b = _native.RudpBatch(n=n, payload_len=total // n, reserved=0, seq=tab.seq.data_ptr(),
+                              ack=tab.ack.data_ptr(), flags=tab.flags.data_ptr(), payload=flat.data_ptr(),
+                              len=lens.data_ptr(), payload_off=None)
+
+        def enc():
+            _native.check(lib.rudp_encode_varlen_checked(ctypes.byref(b), total, frames.data_ptr(),
+                                                         frames.numel(), off.data_ptr(), None, st.data_ptr(),
+                                                         H, 0, stream))
+        specs = {"default": (), "no_sums": ((35, 2),), "skip_overflow": ((35, 4),),
+                 "no_sums_skip_overflow": ((35, 6),), "cap125": ((39, 125),), "cap150": ((39, 150),),
+                 "cap200": ((39, 200),), "no_hchunk": ((36, 0),)}
+        variants = {}
+        for name, kv in specs.items():
+            def setup(kv=kv):
+                for k, v in ((35, 0), (39, 110), (36, 2)):
+                    lib.rudpx_tune(k, v)
+                for k, v in kv:
+                    lib.rudpx_tune(k, v)
+            variants[f"{shape}_{name}"] = (setup, enc)
+        res = interleaved(variants, reps)
+        for k, v in ((35, 0), (39, 110), (36, 2)):
+            lib.rudpx_tune(k, v)
+        # tiles of 16 packets whose payload run exceeds 1.1x the hinted run (+ alignment slack)
+        runs = lens[: (n // 16) * 16].view(-1, 16).sum(1)
+        over = float((runs > (16 * (total // n) * 110 // 100 + 256 - 32)).float().mean().item())
+        alg = n * (2 * (total / n + H) + 12)
+        for k, ms in res.items():
+            out[k] = {"ms": ms, "frac": alg / ms / 1e9 / 8.0}
+        out[f"{shape}_overflow_tile_fraction"] = over
+        del tab, flat, lens, frames, off
+        torch.cuda.empty_cache()
+    return out
+
+
 def decode_sweep(reps):
     dev = torch.device("cuda", 0)
     out = {}
@@ -750,7 +806,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=15)
     ap.add_argument("--L", type=int, default=1472, help="payload length for --only ablate")
-    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "small", "align", "knob", "copydma", "multi", "opsknob", "vdec", "vknob"])
+    ap.add_argument("--only", choices=["encode", "decode", "copy", "ablate", "varlen", "varlen_enc", "utf8", "small", "ragged", "align", "knob", "copydma", "multi", "opsknob", "vdec", "vknob"])
     ap.add_argument("--blocks", type=str, default="", help="encode sweep: workgroup sizes, e.g. 256,512,1024")
     ap.add_argument("--encode-L", type=str, default="", help="encode sweep: payload lengths, e.g. 1472")
     ap.add_argument("--percu", type=str, default="", help="encode sweep: tiles-per-CU caps, e.g. 3,4,5")
@@ -775,6 +831,8 @@ def main():
         result["copy"] = copy_sweep(args.reps)
     if args.only in (None, "decode"):
         result["decode"] = decode_sweep(args.reps)
+    if args.only == "ragged":
+        result["ragged"] = ragged_sweep(args.reps)
     if args.only == "small":
         result["small"] = small_sweep(args.reps)
     if args.only == "utf8":
