@@ -257,8 +257,34 @@ def legs(torch, batch, device, steps):
         "GiB_s": (1 << 20) * 1472 / (ms / 1e3) / GIB, "ms": ms,
         "roofline_frac": (1 << 20) * (algorithmic_bytes_encode(1472) + algorithmic_bytes_decode(1472))
         / (ms / 1e3) / 1e9 / HBM_PEAK_GBS}
-    # BASELINE config 5's shape on one GPU: 16M x 1472 B (23.6 GB in, 23.7 GB out)
+    # end to end from pinned host memory: H2D -> encode -> D2H, two-stream pipeline
+    # (rudp_encode_host); PCIe-bound, recorded in DESIGN.md, never the headline
+    n, L = 1 << 20, 1472
     del w
+    torch.cuda.empty_cache()
+    tab, pay = batch.synth_batch(n, L, SEEDS[L], device=device)
+    pin = lambda shape, dt: torch.empty(shape, dtype=dt, pin_memory=True)  # noqa: E731
+    hp, hs, ha, hf = pin((n, L), torch.uint8), pin((n,), torch.uint16), pin((n,), torch.uint16), pin((n,), torch.uint8)
+    hp.copy_(pay)
+    hs.copy_(tab.seq)
+    ha.copy_(tab.ack)
+    hf.copy_(tab.flags)
+    hout = pin((n, L + 7), torch.uint8)
+    torch.cuda.synchronize()
+    del tab, pay
+    args = ((hs.numpy(), ha.numpy(), hf.numpy()), hp.numpy())
+    batch.pack_batch(*args, "rudp7", out=hout.numpy())
+    reps = 3
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        batch.pack_batch(*args, "rudp7", out=hout.numpy())
+    dt = (time.perf_counter() - t0) / reps
+    out["e2e_host_encode_1Mx1472"] = {
+        "GiB_s": n * L / dt / GIB, "ms": dt * 1e3,
+        "pcie_GBs_each_way": n * (L + 6) / dt / 1e9,
+        "note": "pinned host in/out, rudp_encode_host (H2D, kernel, D2H on two streams)"}
+    del hp, hs, ha, hf, hout
+    # BASELINE config 5's shape on one GPU: 16M x 1472 B (23.6 GB in, 23.7 GB out)
     torch.cuda.empty_cache()
     w16 = Workload(torch, batch, C5_PACKETS, 1472, "rudp7", 0, C5_SEED, device, min_bytes=0)
     ts = sorted(time_events(torch, lambda i: w16.encode(batch, i), max(10, steps // 2), 3))
@@ -396,30 +422,6 @@ def legs(torch, batch, device, steps):
     out["d2d_copy_gridstride_GBs"] = 2 * a.numel() / (ms_gs / 1e3) / 1e9
     del w, a, b
     torch.cuda.empty_cache()
-    # end to end from pinned host memory: H2D -> encode -> D2H, two-stream pipeline
-    # (rudp_encode_host); PCIe-bound, recorded in DESIGN.md, never the headline
-    n, L = 1 << 20, 1472
-    tab, pay = batch.synth_batch(n, L, SEEDS[L], device=device)
-    pin = lambda shape, dt: torch.empty(shape, dtype=dt, pin_memory=True)  # noqa: E731
-    hp, hs, ha, hf = pin((n, L), torch.uint8), pin((n,), torch.uint16), pin((n,), torch.uint16), pin((n,), torch.uint8)
-    hp.copy_(pay)
-    hs.copy_(tab.seq)
-    ha.copy_(tab.ack)
-    hf.copy_(tab.flags)
-    hout = pin((n, L + 7), torch.uint8)
-    torch.cuda.synchronize()
-    del tab, pay
-    args = ((hs.numpy(), ha.numpy(), hf.numpy()), hp.numpy())
-    batch.pack_batch(*args, "rudp7", out=hout.numpy())
-    reps = 3
-    t0 = time.perf_counter()
-    for _ in range(reps):
-        batch.pack_batch(*args, "rudp7", out=hout.numpy())
-    dt = (time.perf_counter() - t0) / reps
-    out["e2e_host_encode_1Mx1472"] = {
-        "GiB_s": n * L / dt / GIB, "ms": dt * 1e3,
-        "pcie_GBs_each_way": n * (L + 6) / dt / 1e9,
-        "note": "pinned host in/out, rudp_encode_host (H2D, kernel, D2H on two streams)"}
     return out
 
 

@@ -154,9 +154,9 @@ struct Tuning {
   std::atomic<int> encode_blocks_per_cu{-1};  // cap resident tiles per CU via LDS reservation; 0 = natural, -1 = auto
   std::atomic<int> decode_glog{-1};   // verify kernel lanes-per-packet log2; -1 = automatic
   // XCD-contiguous tile order (xcd_tile) for the fixed-length encode tile:
-  // 16M x 1472 B 0.540 -> 0.481 ms per 2^20 packets, 1M x 1472 B 0.518 ->
-  // 0.513 ms (tools/launch_split.py, profiles/r02/sweeps/launch_split.json).
-  std::atomic<int> encode_xcd_swizzle{1};
+  // 1 on, 0 off, -1 from 512-B payloads (16M x 1472 B 0.540 -> 0.481 ms per
+  // 2^20 packets; tools/launch_split.py, profiles/r02/sweeps/launch_split.json).
+  std::atomic<int> encode_xcd_swizzle{-1};
   // The same order for the decode, varlen and UTF-8 tile kernels: fixed decode
   // verify 1M x 1472 B 0.240 -> 0.218 ms, x 1024 B 0.170 -> 0.154; copy-out
   // 1472 B 0.523 -> 0.504; varlen decode 1479 B 0.266 -> 0.230, ragged [0, 2944]

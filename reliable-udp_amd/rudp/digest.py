@@ -47,6 +47,12 @@ def chunk_sha256(frames, csum=None, chunk: int = 1 << 20, workers: int = 8
         for item in busy:
             if item is not None:
                 out_frames[item[0]] = item[1].result()
+    del bufs
+    # hand the pinned slots back to the OS: kept in torch's host cache, GBs of
+    # pinned pages slowed later pinned copies in the same process (bench e2e leg)
+    empty = getattr(torch._C, "_host_emptyCache", None)
+    if empty is not None:
+        empty()
     out_cs: List[Optional[str]] = [None] * nchunks
     if csum is not None:
         cs = csum.cpu().numpy().astype("<u2")
