@@ -28,8 +28,11 @@
  *  - The *_host variants take host pointers and are synchronous.
  *  - Return 0 on success or a negative code (RUDP_E*); the message for the
  *    calling thread is available from rudp_last_error().
- *  - Reentrant and thread-safe: the only global state is a mutex-guarded
- *    per-device cache of streams and staging buffers used by *_host calls.
+ *  - Reentrant and thread-safe: the global state is mutex-guarded per-device
+ *    caches (the *_host staging pipeline, the stream-ordered scratch pool,
+ *    the bounds scratch) plus the non-ABI experiment knobs of rudpx_tune,
+ *    which are atomics (a launch concurrent with a knob change may see old
+ *    and new settings mixed; the knobs are for sweeps, not for callers).
  */
 #ifndef RUDP_H_
 #define RUDP_H_
