@@ -592,10 +592,36 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
     if (rc) return hip_fail((hipError_t)rc, "small-frame varlen encode launch");
     return 0;
   }
-  rc = scan_frame_offsets(in->len, in->n, (uint32_t)layout, d_frame_off, chk, s);
-  if (rc) return hip_fail((hipError_t)rc, "frame offset scan");
-  rc = launch_encode_varlen(a, layout, s);
-  if (rc) return hip_fail((hipError_t)rc, "varlen encode launch");
+  // Tiles by payload bytes (checked calls, where the payload size is known on
+  // the host): spans of S = budget - 2 * hint - 64 bytes, so a tile overflows its
+  // LDS budget only through a packet over twice the hint; at most tile_T
+  // packets per tile in LDS (more take the per-packet path).
+  SpanStarts spans{};
+  if (tuning().varlen_btile && chk.status && !in->payload_off && a.tile_T && aligned16(in->payload) &&
+      aligned16(d_frames)) {
+    const uint64_t h = in->payload_len ? in->payload_len : 1u;
+    if (a.tile_cap > 2u * h + 64u + h) {
+      const uint64_t S = a.tile_cap - 2u * h - 64u;
+      uint64_t slots = 4;
+      while (slots < 256 && slots < 3u * S / (2u * h) + 2u) slots <<= 1;
+      spans.bytes = S;
+      spans.count = chk.payload_bytes / S + 1u;
+      void* buf = nullptr;
+      RUDP_HIP(stream_alloc(&buf, (spans.count + 1u) * sizeof(uint32_t), s));
+      spans.start = static_cast<uint32_t*>(buf);
+      a.span_start = spans.start;
+      a.span_count = spans.count;
+      a.tile_T = (uint32_t)slots;
+      a.tile_glog = 0;
+    }
+  }
+  rc = scan_frame_offsets(in->len, in->n, (uint32_t)layout, d_frame_off, chk, s, spans);
+  if (!rc) rc = launch_encode_varlen(a, layout, s);
+  if (spans.start) {
+    const hipError_t e = stream_free(spans.start, s);
+    if (!rc && e != hipSuccess) return hip_fail(e, "hipFreeAsync");
+  }
+  if (rc) return hip_fail((hipError_t)rc, "varlen encode");
   return 0;
 }
 

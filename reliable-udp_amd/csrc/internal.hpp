@@ -109,6 +109,11 @@ struct VarlenArgs {
   uint32_t small_fpt;             // decode small-frame tile: frames per thread (0: not used)
   uint32_t small_cap;             // its LDS run budget in bytes
   uint32_t xcd;                   // tile kernels: XCD-contiguous tile order (xcd_tile)
+  // Byte-tiled encode: workgroup k frames the packets whose payload starts in
+  // [k*S, (k+1)*S) (span_start[k] .. span_start[k+1], from the scan), span_count
+  // workgroups; tile_T is then the most packets a tile holds in LDS, glog 0.
+  const uint32_t* span_start;
+  uint64_t span_count;
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -260,6 +265,10 @@ struct Tuning {
   // Fixed-length encode: batches of more packets than this go out as several
   // launches of at most this many (0: one launch).
   std::atomic<int> encode_launch_packets{0};
+  // Varlen encode tiles by payload bytes (spans from the scan) instead of by
+  // packet count: no tile overflows short of one packet past the budget's
+  // slack, and the sum pass is chunk-parallel (0: packet-count tiles).
+  std::atomic<int> varlen_btile{0};
   std::atomic<int> host_slots{3};     // *_host pipeline: device staging slots (2..8)
   std::atomic<int> host_stage_mb{128};  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
 };
@@ -311,10 +320,17 @@ void scan_block_bases(uint64_t* sums, uint64_t nb, uint64_t* d_frame_off, uint64
 // two passes, then one kernel per tile of kBlock * fpt packets that writes the
 // tile's offsets and assembles its frames in LDS.
 int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int layout, hipStream_t stream);
+// Span starts for the byte-tiled varlen encode: start[k] (k = 0 .. count) is
+// the first packet whose packed payload starts at or after k * bytes.
+struct SpanStarts {
+  uint32_t* start;  // [count + 1], or null
+  uint64_t bytes;
+  uint64_t count;
+};
 int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
-                             const ScanCheck& chk, hipStream_t stream);
+                             const ScanCheck& chk, hipStream_t stream, const SpanStarts& spans = SpanStarts{});
 int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
-                       const ScanCheck& chk, hipStream_t stream);
+                       const ScanCheck& chk, hipStream_t stream, const SpanStarts& spans = SpanStarts{});
 // frame_off[0..n] non-decreasing and inside [0, frames_bytes]: writes
 // *d_status = 0 or RUDP_ST_OFFSETS, asynchronously (bounds.hip).
 int check_frame_offsets(const uint64_t* d_frame_off, uint64_t n, uint64_t frames_bytes, uint32_t* d_status,

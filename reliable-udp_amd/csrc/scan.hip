@@ -103,8 +103,12 @@ __global__ void __launch_bounds__(1024) scan_block_bases_kernel(uint64_t* sums, 
   }
 }
 
+// With spans.start: the packed payload splits into spans of S bytes, and
+// spans.start[k] = the first packet whose payload starts at or after k*S
+// (n for spans after the last packet's start), k = 0 .. spans.count.
 __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len, uint64_t n, uint32_t H,
-                                                            const uint64_t* bases, uint64_t* frame_off) {
+                                                            const uint64_t* bases, uint64_t* frame_off,
+                                                            SpanStarts spans) {
   __shared__ uint32_t s_len[kScanBlockItems];
   __shared__ uint64_t s_off[kScanBlockItems];
   __shared__ uint64_t s_wave[kBlock / 64];
@@ -133,6 +137,26 @@ __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len,
     const uint32_t k = j * kBlock + threadIdx.x;
     if (base + k < n) frame_off[base + k] = s_off[k];
   }
+  if (spans.start) {
+    const uint64_t S = spans.bytes, K = spans.count;
+#pragma unroll
+    for (uint32_t j = 0; j < kScanItems; ++j) {
+      const uint32_t k = j * kBlock + threadIdx.x;
+      const uint64_t p = base + k;
+      if (p >= n) continue;
+      const uint64_t po = s_off[k] - p * H;  // packed payload offset of packet p
+      uint64_t lo = 0;
+      if (p > 0) {
+        const uint64_t prev_len = k > 0 ? s_len[k - 1] - H : len[p - 1];
+        lo = (po - prev_len) / S + 1;  // spans after the one the previous packet starts in
+      }
+      uint64_t hi = po / S;
+      if (hi > K) hi = K;
+      for (uint64_t t = lo; t <= hi; ++t) spans.start[t] = (uint32_t)p;
+      if (p == n - 1)
+        for (uint64_t t = (po / S + 1 > lo ? po / S + 1 : lo); t <= K; ++t) spans.start[t] = (uint32_t)n;
+    }
+  }
 }
 
 void scan_block_sums(const uint32_t* d_len, uint64_t n, uint32_t H, uint32_t items, uint64_t* sums,
@@ -153,7 +177,7 @@ void scan_block_bases(uint64_t* sums, uint64_t nb, uint64_t* d_frame_off, uint64
 }
 
 int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
-                             const ScanCheck& chk, hipStream_t stream) {
+                             const ScanCheck& chk, hipStream_t stream, const SpanStarts& spans) {
   const uint64_t nb = (n + kScanBlockItems - 1) / kScanBlockItems;
   uint64_t* sums = nullptr;
   hipError_t e = stream_alloc(reinterpret_cast<void**>(&sums), nb * sizeof(uint64_t), stream);
@@ -161,7 +185,7 @@ int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint
   scan_block_sums(d_len, n, H, kScanItems, sums, chk, stream);
   scan_block_bases(sums, nb, d_frame_off, n, H, chk, stream);
   hipLaunchKernelGGL(scan_apply_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, stream, d_len, n, H, sums,
-                     d_frame_off);
+                     d_frame_off, spans);
   e = hipGetLastError();
   hipError_t e2 = stream_free(sums, stream);
   if (e != hipSuccess) return (int)e;

@@ -260,7 +260,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // tile bytes; 46: small-frame varlen encode below this hint (0 = off); 47: its
 // packets per thread; 48: fixed-length encode packets per launch (0 = one launch);
 // 49: XCD-contiguous tile order in the decode / varlen / UTF-8 tile kernels;
-// 50: small-frame encode finds its tile bases itself (no pass-2 launch).
+// 50: small-frame encode finds its tile bases itself (no pass-2 launch);
+// 51: varlen encode tiles by payload bytes.
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
@@ -294,7 +295,8 @@ int rudpx_tune(int key, int value) {
             : key == 47 ? &t.varlen_small_fpt
             : key == 48 ? &t.encode_launch_packets
             : key == 49 ? &t.tile_xcd
-            : key == 50 ? &t.varlen_small_fused : nullptr;
+            : key == 50 ? &t.varlen_small_fused
+            : key == 51 ? &t.varlen_btile : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }

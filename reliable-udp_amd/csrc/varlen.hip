@@ -233,6 +233,108 @@ __host__ __device__ inline uint32_t vt_pay_off(uint32_t T, uint32_t cap, uint32_
   return (8u * T + 4u * (T + 1u) + vt_map_bytes(T, cap, H, wide) + 15u) & ~15u;
 }
 
+// Byte tiles, the sum pass: lane t takes a contiguous range of the run's
+// aligned 16-B chunks and walks the packets across it (the packet holding its
+// first chunk by binary search over the tile's offsets), keeping a running
+// LE16 sum for the current packet and adding it into sums[2q] by LDS atomic
+// only when the packet changes (plus once per packet starting mid-chunk).
+// Packet q's payload sits at LDS [d(q), d(q+1)), d(q) = shift + fo[q] - q*H.
+template <int H>
+__device__ __forceinline__ void varlen_tile_chunk_sums(const unsigned char* lds_pay, const uint32_t* fo,
+                                                       uint32_t* sums, uint32_t Tv, uint32_t shift,
+                                                       uint32_t run_end, bool ablate) {
+  if (ablate || run_end <= shift) return;
+  const u32x4* pay16 = reinterpret_cast<const u32x4*>(lds_pay);
+  auto d = [&](uint32_t q) { return shift + fo[q] - q * (uint32_t)H; };
+  const uint32_t cfirst = shift >> 4, clast = (run_end - 1u) >> 4;
+  const uint32_t nch = clast - cfirst + 1u, per = (nch + kBlock - 1u) / kBlock;
+  const uint32_t c0 = cfirst + threadIdx.x * per;
+  if (c0 > clast) return;
+  const uint32_t c1 = c0 + per - 1u < clast ? c0 + per - 1u : clast;
+  // the last packet whose payload starts at or before chunk c0's first byte
+  uint32_t lo = 0, hi = Tv - 1u;
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1u) >> 1;
+    if (d(mid) <= (c0 << 4)) lo = mid;
+    else hi = mid - 1u;
+  }
+  uint32_t q = lo, acc = 0;
+  uint32_t dq = d(q), dn = d(q + 1u);
+  for (uint32_t c = c0; c <= c1; ++c) {
+    const uint32_t X = c << 4;
+    while (dn <= X && q + 1u < Tv) {  // packets ending before this chunk
+      if (acc) atomicAdd(&sums[2u * q], acc);
+      acc = 0;
+      ++q;
+      dq = dn;
+      dn = d(q + 1u);
+    }
+    const u32x4 v = pay16[c];
+    // the current packet's bytes in this chunk, then any packets starting in it
+    uint32_t qq = q, a0 = dq, a1 = dn;
+    while (true) {
+      if (a1 > X && a0 < X + 16u && a1 > a0) {
+        const int rel = (int)X - (int)a0;  // payload index of chunk byte 0
+        const int len = (int)(a1 - a0);
+        const uint64_t lo64v = lo64(v) & byte_mask(-rel, len - rel);
+        const uint64_t hi64v = hi64(v) & byte_mask(-rel - 8, len - rel - 8);
+        const uint32_t part = payload_le16_sum(lo64v, hi64v, rel);
+        if (qq == q) acc += part;
+        else if (part) atomicAdd(&sums[2u * qq], part);
+      }
+      if (a1 >= X + 16u || qq + 1u >= Tv) break;
+      ++qq;
+      a0 = a1;
+      a1 = d(qq + 1u);
+    }
+  }
+  if (acc) atomicAdd(&sums[2u * q], acc);
+}
+
+// Byte tiles, the chunk -> frame map: lane t takes a contiguous range of the
+// output units (unit k's first byte at tile offset lead + 16k) and walks the
+// frames across it; same entries as the per-packet form.
+template <int H>
+__device__ __forceinline__ void varlen_tile_chunk_map(const uint32_t* fo, uint8_t* map, uint16_t* map16, bool wide,
+                                                      uint32_t Tv, uint32_t lead, uint32_t nbytes) {
+  const uint32_t units = nbytes > lead ? (nbytes - lead + 15u) >> 4 : 0u;
+  const uint32_t per = (units + kBlock - 1u) / kBlock;
+  const uint32_t k0 = threadIdx.x * per;
+  if (k0 >= units) return;
+  const uint32_t k1 = k0 + per < units ? k0 + per : units;
+  const uint32_t x0 = lead + 16u * k0;
+  uint32_t lo = 0, hi = Tv - 1u;  // the frame holding byte x0 (frames are >= H bytes)
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi + 1u) >> 1;
+    if (fo[mid] <= x0) lo = mid;
+    else hi = mid - 1u;
+  }
+  uint32_t r = lo, fs = fo[r], fe = fo[r + 1u];
+  for (uint32_t k = k0; k < k1; ++k) {
+    const uint32_t x = lead + 16u * k;
+    while (fe <= x && r + 1u < Tv) {
+      ++r;
+      fs = fe;
+      fe = fo[r + 1u];
+    }
+    if (wide) {
+      const int kk = (int)x - (int)fs;
+      uint32_t e = r;
+      if (kk >= H && x + 16u <= fe) {
+        e |= 0x8000u;
+      } else {
+        const uint32_t nxt = kk >= H ? 1u : 0u;
+        const uint32_t fsp = nxt ? fe : fs;
+        const int i0 = fsp >= lead ? (int)((fsp - lead) >> 4) : -1;
+        e |= (nxt << 8) | ((uint32_t)((int)k - i0) & 1u) << 9;
+      }
+      map16[k] = (uint16_t)e;
+    } else {
+      map[k] = (uint8_t)r;
+    }
+  }
+}
+
 // Varlen encode of a PACKED payload buffer (payload_off == null) through an
 // LDS tile: the same shape as the fixed-length encode_tile_kernel (encode.hip)
 // with per-frame bounds from frame_off.  A workgroup owns packets
@@ -267,9 +369,24 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
 
   const uint32_t tid = threadIdx.x;
   const uint32_t q = tid >> glog, g = tid & (G - 1u);
-  const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
-  const uint64_t left = a.n - p0;
-  const uint32_t Tv = left < T ? (uint32_t)left : T;
+  const uint64_t tile = a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
+  // Byte tiles (span_start set, glog 0): the packets whose payload starts in
+  // span `tile` (clamped, so a rejected batch's unwritten starts stay in range);
+  // else T packets.
+  uint64_t p0;
+  uint32_t Tv, Tall;
+  if (a.span_start) {
+    const uint64_t s0 = a.span_start[tile], s1 = a.span_start[tile + 1];
+    p0 = s0 < a.n ? s0 : a.n;
+    const uint64_t p1 = s1 < a.n ? (s1 > p0 ? s1 : p0) : a.n;
+    Tall = (uint32_t)(p1 - p0);
+    if (Tall == 0) return;
+    Tv = Tall < T ? Tall : T;
+  } else {
+    p0 = tile * T;
+    const uint64_t left = a.n - p0;
+    Tv = Tall = left < T ? (uint32_t)left : T;
+  }
   // Header-table loads first (small tiles): their latency overlaps the
   // offset loads and phase 1 instead of following the barrier.
   uint32_t t_seq = 0, t_ack = 0, t_flags = 0;
@@ -284,9 +401,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   const uint64_t po_end = fo_end - (p0 + Tv) * (uint64_t)H;
   const uint64_t A = po0 & ~15ull;
   const uint64_t run = ((po_end + 15u) & ~15ull) - A;
-  if (run > cap) {  // uniform over the workgroup
+  if (run > cap || Tall > T) {  // uniform over the workgroup
     if (a.ablate & 4u) return;  // diagnostic (wrong output): overflowing tiles do nothing
-    encode_varlen_packet<H>(a, p0 + q, q < Tv, g, glog);
+    for (uint32_t q0 = 0; q0 < Tall; q0 += kBlock >> glog)  // (byte tiles may hold more than T packets)
+      encode_varlen_packet<H>(a, p0 + q0 + q, q0 + q < Tall, g, glog);
     return;
   }
 
@@ -322,6 +440,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     } else {
       for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = (uint32_t)(a.frame_off[p0 + i] - fo0);
     }
+    if (a.span_start)  // byte tiles: per-packet sums accumulate in lds_hdr's low words
+      for (uint32_t i = tid; i < T; i += kBlock) lds_hdr[i] = 0;
   }
   __syncthreads();
 
@@ -330,7 +450,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   const uint32_t nbytes = (uint32_t)(fo_end - fo0);
   const uint32_t lead = (uint32_t)(-(uintptr_t)(a.frames + fo0)) & 15u;
   uint32_t sum = 0;
-  if (q < Tv) {
+  if (a.span_start) {
+    // Byte tiles: lanes take contiguous ranges of chunks, not packets, so a
+    // tile of ragged lengths keeps every lane equally busy.
+    varlen_tile_chunk_sums<H>(lds_pay, lds_fo, reinterpret_cast<uint32_t*>(lds_hdr), Tv, shift,
+                              shift + (uint32_t)(po_end - po0), (a.ablate & 2u) != 0);
+    varlen_tile_chunk_map<H>(lds_fo, lds_map, lds_map16, wide, Tv, lead, nbytes);
+    __syncthreads();
+    if (q < Tv) sum = reinterpret_cast<const uint32_t*>(lds_hdr)[2u * q];
+  } else if (q < Tv) {
     const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
     const uint32_t Lq = fe - fs - H;
     const uint32_t d = shift + fs - q * H;  // LDS offset of the packet's first payload byte
@@ -1485,7 +1613,7 @@ int launch_varlen_tile_w(const VarlenArgs& args, size_t lds, uint64_t blocks, hi
 template <int H>
 int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
   VarlenArgs args = in;
-  const uint64_t blocks = (args.n + args.tile_T - 1) / args.tile_T;
+  const uint64_t blocks = args.span_start ? args.span_count : (args.n + args.tile_T - 1) / args.tile_T;
   const auto tile_lds = [&](uint32_t wide) {
     size_t b = vt_pay_off(args.tile_T, args.tile_cap, H, wide) + 2u * kVTGuard + args.tile_cap;
     if (args.vhc) b = ((b + 15u) & ~size_t(15)) + 32u * args.tile_T;
@@ -1660,10 +1788,10 @@ int launch_validate_utf8(const Utf8Args& args, hipStream_t stream) {
 
 // frame_off[0..n] = exclusive scan of len[i] + H, frame_off[n] = total bytes.
 int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
-                       const ScanCheck& chk, hipStream_t stream) {
-  // the device-side checks live in the three-pass scan only
-  if (tuning().varlen_scan == 1 || chk.status)
-    return scan_frame_offsets_3pass(d_len, n, H, d_frame_off, chk, stream);
+                       const ScanCheck& chk, hipStream_t stream, const SpanStarts& spans) {
+  // the device-side checks and the span starts live in the three-pass scan only
+  if (tuning().varlen_scan == 1 || chk.status || spans.start)
+    return scan_frame_offsets_3pass(d_len, n, H, d_frame_off, chk, stream, spans);
   hipcub::CountingInputIterator<uint64_t> idx(0);
   hipcub::TransformInputIterator<uint64_t, FrameLen, hipcub::CountingInputIterator<uint64_t>> it(
       idx, FrameLen{d_len, H});

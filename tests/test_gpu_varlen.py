@@ -810,3 +810,50 @@ def test_small_frame_tiles_vs_oracle(cuda, fpt):
                     assert np.array_equal(host(g), e), ctx
                 results.append(host(r.frames))
             assert np.array_equal(results[0], results[1]) and np.array_equal(results[0], results[2])
+
+
+@pytest.mark.parametrize("dist", ["ragged", "equal", "bursty", "tiny_runs", "zeros"])
+def test_byte_tiled_varlen_encode_vs_oracle(cuda, dist):
+    """Varlen encode with tiles by payload bytes (key 51: span starts from the
+    scan, chunk-parallel sums and map) == the oracle, checksums included, for
+    ragged / equal lengths, bursts past the budget's slack, long runs of tiny
+    packets (more than a tile's slots) and zero-length packets."""
+    import ctypes
+    from rudp import _native
+    lib = _native.lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    rng = np.random.default_rng(sum(map(ord, dist)))
+    n = 20011
+    if dist == "ragged":
+        lens = rng.integers(0, 2945, n)
+    elif dist == "equal":
+        lens = np.full(n, 1472)
+    elif dist == "bursty":
+        lens = rng.integers(1000, 2000, n)
+        lens[rng.choice(n, 40, replace=False)] = rng.integers(5000, 20000, 40)
+    elif dist == "tiny_runs":
+        lens = rng.integers(1200, 1700, n)
+        for s0 in rng.choice(n - 400, 10, replace=False):
+            lens[s0:s0 + 300] = rng.integers(0, 3, 300)
+    else:
+        lens = rng.integers(0, 2945, n)
+        lens[rng.random(n) < 0.3] = 0
+    lens = lens.astype(np.int32)
+    pay = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    seq, ack, flags, _ = synth.synth(0xB7 + n, 0, n, 0)
+    pays = split_by_lengths(pay, lens)[0]
+    tab = (dev(seq, cuda), dev(ack, cuda), dev(flags, cuda))
+    for layout in (5, 7):
+        want, off, cs = codec_np.encode_varlen(seq, ack, flags, pays, layout)
+        for btile, xcd in ((1, 1), (1, 0), (0, 1)):
+            old = (lib.rudpx_tune(51, btile), lib.rudpx_tune(49, xcd))
+            try:
+                r = batch.pack_batch_varlen(tab, dev(pay, cuda), dev(lens, cuda), layout, want_csum=True,
+                                            check=False).check()
+            finally:
+                lib.rudpx_tune(51, old[0])
+                lib.rudpx_tune(49, old[1])
+            ctx = (dist, layout, btile, xcd)
+            assert np.array_equal(host(r.frames), want), ctx
+            assert np.array_equal(host(r.frame_off), off), ctx
+            assert np.array_equal(host(r.csum), cs), ctx

@@ -493,24 +493,35 @@ def ragged_sweep(reps):
                                                          H, 0, stream))
         specs = {"default": (), "no_sums": ((35, 2),), "skip_overflow": ((35, 4),),
                  "no_sums_skip_overflow": ((35, 6),), "cap125": ((39, 125),), "cap150": ((39, 150),),
-                 "cap200": ((39, 200),), "no_hchunk": ((36, 0),)}
+                 "cap200": ((39, 200),), "no_hchunk": ((36, 0),), "btile": ((51, 1),),
+                 "btile_no_sums": ((51, 1), (35, 2))}
         variants = {}
         for name, kv in specs.items():
             def setup(kv=kv):
-                for k, v in ((35, 0), (39, 110), (36, 2)):
+                for k, v in ((35, 0), (39, 110), (36, 2), (51, 0)):
                     lib.rudpx_tune(k, v)
                 for k, v in kv:
                     lib.rudpx_tune(k, v)
             variants[f"{shape}_{name}"] = (setup, enc)
         res = interleaved(variants, reps)
-        for k, v in ((35, 0), (39, 110), (36, 2)):
+        exact = {}
+        ref = None
+        for name, kv in specs.items():
+            if "no_" in name or "skip" in name:
+                continue
+            variants[f"{shape}_{name}"][0]()
+            enc()
+            if ref is None:
+                ref = (frames.clone(), off.clone())
+            exact[name] = bool(torch.equal(frames, ref[0]) and torch.equal(off, ref[1]) and int(st.item()) == 0)
+        for k, v in ((35, 0), (39, 110), (36, 2), (51, 0)):
             lib.rudpx_tune(k, v)
         # tiles of 16 packets whose payload run exceeds 1.1x the hinted run (+ alignment slack)
         runs = lens[: (n // 16) * 16].view(-1, 16).sum(1)
         over = float((runs > (16 * (total // n) * 110 // 100 + 256 - 32)).float().mean().item())
         alg = n * (2 * (total / n + H) + 12)
         for k, ms in res.items():
-            out[k] = {"ms": ms, "frac": alg / ms / 1e9 / 8.0}
+            out[k] = {"ms": ms, "frac": alg / ms / 1e9 / 8.0, "exact": exact.get(k.split("_", 1)[1])}
         out[f"{shape}_overflow_tile_fraction"] = over
         del tab, flat, lens, frames, off
         torch.cuda.empty_cache()
