@@ -233,62 +233,104 @@ __host__ __device__ inline uint32_t vt_pay_off(uint32_t T, uint32_t cap, uint32_
   return (8u * T + 4u * (T + 1u) + vt_map_bytes(T, cap, H, wide) + 15u) & ~15u;
 }
 
-// Byte tiles, the sum pass: lane t takes a contiguous range of the run's
-// aligned 16-B chunks and walks the packets across it (the packet holding its
-// first chunk by binary search over the tile's offsets), keeping a running
-// LE16 sum for the current packet and adding it into sums[2q] by LDS atomic
-// only when the packet changes (plus once per packet starting mid-chunk).
-// Packet q's payload sits at LDS [d(q), d(q+1)), d(q) = shift + fo[q] - q*H.
+// Byte tiles, the sum pass: lane t takes a contiguous range of (at most
+// kChunkLanes) aligned 16-B chunks of the run and the packet holding its first
+// chunk (binary search over the tile's offsets).  All of its chunk reads are
+// issued first.  When the range touches at most two packets (the common case
+// at MTU sizes) it sums both without further LDS reads, and the wave combines
+// lanes of the same packet with a segmented shuffle scan, so each packet gets
+// one LDS atomic per wave; other ranges walk their packets and add their parts
+// directly.  Packet q's payload sits at LDS [d(q), d(q+1)),
+// d(q) = shift + fo[q] - q*H.
+constexpr uint32_t kChunkLanes = 8;
+
+__device__ __forceinline__ uint32_t masked_le16(u32x4 v, uint32_t X, uint32_t a0, uint32_t a1) {
+  if (a1 <= X || a0 >= X + 16u || a1 <= a0) return 0u;
+  const int rel = (int)X - (int)a0;  // payload index of chunk byte 0
+  const int len = (int)(a1 - a0);
+  return payload_le16_sum(lo64(v) & byte_mask(-rel, len - rel), hi64(v) & byte_mask(-rel - 8, len - rel - 8),
+                          rel);
+}
+
+// Inclusive sum over the lanes of a wave whose key equals this lane's (keys
+// non-decreasing across lanes); true on the last lane of each key's run.
+__device__ __forceinline__ bool segmented_sum(uint32_t key, uint32_t& x) {
+  const uint32_t lane = threadIdx.x & 63u;
+  for (uint32_t d = 1; d < 64; d <<= 1) {
+    const uint32_t y = __shfl_up(x, d, 64);
+    const uint32_t k = __shfl_up(key, d, 64);
+    if (lane >= d && k == key) x += y;
+  }
+  const uint32_t kn = __shfl_down(key, 1, 64);
+  return lane == 63u || kn != key;
+}
+
 template <int H>
 __device__ __forceinline__ void varlen_tile_chunk_sums(const unsigned char* lds_pay, const uint32_t* fo,
                                                        uint32_t* sums, uint32_t Tv, uint32_t shift,
                                                        uint32_t run_end, bool ablate) {
-  if (ablate || run_end <= shift) return;
+  if (ablate || run_end <= shift) return;  // uniform
   const u32x4* pay16 = reinterpret_cast<const u32x4*>(lds_pay);
   auto d = [&](uint32_t q) { return shift + fo[q] - q * (uint32_t)H; };
   const uint32_t cfirst = shift >> 4, clast = (run_end - 1u) >> 4;
-  const uint32_t nch = clast - cfirst + 1u, per = (nch + kBlock - 1u) / kBlock;
+  const uint32_t nch = clast - cfirst + 1u;
+  const uint32_t per = (nch + kBlock - 1u) / kBlock;  // <= kChunkLanes for runs up to 32 KiB
   const uint32_t c0 = cfirst + threadIdx.x * per;
-  if (c0 > clast) return;
-  const uint32_t c1 = c0 + per - 1u < clast ? c0 + per - 1u : clast;
-  // the last packet whose payload starts at or before chunk c0's first byte
-  uint32_t lo = 0, hi = Tv - 1u;
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi + 1u) >> 1;
-    if (d(mid) <= (c0 << 4)) lo = mid;
-    else hi = mid - 1u;
-  }
-  uint32_t q = lo, acc = 0;
-  uint32_t dq = d(q), dn = d(q + 1u);
-  for (uint32_t c = c0; c <= c1; ++c) {
-    const uint32_t X = c << 4;
-    while (dn <= X && q + 1u < Tv) {  // packets ending before this chunk
-      if (acc) atomicAdd(&sums[2u * q], acc);
-      acc = 0;
-      ++q;
-      dq = dn;
-      dn = d(q + 1u);
+  const uint32_t cnt = c0 <= clast ? (clast - c0 + 1u < per ? clast - c0 + 1u : per) : 0u;
+  uint32_t keyA = 0xFFFFFFFFu, keyB = 0xFFFFFFFFu, accA = 0, accB = 0;
+  if (cnt) {
+    u32x4 v[kChunkLanes];
+#pragma unroll
+    for (uint32_t i = 0; i < kChunkLanes; ++i)
+      if (i < cnt) v[i] = pay16[c0 + i];
+    uint32_t lo = 0, hi = Tv - 1u;  // the last packet starting at or before chunk c0's first byte
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi + 1u) >> 1;
+      if (d(mid) <= (c0 << 4)) lo = mid;
+      else hi = mid - 1u;
     }
-    const u32x4 v = pay16[c];
-    // the current packet's bytes in this chunk, then any packets starting in it
-    uint32_t qq = q, a0 = dq, a1 = dn;
-    while (true) {
-      if (a1 > X && a0 < X + 16u && a1 > a0) {
-        const int rel = (int)X - (int)a0;  // payload index of chunk byte 0
-        const int len = (int)(a1 - a0);
-        const uint64_t lo64v = lo64(v) & byte_mask(-rel, len - rel);
-        const uint64_t hi64v = hi64(v) & byte_mask(-rel - 8, len - rel - 8);
-        const uint32_t part = payload_le16_sum(lo64v, hi64v, rel);
-        if (qq == q) acc += part;
-        else if (part) atomicAdd(&sums[2u * qq], part);
+    const uint32_t q = lo;
+    const uint32_t dq = d(q), dn = d(q + 1u);
+    const uint32_t dnn = q + 2u <= Tv ? d(q + 2u) : dn;
+    const uint32_t X1 = (c0 + cnt) << 4;
+    if (per <= kChunkLanes && (q + 1u >= Tv || dnn >= X1)) {  // at most packets q and q + 1
+#pragma unroll
+      for (uint32_t i = 0; i < kChunkLanes; ++i) {
+        if (i < cnt) {
+          const uint32_t X = (c0 + i) << 4;
+          accA += masked_le16(v[i], X, dq, dn);
+          if (q + 1u < Tv) accB += masked_le16(v[i], X, dn, dnn);
+        }
       }
-      if (a1 >= X + 16u || qq + 1u >= Tv) break;
-      ++qq;
-      a0 = a1;
-      a1 = d(qq + 1u);
+      keyA = q;
+      keyB = q + 1u < Tv ? q + 1u : 0xFFFFFFFFu;
+    } else {  // walk the packets across the range (keys stay sorted for the wave scan, sums 0)
+      keyA = q;
+      keyB = q + 1u < Tv ? q + 1u : 0xFFFFFFFFu;
+      for (uint32_t i = 0; i < cnt; ++i) {
+        const uint32_t c = c0 + i, X = c << 4;
+        const u32x4 w = i < kChunkLanes ? v[i] : pay16[c];
+        uint32_t qq = q, a0 = dq, a1 = dn;
+        while (a1 <= X && qq + 1u < Tv) {
+          ++qq;
+          a0 = a1;
+          a1 = d(qq + 1u);
+        }
+        while (true) {
+          const uint32_t part = masked_le16(w, X, a0, a1);
+          if (part) atomicAdd(&sums[2u * qq], part);
+          if (a1 >= X + 16u || qq + 1u >= Tv) break;
+          ++qq;
+          a0 = a1;
+          a1 = d(qq + 1u);
+        }
+      }
     }
   }
-  if (acc) atomicAdd(&sums[2u * q], acc);
+  // every lane takes part in the shuffles (keys sorted across the wave: q is
+  // non-decreasing in the lane index, and lanes without a key sit at the end)
+  if (segmented_sum(keyA, accA) && keyA != 0xFFFFFFFFu && accA) atomicAdd(&sums[2u * keyA], accA);
+  if (segmented_sum(keyB, accB) && keyB != 0xFFFFFFFFu && accB) atomicAdd(&sums[2u * keyB], accB);
 }
 
 // Byte tiles, the chunk -> frame map: lane t takes a contiguous range of the

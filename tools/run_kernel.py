@@ -30,6 +30,8 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--layout", default="rudp7")
     ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--ragged", action="store_true",
+                    help="varlen ops: lengths uniform in [0, 2L] (mean L) instead of all L")
     ap.add_argument("--gap-ms", type=float, default=0.0,
                     help="idle time between launches (synchronize, then sleep): separates a "
                          "per-launch effect from one of sustained back-to-back HBM load")
@@ -60,9 +62,17 @@ def main():
     vsets = []
     if args.op.endswith("varlen"):
         for tab, pay, fr in sets:
-            lens = torch.full((args.n,), args.L, dtype=torch.int32, device=dev)
-            res = batch.pack_batch_varlen(tab, pay.view(-1), lens, args.layout)
-            vsets.append((tab, pay.view(-1), lens, res.frames, res.frame_off))
+            if args.ragged:
+                g = torch.Generator(device=dev).manual_seed(7)
+                lens = torch.randint(0, 2 * args.L + 1, (args.n,), dtype=torch.int32, device=dev, generator=g)
+                tab, big = batch.synth_batch(args.n, 2 * args.L, 0x5EED0004, device=dev)
+                flat = big.view(-1)[: int(lens.sum().item())].contiguous()
+                del big
+            else:
+                lens = torch.full((args.n,), args.L, dtype=torch.int32, device=dev)
+                flat = pay.view(-1)
+            res = batch.pack_batch_varlen(tab, flat, lens, args.layout)
+            vsets.append((tab, flat, lens, res.frames, res.frame_off))
 
     def step(i):
         if vsets:
