@@ -233,16 +233,15 @@ __host__ __device__ inline uint32_t vt_pay_off(uint32_t T, uint32_t cap, uint32_
   return (8u * T + 4u * (T + 1u) + vt_map_bytes(T, cap, H, wide) + 15u) & ~15u;
 }
 
-// Byte tiles, the sum pass: lane t takes a contiguous range of (at most
-// kChunkLanes) aligned 16-B chunks of the run and the packet holding its first
-// chunk (binary search over the tile's offsets).  All of its chunk reads are
-// issued first.  When the range touches at most two packets (the common case
+// Byte tiles, the sum pass: lane t takes a contiguous range of the run's
+// aligned 16-B chunks and the packet holding its first chunk (binary search
+// over the tile's offsets).  Chunk reads go out kChunkRound at a time.  When the range touches at most two packets (the common case
 // at MTU sizes) it sums both without further LDS reads, and the wave combines
 // lanes of the same packet with a segmented shuffle scan, so each packet gets
 // one LDS atomic per wave; other ranges walk their packets and add their parts
 // directly.  Packet q's payload sits at LDS [d(q), d(q+1)),
 // d(q) = shift + fo[q] - q*H.
-constexpr uint32_t kChunkLanes = 8;
+constexpr uint32_t kChunkRound = 4;
 
 __device__ __forceinline__ uint32_t masked_le16(u32x4 v, uint32_t X, uint32_t a0, uint32_t a1) {
   if (a1 <= X || a0 >= X + 16u || a1 <= a0) return 0u;
@@ -274,15 +273,11 @@ __device__ __forceinline__ void varlen_tile_chunk_sums(const unsigned char* lds_
   auto d = [&](uint32_t q) { return shift + fo[q] - q * (uint32_t)H; };
   const uint32_t cfirst = shift >> 4, clast = (run_end - 1u) >> 4;
   const uint32_t nch = clast - cfirst + 1u;
-  const uint32_t per = (nch + kBlock - 1u) / kBlock;  // <= kChunkLanes for runs up to 32 KiB
+  const uint32_t per = (nch + kBlock - 1u) / kBlock;
   const uint32_t c0 = cfirst + threadIdx.x * per;
   const uint32_t cnt = c0 <= clast ? (clast - c0 + 1u < per ? clast - c0 + 1u : per) : 0u;
   uint32_t keyA = 0xFFFFFFFFu, keyB = 0xFFFFFFFFu, accA = 0, accB = 0;
   if (cnt) {
-    u32x4 v[kChunkLanes];
-#pragma unroll
-    for (uint32_t i = 0; i < kChunkLanes; ++i)
-      if (i < cnt) v[i] = pay16[c0 + i];
     uint32_t lo = 0, hi = Tv - 1u;  // the last packet starting at or before chunk c0's first byte
     while (lo < hi) {
       const uint32_t mid = (lo + hi + 1u) >> 1;
@@ -293,13 +288,20 @@ __device__ __forceinline__ void varlen_tile_chunk_sums(const unsigned char* lds_
     const uint32_t dq = d(q), dn = d(q + 1u);
     const uint32_t dnn = q + 2u <= Tv ? d(q + 2u) : dn;
     const uint32_t X1 = (c0 + cnt) << 4;
-    if (per <= kChunkLanes && (q + 1u >= Tv || dnn >= X1)) {  // at most packets q and q + 1
+    if (q + 1u >= Tv || dnn >= X1) {  // at most packets q and q + 1
+      // rounds of kChunkRound chunk reads issued together, then summed
+      for (uint32_t i0 = 0; i0 < cnt; i0 += kChunkRound) {
+        u32x4 v[kChunkRound];
 #pragma unroll
-      for (uint32_t i = 0; i < kChunkLanes; ++i) {
-        if (i < cnt) {
-          const uint32_t X = (c0 + i) << 4;
-          accA += masked_le16(v[i], X, dq, dn);
-          if (q + 1u < Tv) accB += masked_le16(v[i], X, dn, dnn);
+        for (uint32_t i = 0; i < kChunkRound; ++i)
+          if (i0 + i < cnt) v[i] = pay16[c0 + i0 + i];
+#pragma unroll
+        for (uint32_t i = 0; i < kChunkRound; ++i) {
+          if (i0 + i < cnt) {
+            const uint32_t X = (c0 + i0 + i) << 4;
+            accA += masked_le16(v[i], X, dq, dn);
+            if (q + 1u < Tv) accB += masked_le16(v[i], X, dn, dnn);
+          }
         }
       }
       keyA = q;
@@ -309,7 +311,7 @@ __device__ __forceinline__ void varlen_tile_chunk_sums(const unsigned char* lds_
       keyB = q + 1u < Tv ? q + 1u : 0xFFFFFFFFu;
       for (uint32_t i = 0; i < cnt; ++i) {
         const uint32_t c = c0 + i, X = c << 4;
-        const u32x4 w = i < kChunkLanes ? v[i] : pay16[c];
+        const u32x4 w = pay16[c];  // (no runtime index into v: that would move it to scratch)
         uint32_t qq = q, a0 = dq, a1 = dn;
         while (a1 <= X && qq + 1u < Tv) {
           ++qq;
@@ -398,7 +400,9 @@ __device__ __forceinline__ void varlen_tile_chunk_map(const uint32_t* fo, uint8_
 // A tile whose run exceeds tile_cap (lengths far above the caller's hint)
 // encodes its packets with the per-packet vector path instead.
 // W: minimum waves per SIMD the register allocation must allow (1 = none).
-template <int H, int W>
+// BT: byte tiles (a.span_start set; chunk-parallel sum pass and map), its own
+// instantiation so the packet-count form keeps its register budget.
+template <int H, int W, bool BT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))) encode_varlen_tile_kernel(VarlenArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const uint32_t T = a.tile_T, glog = a.tile_glog, G = 1u << glog, cap = a.tile_cap;
@@ -417,7 +421,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   // else T packets.
   uint64_t p0;
   uint32_t Tv, Tall;
-  if (a.span_start) {
+  if (BT) {
     const uint64_t s0 = a.span_start[tile], s1 = a.span_start[tile + 1];
     p0 = s0 < a.n ? s0 : a.n;
     const uint64_t p1 = s1 < a.n ? (s1 > p0 ? s1 : p0) : a.n;
@@ -482,7 +486,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     } else {
       for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = (uint32_t)(a.frame_off[p0 + i] - fo0);
     }
-    if (a.span_start)  // byte tiles: per-packet sums accumulate in lds_hdr's low words
+    if (BT)  // byte tiles: per-packet sums accumulate in lds_hdr's low words
       for (uint32_t i = tid; i < T; i += kBlock) lds_hdr[i] = 0;
   }
   __syncthreads();
@@ -492,7 +496,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   const uint32_t nbytes = (uint32_t)(fo_end - fo0);
   const uint32_t lead = (uint32_t)(-(uintptr_t)(a.frames + fo0)) & 15u;
   uint32_t sum = 0;
-  if (a.span_start) {
+  if (BT) {
     // Byte tiles: lanes take contiguous ranges of chunks, not packets, so a
     // tile of ragged lengths keeps every lane equally busy.
     varlen_tile_chunk_sums<H>(lds_pay, lds_fo, reinterpret_cast<uint32_t*>(lds_hdr), Tv, shift,
@@ -1641,14 +1645,15 @@ int launch_decode_small(const VarlenArgs& args, hipStream_t stream) {
   }
 }
 
-template <int H, int W>
+template <int H, int W, bool BT = false>
 int launch_varlen_tile_w(const VarlenArgs& args, size_t lds, uint64_t blocks, hipStream_t stream) {
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_varlen_tile_kernel<H, W>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_varlen_tile_kernel<H, W, BT>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL((encode_varlen_tile_kernel<H, W>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
+  hipLaunchKernelGGL((encode_varlen_tile_kernel<H, W, BT>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream,
+                     args);
   return (int)hipGetLastError();
 }
 
@@ -1684,6 +1689,8 @@ int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
     const size_t per_cu = kLdsPerCu / lds;
     w = per_cu >= 7 ? 7 : per_cu == 6 ? 6 : 1;
   }
+  if (args.span_start)  // byte tiles: register budget for the LDS occupancy (5 tiles per CU at MTU hints)
+    return launch_varlen_tile_w<H, 5, true>(args, lds, blocks, stream);
   return w == 6 ? launch_varlen_tile_w<H, 6>(args, lds, blocks, stream)
        : w == 7 ? launch_varlen_tile_w<H, 7>(args, lds, blocks, stream)
        : w == 8 ? launch_varlen_tile_w<H, 8>(args, lds, blocks, stream)
