@@ -613,6 +613,7 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
       a.span_count = spans.count;
       a.tile_T = (uint32_t)slots;
       a.tile_glog = 0;
+      a.btile_sums = tuning().varlen_btile_sums == 1 ? 1u : 0u;
     }
   }
   rc = scan_frame_offsets(in->len, in->n, (uint32_t)layout, d_frame_off, chk, s, spans);

@@ -114,6 +114,7 @@ struct VarlenArgs {
   // workgroups; tile_T is then the most packets a tile holds in LDS, glog 0.
   const uint32_t* span_start;
   uint64_t span_count;
+  uint32_t btile_sums;            // byte tiles' sum pass: 0 rounds of 16 packets x 16 lanes, 1 chunk-parallel
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -269,6 +270,7 @@ struct Tuning {
   // packet count: no tile overflows short of one packet past the budget's
   // slack, and the sum pass is chunk-parallel (0: packet-count tiles).
   std::atomic<int> varlen_btile{0};
+  std::atomic<int> varlen_btile_sums{0};  // byte tiles' sum pass (VarlenArgs::btile_sums)
   std::atomic<int> host_slots{3};     // *_host pipeline: device staging slots (2..8)
   std::atomic<int> host_stage_mb{128};  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
 };

@@ -242,6 +242,9 @@ __host__ __device__ inline uint32_t vt_pay_off(uint32_t T, uint32_t cap, uint32_
 // directly.  Packet q's payload sits at LDS [d(q), d(q+1)),
 // d(q) = shift + fo[q] - q*H.
 constexpr uint32_t kChunkRound = 4;
+// Combine a wave's lanes per packet with a segmented shuffle scan before the
+// LDS atomics (1), or let every lane add its own part (0).
+constexpr bool kWaveCombine = false;
 
 __device__ __forceinline__ uint32_t masked_le16(u32x4 v, uint32_t X, uint32_t a0, uint32_t a1) {
   if (a1 <= X || a0 >= X + 16u || a1 <= a0) return 0u;
@@ -329,10 +332,15 @@ __device__ __forceinline__ void varlen_tile_chunk_sums(const unsigned char* lds_
       }
     }
   }
-  // every lane takes part in the shuffles (keys sorted across the wave: q is
-  // non-decreasing in the lane index, and lanes without a key sit at the end)
-  if (segmented_sum(keyA, accA) && keyA != 0xFFFFFFFFu && accA) atomicAdd(&sums[2u * keyA], accA);
-  if (segmented_sum(keyB, accB) && keyB != 0xFFFFFFFFu && accB) atomicAdd(&sums[2u * keyB], accB);
+  if (kWaveCombine) {
+    // every lane takes part in the shuffles (keys sorted across the wave: q is
+    // non-decreasing in the lane index, and lanes without a key sit at the end)
+    if (segmented_sum(keyA, accA) && keyA != 0xFFFFFFFFu && accA) atomicAdd(&sums[2u * keyA], accA);
+    if (segmented_sum(keyB, accB) && keyB != 0xFFFFFFFFu && accB) atomicAdd(&sums[2u * keyB], accB);
+  } else {
+    if (accA) atomicAdd(&sums[2u * keyA], accA);
+    if (accB) atomicAdd(&sums[2u * keyB], accB);
+  }
 }
 
 // Byte tiles, the chunk -> frame map: lane t takes a contiguous range of the
@@ -499,8 +507,34 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   if (BT) {
     // Byte tiles: lanes take contiguous ranges of chunks, not packets, so a
     // tile of ragged lengths keeps every lane equally busy.
-    varlen_tile_chunk_sums<H>(lds_pay, lds_fo, reinterpret_cast<uint32_t*>(lds_hdr), Tv, shift,
-                              shift + (uint32_t)(po_end - po0), (a.ablate & 2u) != 0);
+    if (a.btile_sums == 1) {
+      varlen_tile_chunk_sums<H>(lds_pay, lds_fo, reinterpret_cast<uint32_t*>(lds_hdr), Tv, shift,
+                                shift + (uint32_t)(po_end - po0), (a.ablate & 2u) != 0);
+    } else {
+      // rounds of 16 packets, 16 lanes each (the packet-count tile's sum pass)
+      uint32_t* sums = reinterpret_cast<uint32_t*>(lds_hdr);
+      const u32x4* pay16 = reinterpret_cast<const u32x4*>(lds_pay);
+      for (uint32_t r0 = 0; r0 < Tv; r0 += kBlock / 16u) {
+        const uint32_t qq = r0 + (tid >> 4), gg = tid & 15u;
+        uint32_t part = 0;
+        if (qq < Tv && !(a.ablate & 2u)) {
+          const uint32_t fs = lds_fo[qq], fe = lds_fo[qq + 1];
+          const uint32_t Lq = fe - fs - H;
+          const uint32_t d = shift + fs - qq * H;
+          if (Lq) {
+            const uint32_t c1 = (d + Lq - 1u) >> 4;
+            for (uint32_t c = (d >> 4) + gg; c <= c1; c += 16u) {
+              const u32x4 v = pay16[c];
+              const int rel = (int)(c << 4) - (int)d;
+              part += payload_le16_sum(lo64(v) & byte_mask(-rel, (int)Lq - rel),
+                                       hi64(v) & byte_mask(-rel - 8, (int)Lq - rel - 8), rel);
+            }
+          }
+        }
+        for (uint32_t m = 8; m > 0; m >>= 1) part += __shfl_xor(part, (int)m, 64);
+        if (qq < Tv && gg == 0) sums[2u * qq] = part;
+      }
+    }
     varlen_tile_chunk_map<H>(lds_fo, lds_map, lds_map16, wide, Tv, lead, nbytes);
     __syncthreads();
     if (q < Tv) sum = reinterpret_cast<const uint32_t*>(lds_hdr)[2u * q];
