@@ -118,7 +118,7 @@ def encode_sweep(reps):
     lib.rudpx_tune(1, 1)
     lib.rudpx_tune(2, 0)
     lib.rudpx_tune(3, 8)
-    lib.rudpx_tune(5, 0)
+    lib.rudpx_tune(5, -1)
     lib.rudpx_tune(6, -1)
     lib.rudpx_tune(7, 1)
     lib.rudpx_tune(10, 256)
