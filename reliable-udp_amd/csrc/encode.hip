@@ -169,7 +169,7 @@ __device__ __forceinline__ void encode_phase2_hc(const EncodeTileArgs& a, const 
   }
 }
 
-template <int H, bool NTL, bool NTS, int P1, bool CONTIG, int BLOCK = kBlock, bool DMA = false>
+template <int H, bool NTL, bool NTS, int P1, int BLOCK = kBlock, bool DMA = false>
 __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   uint64_t* lds_hdr = reinterpret_cast<uint64_t*>(lds);  // [T + 1]
@@ -203,7 +203,7 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
     t_flags = a.flags[p0 + q];
   }
   uint32_t sum = 0;
-  if (CONTIG) {
+  {
     // The tile's payload is one contiguous run: stream it like a copy (lane t
     // takes vectors t, t+256, ...: every wave-instruction reads 1 KiB
     // contiguous), then sum each packet back out of LDS.
@@ -238,26 +238,6 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
     if (q < Tv && !(a.ablate & 1u)) {
       const u32x4* mine = dst + q * V;
       for (uint32_t v = g; v < V; v += G) sum += le16_sum(mine[v]);
-    }
-  } else if (q < Tv) {
-    const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + (p0 + q) * (uint64_t)L);
-    u32x4* dst = reinterpret_cast<u32x4*>(lds_pay + kLdsGuard + q * L);
-    // P1 loads in flight per lane per round
-    for (uint32_t v0 = g; v0 < V; v0 += (uint32_t)P1 * G) {
-      u32x4 r[P1];
-#pragma unroll
-      for (int u = 0; u < P1; ++u) {
-        uint32_t v = v0 + (uint32_t)u * G;
-        if (v < V) r[u] = load16<NTL>(src + v);
-      }
-#pragma unroll
-      for (int u = 0; u < P1; ++u) {
-        uint32_t v = v0 + (uint32_t)u * G;
-        if (v < V) {
-          sum += le16_sum(r[u]);
-          dst[v] = r[u];
-        }
-      }
     }
   }
   for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
@@ -336,7 +316,7 @@ __global__ void __launch_bounds__(kBlock) encode_bytes_kernel(EncodeTileArgs a) 
 }
 
 
-template <int H, bool NTL, bool NTS, int P1, bool CONTIG, int BLOCK = kBlock, bool DMA = false>
+template <int H, bool NTL, bool NTS, int P1, int BLOCK = kBlock, bool DMA = false>
 int launch_tile(const EncodeTileArgs& args, hipStream_t stream) {
   const uint64_t blocks = (args.n + args.T - 1) / args.T;
   size_t lds = args.hdr_bytes + kLdsGuard + (size_t)args.T * args.L + 32;
@@ -357,22 +337,22 @@ int launch_tile(const EncodeTileArgs& args, hipStream_t stream) {
     if (want > lds) lds = want;
   }
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_tile_kernel<H, NTL, NTS, P1, CONTIG, BLOCK, DMA>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_tile_kernel<H, NTL, NTS, P1, BLOCK, DMA>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL((encode_tile_kernel<H, NTL, NTS, P1, CONTIG, BLOCK, DMA>), dim3((uint32_t)blocks), dim3(BLOCK), lds,
+  hipLaunchKernelGGL((encode_tile_kernel<H, NTL, NTS, P1, BLOCK, DMA>), dim3((uint32_t)blocks), dim3(BLOCK), lds,
                      stream, args);
   return (int)hipGetLastError();
 }
 
-template <int H, int P1, bool CONTIG>
+template <int H, int P1>
 int launch_tile_nt(const EncodeTileArgs& args, hipStream_t stream) {
   const Tuning& t = tuning();
-  if (t.encode_nt_load && t.encode_nt_store) return launch_tile<H, true, true, P1, CONTIG>(args, stream);
-  if (t.encode_nt_load) return launch_tile<H, true, false, P1, CONTIG>(args, stream);
-  if (t.encode_nt_store) return launch_tile<H, false, true, P1, CONTIG>(args, stream);
-  return launch_tile<H, false, false, P1, CONTIG>(args, stream);
+  if (t.encode_nt_load && t.encode_nt_store) return launch_tile<H, true, true, P1>(args, stream);
+  if (t.encode_nt_load) return launch_tile<H, true, false, P1>(args, stream);
+  if (t.encode_nt_store) return launch_tile<H, false, true, P1>(args, stream);
+  return launch_tile<H, false, false, P1>(args, stream);
 }
 
 template <int H>
@@ -383,24 +363,19 @@ int launch_tile_policy(const EncodeTileArgs& args, hipStream_t stream) {
   // blocks give each packet (256/T)*(block/256) lanes, so keep that <= 64.
   if (block > 256 && (uint64_t)(256u / args.T) * (uint32_t)(block / 256) > 64u) block = 256;
   const Tuning& t = tuning();
-  if (t.encode_dma && block == 256 && t.encode_contig) {
-    if (t.encode_nt_load && t.encode_nt_store) return launch_tile<H, true, true, 8, true, kBlock, true>(args, stream);
-    if (t.encode_nt_load) return launch_tile<H, true, false, 8, true, kBlock, true>(args, stream);
-    if (t.encode_nt_store) return launch_tile<H, false, true, 8, true, kBlock, true>(args, stream);
-    return launch_tile<H, false, false, 8, true, kBlock, true>(args, stream);
+  if (t.encode_dma && block == 256) {
+    if (t.encode_nt_load && t.encode_nt_store) return launch_tile<H, true, true, 8, kBlock, true>(args, stream);
+    if (t.encode_nt_load) return launch_tile<H, true, false, 8, kBlock, true>(args, stream);
+    if (t.encode_nt_store) return launch_tile<H, false, true, 8, kBlock, true>(args, stream);
+    return launch_tile<H, false, false, 8, kBlock, true>(args, stream);
   }
-  if (block == 64 && args.T <= 64) return launch_tile<H, true, true, 8, true, 64>(args, stream);
-  if (block == 128 && args.T <= 128) return launch_tile<H, true, true, 8, true, 128>(args, stream);
-  if (block == 512) return launch_tile<H, true, true, 8, true, 512>(args, stream);
-  if (block == 1024) return launch_tile<H, true, true, 8, true, 1024>(args, stream);
-  if (tuning().encode_contig) {
-    if (p1 == 2) return launch_tile_nt<H, 2, true>(args, stream);
-    if (p1 == 4) return launch_tile_nt<H, 4, true>(args, stream);
-    return launch_tile_nt<H, 8, true>(args, stream);
-  }
-  if (p1 == 2) return launch_tile_nt<H, 2, false>(args, stream);
-  if (p1 == 4) return launch_tile_nt<H, 4, false>(args, stream);
-  return launch_tile_nt<H, 8, false>(args, stream);
+  if (block == 64 && args.T <= 64) return launch_tile<H, true, true, 8, 64>(args, stream);
+  if (block == 128 && args.T <= 128) return launch_tile<H, true, true, 8, 128>(args, stream);
+  if (block == 512) return launch_tile<H, true, true, 8, 512>(args, stream);
+  if (block == 1024) return launch_tile<H, true, true, 8, 1024>(args, stream);
+  if (p1 == 2) return launch_tile_nt<H, 2>(args, stream);
+  if (p1 == 4) return launch_tile_nt<H, 4>(args, stream);
+  return launch_tile_nt<H, 8>(args, stream);
 }
 
 

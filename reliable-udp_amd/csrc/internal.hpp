@@ -170,7 +170,6 @@ struct Tuning {
   // within noise, fixed copy-out at 64 B 5% slower, so the fixed decode keeps
   // it off below 128-B frames (profiles/r02/sweeps/tile_xcd_*.json).
   std::atomic<int> tile_xcd{1};
-  std::atomic<int> encode_contig{1};  // phase 1 streams the tile contiguously, sums from LDS
   std::atomic<int> encode_block{256};  // tile workgroup size (64, 128 when T <= block; 256, 512, 1024)
   std::atomic<int> decode_copy_tile{1};  // copy-out decode through an LDS tile (0: register windows)
   std::atomic<int> decode_verify_tile{1};  // verify-only decode through an LDS tile (0: aligned-chunk kernel)

@@ -238,7 +238,7 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // 2: packets per encode tile (power of two 16..256, 0 = auto); 3: encode phase-1
 // loads in flight per lane (2, 4, 8); 4: decode-verify log2 lanes per packet
 // (1..4, -1 = auto); 5: XCD-contiguous tile order; 6: encode tiles per CU cap;
-// 7: contiguous phase-1 stream with checksums summed from LDS; 8: host pipeline
+// (7: per-packet phase-1 loads, lost to the contiguous stream, removed); 8: host pipeline
 // slots; 9: host pipeline MiB per slot; 10: encode tile workgroup size;
 // 11: copy-out decode through an LDS tile; 12: verify-only decode through an LDS tile;
 // 13: encode stage ablation; 14: varlen vector kernels; 15: varlen lanes log2;
@@ -268,7 +268,7 @@ int rudpx_tune(int key, int value) {
   std::atomic<int>* slot = key == 0 ? &t.encode_nt_load : key == 1 ? &t.encode_nt_store
             : key == 2 ? &t.encode_tile : key == 3 ? &t.encode_p1
             : key == 4 ? &t.decode_glog : key == 5 ? &t.encode_xcd_swizzle
-            : key == 6 ? &t.encode_blocks_per_cu : key == 7 ? &t.encode_contig
+            : key == 6 ? &t.encode_blocks_per_cu
             : key == 8 ? &t.host_slots : key == 9 ? &t.host_stage_mb
             : key == 10 ? &t.encode_block : key == 11 ? &t.decode_copy_tile
             : key == 12 ? &t.decode_verify_tile : key == 13 ? &t.encode_ablate : key == 14 ? &t.varlen_vec : key == 15 ? &t.varlen_glog

@@ -71,10 +71,10 @@ def test_prebuilt_header_chunks_vs_oracle(cuda, L):
 
 
 # (key, values) of launch-policy knobs not covered elsewhere: encode nt load /
-# store (0, 1), phase-1 loads in flight (3), XCD-contiguous tile order (5),
-# per-packet phase 1 (7 = 0); decode lanes per packet (4); varlen lanes (15)
+# store (0, 1), phase-1 loads in flight (3), XCD-contiguous tile order (5);
+# decode lanes per packet (4); varlen lanes (15)
 # and varlen tile geometry (17, 18).
-_ENCODE_KNOBS = [(0, (0,)), (1, (0,)), (3, (2, 4)), (5, (1,)), (7, (0,))]
+_ENCODE_KNOBS = [(0, (0,)), (1, (0,)), (3, (2, 4)), (5, (1,))]
 
 
 @pytest.mark.parametrize("L", [64, 256, 1472])

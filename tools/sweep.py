@@ -103,9 +103,8 @@ def encode_sweep(reps):
         alg = n * (2 * L + 12)
         # every variant must produce the default kernel's frames bit for bit
         tab0, pay0, _ = sets[0]
-        lib.rudpx_tune(7, 0), lib.rudpx_tune(3, 8), lib.rudpx_tune(6, 0), lib.rudpx_tune(10, 256)
-        lib.rudpx_tune(2, 16 if L > 256 else 128)
-        want, _ = batch.pack_batch(tab0, pay0, 7)  # the original per-packet phase 1
+        lib.rudpx_tune(3, 8), lib.rudpx_tune(6, -1), lib.rudpx_tune(10, 256), lib.rudpx_tune(2, 0)
+        want, _ = batch.pack_batch(tab0, pay0, 7)  # the default kernel
         for k, (setup, _) in variants.items():
             setup()
             got, _ = batch.pack_batch(tab0, pay0, 7)
@@ -120,7 +119,6 @@ def encode_sweep(reps):
     lib.rudpx_tune(3, 8)
     lib.rudpx_tune(5, -1)
     lib.rudpx_tune(6, -1)
-    lib.rudpx_tune(7, 1)
     lib.rudpx_tune(10, 256)
     return out
 
