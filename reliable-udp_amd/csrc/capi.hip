@@ -607,19 +607,20 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
       spans.bytes = S;
       spans.count = chk.payload_bytes / S + 1u;
       void* buf = nullptr;
-      RUDP_HIP(stream_alloc(&buf, (spans.count + 1u) * sizeof(uint32_t), s));
-      spans.start = static_cast<uint32_t*>(buf);
-      a.span_start = spans.start;
+      RUDP_HIP(stream_alloc(&buf, (spans.count + 1u) * sizeof(SpanRec), s));
+      spans.rec = static_cast<SpanRec*>(buf);
+      a.span_rec = spans.rec;
       a.span_count = spans.count;
       a.tile_T = (uint32_t)slots;
       a.tile_glog = 0;
-      a.btile_sums = tuning().varlen_btile_sums == 1 ? 1u : 0u;
+      const int bs = tuning().varlen_btile_sums;
+      a.btile_sums = bs == 1 || bs == 2 ? (uint32_t)bs : 0u;
     }
   }
   rc = scan_frame_offsets(in->len, in->n, (uint32_t)layout, d_frame_off, chk, s, spans);
   if (!rc) rc = launch_encode_varlen(a, layout, s);
-  if (spans.start) {
-    const hipError_t e = stream_free(spans.start, s);
+  if (spans.rec) {
+    const hipError_t e = stream_free(spans.rec, s);
     if (!rc && e != hipSuccess) return hip_fail(e, "hipFreeAsync");
   }
   if (rc) return hip_fail((hipError_t)rc, "varlen encode");

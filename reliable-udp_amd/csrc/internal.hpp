@@ -64,6 +64,12 @@ struct SynthArgs {
   unsigned char* payload;
 };
 
+// One span of the byte-tiled varlen encode (SpanStarts).
+struct SpanRec {
+  uint64_t fo;  // frame_off[p]
+  uint32_t p;   // first packet whose payload starts in the span (n past the last)
+  uint32_t pad;
+};
 struct VarlenArgs {
   const unsigned char* payload;   // encode: payload buffer
   const uint32_t* len;            // encode: payload bytes per packet
@@ -92,7 +98,8 @@ struct VarlenArgs {
   uint32_t align64;               // tile kernel: wave stores start on 64-B sector boundaries
   uint32_t early_table;           // tile kernel: header-table loads before phase 1
   uint32_t ablate;                // diagnostics only (wrong output): 1 = phase 2 without the frame walk,
-                                  // 2 = no sum pass, 4 = tiles over their LDS budget do nothing
+                                  // 2 = no sum pass, 4 = tiles over their LDS budget do nothing,
+                                  // 8 = byte tiles with a zero chunk map
   uint32_t vhc;                   // tile kernel: prebuilt header chunks + pure-chunk fast phase 2
   uint32_t hc_off;                // LDS byte offset of the header-chunk array (set by the launcher)
   uint32_t early_fo;              // tile kernels: the tile's frame offsets loaded before phase 1
@@ -110,11 +117,11 @@ struct VarlenArgs {
   uint32_t small_cap;             // its LDS run budget in bytes
   uint32_t xcd;                   // tile kernels: XCD-contiguous tile order (xcd_tile)
   // Byte-tiled encode: workgroup k frames the packets whose payload starts in
-  // [k*S, (k+1)*S) (span_start[k] .. span_start[k+1], from the scan), span_count
+  // [k*S, (k+1)*S) (span_rec[k].p .. span_rec[k+1].p, from the scan), span_count
   // workgroups; tile_T is then the most packets a tile holds in LDS, glog 0.
-  const uint32_t* span_start;
+  const struct SpanRec* span_rec;
   uint64_t span_count;
-  uint32_t btile_sums;            // byte tiles' sum pass: 0 rounds of 16 packets x 16 lanes, 1 chunk-parallel
+  uint32_t btile_sums;            // byte tiles' sum pass: 0 rounds of 16 packets x 16 lanes, 1 chunk-parallel, 2 block sums
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -321,10 +328,12 @@ void scan_block_bases(uint64_t* sums, uint64_t nb, uint64_t* d_frame_off, uint64
 // two passes, then one kernel per tile of kBlock * fpt packets that writes the
 // tile's offsets and assembles its frames in LDS.
 int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int layout, hipStream_t stream);
-// Span starts for the byte-tiled varlen encode: start[k] (k = 0 .. count) is
-// the first packet whose packed payload starts at or after k * bytes.
+// Span starts for the byte-tiled varlen encode: rec[k] (k = 0 .. count) holds
+// p, the first packet whose packed payload starts at or after k * bytes, and
+// fo = frame_off[p], so a tile has its packet range and frame run from two
+// adjacent records in one round trip.
 struct SpanStarts {
-  uint32_t* start;  // [count + 1], or null
+  SpanRec* rec;  // [count + 1], or null
   uint64_t bytes;
   uint64_t count;
 };

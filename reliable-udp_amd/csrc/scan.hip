@@ -103,9 +103,9 @@ __global__ void __launch_bounds__(1024) scan_block_bases_kernel(uint64_t* sums, 
   }
 }
 
-// With spans.start: the packed payload splits into spans of S bytes, and
-// spans.start[k] = the first packet whose payload starts at or after k*S
-// (n for spans after the last packet's start), k = 0 .. spans.count.
+// With spans.rec: the packed payload splits into spans of S bytes, and
+// spans.rec[k] = {frame_off[p], p} for p the first packet whose payload starts
+// at or after k*S (n for spans after the last packet's start), k = 0 .. spans.count.
 __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len, uint64_t n, uint32_t H,
                                                             const uint64_t* bases, uint64_t* frame_off,
                                                             SpanStarts spans) {
@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len,
     const uint32_t k = j * kBlock + threadIdx.x;
     if (base + k < n) frame_off[base + k] = s_off[k];
   }
-  if (spans.start) {
+  if (spans.rec) {
     const uint64_t S = spans.bytes, K = spans.count;
 #pragma unroll
     for (uint32_t j = 0; j < kScanItems; ++j) {
@@ -152,9 +152,10 @@ __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len,
       }
       uint64_t hi = po / S;
       if (hi > K) hi = K;
-      for (uint64_t t = lo; t <= hi; ++t) spans.start[t] = (uint32_t)p;
+      for (uint64_t t = lo; t <= hi; ++t) spans.rec[t] = SpanRec{s_off[k], (uint32_t)p, 0u};
       if (p == n - 1)
-        for (uint64_t t = (po / S + 1 > lo ? po / S + 1 : lo); t <= K; ++t) spans.start[t] = (uint32_t)n;
+        for (uint64_t t = (po / S + 1 > lo ? po / S + 1 : lo); t <= K; ++t)
+          spans.rec[t] = SpanRec{s_off[k] + s_len[k], (uint32_t)n, 0u};
     }
   }
 }

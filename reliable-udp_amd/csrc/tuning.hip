@@ -261,7 +261,7 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // packets per thread; 48: fixed-length encode packets per launch (0 = one launch);
 // 49: XCD-contiguous tile order in the decode / varlen / UTF-8 tile kernels;
 // 50: small-frame encode finds its tile bases itself (no pass-2 launch);
-// 51: varlen encode tiles by payload bytes; 52: their sum pass (0 packet rounds, 1 chunk-parallel).
+// 51: varlen encode tiles by payload bytes; 52: their sum pass (0 packet rounds, 1 chunk-parallel, 2 block sums).
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();

@@ -221,16 +221,48 @@ constexpr uint32_t kVTGuard = 32;
 // The map holds one u8 (owner frame) per output chunk, or with the coded map
 // (vhc == 2) one u16: owner frame in bits 0-7, bit 15 = pure payload chunk,
 // else bit 8 = header chunk of the next frame and bit 9 = its slot.
-__host__ __device__ inline uint32_t vt_map_bytes(uint32_t T, uint32_t cap, uint32_t H, uint32_t wide) {
-  return (((cap + T * H) >> 4) + 4u) << (wide ? 1 : 0);
+// Byte tiles with the block-sum pass (btile_sums 2) reuse the map's bytes for
+// the run's 64-B block sums first: u64 per block, 8-B aligned.
+__host__ __device__ inline uint32_t vt_map_bytes(uint32_t T, uint32_t cap, uint32_t H, uint32_t wide,
+                                                 uint32_t pfx = 0) {
+  const uint32_t map = (((cap + T * H) >> 4) + 4u) << (wide ? 1 : 0);
+  const uint32_t blocks = 8u * ((cap >> 6) + 3u) + 8u;
+  return pfx && blocks > map ? blocks : map;
 }
 // Frames of at least this many bytes: an aligned 16-B chunk overlaps at most
 // one header, and the 16 payload bytes before a frame's payload belong to the
 // previous frame (the varlen tile's fast phase 2).
 constexpr uint32_t kVHCMinFrame = 32;
 
-__host__ __device__ inline uint32_t vt_pay_off(uint32_t T, uint32_t cap, uint32_t H, uint32_t wide) {
-  return (8u * T + 4u * (T + 1u) + vt_map_bytes(T, cap, H, wide) + 15u) & ~15u;
+__host__ __device__ inline uint32_t vt_pay_off(uint32_t T, uint32_t cap, uint32_t H, uint32_t wide,
+                                               uint32_t pfx = 0) {
+  return (8u * T + 4u * (T + 1u) + vt_map_bytes(T, cap, H, wide, pfx) + 15u) & ~15u;
+}
+
+// Byte tiles, the block-sum pass (btile_sums 2).  The packet-count tile gives
+// every packet G lanes; with ragged lengths in a byte tile that leaves most
+// lanes idle while the longest packet is summed.  Instead every 64-B block of
+// the run gets its even- and odd-address byte sums as phase 1 streams it
+// through registers (a quad of lanes holds the block's four vectors), and a
+// packet adds the block sums inside its payload plus its two edge blocks
+// chunk by chunk (8 lanes per packet): 16 times fewer LDS reads per packet
+// byte than summing its chunks.
+// Even/odd byte sums of a 16-B chunk, packed e | o << 16 (each at most 2040).
+__device__ __forceinline__ uint32_t eo_sum(uint64_t lo, uint64_t hi) {
+  constexpr uint64_t M = 0x00FF00FF00FF00FFull;
+  const uint64_t ev = (lo & M) + (hi & M), od = ((lo >> 8) & M) + ((hi >> 8) & M);
+  const uint32_t e2 = (uint32_t)ev + (uint32_t)(ev >> 32), o2 = (uint32_t)od + (uint32_t)(od >> 32);
+  return ((e2 & 0xFFFFu) + (e2 >> 16)) | (((o2 & 0xFFFFu) + (o2 >> 16)) << 16);
+}
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+// Sum over the 4 lanes of a quad (all 4 active).
+__device__ __forceinline__ uint32_t quad_sum(uint32_t x) {
+  x += dpp_u32<0xB1>(x);  // quad_perm [1, 0, 3, 2]
+  x += dpp_u32<0x4E>(x);  // quad_perm [2, 3, 0, 1]
+  return x;
 }
 
 // Byte tiles, the sum pass: lane t takes a contiguous range of the run's
@@ -408,7 +440,7 @@ __device__ __forceinline__ void varlen_tile_chunk_map(const uint32_t* fo, uint8_
 // A tile whose run exceeds tile_cap (lengths far above the caller's hint)
 // encodes its packets with the per-packet vector path instead.
 // W: minimum waves per SIMD the register allocation must allow (1 = none).
-// BT: byte tiles (a.span_start set; chunk-parallel sum pass and map), its own
+// BT: byte tiles (a.span_rec set; their own sum passes and map), its own
 // instantiation so the packet-count form keeps its register budget.
 template <int H, int W, bool BT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))) encode_varlen_tile_kernel(VarlenArgs a) {
@@ -419,27 +451,33 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   const bool wide = a.vhc == 2u;  // coded chunk map (u16 entries)
   uint8_t* lds_map = reinterpret_cast<uint8_t*>(lds_fo + T + 1u);
   uint16_t* lds_map16 = reinterpret_cast<uint16_t*>(lds_map);
-  unsigned char* lds_pay = lds + vt_pay_off(T, cap, H, wide ? 1u : 0u);
+  const bool pfx_sums = BT && a.btile_sums == 2u;  // byte tiles' block-sum pass
+  uint64_t* lds_pfx = reinterpret_cast<uint64_t*>(lds + ((8u * T + 4u * (T + 1u) + 7u) & ~7u));
+  unsigned char* lds_pay = lds + vt_pay_off(T, cap, H, wide ? 1u : 0u, pfx_sums ? 1u : 0u);
 
   const uint32_t tid = threadIdx.x;
   const uint32_t q = tid >> glog, g = tid & (G - 1u);
   const uint64_t tile = a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
-  // Byte tiles (span_start set, glog 0): the packets whose payload starts in
-  // span `tile` (clamped, so a rejected batch's unwritten starts stay in range);
-  // else T packets.
-  uint64_t p0;
+  // Byte tiles (span_rec set, glog 0): the packets whose payload starts in
+  // span `tile` (clamped, so a rejected batch's unwritten records stay in
+  // range), their frame run from the same two records; else T packets.
+  uint64_t p0, fo0, fo_end = 0;
   uint32_t Tv, Tall;
   if (BT) {
-    const uint64_t s0 = a.span_start[tile], s1 = a.span_start[tile + 1];
-    p0 = s0 < a.n ? s0 : a.n;
-    const uint64_t p1 = s1 < a.n ? (s1 > p0 ? s1 : p0) : a.n;
+    const SpanRec r0 = a.span_rec[tile], r1 = a.span_rec[tile + 1];
+    p0 = r0.p < a.n ? r0.p : a.n;
+    const uint64_t p1 = r1.p < a.n ? (r1.p > p0 ? r1.p : p0) : a.n;
     Tall = (uint32_t)(p1 - p0);
     if (Tall == 0) return;
     Tv = Tall < T ? Tall : T;
+    fo0 = r0.fo;
+    fo_end = r1.fo;  // frame_off[p0 + Tv] when Tall <= T (else the per-packet path)
   } else {
     p0 = tile * T;
     const uint64_t left = a.n - p0;
     Tv = Tall = left < T ? (uint32_t)left : T;
+    fo0 = a.frame_off[p0];
+    fo_end = a.frame_off[p0 + Tv];
   }
   // Header-table loads first (small tiles): their latency overlaps the
   // offset loads and phase 1 instead of following the barrier.
@@ -449,13 +487,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     t_ack = a.ack_in[p0 + q];
     t_flags = a.flags_in[p0 + q];
   }
-  const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
   if (call_failed(a.status)) return;  // issued with the offset loads: one round trip for both
   const uint64_t po0 = fo0 - p0 * (uint64_t)H;
   const uint64_t po_end = fo_end - (p0 + Tv) * (uint64_t)H;
   const uint64_t A = po0 & ~15ull;
   const uint64_t run = ((po_end + 15u) & ~15ull) - A;
-  if (run > cap || Tall > T) {  // uniform over the workgroup
+  if (Tall > T || run > cap) {  // uniform over the workgroup
     if (a.ablate & 4u) return;  // diagnostic (wrong output): overflowing tiles do nothing
     for (uint32_t q0 = 0; q0 < Tall; q0 += kBlock >> glog)  // (byte tiles may hold more than T packets)
       encode_varlen_packet<H>(a, p0 + q0 + q, q0 + q < Tall, g, glog);
@@ -486,6 +523,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
       for (uint32_t u = 0; u < P; ++u) {
         const uint32_t v = v0 + u * kBlock;
         if (v < nvec) dst[v] = r[u];
+        // byte tiles' block sums from the registers: whole 64-B blocks only
+        // (uniform per quad; the run's partial last block is never inside a
+        // packet's payload, only its edge)
+        if (pfx_sums && (v | 3u) < nvec) {
+          const uint32_t eo = quad_sum(eo_sum(lo64(r[u]), hi64(r[u])));
+          if ((tid & 3u) == 0) lds_pfx[v >> 2] = (uint64_t)(eo & 0xFFFFu) | ((uint64_t)(eo >> 16) << 32);
+        }
       }
     }
     if (a.early_fo) {
@@ -507,7 +551,47 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   if (BT) {
     // Byte tiles: lanes take contiguous ranges of chunks, not packets, so a
     // tile of ragged lengths keeps every lane equally busy.
-    if (a.btile_sums == 1) {
+    if (pfx_sums) {
+      const u32x4* run16 = reinterpret_cast<const u32x4*>(lds_pay + kVTGuard);
+      // 8 lanes per packet: lanes 0-3 take the chunks of the block holding the
+      // payload's first byte, lanes 4-7 those of the block holding its last
+      // (each masked to the payload), and all 8 the block sums between
+      uint32_t* sums = reinterpret_cast<uint32_t*>(lds_hdr);
+      for (uint32_t r0 = 0; r0 < Tv; r0 += kBlock / 8u) {
+        const uint32_t qq = r0 + (tid >> 3), l = tid & 7u;
+        uint32_t e = 0, o = 0, odd = 0;
+        if (qq < Tv && !(a.ablate & 2u)) {
+          const uint32_t fs = lds_fo[qq], fe = lds_fo[qq + 1];
+          const uint32_t d = shift + fs - qq * H;  // payload [d, d + Lq) in LDS
+          odd = d & 1u;
+          if (fe - fs > (uint32_t)H) {
+            const uint32_t x0 = d - kVTGuard, x1 = x0 + (fe - fs - H);  // run offsets
+            const uint32_t j0 = x0 >> 6, j1 = (x1 - 1u) >> 6;
+            const uint32_t j = l < 4u ? j0 : j1;
+            const uint32_t cx = (j << 6) + ((l & 3u) << 4);
+            if ((l < 4u || j1 != j0) && cx < x1 && cx + 16u > x0) {  // (no reads past the run)
+              const u32x4 w = run16[cx >> 4];
+              const int lo = (int)x0 - (int)cx, hi = (int)x1 - (int)cx;
+              const uint32_t eo = eo_sum(lo64(w) & byte_mask(lo, hi), hi64(w) & byte_mask(lo - 8, hi - 8));
+              e = eo & 0xFFFFu;
+              o = eo >> 16;
+            }
+            for (uint32_t jj = j0 + 1u + l; jj < j1; jj += 8u) {
+              const uint64_t bs = lds_pfx[jj];
+              e += (uint32_t)bs;
+              o += (uint32_t)(bs >> 32);
+            }
+          }
+        }
+        e = quad_sum(e);
+        o = quad_sum(o);
+        e += __shfl_xor(e, 4, 64);
+        o += __shfl_xor(o, 4, 64);
+        // payload byte x - d is a low byte when even
+        if (qq < Tv && l == 0) sums[2u * qq] = odd ? (e << 8) + o : e + (o << 8);
+      }
+      __syncthreads();  // the map below overwrites the block sums
+    } else if (a.btile_sums == 1) {
       varlen_tile_chunk_sums<H>(lds_pay, lds_fo, reinterpret_cast<uint32_t*>(lds_hdr), Tv, shift,
                                 shift + (uint32_t)(po_end - po0), (a.ablate & 2u) != 0);
     } else {
@@ -535,7 +619,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
         if (qq < Tv && gg == 0) sums[2u * qq] = part;
       }
     }
-    varlen_tile_chunk_map<H>(lds_fo, lds_map, lds_map16, wide, Tv, lead, nbytes);
+    if (a.ablate & 8u) {  // diagnostic (wrong output): a zero map, coalesced, no frame search
+      const uint32_t units = nbytes > lead ? (nbytes - lead + 15u) >> 4 : 0u;
+      for (uint32_t k = tid; k < units; k += kBlock) {
+        if (wide) lds_map16[k] = 0;
+        else lds_map[k] = 0;
+      }
+    } else {
+      varlen_tile_chunk_map<H>(lds_fo, lds_map, lds_map16, wide, Tv, lead, nbytes);
+    }
     __syncthreads();
     if (q < Tv) sum = reinterpret_cast<const uint32_t*>(lds_hdr)[2u * q];
   } else if (q < Tv) {
@@ -1694,9 +1786,10 @@ int launch_varlen_tile_w(const VarlenArgs& args, size_t lds, uint64_t blocks, hi
 template <int H>
 int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
   VarlenArgs args = in;
-  const uint64_t blocks = args.span_start ? args.span_count : (args.n + args.tile_T - 1) / args.tile_T;
+  const uint64_t blocks = args.span_rec ? args.span_count : (args.n + args.tile_T - 1) / args.tile_T;
   const auto tile_lds = [&](uint32_t wide) {
-    size_t b = vt_pay_off(args.tile_T, args.tile_cap, H, wide) + 2u * kVTGuard + args.tile_cap;
+    size_t b = vt_pay_off(args.tile_T, args.tile_cap, H, wide, args.btile_sums == 2u) + 2u * kVTGuard +
+               args.tile_cap;
     if (args.vhc) b = ((b + 15u) & ~size_t(15)) + 32u * args.tile_T;
     return b;
   };
@@ -1705,7 +1798,8 @@ int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
   // used instead (profiles/r01/sweeps/varlen_coded_map.json).
   constexpr size_t kLdsPerCu = 160u * 1024u;
   if (args.vhc == 2u && kLdsPerCu / tile_lds(1) < 4u && kLdsPerCu / tile_lds(0) >= 4u) args.vhc = 1u;
-  size_t lds = vt_pay_off(args.tile_T, args.tile_cap, H, args.vhc == 2u ? 1u : 0u) + 2u * kVTGuard + args.tile_cap;
+  size_t lds = vt_pay_off(args.tile_T, args.tile_cap, H, args.vhc == 2u ? 1u : 0u, args.btile_sums == 2u) +
+               2u * kVTGuard + args.tile_cap;
   if (args.vhc) {  // prebuilt header chunks [T][2] x 16 B after the payload run
     lds = (lds + 15u) & ~size_t(15);
     args.hc_off = (uint32_t)lds;
@@ -1723,7 +1817,7 @@ int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
     const size_t per_cu = kLdsPerCu / lds;
     w = per_cu >= 7 ? 7 : per_cu == 6 ? 6 : 1;
   }
-  if (args.span_start)  // byte tiles: register budget for the LDS occupancy (5 tiles per CU at MTU hints)
+  if (args.span_rec)  // byte tiles: register budget for the LDS occupancy (5 tiles per CU at MTU hints)
     return launch_varlen_tile_w<H, 5, true>(args, lds, blocks, stream);
   return w == 6 ? launch_varlen_tile_w<H, 6>(args, lds, blocks, stream)
        : w == 7 ? launch_varlen_tile_w<H, 7>(args, lds, blocks, stream)
@@ -1873,7 +1967,7 @@ int launch_validate_utf8(const Utf8Args& args, hipStream_t stream) {
 int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
                        const ScanCheck& chk, hipStream_t stream, const SpanStarts& spans) {
   // the device-side checks and the span starts live in the three-pass scan only
-  if (tuning().varlen_scan == 1 || chk.status || spans.start)
+  if (tuning().varlen_scan == 1 || chk.status || spans.rec)
     return scan_frame_offsets_3pass(d_len, n, H, d_frame_off, chk, stream, spans);
   hipcub::CountingInputIterator<uint64_t> idx(0);
   hipcub::TransformInputIterator<uint64_t, FrameLen, hipcub::CountingInputIterator<uint64_t>> it(

@@ -9,10 +9,13 @@ pointers / streams from torch are valid in it.
 from __future__ import annotations
 
 import ctypes
+import os
 import threading
 from pathlib import Path
 
-LIB_PATH = Path(__file__).resolve().parent / "librudp.so"
+# RUDP_LIB names another build of the same ABI (A/B timing of two builds in one
+# GPU call, tools/ only); the default is the in-tree build.
+LIB_PATH = Path(os.environ.get("RUDP_LIB") or Path(__file__).resolve().parent / "librudp.so")
 
 LAYOUT_RUDP5 = 5
 LAYOUT_RUDP7 = 7

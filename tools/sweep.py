@@ -492,7 +492,9 @@ def ragged_sweep(reps):
         specs = {"default": (), "no_sums": ((35, 2),), "skip_overflow": ((35, 4),),
                  "no_sums_skip_overflow": ((35, 6),), "cap125": ((39, 125),), "cap150": ((39, 150),),
                  "cap200": ((39, 200),), "no_hchunk": ((36, 0),), "btile": ((51, 1),),
-                 "btile_chunksums": ((51, 1), (52, 1)), "btile_no_sums": ((51, 1), (35, 2))}
+                 "btile_chunksums": ((51, 1), (52, 1)), "btile_blocksums": ((51, 1), (52, 2)),
+                 "btile_no_sums": ((51, 1), (35, 2)), "btile_blocksums_no_map": ((51, 1), (52, 2), (35, 8)),
+                 "btile_no_sums_no_map": ((51, 1), (35, 10))}
         variants = {}
         for name, kv in specs.items():
             def setup(kv=kv):
