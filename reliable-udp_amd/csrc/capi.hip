@@ -596,6 +596,8 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
   // the host): spans of S = budget - 2 * hint - 64 bytes, so a tile overflows its
   // LDS budget only through a packet over twice the hint; at most tile_T
   // packets per tile in LDS (more take the per-packet path).
+  // Sum pass of the tile kernels: 2 = from 64-B block sums (either tile form)
+  a.tile_sums = tuning().varlen_tile_sums == 2 ? 2u : 0u;
   SpanStarts spans{};
   if (tuning().varlen_btile && chk.status && !in->payload_off && a.tile_T && aligned16(in->payload) &&
       aligned16(d_frames)) {
@@ -612,9 +614,7 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
       a.span_rec = spans.rec;
       a.span_count = spans.count;
       a.tile_T = (uint32_t)slots;
-      a.tile_glog = 0;
-      const int bs = tuning().varlen_btile_sums;
-      a.btile_sums = bs == 1 || bs == 2 ? (uint32_t)bs : 0u;
+      a.tile_glog = 0;  // (per tile, from its packet count)
     }
   }
   rc = scan_frame_offsets(in->len, in->n, (uint32_t)layout, d_frame_off, chk, s, spans);

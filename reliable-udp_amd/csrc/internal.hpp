@@ -98,8 +98,7 @@ struct VarlenArgs {
   uint32_t align64;               // tile kernel: wave stores start on 64-B sector boundaries
   uint32_t early_table;           // tile kernel: header-table loads before phase 1
   uint32_t ablate;                // diagnostics only (wrong output): 1 = phase 2 without the frame walk,
-                                  // 2 = no sum pass, 4 = tiles over their LDS budget do nothing,
-                                  // 8 = byte tiles with a zero chunk map
+                                  // 2 = no sum pass, 4 = tiles over their LDS budget do nothing
   uint32_t vhc;                   // tile kernel: prebuilt header chunks + pure-chunk fast phase 2
   uint32_t hc_off;                // LDS byte offset of the header-chunk array (set by the launcher)
   uint32_t early_fo;              // tile kernels: the tile's frame offsets loaded before phase 1
@@ -118,10 +117,12 @@ struct VarlenArgs {
   uint32_t xcd;                   // tile kernels: XCD-contiguous tile order (xcd_tile)
   // Byte-tiled encode: workgroup k frames the packets whose payload starts in
   // [k*S, (k+1)*S) (span_rec[k].p .. span_rec[k+1].p, from the scan), span_count
-  // workgroups; tile_T is then the most packets a tile holds in LDS, glog 0.
+  // workgroups; tile_T is then the most packets a tile holds in LDS (lanes per packet
+  // from each tile's packet count).
   const struct SpanRec* span_rec;
   uint64_t span_count;
-  uint32_t btile_sums;            // byte tiles' sum pass: 0 rounds of 16 packets x 16 lanes, 1 chunk-parallel, 2 block sums
+  uint32_t tile_sums;             // tile sum pass: 2 from 64-B block sums (byte tiles always), 0 G lanes
+                                  // per packet
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -276,7 +277,11 @@ struct Tuning {
   // packet count: no tile overflows short of one packet past the budget's
   // slack, and the sum pass is chunk-parallel (0: packet-count tiles).
   std::atomic<int> varlen_btile{0};
-  std::atomic<int> varlen_btile_sums{0};  // byte tiles' sum pass (VarlenArgs::btile_sums)
+  std::atomic<int> varlen_lds_pad{0};  // extra dynamic LDS per varlen encode tile (sweeps only)
+  // Varlen tile sum pass from 128-B block sums (VarlenArgs::tile_sums 2): 1M x
+  // 1472 B 0.544 -> 0.527 ms, lengths uniform in [0, 2944] 0.808 -> 0.729
+  // (profiles/r02/sweeps/ragged_blocksums.json).
+  std::atomic<int> varlen_tile_sums{2};
   std::atomic<int> host_slots{3};     // *_host pipeline: device staging slots (2..8)
   std::atomic<int> host_stage_mb{128};  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
 };

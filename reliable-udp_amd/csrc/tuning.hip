@@ -261,7 +261,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // packets per thread; 48: fixed-length encode packets per launch (0 = one launch);
 // 49: XCD-contiguous tile order in the decode / varlen / UTF-8 tile kernels;
 // 50: small-frame encode finds its tile bases itself (no pass-2 launch);
-// 51: varlen encode tiles by payload bytes; 52: their sum pass (0 packet rounds, 1 chunk-parallel, 2 block sums).
+// 51: varlen encode tiles by payload bytes; 52: varlen tile sum pass (2 from 64-B block sums, 0 G lanes per
+// packet; byte tiles always 2).
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
@@ -297,7 +298,7 @@ int rudpx_tune(int key, int value) {
             : key == 49 ? &t.tile_xcd
             : key == 50 ? &t.varlen_small_fused
             : key == 51 ? &t.varlen_btile
-            : key == 52 ? &t.varlen_btile_sums : nullptr;
+            : key == 52 ? &t.varlen_tile_sums : key == 53 ? &t.varlen_lds_pad : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }

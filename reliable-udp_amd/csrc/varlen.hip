@@ -215,38 +215,34 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_vec_kernel(VarlenArgs a)
 }
 
 // LDS layout of the varlen encode tile: header words u64[T], tile-relative
-// frame offsets u32[T + 1], the chunk -> frame map u8[], then the payload run
+// frame offsets u32[T + 1], the chunk -> frame map u8[] (first holding the
+// block-sum pass's u32 sums of the run's 128-B blocks), then the payload run
 // (guard, cap bytes, guard).  Shared by the launcher (LDS size) and the kernel.
 constexpr uint32_t kVTGuard = 32;
 // The map holds one u8 (owner frame) per output chunk, or with the coded map
 // (vhc == 2) one u16: owner frame in bits 0-7, bit 15 = pure payload chunk,
 // else bit 8 = header chunk of the next frame and bit 9 = its slot.
-// Byte tiles with the block-sum pass (btile_sums 2) reuse the map's bytes for
-// the run's 64-B block sums first: u64 per block, 8-B aligned.
-__host__ __device__ inline uint32_t vt_map_bytes(uint32_t T, uint32_t cap, uint32_t H, uint32_t wide,
-                                                 uint32_t pfx = 0) {
-  const uint32_t map = (((cap + T * H) >> 4) + 4u) << (wide ? 1 : 0);
-  const uint32_t blocks = 8u * ((cap >> 6) + 3u) + 8u;
-  return pfx && blocks > map ? blocks : map;
+__host__ __device__ inline uint32_t vt_map_bytes(uint32_t T, uint32_t cap, uint32_t H, uint32_t wide) {
+  return (((cap + T * H) >> 4) + 4u) << (wide ? 1 : 0);
 }
 // Frames of at least this many bytes: an aligned 16-B chunk overlaps at most
 // one header, and the 16 payload bytes before a frame's payload belong to the
 // previous frame (the varlen tile's fast phase 2).
 constexpr uint32_t kVHCMinFrame = 32;
 
-__host__ __device__ inline uint32_t vt_pay_off(uint32_t T, uint32_t cap, uint32_t H, uint32_t wide,
-                                               uint32_t pfx = 0) {
-  return (8u * T + 4u * (T + 1u) + vt_map_bytes(T, cap, H, wide, pfx) + 15u) & ~15u;
+// (the map's bytes hold the block sums, 4 B per 128 B of run, before it)
+__host__ __device__ inline uint32_t vt_pay_off(uint32_t T, uint32_t cap, uint32_t H, uint32_t wide) {
+  return (8u * T + 4u * (T + 1u) + vt_map_bytes(T, cap, H, wide) + 15u) & ~15u;
 }
 
-// Byte tiles, the block-sum pass (btile_sums 2).  The packet-count tile gives
-// every packet G lanes; with ragged lengths in a byte tile that leaves most
-// lanes idle while the longest packet is summed.  Instead every 64-B block of
-// the run gets its even- and odd-address byte sums as phase 1 streams it
-// through registers (a quad of lanes holds the block's four vectors), and a
-// packet adds the block sums inside its payload plus its two edge blocks
-// chunk by chunk (8 lanes per packet): 16 times fewer LDS reads per packet
-// byte than summing its chunks.
+// The block-sum pass (tile_sums 2).  Summing a packet's payload chunk by
+// chunk out of LDS gives its G lanes work in proportion to its length, so a
+// tile of ragged lengths waits for its longest packet.  Instead every 128-B
+// block of the run gets its even- and odd-address byte sums as phase 1
+// streams it through registers (8 lanes hold the block's 8 vectors), and a
+// packet's G lanes add the block sums inside its payload plus the 16 chunks
+// of its two edge blocks, masked: one LDS read per 128 payload bytes instead
+// of 8.
 // Even/odd byte sums of a 16-B chunk, packed e | o << 16 (each at most 2040).
 __device__ __forceinline__ uint32_t eo_sum(uint64_t lo, uint64_t hi) {
   constexpr uint64_t M = 0x00FF00FF00FF00FFull;
@@ -258,121 +254,12 @@ template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
   return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
 }
-// Sum over the 4 lanes of a quad (all 4 active).
-__device__ __forceinline__ uint32_t quad_sum(uint32_t x) {
-  x += dpp_u32<0xB1>(x);  // quad_perm [1, 0, 3, 2]
-  x += dpp_u32<0x4E>(x);  // quad_perm [2, 3, 0, 1]
+// Sum over 8 consecutive lanes (all 8 active).
+__device__ __forceinline__ uint32_t octet_sum(uint32_t x) {
+  x += dpp_u32<0xB1>(x);   // quad_perm [1, 0, 3, 2]
+  x += dpp_u32<0x4E>(x);   // quad_perm [2, 3, 0, 1]
+  x += dpp_u32<0x141>(x);  // row_half_mirror: the other quad of the 8
   return x;
-}
-
-// Byte tiles, the sum pass: lane t takes a contiguous range of the run's
-// aligned 16-B chunks and the packet holding its first chunk (binary search
-// over the tile's offsets).  Chunk reads go out kChunkRound at a time.  When the range touches at most two packets (the common case
-// at MTU sizes) it sums both without further LDS reads, and the wave combines
-// lanes of the same packet with a segmented shuffle scan, so each packet gets
-// one LDS atomic per wave; other ranges walk their packets and add their parts
-// directly.  Packet q's payload sits at LDS [d(q), d(q+1)),
-// d(q) = shift + fo[q] - q*H.
-constexpr uint32_t kChunkRound = 4;
-// Combine a wave's lanes per packet with a segmented shuffle scan before the
-// LDS atomics (1), or let every lane add its own part (0).
-constexpr bool kWaveCombine = false;
-
-__device__ __forceinline__ uint32_t masked_le16(u32x4 v, uint32_t X, uint32_t a0, uint32_t a1) {
-  if (a1 <= X || a0 >= X + 16u || a1 <= a0) return 0u;
-  const int rel = (int)X - (int)a0;  // payload index of chunk byte 0
-  const int len = (int)(a1 - a0);
-  return payload_le16_sum(lo64(v) & byte_mask(-rel, len - rel), hi64(v) & byte_mask(-rel - 8, len - rel - 8),
-                          rel);
-}
-
-// Inclusive sum over the lanes of a wave whose key equals this lane's (keys
-// non-decreasing across lanes); true on the last lane of each key's run.
-__device__ __forceinline__ bool segmented_sum(uint32_t key, uint32_t& x) {
-  const uint32_t lane = threadIdx.x & 63u;
-  for (uint32_t d = 1; d < 64; d <<= 1) {
-    const uint32_t y = __shfl_up(x, d, 64);
-    const uint32_t k = __shfl_up(key, d, 64);
-    if (lane >= d && k == key) x += y;
-  }
-  const uint32_t kn = __shfl_down(key, 1, 64);
-  return lane == 63u || kn != key;
-}
-
-template <int H>
-__device__ __forceinline__ void varlen_tile_chunk_sums(const unsigned char* lds_pay, const uint32_t* fo,
-                                                       uint32_t* sums, uint32_t Tv, uint32_t shift,
-                                                       uint32_t run_end, bool ablate) {
-  if (ablate || run_end <= shift) return;  // uniform
-  const u32x4* pay16 = reinterpret_cast<const u32x4*>(lds_pay);
-  auto d = [&](uint32_t q) { return shift + fo[q] - q * (uint32_t)H; };
-  const uint32_t cfirst = shift >> 4, clast = (run_end - 1u) >> 4;
-  const uint32_t nch = clast - cfirst + 1u;
-  const uint32_t per = (nch + kBlock - 1u) / kBlock;
-  const uint32_t c0 = cfirst + threadIdx.x * per;
-  const uint32_t cnt = c0 <= clast ? (clast - c0 + 1u < per ? clast - c0 + 1u : per) : 0u;
-  uint32_t keyA = 0xFFFFFFFFu, keyB = 0xFFFFFFFFu, accA = 0, accB = 0;
-  if (cnt) {
-    uint32_t lo = 0, hi = Tv - 1u;  // the last packet starting at or before chunk c0's first byte
-    while (lo < hi) {
-      const uint32_t mid = (lo + hi + 1u) >> 1;
-      if (d(mid) <= (c0 << 4)) lo = mid;
-      else hi = mid - 1u;
-    }
-    const uint32_t q = lo;
-    const uint32_t dq = d(q), dn = d(q + 1u);
-    const uint32_t dnn = q + 2u <= Tv ? d(q + 2u) : dn;
-    const uint32_t X1 = (c0 + cnt) << 4;
-    if (q + 1u >= Tv || dnn >= X1) {  // at most packets q and q + 1
-      // rounds of kChunkRound chunk reads issued together, then summed
-      for (uint32_t i0 = 0; i0 < cnt; i0 += kChunkRound) {
-        u32x4 v[kChunkRound];
-#pragma unroll
-        for (uint32_t i = 0; i < kChunkRound; ++i)
-          if (i0 + i < cnt) v[i] = pay16[c0 + i0 + i];
-#pragma unroll
-        for (uint32_t i = 0; i < kChunkRound; ++i) {
-          if (i0 + i < cnt) {
-            const uint32_t X = (c0 + i0 + i) << 4;
-            accA += masked_le16(v[i], X, dq, dn);
-            if (q + 1u < Tv) accB += masked_le16(v[i], X, dn, dnn);
-          }
-        }
-      }
-      keyA = q;
-      keyB = q + 1u < Tv ? q + 1u : 0xFFFFFFFFu;
-    } else {  // walk the packets across the range (keys stay sorted for the wave scan, sums 0)
-      keyA = q;
-      keyB = q + 1u < Tv ? q + 1u : 0xFFFFFFFFu;
-      for (uint32_t i = 0; i < cnt; ++i) {
-        const uint32_t c = c0 + i, X = c << 4;
-        const u32x4 w = pay16[c];  // (no runtime index into v: that would move it to scratch)
-        uint32_t qq = q, a0 = dq, a1 = dn;
-        while (a1 <= X && qq + 1u < Tv) {
-          ++qq;
-          a0 = a1;
-          a1 = d(qq + 1u);
-        }
-        while (true) {
-          const uint32_t part = masked_le16(w, X, a0, a1);
-          if (part) atomicAdd(&sums[2u * qq], part);
-          if (a1 >= X + 16u || qq + 1u >= Tv) break;
-          ++qq;
-          a0 = a1;
-          a1 = d(qq + 1u);
-        }
-      }
-    }
-  }
-  if (kWaveCombine) {
-    // every lane takes part in the shuffles (keys sorted across the wave: q is
-    // non-decreasing in the lane index, and lanes without a key sit at the end)
-    if (segmented_sum(keyA, accA) && keyA != 0xFFFFFFFFu && accA) atomicAdd(&sums[2u * keyA], accA);
-    if (segmented_sum(keyB, accB) && keyB != 0xFFFFFFFFu && accB) atomicAdd(&sums[2u * keyB], accB);
-  } else {
-    if (accA) atomicAdd(&sums[2u * keyA], accA);
-    if (accB) atomicAdd(&sums[2u * keyB], accB);
-  }
 }
 
 // Byte tiles, the chunk -> frame map: lane t takes a contiguous range of the
@@ -445,20 +332,19 @@ __device__ __forceinline__ void varlen_tile_chunk_map(const uint32_t* fo, uint8_
 template <int H, int W, bool BT>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))) encode_varlen_tile_kernel(VarlenArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const uint32_t T = a.tile_T, glog = a.tile_glog, G = 1u << glog, cap = a.tile_cap;
+  const uint32_t T = a.tile_T, cap = a.tile_cap;
   uint64_t* lds_hdr = reinterpret_cast<uint64_t*>(lds);
   uint32_t* lds_fo = reinterpret_cast<uint32_t*>(lds + 8u * T);
   const bool wide = a.vhc == 2u;  // coded chunk map (u16 entries)
+  const bool blk_sums = a.tile_sums == 2u;  // the block-sum pass
   uint8_t* lds_map = reinterpret_cast<uint8_t*>(lds_fo + T + 1u);
   uint16_t* lds_map16 = reinterpret_cast<uint16_t*>(lds_map);
-  const bool pfx_sums = BT && a.btile_sums == 2u;  // byte tiles' block-sum pass
-  uint64_t* lds_pfx = reinterpret_cast<uint64_t*>(lds + ((8u * T + 4u * (T + 1u) + 7u) & ~7u));
-  unsigned char* lds_pay = lds + vt_pay_off(T, cap, H, wide ? 1u : 0u, pfx_sums ? 1u : 0u);
+  uint32_t* lds_blk = reinterpret_cast<uint32_t*>(lds_map);  // (until the map is built)
+  unsigned char* lds_pay = lds + vt_pay_off(T, cap, H, wide ? 1u : 0u);
 
   const uint32_t tid = threadIdx.x;
-  const uint32_t q = tid >> glog, g = tid & (G - 1u);
   const uint64_t tile = a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
-  // Byte tiles (span_rec set, glog 0): the packets whose payload starts in
+  // Byte tiles (span_rec set): the packets whose payload starts in
   // span `tile` (clamped, so a rejected batch's unwritten records stay in
   // range), their frame run from the same two records; else T packets.
   uint64_t p0, fo0, fo_end = 0;
@@ -479,6 +365,14 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     fo0 = a.frame_off[p0];
     fo_end = a.frame_off[p0 + Tv];
   }
+  // G = 2^glog lanes per packet: the launcher's for packet tiles; for a byte
+  // tile as many as its packet count leaves (all four waves busy)
+  uint32_t glog = a.tile_glog;
+  if (BT) {
+    glog = 0;
+    while (glog < 6u && (Tv << (glog + 1u)) <= kBlock) ++glog;
+  }
+  const uint32_t G = 1u << glog, q = tid >> glog, g = tid & (G - 1u);
   // Header-table loads first (small tiles): their latency overlaps the
   // offset loads and phase 1 instead of following the barrier.
   uint32_t t_seq = 0, t_ack = 0, t_flags = 0;
@@ -488,6 +382,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     t_flags = a.flags_in[p0 + q];
   }
   if (call_failed(a.status)) return;  // issued with the offset loads: one round trip for both
+  const bool early_tab = a.early_table;
   const uint64_t po0 = fo0 - p0 * (uint64_t)H;
   const uint64_t po_end = fo_end - (p0 + Tv) * (uint64_t)H;
   const uint64_t A = po0 & ~15ull;
@@ -523,12 +418,12 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
       for (uint32_t u = 0; u < P; ++u) {
         const uint32_t v = v0 + u * kBlock;
         if (v < nvec) dst[v] = r[u];
-        // byte tiles' block sums from the registers: whole 64-B blocks only
-        // (uniform per quad; the run's partial last block is never inside a
+        // block sums from the registers: whole 128-B blocks only (uniform
+        // per 8 lanes; the run's partial last block is never inside a
         // packet's payload, only its edge)
-        if (pfx_sums && (v | 3u) < nvec) {
-          const uint32_t eo = quad_sum(eo_sum(lo64(r[u]), hi64(r[u])));
-          if ((tid & 3u) == 0) lds_pfx[v >> 2] = (uint64_t)(eo & 0xFFFFu) | ((uint64_t)(eo >> 16) << 32);
+        if (blk_sums && (v | 7u) < nvec) {
+          const uint32_t eo = octet_sum(eo_sum(lo64(r[u]), hi64(r[u])));
+          if ((tid & 7u) == 0) lds_blk[v >> 3] = eo;  // (e, o at most 16320 each)
         }
       }
     }
@@ -538,8 +433,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     } else {
       for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = (uint32_t)(a.frame_off[p0 + i] - fo0);
     }
-    if (BT)  // byte tiles: per-packet sums accumulate in lds_hdr's low words
-      for (uint32_t i = tid; i < T; i += kBlock) lds_hdr[i] = 0;
   }
   __syncthreads();
 
@@ -548,103 +441,54 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   const uint32_t nbytes = (uint32_t)(fo_end - fo0);
   const uint32_t lead = (uint32_t)(-(uintptr_t)(a.frames + fo0)) & 15u;
   uint32_t sum = 0;
-  if (BT) {
-    // Byte tiles: lanes take contiguous ranges of chunks, not packets, so a
-    // tile of ragged lengths keeps every lane equally busy.
-    if (pfx_sums) {
-      const u32x4* run16 = reinterpret_cast<const u32x4*>(lds_pay + kVTGuard);
-      // 8 lanes per packet: lanes 0-3 take the chunks of the block holding the
-      // payload's first byte, lanes 4-7 those of the block holding its last
-      // (each masked to the payload), and all 8 the block sums between
-      uint32_t* sums = reinterpret_cast<uint32_t*>(lds_hdr);
-      for (uint32_t r0 = 0; r0 < Tv; r0 += kBlock / 8u) {
-        const uint32_t qq = r0 + (tid >> 3), l = tid & 7u;
-        uint32_t e = 0, o = 0, odd = 0;
-        if (qq < Tv && !(a.ablate & 2u)) {
-          const uint32_t fs = lds_fo[qq], fe = lds_fo[qq + 1];
-          const uint32_t d = shift + fs - qq * H;  // payload [d, d + Lq) in LDS
-          odd = d & 1u;
-          if (fe - fs > (uint32_t)H) {
-            const uint32_t x0 = d - kVTGuard, x1 = x0 + (fe - fs - H);  // run offsets
-            const uint32_t j0 = x0 >> 6, j1 = (x1 - 1u) >> 6;
-            const uint32_t j = l < 4u ? j0 : j1;
-            const uint32_t cx = (j << 6) + ((l & 3u) << 4);
-            if ((l < 4u || j1 != j0) && cx < x1 && cx + 16u > x0) {  // (no reads past the run)
-              const u32x4 w = run16[cx >> 4];
-              const int lo = (int)x0 - (int)cx, hi = (int)x1 - (int)cx;
-              const uint32_t eo = eo_sum(lo64(w) & byte_mask(lo, hi), hi64(w) & byte_mask(lo - 8, hi - 8));
-              e = eo & 0xFFFFu;
-              o = eo >> 16;
-            }
-            for (uint32_t jj = j0 + 1u + l; jj < j1; jj += 8u) {
-              const uint64_t bs = lds_pfx[jj];
-              e += (uint32_t)bs;
-              o += (uint32_t)(bs >> 32);
-            }
-          }
-        }
-        e = quad_sum(e);
-        o = quad_sum(o);
-        e += __shfl_xor(e, 4, 64);
-        o += __shfl_xor(o, 4, 64);
-        // payload byte x - d is a low byte when even
-        if (qq < Tv && l == 0) sums[2u * qq] = odd ? (e << 8) + o : e + (o << 8);
-      }
-      __syncthreads();  // the map below overwrites the block sums
-    } else if (a.btile_sums == 1) {
-      varlen_tile_chunk_sums<H>(lds_pay, lds_fo, reinterpret_cast<uint32_t*>(lds_hdr), Tv, shift,
-                                shift + (uint32_t)(po_end - po0), (a.ablate & 2u) != 0);
-    } else {
-      // rounds of 16 packets, 16 lanes each (the packet-count tile's sum pass)
-      uint32_t* sums = reinterpret_cast<uint32_t*>(lds_hdr);
-      const u32x4* pay16 = reinterpret_cast<const u32x4*>(lds_pay);
-      for (uint32_t r0 = 0; r0 < Tv; r0 += kBlock / 16u) {
-        const uint32_t qq = r0 + (tid >> 4), gg = tid & 15u;
-        uint32_t part = 0;
-        if (qq < Tv && !(a.ablate & 2u)) {
-          const uint32_t fs = lds_fo[qq], fe = lds_fo[qq + 1];
-          const uint32_t Lq = fe - fs - H;
-          const uint32_t d = shift + fs - qq * H;
-          if (Lq) {
-            const uint32_t c1 = (d + Lq - 1u) >> 4;
-            for (uint32_t c = (d >> 4) + gg; c <= c1; c += 16u) {
-              const u32x4 v = pay16[c];
-              const int rel = (int)(c << 4) - (int)d;
-              part += payload_le16_sum(lo64(v) & byte_mask(-rel, (int)Lq - rel),
-                                       hi64(v) & byte_mask(-rel - 8, (int)Lq - rel - 8), rel);
-            }
-          }
-        }
-        for (uint32_t m = 8; m > 0; m >>= 1) part += __shfl_xor(part, (int)m, 64);
-        if (qq < Tv && gg == 0) sums[2u * qq] = part;
-      }
-    }
-    if (a.ablate & 8u) {  // diagnostic (wrong output): a zero map, coalesced, no frame search
-      const uint32_t units = nbytes > lead ? (nbytes - lead + 15u) >> 4 : 0u;
-      for (uint32_t k = tid; k < units; k += kBlock) {
-        if (wide) lds_map16[k] = 0;
-        else lds_map[k] = 0;
-      }
-    } else {
-      varlen_tile_chunk_map<H>(lds_fo, lds_map, lds_map16, wide, Tv, lead, nbytes);
-    }
-    __syncthreads();
-    if (q < Tv) sum = reinterpret_cast<const uint32_t*>(lds_hdr)[2u * q];
-  } else if (q < Tv) {
+  if (q < Tv) {
     const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
     const uint32_t Lq = fe - fs - H;
     const uint32_t d = shift + fs - q * H;  // LDS offset of the packet's first payload byte
     if (Lq && !(a.ablate & 2u)) {  // ablate bit 2 (diagnostic, wrong output): no sum pass
-      const u32x4* pay16 = reinterpret_cast<const u32x4*>(lds_pay);
-      const uint32_t c1 = (d + Lq - 1u) >> 4;
-      for (uint32_t c = (d >> 4) + g; c <= c1; c += G) {
-        const u32x4 v = pay16[c];
-        const int rel = (int)(c << 4) - (int)d;  // payload index of chunk byte 0
-        const uint64_t lo = lo64(v) & byte_mask(-rel, (int)Lq - rel);
-        const uint64_t hi = hi64(v) & byte_mask(-rel - 8, (int)Lq - rel - 8);
-        sum += payload_le16_sum(lo, hi, rel);
+      if (blk_sums) {
+        // the 16 chunks of the blocks holding the payload's first and last
+        // bytes (each masked to the payload), then the block sums between
+        const u32x4* run16 = reinterpret_cast<const u32x4*>(lds_pay + kVTGuard);
+        const uint32_t x0 = d - kVTGuard, x1 = x0 + Lq;  // run offsets
+        const uint32_t j0 = x0 >> 7, j1 = (x1 - 1u) >> 7;
+        uint32_t e = 0, o = 0;
+        for (uint32_t c = g; c < 16u; c += G) {
+          const uint32_t cx = ((c < 8u ? j0 : j1) << 7) + ((c & 7u) << 4);
+          if ((c < 8u || j1 != j0) && cx < x1 && cx + 16u > x0) {  // (no reads past the run)
+            const u32x4 w = run16[cx >> 4];
+            const int lo = (int)x0 - (int)cx, hi = (int)x1 - (int)cx;
+            const uint32_t eo = eo_sum(lo64(w) & byte_mask(lo, hi), hi64(w) & byte_mask(lo - 8, hi - 8));
+            e += eo & 0xFFFFu;
+            o += eo >> 16;
+          }
+        }
+        for (uint32_t j = j0 + 1u + g; j < j1; j += G) {
+          const uint32_t bs = lds_blk[j];
+          e += bs & 0xFFFFu;
+          o += bs >> 16;
+        }
+        sum = (d & 1u) ? (e << 8) + o : e + (o << 8);  // payload byte x - d is a low byte when even
+      } else {
+        const u32x4* pay16 = reinterpret_cast<const u32x4*>(lds_pay);
+        const uint32_t c1 = (d + Lq - 1u) >> 4;
+        for (uint32_t c = (d >> 4) + g; c <= c1; c += G) {
+          const u32x4 v = pay16[c];
+          const int rel = (int)(c << 4) - (int)d;  // payload index of chunk byte 0
+          const uint64_t lo = lo64(v) & byte_mask(-rel, (int)Lq - rel);
+          const uint64_t hi = hi64(v) & byte_mask(-rel - 8, (int)Lq - rel - 8);
+          sum += payload_le16_sum(lo, hi, rel);
+        }
       }
     }
+  }
+  if (blk_sums) __syncthreads();  // the map overwrites the block sums
+  if (BT) {
+    // Byte tiles: lanes take contiguous ranges of output chunks for the map,
+    // not packets, so a tile of ragged lengths keeps every lane equally busy.
+    varlen_tile_chunk_map<H>(lds_fo, lds_map, lds_map16, wide, Tv, lead, nbytes);
+  } else if (q < Tv) {
+    const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
     // map[k] = q for the output units k whose first byte lead + 16k lies in [fs, fe)
     const uint32_t klo = fs > lead ? (fs - lead + 15u) >> 4 : 0u;
     const uint32_t khi = fe > lead ? (fe - lead + 15u) >> 4 : 0u;
@@ -672,7 +516,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
   if (g == 0 && q < Tv) {
     const uint64_t p = p0 + q;
-    const bool late = !a.early_table;
+    const bool late = !early_tab;
     const uint32_t s = late ? a.seq_in[p] : t_seq, k = late ? a.ack_in[p] : t_ack,
                    f = late ? a.flags_in[p] : t_flags;
     const uint32_t c = packet_csum(sum, s, k, f);
@@ -1788,8 +1632,7 @@ int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
   VarlenArgs args = in;
   const uint64_t blocks = args.span_rec ? args.span_count : (args.n + args.tile_T - 1) / args.tile_T;
   const auto tile_lds = [&](uint32_t wide) {
-    size_t b = vt_pay_off(args.tile_T, args.tile_cap, H, wide, args.btile_sums == 2u) + 2u * kVTGuard +
-               args.tile_cap;
+    size_t b = vt_pay_off(args.tile_T, args.tile_cap, H, wide) + 2u * kVTGuard + args.tile_cap;
     if (args.vhc) b = ((b + 15u) & ~size_t(15)) + 32u * args.tile_T;
     return b;
   };
@@ -1798,13 +1641,13 @@ int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
   // used instead (profiles/r01/sweeps/varlen_coded_map.json).
   constexpr size_t kLdsPerCu = 160u * 1024u;
   if (args.vhc == 2u && kLdsPerCu / tile_lds(1) < 4u && kLdsPerCu / tile_lds(0) >= 4u) args.vhc = 1u;
-  size_t lds = vt_pay_off(args.tile_T, args.tile_cap, H, args.vhc == 2u ? 1u : 0u, args.btile_sums == 2u) +
-               2u * kVTGuard + args.tile_cap;
+  size_t lds = vt_pay_off(args.tile_T, args.tile_cap, H, args.vhc == 2u ? 1u : 0u) + 2u * kVTGuard + args.tile_cap;
   if (args.vhc) {  // prebuilt header chunks [T][2] x 16 B after the payload run
     lds = (lds + 15u) & ~size_t(15);
     args.hc_off = (uint32_t)lds;
     lds += 32u * args.tile_T;
   }
+  lds += (size_t)tuning().varlen_lds_pad;  // (sweeps: LDS occupancy probe)
   // Register budget to match the LDS occupancy: the kernel needs 88 VGPRs (5
   // waves per SIMD) unconstrained, so tiles small enough for 6-7 per CU ask
   // the allocator for that many waves (a few spills in the per-packet

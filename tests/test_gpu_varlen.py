@@ -814,8 +814,7 @@ def test_small_frame_tiles_vs_oracle(cuda, fpt):
 
 @pytest.mark.parametrize("dist", ["ragged", "equal", "bursty", "tiny_runs", "zeros"])
 def test_byte_tiled_varlen_encode_vs_oracle(cuda, dist):
-    """Varlen encode with tiles by payload bytes (key 51: span starts from the
-    scan; key 52: each sum pass) == the oracle, checksums included, for
+    """Varlen encode tile forms (key 51 byte tiles; 52 each sum pass) == the oracle, checksums included, for
     ragged / equal lengths, bursts past the budget's slack, long runs of tiny
     packets (more than a tile's slots) and zero-length packets."""
     import ctypes
@@ -845,16 +844,16 @@ def test_byte_tiled_varlen_encode_vs_oracle(cuda, dist):
     tab = (dev(seq, cuda), dev(ack, cuda), dev(flags, cuda))
     for layout in (5, 7):
         want, off, cs = codec_np.encode_varlen(seq, ack, flags, pays, layout)
-        # (byte tiles, their sum pass: 0 packet rounds / 1 chunk-parallel / 2 block sums, XCD order)
-        for btile, sums, xcd in ((1, 0, 1), (1, 1, 1), (1, 2, 1), (1, 2, 0), (0, 0, 1)):
-            old = (lib.rudpx_tune(51, btile), lib.rudpx_tune(52, sums), lib.rudpx_tune(49, xcd))
+        # (byte tiles, sum pass: 2 block sums / 0 per-packet lanes, XCD order)
+        for knobs in ((1, 2, 1), (1, 2, 0), (0, 0, 1), (0, 2, 1), (0, 2, 0)):
+            old = [lib.rudpx_tune(key, v) for key, v in zip((51, 52, 49), knobs)]
             try:
                 r = batch.pack_batch_varlen(tab, dev(pay, cuda), dev(lens, cuda), layout, want_csum=True,
                                             check=False).check()
             finally:
                 for key, v in zip((51, 52, 49), old):
                     lib.rudpx_tune(key, v)
-            ctx = (dist, layout, btile, sums, xcd)
+            ctx = (dist, layout, knobs)
             assert np.array_equal(host(r.frames), want), ctx
             assert np.array_equal(host(r.frame_off), off), ctx
             assert np.array_equal(host(r.csum), cs), ctx

@@ -1,7 +1,7 @@
 """Run one codec op repeatedly on one shape, for rocprofv3 captures.
 
 usage: python tools/run_kernel.py --op encode|decode|roundtrip [--L 1472] [--n 1048576]
-          [--layout rudp7] [--steps 20]
+          [--layout rudp7] [--steps 20] [--ragged] [--tune 51=1,52=2]
 Prints the HIP-event time per launch so it can be set beside the profiler's
 kernel-trace average.
 """
@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--ragged", action="store_true",
                     help="varlen ops: lengths uniform in [0, 2L] (mean L) instead of all L")
+    ap.add_argument("--tune", default="",
+                    help="rudpx_tune knobs to set first, as key=value[,key=value...]")
     ap.add_argument("--gap-ms", type=float, default=0.0,
                     help="idle time between launches (synchronize, then sleep): separates a "
                          "per-launch effect from one of sustained back-to-back HBM load")
@@ -48,6 +50,9 @@ def main():
     import ctypes
     from rudp import _native
     lib = _native.lib()
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=")
+        lib.rudpx_tune(int(k), int(v))
     scratch = [torch.empty(args.n, dtype=torch.uint16, device=dev) for _ in range(2)] + \
               [torch.empty(args.n, dtype=torch.uint8, device=dev) for _ in range(2)]
 
@@ -102,7 +107,8 @@ def main():
             time.sleep(args.gap_ms / 1e3)
     e.record()
     e.synchronize()
-    print(json.dumps({"op": args.op, "L": args.L, "n": args.n, "layout": args.layout,
+    print(json.dumps({"op": args.op, "L": args.L, "n": args.n, "layout": args.layout, "tune": args.tune,
+                      "ragged": args.ragged,
                       "buffer_sets": nsets, "ms_per_launch": s.elapsed_time(e) / args.steps}))
 
 
