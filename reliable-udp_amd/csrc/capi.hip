@@ -592,29 +592,38 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
     if (rc) return hip_fail((hipError_t)rc, "small-frame varlen encode launch");
     return 0;
   }
+  // Sum pass of the tile kernel: 2 = from 128-B block sums
+  a.tile_sums = tuning().varlen_tile_sums == 2 ? 2u : 0u;
   // Tiles by payload bytes (checked calls, where the payload size is known on
   // the host): spans of S = budget - 2 * hint - 64 bytes, so a tile overflows its
-  // LDS budget only through a packet over twice the hint; at most tile_T
-  // packets per tile in LDS (more take the per-packet path).
-  // Sum pass of the tile kernels: 2 = from 64-B block sums (either tile form)
-  a.tile_sums = tuning().varlen_tile_sums == 2 ? 2u : 0u;
+  // LDS budget only through a packet over twice the hint; at most bt_slots
+  // packets per tile in LDS (more take the per-packet path).  The scan counts
+  // the packet tiles that would overflow, and the tile kernel takes byte tiles
+  // when they are bt_min_over or more (varlen_btile 1: 1/32 of the tiles).
   SpanStarts spans{};
-  if (tuning().varlen_btile && chk.status && !in->payload_off && a.tile_T && aligned16(in->payload) &&
-      aligned16(d_frames)) {
+  const int btile = tuning().varlen_btile;
+  if (btile > 0 && chk.status && !in->payload_off && a.tile_T && aligned16(in->payload) && aligned16(d_frames)) {
     const uint64_t h = in->payload_len ? in->payload_len : 1u;
-    if (a.tile_cap > 2u * h + 64u + h) {
-      const uint64_t S = a.tile_cap - 2u * h - 64u;
-      uint64_t slots = 4;
-      while (slots < 256 && slots < 3u * S / (2u * h) + 2u) slots <<= 1;
+    const uint64_t ptiles = (in->n + a.tile_T - 1u) / a.tile_T;
+    const uint64_t S = a.tile_cap > 2u * h + 64u + h ? a.tile_cap - 2u * h - 64u : 0u;
+    uint64_t slots = 4;
+    while (S && slots < 256 && slots < 3u * S / (2u * h) + 2u) slots <<= 1;
+    if (S && (btile == 2 || varlen_btile_ok(a.tile_T, (uint32_t)slots, a.tile_cap, (uint32_t)layout, a.vhc, ptiles,
+                                           chk.payload_bytes / S + 1u))) {
       spans.bytes = S;
       spans.count = chk.payload_bytes / S + 1u;
       void* buf = nullptr;
-      RUDP_HIP(stream_alloc(&buf, (spans.count + 1u) * sizeof(SpanRec), s));
+      // records [count + 1], then the scan's overflow counter
+      RUDP_HIP(stream_alloc(&buf, (spans.count + 2u) * sizeof(SpanRec), s));
       spans.rec = static_cast<SpanRec*>(buf);
+      spans.over = reinterpret_cast<uint32_t*>(spans.rec + spans.count + 1u);
+      spans.tile_T = a.tile_T;
+      spans.tile_cap = a.tile_cap;
       a.span_rec = spans.rec;
       a.span_count = spans.count;
-      a.tile_T = (uint32_t)slots;
-      a.tile_glog = 0;  // (per tile, from its packet count)
+      a.tile_over = spans.over;
+      a.bt_slots = (uint32_t)slots;
+      a.bt_min_over = btile == 2 ? 0u : (uint32_t)(ptiles / 32u + 1u);
     }
   }
   rc = scan_frame_offsets(in->len, in->n, (uint32_t)layout, d_frame_off, chk, s, spans);

@@ -115,14 +115,19 @@ struct VarlenArgs {
   uint32_t small_fpt;             // decode small-frame tile: frames per thread (0: not used)
   uint32_t small_cap;             // its LDS run budget in bytes
   uint32_t xcd;                   // tile kernels: XCD-contiguous tile order (xcd_tile)
-  // Byte-tiled encode: workgroup k frames the packets whose payload starts in
-  // [k*S, (k+1)*S) (span_rec[k].p .. span_rec[k+1].p, from the scan), span_count
-  // workgroups; tile_T is then the most packets a tile holds in LDS (lanes per packet
-  // from each tile's packet count).
+  // Byte tiles (span_rec set): workgroup k may frame the packets whose payload
+  // starts in [k*S, (k+1)*S) (span_rec[k].p .. span_rec[k+1].p, from the scan)
+  // instead of packet tile k.  The launch picks per call on the device: byte
+  // tiles when the scan counted at least bt_min_over packet tiles over their
+  // LDS budget (*tile_over).  bt_slots is the most packets a byte tile holds
+  // in LDS; tile_Tl = max(tile_T, bt_slots) sizes the LDS arrays.
   const struct SpanRec* span_rec;
   uint64_t span_count;
-  uint32_t tile_sums;             // tile sum pass: 2 from 64-B block sums (byte tiles always), 0 G lanes
-                                  // per packet
+  const uint32_t* tile_over;
+  uint32_t bt_min_over;
+  uint32_t bt_slots;
+  uint32_t tile_Tl;
+  uint32_t tile_sums;             // tile sum pass: 2 from 128-B block sums, 0 chunk by chunk
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -275,8 +280,11 @@ struct Tuning {
   std::atomic<int> encode_launch_packets{0};
   // Varlen encode tiles by payload bytes (spans from the scan) instead of by
   // packet count: no tile overflows short of one packet past the budget's
-  // slack, and the sum pass is chunk-parallel (0: packet-count tiles).
-  std::atomic<int> varlen_btile{0};
+  // slack.  0: packet tiles; 1: byte tiles when over 1/32 of the packet tiles
+  // would overflow (decided on the device per call); 2: byte tiles.  1M x
+  // 1472 B: packet 0.540 / byte 0.621 ms; lengths uniform in [0, 2944]:
+  // 0.728 / 0.644 (profiles/r02/sweeps/ragged_blocksums.json).
+  std::atomic<int> varlen_btile{1};
   std::atomic<int> varlen_lds_pad{0};  // extra dynamic LDS per varlen encode tile (sweeps only)
   // Varlen tile sum pass from 128-B block sums (VarlenArgs::tile_sums 2): 1M x
   // 1472 B 0.544 -> 0.527 ms, lengths uniform in [0, 2944] 0.808 -> 0.729
@@ -295,6 +303,8 @@ int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStr
 int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream_t stream);
 int launch_synth(const SynthArgs& args, hipStream_t stream);
 void varlen_tile_geometry(uint32_t len_hint, uint32_t* T, uint32_t* glog, uint32_t* cap);
+bool varlen_btile_ok(uint32_t tile_T, uint32_t bt_slots, uint32_t cap, uint32_t H, uint32_t vhc,
+                     uint64_t packet_tiles, uint64_t spans);
 int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream);
 int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream);
 int launch_validate_utf8(const Utf8Args& args, hipStream_t stream);
@@ -328,7 +338,7 @@ struct ScanCheck {
 void scan_block_sums(const uint32_t* d_len, uint64_t n, uint32_t H, uint32_t items, uint64_t* sums,
                      const ScanCheck& chk, hipStream_t stream);
 void scan_block_bases(uint64_t* sums, uint64_t nb, uint64_t* d_frame_off, uint64_t n, uint32_t H,
-                      const ScanCheck& chk, hipStream_t stream);
+                      const ScanCheck& chk, hipStream_t stream, uint32_t* zero = nullptr);
 // Small-frame varlen encode of packed payloads (varlen.hip): the scan's first
 // two passes, then one kernel per tile of kBlock * fpt packets that writes the
 // tile's offsets and assembles its frames in LDS.
@@ -337,10 +347,14 @@ int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int
 // p, the first packet whose packed payload starts at or after k * bytes, and
 // fo = frame_off[p], so a tile has its packet range and frame run from two
 // adjacent records in one round trip.
+// With over set, the scan also counts into *over the tiles of tile_T packets
+// whose payload run (16-B aligned) exceeds tile_cap.
 struct SpanStarts {
   SpanRec* rec;  // [count + 1], or null
   uint64_t bytes;
   uint64_t count;
+  uint32_t* over;
+  uint32_t tile_T, tile_cap;
 };
 int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
                              const ScanCheck& chk, hipStream_t stream, const SpanStarts& spans = SpanStarts{});

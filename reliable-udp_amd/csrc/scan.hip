@@ -70,10 +70,11 @@ __global__ void __launch_bounds__(kBlock) scan_block_sums_kernel(const uint32_t*
 // with a ScanCheck, the call's status word.
 __global__ void __launch_bounds__(1024) scan_block_bases_kernel(uint64_t* sums, uint64_t nb,
                                                                uint64_t* frame_off, uint64_t n,
-                                                               uint32_t H, ScanCheck chk) {
+                                                               uint32_t H, ScanCheck chk, uint32_t* zero) {
   __shared__ uint64_t s_wave[1024 / 64];
   __shared__ uint32_t s_bits;
   if (threadIdx.x == 0) s_bits = 0;
+  if (zero && threadIdx.x == 0) *zero = 0;  // (pass 3's counter)
   const uint64_t per = (nb + 1023) / 1024;
   const uint64_t lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
   uint64_t mine = 0;
@@ -106,6 +107,8 @@ __global__ void __launch_bounds__(1024) scan_block_bases_kernel(uint64_t* sums, 
 // With spans.rec: the packed payload splits into spans of S bytes, and
 // spans.rec[k] = {frame_off[p], p} for p the first packet whose payload starts
 // at or after k*S (n for spans after the last packet's start), k = 0 .. spans.count.
+// With spans.over: the tiles of spans.tile_T packets (which divides the
+// block's packets) whose run exceeds spans.tile_cap are counted into *over.
 __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len, uint64_t n, uint32_t H,
                                                             const uint64_t* bases, uint64_t* frame_off,
                                                             SpanStarts spans) {
@@ -139,6 +142,16 @@ __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len,
   }
   if (spans.rec) {
     const uint64_t S = spans.bytes, K = spans.count;
+    // x / S through the double reciprocal, corrected to the exact quotient
+    // (x < 2^53: the estimate is off by at most one); a u64 division per
+    // packet cost 10 us on 1M packets
+    const double inv = 1.0 / (double)S;
+    auto div_s = [&](uint64_t x) {
+      uint64_t d = (uint64_t)((double)x * inv);
+      if (d * S > x) --d;
+      if ((d + 1u) * S <= x) ++d;
+      return d;
+    };
 #pragma unroll
     for (uint32_t j = 0; j < kScanItems; ++j) {
       const uint32_t k = j * kBlock + threadIdx.x;
@@ -148,15 +161,33 @@ __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len,
       uint64_t lo = 0;
       if (p > 0) {
         const uint64_t prev_len = k > 0 ? s_len[k - 1] - H : len[p - 1];
-        lo = (po - prev_len) / S + 1;  // spans after the one the previous packet starts in
+        lo = div_s(po - prev_len) + 1;  // spans after the one the previous packet starts in
       }
-      uint64_t hi = po / S;
-      if (hi > K) hi = K;
+      const uint64_t qpo = div_s(po);
+      const uint64_t hi = qpo < K ? qpo : K;
       for (uint64_t t = lo; t <= hi; ++t) spans.rec[t] = SpanRec{s_off[k], (uint32_t)p, 0u};
       if (p == n - 1)
-        for (uint64_t t = (po / S + 1 > lo ? po / S + 1 : lo); t <= K; ++t)
+        for (uint64_t t = (qpo + 1 > lo ? qpo + 1 : lo); t <= K; ++t)
           spans.rec[t] = SpanRec{s_off[k] + s_len[k], (uint32_t)n, 0u};
     }
+  }
+  if (spans.over) {
+    // tile k of this block: packets [k T, k T + T) (capped at n); its run
+    // from the 16-B aligned payload offsets at both ends
+    const uint32_t T = spans.tile_T, tiles = kScanBlockItems / T;
+    uint32_t c = 0;
+    for (uint32_t t0 = 0; t0 < tiles; t0 += kBlock) {  // (uniform rounds)
+      bool over = false;
+      const uint64_t k0 = (uint64_t)(t0 + threadIdx.x) * T;
+      if (t0 + threadIdx.x < tiles && base + k0 < n) {
+        const uint64_t k1 = base + k0 + T < n ? k0 + T : n - base;
+        const uint64_t f1 = k1 < kScanBlockItems ? s_off[k1] : s_off[k1 - 1] + s_len[k1 - 1];
+        const uint64_t pa = s_off[k0] - (base + k0) * H, pb = f1 - (base + k1) * H;
+        over = ((pb + 15u) & ~15ull) - (pa & ~15ull) > spans.tile_cap;
+      }
+      c += (uint32_t)__syncthreads_count(over);
+    }
+    if (threadIdx.x == 0 && c) atomicAdd(spans.over, c);
   }
 }
 
@@ -173,8 +204,9 @@ void scan_block_sums(const uint32_t* d_len, uint64_t n, uint32_t H, uint32_t ite
 }
 
 void scan_block_bases(uint64_t* sums, uint64_t nb, uint64_t* d_frame_off, uint64_t n, uint32_t H,
-                      const ScanCheck& chk, hipStream_t stream) {
-  hipLaunchKernelGGL(scan_block_bases_kernel, dim3(1), dim3(1024), 0, stream, sums, nb, d_frame_off, n, H, chk);
+                      const ScanCheck& chk, hipStream_t stream, uint32_t* zero) {
+  hipLaunchKernelGGL(scan_block_bases_kernel, dim3(1), dim3(1024), 0, stream, sums, nb, d_frame_off, n, H, chk,
+                     zero);
 }
 
 int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
@@ -184,7 +216,7 @@ int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint
   hipError_t e = stream_alloc(reinterpret_cast<void**>(&sums), nb * sizeof(uint64_t), stream);
   if (e != hipSuccess) return (int)e;
   scan_block_sums(d_len, n, H, kScanItems, sums, chk, stream);
-  scan_block_bases(sums, nb, d_frame_off, n, H, chk, stream);
+  scan_block_bases(sums, nb, d_frame_off, n, H, chk, stream, spans.over);
   hipLaunchKernelGGL(scan_apply_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, stream, d_len, n, H, sums,
                      d_frame_off, spans);
   e = hipGetLastError();

@@ -261,8 +261,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // packets per thread; 48: fixed-length encode packets per launch (0 = one launch);
 // 49: XCD-contiguous tile order in the decode / varlen / UTF-8 tile kernels;
 // 50: small-frame encode finds its tile bases itself (no pass-2 launch);
-// 51: varlen encode tiles by payload bytes; 52: varlen tile sum pass (2 from 64-B block sums, 0 G lanes per
-// packet; byte tiles always 2).
+// 51: varlen byte tiles (0 never, 1 when the scan counts overflowing packet tiles, 2 always);
+// 52: varlen tile sum pass (2 from 128-B block sums, 0 chunk by chunk).
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();

@@ -326,63 +326,78 @@ __device__ __forceinline__ void varlen_tile_chunk_map(const uint32_t* fo, uint8_
 //            with the neighbour tiles are written bytewise.
 // A tile whose run exceeds tile_cap (lengths far above the caller's hint)
 // encodes its packets with the per-packet vector path instead.
+// Byte tiles (a.span_rec set and the scan's count of overflowing packet tiles
+// at least bt_min_over, read per launch): workgroup k frames the packets whose
+// payload starts in span k instead, their lanes per packet from their count,
+// the map by ranges of output chunks.  The grid covers both forms.
 // W: minimum waves per SIMD the register allocation must allow (1 = none).
-// BT: byte tiles (a.span_rec set; their own sum passes and map), its own
-// instantiation so the packet-count form keeps its register budget.
-template <int H, int W, bool BT>
+template <int H, int W>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))) encode_varlen_tile_kernel(VarlenArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
-  const uint32_t T = a.tile_T, cap = a.tile_cap;
+  const uint32_t Tl = a.tile_Tl, cap = a.tile_cap;
   uint64_t* lds_hdr = reinterpret_cast<uint64_t*>(lds);
-  uint32_t* lds_fo = reinterpret_cast<uint32_t*>(lds + 8u * T);
+  uint32_t* lds_fo = reinterpret_cast<uint32_t*>(lds + 8u * Tl);
   const bool wide = a.vhc == 2u;  // coded chunk map (u16 entries)
   const bool blk_sums = a.tile_sums == 2u;  // the block-sum pass
-  uint8_t* lds_map = reinterpret_cast<uint8_t*>(lds_fo + T + 1u);
+  uint8_t* lds_map = reinterpret_cast<uint8_t*>(lds_fo + Tl + 1u);
   uint16_t* lds_map16 = reinterpret_cast<uint16_t*>(lds_map);
   uint32_t* lds_blk = reinterpret_cast<uint32_t*>(lds_map);  // (until the map is built)
-  unsigned char* lds_pay = lds + vt_pay_off(T, cap, H, wide ? 1u : 0u);
+  unsigned char* lds_pay = lds + vt_pay_off(Tl, cap, H, wide ? 1u : 0u);
 
   const uint32_t tid = threadIdx.x;
   const uint64_t tile = a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
-  // Byte tiles (span_rec set): the packets whose payload starts in
-  // span `tile` (clamped, so a rejected batch's unwritten records stay in
-  // range), their frame run from the same two records; else T packets.
-  uint64_t p0, fo0, fo_end = 0;
-  uint32_t Tv, Tall;
-  if (BT) {
-    const SpanRec r0 = a.span_rec[tile], r1 = a.span_rec[tile + 1];
+  // Both forms' loads go out together (one round trip): the form, the span
+  // records, the packet tile's offsets.
+  const uint64_t ptiles = (a.n + a.tile_T - 1u) / a.tile_T;
+  const uint64_t pp0 = (tile < ptiles ? tile : ptiles - 1u) * a.tile_T;
+  const uint32_t pTv = a.n - pp0 < a.tile_T ? (uint32_t)(a.n - pp0) : a.tile_T;
+  const uint64_t pfo0 = a.frame_off[pp0], pfo_end = a.frame_off[pp0 + pTv];
+  bool bt = false;
+  SpanRec r0{}, r1{};
+  if (a.span_rec) {
+    bt = *a.tile_over >= a.bt_min_over;
+    if (tile < a.span_count) {
+      r0 = a.span_rec[tile];
+      r1 = a.span_rec[tile + 1];
+    }
+  }
+  uint64_t p0, fo0, fo_end;
+  uint32_t Tv, Tall, T, glog;
+  if (bt) {
+    // the packets whose payload starts in span `tile` (clamped, so a rejected
+    // batch's unwritten records stay in range), their frame run from the same
+    // two records
+    if (tile >= a.span_count) return;
     p0 = r0.p < a.n ? r0.p : a.n;
     const uint64_t p1 = r1.p < a.n ? (r1.p > p0 ? r1.p : p0) : a.n;
     Tall = (uint32_t)(p1 - p0);
     if (Tall == 0) return;
+    T = a.bt_slots;
     Tv = Tall < T ? Tall : T;
     fo0 = r0.fo;
     fo_end = r1.fo;  // frame_off[p0 + Tv] when Tall <= T (else the per-packet path)
-  } else {
-    p0 = tile * T;
-    const uint64_t left = a.n - p0;
-    Tv = Tall = left < T ? (uint32_t)left : T;
-    fo0 = a.frame_off[p0];
-    fo_end = a.frame_off[p0 + Tv];
-  }
-  // G = 2^glog lanes per packet: the launcher's for packet tiles; for a byte
-  // tile as many as its packet count leaves (all four waves busy)
-  uint32_t glog = a.tile_glog;
-  if (BT) {
+    // lanes per packet: as many as the tile's packet count leaves
     glog = 0;
     while (glog < 6u && (Tv << (glog + 1u)) <= kBlock) ++glog;
+  } else {
+    if (tile >= ptiles) return;
+    p0 = pp0;
+    T = a.tile_T;
+    Tv = Tall = pTv;
+    fo0 = pfo0;
+    fo_end = pfo_end;
+    glog = a.tile_glog;
   }
   const uint32_t G = 1u << glog, q = tid >> glog, g = tid & (G - 1u);
-  // Header-table loads first (small tiles): their latency overlaps the
-  // offset loads and phase 1 instead of following the barrier.
+  // Header-table loads before phase 1: their latency overlaps its stream
+  // instead of following the barrier.
   uint32_t t_seq = 0, t_ack = 0, t_flags = 0;
   if (a.early_table && g == 0 && q < Tv) {
     t_seq = a.seq_in[p0 + q];
     t_ack = a.ack_in[p0 + q];
     t_flags = a.flags_in[p0 + q];
   }
-  if (call_failed(a.status)) return;  // issued with the offset loads: one round trip for both
-  const bool early_tab = a.early_table;
+  if (call_failed(a.status)) return;
   const uint64_t po0 = fo0 - p0 * (uint64_t)H;
   const uint64_t po_end = fo_end - (p0 + Tv) * (uint64_t)H;
   const uint64_t A = po0 & ~15ull;
@@ -393,6 +408,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
       encode_varlen_packet<H>(a, p0 + q0 + q, q0 + q < Tall, g, glog);
     return;
   }
+  const bool early_tab = a.early_table;
 
   // ---- phase 1: payload run -> LDS, frame offsets ------------------------
   {
@@ -483,7 +499,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     }
   }
   if (blk_sums) __syncthreads();  // the map overwrites the block sums
-  if (BT) {
+  if (bt) {
     // Byte tiles: lanes take contiguous ranges of output chunks for the map,
     // not packets, so a tile of ragged lengths keeps every lane equally busy.
     varlen_tile_chunk_map<H>(lds_fo, lds_map, lds_map16, wide, Tv, lead, nbytes);
@@ -1615,39 +1631,60 @@ int launch_decode_small(const VarlenArgs& args, hipStream_t stream) {
   }
 }
 
-template <int H, int W, bool BT = false>
+// Dynamic LDS of one varlen encode tile whose arrays hold Tl packets.
+static size_t varlen_tile_lds(uint32_t Tl, uint32_t cap, uint32_t H, uint32_t vhc) {
+  size_t b = vt_pay_off(Tl, cap, H, vhc == 2u ? 1u : 0u) + 2u * kVTGuard + cap;
+  if (vhc) b = ((b + 15u) & ~size_t(15)) + 32u * Tl;
+  return b;
+}
+
+// Byte tiles of bt_slots packets as an alternative to packet tiles of tile_T:
+// only for packet tiles of 16 or fewer (hints from 1 KiB: below, ragged
+// lengths rarely overflow and byte tiles lost, lengths uniform in [0, 512]
+// 0.204 -> 0.248 ms), where their arrays leave the tiles per CU unchanged
+// (1M x 512 B: 64 slots would take 7 packet tiles per CU to 6, 8% slower) and
+// their grid is at most 5% larger (the surplus workgroups of the form not
+// taken still occupy LDS for a round trip: 4000-B hints, 50% slower).
+bool varlen_btile_ok(uint32_t tile_T, uint32_t bt_slots, uint32_t cap, uint32_t H, uint32_t vhc,
+                     uint64_t packet_tiles, uint64_t spans) {
+  constexpr size_t kLdsPerCu = 160u * 1024u;
+  if (tile_T > 16u) return false;
+  const uint32_t Tl = bt_slots > tile_T ? bt_slots : tile_T;
+  if (kLdsPerCu / varlen_tile_lds(Tl, cap, H, vhc) < kLdsPerCu / varlen_tile_lds(tile_T, cap, H, vhc)) return false;
+  return spans * 20u <= packet_tiles * 21u;
+}
+
+template <int H, int W>
 int launch_varlen_tile_w(const VarlenArgs& args, size_t lds, uint64_t blocks, hipStream_t stream) {
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_varlen_tile_kernel<H, W, BT>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_varlen_tile_kernel<H, W>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL((encode_varlen_tile_kernel<H, W, BT>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream,
-                     args);
+  hipLaunchKernelGGL((encode_varlen_tile_kernel<H, W>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
   return (int)hipGetLastError();
 }
 
 template <int H>
 int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
   VarlenArgs args = in;
-  const uint64_t blocks = args.span_rec ? args.span_count : (args.n + args.tile_T - 1) / args.tile_T;
-  const auto tile_lds = [&](uint32_t wide) {
-    size_t b = vt_pay_off(args.tile_T, args.tile_cap, H, wide) + 2u * kVTGuard + args.tile_cap;
-    if (args.vhc) b = ((b + 15u) & ~size_t(15)) + 32u * args.tile_T;
-    return b;
-  };
+  uint64_t blocks = (args.n + args.tile_T - 1) / args.tile_T;
+  if (args.span_rec && args.span_count > blocks) blocks = args.span_count;
+  const uint32_t Tl = args.span_rec && args.bt_slots > args.tile_T ? args.bt_slots : args.tile_T;
+  args.tile_Tl = Tl;
   // The coded map costs 1 B more per output chunk.  Where that would leave
   // fewer than 4 tiles per CU (1M x 1024 B: 4 -> 3, 9% slower) the u8 map is
   // used instead (profiles/r01/sweeps/varlen_coded_map.json).
   constexpr size_t kLdsPerCu = 160u * 1024u;
-  if (args.vhc == 2u && kLdsPerCu / tile_lds(1) < 4u && kLdsPerCu / tile_lds(0) >= 4u) args.vhc = 1u;
-  size_t lds = vt_pay_off(args.tile_T, args.tile_cap, H, args.vhc == 2u ? 1u : 0u) + 2u * kVTGuard + args.tile_cap;
-  if (args.vhc) {  // prebuilt header chunks [T][2] x 16 B after the payload run
+  if (args.vhc == 2u && kLdsPerCu / varlen_tile_lds(Tl, args.tile_cap, H, 2u) < 4u &&
+      kLdsPerCu / varlen_tile_lds(Tl, args.tile_cap, H, 1u) >= 4u)
+    args.vhc = 1u;
+  size_t lds = vt_pay_off(Tl, args.tile_cap, H, args.vhc == 2u ? 1u : 0u) + 2u * kVTGuard + args.tile_cap;
+  if (args.vhc) {  // prebuilt header chunks [Tl][2] x 16 B after the payload run
     lds = (lds + 15u) & ~size_t(15);
     args.hc_off = (uint32_t)lds;
-    lds += 32u * args.tile_T;
+    lds += 32u * Tl;
   }
-  lds += (size_t)tuning().varlen_lds_pad;  // (sweeps: LDS occupancy probe)
   // Register budget to match the LDS occupancy: the kernel needs 88 VGPRs (5
   // waves per SIMD) unconstrained, so tiles small enough for 6-7 per CU ask
   // the allocator for that many waves (a few spills in the per-packet
@@ -1660,8 +1697,6 @@ int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
     const size_t per_cu = kLdsPerCu / lds;
     w = per_cu >= 7 ? 7 : per_cu == 6 ? 6 : 1;
   }
-  if (args.span_rec)  // byte tiles: register budget for the LDS occupancy (5 tiles per CU at MTU hints)
-    return launch_varlen_tile_w<H, 5, true>(args, lds, blocks, stream);
   return w == 6 ? launch_varlen_tile_w<H, 6>(args, lds, blocks, stream)
        : w == 7 ? launch_varlen_tile_w<H, 7>(args, lds, blocks, stream)
        : w == 8 ? launch_varlen_tile_w<H, 8>(args, lds, blocks, stream)

@@ -814,7 +814,8 @@ def test_small_frame_tiles_vs_oracle(cuda, fpt):
 
 @pytest.mark.parametrize("dist", ["ragged", "equal", "bursty", "tiny_runs", "zeros"])
 def test_byte_tiled_varlen_encode_vs_oracle(cuda, dist):
-    """Varlen encode tile forms (key 51 byte tiles; 52 each sum pass) == the oracle, checksums included, for
+    """Varlen encode tile forms (key 51 packet / byte tiles / the device's choice;
+    52 each sum pass) == the oracle, checksums included, for
     ragged / equal lengths, bursts past the budget's slack, long runs of tiny
     packets (more than a tile's slots) and zero-length packets."""
     import ctypes
@@ -844,8 +845,8 @@ def test_byte_tiled_varlen_encode_vs_oracle(cuda, dist):
     tab = (dev(seq, cuda), dev(ack, cuda), dev(flags, cuda))
     for layout in (5, 7):
         want, off, cs = codec_np.encode_varlen(seq, ack, flags, pays, layout)
-        # (byte tiles, sum pass: 2 block sums / 0 per-packet lanes, XCD order)
-        for knobs in ((1, 2, 1), (1, 2, 0), (0, 0, 1), (0, 2, 1), (0, 2, 0)):
+        # (tile form: 1 auto / 2 byte tiles / 0 packet tiles, sum pass: 2 block sums / 0 chunks, XCD order)
+        for knobs in ((1, 2, 1), (2, 2, 1), (2, 2, 0), (2, 0, 1), (0, 2, 1), (0, 0, 1), (0, 2, 0)):
             old = [lib.rudpx_tune(key, v) for key, v in zip((51, 52, 49), knobs)]
             try:
                 r = batch.pack_batch_varlen(tab, dev(pay, cuda), dev(lens, cuda), layout, want_csum=True,

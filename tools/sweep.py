@@ -491,12 +491,12 @@ def ragged_sweep(reps):
                                                          H, 0, stream))
         specs = {"default": (), "no_sums": ((35, 2),), "skip_overflow": ((35, 4),),
                  "no_sums_skip_overflow": ((35, 6),), "cap125": ((39, 125),), "cap150": ((39, 150),),
-                 "cap200": ((39, 200),), "no_hchunk": ((36, 0),), "btile": ((51, 1),),
-                 "btile_no_sums": ((51, 1), (35, 2)), "chunksums": ((52, 0),), "btile_chunksums": ((51, 1), (52, 0))}
+                 "cap200": ((39, 200),), "no_hchunk": ((36, 0),), "btile": ((51, 2),),
+                 "btile_no_sums": ((51, 2), (35, 2)), "chunksums": ((52, 0),), "packet": ((51, 0),)}
         variants = {}
         for name, kv in specs.items():
             def setup(kv=kv):
-                for k, v in ((35, 0), (39, 110), (36, 2), (51, 0), (52, 2), (53, 0)):
+                for k, v in ((35, 0), (39, 110), (36, 2), (51, 1), (52, 2)):
                     lib.rudpx_tune(k, v)
                 for k, v in kv:
                     lib.rudpx_tune(k, v)
@@ -512,7 +512,7 @@ def ragged_sweep(reps):
             if ref is None:
                 ref = (frames.clone(), off.clone())
             exact[name] = bool(torch.equal(frames, ref[0]) and torch.equal(off, ref[1]) and int(st.item()) == 0)
-        for k, v in ((35, 0), (39, 110), (36, 2), (51, 0), (52, 2), (53, 0)):
+        for k, v in ((35, 0), (39, 110), (36, 2), (51, 1), (52, 2)):
             lib.rudpx_tune(k, v)
         # tiles of 16 packets whose payload run exceeds 1.1x the hinted run (+ alignment slack)
         runs = lens[: (n // 16) * 16].view(-1, 16).sum(1)
