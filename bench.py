@@ -393,6 +393,28 @@ def legs(torch, batch, device, steps):
         "note": "Python entry, sync-free (offset scan and device-side checks included); medians of "
                 "7 interleaved rounds beside the eager-check and raw C-ABI forms"}
     del tabm, paym, lensm, flatm, encm
+    # ragged MTU-range lengths: uniform in [0, 2944] (mean 1472), packed; the tile
+    # kernel takes byte tiles for this batch (the scan counts its overflowing
+    # packet tiles), against the equal-length 1472-B leg above
+    g = torch.Generator(device=device).manual_seed(SEEDS[1472])
+    lensr = torch.randint(0, 2945, (n1,), dtype=torch.int32, device=device, generator=g)
+    totr = int(lensr.sum().item())
+    tabr, _ = batch.synth_batch(n1, 0, SEEDS[1472], device=device)
+    flatr = torch.randint(0, 256, (totr,), dtype=torch.uint8, device=device, generator=g)
+    encr = batch.pack_batch_varlen(tabr, flatr, lensr, "rudp7")
+    tr = varlen_pair(tabr, flatr, lensr, "rudp7", encr.frames, encr.frame_off, None)
+    ms_er, ms_dr = tr["encode"], tr["decode"]
+    out["varlen_1M_ragged_0_2944"] = {
+        "payload_bytes": totr,
+        "encode_GiB_s": totr / (ms_er / 1e3) / GIB, "encode_ms": ms_er,
+        "encode_roofline_frac": (2 * totr + n1 * (9 + 7 + 8)) / (ms_er / 1e3) / 1e9 / HBM_PEAK_GBS,
+        "encode_vs_equal_lengths": ms_er / ms_em * (n1 * 1472) / totr,
+        "decode_GiB_s": totr / (ms_dr / 1e3) / GIB, "decode_ms": ms_dr,
+        "decode_roofline_frac": (totr + n1 * (7 + 8 + 8)) / (ms_dr / 1e3) / 1e9 / HBM_PEAK_GBS,
+        "ms_by_form": tr,
+        "note": "lengths uniform in [0, 2944]; encode_vs_equal_lengths = time per payload byte over "
+                "the equal 1472-B leg's"}
+    del tabr, flatr, lensr, encr
     # the proxy's retransmission check (proxy.py:90, 500-deep history) over the same 1M datagrams
     ms_x = time_loop(torch, lambda i: batch.detect_retransmissions(enc.frames, frame_off=enc.frame_off,
                                                                    window=500), steps, 3) / steps

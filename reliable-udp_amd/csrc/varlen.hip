@@ -345,29 +345,34 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   unsigned char* lds_pay = lds + vt_pay_off(Tl, cap, H, wide ? 1u : 0u);
 
   const uint32_t tid = threadIdx.x;
-  const uint64_t tile = a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
   // Both forms' loads go out together (one round trip): the form, the span
-  // records, the packet tile's offsets.
-  const uint64_t ptiles = (a.n + a.tile_T - 1u) / a.tile_T;
-  const uint64_t pp0 = (tile < ptiles ? tile : ptiles - 1u) * a.tile_T;
+  // records, the packet tile's offsets.  Each form numbers its own tiles
+  // (XCD-contiguous over its own count) and leaves the surplus workgroups,
+  // the highest, idle: spread over the XCDs.
+  const uint32_t b = blockIdx.x;
+  const uint32_t ptiles = (uint32_t)((a.n + a.tile_T - 1u) / a.tile_T);
+  const uint32_t tile_p = b < ptiles ? (a.xcd ? xcd_tile(b, ptiles) : b) : ptiles - 1u;
+  const uint64_t pp0 = (uint64_t)tile_p * a.tile_T;
   const uint32_t pTv = a.n - pp0 < a.tile_T ? (uint32_t)(a.n - pp0) : a.tile_T;
   const uint64_t pfo0 = a.frame_off[pp0], pfo_end = a.frame_off[pp0 + pTv];
   bool bt = false;
   SpanRec r0{}, r1{};
+  const uint32_t spans = (uint32_t)a.span_count;
+  const uint32_t tile_s = b < spans ? (a.xcd ? xcd_tile(b, spans) : b) : 0u;
   if (a.span_rec) {
     bt = *a.tile_over >= a.bt_min_over;
-    if (tile < a.span_count) {
-      r0 = a.span_rec[tile];
-      r1 = a.span_rec[tile + 1];
+    if (b < spans) {
+      r0 = a.span_rec[tile_s];
+      r1 = a.span_rec[tile_s + 1];
     }
   }
   uint64_t p0, fo0, fo_end;
   uint32_t Tv, Tall, T, glog;
   if (bt) {
-    // the packets whose payload starts in span `tile` (clamped, so a rejected
+    // the packets whose payload starts in span tile_s (clamped, so a rejected
     // batch's unwritten records stay in range), their frame run from the same
     // two records
-    if (tile >= a.span_count) return;
+    if (b >= spans) return;
     p0 = r0.p < a.n ? r0.p : a.n;
     const uint64_t p1 = r1.p < a.n ? (r1.p > p0 ? r1.p : p0) : a.n;
     Tall = (uint32_t)(p1 - p0);
@@ -380,7 +385,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     glog = 0;
     while (glog < 6u && (Tv << (glog + 1u)) <= kBlock) ++glog;
   } else {
-    if (tile >= ptiles) return;
+    if (b >= ptiles) return;
     p0 = pp0;
     T = a.tile_T;
     Tv = Tall = pTv;
