@@ -262,50 +262,6 @@ __device__ __forceinline__ uint32_t octet_sum(uint32_t x) {
   return x;
 }
 
-// Byte tiles, the chunk -> frame map: lane t takes a contiguous range of the
-// output units (unit k's first byte at tile offset lead + 16k) and walks the
-// frames across it; same entries as the per-packet form.
-template <int H>
-__device__ __forceinline__ void varlen_tile_chunk_map(const uint32_t* fo, uint8_t* map, uint16_t* map16, bool wide,
-                                                      uint32_t Tv, uint32_t lead, uint32_t nbytes) {
-  const uint32_t units = nbytes > lead ? (nbytes - lead + 15u) >> 4 : 0u;
-  const uint32_t per = (units + kBlock - 1u) / kBlock;
-  const uint32_t k0 = threadIdx.x * per;
-  if (k0 >= units) return;
-  const uint32_t k1 = k0 + per < units ? k0 + per : units;
-  const uint32_t x0 = lead + 16u * k0;
-  uint32_t lo = 0, hi = Tv - 1u;  // the frame holding byte x0 (frames are >= H bytes)
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi + 1u) >> 1;
-    if (fo[mid] <= x0) lo = mid;
-    else hi = mid - 1u;
-  }
-  uint32_t r = lo, fs = fo[r], fe = fo[r + 1u];
-  for (uint32_t k = k0; k < k1; ++k) {
-    const uint32_t x = lead + 16u * k;
-    while (fe <= x && r + 1u < Tv) {
-      ++r;
-      fs = fe;
-      fe = fo[r + 1u];
-    }
-    if (wide) {
-      const int kk = (int)x - (int)fs;
-      uint32_t e = r;
-      if (kk >= H && x + 16u <= fe) {
-        e |= 0x8000u;
-      } else {
-        const uint32_t nxt = kk >= H ? 1u : 0u;
-        const uint32_t fsp = nxt ? fe : fs;
-        const int i0 = fsp >= lead ? (int)((fsp - lead) >> 4) : -1;
-        e |= (nxt << 8) | ((uint32_t)((int)k - i0) & 1u) << 9;
-      }
-      map16[k] = (uint16_t)e;
-    } else {
-      map[k] = (uint8_t)r;
-    }
-  }
-}
-
 // Varlen encode of a PACKED payload buffer (payload_off == null) through an
 // LDS tile: the same shape as the fixed-length encode_tile_kernel (encode.hip)
 // with per-frame bounds from frame_off.  A workgroup owns packets
@@ -328,8 +284,8 @@ __device__ __forceinline__ void varlen_tile_chunk_map(const uint32_t* fo, uint8_
 // encodes its packets with the per-packet vector path instead.
 // Byte tiles (a.span_rec set and the scan's count of overflowing packet tiles
 // at least bt_min_over, read per launch): workgroup k frames the packets whose
-// payload starts in span k instead, their lanes per packet from their count,
-// the map by ranges of output chunks.  The grid covers both forms.
+// payload starts in span k instead, their lanes per packet from their count.
+// The grid covers both forms.
 // W: minimum waves per SIMD the register allocation must allow (1 = none).
 template <int H, int W>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))) encode_varlen_tile_kernel(VarlenArgs a) {
@@ -504,11 +460,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     }
   }
   if (blk_sums) __syncthreads();  // the map overwrites the block sums
-  if (bt) {
-    // Byte tiles: lanes take contiguous ranges of output chunks for the map,
-    // not packets, so a tile of ragged lengths keeps every lane equally busy.
-    varlen_tile_chunk_map<H>(lds_fo, lds_map, lds_map16, wide, Tv, lead, nbytes);
-  } else if (q < Tv) {
+  if (q < Tv) {
     const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
     // map[k] = q for the output units k whose first byte lead + 16k lies in [fs, fe)
     const uint32_t klo = fs > lead ? (fs - lead + 15u) >> 4 : 0u;

@@ -812,12 +812,13 @@ def test_small_frame_tiles_vs_oracle(cuda, fpt):
             assert np.array_equal(results[0], results[1]) and np.array_equal(results[0], results[2])
 
 
-@pytest.mark.parametrize("dist", ["ragged", "equal", "bursty", "tiny_runs", "zeros"])
-def test_byte_tiled_varlen_encode_vs_oracle(cuda, dist):
+@pytest.mark.parametrize("dist", ["ragged", "equal", "bursty", "tiny_runs", "zeros", "jumbo"])
+def test_varlen_tile_forms_vs_oracle(cuda, dist):
     """Varlen encode tile forms (key 51 packet / byte tiles / the device's choice;
     52 each sum pass) == the oracle, checksums included, for
     ragged / equal lengths, bursts past the budget's slack, long runs of tiny
-    packets (more than a tile's slots) and zero-length packets."""
+    packets (more than a tile's slots), zero-length packets and packets longer
+    than a whole tile's LDS budget."""
     import ctypes
     from rudp import _native
     lib = _native.lib()
@@ -835,9 +836,12 @@ def test_byte_tiled_varlen_encode_vs_oracle(cuda, dist):
         lens = rng.integers(1200, 1700, n)
         for s0 in rng.choice(n - 400, 10, replace=False):
             lens[s0:s0 + 300] = rng.integers(0, 3, 300)
-    else:
+    elif dist == "zeros":
         lens = rng.integers(0, 2945, n)
         lens[rng.random(n) < 0.3] = 0
+    else:  # jumbo: a few packets over a whole tile's budget (~27 KB at a 1.5-KB hint)
+        lens = rng.integers(1000, 2000, n)
+        lens[rng.choice(n, 12, replace=False)] = rng.integers(30000, 60000, 12)
     lens = lens.astype(np.int32)
     pay = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
     seq, ack, flags, _ = synth.synth(0xB7 + n, 0, n, 0)
