@@ -385,15 +385,17 @@ def small_sweep(reps):
     """Small frames (the reference's one-character datagrams and a few other
     tiny shapes): varlen encode and decode-verify through the sync-free C ABI
     (preallocated outputs), with the small-frame tile kernels at 1/2/4/8
-    packets per thread (keys 46/47) against the per-packet vector kernels.
+    packets per thread (keys 46/47), two or three launches (key 50), against
+    the per-packet vector kernels.
     Every variant is checked bit-exact against the vector kernels."""
     import ctypes
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream().cuda_stream
     out = {}
-    specs = {"vec": ((46, 0),), "fpt1": ((46, 16), (47, 1)), "fpt2": ((46, 16), (47, 2)),
-             "fpt4": ((46, 16), (47, 4)), "fpt8": ((46, 16), (47, 8))}
-    old = {k: lib.rudpx_tune(k, 0) for k in (46, 47)}
+    specs = {"vec": ((46, 0), (50, 1)), "fpt1": ((46, 16), (47, 1), (50, 1)), "fpt2": ((46, 16), (47, 2), (50, 1)),
+             "fpt4": ((46, 16), (47, 4), (50, 1)), "fpt8": ((46, 16), (47, 8), (50, 1)),
+             "auto": ((46, 16), (47, 0), (50, 1)), "auto_3launch": ((46, 16), (47, 0), (50, 0))}
+    old = {k: lib.rudpx_tune(k, 0) for k in (46, 47, 50)}
     for k, v in old.items():
         lib.rudpx_tune(k, v)
     for shape in ("L1", "L4", "U1-4", "L9", "L15"):
@@ -453,7 +455,7 @@ def small_sweep(reps):
         alg_d = n * (mean_f + 8 + 8)                      # frames, offsets in; seq/ack/flags/ok/csum out
         for k, ms in res.items():
             alg = alg_e if "_enc_" in k else alg_d
-            out[k] = {"ms": ms, "frac": alg / ms / 1e9 / 8.0, "exact": exact[k.rsplit("_", 1)[1]]}
+            out[k] = {"ms": ms, "frac": alg / ms / 1e9 / 8.0, "exact": exact[k.split("_", 2)[2]]}
         del tab, flat, lens, frames, off
         torch.cuda.empty_cache()
     return out
