@@ -419,13 +419,13 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
             raise ValueError(f"{name} has {t.shape[0]} entries for {n} packets")
     if payload_off is not None:
         _int_tensor(payload_off, "payload_off", dev, n, dtypes=(torch.int64,))
+    frames = None
     if out is not None:
         _dev_check(out, "out", torch.uint8, 1, dev)
         frames = out
         lsum = max(out.numel() - n * H, 0)  # at most; only the lanes hint reads it
     elif payload_off is None:
         lsum = payload.numel()  # exact for a valid packed batch; the device checks it
-        frames = torch.empty((lsum + n * H,), dtype=torch.uint8, device=dev)
     else:
         # gathered payloads: the frame bytes are unknown until the lengths are summed
         # (rudp_varlen_bounds, one 40-byte device read); lengths are read as u32
@@ -439,13 +439,21 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
             raise ValueError("lengths must lie in [0, 65535]")
         if omin < 0 or oend > payload.numel():
             raise ValueError("payload_off + lengths must stay inside payload")
-        frames = torch.empty((lsum + n * H,), dtype=torch.uint8, device=dev)
     if want_csum is None:
         want_csum = H == 5
-    aux = torch.empty((n + 2,), dtype=torch.int64, device=dev)  # frame_off [n + 1] | status
-    frame_off = aux[:n + 1]
-    status = aux[n + 1:].view(torch.int32)[:1]
-    csum = torch.empty((n,), dtype=torch.uint16, device=dev) if want_csum else None
+    # one allocation: frame_off (i64 [n + 1]) | status (i32) | pad | csum (u16 [n]) |
+    # pad to 16 B | frames (unless the caller's), split by one call
+    cs_bytes = 2 * n if want_csum else 0
+    head = 8 * (n + 1) + 8 + cs_bytes
+    pad = -head % 16
+    f_bytes = 0 if frames is not None else lsum + n * H
+    frame_off, status, _, csum, _, fr = torch.empty(
+        (head + pad + f_bytes,), dtype=torch.uint8, device=dev).split_with_sizes(
+        (8 * (n + 1), 4, 4, cs_bytes, pad, f_bytes))
+    frame_off, status = frame_off.view(torch.int64), status.view(torch.int32)
+    csum = csum.view(torch.uint16) if want_csum else None
+    if frames is None:
+        frames = fr
     # payload_len carries the mean payload length: a hint that picks lanes per packet
     b = _native.RudpBatch(n=n, payload_len=min(lsum // n, 65535) if n else 0, reserved=0,
                           seq=tab.seq.data_ptr(), ack=tab.ack.data_ptr(), flags=tab.flags.data_ptr(),
@@ -499,11 +507,13 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
         _dev_check(csum, "csum", torch.uint16, 1, dev)
         if csum.shape[0] != n:
             raise ValueError(f"csum has {csum.shape[0]} entries for {n} frames")
-    # one allocation for every output: seq | ack | csum (u16) | flags | ok (u8) | status (i32)
-    out = torch.empty((8 * n + 8,), dtype=torch.uint8, device=dev)
-    seq, ack, cs = (out[k * 2 * n:(k + 1) * 2 * n].view(torch.uint16) for k in range(3))
-    flags, ok = out[6 * n:7 * n], out[7 * n:8 * n]
-    status = out[8 * n:8 * n + 4].view(torch.int32)
+    # one allocation for every output: seq | ack | csum (u16) | flags | ok (u8) |
+    # status (i32), split by one call (per-view Python slicing was most of the
+    # entry's host time at small batches)
+    u16 = torch.uint16
+    seq, ack, cs, flags, ok, status = torch.empty((8 * n + 4,), dtype=torch.uint8, device=dev).split_with_sizes(
+        (2 * n, 2 * n, 2 * n, n, n, 4))
+    seq, ack, cs, status = seq.view(u16), ack.view(u16), cs.view(u16), status.view(torch.int32)
     # mean frame length from the buffer size: a hint that picks lanes / tiles per frame
     hint = min(frames.numel() // n, 0xFFFFFFFF) if n else 0
     _native.check(_native.lib().rudp_decode_varlen_checked(
