@@ -153,11 +153,10 @@ def time_events(torch, fn, steps, warmup):
 
 def rank_slice(rank: int, world: int, total: int):
     """Packets rank r frames when `total` packets are split over `world` ranks:
-    [r*total/world, (r+1)*total/world) (no exchange step)."""
-    if total % world:
-        raise ValueError("the packet count must divide evenly over the ranks")
-    n = total // world
-    return rank * n, n
+    [r*total/world, (r+1)*total/world) (SURVEY.md §8e; no exchange step;
+    rudp.shard.rank_slice)."""
+    from rudp.shard import rank_slice as _rank_slice
+    return _rank_slice(rank, world, total)
 
 
 def verify_c5(w, first, n):

@@ -862,3 +862,36 @@ def test_varlen_tile_forms_vs_oracle(cuda, dist):
             assert np.array_equal(host(r.frames), want), ctx
             assert np.array_equal(host(r.frame_off), off), ctx
             assert np.array_equal(host(r.csum), cs), ctx
+
+
+@pytest.mark.parametrize("world", [2, 8])
+def test_varlen_rank_shards_rebase_to_unsharded(cuda, world):
+    """SURVEY.md §8e for variable lengths: each rank encodes its packet slice on
+    the GPU (its own scan, offsets from 0); rebased by rudp.shard.frame_base
+    the shards concatenate to the unsharded GPU encode and the oracle."""
+    from rudp import shard
+    rng = np.random.default_rng(0x5A + world)
+    n = 8192
+    lens = rng.integers(0, 2945, n).astype(np.int32)
+    pay = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    seq, ack, flags, _ = synth.synth(0x5A, 0, n, 0)
+    bounds = np.concatenate([[0], np.cumsum(lens)])
+    want, want_off, want_cs = codec_np.encode_varlen(seq, ack, flags, split_by_lengths(pay, lens)[0], 7)
+    full = batch.pack_batch_varlen((dev(seq, cuda), dev(ack, cuda), dev(flags, cuda)), dev(pay, cuda),
+                                   dev(lens, cuda), 7, want_csum=True)
+    frames, offs, csums, totals = [], [], [], []
+    for r in range(world):
+        first, m = shard.rank_slice(r, world, n)
+        sl = slice(first, first + m)
+        res = batch.pack_batch_varlen((dev(seq[sl], cuda), dev(ack[sl], cuda), dev(flags[sl], cuda)),
+                                      dev(pay[bounds[first]:bounds[first + m]], cuda), dev(lens[sl], cuda), 7,
+                                      want_csum=True)
+        frames.append(host(res.frames))
+        offs.append(host(res.frame_off).astype(np.int64))
+        csums.append(host(res.csum))
+        totals.append(int(offs[-1][-1]))
+    glob = [o + shard.frame_base(totals, r) for r, o in enumerate(offs)]
+    got_off = np.concatenate([g[:-1] for g in glob] + [glob[-1][-1:]])
+    assert np.array_equal(np.concatenate(frames), want) and np.array_equal(host(full.frames), want)
+    assert np.array_equal(got_off, np.asarray(want_off)) and np.array_equal(host(full.frame_off), np.asarray(want_off))
+    assert np.array_equal(np.concatenate(csums), want_cs)
