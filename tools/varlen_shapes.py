@@ -1,6 +1,6 @@
-"""Checked varlen encode (the sync-free Python entry) across length shapes:
-equal lengths at several hints and uniform ragged ones, median of HIP-event
-pairs per call.  Run under two builds (RUDP_LIB) for an A/B.
+"""Checked varlen encode and decode-verify (the sync-free Python entries)
+across length shapes: equal lengths at several hints and uniform ragged ones,
+median of HIP-event pairs per call.  Run under two builds (RUDP_LIB) for an A/B.
 
 usage: python tools/varlen_shapes.py [--reps 30] [--only L64,U0-512]
 """
@@ -56,7 +56,23 @@ def main():
         ms = statistics.median(x.elapsed_time(y) for x, y in ts)
         alg = 2 * total + n * (7 + 4 + 5 + 8)
         same = bool(torch.equal(frames, res.frames))
-        out[name] = {"n": n, "ms": ms, "frac": alg / ms / 1e9 / 8.0, "exact_vs_first_call": same}
+        # decode-verify of the same frames (sync-free entry)
+        want = batch.unpack_batch_varlen(res.frames, res.frame_off, "rudp7").ok
+        for _ in range(3):
+            batch.unpack_batch_varlen(res.frames, res.frame_off, "rudp7", check=False)
+        td = []
+        for _ in range(args.reps):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            d = batch.unpack_batch_varlen(res.frames, res.frame_off, "rudp7", check=False)
+            b.record()
+            td.append((a, b))
+        torch.cuda.synchronize()
+        ms_d = statistics.median(x.elapsed_time(y) for x, y in td)
+        ok = bool(torch.equal(d.ok, want) and bool((want == 1).all().item()))
+        out[name] = {"n": n, "ms": ms, "frac": alg / ms / 1e9 / 8.0, "exact_vs_first_call": same,
+                     "decode_ms": ms_d, "decode_frac": (total + n * (7 + 16 + 8)) / ms_d / 1e9 / 8.0,
+                     "decode_all_ok": ok}
         del lens, pay, tab, res, frames
         torch.cuda.empty_cache()
     print(json.dumps(out, indent=1))
