@@ -184,10 +184,13 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   const uint32_t glog = (uint32_t)((int)a.glog + kLogBlock - 8);
   const uint32_t G = 1u << glog;
   uint32_t tile = blockIdx.x;
-  if (a.xcd_swizzle) tile = xcd_tile(tile, a.num_tiles);  // each XCD streams its own slice
+  if (a.xcd_swizzle == 1) tile = xcd_tile(tile, a.num_tiles);  // each XCD streams its own slice
+  else if (a.xcd_swizzle == 2) tile = xcd_tile_chunked(tile, a.num_tiles, a.xcd_chunk);
+  else if (a.xcd_swizzle == 3) tile = xcd_tile_rot(tile, a.num_tiles);
   const uint64_t p0 = (uint64_t)tile * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
+  const uint64_t t_start = a.trace ? (uint64_t)wall_clock64() : 0ull;
 
   // ---- phase 1: payload -> LDS, per-packet LE16 sums --------------------
   const uint32_t q = tid >> glog;
@@ -287,6 +290,16 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
     encode_phase2_hc<H, NTS, BLOCK>(a, lds_pay, reinterpret_cast<const u32x4*>(lds + a.hc_off), p0, Tv, tid);
   else
     encode_phase2<H, NTS, BLOCK>(a, lds_pay, lds_hdr, p0, Tv, tid);
+  if (a.trace) {  // diagnostics: the tile's timeline (100 MHz wall clock), XCD and CU
+    __syncthreads();
+    if (tid == 0) {
+      const uint64_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // XCC_ID[3:0]
+      u32x4* rec = reinterpret_cast<u32x4*>(a.trace + 4ull * tile);
+      const uint64_t t_end = (uint64_t)wall_clock64();
+      rec[0] = make_u32x4(t_start, t_end);
+      rec[1] = make_u32x4(xcc, (uint64_t)__smid());
+    }
+  }
 }
 
 // Any payload length / alignment: one wave per packet, byte-granular.

@@ -1,0 +1,124 @@
+"""Timeline of one fixed-length encode launch, tile by tile (rudpx_encode_trace).
+
+Every tile records its start and end (100 MHz wall clock), its XCD and CU.
+From one traced launch per shape this prints:
+  span_us            first start to last end
+  per_xcd            tiles, first start / last end (us from the launch start),
+                     mean tile time
+  ramp_us / tail_us  time until the resident tile count first reaches 90 %
+                     of its median, and from its last time there to the end
+  tile_us            mean tile time in the first / middle / last tenth of the span
+  untraced_ms        the same launch without the trace, median of events
+Shapes: the headline (1M x 1472 B in buffers of its own) and a 16M launch.
+
+usage: python tools/tile_timeline.py [--L 1472] [--no-16m]
+"""
+from __future__ import annotations
+
+import argparse
+import ctypes
+import json
+import statistics
+import sys
+from pathlib import Path
+
+import numpy as np
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(REPO), str(REPO / "reliable-udp_amd")]
+
+import torch  # noqa: E402
+
+from rudp import _native, batch  # noqa: E402
+
+TICK_US = 0.01  # wall_clock64 runs at 100 MHz
+
+
+def analyse(rec: np.ndarray) -> dict:
+    t0 = rec[:, 0].astype(np.int64)
+    t1 = rec[:, 1].astype(np.int64)
+    xcc = rec[:, 2].astype(np.int64)
+    base = t0.min()
+    s, e = (t0 - base) * TICK_US, (t1 - base) * TICK_US
+    span = float(e.max())
+    per = {}
+    for x in sorted(set(xcc.tolist())):
+        m = xcc == x
+        per[int(x)] = {"tiles": int(m.sum()), "first_start_us": float(s[m].min()),
+                       "last_end_us": float(e[m].max()), "mean_tile_us": float((e[m] - s[m]).mean())}
+    # resident tiles over time, 1-us bins
+    nb = int(span) + 2
+    conc = np.zeros(nb + 1)
+    np.add.at(conc, np.floor(s).astype(int), 1)
+    np.add.at(conc, np.floor(e).astype(int), -1)
+    conc = np.cumsum(conc)[:nb]
+    med = float(np.median(conc[: max(1, int(span))]))
+    hi = np.nonzero(conc >= 0.9 * med)[0]
+    ramp = float(hi[0]) if len(hi) else span
+    tail = float(span - hi[-1]) if len(hi) else span
+    d = e - s
+    tenth = span / 10
+    first = d[s < tenth].mean()
+    mid = d[(s >= 4.5 * tenth) & (s < 5.5 * tenth)].mean()
+    last = d[s >= 9 * tenth].mean()
+    return {"span_us": span, "tiles": int(len(rec)), "median_resident_tiles": med,
+            "ramp_us": ramp, "tail_us": tail,
+            "tile_us": {"first_tenth": float(first), "middle": float(mid), "last_tenth": float(last)},
+            "xcd_last_end_spread_us": float(max(v["last_end_us"] for v in per.values())
+                                            - min(v["last_end_us"] for v in per.values())),
+            "per_xcd": per}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--L", type=int, default=1472)
+    ap.add_argument("--no-16m", action="store_true")
+    args = ap.parse_args()
+    dev = torch.device("cuda", 0)
+    lib = _native.lib()
+    lib.rudpx_encode_trace.argtypes = [ctypes.c_void_p]
+    L, M = args.L, 1 << 20
+    shapes = {"own_1M": M}
+    if not args.no_16m:
+        shapes["launch_16M"] = 16 * M
+    out = {}
+    for name, n in shapes.items():
+        tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
+        fr = torch.empty((n, L + 7), dtype=torch.uint8, device=dev)
+
+        def enc():
+            batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
+        for _ in range(3):
+            enc()
+        ts = []
+        for _ in range(8):
+            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            a.record()
+            enc()
+            b.record()
+            b.synchronize()
+            ts.append(a.elapsed_time(b))
+        tiles = (n + 15) // 16  # T = 16 at L >= 512
+        buf = torch.zeros((tiles * 4,), dtype=torch.int64, device=dev)
+        res = {"untraced_ms": statistics.median(ts)}
+        runs = []
+        for k in range(3):
+            enc()  # back to back with the traced launch, as in the bench
+            lib.rudpx_encode_trace(buf.data_ptr())
+            enc()
+            lib.rudpx_encode_trace(None)
+            torch.cuda.synchronize()
+            rec = buf.view(-1, 4).cpu().numpy()
+            if (rec[:, 1] == 0).any():
+                raise RuntimeError("trace incomplete: tile geometry is not T = 16")
+            runs.append(analyse(rec))
+        res["traced"] = runs
+        out[name] = res
+        del tab, pay, fr, buf
+        torch.cuda.empty_cache()
+        print(f"{name} done", file=sys.stderr, flush=True)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
