@@ -154,6 +154,15 @@ __global__ void __launch_bounds__(kBlock) copy_tile_dma_kernel(const u32x4* __re
   }
 }
 
+// Diagnostics: one lane writes the 100 MHz wall clock (a vector store), so a
+// tool can stamp the stream before and after a launch.
+__global__ void stamp_kernel(uint64_t* dst) {
+  if (threadIdx.x == 0) {
+    const uint64_t t = (uint64_t)wall_clock64();
+    *reinterpret_cast<u32x4*>(dst) = u32x4{(uint32_t)t, (uint32_t)(t >> 32), 0u, 0u};
+  }
+}
+
 }  // namespace rudp
 
 extern "C" {
@@ -311,6 +320,12 @@ int rudpx_tune(int key, int value) {
 int rudpx_encode_trace(uint64_t* buf) {
   rudp::tuning().encode_trace.store(buf);
   return 0;
+}
+
+// Writes the wall clock at dst[0] (dst 16-B aligned) when the stream gets there.
+int rudpx_stamp(uint64_t* dst, void* stream) {
+  hipLaunchKernelGGL(rudp::stamp_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, dst);
+  return (int)hipGetLastError();
 }
 
 // Copy n16 16-byte vectors (both pointers 16-byte aligned) with `blocks` workgroups.

@@ -9,6 +9,10 @@ From one traced launch per shape this prints:
                      of its median, and from its last time there to the end
   tile_us            mean tile time in the first / middle / last tenth of the span
   untraced_ms        the same launch without the trace, median of events
+  stamp_to_first_tile_us / last_tile_to_stamp_us
+                     a one-lane kernel stamps the wall clock on the stream just
+                     before and just after the traced launch: the launch's time
+                     outside its tiles (plus two kernel boundaries)
 Shapes: the headline (1M x 1472 B in buffers of its own) and a 16M launch.
 
 usage: python tools/tile_timeline.py [--L 1472] [--no-16m]
@@ -73,16 +77,25 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--L", type=int, default=1472)
     ap.add_argument("--no-16m", action="store_true")
+    ap.add_argument("--save", default="", help="directory for the raw 1M traces (.npy)")
+    ap.add_argument("--percu", default="", help="also trace 1M under these tiles-per-CU caps (rudpx_tune 6)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     lib = _native.lib()
     lib.rudpx_encode_trace.argtypes = [ctypes.c_void_p]
+    lib.rudpx_stamp.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
+    stream = torch.cuda.current_stream().cuda_stream
+    stamps = torch.zeros((4,), dtype=torch.int64, device=dev)
     L, M = args.L, 1 << 20
-    shapes = {"own_1M": M}
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    shapes = {"own_1M": (M, -1)}
+    for c in filter(None, args.percu.split(",")):
+        shapes[f"own_1M_percu{c}"] = (M, int(c))
     if not args.no_16m:
-        shapes["launch_16M"] = 16 * M
+        shapes["launch_16M"] = (16 * M, -1)
     out = {}
-    for name, n in shapes.items():
+    for name, (n, percu) in shapes.items():
+        lib.rudpx_tune(6, percu)
         tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
         fr = torch.empty((n, L + 7), dtype=torch.uint8, device=dev)
 
@@ -104,19 +117,29 @@ def main():
         runs = []
         for k in range(3):
             enc()  # back to back with the traced launch, as in the bench
+            lib.rudpx_stamp(stamps.data_ptr(), stream)
             lib.rudpx_encode_trace(buf.data_ptr())
             enc()
             lib.rudpx_encode_trace(None)
+            lib.rudpx_stamp(stamps[2:].data_ptr(), stream)
+            enc()
             torch.cuda.synchronize()
             rec = buf.view(-1, 4).cpu().numpy()
             if (rec[:, 1] == 0).any():
                 raise RuntimeError("trace incomplete: tile geometry is not T = 16")
-            runs.append(analyse(rec))
+            r = analyse(rec)
+            if args.save and n == M:
+                np.save(Path(args.save) / f"tile_trace_{name}_{k}.npy", rec)
+            st = stamps.cpu().numpy()
+            r["stamp_to_first_tile_us"] = float((rec[:, 0].min() - st[0]) * TICK_US)
+            r["last_tile_to_stamp_us"] = float((st[2] - rec[:, 1].max()) * TICK_US)
+            runs.append(r)
         res["traced"] = runs
         out[name] = res
         del tab, pay, fr, buf
         torch.cuda.empty_cache()
         print(f"{name} done", file=sys.stderr, flush=True)
+    lib.rudpx_tune(6, -1)
     print(json.dumps(out, indent=1))
 
 
