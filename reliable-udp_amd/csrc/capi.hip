@@ -590,6 +590,7 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
     const uint64_t T = (uint64_t)256u * a.small_fpt;
     const uint64_t hint = in->payload_len ? in->payload_len : 1u;
     a.small_cap = (uint32_t)((T * hint * 5u / 4u + 256u + 15u) & ~15ull);
+    a.trace = tuning().encode_trace.load();
     rc = launch_encode_varlen_small(a, chk, layout, s);
     if (rc) return hip_fail((hipError_t)rc, "small-frame varlen encode launch");
     return 0;

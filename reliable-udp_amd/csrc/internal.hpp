@@ -115,6 +115,7 @@ struct VarlenArgs {
   // an unchecked caller, the limit is frame_off[n].
   uint64_t frames_lim;
   uint32_t* status_out;
+  uint64_t* trace;                // diagnostics (rudpx_encode_trace): small-frame encode timeline per tile
   uint32_t small_fpt;             // decode small-frame tile: frames per thread (0: not used)
   uint32_t small_cap;             // its LDS run budget in bytes
   uint32_t xcd;                   // tile kernels: XCD-contiguous tile order (xcd_tile)

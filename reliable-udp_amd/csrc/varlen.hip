@@ -1262,6 +1262,7 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
   const uint64_t p0 = tile * T;
   const uint32_t Tv = a.n - p0 < T ? (uint32_t)(a.n - p0) : T;
   uint64_t fo0, fo_end;
+  const uint64_t t_start = a.trace ? (uint64_t)wall_clock64() : 0ull;  // diagnostics
   if (FUSED) {
     __shared__ uint64_t s_pre[kBlock / 64], s_all[kBlock / 64];
     __shared__ uint32_t s_bits;
@@ -1308,6 +1309,7 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
     fo_end = p0 + T < a.n ? sums[tile + 1] : a.frame_off[a.n];
     if (call_failed(a.status)) return;
   }
+  const uint64_t t_base = a.trace ? (uint64_t)wall_clock64() : 0ull;
   const uint64_t po0 = fo0 - p0 * (uint64_t)H, po_end = fo_end - (p0 + Tv) * (uint64_t)H;
   const uint64_t A = po0 & ~15ull, OA = fo0 & ~15ull;
   const uint64_t prun = ((po_end + 15u) & ~15ull) - A;
@@ -1431,6 +1433,14 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
     } else {
       const uint32_t lo = X > lead ? X : lead, hi = X + 16u < end ? X + 16u : end;
       for (uint32_t b = lo; b < hi; ++b) out[b] = img[b];
+    }
+  }
+  if (a.trace) {  // diagnostics: {start, base known, end, XCC} per tile (tools/small_timeline.py)
+    __syncthreads();
+    if (tid == 0) {
+      u32x4* rec = reinterpret_cast<u32x4*>(a.trace + 4ull * tile);
+      rec[0] = make_u32x4(t_start, t_base);
+      rec[1] = make_u32x4((uint64_t)wall_clock64(), __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20));
     }
   }
 }
