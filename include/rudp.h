@@ -30,9 +30,10 @@
  *    calling thread is available from rudp_last_error().
  *  - Reentrant and thread-safe: the global state is mutex-guarded per-device
  *    caches (the *_host staging pipeline, the stream-ordered scratch pool,
- *    the bounds scratch) plus the non-ABI experiment knobs of rudpx_tune,
- *    which are atomics (a launch concurrent with a knob change may see old
- *    and new settings mixed; the knobs are for sweeps, not for callers).
+ *    the bounds scratch) plus the non-ABI experiment knobs of rudpx_tune and
+ *    the rudpx_encode_trace buffer pointer, which are atomics (a launch
+ *    concurrent with a change may see old and new settings mixed; they are
+ *    for sweeps and timelines, not for callers).
  */
 #ifndef RUDP_H_
 #define RUDP_H_

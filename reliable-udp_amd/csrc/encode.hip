@@ -191,6 +191,7 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
   const uint64_t t_start = a.trace ? (uint64_t)wall_clock64() : 0ull;
+  uint64_t t_loaded = 0, t_summed = 0;
 
   // ---- phase 1: payload -> LDS, per-packet LE16 sums --------------------
   const uint32_t q = tid >> glog;
@@ -238,6 +239,7 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
       }
     }
     __syncthreads();
+    if (a.trace && tid == 0) t_loaded = (uint64_t)wall_clock64();
     if (q < Tv && !(a.ablate & 1u)) {
       const u32x4* mine = dst + q * V;
       for (uint32_t v = g; v < V; v += G) sum += le16_sum(mine[v]);
@@ -285,6 +287,7 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
     }
   }
   __syncthreads();
+  if (a.trace && tid == 0) t_summed = (uint64_t)wall_clock64();
 
   if (a.hchunk)
     encode_phase2_hc<H, NTS, BLOCK>(a, lds_pay, reinterpret_cast<const u32x4*>(lds + a.hc_off), p0, Tv, tid);
@@ -294,10 +297,11 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
     __syncthreads();
     if (tid == 0) {
       const uint64_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // XCC_ID[3:0]
-      u32x4* rec = reinterpret_cast<u32x4*>(a.trace + 4ull * tile);
+      u32x4* rec = reinterpret_cast<u32x4*>(a.trace + 6ull * tile);
       const uint64_t t_end = (uint64_t)wall_clock64();
       rec[0] = make_u32x4(t_start, t_end);
       rec[1] = make_u32x4(xcc, (uint64_t)__smid());
+      rec[2] = make_u32x4(t_loaded, t_summed);  // phase-1 loads landed, sums + headers done
     }
   }
 }

@@ -315,8 +315,9 @@ int rudpx_tune(int key, int value) {
 }
 
 // Diagnostics: while `buf` is non-null, every fixed-length encode tile writes
-// {start, end (100 MHz wall clock), XCC id, CU id} as 4 u64 at buf[4 * tile]
-// (buf holds 4 u64 per tile of the launch).  Not thread-safe; tools only.
+// {start, end (100 MHz wall clock), XCC id, CU id, phase-1 loads landed, sums
+// done} as 6 u64 at buf[6 * tile], and every small-frame encode tile {start,
+// base known, end, XCC id} at buf[4 * tile].  Not thread-safe; tools only.
 int rudpx_encode_trace(uint64_t* buf) {
   rudp::tuning().encode_trace.store(buf);
   return 0;

@@ -8,6 +8,8 @@ From one traced launch per shape this prints:
   ramp_us / tail_us  time until the resident tile count first reaches 90 %
                      of its median, and from its last time there to the end
   tile_us            mean tile time in the first / middle / last tenth of the span
+  phases             per-tile percentiles: phase-1 loads (start to landed), sums and
+                     headers (landed to the second barrier), phase-2 stores (to the end)
   untraced_ms        the same launch without the trace, median of events
   stamp_to_first_tile_us / last_tile_to_stamp_us
                      a one-lane kernel stamps the wall clock on the stream just
@@ -38,6 +40,10 @@ from rudp import _native, batch  # noqa: E402
 TICK_US = 0.01  # wall_clock64 runs at 100 MHz
 
 
+def pct(x):
+    return {p: round(float(np.percentile(x, p)), 3) for p in (10, 50, 90)}
+
+
 def analyse(rec: np.ndarray) -> dict:
     t0 = rec[:, 0].astype(np.int64)
     t1 = rec[:, 1].astype(np.int64)
@@ -65,7 +71,10 @@ def analyse(rec: np.ndarray) -> dict:
     first = d[s < tenth].mean()
     mid = d[(s >= 4.5 * tenth) & (s < 5.5 * tenth)].mean()
     last = d[s >= 9 * tenth].mean()
-    return {"span_us": span, "tiles": int(len(rec)), "median_resident_tiles": med,
+    t_ld = (rec[:, 4].astype(np.int64) - t0) * TICK_US
+    t_sm = (rec[:, 5].astype(np.int64) - t0) * TICK_US
+    phases = {"load_us": pct(t_ld), "sum_us": pct(t_sm - t_ld), "store_us": pct(d - t_sm)}
+    return {"span_us": span, "tiles": int(len(rec)), "median_resident_tiles": med, "phases": phases,
             "ramp_us": ramp, "tail_us": tail,
             "tile_us": {"first_tenth": float(first), "middle": float(mid), "last_tenth": float(last)},
             "xcd_last_end_spread_us": float(max(v["last_end_us"] for v in per.values())
@@ -112,7 +121,7 @@ def main():
             b.synchronize()
             ts.append(a.elapsed_time(b))
         tiles = (n + 15) // 16  # T = 16 at L >= 512
-        buf = torch.zeros((tiles * 4,), dtype=torch.int64, device=dev)
+        buf = torch.zeros((tiles * 6,), dtype=torch.int64, device=dev)
         res = {"untraced_ms": statistics.median(ts)}
         runs = []
         for k in range(3):
@@ -124,7 +133,7 @@ def main():
             lib.rudpx_stamp(stamps[2:].data_ptr(), stream)
             enc()
             torch.cuda.synchronize()
-            rec = buf.view(-1, 4).cpu().numpy()
+            rec = buf.view(-1, 6).cpu().numpy()
             if (rec[:, 1] == 0).any():
                 raise RuntimeError("trace incomplete: tile geometry is not T = 16")
             r = analyse(rec)
