@@ -88,6 +88,7 @@ def main():
     ap.add_argument("--no-16m", action="store_true")
     ap.add_argument("--save", default="", help="directory for the raw 1M traces (.npy)")
     ap.add_argument("--percu", default="", help="also trace 1M under these tiles-per-CU caps (rudpx_tune 6)")
+    ap.add_argument("--early", action="store_true", help="also trace 1M with the header-table loads before phase 1 (rudpx_tune 30)")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     lib = _native.lib()
@@ -100,11 +101,14 @@ def main():
     shapes = {"own_1M": (M, -1)}
     for c in filter(None, args.percu.split(",")):
         shapes[f"own_1M_percu{c}"] = (M, int(c))
+    if args.early:
+        shapes["own_1M_early_table"] = (M, -1)
     if not args.no_16m:
         shapes["launch_16M"] = (16 * M, -1)
     out = {}
     for name, (n, percu) in shapes.items():
         lib.rudpx_tune(6, percu)
+        lib.rudpx_tune(30, 1 if name.endswith("early_table") else -1)
         tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
         fr = torch.empty((n, L + 7), dtype=torch.uint8, device=dev)
 
@@ -149,6 +153,7 @@ def main():
         torch.cuda.empty_cache()
         print(f"{name} done", file=sys.stderr, flush=True)
     lib.rudpx_tune(6, -1)
+    lib.rudpx_tune(30, -1)
     print(json.dumps(out, indent=1))
 
 
