@@ -27,3 +27,22 @@ bash tools/gpu/run.sh sweep ragged --only ragged --reps 9          # ragged.json
 bash tools/gpu/run.sh py e2e tools/e2e_sweep.py                    # e2e.json
 # N = 2 rehearsal on one GPU (gloo), bench_n2_share_device.json
 timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 --master-port 29511 bench.py --gpus 2 --share-device --steps 10 --warmup 2
+# session 3 of round 2: where the headline's last 8% goes (profiles/r02/headline/)
+bash tools/gpu/run.sh py launch_length tools/launch_length.py                       # launch_length.json
+bash tools/gpu/run.sh py xcd_orders tools/launch_length.py --orders --rounds 3 --reps 10   # xcd_orders.json
+bash tools/gpu/run.sh py tile_timeline tools/tile_timeline.py                       # tile_timeline.json
+bash tools/gpu/run.sh py tile_timeline2 tools/tile_timeline.py --no-16m --save gpurun_out/tt --percu 4,6,0   # tile_timeline_percu.json
+bash tools/gpu/run.sh py tile_phases tools/tile_timeline.py --no-16m --percu 0      # tile_phases.json
+bash tools/gpu/run.sh py tile_phases_early tools/tile_timeline.py --no-16m --early   # tile_phases_early_table.json
+bash tools/gpu/run.sh py sustained tools/sustained.py --n 300                       # sustained.json
+bash tools/gpu/run.sh py sustained2 tools/sustained.py --n 100 --variants           # sustained_variants.json
+bash tools/gpu/run.sh py power tools/power_probe.py                                 # power_encode_vs_copy.json
+timeout -s KILL 240 rocprofv3 --kernel-trace --pmc GRBM_GUI_ACTIVE GRBM_COUNT -f csv -d gpurun_out/clk -o run -- python3 tools/sustained.py --n 100   # sclk_encode_vs_copy.json
+bash tools/gpu/run.sh sweep early --only knob --key 30 --values=-1,1,0 --encode-L 1472 --reps 15    # early_table_1472.json
+bash tools/gpu/run.sh sweep regsum --only knob --key 56 --values=0,1 --encode-L 1472,1024 --reps 15  # regsum_1472_1024.json (form removed)
+bash tools/gpu/run.sh sweep small1 --only small --reps 7                            # small_onepass/ (form removed)
+bash tools/gpu/run.sh py small_timeline tools/small_timeline.py                     # small_onepass/timeline_xcd_order.json
+# end-of-round refresh
+bash tools/gpu/run.sh tests && bash tools/gpu/run.sh smoke && bash tools/gpu/run.sh bench r02j
+bash tools/gpu/run.sh trace enc1M bench.py --no-legs --no-cpu-baseline
+bash tools/gpu/run.sh pmc enc1M bench.py --no-legs --no-cpu-baseline --steps 10 --warmup 2
