@@ -46,3 +46,7 @@ bash tools/gpu/run.sh py small_timeline tools/small_timeline.py                 
 bash tools/gpu/run.sh tests && bash tools/gpu/run.sh smoke && bash tools/gpu/run.sh bench r02j
 bash tools/gpu/run.sh trace enc1M bench.py --no-legs --no-cpu-baseline
 bash tools/gpu/run.sh pmc enc1M bench.py --no-legs --no-cpu-baseline --steps 10 --warmup 2
+bash tools/gpu/run.sh sweep tabdma --only knob --key 30 --values=-1,2,1 --encode-L 1472,1024,512 --reps 15   # table_dma.json
+bash tools/gpu/run.sh sweep tabdma2 --only knob --key 30 --values=-1,2 --encode-L 1472,512,768 --reps 25   # table_dma_repeat.json
+bash tools/gpu/run.sh tests && bash tools/gpu/run.sh smoke && bash tools/gpu/run.sh bench r02k   # after the table-by-DMA default
+bash tools/gpu/run.sh py tile_phases_dma tools/tile_timeline.py --no-16m   # tile_phases_table_dma.json

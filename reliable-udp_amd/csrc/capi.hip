@@ -107,8 +107,20 @@ EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t*
   if (encode_tile_ok(a.L, in->payload, frames)) {
     encode_tile_geometry(a.L, &a.T, &a.glog);
     a.hdr_bytes = ((a.T + 1u) * 8u + 15u) & ~15u;
+    // Header-table loads: before phase 1 for tiles of at most 16 KiB; above
+    // (automatic) or with early = 2, the tile's 80 table bytes go by LDS-DMA
+    // with the payload (T = 16, 16-B aligned arrays): 1M x 1472 B 0.5126 ->
+    // 0.5086 and 0.5102 -> 0.5069 ms on two boxes, where the leaders' loads
+    // after phase 1 were a dependent round trip inside the sum phase
+    // (profiles/r02/headline/tile_phases.json, table_dma*.json).
     const int early = tuning().encode_early_table;
     a.early_table = (early == 1 || (early < 0 && a.T * a.L <= 16384u)) ? 1u : 0u;
+    if ((early == 2 || (early < 0 && a.T * a.L > 16384u)) && a.T == 16u && aligned16(in->seq) &&
+        aligned16(in->ack) && aligned16(in->flags)) {
+      a.early_table = 2;  // the tile's 80 table bytes ride the payload's LDS-DMA stream
+      a.tab_off = a.hdr_bytes;
+      a.hdr_bytes += 80u;
+    }
     if (tuning().encode_hchunk && a.T % 16u == 0 && !(tuning().encode_ablate & ~32)) {
       a.hchunk = 1;
       a.hc_off = a.hdr_bytes;

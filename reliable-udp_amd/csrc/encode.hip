@@ -201,7 +201,8 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   // overlaps phase 1 instead of adding a round trip after the barrier.
   const bool tab = !(a.ablate & 4u);
   uint32_t t_seq = 1u, t_ack = 2u, t_flags = 3u;
-  if (a.early_table && tab && g == 0 && q < Tv) {
+  const bool dma_tab = DMA && a.early_table == 2u && Tv == T && tab;  // uniform
+  if (a.early_table == 1u && tab && g == 0 && q < Tv) {
     t_seq = a.seq[p0 + q];
     t_ack = a.ack[p0 + q];
     t_flags = a.flags[p0 + q];
@@ -217,6 +218,14 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
     if (DMA) {
       // LDS-DMA (global_load_lds_dwordx4): each wave-instruction moves 1 KiB
       // from HBM straight into the tile, lane-linear, no VGPR round trip.
+      if (dma_tab && tid < 5u) {  // the tile's table: seq 2 x 16 B, ack 2 x 16 B, flags 16 B
+        const unsigned char* g_src = tid < 2u ? reinterpret_cast<const unsigned char*>(a.seq + p0) + 16u * tid
+                                   : tid < 4u ? reinterpret_cast<const unsigned char*>(a.ack + p0) + 16u * (tid - 2u)
+                                              : reinterpret_cast<const unsigned char*>(a.flags + p0);
+        __builtin_amdgcn_global_load_lds((const void __attribute__((address_space(1)))*)g_src,
+                                         (void __attribute__((address_space(3)))*)(lds + a.tab_off), 16, 0,
+                                         NTL ? 2 : 0);
+      }
       const uint32_t wbase = tid & ~63u;
       for (uint32_t v0 = wbase; v0 < nvec; v0 += BLOCK) {
         if (v0 + (tid & 63u) < nvec)
@@ -248,8 +257,14 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
   if (g == 0 && q < Tv) {
     const uint64_t p = p0 + q;
-    const bool late = tab && !a.early_table;
-    const uint32_t s = late ? a.seq[p] : t_seq, k = late ? a.ack[p] : t_ack, f = late ? a.flags[p] : t_flags;
+    const bool late = tab && a.early_table != 1u && !dma_tab;
+    uint32_t s = late ? a.seq[p] : t_seq, k = late ? a.ack[p] : t_ack, f = late ? a.flags[p] : t_flags;
+    if (dma_tab) {
+      const unsigned char* tb = lds + a.tab_off;
+      s = reinterpret_cast<const uint16_t*>(tb)[q];
+      k = reinterpret_cast<const uint16_t*>(tb + 32)[q];
+      f = tb[64 + q];
+    }
     const uint32_t c = packet_csum(sum, s, k, f);
     const uint64_t h = pack_header<H>(s, k, f, c);
     lds_hdr[q] = h;

@@ -29,7 +29,9 @@ struct EncodeTileArgs {
   uint32_t ablate;      // diagnostics only (wrong output): 1 no LDS sum pass, 2 plain phase-2
                         // LDS reads, 4 no header-table loads, 32 no header-chunk build
   uint32_t out_align64; // phase 2 deals full chunks from the tile's first 64-B boundary
-  uint32_t early_table;     // tile kernel: header-table loads issued before phase 1
+  uint32_t early_table;     // tile kernel: header-table loads issued before phase 1 (2: by LDS-DMA
+                            // into tab_off with the payload, full tiles of T = 16)
+  uint32_t tab_off;         // LDS byte offset of that table copy: seq [16] u16, ack [16] u16, flags [16] u8
   uint32_t hchunk;          // tile kernel (T % 16 == 0): leaders prebuild header chunks in LDS
   uint32_t hc_off;          // LDS byte offset of the header-chunk array [T + 1][2] x 16 B
   uint32_t hc_scratch;      // leaders build header chunks through a 48-B LDS scratch per packet
@@ -214,10 +216,12 @@ struct Tuning {
   // (T % 16 == 0): 1M x 64 B 0.0295 -> 0.0287 ms, x 256 B 0.0962 -> 0.0938,
   // x 1024 B 0.3712 -> 0.3683, x 1472 B equal (profiles/r01/sweeps/encode_hchunk.json).
   std::atomic<int> encode_hchunk{1};
-  // Encode tile header-table loads before phase 1 (1), after it (0), or -1 =
-  // automatic: before for tiles of at most 16 KiB of payload (1M x 64 B
+  // Encode tile header-table loads before phase 1 (1), after it (0), by
+  // LDS-DMA with the payload stream (2: full 16-packet tiles, aligned arrays),
+  // or -1 = automatic: before for tiles of at most 16 KiB of payload (1M x 64 B
   // 0.0287 -> 0.0267 ms, x 256 B 0.0934 -> 0.0892, x 1024 B 0.3606 ->
-  // 0.3557), after above (x 1472 B 0.5208 vs 0.5291 early).
+  // 0.3557), by LDS-DMA above (x 1472 B 0.5126 -> 0.5086; round 1: after,
+  // 0.5208 vs 0.5291 early).
   std::atomic<int> encode_early_table{-1};
   // Leaders build header chunks through a 48-B LDS scratch per packet
   // (constant shifts, one window per chunk) instead of variable-shift

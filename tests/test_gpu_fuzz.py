@@ -14,7 +14,7 @@ from rudp import _native, batch
 pytestmark = pytest.mark.gpu
 
 # (key, choices) drawn per case; the first choice is the default
-_KNOBS = {2: (0, 16, 32, 64, 128, 256), 23: (-1, 0, 1), 30: (-1, 0, 1), 29: (1, 0), 37: (-1, 0, 1),
+_KNOBS = {2: (0, 16, 32, 64, 128, 256), 23: (-1, 0, 1), 30: (-1, 0, 1, 2), 29: (1, 0), 37: (-1, 0, 1),
           25: (1, 0), 34: (1, 0), 12: (1, 0), 11: (1, 0), 5: (1, 0, 2, 3), 54: (64, 1, 3), 49: (0, 1), 48: (0, 256, 4096)}
 
 
@@ -71,7 +71,7 @@ def test_random_shapes_and_knobs_vs_oracle(cuda, seed):
                 lib.rudpx_tune(k, v)
 
 
-_VKNOBS = {51: (1, 0, 2), 52: (2, 0), 49: (0, 1), 46: (16, 0, 64), 47: (0, 1, 2, 4, 8), 50: (1, 0), 14: (1, 0), 16: (1, 0), 36: (1, 2, 0), 43: (1, 0), 44: (-1, 0, 6, 7, 8), 45: (34816, 0, 16384), 30: (-1, 0, 1), 39: (110, 125, 100), 33: (1, 2, 0),
+_VKNOBS = {51: (1, 0, 2), 52: (2, 0), 49: (0, 1), 46: (16, 0, 64), 47: (0, 1, 2, 4, 8), 50: (1, 0), 14: (1, 0), 16: (1, 0), 36: (1, 2, 0), 43: (1, 0), 44: (-1, 0, 6, 7, 8), 45: (34816, 0, 16384), 30: (-1, 0, 1, 2), 39: (110, 125, 100), 33: (1, 2, 0),
            38: (110, 125), 41: (1, 0), 42: (130, 110)}
 
 
