@@ -111,6 +111,28 @@ def test_misaligned_buffers_take_byte_path(cuda):
     assert (host(d.ok) == 1).all() and np.array_equal(host(d.payload), pay)
 
 
+@pytest.mark.parametrize("shift", [0, 1, 3])
+def test_header_table_views_any_alignment(cuda, shift):
+    """The encode tile takes a full tile's header table by LDS-DMA only when
+    the seq/ack/flags arrays are 16-B aligned (1472-B payloads); tables that are
+    views at odd element offsets, and the batch's partial last tile, take the
+    leaders' own loads.  Frames and checksums equal the oracle's either way."""
+    import torch
+    n, L = 16 * 300 + 5, 1472
+    seq, ack, flags, pay = synth.synth(91 + shift, 0, n, L, ascii=False)
+    cols = []
+    for a, dt in ((seq, torch.uint16), (ack, torch.uint16), (flags, torch.uint8)):
+        raw = torch.zeros(n + 8, dtype=dt, device=cuda)
+        v = raw[shift:shift + n]
+        v.copy_(dev(a, cuda))
+        cols.append(v)
+    for layout in (5, 7):
+        fr, cs = batch.pack_batch(tuple(cols), dev(pay, cuda), layout, want_csum=True)
+        want_fr, want_cs = codec_np.encode(seq, ack, flags, pay, layout)
+        assert np.array_equal(host(fr), want_fr), (shift, layout)
+        assert np.array_equal(host(cs), want_cs), (shift, layout)
+
+
 @pytest.mark.parametrize("layout", [5, 7])
 def test_single_byte_corruption_detected(cuda, layout):
     n, L = 4096, 1472
