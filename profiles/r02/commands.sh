@@ -51,3 +51,4 @@ bash tools/gpu/run.sh sweep tabdma2 --only knob --key 30 --values=-1,2 --encode-
 bash tools/gpu/run.sh tests && bash tools/gpu/run.sh smoke && bash tools/gpu/run.sh bench r02k   # after the table-by-DMA default
 bash tools/gpu/run.sh py tile_phases_dma tools/tile_timeline.py --no-16m   # tile_phases_table_dma.json
 bash tools/gpu/run.sh trace enc16M tools/run_kernel.py --op encode --n 16777216 --steps 20 && bash tools/gpu/run.sh pmc enc16M tools/run_kernel.py --op encode --n 16777216 --steps 5   # encode_16Mx1472_summary.json (refresh)
+bash tools/gpu/run.sh tests && bash tools/gpu/run.sh smoke && bash tools/gpu/run.sh bench r02l   # final tree (XCD sweep forms removed): 204 GPU tests

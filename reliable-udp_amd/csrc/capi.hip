@@ -138,9 +138,8 @@ EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t*
     // x 512 B 0.177 -> 0.173, 16M x 1472 B 8.64 -> 7.70 ms; x 256 B equal, x 64 B
     // 0.0259 -> 0.0279 (profiles/r02/sweeps/encode_xcd.json, launch_split.json)
     const int xs = tuning().encode_xcd_swizzle;
-    a.xcd_swizzle = xs >= 1 ? (uint32_t)xs : (xs < 0 && a.L >= 512u) ? 1u : 0u;
+    a.xcd_swizzle = (xs == 1 || (xs < 0 && a.L >= 512u)) ? 1u : 0u;
     a.trace = tuning().encode_trace.load();
-    a.xcd_chunk = (uint32_t)(tuning().encode_xcd_chunk > 0 ? tuning().encode_xcd_chunk.load() : 1);
     a.ablate = (uint32_t)tuning().encode_ablate;
     const int al = tuning().out_align64;
     // Fixed-length encode deals wave stores from the first 64-B boundary at

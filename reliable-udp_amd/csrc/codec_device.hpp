@@ -30,24 +30,6 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nt) {
   return x * per + (x < rem ? x : rem) + k;
 }
 
-// Sweep forms of the XCD order (tuning key 5 = 2 / 3): chunks of k tiles dealt
-// round-robin over the XCDs (k = 1 is the hardware's own order), and
-// contiguous slices whose XCD x starts x/8 of the way into its slice (so the
-// eight concurrent streams are not a whole slice length apart).  Bijective.
-__device__ __forceinline__ uint32_t xcd_tile_chunked(uint32_t b, uint32_t nt, uint32_t k) {
-  const uint32_t span = kXcds * k, nfull = nt / span * span;
-  if (b >= nfull) return b;
-  const uint32_t x = b % kXcds, j = b / kXcds;
-  return ((j / k) * kXcds + x) * k + j % k;
-}
-__device__ __forceinline__ uint32_t xcd_tile_rot(uint32_t b, uint32_t nt) {
-  const uint32_t per = nt / kXcds, rem = nt % kXcds;
-  const uint32_t x = b % kXcds, len = per + (x < rem ? 1u : 0u);
-  uint32_t k = b / kXcds + x * (len / kXcds);
-  if (k >= len) k -= len;
-  return x * per + (x < rem ? x : rem) + k;
-}
-
 // End-around-carry fold of a 32-bit partial sum to 16 bits.
 __device__ __forceinline__ uint32_t fold16(uint32_t s) {
   s = (s & 0xFFFFu) + (s >> 16);

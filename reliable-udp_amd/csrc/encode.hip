@@ -184,9 +184,7 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   const uint32_t glog = (uint32_t)((int)a.glog + kLogBlock - 8);
   const uint32_t G = 1u << glog;
   uint32_t tile = blockIdx.x;
-  if (a.xcd_swizzle == 1) tile = xcd_tile(tile, a.num_tiles);  // each XCD streams its own slice
-  else if (a.xcd_swizzle == 2) tile = xcd_tile_chunked(tile, a.num_tiles, a.xcd_chunk);
-  else if (a.xcd_swizzle == 3) tile = xcd_tile_rot(tile, a.num_tiles);
+  if (a.xcd_swizzle) tile = xcd_tile(tile, a.num_tiles);  // each XCD streams its own slice
   const uint64_t p0 = (uint64_t)tile * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;

@@ -22,9 +22,7 @@ struct EncodeTileArgs {
   uint32_t glog;        // log2(256 / T): lanes per packet
   uint32_t hdr_bytes;   // LDS bytes reserved for the tile's header words
   uint64_t invF;        // ceil(2^32 / (L + H)) for exact x / F, x < T*F
-  uint32_t xcd_swizzle; // 1: map blocks b, b+8, ... to consecutive tiles (one XCD each);
-                        // 2 / 3: sweep forms (xcd_tile_chunked, xcd_tile_rot)
-  uint32_t xcd_chunk;   // tiles per chunk for xcd_swizzle 2
+  uint32_t xcd_swizzle; // 1: map blocks b, b+8, ... to consecutive tiles (one XCD each)
   uint32_t num_tiles;
   uint32_t ablate;      // diagnostics only (wrong output): 1 no LDS sum pass, 2 plain phase-2
                         // LDS reads, 4 no header-table loads, 32 no header-chunk build
@@ -182,8 +180,7 @@ struct Tuning {
   // 1 on, 0 off, -1 from 512-B payloads (16M x 1472 B 0.540 -> 0.481 ms per
   // 2^20 packets; tools/launch_split.py, profiles/r02/sweeps/launch_split.json).
   std::atomic<int> encode_xcd_swizzle{-1};
-  std::atomic<int> encode_xcd_chunk{64};
-  std::atomic<uint64_t*> encode_trace{nullptr};  // diagnostics: tile timeline buffer (tools only)  // tiles per chunk when encode_xcd_swizzle = 2 (sweeps)
+  std::atomic<uint64_t*> encode_trace{nullptr};  // diagnostics: tile timeline buffer (tools only)
   // The same order for the decode, varlen and UTF-8 tile kernels: fixed decode
   // verify 1M x 1472 B 0.240 -> 0.218 ms, x 1024 B 0.170 -> 0.154; copy-out
   // 1472 B 0.523 -> 0.504; varlen decode 1479 B 0.266 -> 0.230, ragged [0, 2944]

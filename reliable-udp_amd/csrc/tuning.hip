@@ -271,8 +271,9 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // 49: XCD-contiguous tile order in the decode / varlen / UTF-8 tile kernels;
 // 50: small-frame encode finds its tile bases itself (no pass-2 launch);
 // 51: varlen byte tiles (0 never, 1 when the scan counts overflowing packet tiles, 2 always);
-// 52: varlen tile sum pass (2 from 128-B block sums, 0 chunk by chunk);
-// 54: tiles per chunk of the chunked XCD order (key 5 = 2; sweeps).
+// 52: varlen tile sum pass (2 from 128-B block sums, 0 chunk by chunk).
+// (54: chunked / rotated XCD orders, measured within 2% and removed;
+// profiles/r02/headline/xcd_orders.json.)
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
@@ -308,8 +309,7 @@ int rudpx_tune(int key, int value) {
             : key == 49 ? &t.tile_xcd
             : key == 50 ? &t.varlen_small_fused
             : key == 51 ? &t.varlen_btile
-            : key == 52 ? &t.varlen_tile_sums : key == 53 ? &t.varlen_lds_pad
-            : key == 54 ? &t.encode_xcd_chunk : nullptr;
+            : key == 52 ? &t.varlen_tile_sums : key == 53 ? &t.varlen_lds_pad : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }

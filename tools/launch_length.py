@@ -8,8 +8,9 @@ Per launch (median of HIP-event pairs), interleaved round by round:
 Separates the launch length (a fixed cost per launch) from the allocation the
 buffers come from (page fragments).  Prints one JSON object.
 
-With --orders, the same shapes under each XCD tile order of the encode
-(rudpx_tune 5 / 54: contiguous slices, chunks of k tiles, rotated slices).
+With --orders, the same shapes with the XCD tile order on and off
+(rudpx_tune 5).  The chunked and rotated orders of
+profiles/r02/headline/xcd_orders.json were measured within 2% and removed.
 
 usage: python tools/launch_length.py [--reps 12] [--rounds 3] [--orders]
 """
@@ -62,20 +63,17 @@ def main():
     cases = {}
     if args.orders:
         lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
-        orders = {"contig": (1, 64), "hw_rr": (0, 64), "rot": (3, 64)}
-        for k in (4, 32, 256, 1024):
-            orders[f"chunk{k}"] = (2, k)
+        orders = {"contig": 1, "hw_rr": 0}
 
-        def tuned(fn, mode, k):
+        def tuned(fn, mode):
             def run():
                 lib.rudpx_tune(5, mode)
-                lib.rudpx_tune(54, k)
                 fn()
             return run
-        for oname, (mode, k) in orders.items():
-            cases[f"{oname}/own_1M"] = (tuned(own, mode, k), 1)
-            cases[f"{oname}/big_1M@15"] = (tuned(enc_slice(15, 1), mode, k), 1)
-            cases[f"{oname}/big_16M"] = (tuned(enc_slice(0, 16), mode, k), 16)
+        for oname, mode in orders.items():
+            cases[f"{oname}/own_1M"] = (tuned(own, mode), 1)
+            cases[f"{oname}/big_1M@15"] = (tuned(enc_slice(15, 1), mode), 1)
+            cases[f"{oname}/big_16M"] = (tuned(enc_slice(0, 16), mode), 16)
     else:
         cases["own_1M"] = (own, 1)
         for k in (0, 5, 15):
@@ -100,6 +98,8 @@ def main():
             torch.cuda.synchronize()
             per[name] += [a.elapsed_time(b) / n for a, b in ev]
         print(f"round {r} done", file=sys.stderr, flush=True)
+    if args.orders:
+        lib.rudpx_tune(5, -1)
     res = {}
     for name, ts in per.items():
         ts.sort()
