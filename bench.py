@@ -159,21 +159,41 @@ def rank_slice(rank: int, world: int, total: int):
     return _rank_slice(rank, world, total)
 
 
-def verify_c5(w, first, n):
-    """Hash this rank's C5 frames per 2^20-packet chunk and compare them with the
-    digests utils/packet.py produced (tests/golden/digests.json).  Returns
-    (chunks checked, chunks matching), or None when the fixture is absent."""
+def verify_digests(w, cfg_name, first, n):
+    """Hash this rank's frames of BASELINE config `cfg_name` per 2^20-packet chunk
+    and compare them with the digests utils/packet.py produced
+    (tests/golden/digests.json; make_golden.py).  Every buffer set of the
+    workload holds the same batch; all of them are checked.  Returns (chunks
+    checked, chunks matching), or None when the fixture has no entry for this
+    shape and layout."""
     path = REPO / "tests" / "golden" / "digests.json"
     if not path.exists():
         return None
-    cfg = json.loads(path.read_text())["C5"]
+    cfg = json.loads(path.read_text()).get(cfg_name)
+    if cfg is None:
+        return None
     want = cfg["layouts"].get(str(w.H))
     if want is None or first % cfg["chunk"] or n % cfg["chunk"] or w.L != cfg["L"]:
         return None
-    from rudp import digest
-    got = digest.chunk_sha256(w.sets[0][2], None, cfg["chunk"])
     k0 = first // cfg["chunk"]
-    return len(got), sum(h == want["frames"][k0 + k] for k, (h, _) in enumerate(got))
+    if k0 + n // cfg["chunk"] > len(want["frames"]):
+        return None
+    from rudp import digest
+    checked = matching = 0
+    for tab, pay, out in w.sets:
+        got = digest.chunk_sha256(out, None, cfg["chunk"])
+        checked += len(got)
+        matching += sum(h == want["frames"][k0 + k] for k, (h, _) in enumerate(got))
+    return checked, matching
+
+
+def verify_c5(w, first, n):
+    """verify_digests for BASELINE config 5 (16M x 1472 B)."""
+    return verify_digests(w, "C5", first, n)
+
+
+def digest_field(chk):
+    return None if chk is None else f"{chk[1]}/{chk[0]}"
 
 
 def time_loop(torch, fn, steps, warmup):
@@ -232,13 +252,17 @@ def c5_strong_leg(torch, dist, batch, device, world, rank, layout, share_device,
 
 def legs(torch, batch, device, steps):
     out = {}
-    for L in (1024, 64):
+    for L, cfg_name in ((1024, "C2"), (64, "C3")):
         w = Workload(torch, batch, 1 << 20, L, "rudp7", 0, SEEDS[L], device)
         ms = time_loop(torch, lambda i: w.encode(batch, i), steps, 3) / steps
+        # every buffer set's frames against the reference digests, outside the clock
+        chk = verify_digests(w, cfg_name, 0, 1 << 20)
         out[f"encode_1Mx{L}"] = {
             "GiB_s": (1 << 20) * L / (ms / 1e3) / GIB, "ms": ms,
             "roofline_frac": (1 << 20) * algorithmic_bytes_encode(L) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
-            "buffer_sets": len(w.sets)}
+            "buffer_sets": len(w.sets),
+            "matches_reference": None if chk is None else chk[0] == chk[1] > 0,
+            "chunks_matching_reference_digests": digest_field(chk)}
         del w
     w = Workload(torch, batch, 1 << 20, 1472, "rudp7", 0, SEEDS[1472], device)
     for i in range(len(w.sets)):
@@ -252,10 +276,22 @@ def legs(torch, batch, device, steps):
         w.encode(batch, i)
         w.decode(batch, i)
     ms = time_loop(torch, rt, steps, 3) / steps
+    # C4: the frames of every buffer set against the reference digest, and the
+    # last decode's fields and checksum status against the inputs (outside the clock)
+    chk = verify_digests(w, "C4", 0, 1 << 20)
+    d = w.decode(batch, 0)
+    tab0 = w.sets[0][0]
+    rt_ok = (bool((d.ok == 1).all()) and torch.equal(d.seq.view(torch.int16), tab0.seq.view(torch.int16))
+             and torch.equal(d.ack.view(torch.int16), tab0.ack.view(torch.int16))
+             and torch.equal(d.flags, tab0.flags))
     out["roundtrip_1Mx1472"] = {
         "GiB_s": (1 << 20) * 1472 / (ms / 1e3) / GIB, "ms": ms,
         "roofline_frac": (1 << 20) * (algorithmic_bytes_encode(1472) + algorithmic_bytes_decode(1472))
-        / (ms / 1e3) / 1e9 / HBM_PEAK_GBS}
+        / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
+        "matches_reference": None if chk is None else chk[0] == chk[1] > 0 and rt_ok,
+        "chunks_matching_reference_digests": digest_field(chk),
+        "decode_fields_equal_inputs": rt_ok}
+    del d
     # end to end from pinned host memory: H2D -> encode -> D2H, two-stream pipeline
     # (rudp_encode_host); PCIe-bound, recorded in DESIGN.md, never the headline
     n, L = 1 << 20, 1472
@@ -294,7 +330,7 @@ def legs(torch, batch, device, steps):
         "roofline_frac": C5_PACKETS * algorithmic_bytes_encode(1472) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS,
         "timing": f"median of {len(ts)} per-launch HIP-event pairs after 3 warmups",
         "ms_min_max": [ts[0], ts[-1]],
-        "chunks_matching_reference_digests": None if chk is None else f"{chk[1]}/{chk[0]}"}
+        "chunks_matching_reference_digests": digest_field(chk)}
     del w16
     torch.cuda.empty_cache()
     w = Workload(torch, batch, 1 << 20, 1472, "rudp7", 0, SEEDS[1472], device)
@@ -572,11 +608,10 @@ def main():
     n, L = args.packets, args.payload
     first = rank * n
     if args.total_packets:
-        if args.total_packets % world:
-            raise SystemExit("--total-packets must divide evenly over the ranks")
         first, n = rank_slice(rank, world, args.total_packets)
     seed = SEEDS.get(L, 0x5EED0004)
     w = Workload(torch, batch, n, L, args.layout, first, seed, device)
+    nsets = len(w.sets)
     for i in range(args.warmup):
         w.encode(batch, i)
     torch.cuda.synchronize()
@@ -602,6 +637,10 @@ def main():
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
     wall_max = float(t.item())
 
+    # the timed frames against the reference (BASELINE configs 2-4 by payload size), outside the clock
+    head_chk = verify_digests(w, {1024: "C2", 64: "C3", 1472: "C4"}.get(L, ""), first, n)
+    del w
+    torch.cuda.empty_cache()
     extra = legs(torch, batch, device, max(10, args.steps // 2)) if (
         rank == 0 and world == 1 and not args.no_legs) else None
     if world > 1 and not args.no_legs and not args.total_packets:
@@ -611,7 +650,8 @@ def main():
                                                       args.layout, args.share_device)}
 
     if rank == 0:
-        total_payload = world * n * L * args.steps
+        # strong scaling: the ranks' slices add up to --total-packets (rank_slice)
+        total_payload = (args.total_packets or world * n) * L * args.steps
         per_launch_s = kernel_ms / 1e3 / args.steps
         achieved = n * algorithmic_bytes_encode(L) / per_launch_s / 1e9
         traffic, traffic_src = read_pmc_traffic(L, n)
@@ -633,7 +673,8 @@ def main():
                             f"(BASELINE config 4/5 shape), device-resident",
                 "packets_per_gpu": n, "payload_bytes": L, "layout": args.layout,
                 "global_batch": world * n, "parallelism": f"packet-slice x{world}, no collective",
-                "buffer_sets": len(w.sets),
+                "buffer_sets": nsets,
+                "matches_reference": None if head_chk is None else head_chk[0] == head_chk[1] > 0,
             },
             "roofline": {
                 "bound": "hbm",

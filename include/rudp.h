@@ -60,7 +60,12 @@ extern "C" {
 /*
  * Status word of the sync-free variable-length calls (*_checked): written on
  * the device by the call itself, 0 when the batch is valid, else these bits.
- * A call whose status is non-zero writes none of its outputs past the offsets.
+ * Encode rejects the whole batch: with a non-zero status it writes no frames
+ * and no checksums, and of d_frame_off only d_frame_off[n] (the total its scan
+ * found); d_frame_off[0..n-1] are then unspecified.  Decode rejects frame by
+ * frame: every frame whose pair of offsets is bad gets d_ok =
+ * RUDP_OK_BAD_OFFSETS and nothing of it is read, every other frame is fully
+ * decoded, and RUDP_ST_OFFSETS is set when any frame was rejected.
  */
 #define RUDP_ST_LEN 1u        /* a len[i] > 65535 */
 #define RUDP_ST_PAYLOAD 2u    /* packed: sum(len) != payload_bytes; gathered: payload outside the buffer */
@@ -158,7 +163,8 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
  * rudp_encode_varlen_checked: payload_bytes = size of in->payload; frames_cap =
  *   capacity of d_frames.  Packed payloads (payload_off NULL) must satisfy
  *   sum(len) == payload_bytes; gathered ones payload_off[i] + len[i] <=
- *   payload_bytes.  d_frame_off is always written (n + 1 entries).
+ *   payload_bytes.  d_frame_off[n] is always written; d_frame_off[0..n-1]
+ *   when the batch is valid (status 0).
  * rudp_decode_varlen_checked: rudp_decode with offsets (zero-copy payload);
  *   frame_off[0..n] must be non-decreasing and <= frames_bytes.
  * rudp_frame_off_check: only the offset check, for callers that run their own

@@ -423,9 +423,14 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
     if out is not None:
         _dev_check(out, "out", torch.uint8, 1, dev)
         frames = out
-        lsum = max(out.numel() - n * H, 0)  # at most; only the lanes hint reads it
-    elif payload_off is None:
-        lsum = payload.numel()  # exact for a valid packed batch; the device checks it
+    if payload_off is None:
+        # exact for a valid packed batch (the device checks it); an oversized `out`
+        # is only capacity and never inflates the hint that picks the kernel's tiles
+        lsum = payload.numel()
+    elif out is not None:
+        # gathered into the caller's buffer: no device read, the hint is bounded by
+        # both the payload buffer and the frame buffer
+        lsum = min(payload.numel(), max(out.numel() - n * H, 0))
     else:
         # gathered payloads: the frame bytes are unknown until the lengths are summed
         # (rudp_varlen_bounds, one 40-byte device read); lengths are read as u32

@@ -19,13 +19,14 @@ from typing import Sequence, Tuple
 
 def rank_slice(rank: int, world: int, total: int) -> Tuple[int, int]:
     """(first, count): the packets rank r frames when `total` packets are split
-    over `world` ranks, [r*total/world, (r+1)*total/world)."""
+    over `world` ranks, [r*total//world, (r+1)*total//world): any world size,
+    shard sizes differing by at most one packet when world does not divide total."""
     if world < 1 or not 0 <= rank < world:
         raise ValueError(f"rank {rank} outside a world of {world}")
-    if total % world:
-        raise ValueError("the packet count must divide evenly over the ranks")
-    n = total // world
-    return rank * n, n
+    if total < 0:
+        raise ValueError(f"negative packet count {total}")
+    first = rank * total // world
+    return first, (rank + 1) * total // world - first
 
 
 def frame_base(shard_frame_bytes: Sequence[int], rank: int) -> int:

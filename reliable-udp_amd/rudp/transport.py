@@ -17,7 +17,9 @@ Protocol (one character of payload per datagram, utils/reliableUDP.py:11):
   An ACK moves k to ack_num - ISN.  After the last frame it keeps waiting for
   the receiver's FIN, answers it with ACK(seq = ISN + k, ack = peer seq + 1)
   and returns.
-* receiver — accepts a SYN (unless it repeats the previous transfer's ISN) as
+* receiver — answers the sender of the last SYN it accepted (kept across
+  recv() calls, so a stray frame before the next SYN is ACKed there); accepts
+  a SYN (unless it repeats the previous transfer's ISN) as
   a new transfer and then the frame whose seq - ISN equals the characters
   received so far; every datagram is answered with ACK(ack = ISN + characters
   received).  After accepting a FIN frame it sends FIN|ACK(ack = ISN + length)
@@ -85,6 +87,10 @@ class ReliableUDP:
         self._draw_isn = isn_source or (lambda: random.randint(1, 5000))
         self._codec_device = codec_device
         self._last_isn: Optional[int] = None  # the previous transfer's ISN (a repeated SYN is ignored)
+        # the sender of the last SYN, kept across recv() calls as the reference
+        # keeps self.target_addr (utils/reliableUDP.py:18, :131 only ever set it):
+        # a stray non-SYN datagram at the start of a later recv() is answered there
+        self._peer: Any = None
 
     # ------------------------------------------------------------ socket
     def create(self):
@@ -184,7 +190,7 @@ class ReliableUDP:
     # ----------------------------------------------------------- receiver
     def recv(self) -> str:
         self.flush_recv_buffer()
-        isn, text, peer = 0, "", None
+        isn, text, peer = 0, "", self._peer
         received = 0  # characters accepted so far (the next in-order frame is isn + received)
         while True:
             reply, addr = self._receive(None)
@@ -194,6 +200,7 @@ class ReliableUDP:
             finished = False
             if syn and not repeated_syn:  # a new transfer starts here
                 isn, received, peer, text = reply.seq, 0, addr, ""
+                self._peer = peer
             if (in_order or syn) and not repeated_syn:
                 text += reply.payload
                 received = len(text)

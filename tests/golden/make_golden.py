@@ -18,6 +18,9 @@ The rudp7 checksum field VALUE is build-defined (the reference has none): it
 comes from oracle/codec_np.py and is only *framed* by the reference.
 
 usage: python tests/golden/make_golden.py [--skip-digests] [--jobs 8]
+       python tests/golden/make_golden.py --only-digests --configs C2,C3
+         (recomputes those configs' digests, every layout, and merges them into
+         the existing digests.json; the other configs' entries are kept)
 """
 from __future__ import annotations
 
@@ -43,8 +46,8 @@ from oracle import codec_np, synth  # noqa: E402
 
 # BASELINE.json configs; seeds fixed per config index.
 CONFIGS = {
-    "C2": dict(seed=0x5EED0002, n=1 << 20, L=1024, layouts=(5,)),
-    "C3": dict(seed=0x5EED0003, n=1 << 20, L=64, layouts=(5,)),
+    "C2": dict(seed=0x5EED0002, n=1 << 20, L=1024, layouts=(5, 7)),
+    "C3": dict(seed=0x5EED0003, n=1 << 20, L=64, layouts=(5, 7)),
     "C4": dict(seed=0x5EED0004, n=1 << 20, L=1472, layouts=(5, 7)),
     "C5": dict(seed=0x5EED0005, n=1 << 24, L=1472, layouts=(5, 7)),
 }
@@ -320,14 +323,17 @@ def _digest_task(args):
     return cfg, layout, chunk_index, h_frames.hexdigest(), h_csum.hexdigest()
 
 
-def make_digests(jobs: int):
+def make_digests(jobs: int, configs=None):
+    """Digests of the named configs (all of CONFIGS when None), every layout."""
+    configs = list(CONFIGS) if configs is None else configs
     tasks = []
-    for cfg, c in CONFIGS.items():
+    for cfg in configs:
+        c = CONFIGS[cfg]
         chunks = (c["n"] + DIGEST_CHUNK - 1) // DIGEST_CHUNK
         for layout in c["layouts"]:
             tasks += [(cfg, layout, k) for k in range(chunks)]
-    out = {cfg: dict(seed=c["seed"], n=c["n"], L=c["L"], chunk=DIGEST_CHUNK, layouts={})
-           for cfg, c in CONFIGS.items()}
+    out = {cfg: dict(seed=CONFIGS[cfg]["seed"], n=CONFIGS[cfg]["n"], L=CONFIGS[cfg]["L"],
+                     chunk=DIGEST_CHUNK, layouts={}) for cfg in configs}
     t0 = time.time()
     with Pool(jobs) as pool:
         for i, (cfg, layout, k, hf, hc) in enumerate(pool.imap_unordered(_digest_task, tasks)):
@@ -391,6 +397,7 @@ def main():
     ap.add_argument("--skip-digests", action="store_true")
     ap.add_argument("--only-digests", action="store_true")
     ap.add_argument("--jobs", type=int, default=min(8, os.cpu_count() or 1))
+    ap.add_argument("--configs", default="", help="comma-separated subset of CONFIGS to (re)digest and merge")
     args = ap.parse_args()
     mod = ref()
     if not args.only_digests:
@@ -401,7 +408,20 @@ def main():
         np.savez_compressed(HERE / "dedup.npz", **make_dedup(mod))
         print("wrote edge_cases.json, frames_small.npz, wire_trace.json, varlen.npz, dedup.npz")
     if not args.skip_digests:
-        (HERE / "digests.json").write_text(json.dumps(make_digests(args.jobs), indent=1) + "\n")
+        path = HERE / "digests.json"
+        if args.configs:
+            sel = [c for c in args.configs.split(",") if c]
+            old = json.loads(path.read_text()) if path.exists() else {}
+            new = make_digests(args.jobs, sel)
+            for cfg in sel:  # a layout digested before must come out the same again
+                for layout, d in old.get(cfg, {}).get("layouts", {}).items():
+                    if layout in new[cfg]["layouts"] and new[cfg]["layouts"][layout] != d:
+                        raise SystemExit(f"{cfg} rudp{layout}: recomputed digests differ from the committed ones")
+            old.update(new)
+            digests = {cfg: old[cfg] for cfg in CONFIGS if cfg in old}
+        else:
+            digests = make_digests(args.jobs)
+        path.write_text(json.dumps(digests, indent=1) + "\n")
         print("wrote digests.json")
 
 

@@ -214,7 +214,8 @@ def _digest_run(cuda, cfg, layout, chunk_index):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("name,layout,chunk", [("C2", 5, 0), ("C3", 5, 0), ("C4", 5, 0), ("C4", 7, 0),
+@pytest.mark.parametrize("name,layout,chunk", [("C2", 5, 0), ("C2", 7, 0), ("C3", 5, 0), ("C3", 7, 0),
+                                               ("C4", 5, 0), ("C4", 7, 0),
                                                ("C5", 7, 0), ("C5", 7, 9), ("C5", 5, 15)])
 def test_full_size_digests(cuda, digests, name, layout, chunk):
     cfg = digests[name]

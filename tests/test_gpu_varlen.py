@@ -676,9 +676,16 @@ def test_varlen_device_checks_reject_bad_batches(cuda):
     rejected("inside payload", payload_off=dev(offs2, cuda))
     small = torch.full((n * 10 - 1,), 0x5C, dtype=torch.uint8, device=cuda)
     rejected("too small", out=small)
-    # without check the call returns at once; the status tells
+    # without check the call returns at once; the status tells.  Contract on a
+    # rejected batch (include/rudp.h): frame_off[n] holds the scan's total on every
+    # path -- the small-frame kernel (hint 4 B) and the scan + tile path (300 B).
     r = batch.pack_batch_varlen(tab, pay, dev(lens + 1, cuda), 7, check=False)
     assert int(r.status.item()) & 2
+    assert int(r.frame_off[-1].item()) == 4 * n + 7 * n
+    big = np.full(n, 300, np.int32)
+    r = batch.pack_batch_varlen(tab, dev(np.zeros(300 * n - 1, np.uint8), cuda), dev(big, cuda), 7, check=False)
+    assert int(r.status.item()) & 2
+    assert int(r.frame_off[-1].item()) == 307 * n
     # decode: offsets decreasing, past the buffer, negative
     fr = batch.pack_batch_varlen(tab, pay, dev(lens, cuda), 7)
     for mut in ((7, 3), (n, 10 ** 9), (0, -8)):

@@ -117,7 +117,7 @@ def test_c_restatement_matches_numpy_and_goldens(golden_small):
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("name,layout", [("C3", 5), ("C4", 7)])
+@pytest.mark.parametrize("name,layout", [("C3", 5), ("C3", 7), ("C4", 7)])
 def test_c_oracle_reproduces_reference_digest(digests, name, layout):
     """The C restatement frames BASELINE config chunk 0 exactly as utils/packet.py did."""
     import hashlib

@@ -28,8 +28,21 @@ def shard_range(rank, world, n_total):
 
 def test_rank_slice_rule():
     assert [bench.rank_slice(r, 8, 1 << 24) for r in (0, 7)] == [(0, 1 << 21), (7 << 21, 1 << 21)]
-    with pytest.raises(ValueError):
-        bench.rank_slice(0, 3, 1 << 24)
+    # any world size: the slices tile [0, total) in rank order, sizes within one packet
+    for world in (1, 2, 3, 5, 6, 7, 8, 16):
+        for total in (0, 1, 7, 1000, 1 << 24):
+            sl = [bench.rank_slice(r, world, total) for r in range(world)]
+            assert sl[0][0] == 0 and all(a[0] + a[1] == b[0] for a, b in zip(sl, sl[1:]))
+            assert sum(n for _, n in sl) == total
+            assert max(n for _, n in sl) - min(n for _, n in sl) <= 1
+
+
+@pytest.mark.parametrize("world", [3, 5, 6])
+def test_uneven_virtual_shards_concatenate_to_unsharded(world):
+    full_fr, _ = codec_c.encode(*synth.synth(SEED, 0, 1000, 64), 7)
+    parts = [codec_c.encode(*synth.synth(SEED, *bench.rank_slice(r, world, 1000), 64), 7)[0]
+             for r in range(world)]
+    assert np.array_equal(np.concatenate(parts), full_fr)
 
 
 @pytest.mark.parametrize("world", [1, 2, 4, 8])

@@ -166,3 +166,38 @@ def test_relay_history_equals_proxy_list_scan():
         assert (relay.retransmitted - before == 1) == want[-1], i
     relay.sock.close()
     assert any(want) and not all(want)
+
+
+def test_receiver_answers_previous_peer_across_recv_calls():
+    """The receiver keeps its peer across recv() calls, as the reference keeps
+    self.target_addr (utils/reliableUDP.py:18, :131, :140-146): a stray non-SYN
+    datagram at the start of a later recv() -- here the previous sender's last
+    frame, resent late -- is ACKed to that sender (ack = 0 + 0: no transfer yet),
+    and the next transfer still goes through."""
+    from rudp.transport import ACK, build, parse
+    server = ReliableUDP().create()
+    server.bind("127.0.0.1", 0)
+    sport = server.socket.getsockname()[1]
+    got = []
+    t = threading.Thread(target=lambda: got.append(server.recv()), daemon=True)
+    t.start()
+    time.sleep(0.05)
+    client = ReliableUDP(timeout=0.2, isn_source=lambda: 100).create()
+    client.send("hi", "127.0.0.1", sport)
+    t.join(timeout=30)
+    assert got == ["hi"]
+    t2 = threading.Thread(target=lambda: got.append(server.recv()), daemon=True)
+    t2.start()
+    time.sleep(0.05)
+    late = build(100 + 1, 0, 0x20, "i")          # the first transfer's FIN frame, again
+    client.socket.sendto(late, ("127.0.0.1", sport))
+    client.socket.settimeout(5)
+    data, _ = client.socket.recvfrom(1024)
+    reply = parse(data)
+    assert reply.flags == ACK and reply.ack == 0 and reply.seq == 0
+    other = ReliableUDP(timeout=0.2, isn_source=lambda: 200).create()
+    other.send("ok", "127.0.0.1", sport)
+    t2.join(timeout=30)
+    assert got == ["hi", "ok"]
+    for s in (client, other, server):
+        s.close()
