@@ -353,7 +353,7 @@ def legs(torch, batch, device, steps):
     def varlen_pair(tab, flat, lens, layout, frames, off, csum, rounds=7):
         """Sync-free and eager-check encode / decode through the Python entry, and the
         raw C-ABI call chain beside them (preallocated outputs, no Python wrapper),
-        interleaved round by round so all four see the same box state; medians
+        interleaved round by round so all forms see the same box state; medians
         of the per-round means (ms per call)."""
         import ctypes
         from rudp import _native
@@ -379,18 +379,30 @@ def legs(torch, batch, device, steps):
         def d(i, check=False):
             last["d"] = batch.unpack_batch_varlen(frames, off, layout, csum=csum, check=check)
 
+        # the same with the outputs of an earlier call reused (no allocation per call)
+        e(0)
+        d(0)
+
+        def e_reuse(i):
+            last["e"] = batch.pack_batch_varlen(tab, flat, lens, layout, want_csum=csum is not None,
+                                                check=False, reuse=last["e"])
+
+        def d_reuse(i):
+            last["d"] = batch.unpack_batch_varlen(frames, off, layout, csum=csum, check=False, reuse=last["d"])
+
         def e_abi(i):
             lib.rudp_encode_varlen_checked(ctypes.byref(rb), flat.numel(), f_out.data_ptr(), f_out.numel(),
                                            o_out.data_ptr(), c_out.data_ptr() if c_out is not None else None,
                                            st.data_ptr(), H, device.index or 0, sp)
 
-        def d_abi(i):
+        def d_abi(i):  # no status word: the one-kernel form the Python entry uses
             lib.rudp_decode_varlen_checked(frames.data_ptr(), frames.numel(), off.data_ptr(),
                                            frames.numel() // n, n,
                                            csum.data_ptr() if csum is not None else None,
-                                           *[t.data_ptr() for t in d_out], st.data_ptr(), H,
+                                           *[t.data_ptr() for t in d_out], None, H,
                                            device.index or 0, sp)
-        fns = {"encode": e, "decode": d, "encode_eager_check": lambda i: e(i, True),
+        fns = {"encode": e, "decode": d, "encode_reuse": e_reuse, "decode_reuse": d_reuse,
+               "encode_eager_check": lambda i: e(i, True),
                "decode_eager_check": lambda i: d(i, True), "encode_abi": e_abi, "decode_abi": d_abi}
         per = {k: [] for k in fns}
         for r in range(rounds):
@@ -398,7 +410,7 @@ def legs(torch, batch, device, steps):
                 per[k].append(time_loop(torch, fn, steps, 2 if r == 0 else 1) / steps)
         last["e"].check()
         last["d"].check()
-        if int(st.item()):
+        if int(st.item()) or bool((d_out[3] == _native.OK_BAD_OFFSETS).any()):
             raise RuntimeError("the raw C-ABI varlen calls rejected the bench batch")
         return {k: sorted(v)[len(v) // 2] for k, v in per.items()}
 
@@ -407,7 +419,8 @@ def legs(torch, batch, device, steps):
                                 "decode_verify_Mpkt_s": n1 / t1["decode"] / 1e3, "decode_ms": t1["decode"],
                                 "ms_by_form": t1,
                                 "note": "Python entry, sync-free (device-side argument checks, status "
-                                        "read after the loop); *_eager_check: one sync per call; *_abi: "
+                                        "read after the loop); *_reuse: outputs of an earlier call reused "
+                                        "(reuse=); *_eager_check: one sync per call; *_abi: "
                                         "the C-ABI calls alone; medians of 7 interleaved rounds"}
     # the varlen path at MTU size: 1M x 1472 B payloads packed back to back
     # (frames at odd offsets), encode (scan + tile kernel) and decode-verify

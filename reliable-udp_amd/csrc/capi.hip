@@ -16,7 +16,8 @@ namespace rudp {
 int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t len_hint, uint64_t n,
                   const uint16_t* d_csum_in, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
                   uint8_t* d_ok, uint16_t* d_csum_out, uint8_t* d_payload_out, int layout,
-                  int device, void* hip_stream, uint32_t* status_out = nullptr, uint64_t frames_lim = 0);
+                  int device, void* hip_stream, bool checked = false, uint32_t* status_out = nullptr,
+                  uint64_t frames_lim = 0);
 namespace {
 
 thread_local std::string g_last_error;
@@ -323,7 +324,7 @@ uint32_t decode_group_log2(uint32_t L) {
 int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t len_hint, uint64_t n,
                   const uint16_t* d_csum_in, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
                   uint8_t* d_ok, uint16_t* d_csum_out, uint8_t* d_payload_out, int layout,
-                  int device, void* hip_stream, uint32_t* status_out, uint64_t frames_lim) {
+                  int device, void* hip_stream, bool checked, uint32_t* status_out, uint64_t frames_lim) {
   if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
     return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
   if (d_payload_out)
@@ -394,6 +395,7 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
   }
   a.status_out = status_out;
   a.frames_lim = frames_lim;
+  a.lim_checked = checked ? 1u : 0u;
   rc = launch_decode_varlen(a, layout, (hipStream_t)hip_stream);
   if (rc) return hip_fail((hipError_t)rc, "varlen decode launch");
   return 0;
@@ -681,13 +683,14 @@ int rudp_decode_varlen_checked(const uint8_t* d_frames, uint64_t frames_bytes, c
                                uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags, uint8_t* d_ok,
                                uint16_t* d_csum_out_or_null, uint32_t* d_status, int layout, int device,
                                void* hip_stream) {
-  if (!d_frame_off || !d_status) return fail(RUDP_EINVAL, "rudp_decode_varlen_checked: NULL pointer");
+  if (!d_frame_off) return fail(RUDP_EINVAL, "rudp_decode_varlen_checked: frame_off is NULL");
   if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
     return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
-  {
+  if (d_status) {
     // every frame checks its own pair of offsets inside the decode kernels
     // (a valid batch is exactly one whose frames all pass); they or
-    // RUDP_ST_OFFSETS into the zeroed status word
+    // RUDP_ST_OFFSETS into the zeroed status word.  Without a status word the
+    // call is the one kernel: d_ok == RUDP_OK_BAD_OFFSETS marks the rejections.
     DeviceScope dev_scope;
     int rc = dev_scope.set(device);
     if (rc) return rc;
@@ -695,7 +698,7 @@ int rudp_decode_varlen_checked(const uint8_t* d_frames, uint64_t frames_bytes, c
   }
   if (n == 0) return 0;
   return decode_varlen(d_frames, d_frame_off, len_hint, n, d_csum_in_or_null, d_seq, d_ack, d_flags, d_ok,
-                       d_csum_out_or_null, nullptr, layout, device, hip_stream, d_status, frames_bytes);
+                       d_csum_out_or_null, nullptr, layout, device, hip_stream, true, d_status, frames_bytes);
 }
 
 int rudp_frame_off_check(const uint64_t* d_frame_off, uint64_t n, uint64_t frames_bytes, uint32_t* d_status,

@@ -111,10 +111,11 @@ struct VarlenArgs {
   const uint32_t* status;
   // Decode: frames reach at most frames_lim bytes into the buffer, and a frame
   // whose offsets are decreasing or past it is rejected (ok = RUDP_OK_BAD_OFFSETS,
-  // RUDP_ST_OFFSETS or'ed into *status_out, nothing read).  status_out null:
-  // an unchecked caller, the limit is frame_off[n].
+  // RUDP_ST_OFFSETS or'ed into *status_out when there is one, nothing read).
+  // lim_checked 0: an unchecked caller, the limit is frame_off[n].
   uint64_t frames_lim;
-  uint32_t* status_out;
+  uint32_t* status_out;           // may be null also for a checked call (the rejections are in ok[])
+  uint32_t lim_checked;           // decode: frames_lim bounds the frames (checked calls)
   uint64_t* trace;                // diagnostics (rudpx_encode_trace): small-frame encode timeline per tile
   uint32_t small_fpt;             // decode small-frame tile: frames per thread (0: not used)
   uint32_t small_cap;             // its LDS run budget in bytes

@@ -624,7 +624,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
 // Byte limit of a decode's frames: the caller's buffer size for checked
 // calls, else (unchecked callers) the last offset.
 __device__ __forceinline__ uint64_t frames_limit(const VarlenArgs& a) {
-  return a.status_out ? a.frames_lim : a.frame_off[a.n];
+  return a.lim_checked ? a.frames_lim : a.frame_off[a.n];
 }
 
 // A frame whose offsets are invalid: no byte of it is read.

@@ -19,7 +19,7 @@ LIB_PATH = Path(os.environ.get("RUDP_LIB") or Path(__file__).resolve().parent / 
 
 LAYOUT_RUDP5 = 5
 LAYOUT_RUDP7 = 7
-OK_BAD_CSUM, OK_GOOD, OK_SHORT, OK_UNVERIFIED = 0, 1, 2, 3
+OK_BAD_CSUM, OK_GOOD, OK_SHORT, OK_UNVERIFIED, OK_BAD_OFFSETS = 0, 1, 2, 3, 4
 EINVAL, ENOMEM, ENOTSUP, EHIP_BASE = -22, -12, -95, -1000
 ABI_VERSION = 4
 # status bits of the sync-free varlen calls (RUDP_ST_*)

@@ -23,6 +23,7 @@ Layouts:
 from __future__ import annotations
 
 import ctypes
+import threading
 from dataclasses import dataclass
 from typing import Any, NamedTuple, Optional, Tuple, Union
 
@@ -359,16 +360,165 @@ def synth_batch(n: int, payload_len: int, seed: int, *, first_index: int = 0, as
 
 
 # ------------------------------------------------------- variable-length batches
-class VarlenFrames(NamedTuple):
-    frames: Any      # u8 [frame_off[-1]] — frames back to back (or the caller's ``out``)
-    frame_off: Any   # int64 [N + 1] — frame i = frames[frame_off[i]:frame_off[i + 1]]
-    csum: Any        # u16 [N] or None
-    status: Any = None  # device u32[1], RUDP_ST_* of the call (0 = valid)
+class VarlenFrames:
+    """Result of ``pack_batch_varlen``: ``frames`` (u8, frames back to back, or
+    the caller's ``out``), ``frame_off`` (int64 [N + 1]: frame i =
+    frames[frame_off[i]:frame_off[i + 1]]), ``csum`` (u16 [N] or None) and
+    ``status`` (device int32 [1], RUDP_ST_* of the call, 0 = valid).
+
+    All of them live in one device allocation and are cut out of it on first
+    access, so a sync-free caller that only keeps the result pays for one
+    allocation and the launch.  Iterates as (frames, frame_off, csum, status).
+    """
+
+    __slots__ = ("_buf", "_n", "_cs_bytes", "_f_at", "_frames", "_frame_off", "_csum", "_status")
+
+    # one allocation: frame_off (i64 [n + 1]) | status (i32) | pad | csum (u16 [n]) |
+    # pad to 16 B | frames (unless the caller's)
+    def __init__(self, buf, n: int, cs_bytes: int, f_at: int, frames=None):
+        self._buf, self._n, self._cs_bytes, self._f_at = buf, n, cs_bytes, f_at
+        self._frames, self._frame_off, self._csum, self._status = frames, None, None, None
+
+    @staticmethod
+    def layout(n: int, want_csum: bool):
+        """(bytes before the frames, csum bytes): the allocation's head."""
+        cs_bytes = 2 * n if want_csum else 0
+        head = 8 * (n + 1) + 8 + cs_bytes
+        return head + (-head % 16), cs_bytes
+
+    @property
+    def frames(self):
+        if self._frames is None:
+            self._frames = self._buf[self._f_at:]
+        return self._frames
+
+    @property
+    def frame_off(self):
+        if self._frame_off is None:
+            import torch
+            self._frame_off = self._buf[:8 * (self._n + 1)].view(torch.int64)
+        return self._frame_off
+
+    @property
+    def status(self):
+        if self._status is None:
+            import torch
+            at = 8 * (self._n + 1)
+            self._status = self._buf[at:at + 4].view(torch.int32)
+        return self._status
+
+    @property
+    def csum(self):
+        if self._csum is None and self._cs_bytes:
+            import torch
+            at = 8 * (self._n + 1) + 8
+            self._csum = self._buf[at:at + self._cs_bytes].view(torch.uint16)
+        return self._csum
+
+    def __iter__(self):
+        return iter((self.frames, self.frame_off, self.csum, self.status))
+
+    def __getitem__(self, i):
+        return tuple(self)[i]
+
+    def __len__(self):
+        return 4
 
     def check(self) -> "VarlenFrames":
         """Raise ValueError if the device rejected the batch (one synchronization)."""
         _raise_status(self.status)
         return self
+
+
+class _RejectedFrames:
+    """Status of a sync-free variable-length decode, read from its ``ok`` array
+    on demand: RUDP_ST_OFFSETS when a frame was rejected for bad offsets
+    (ok == RUDP_OK_BAD_OFFSETS), else 0.  The decode keeps no status word of its
+    own, so a call is its one kernel (rudp_decode_varlen_checked, d_status NULL)."""
+
+    __slots__ = ("_ok",)
+
+    def __init__(self, ok):
+        self._ok = ok
+
+    def item(self) -> int:
+        return _native.ST_OFFSETS if bool((self._ok == _native.OK_BAD_OFFSETS).any()) else 0
+
+
+class VarlenDecoded:
+    """Result of ``unpack_batch_varlen``, with the fields of ``DecodedBatch``:
+    seq, ack (u16 [N]), flags, ok (u8 [N]), csum (u16 [N]), payload
+    (``PayloadSpans``) and status.  The five output arrays share one device
+    allocation and are cut out of it on first access.  Iterates as
+    (seq, ack, flags, ok, csum, payload, status)."""
+
+    __slots__ = ("_buf", "_n", "payload", "_v")
+
+    def __init__(self, buf, n: int, payload):
+        self._buf, self._n, self.payload, self._v = buf, n, payload, {}
+
+    # one allocation: seq | ack | csum (u16 [n] each) | flags | ok (u8 [n] each)
+    def _cut(self, name, at, nbytes, dtype):
+        v = self._v.get(name)
+        if v is None:
+            v = self._buf[at:at + nbytes]
+            if dtype is not None:
+                v = v.view(dtype)
+            self._v[name] = v
+        return v
+
+    @property
+    def seq(self):
+        import torch
+        return self._cut("seq", 0, 2 * self._n, torch.uint16)
+
+    @property
+    def ack(self):
+        import torch
+        return self._cut("ack", 2 * self._n, 2 * self._n, torch.uint16)
+
+    @property
+    def csum(self):
+        import torch
+        return self._cut("csum", 4 * self._n, 2 * self._n, torch.uint16)
+
+    @property
+    def flags(self):
+        return self._cut("flags", 6 * self._n, self._n, None)
+
+    @property
+    def ok(self):
+        return self._cut("ok", 7 * self._n, self._n, None)
+
+    @property
+    def status(self):
+        return _RejectedFrames(self.ok)
+
+    def __iter__(self):
+        return iter((self.seq, self.ack, self.flags, self.ok, self.csum, self.payload, self.status))
+
+    def __getitem__(self, i):
+        return tuple(self)[i]
+
+    def __len__(self):
+        return 7
+
+    def check(self) -> "VarlenDecoded":
+        """Raise ValueError if a frame was rejected for bad offsets (reads ok[]: one
+        device reduction and one synchronization)."""
+        _raise_status(self.status)
+        return self
+
+
+_tls = threading.local()
+
+
+def _batch_struct() -> "_native.RudpBatch":
+    """This thread's reusable struct rudp_batch (the C call only reads it during the call)."""
+    b = getattr(_tls, "batch", None)
+    if b is None:
+        b = _tls.batch = _native.RudpBatch()
+    return b
 
 
 def _int_tensor(t, name, device, n=None, dtypes=None):
@@ -383,7 +533,7 @@ def _int_tensor(t, name, device, n=None, dtypes=None):
 
 def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp7", *,
                       payload_off=None, want_csum: Optional[bool] = None, stream=None, out=None,
-                      check: bool = True) -> VarlenFrames:
+                      check: bool = True, reuse: Optional[VarlenFrames] = None) -> VarlenFrames:
     """Frame + checksum a variable-length batch on a HIP device.
 
     ``payload``: u8 1-D tensor holding the payload bytes; ``lengths``: int32
@@ -401,7 +551,9 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
     of at least sum(lengths) + N * header bytes (its first frame_off[-1] bytes
     are the frames).  Without ``out`` the frame buffer is sized on the host for
     packed payloads (payload.numel() + N * header bytes) and, for gathered
-    payloads, from one device read of the lengths' sum.
+    payloads, from one device read of the lengths' sum.  ``reuse``: an earlier
+    result of this call for the same N and csum choice, whose buffers take this
+    call's outputs (no allocation; the earlier result's contents are replaced).
     """
     import torch
     H = layout_header_len(layout)
@@ -446,30 +598,32 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
             raise ValueError("payload_off + lengths must stay inside payload")
     if want_csum is None:
         want_csum = H == 5
-    # one allocation: frame_off (i64 [n + 1]) | status (i32) | pad | csum (u16 [n]) |
-    # pad to 16 B | frames (unless the caller's), split by one call
-    cs_bytes = 2 * n if want_csum else 0
-    head = 8 * (n + 1) + 8 + cs_bytes
-    pad = -head % 16
-    f_bytes = 0 if frames is not None else lsum + n * H
-    frame_off, status, _, csum, _, fr = torch.empty(
-        (head + pad + f_bytes,), dtype=torch.uint8, device=dev).split_with_sizes(
-        (8 * (n + 1), 4, 4, cs_bytes, pad, f_bytes))
-    frame_off, status = frame_off.view(torch.int64), status.view(torch.int32)
-    csum = csum.view(torch.uint16) if want_csum else None
-    if frames is None:
-        frames = fr
+    f_at, cs_bytes = VarlenFrames.layout(n, want_csum)
+    if reuse is not None:
+        # the caller's earlier result of the same shape: its buffer takes this call's outputs
+        need = f_at + (0 if frames is not None else lsum + n * H)
+        if not isinstance(reuse, VarlenFrames) or reuse._n != n or reuse._cs_bytes != cs_bytes \
+                or reuse._buf.device != dev or reuse._buf.numel() != need:
+            raise ValueError("reuse= must be an earlier pack_batch_varlen result for the same N, "
+                             "csum choice, device and frame bytes (and out= or not, as then)")
+        buf = reuse._buf
+    else:
+        buf = torch.empty((f_at + (0 if frames is not None else lsum + n * H),), dtype=torch.uint8, device=dev)
+    base = buf.data_ptr()
+    f_ptr = frames.data_ptr() if frames is not None else base + f_at
+    f_cap = frames.numel() if frames is not None else buf.numel() - f_at
     # payload_len carries the mean payload length: a hint that picks lanes per packet
-    b = _native.RudpBatch(n=n, payload_len=min(lsum // n, 65535) if n else 0, reserved=0,
-                          seq=tab.seq.data_ptr(), ack=tab.ack.data_ptr(), flags=tab.flags.data_ptr(),
-                          payload=payload.data_ptr() if payload.numel() else 16,  # never read: all lengths 0
-                          len=lengths.data_ptr(),
-                          payload_off=payload_off.data_ptr() if payload_off is not None else None)
+    b = _batch_struct()
+    b.n, b.payload_len = n, min(lsum // n, 65535) if n else 0
+    b.seq, b.ack, b.flags = tab.seq.data_ptr(), tab.ack.data_ptr(), tab.flags.data_ptr()
+    b.payload = payload.data_ptr() if payload.numel() else 16  # never read: all lengths 0
+    b.len = lengths.data_ptr()
+    b.payload_off = payload_off.data_ptr() if payload_off is not None else None
     _native.check(_native.lib().rudp_encode_varlen_checked(
-        ctypes.byref(b), payload.numel(), frames.data_ptr() if frames.numel() else 16, frames.numel(),
-        frame_off.data_ptr(), csum.data_ptr() if csum is not None else None, status.data_ptr(), H,
+        ctypes.byref(b), payload.numel(), f_ptr if f_cap else 16, f_cap,
+        base, base + 8 * (n + 1) + 8 if cs_bytes else None, base + 8 * (n + 1), H,
         dev.index or 0, _stream_ptr(stream, dev)))
-    res = VarlenFrames(frames, frame_off, csum, status)
+    res = VarlenFrames(buf, n, cs_bytes, f_at, frames)
     return res.check() if check else res
 
 
@@ -488,15 +642,19 @@ def _check_offsets(frames, frame_off, stream=None) -> int:
 
 
 def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *, csum=None,
-                        stream=None, check: bool = True) -> DecodedBatch:
+                        stream=None, check: bool = True, reuse: Optional["VarlenDecoded"] = None
+                        ) -> "VarlenDecoded":
     """Parse + verify frames packed back to back (offsets as pack_batch_varlen returns).
 
     The payload is zero-copy: ``payload`` is the pair ``(start, end)`` of int64
     [N] tensors indexing ``frames`` (empty for frames shorter than the header),
     as a ``PayloadSpans`` that computes ``start`` on first use.  The offsets
     are checked on the device inside the call (rudp_decode_varlen_checked):
-    ``check=True`` waits and raises ValueError on bad offsets; ``check=False``
-    never waits, and the result's ``check()`` raises later.
+    every frame with bad offsets gets ok == RUDP_OK_BAD_OFFSETS, and
+    ``check=True`` waits and raises ValueError when there is one;
+    ``check=False`` never waits, and the result's ``check()`` raises later.
+    ``reuse``: an earlier result for the same N whose output buffer takes this
+    call's outputs (no allocation).
     """
     import torch
     H = layout_header_len(layout)
@@ -512,21 +670,24 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
         _dev_check(csum, "csum", torch.uint16, 1, dev)
         if csum.shape[0] != n:
             raise ValueError(f"csum has {csum.shape[0]} entries for {n} frames")
-    # one allocation for every output: seq | ack | csum (u16) | flags | ok (u8) |
-    # status (i32), split by one call (per-view Python slicing was most of the
+    # one allocation for every output: seq | ack | csum (u16) | flags | ok (u8), cut
+    # into views only when the caller reads them (per-view slicing was most of the
     # entry's host time at small batches)
-    u16 = torch.uint16
-    seq, ack, cs, flags, ok, status = torch.empty((8 * n + 4,), dtype=torch.uint8, device=dev).split_with_sizes(
-        (2 * n, 2 * n, 2 * n, n, n, 4))
-    seq, ack, cs, status = seq.view(u16), ack.view(u16), cs.view(u16), status.view(torch.int32)
+    if reuse is not None:
+        if not isinstance(reuse, VarlenDecoded) or reuse._n != n or reuse._buf.device != dev:
+            raise ValueError("reuse= must be an earlier unpack_batch_varlen result for the same N and device")
+        buf = reuse._buf
+    else:
+        buf = torch.empty((8 * n,), dtype=torch.uint8, device=dev)
+    base = buf.data_ptr()
     # mean frame length from the buffer size: a hint that picks lanes / tiles per frame
     hint = min(frames.numel() // n, 0xFFFFFFFF) if n else 0
+    # no status word: a rejected frame is ok == RUDP_OK_BAD_OFFSETS (check() reads that)
     _native.check(_native.lib().rudp_decode_varlen_checked(
         frames.data_ptr() if frames.numel() else 16, frames.numel(), frame_off.data_ptr(), hint, n,
-        csum.data_ptr() if csum is not None else None, seq.data_ptr(), ack.data_ptr(),
-        flags.data_ptr(), ok.data_ptr(), cs.data_ptr(), status.data_ptr(), H, dev.index or 0,
-        _stream_ptr(stream, dev)))
-    res = DecodedBatch(seq, ack, flags, ok, cs, PayloadSpans(frame_off, H), status)
+        csum.data_ptr() if csum is not None else None, base, base + 2 * n, base + 6 * n, base + 7 * n,
+        base + 4 * n, None, H, dev.index or 0, _stream_ptr(stream, dev)))
+    res = VarlenDecoded(buf, n, PayloadSpans(frame_off, H))
     return res.check() if check else res
 
 

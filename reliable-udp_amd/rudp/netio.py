@@ -122,7 +122,7 @@ class BatchReceiver:
     def decode(self, layout="rudp5", device=None, csum=None, stream=None, check=False):
         """H2D of the received frames, then parse + verify them on the device.
 
-        Returns ``(DecodedBatch, d_frames, d_frame_off)``; the device buffers are
+        Returns ``(VarlenDecoded, d_frames, d_frame_off)``; the device buffers are
         fresh (the caller owns them; the payload spans index ``d_frames``).
         ``check=True`` also waits for the device's offset check and raises on
         bad offsets (recvmmsg writes valid ones, so the default is not to wait).
@@ -148,6 +148,6 @@ class BatchReceiver:
         cur = torch.cuda.current_stream(self.device)
         cur.wait_stream(s)
         # allocated on `s`, used on the caller's stream from here on
-        for t in (d_frames, d_off, dec.seq, dec.ack, dec.flags, dec.ok, dec.csum, dec.status):
+        for t in (d_frames, d_off, dec._buf):  # the decode's outputs are views of one buffer
             t.record_stream(cur)
         return (dec.check() if check else dec), d_frames, d_off

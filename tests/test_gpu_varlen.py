@@ -9,7 +9,7 @@ import pytest
 
 from conftest import split_by_lengths
 from oracle import codec_np, synth
-from rudp import batch
+from rudp import _native, batch
 
 pytestmark = pytest.mark.gpu
 
@@ -902,3 +902,42 @@ def test_varlen_rank_shards_rebase_to_unsharded(cuda, world):
     assert np.array_equal(np.concatenate(frames), want) and np.array_equal(host(full.frames), want)
     assert np.array_equal(got_off, np.asarray(want_off)) and np.array_equal(host(full.frame_off), np.asarray(want_off))
     assert np.array_equal(np.concatenate(csums), want_cs)
+
+
+@pytest.mark.parametrize("L", [1, 300])
+def test_varlen_reuse_outputs_equal_fresh(cuda, L):
+    """reuse= hands an earlier result's buffers to the next call (no allocation):
+    the outputs equal a fresh call's and the oracle's; a mismatched shape is refused;
+    the decode's status (no status word) still reports a rejected frame."""
+    import torch
+    n = 5000
+    seq, ack, flags, pay = synth.synth(21, 0, n, L)
+    tab = (dev(seq, cuda), dev(ack, cuda), dev(flags, cuda))
+    lens = dev(np.full(n, L, np.int32), cuda)
+    flat = dev(pay.reshape(-1), cuda)
+    want_fr, want_off, want_cs = codec_np.encode_varlen(seq, ack, flags, [p.tobytes() for p in pay], 5)
+    first = batch.pack_batch_varlen(tab, flat, lens, 5, want_csum=True)
+    keep = first.frames.clone()
+    seq2, ack2, flags2, pay2 = synth.synth(22, 0, n, L)
+    tab2 = (dev(seq2, cuda), dev(ack2, cuda), dev(flags2, cuda))
+    again = batch.pack_batch_varlen(tab2, dev(pay2.reshape(-1), cuda), lens, 5, want_csum=True, reuse=first,
+                                    check=False).check()
+    assert again._buf.data_ptr() == first._buf.data_ptr()
+    want2, _, want_cs2 = codec_np.encode_varlen(seq2, ack2, flags2, [p.tobytes() for p in pay2], 5)
+    assert np.array_equal(host(again.frames), want2) and np.array_equal(host(again.csum), want_cs2)
+    assert np.array_equal(host(keep), want_fr) and np.array_equal(host(again.frame_off), want_off)
+    with pytest.raises(ValueError, match="reuse"):
+        batch.pack_batch_varlen(tab, flat, lens, 5, want_csum=False, reuse=again)
+    d1 = batch.unpack_batch_varlen(again.frames, again.frame_off, 5, csum=again.csum)
+    d2 = batch.unpack_batch_varlen(again.frames, again.frame_off, 5, csum=again.csum, reuse=d1, check=False)
+    assert d2._buf.data_ptr() == d1._buf.data_ptr()
+    want_d = codec_np.decode_varlen(want2, want_off, 5, want_cs2)
+    for got, exp in zip((d2.seq, d2.ack, d2.flags, d2.ok, d2.csum), want_d):
+        assert np.array_equal(host(got), exp)
+    bad = again.frame_off.clone()
+    bad[17] = bad[18] + 1
+    d3 = batch.unpack_batch_varlen(again.frames, bad, 5, csum=again.csum, reuse=d2, check=False)
+    assert int(d3.status.item()) == _native.ST_OFFSETS and int(d3.ok[16].item()) == _native.OK_BAD_OFFSETS
+    with pytest.raises(ValueError, match="non-decreasing"):
+        d3.check()
+    assert torch.equal(d3.ok[:16], torch.ones(16, dtype=torch.uint8, device=cuda))

@@ -4,6 +4,11 @@ usage: python tools/prof_summary.py --round r01 --tag encode_1Mx1472 \
           --kt gpurun_out/prof_kt --fetch gpurun_out/prof_fetch --write gpurun_out/prof_write \
           --kernel encode_tile_kernel --n 1048576 --L 1472 --alg-bytes-per-unit 2956
 
+--kernel takes a comma-separated list for a call that is a chain of launches
+(e.g. the varlen encode: scan passes + tile kernel): the summary's avg_us is
+then the sum of the kernels' averages (each runs once per call) and the HBM
+bytes the sum of their medians; per-kernel entries are listed under "chain".
+
 Writes profiles/<round>/<tag>_kernel_stats.csv (the rocprofv3 --stats table),
 profiles/<round>/<tag>_summary.json, and (with --pmc-out) the per-launch HBM
 traffic bench.py reads.  HBM bytes follow MI355X_MICROARCH.md §HBM: FETCH_SIZE
@@ -65,25 +70,35 @@ def main():
     out_dir = REPO / "profiles" / args.round
     out_dir.mkdir(parents=True, exist_ok=True)
     shutil.copy(_one(args.kt, "kernel_stats.csv"), out_dir / f"{args.tag}_kernel_stats.csv")
-    st = kernel_stats(args.kt, args.kernel)
+    names = [k for k in args.kernel.split(",") if k]
+    stats = [kernel_stats(args.kt, k) for k in names]
+    avg_ns = sum(st["avg_ns"] for st in stats)
     alg = args.n * args.alg_bytes_per_unit
     summary = {
-        "kernel": st["name"], "calls": st["calls"], "avg_us": st["avg_ns"] / 1e3,
-        "min_us": st["min_ns"] / 1e3, "max_us": st["max_ns"] / 1e3,
+        "kernel": stats[0]["name"], "calls": stats[0]["calls"], "avg_us": avg_ns / 1e3,
+        "min_us": sum(st["min_ns"] for st in stats) / 1e3, "max_us": sum(st["max_ns"] for st in stats) / 1e3,
         "units_per_launch": args.n, "payload_bytes": args.L,
         "algorithmic_bytes_per_unit": args.alg_bytes_per_unit,
         "algorithmic_bytes_per_launch": alg,
-        "achieved_GBs_at_avg": alg / (st["avg_ns"] * 1e-9) / 1e9,
+        "achieved_GBs_at_avg": alg / (avg_ns * 1e-9) / 1e9,
         "hbm_peak_GBs": 8000.0,
     }
+    if len(stats) > 1:
+        summary["chain"] = [{"kernel": st["name"], "calls": st["calls"], "avg_us": st["avg_ns"] / 1e3}
+                            for st in stats]
+        summary["chain_note"] = "avg_us/min_us/max_us are sums over the chain's kernels (one launch each per call)"
     summary["roofline_frac_at_avg"] = summary["achieved_GBs_at_avg"] / 8000.0
     if args.fetch and args.write:
-        fetch = counter_values(args.fetch, args.kernel, "FETCH_SIZE")
-        write = counter_values(args.write, args.kernel, "WRITE_SIZE")
-        rd = statistics.median(fetch) * 1024 * 2   # KiB; x2 gfx950 FETCH_SIZE correction
-        wr = statistics.median(write) * 1024
+        rd = wr = 0.0
+        nf = nw = 0
+        for k, st in zip(names, stats):
+            fetch = counter_values(args.fetch, k, "FETCH_SIZE")
+            write = counter_values(args.write, k, "WRITE_SIZE")
+            rd += statistics.median(fetch) * 1024 * 2   # KiB; x2 gfx950 FETCH_SIZE correction
+            wr += statistics.median(write) * 1024
+            nf, nw = nf + len(fetch), nw + len(write)
         summary.update({
-            "pmc_launches": [len(fetch), len(write)],
+            "pmc_launches": [nf, nw],
             "hbm_read_bytes_per_launch": rd, "hbm_write_bytes_per_launch": wr,
             "hbm_bytes_per_launch": rd + wr,
             "traffic_over_algorithmic": (rd + wr) / alg,
@@ -92,7 +107,7 @@ def main():
         })
         if args.pmc_out:
             args.pmc_out.write_text(json.dumps({
-                "L": args.L, "n": args.n, "kernel": st["name"],
+                "L": args.L, "n": args.n, "kernel": stats[0]["name"],
                 "hbm_bytes_per_launch": rd + wr, "source": f"profiles/{args.round}/{args.tag}_summary.json",
             }, indent=1) + "\n")
     (out_dir / f"{args.tag}_summary.json").write_text(json.dumps(summary, indent=1) + "\n")

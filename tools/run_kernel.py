@@ -1,6 +1,7 @@
 """Run one codec op repeatedly on one shape, for rocprofv3 captures.
 
-usage: python tools/run_kernel.py --op encode|decode|roundtrip [--L 1472] [--n 1048576]
+usage: python tools/run_kernel.py --op encode|decode|roundtrip|encode_varlen|decode_varlen|utf8|dedup
+          [--L 1472] [--n 1048576]
           [--layout rudp7] [--steps 20] [--ragged] [--tune 51=1,52=2]
 Prints the HIP-event time per launch so it can be set beside the profiler's
 kernel-trace average.
@@ -25,7 +26,10 @@ from rudp import batch  # noqa: E402
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--op", choices=["encode", "decode", "decode_copy", "roundtrip", "encode_varlen",
-                                     "decode_varlen"], default="encode")
+                                     "decode_varlen", "utf8", "dedup"], default="encode",
+                    help="utf8: strict UTF-8 check of the fixed-stride frames (bench leg "
+                         "utf8_validate_1Mx1472); dedup: the proxy's 500-deep retransmission check "
+                         "over packed frames of L-byte payloads (bench leg proxy_dedup_1M_window500, L = 1)")
     ap.add_argument("--L", type=int, default=1472)
     ap.add_argument("--n", type=int, default=1 << 20)
     ap.add_argument("--layout", default="rudp7")
@@ -65,7 +69,7 @@ def main():
     del ctypes
 
     vsets = []
-    if args.op.endswith("varlen"):
+    if args.op.endswith("varlen") or args.op == "dedup":
         for tab, pay, fr in sets:
             if args.ragged:
                 g = torch.Generator(device=dev).manual_seed(7)
@@ -76,7 +80,7 @@ def main():
             else:
                 lens = torch.full((args.n,), args.L, dtype=torch.int32, device=dev)
                 flat = pay.view(-1)
-            res = batch.pack_batch_varlen(tab, flat, lens, args.layout)
+            res = batch.pack_batch_varlen(tab, flat, lens, "rudp5" if args.op == "dedup" else args.layout)
             vsets.append((tab, flat, lens, res.frames, res.frame_off))
 
     def step(i):
@@ -84,6 +88,8 @@ def main():
             tab, flat, lens, vfr, voff = vsets[i % nsets]
             if args.op == "encode_varlen":
                 batch.pack_batch_varlen(tab, flat, lens, args.layout)
+            elif args.op == "dedup":
+                batch.detect_retransmissions(vfr, frame_off=voff, window=500)
             else:
                 batch.unpack_batch_varlen(vfr, voff, args.layout)
             return
@@ -94,6 +100,8 @@ def main():
             batch.unpack_batch(fr, args.layout)
         if args.op == "decode_copy":
             decode_copy(tab, pay, fr)
+        if args.op == "utf8":
+            batch.validate_utf8(fr, args.layout)
 
     for i in range(3):
         step(i)

@@ -15,9 +15,12 @@ From one traced launch per shape this prints:
                      a one-lane kernel stamps the wall clock on the stream just
                      before and just after the traced launch: the launch's time
                      outside its tiles (plus two kernel boundaries)
-Shapes: the headline (1M x 1472 B in buffers of its own) and a 16M launch.
+Shapes: the headline (1M x 1472 B in buffers of its own) and a 16M launch;
+any --L (tiles of T packets as encode_tile_geometry picks them: 16 from 512 B,
+128 at 64 B).  --sets K rotates K buffer sets (as the bench does below 1 GiB
+per set, so the traced launch does not find its inputs in the Infinity Cache).
 
-usage: python tools/tile_timeline.py [--L 1472] [--no-16m]
+usage: python tools/tile_timeline.py [--L 1472] [--no-16m] [--sets 8]
 """
 from __future__ import annotations
 
@@ -89,6 +92,8 @@ def main():
     ap.add_argument("--save", default="", help="directory for the raw 1M traces (.npy)")
     ap.add_argument("--percu", default="", help="also trace 1M under these tiles-per-CU caps (rudpx_tune 6)")
     ap.add_argument("--early", action="store_true", help="also trace 1M with the header-table loads before phase 1 (rudpx_tune 30)")
+    ap.add_argument("--sets", type=int, default=1, help="rotating buffer sets (the traced launch uses the next one)")
+    ap.add_argument("--tune", default="", help="rudpx_tune knobs for every shape, key=value[,key=value]")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
     lib = _native.lib()
@@ -105,14 +110,26 @@ def main():
         shapes["own_1M_early_table"] = (M, -1)
     if not args.no_16m:
         shapes["launch_16M"] = (16 * M, -1)
-    out = {}
+    for kv in filter(None, args.tune.split(",")):
+        k, v = kv.split("=")
+        lib.rudpx_tune(int(k), int(v))
+    # packets per tile, as encode_tile_geometry (capi.hip) picks them
+    T = 16
+    while T * 2 <= min(8192 // L, 256):
+        T *= 2
+    out = {"L": L, "packets_per_tile": T, "buffer_sets": args.sets, "tune": args.tune}
     for name, (n, percu) in shapes.items():
         lib.rudpx_tune(6, percu)
         lib.rudpx_tune(30, 1 if name.endswith("early_table") else -1)
-        tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
-        fr = torch.empty((n, L + 7), dtype=torch.uint8, device=dev)
+        sets = []
+        for _ in range(args.sets if n == M else 1):
+            tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
+            sets.append((tab, pay, torch.empty((n, L + 7), dtype=torch.uint8, device=dev)))
+        cur = [0]
 
         def enc():
+            tab, pay, fr = sets[cur[0] % len(sets)]
+            cur[0] += 1
             batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
         for _ in range(3):
             enc()
@@ -124,7 +141,7 @@ def main():
             b.record()
             b.synchronize()
             ts.append(a.elapsed_time(b))
-        tiles = (n + 15) // 16  # T = 16 at L >= 512
+        tiles = (n + T - 1) // T
         buf = torch.zeros((tiles * 6,), dtype=torch.int64, device=dev)
         res = {"untraced_ms": statistics.median(ts)}
         runs = []
@@ -139,7 +156,7 @@ def main():
             torch.cuda.synchronize()
             rec = buf.view(-1, 6).cpu().numpy()
             if (rec[:, 1] == 0).any():
-                raise RuntimeError("trace incomplete: tile geometry is not T = 16")
+                raise RuntimeError(f"trace incomplete: tile geometry is not T = {T}")
             r = analyse(rec)
             if args.save and n == M:
                 np.save(Path(args.save) / f"tile_trace_{name}_{k}.npy", rec)
@@ -149,7 +166,7 @@ def main():
             runs.append(r)
         res["traced"] = runs
         out[name] = res
-        del tab, pay, fr, buf
+        del sets, buf
         torch.cuda.empty_cache()
         print(f"{name} done", file=sys.stderr, flush=True)
     lib.rudpx_tune(6, -1)
