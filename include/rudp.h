@@ -44,7 +44,7 @@
 extern "C" {
 #endif
 
-#define RUDP_ABI_VERSION 4
+#define RUDP_ABI_VERSION 5
 
 /* Frame layouts: the value is the header length in bytes. */
 #define RUDP_LAYOUT_RUDP5 5 /* reference-exact 5-byte header, checksum sideband */
@@ -166,7 +166,10 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
  *   payload_bytes.  d_frame_off[n] is always written; d_frame_off[0..n-1]
  *   when the batch is valid (status 0).
  * rudp_decode_varlen_checked: rudp_decode with offsets (zero-copy payload);
- *   frame_off[0..n] must be non-decreasing and <= frames_bytes.
+ *   frame_off[0..n] must be non-decreasing and <= frames_bytes.  d_status may
+ *   be NULL (ABI 5): the call is then its one decode kernel, and the rejected
+ *   frames are exactly those with d_ok == RUDP_OK_BAD_OFFSETS; with a status
+ *   word the call zeroes it first (one more stream operation).
  * rudp_frame_off_check: only the offset check, for callers that run their own
  *   kernels on the frames afterwards.
  */
@@ -242,6 +245,21 @@ int rudp_udp_recv_batch(int fd, uint8_t* h_frames, uint64_t cap_bytes, uint32_t 
                         uint32_t max_msgs, uint64_t* h_frame_off, int timeout_ms);
 int rudp_udp_send_batch(int fd, const uint8_t* h_frames, const uint64_t* h_frame_off, uint64_t n,
                         const char* ip, uint16_t port);
+
+/*
+ * The same for a relay in the reference proxy's role, which forwards every
+ * datagram by its source address (proxy.py:129-145) over one socket.  An
+ * IPv4 endpoint travels as one integer: address (host byte order) << 16 | port.
+ * rudp_udp_recv_batch_from: as rudp_udp_recv_batch, and h_src_or_null[i]
+ *   receives datagram i's source (0 for a non-IPv4 source).
+ * rudp_udp_send_batch_to: sends frame i to h_dst[i] (per_datagram != 0) or
+ *   every frame to h_dst[0].  Returns the count sent or a negative errno.
+ */
+int rudp_udp_recv_batch_from(int fd, uint8_t* h_frames, uint64_t cap_bytes, uint32_t slot_bytes,
+                             uint32_t max_msgs, uint64_t* h_frame_off, uint64_t* h_src_or_null,
+                             int timeout_ms);
+int rudp_udp_send_batch_to(int fd, const uint8_t* h_frames, const uint64_t* h_frame_off, uint64_t n,
+                           const uint64_t* h_dst, int per_datagram);
 
 /*
  * Host-memory conveniences: same semantics, host pointers in and out.

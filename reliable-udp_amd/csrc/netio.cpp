@@ -24,11 +24,13 @@ constexpr unsigned kMaxVec = 1024;  // datagrams per recvmmsg/sendmmsg call
 
 thread_local std::vector<mmsghdr> t_msgs;
 thread_local std::vector<iovec> t_iov;
+thread_local std::vector<sockaddr_in> t_names;
 
 void reserve(unsigned n) {
   if (t_msgs.size() < n) {
     t_msgs.resize(n);
     t_iov.resize(n);
+    t_names.resize(n);
   }
 }
 
@@ -36,8 +38,29 @@ void reserve(unsigned n) {
 
 extern "C" {
 
+// Source / destination of a datagram as one integer: IPv4 address (host byte
+// order) << 16 | port.
+static uint64_t addr_key(const sockaddr_in& a) {
+  return ((uint64_t)ntohl(a.sin_addr.s_addr) << 16) | ntohs(a.sin_port);
+}
+
+static sockaddr_in key_addr(uint64_t k) {
+  sockaddr_in a{};
+  a.sin_family = AF_INET;
+  a.sin_port = htons((uint16_t)(k & 0xFFFFu));
+  a.sin_addr.s_addr = htonl((uint32_t)(k >> 16));
+  return a;
+}
+
 int rudp_udp_recv_batch(int fd, uint8_t* h_frames, uint64_t cap_bytes, uint32_t slot_bytes,
                         uint32_t max_msgs, uint64_t* h_frame_off, int timeout_ms) {
+  return rudp_udp_recv_batch_from(fd, h_frames, cap_bytes, slot_bytes, max_msgs, h_frame_off, nullptr,
+                                  timeout_ms);
+}
+
+int rudp_udp_recv_batch_from(int fd, uint8_t* h_frames, uint64_t cap_bytes, uint32_t slot_bytes,
+                             uint32_t max_msgs, uint64_t* h_frame_off, uint64_t* h_src_or_null,
+                             int timeout_ms) {
   if (fd < 0 || !h_frames || !h_frame_off || slot_bytes == 0) return RUDP_EINVAL;
   uint64_t want = cap_bytes / slot_bytes;
   if (want > max_msgs) want = max_msgs;
@@ -65,6 +88,11 @@ int rudp_udp_recv_batch(int fd, uint8_t* h_frames, uint64_t cap_bytes, uint32_t 
       memset(&t_msgs[i], 0, sizeof(mmsghdr));
       t_msgs[i].msg_hdr.msg_iov = &t_iov[i];
       t_msgs[i].msg_hdr.msg_iovlen = 1;
+      if (h_src_or_null) {
+        t_names[i] = sockaddr_in{};
+        t_msgs[i].msg_hdr.msg_name = &t_names[i];
+        t_msgs[i].msg_hdr.msg_namelen = sizeof(sockaddr_in);
+      }
     }
     int r;
     do {
@@ -81,6 +109,8 @@ int rudp_udp_recv_batch(int fd, uint8_t* h_frames, uint64_t cap_bytes, uint32_t 
       if (h_frames + packed != src) memmove(h_frames + packed, src, len);
       packed += len;
       h_frame_off[got + i + 1] = packed;
+      if (h_src_or_null)
+        h_src_or_null[got + i] = t_names[i].sin_family == AF_INET ? addr_key(t_names[i]) : 0;
     }
     got += (uint64_t)r;
     if ((unsigned)r < chunk) break;  // socket drained
@@ -90,11 +120,18 @@ int rudp_udp_recv_batch(int fd, uint8_t* h_frames, uint64_t cap_bytes, uint32_t 
 
 int rudp_udp_send_batch(int fd, const uint8_t* h_frames, const uint64_t* h_frame_off, uint64_t n,
                         const char* ip, uint16_t port) {
-  if (fd < 0 || (n && (!h_frames || !h_frame_off)) || !ip) return RUDP_EINVAL;
+  if (!ip) return RUDP_EINVAL;
   sockaddr_in dst{};
   dst.sin_family = AF_INET;
   dst.sin_port = htons(port);
   if (inet_pton(AF_INET, ip, &dst.sin_addr) != 1) return RUDP_EINVAL;
+  const uint64_t key = addr_key(dst);
+  return rudp_udp_send_batch_to(fd, h_frames, h_frame_off, n, &key, 0);
+}
+
+int rudp_udp_send_batch_to(int fd, const uint8_t* h_frames, const uint64_t* h_frame_off, uint64_t n,
+                           const uint64_t* h_dst, int per_datagram) {
+  if (fd < 0 || (n && (!h_frames || !h_frame_off)) || !h_dst) return RUDP_EINVAL;
   uint64_t sent = 0;
   while (sent < n) {
     const unsigned chunk = (unsigned)((n - sent) < kMaxVec ? (n - sent) : kMaxVec);
@@ -104,8 +141,9 @@ int rudp_udp_send_batch(int fd, const uint8_t* h_frames, const uint64_t* h_frame
       t_iov[i].iov_base = const_cast<uint8_t*>(h_frames + h_frame_off[k]);
       t_iov[i].iov_len = h_frame_off[k + 1] - h_frame_off[k];
       memset(&t_msgs[i], 0, sizeof(mmsghdr));
-      t_msgs[i].msg_hdr.msg_name = &dst;
-      t_msgs[i].msg_hdr.msg_namelen = sizeof dst;
+      t_names[i] = key_addr(h_dst[per_datagram ? k : 0]);
+      t_msgs[i].msg_hdr.msg_name = &t_names[i];
+      t_msgs[i].msg_hdr.msg_namelen = sizeof(sockaddr_in);
       t_msgs[i].msg_hdr.msg_iov = &t_iov[i];
       t_msgs[i].msg_hdr.msg_iovlen = 1;
     }

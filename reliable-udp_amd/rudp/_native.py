@@ -21,7 +21,7 @@ LAYOUT_RUDP5 = 5
 LAYOUT_RUDP7 = 7
 OK_BAD_CSUM, OK_GOOD, OK_SHORT, OK_UNVERIFIED, OK_BAD_OFFSETS = 0, 1, 2, 3, 4
 EINVAL, ENOMEM, ENOTSUP, EHIP_BASE = -22, -12, -95, -1000
-ABI_VERSION = 4
+ABI_VERSION = 5
 # status bits of the sync-free varlen calls (RUDP_ST_*)
 ST_LEN, ST_PAYLOAD, ST_FRAMES_CAP, ST_OFFSETS = 1, 2, 4, 8
 
@@ -32,6 +32,7 @@ EXPORTS = (
     "rudp_encode_varlen", "rudp_validate_utf8", "rudp_dedup_window",
     "rudp_udp_recv_batch", "rudp_udp_send_batch", "rudp_varlen_bounds", "rudp_frame_off_bounds",
     "rudp_encode_varlen_checked", "rudp_decode_varlen_checked", "rudp_frame_off_check",
+    "rudp_udp_recv_batch_from", "rudp_udp_send_batch_to",
 )
 
 
@@ -73,6 +74,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rudp_dedup_window": [P, P, U32, U64, U32, P, I, P],
         "rudp_udp_recv_batch": [I, P, U64, U32, U32, P, I],
         "rudp_udp_send_batch": [I, P, P, U64, ctypes.c_char_p, ctypes.c_uint16],
+        "rudp_udp_recv_batch_from": [I, P, U64, U32, U32, P, P, I],
+        "rudp_udp_send_batch_to": [I, P, P, U64, P, I],
         "rudp_varlen_bounds": [P, P, U64, P, I, P],
         "rudp_frame_off_bounds": [P, U64, P, I, P],
         "rudp_encode_varlen_checked": [ctypes.POINTER(RudpBatch), U64, P, U64, P, P, P, I, I, P],

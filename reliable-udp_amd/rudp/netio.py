@@ -27,12 +27,25 @@ def _np_ptr(a) -> int:
     return a.ctypes.data
 
 
+def addr_key(ip: str, port: int) -> int:
+    """An IPv4 endpoint as the one integer the batched socket calls use:
+    address (host byte order) << 16 | port."""
+    return int.from_bytes(_socket.inet_aton(ip), "big") << 16 | port
+
+
+def key_addr(key: int):
+    """(ip, port) of an ``addr_key``."""
+    return _socket.inet_ntoa(int(key >> 16).to_bytes(4, "big")), int(key & 0xFFFF)
+
+
 def recv_batch(sock: _socket.socket, frames: np.ndarray, frame_off: np.ndarray, *,
-               slot_bytes: int = 1024, max_msgs: int | None = None, timeout_ms: int = -1) -> int:
+               slot_bytes: int = 1024, max_msgs: int | None = None, timeout_ms: int = -1,
+               sources: np.ndarray | None = None) -> int:
     """Receive up to ``max_msgs`` datagrams into ``frames`` (u8, packed) and
     ``frame_off`` (int64, count + 1).  Datagrams longer than ``slot_bytes`` are
-    truncated, as recvfrom(1024) truncates in the reference.  Returns the count
-    (0 on timeout)."""
+    truncated, as recvfrom(1024) truncates in the reference.  ``sources``
+    (u64, optional) receives each datagram's source as an ``addr_key``.
+    Returns the count (0 on timeout)."""
     if frames.dtype != np.uint8 or frames.ndim != 1 or not frames.flags["C_CONTIGUOUS"]:
         raise TypeError("frames must be a contiguous 1-D uint8 array")
     if frame_off.dtype != np.int64 or frame_off.ndim != 1 or not frame_off.flags["C_CONTIGUOUS"]:
@@ -41,8 +54,15 @@ def recv_batch(sock: _socket.socket, frames: np.ndarray, frame_off: np.ndarray, 
     max_msgs = cap_msgs if max_msgs is None else min(max_msgs, cap_msgs)
     if max_msgs < 0:
         raise ValueError("frame_off needs at least one entry")
-    rc = _native.lib().rudp_udp_recv_batch(sock.fileno(), _np_ptr(frames), frames.nbytes,
-                                           slot_bytes, max_msgs, _np_ptr(frame_off), timeout_ms)
+    src_ptr = None
+    if sources is not None:
+        if sources.dtype != np.uint64 or sources.ndim != 1 or not sources.flags["C_CONTIGUOUS"]:
+            raise TypeError("sources must be a contiguous 1-D uint64 array")
+        max_msgs = min(max_msgs, sources.shape[0])
+        src_ptr = _np_ptr(sources)
+    rc = _native.lib().rudp_udp_recv_batch_from(sock.fileno(), _np_ptr(frames), frames.nbytes,
+                                                slot_bytes, max_msgs, _np_ptr(frame_off), src_ptr,
+                                                timeout_ms)
     if rc < 0:
         raise OSError(-rc, f"recvmmsg: {rc}")
     return rc
@@ -58,6 +78,25 @@ def send_batch(sock: _socket.socket, frames: np.ndarray, frame_off: np.ndarray, 
         raise ValueError("frame_off must be non-decreasing offsets inside frames")
     rc = _native.lib().rudp_udp_send_batch(sock.fileno(), _np_ptr(frames) if frames.size else None,
                                            _np_ptr(frame_off), max(n, 0), ip.encode(), port)
+    if rc < 0:
+        raise OSError(-rc, f"sendmmsg: {rc}")
+    return rc
+
+
+def send_batch_to(sock: _socket.socket, frames: np.ndarray, frame_off: np.ndarray, dst: np.ndarray) -> int:
+    """Send frame i to ``dst[i]`` (u64 ``addr_key`` per datagram); returns the count sent."""
+    frames = np.ascontiguousarray(frames, dtype=np.uint8)
+    frame_off = np.ascontiguousarray(frame_off, dtype=np.int64)
+    dst = np.ascontiguousarray(dst, dtype=np.uint64)
+    n = frame_off.shape[0] - 1
+    if dst.shape[0] < n:
+        raise ValueError(f"dst has {dst.shape[0]} entries for {n} frames")
+    if n > 0 and (frame_off[0] < 0 or frame_off[-1] > frames.nbytes or (np.diff(frame_off) < 0).any()):
+        raise ValueError("frame_off must be non-decreasing offsets inside frames")
+    if n <= 0:
+        return 0
+    rc = _native.lib().rudp_udp_send_batch_to(sock.fileno(), _np_ptr(frames) if frames.size else None,
+                                              _np_ptr(frame_off), n, _np_ptr(dst), 1)
     if rc < 0:
         raise OSError(-rc, f"sendmmsg: {rc}")
     return rc
@@ -81,7 +120,7 @@ class BatchReceiver:
     """
 
     def __init__(self, sock: _socket.socket, max_msgs: int = 65536, slot_bytes: int = 1024,
-                 slots: int = 3, device=None, stream=None):
+                 slots: int = 3, device=None, stream=None, with_sources: bool = False):
         import torch
         if slots < 1:
             raise ValueError("slots must be >= 1")
@@ -93,6 +132,8 @@ class BatchReceiver:
         self._frames_t = [torch.empty((max_msgs * slot_bytes,), dtype=torch.uint8, pin_memory=True)
                           for _ in range(slots)]
         self._off_t = [torch.empty((max_msgs + 1,), dtype=torch.int64, pin_memory=True) for _ in range(slots)]
+        # each datagram's source (addr_key), for callers that route by it (the relay)
+        self._src = [np.empty((max_msgs,), dtype=np.uint64) for _ in range(slots)] if with_sources else None
         self._copied = [None] * slots   # event behind the last H2D copy out of each slot
         self._slot = -1
         self.count = 0
@@ -106,6 +147,13 @@ class BatchReceiver:
     def frame_off(self) -> np.ndarray:
         return self._off_t[self._slot].numpy()
 
+    @property
+    def sources(self) -> np.ndarray:
+        """Sources (addr_key) of the datagrams the last recv() took (with_sources=True)."""
+        if self._src is None:
+            raise RuntimeError("BatchReceiver(with_sources=True) keeps the sources")
+        return self._src[self._slot][:self.count]
+
     def recv(self, timeout_ms: int = -1) -> int:
         k = (self._slot + 1) % len(self._frames_t)
         if self._copied[k] is not None:
@@ -113,7 +161,8 @@ class BatchReceiver:
             self._copied[k] = None
         self._slot = k
         self.count = recv_batch(self.sock, self._frames_t[k].numpy(), self._off_t[k].numpy(),
-                                slot_bytes=self.slot_bytes, max_msgs=self.max_msgs, timeout_ms=timeout_ms)
+                                slot_bytes=self.slot_bytes, max_msgs=self.max_msgs, timeout_ms=timeout_ms,
+                                sources=self._src[k] if self._src is not None else None)
         return self.count
 
     def frame(self, i: int) -> bytes:

@@ -14,6 +14,15 @@ multiset of keys: two datagrams are Packet-equal (same get_hex(), i.e. same
 bit string) exactly when their bytes are equal, except that an empty datagram
 parses as the 40-bit zero header (utils/packet.py:16) and so equals five zero
 bytes.  O(1) per datagram instead of up to 500 __eq__ calls.
+
+``Relay(..., batched=True)`` is the batched form:
+every recvmmsg takes up to ``max_msgs`` datagrams with their source addresses
+(rudp_udp_recv_batch_from); the retransmission flags of the whole batch come
+from one GPU launch of rudp_dedup_window over the last MAX_MEMORY datagrams
+of the earlier batches followed by this batch (the history carried across
+batches), and the datagrams that are not dropped leave in one sendmmsg with
+per-datagram destinations (rudp_udp_send_batch_to).  Same forwarding, log and
+counters as the per-datagram loop.
 """
 from __future__ import annotations
 
@@ -22,7 +31,10 @@ import threading
 from collections import Counter, deque
 from typing import Callable, Dict, List
 
+import numpy as np
+
 MAX_MEMORY = 500  # proxy.py:17
+SLOT_BYTES = 1024  # recvfrom(1024), proxy.py:129
 
 
 class Relay(threading.Thread):
@@ -34,7 +46,7 @@ class Relay(threading.Thread):
     """
 
     def __init__(self, server_port: int, drop: Callable[[str, int], bool] = lambda d, i: False,
-                 host: str = "127.0.0.1"):
+                 host: str = "127.0.0.1", batched: bool = False, device=None, max_msgs: int = 1024):
         super().__init__(daemon=True)
         self.sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
         self.sock.bind((host, 0))
@@ -49,6 +61,18 @@ class Relay(threading.Thread):
         self._history: deque = deque()
         self._seen: Counter = Counter()
         self.stop_event = threading.Event()
+        self.batched = batched
+        self.batches = 0
+        if batched:
+            import torch
+            self._device = torch.device(device) if device is not None else torch.device("cuda", 0)
+            self._max_msgs = max_msgs
+            from .netio import addr_key
+            self._server_key = addr_key(host, server_port)
+            self._client_key = None
+            # the last MAX_MEMORY datagrams (both directions), packed, for the next batch's check
+            self._hist_frames = np.zeros(0, np.uint8)
+            self._hist_off = np.zeros(1, np.int64)
 
     @property
     def retransmitted(self) -> int:
@@ -68,7 +92,80 @@ class Relay(threading.Thread):
             old = self._history.popleft()
             self._seen[old] -= 1
 
+    def _dup_flags(self, frames: np.ndarray, off: np.ndarray) -> np.ndarray:
+        """Retransmission flags of a batch (frames[off[i]:off[i+1]], i < k) against the
+        carried history and the batch's own earlier datagrams: one GPU launch of the
+        proxy's `Packet(data) in self.packets` (proxy.py:90), window MAX_MEMORY."""
+        import torch
+        from . import batch
+        k = off.shape[0] - 1
+        h = self._hist_off.shape[0] - 1
+        body = frames[off[0]:off[k]]
+        # one spare byte keeps the buffer non-empty when every datagram is empty
+        allf = np.concatenate([self._hist_frames, body, np.zeros(1, np.uint8)])
+        allo = np.concatenate([self._hist_off, self._hist_off[-1] + (off[1:] - off[0])])
+        d_frames = torch.from_numpy(allf).to(self._device)
+        d_off = torch.from_numpy(allo).to(self._device)
+        dup = batch.detect_retransmissions(d_frames, frame_off=d_off, window=MAX_MEMORY).cpu().numpy()[h:]
+        # carry the last MAX_MEMORY datagrams into the next batch
+        keep = min(MAX_MEMORY, h + k)
+        first = h + k - keep
+        self._hist_frames = allf[allo[first]:allo[-1]].copy()
+        self._hist_off = allo[first:] - allo[first]
+        return dup.astype(bool)
+
+    def _relay_batch(self, frames: np.ndarray, off: np.ndarray, src: np.ndarray) -> None:
+        """Record and forward one received batch (the per-datagram loop's work, batched)."""
+        from . import netio
+        k = off.shape[0] - 1
+        dst = np.zeros(k, np.uint64)
+        dropped = np.zeros(k, bool)
+        from_server = src == self._server_key
+        for i in range(k):
+            data = frames[off[i]:off[i + 1]].tobytes()
+            if from_server[i]:
+                direction = "s2c"
+            else:
+                direction = "c2s"
+                self.client = netio.key_addr(int(src[i]))
+                self._client_key = int(src[i])
+            index = len(self.log[direction])
+            self.log[direction].append(data)
+            dropped[i] = bool(self.drop(direction, index))
+            # a server datagram before any client one has nowhere to go (dst 0: not sent)
+            dst[i] = self._server_key if not from_server[i] else (self._client_key or 0)
+        dup = self._dup_flags(frames, off)
+        # proxy.py:79-94, summed over the batch
+        for side, m in (("server", from_server), ("client", ~from_server)):
+            other = "client" if side == "server" else "server"
+            self.stats[f"{side}_sent"] += int(m.sum())
+            self.stats[f"{side}_dropped"] += int((m & dropped).sum())
+            self.stats[f"{other}_received"] += int((m & ~dropped).sum())
+            self.stats[f"{side}_retransmitted"] += int((m & dup).sum())
+        send = ~dropped & (dst != 0)
+        if send.any():
+            lens = np.diff(off)
+            body = frames[off[0]:off[k]]
+            out = body[np.repeat(send, lens)] if body.size else body
+            out_off = np.concatenate([[0], np.cumsum(lens[send])]).astype(np.int64)
+            netio.send_batch_to(self.sock, out, out_off, dst[send])
+        self.batches += 1
+
+    def _run_batched(self) -> None:
+        from . import netio
+        frames = np.empty(self._max_msgs * SLOT_BYTES, np.uint8)
+        off = np.empty(self._max_msgs + 1, np.int64)
+        src = np.empty(self._max_msgs, np.uint64)
+        while not self.stop_event.is_set():
+            k = netio.recv_batch(self.sock, frames, off, slot_bytes=SLOT_BYTES, max_msgs=self._max_msgs,
+                                 timeout_ms=50, sources=src)
+            if k:
+                self._relay_batch(frames, off[:k + 1], src[:k])
+
     def run(self) -> None:
+        if self.batched:
+            self._run_batched()
+            return
         while not self.stop_event.is_set():
             try:
                 data, addr = self.sock.recvfrom(1024)  # proxy.py:129

@@ -18,11 +18,12 @@ from rudp.relay import Relay
 from rudp.transport import ReliableUDP
 
 
-def run_transfer(message, isn, drop=None, client_timeout=1, codec_device=None):
+def run_transfer(message, isn, drop=None, client_timeout=1, codec_device=None, batched=False):
     server = ReliableUDP().create()
     server.bind("127.0.0.1", 0)
     sport = server.socket.getsockname()[1]
-    relay = Relay(sport, drop or (lambda d, i: False))
+    relay = Relay(sport, drop or (lambda d, i: False), batched=batched,
+                  device="cuda:0" if batched else None)
     relay.start()
     got = {}
     t = threading.Thread(target=lambda: got.setdefault("msg", server.recv()), daemon=True)
@@ -201,3 +202,106 @@ def test_receiver_answers_previous_peer_across_recv_calls():
     assert got == ["hi", "ok"]
     for s in (client, other, server):
         s.close()
+
+
+# ------------------------------------------------------------ batched relay
+@pytest.mark.gpu
+def test_batched_relay_wire_trace_and_drops(wire_trace):
+    """Config 1 through the batched relay (recvmmsg with sources, GPU retransmission
+    flags, sendmmsg with per-datagram destinations): the reference wire trace and
+    counters without drops; the message survives drops, whose retransmissions the
+    GPU check counts."""
+    msg, relay, _ = run_transfer(wire_trace["message"], wire_trace["isn"], batched=True)
+    assert msg == wire_trace["message"]
+    assert [d.hex() for d in relay.log["c2s"]] == wire_trace["client_to_server"]
+    assert [d.hex() for d in relay.log["s2c"]] == wire_trace["server_to_client"]
+    n_c, n_s = len(wire_trace["client_to_server"]), len(wire_trace["server_to_client"])
+    assert relay.stats == {"client_sent": n_c, "client_received": n_s, "client_dropped": 0,
+                           "client_retransmitted": 0, "server_sent": n_s, "server_received": n_c,
+                           "server_dropped": 0, "server_retransmitted": 0}
+    assert relay.batches > 0
+    dropped = set()
+
+    def drop(direction, index):
+        key = (direction, index)
+        if key in {("c2s", 1), ("s2c", 0)} and key not in dropped:
+            dropped.add(key)
+            return True
+        return False
+    msg, relay, _ = run_transfer(wire_trace["message"], wire_trace["isn"], drop=drop, client_timeout=0.1,
+                                 batched=True)
+    assert msg == wire_trace["message"] and relay.retransmitted >= 2
+
+
+@pytest.mark.gpu
+def test_batched_relay_counters_equal_scalar_relay():
+    """Batches of 1..700 datagrams with repeats inside and across batches (the
+    500-deep history carried over), empty datagrams and drops: the batched relay's
+    counters, log and forwarded datagrams equal the per-datagram relay's."""
+    import random as _r
+
+    import numpy as np
+    from rudp import netio
+    rng = _r.Random(11)
+    sink_srv = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    sink_srv.bind(("127.0.0.1", 0))
+    sink_cli = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    sink_cli.bind(("127.0.0.1", 0))
+    for s_ in (sink_srv, sink_cli):
+        s_.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 24)
+    srv_port, cli_port = sink_srv.getsockname()[1], sink_cli.getsockname()[1]
+    pool = [b"", bytes(5), b"\x00", bytes(6)] + [bytes(rng.randrange(256) for _ in range(rng.randrange(1, 12)))
+                                                  for _ in range(300)]
+    seq = []
+    for _ in range(4000):
+        r = rng.random()
+        if r < 0.3 and seq:
+            seq.append(seq[-rng.randint(1, min(len(seq), 800))])
+        else:
+            seq.append(rng.choice(pool))
+    from_server = [rng.random() < 0.4 for _ in seq]
+    from_server[0] = False  # the client speaks first
+    drops = {i for i in range(len(seq)) if rng.random() < 0.1}
+    index = {"c2s": 0, "s2c": 0}
+    order = []
+    for i, fs in enumerate(from_server):
+        d = "s2c" if fs else "c2s"
+        order.append((d, index[d]))
+        index[d] += 1
+    drop_set = {order[i] for i in drops}
+    rule = lambda d, i: (d, i) in drop_set  # noqa: E731
+    scalar = Relay(srv_port, rule)
+    batched = Relay(srv_port, rule, batched=True, device="cuda:0")
+    cli_key = netio.addr_key("127.0.0.1", cli_port)
+    pos = 0
+    while pos < len(seq):
+        k = min(rng.randint(1, 700), len(seq) - pos)
+        part = seq[pos:pos + k]
+        frames = np.frombuffer(b"".join(part), np.uint8) if any(part) else np.zeros(0, np.uint8)
+        off = np.concatenate([[0], np.cumsum([len(p) for p in part])]).astype(np.int64)
+        src = np.array([batched._server_key if from_server[pos + j] else cli_key for j in range(k)], np.uint64)
+        batched._relay_batch(frames, off, src)
+        pos += k
+    for i, data in enumerate(seq):
+        d, j = order[i]
+        scalar.log[d].append(data)
+        scalar._record("server" if from_server[i] else "client", data, (d, j) in drop_set)
+    assert batched.stats == scalar.stats
+    assert batched.log == scalar.log
+    assert batched.retransmitted > 100
+    # what reached the two sinks: every non-dropped datagram of its direction, in order
+    want = {"s2c": [], "c2s": []}
+    for i, data in enumerate(seq):
+        if i not in drops:
+            want[order[i][0]].append(data)
+    for sink, d in ((sink_srv, "c2s"), (sink_cli, "s2c")):
+        sink.settimeout(0.5)
+        got = []
+        try:
+            while True:
+                got.append(sink.recvfrom(2048)[0])
+        except socket.timeout:
+            pass
+        assert got == want[d], d
+    for s_ in (scalar.sock, batched.sock, sink_srv, sink_cli):
+        s_.close()
