@@ -474,13 +474,10 @@ def legs(torch, batch, device, steps):
     # device-to-device streaming-copy ceiling, same byte count as one encode's payload:
     # the fastest copy in tools/sweep.py (one dwordx4 per thread, nt loads and stores,
     # rudpx_copy_vpt) and, for reference, the grid-stride copy (rudpx_copy, 65536 blocks)
-    import ctypes
+    # (the copy kernels live in the diagnostics build, librudp_tools.so; the codec legs
+    # above all ran librudp.so)
     from rudp import _native
-    lib = _native.lib()
-    lib.rudpx_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,
-                               ctypes.c_void_p]
-    lib.rudpx_copy_vpt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
-                                   ctypes.c_int, ctypes.c_void_p]
+    lib = _native.tools_lib(activate=False)
     a = w.sets[0][1]
     b = torch.empty_like(a)
     stream = torch.cuda.current_stream().cuda_stream
@@ -562,6 +559,14 @@ def config1_loopback():
     return out
 
 
+def device_record(torch, rank, local_rank, dev_index):
+    """The GPU this rank drives: HIP device index, PCI domain:bus:device, UUID."""
+    p = torch.cuda.get_device_properties(dev_index)
+    pci = f"{getattr(p, 'pci_domain_id', 0):04x}:{getattr(p, 'pci_bus_id', 0):02x}:{getattr(p, 'pci_device_id', 0):02x}"
+    return {"rank": rank, "local_rank": local_rank, "device_index": dev_index, "pci": pci,
+            "uuid": str(getattr(p, "uuid", "")), "name": p.name}
+
+
 def read_pmc_traffic(L, n):
     """HBM bytes per launch from the committed rocprofv3 PMC summary, if any."""
     path = REPO / "profiles" / "pmc_encode.json"
@@ -617,6 +622,17 @@ def main():
             dist.init_process_group("gloo")
         else:
             dist.init_process_group("nccl", device_id=device)
+
+    # which physical GPU each rank drives: index, PCI address and UUID, gathered to
+    # rank 0 for the line; without --share-device every rank must hold its own GPU
+    devices = [device_record(torch, rank, local_rank, dev_index)]
+    if world > 1:
+        gathered = [None] * world
+        dist.all_gather_object(gathered, devices[0])
+        devices = gathered
+    distinct = len({d["pci"] for d in devices}) == len(devices)
+    if world > 1 and not args.share_device and not distinct:
+        raise SystemExit(f"ranks share a GPU without --share-device: {devices}")
 
     n, L = args.packets, args.payload
     first = rank * n
@@ -688,6 +704,8 @@ def main():
                 "global_batch": world * n, "parallelism": f"packet-slice x{world}, no collective",
                 "buffer_sets": nsets,
                 "matches_reference": None if head_chk is None else head_chk[0] == head_chk[1] > 0,
+                "devices": devices,
+                "distinct_gpus": distinct,
             },
             "roofline": {
                 "bound": "hbm",

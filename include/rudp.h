@@ -28,12 +28,12 @@
  *  - The *_host variants take host pointers and are synchronous.
  *  - Return 0 on success or a negative code (RUDP_E*); the message for the
  *    calling thread is available from rudp_last_error().
- *  - Reentrant and thread-safe: the global state is mutex-guarded per-device
- *    caches (the *_host staging pipeline, the stream-ordered scratch pool,
- *    the bounds scratch) plus the non-ABI experiment knobs of rudpx_tune and
- *    the rudpx_encode_trace buffer pointer, which are atomics (a launch
- *    concurrent with a change may see old and new settings mixed; they are
- *    for sweeps and timelines, not for callers).
+ *  - Reentrant and thread-safe: the only global state is mutex-guarded
+ *    per-device caches (the *_host staging pipeline, the stream-ordered
+ *    scratch pool, the bounds scratch).  Every launch choice is fixed at its
+ *    measured default; librudp.so exports exactly the functions below.  (The
+ *    diagnostics build of the same sources, librudp_tools.so, adds non-ABI
+ *    rudpx_* sweep knobs and timelines for tools/ and is not a product library.)
  */
 #ifndef RUDP_H_
 #define RUDP_H_

@@ -122,7 +122,7 @@ EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t*
       a.tab_off = a.hdr_bytes;
       a.hdr_bytes += 80u;
     }
-    if (tuning().encode_hchunk && a.T % 16u == 0 && !(tuning().encode_ablate & ~32)) {
+    if (tuning().encode_hchunk && a.T % 16u == 0) {
       a.hchunk = 1;
       a.hc_off = a.hdr_bytes;
       a.hdr_bytes += (a.T + 1u) * 32u;
@@ -140,8 +140,9 @@ EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t*
     // 0.0259 -> 0.0279 (profiles/r02/sweeps/encode_xcd.json, launch_split.json)
     const int xs = tuning().encode_xcd_swizzle;
     a.xcd_swizzle = (xs == 1 || (xs < 0 && a.L >= 512u)) ? 1u : 0u;
+#if RUDP_TOOLS
     a.trace = tuning().encode_trace.load();
-    a.ablate = (uint32_t)tuning().encode_ablate;
+#endif
     const int al = tuning().out_align64;
     // Fixed-length encode deals wave stores from the first 64-B boundary at
     // every tile size (since LDS-DMA phase 1 and the header-chunk phase 2 it
@@ -581,7 +582,6 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
     const int early = tuning().encode_early_table;
     a.early_table = (early == 1 || (early < 0 && in->payload_len >= 128u)) ? 1u : 0u;
   }
-  a.ablate = (uint32_t)tuning().varlen_ablate;
   {
     const int vhc = tuning().varlen_hchunk;
     a.vhc = (uint32_t)(vhc < 0 ? 0 : vhc > 2 ? 2 : vhc);
@@ -603,7 +603,9 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
     const uint64_t T = (uint64_t)256u * a.small_fpt;
     const uint64_t hint = in->payload_len ? in->payload_len : 1u;
     a.small_cap = (uint32_t)((T * hint * 5u / 4u + 256u + 15u) & ~15ull);
+#if RUDP_TOOLS
     a.trace = tuning().encode_trace.load();
+#endif
     rc = launch_encode_varlen_small(a, chk, layout, s);
     if (rc) return hip_fail((hipError_t)rc, "small-frame varlen encode launch");
     return 0;

@@ -11,7 +11,7 @@
 // chunks are written bytewise by their owners.
 //   phase 1  the tile's payload is one contiguous run: it streams into an
 //            LDS tile by LDS-DMA (global_load_lds_dwordx4 nt, 1 KiB per
-//            wave-instruction; register staging behind a tuning knob).  For
+//            wave-instruction; register staging in the tools build's sweeps).  For
 //            tiles up to 16 KiB the leaders' header-table loads go out first.
 //   sums     G = 256/T lanes per packet sum its LE u16 halves out of LDS; a
 //            shfl_xor butterfly combines them; the leader writes the 5/7-byte
@@ -92,11 +92,6 @@ __device__ __forceinline__ void encode_phase2(const EncodeTileArgs& a, const uns
       x = lead + 16u * nfull; lo_b = 0; hi_b = nbytes > x ? nbytes - x : 0u;
     }
     if (hi_b <= lo_b) continue;
-    if (a.ablate & 2u) {  // diagnostic: aligned LDS read in place of the window assembly
-      const u32x4 v = reinterpret_cast<const u32x4*>(lds_pay + kLdsGuard)[k < nfull ? k : 0u];
-      if (hi_b == 16u) store16<NTS>(v, reinterpret_cast<u32x4*>(out + x));
-      continue;
-    }
     const uint32_t qq = (uint32_t)(((uint64_t)x * a.invF) >> 32);  // x / F
     const uint32_t r = x - qq * F;           // frame position of chunk byte 0
     const int kA0 = r < (uint32_t)H ? H - (int)r : 0;  // first payload byte of qq
@@ -188,8 +183,10 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   const uint64_t p0 = (uint64_t)tile * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
+#if RUDP_TOOLS
   const uint64_t t_start = a.trace ? (uint64_t)wall_clock64() : 0ull;
   uint64_t t_loaded = 0, t_summed = 0;
+#endif
 
   // ---- phase 1: payload -> LDS, per-packet LE16 sums --------------------
   const uint32_t q = tid >> glog;
@@ -197,10 +194,9 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   const uint32_t V = L >> 4;  // 16 B vectors per packet
   // Header-table loads can go out before the payload stream, so their latency
   // overlaps phase 1 instead of adding a round trip after the barrier.
-  const bool tab = !(a.ablate & 4u);
   uint32_t t_seq = 1u, t_ack = 2u, t_flags = 3u;
-  const bool dma_tab = DMA && a.early_table == 2u && Tv == T && tab;  // uniform
-  if (a.early_table == 1u && tab && g == 0 && q < Tv) {
+  const bool dma_tab = DMA && a.early_table == 2u && Tv == T;  // uniform
+  if (a.early_table == 1u && g == 0 && q < Tv) {
     t_seq = a.seq[p0 + q];
     t_ack = a.ack[p0 + q];
     t_flags = a.flags[p0 + q];
@@ -246,8 +242,10 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
       }
     }
     __syncthreads();
+#if RUDP_TOOLS
     if (a.trace && tid == 0) t_loaded = (uint64_t)wall_clock64();
-    if (q < Tv && !(a.ablate & 1u)) {
+#endif
+    if (q < Tv) {
       const u32x4* mine = dst + q * V;
       for (uint32_t v = g; v < V; v += G) sum += le16_sum(mine[v]);
     }
@@ -255,7 +253,7 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
   if (g == 0 && q < Tv) {
     const uint64_t p = p0 + q;
-    const bool late = tab && a.early_table != 1u && !dma_tab;
+    const bool late = a.early_table != 1u && !dma_tab;
     uint32_t s = late ? a.seq[p] : t_seq, k = late ? a.ack[p] : t_ack, f = late ? a.flags[p] : t_flags;
     if (dma_tab) {
       const unsigned char* tb = lds + a.tab_off;
@@ -267,7 +265,7 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
     const uint64_t h = pack_header<H>(s, k, f, c);
     lds_hdr[q] = h;
     if (a.csum) a.csum[p] = (uint16_t)c;
-    if (a.hchunk && !(a.ablate & 32u)) {  // this packet's 1-2 header chunks, for encode_phase2_hc
+    if (a.hchunk) {  // this packet's 1-2 header chunks, for encode_phase2_hc
       const u32x4* img = reinterpret_cast<const u32x4*>(lds_pay + kLdsGuard);
       const uint32_t P = q * (L + H) + H;
       u32x4* hc = reinterpret_cast<u32x4*>(lds + a.hc_off) + 2u * q;
@@ -300,12 +298,15 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
     }
   }
   __syncthreads();
+#if RUDP_TOOLS
   if (a.trace && tid == 0) t_summed = (uint64_t)wall_clock64();
+#endif
 
   if (a.hchunk)
     encode_phase2_hc<H, NTS, BLOCK>(a, lds_pay, reinterpret_cast<const u32x4*>(lds + a.hc_off), p0, Tv, tid);
   else
     encode_phase2<H, NTS, BLOCK>(a, lds_pay, lds_hdr, p0, Tv, tid);
+#if RUDP_TOOLS
   if (a.trace) {  // diagnostics: the tile's timeline (100 MHz wall clock), XCD and CU
     __syncthreads();
     if (tid == 0) {
@@ -317,6 +318,7 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
       rec[2] = make_u32x4(t_loaded, t_summed);  // phase-1 loads landed, sums + headers done
     }
   }
+#endif
 }
 
 // Any payload length / alignment: one wave per packet, byte-granular.
@@ -376,6 +378,7 @@ int launch_tile(const EncodeTileArgs& args, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+#if RUDP_TOOLS
 template <int H, int P1>
 int launch_tile_nt(const EncodeTileArgs& args, hipStream_t stream) {
   const Tuning& t = tuning();
@@ -385,6 +388,8 @@ int launch_tile_nt(const EncodeTileArgs& args, hipStream_t stream) {
   return launch_tile<H, false, false, P1>(args, stream);
 }
 
+// The tools build's sweep forms: register-staged phase 1 (P1 loads in flight
+// per lane), temporal loads or stores, 64- to 1024-thread workgroups.
 template <int H>
 int launch_tile_policy(const EncodeTileArgs& args, hipStream_t stream) {
   const int p1 = tuning().encode_p1;
@@ -407,6 +412,14 @@ int launch_tile_policy(const EncodeTileArgs& args, hipStream_t stream) {
   if (p1 == 4) return launch_tile_nt<H, 4>(args, stream);
   return launch_tile_nt<H, 8>(args, stream);
 }
+#else
+// The measured form: LDS-DMA phase 1, non-temporal loads and stores,
+// 256-thread workgroups (profiles/r01/sweeps/encode_dma*.json, encode_block_sizes.json).
+template <int H>
+int launch_tile_policy(const EncodeTileArgs& args, hipStream_t stream) {
+  return launch_tile<H, true, true, 8, kBlock, true>(args, stream);
+}
+#endif
 
 
 int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStream_t stream) {

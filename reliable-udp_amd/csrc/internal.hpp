@@ -1,4 +1,13 @@
 // Launcher interface between the C ABI (capi.hip) and the kernels.
+//
+// Two builds come from these sources (rudp/_build.py):
+//   librudp.so        the product: every launch choice is the measured default
+//                     (the Tuning values below are compile-time constants), no
+//                     diagnostics in any kernel, only the include/rudp.h ABI;
+//   librudp_tools.so  RUDP_TOOLS=1, for tools/ and the tests of the non-default
+//                     kernel forms: the same ABI plus rudpx_tune (every Tuning
+//                     value a runtime knob), rudpx_encode_trace (tile timelines),
+//                     rudpx_stamp and the streaming-copy ceilings (tuning.hip).
 #pragma once
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -6,6 +15,10 @@
 #include <atomic>
 
 #include "../../include/rudp.h"
+
+#ifndef RUDP_TOOLS
+#define RUDP_TOOLS 0
+#endif
 
 namespace rudp {
 
@@ -24,8 +37,6 @@ struct EncodeTileArgs {
   uint64_t invF;        // ceil(2^32 / (L + H)) for exact x / F, x < T*F
   uint32_t xcd_swizzle; // 1: map blocks b, b+8, ... to consecutive tiles (one XCD each)
   uint32_t num_tiles;
-  uint32_t ablate;      // diagnostics only (wrong output): 1 no LDS sum pass, 2 plain phase-2
-                        // LDS reads, 4 no header-table loads, 32 no header-chunk build
   uint32_t out_align64; // phase 2 deals full chunks from the tile's first 64-B boundary
   uint32_t early_table;     // tile kernel: header-table loads issued before phase 1 (2: by LDS-DMA
                             // into tab_off with the payload, full tiles of T = 16)
@@ -34,7 +45,9 @@ struct EncodeTileArgs {
   uint32_t hc_off;          // LDS byte offset of the header-chunk array [T + 1][2] x 16 B
   uint32_t hc_scratch;      // leaders build header chunks through a 48-B LDS scratch per packet
   uint32_t scr_off;         // LDS byte offset of that scratch [T][48 B]
+#if RUDP_TOOLS
   uint64_t* trace;          // diagnostics (rudpx_encode_trace): per tile {start, end, XCC, CU}
+#endif
 };
 
 struct DecodeArgs {
@@ -100,8 +113,6 @@ struct VarlenArgs {
   uint32_t tile_cap;
   uint32_t align64;               // tile kernel: wave stores start on 64-B sector boundaries
   uint32_t early_table;           // tile kernel: header-table loads before phase 1
-  uint32_t ablate;                // diagnostics only (wrong output): 1 = phase 2 without the frame walk,
-                                  // 2 = no sum pass, 4 = tiles over their LDS budget do nothing
   uint32_t vhc;                   // tile kernel: prebuilt header chunks + pure-chunk fast phase 2
   uint32_t hc_off;                // LDS byte offset of the header-chunk array (set by the launcher)
   uint32_t early_fo;              // tile kernels: the tile's frame offsets loaded before phase 1
@@ -116,7 +127,9 @@ struct VarlenArgs {
   uint64_t frames_lim;
   uint32_t* status_out;           // may be null also for a checked call (the rejections are in ok[])
   uint32_t lim_checked;           // decode: frames_lim bounds the frames (checked calls)
+#if RUDP_TOOLS
   uint64_t* trace;                // diagnostics (rudpx_encode_trace): small-frame encode timeline per tile
+#endif
   uint32_t small_fpt;             // decode small-frame tile: frames per thread (0: not used)
   uint32_t small_cap;             // its LDS run budget in bytes
   uint32_t xcd;                   // tile kernels: XCD-contiguous tile order (xcd_tile)
@@ -166,74 +179,80 @@ constexpr uint32_t kMaxPayload = 65535;
 
 enum class DecodePath { kBytes, kCopy, kCopyTile, kVerify, kVerifyTile };
 
-// Non-ABI tuning knobs (rudpx_tune in tuning.hip), read at launch.  Each
-// knob is an atomic int, so a concurrent rudpx_tune is not a data race; a
-// launch that runs while knobs change may see some old and some new values
-// (the knobs are for sweeps, not for production callers).
+// Launch choices, each at its measured default.  In librudp.so they are
+// compile-time constants.  In the tools build each is an atomic int set by
+// rudpx_tune (tuning.hip), read at launch, so a concurrent rudpx_tune is not a
+// data race; a launch that runs while knobs change may see some old and some
+// new values (the knobs are for sweeps, not for production callers).
+#if RUDP_TOOLS
+#define RUDP_KNOB(name, value) std::atomic<int> name{value};
+#else
+#define RUDP_KNOB(name, value) static constexpr int name = value;
+#endif
 struct Tuning {
-  std::atomic<int> encode_nt_load{1};
-  std::atomic<int> encode_nt_store{1};
-  std::atomic<int> encode_tile{0};    // packets per tile; 0 = automatic
-  std::atomic<int> encode_p1{8};      // phase-1 loads in flight per lane (2, 4, 8)
-  std::atomic<int> encode_blocks_per_cu{-1};  // cap resident tiles per CU via LDS reservation; 0 = natural, -1 = auto
-  std::atomic<int> decode_glog{-1};   // verify kernel lanes-per-packet log2; -1 = automatic
+  RUDP_KNOB(encode_nt_load, 1)
+  RUDP_KNOB(encode_nt_store, 1)
+  RUDP_KNOB(encode_tile, 0)    // packets per tile; 0 = automatic
+  RUDP_KNOB(encode_p1, 8)      // phase-1 loads in flight per lane (2, 4, 8)
+  RUDP_KNOB(encode_blocks_per_cu, -1)  // cap resident tiles per CU via LDS reservation; 0 = natural, -1 = auto
+  RUDP_KNOB(decode_glog, -1)   // verify kernel lanes-per-packet log2; -1 = automatic
   // XCD-contiguous tile order (xcd_tile) for the fixed-length encode tile:
   // 1 on, 0 off, -1 from 512-B payloads (16M x 1472 B 0.540 -> 0.481 ms per
   // 2^20 packets; tools/launch_split.py, profiles/r02/sweeps/launch_split.json).
-  std::atomic<int> encode_xcd_swizzle{-1};
+  RUDP_KNOB(encode_xcd_swizzle, -1)
+#if RUDP_TOOLS
   std::atomic<uint64_t*> encode_trace{nullptr};  // diagnostics: tile timeline buffer (tools only)
+#endif
   // The same order for the decode, varlen and UTF-8 tile kernels: fixed decode
   // verify 1M x 1472 B 0.240 -> 0.218 ms, x 1024 B 0.170 -> 0.154; copy-out
   // 1472 B 0.523 -> 0.504; varlen decode 1479 B 0.266 -> 0.230, ragged [0, 2944]
   // 0.306 -> 0.284; varlen encode 1472 B 0.587 -> 0.557; 256 B and below
   // within noise, fixed copy-out at 64 B 5% slower, so the fixed decode keeps
   // it off below 128-B frames (profiles/r02/sweeps/tile_xcd_*.json).
-  std::atomic<int> tile_xcd{1};
-  std::atomic<int> encode_block{256};  // tile workgroup size (64, 128 when T <= block; 256, 512, 1024)
-  std::atomic<int> decode_copy_tile{1};  // copy-out decode through an LDS tile (0: register windows)
-  std::atomic<int> decode_verify_tile{1};  // verify-only decode through an LDS tile (0: aligned-chunk kernel)
-  std::atomic<int> varlen_vec{1};     // varlen encode/decode: vector kernels (0: byte kernels)
-  std::atomic<int> varlen_glog{-1};   // varlen lanes-per-packet log2 (0..6); -1 = from the length hint
-  std::atomic<int> varlen_tile{1};    // varlen encode of packed payloads through LDS tiles (0: vector kernel)
-  std::atomic<int> varlen_tile_maxT{256};     // varlen encode tile: most packets per tile
-  std::atomic<int> varlen_tile_bytes{0};  // varlen encode tile: payload bytes per tile at the hint (0 = automatic)
-  std::atomic<int> encode_ablate{0};  // EncodeTileArgs::ablate (sweeps only)
+  RUDP_KNOB(tile_xcd, 1)
+  RUDP_KNOB(encode_block, 256)  // tile workgroup size (64, 128 when T <= block; 256, 512, 1024)
+  RUDP_KNOB(decode_copy_tile, 1)  // copy-out decode through an LDS tile (0: register windows)
+  RUDP_KNOB(decode_verify_tile, 1)  // verify-only decode through an LDS tile (0: aligned-chunk kernel)
+  RUDP_KNOB(varlen_vec, 1)     // varlen encode/decode: vector kernels (0: byte kernels)
+  RUDP_KNOB(varlen_glog, -1)   // varlen lanes-per-packet log2 (0..6); -1 = from the length hint
+  RUDP_KNOB(varlen_tile, 1)    // varlen encode of packed payloads through LDS tiles (0: vector kernel)
+  RUDP_KNOB(varlen_tile_maxT, 256)     // varlen encode tile: most packets per tile
+  RUDP_KNOB(varlen_tile_bytes, 0)  // varlen encode tile: payload bytes per tile at the hint (0 = automatic)
   // Wave loads/stores of the tile kernels start on a 64-B sector boundary
   // (1) or on the first 16-B one (0).  -1 = automatic: on for fixed-length
   // encode at every tile size (1M x 1472 B: 0.516 vs 0.533 ms; smaller
   // tiles equal or up to 1.3% faster since LDS-DMA phase 1), off for decode
   // and varlen, where it measured 1-3% slower
   // (profiles/r01/sweeps/align64.json, align64_after_dma.json).
-  std::atomic<int> out_align64{-1};
+  RUDP_KNOB(out_align64, -1)
   // Encode tile phase 1 by LDS-DMA (global_load_lds_dwordx4) in place of
   // register staging (256-thread contiguous tiles, nt loads and stores):
   // 1M x 256 B 0.0967 -> 0.0946 ms, x 512 B 0.1884 -> 0.1854, x 64 B 0.0301
   // -> 0.0292; x 1024 B and x 1472 B unchanged (profiles/r01/sweeps/span_vs_tile.json).
-  std::atomic<int> encode_dma{1};
+  RUDP_KNOB(encode_dma, 1)
   // Encode tile phase 2 with header chunks prebuilt by the packet leaders
   // (T % 16 == 0): 1M x 64 B 0.0295 -> 0.0287 ms, x 256 B 0.0962 -> 0.0938,
   // x 1024 B 0.3712 -> 0.3683, x 1472 B equal (profiles/r01/sweeps/encode_hchunk.json).
-  std::atomic<int> encode_hchunk{1};
+  RUDP_KNOB(encode_hchunk, 1)
   // Encode tile header-table loads before phase 1 (1), after it (0), by
   // LDS-DMA with the payload stream (2: full 16-packet tiles, aligned arrays),
   // or -1 = automatic: before for tiles of at most 16 KiB of payload (1M x 64 B
   // 0.0287 -> 0.0267 ms, x 256 B 0.0934 -> 0.0892, x 1024 B 0.3606 ->
   // 0.3557), by LDS-DMA above (x 1472 B 0.5126 -> 0.5086; round 1: after,
   // 0.5208 vs 0.5291 early).
-  std::atomic<int> encode_early_table{-1};
+  RUDP_KNOB(encode_early_table, -1)
   // Leaders build header chunks through a 48-B LDS scratch per packet
   // (constant shifts, one window per chunk) instead of variable-shift
   // funnels: 1, 0, or -1 = automatic (tiles of at most 16 KiB: 1M x 64 B
   // 0.0272 -> 0.0266 ms, x 256 B 0.0923 -> 0.0912; x 1472 B within noise;
   // profiles/r01/sweeps/encode_hc_scratch.json).
-  std::atomic<int> encode_hc_scratch{-1};
+  RUDP_KNOB(encode_hc_scratch, -1)
   // Decode tile outputs staged in LDS and written as whole dwords (output
   // pointers 4-B aligned): 1M x 256 B verify 0.0489 -> 0.0470 ms, x 64 B
   // 0.0156 -> 0.0152, x 1472 B equal; copy-out equal to +1%
   // (profiles/r01/sweeps/decode_stage_out.json).
-  std::atomic<int> decode_stage_out{1};
-  std::atomic<int> decode_blocks_per_cu{-1};  // decode tile: cap resident tiles per CU (0 = natural, -1 = auto)
-  std::atomic<int> varlen_ablate{0};  // VarlenArgs::ablate (sweeps only)
+  RUDP_KNOB(decode_stage_out, 1)
+  RUDP_KNOB(decode_blocks_per_cu, -1)  // decode tile: cap resident tiles per CU (0 = natural, -1 = auto)
   // Varlen encode tile: prebuilt header chunks and a one-window phase 2 for
   // tiles whose frames are all >= 32 B: 1M x 1472 B 0.738 -> 0.631 ms, x 1024
   // B 0.562 -> 0.477, x 256 B 0.196 -> 0.169 (Python entry, one box;
@@ -242,66 +261,73 @@ struct Tuning {
   // phase-2 chunk needs no frame-offset reads: 1M x 1472 B 0.581 -> 0.569 ms,
   // x 512 B 0.265 -> 0.256, x 256 B 0.165 -> 0.160, x 1024 B kept on the u8
   // map by the occupancy rule (profiles/r01/sweeps/varlen_coded_map.json).
-  std::atomic<int> varlen_hchunk{2};
+  RUDP_KNOB(varlen_hchunk, 2)
   // Varlen decode tile: LDS budget in % of the hinted run.  110 lets six
   // 1472-B tiles share a CU (125 held five): 1M x 1479 B 0.288 -> 0.277 ms,
   // lengths uniform in [0, 2944] 0.315 -> 0.306 (overflowing tiles take the
   // per-frame path in the launch; profiles/r01/sweeps/varlen_decode_cap.json).
-  std::atomic<int> varlen_decode_cap_pct{110};
+  RUDP_KNOB(varlen_decode_cap_pct, 110)
   // Varlen encode tile: LDS budget in % of the hinted run (110: 1M x 1472 B
   // 0.619 -> 0.586 ms, x 1024 B 0.468 -> 0.463, x 256 B 0.167 -> 0.164 vs
   // 125; profiles/r01/sweeps/varlen_encode_cap.json).
-  std::atomic<int> varlen_encode_cap_pct{110};
-  std::atomic<int> varlen_decode_tile{1};  // varlen decode through LDS tiles for hints >= 128 B (2: any hint; 0: never)
-  std::atomic<int> dedup_table{1};    // dedup window pass by LDS hash table (0: every frame scans its window)
-  std::atomic<int> utf8_tile{1};
+  RUDP_KNOB(varlen_encode_cap_pct, 110)
+  RUDP_KNOB(varlen_decode_tile, 1)  // varlen decode through LDS tiles for hints >= 128 B (2: any hint; 0: never)
+  RUDP_KNOB(dedup_table, 1)    // dedup window pass by LDS hash table (0: every frame scans its window)
+  RUDP_KNOB(utf8_tile, 1)
   // Packed-frame UTF-8 validation through LDS tiles (hints >= 128 B) and its
   // LDS budget in % of the hinted run: 1M x 1479 B ASCII frames 0.287 ->
   // 0.279 ms, lengths uniform in [0, 2944] 0.373 -> 0.370 at 130% (110%:
   // more tiles overflow to the HBM path on ragged lengths; 150%: fewer tiles
   // per CU; tools/utf8_varlen_sweep.py, profiles/r01/sweeps/utf8_varlen_tile.json).
-  std::atomic<int> utf8_vtile{1};
-  std::atomic<int> utf8_vtile_cap_pct{130};      // fixed-stride UTF-8 validation through LDS tiles (0: per-frame vector kernel)
+  RUDP_KNOB(utf8_vtile, 1)
+  RUDP_KNOB(utf8_vtile_cap_pct, 130)      // fixed-stride UTF-8 validation through LDS tiles (0: per-frame vector kernel)
   // Varlen tile kernels load the tile's frame offsets into registers before
   // phase 1 (1) instead of after its payload loads (0): decode 1M x 1479 B
   // 0.280 -> 0.265 ms, x 1031 B 0.222 -> 0.215; encode (Python entry) 1472 B
   // 0.583 -> 0.579, 1024 B 0.433 -> 0.428 (profiles/r01/sweeps/varlen_early_fo.json).
-  std::atomic<int> varlen_early_fo{1};
+  RUDP_KNOB(varlen_early_fo, 1)
   // Varlen encode tile: minimum waves per SIMD imposed on its register
   // allocation (amdgpu_waves_per_eu: 6, 7, 8; 0 = none, 88 VGPRs = 5 waves;
   // -1 = automatic from the tile's LDS occupancy, see launch_varlen_tile).
-  std::atomic<int> varlen_waves{-1};
+  RUDP_KNOB(varlen_waves, -1)
   // Packed-frame UTF-8 tile: the most frames per tile whose LDS budget stays
   // within these bytes (0: lanes from chunks per lane).  A 34 KiB raw run
   // (T = 64 at 519 B) gave 0.164 -> 0.136 ms there but 0.228 -> 0.247 at
   // 1031 B (3 tiles per CU at the 130% budget; varlen_decode_lanes.json).
-  std::atomic<int> utf8_vtile_bytes{34816};
-  std::atomic<int> varlen_scan{1};    // frame offsets: 1 = reduce-then-scan (scan.hip), 0 = hipcub
+  RUDP_KNOB(utf8_vtile_bytes, 34816)
+  RUDP_KNOB(varlen_scan, 1)    // frame offsets: 1 = reduce-then-scan (scan.hip), 0 = hipcub
   // Small-frame varlen encode (scan's last pass + framing in one tile kernel)
   // for packed batches whose mean payload hint is under this many bytes (0: off),
   // and its packets per thread (1, 2, 4, 8: tiles of 256 * fpt packets).
-  std::atomic<int> varlen_small{16};
-  std::atomic<int> varlen_small_fpt{0};  // 0: 4 for hints up to 4 B, 2 above (profiles/r02/sweeps/small.json)
-  std::atomic<int> varlen_small_fused{1};  // the framing kernel finds its own base (no pass-2 launch)
+  RUDP_KNOB(varlen_small, 16)
+  RUDP_KNOB(varlen_small_fpt, 0)  // 0: 4 for hints up to 4 B, 2 above (profiles/r02/sweeps/small.json)
+  RUDP_KNOB(varlen_small_fused, 1)  // the framing kernel finds its own base (no pass-2 launch)
   // Fixed-length encode: batches of more packets than this go out as several
   // launches of at most this many (0: one launch).
-  std::atomic<int> encode_launch_packets{0};
+  RUDP_KNOB(encode_launch_packets, 0)
   // Varlen encode tiles by payload bytes (spans from the scan) instead of by
   // packet count: no tile overflows short of one packet past the budget's
   // slack.  0: packet tiles; 1: byte tiles when over 1/32 of the packet tiles
   // would overflow (decided on the device per call); 2: byte tiles.  1M x
   // 1472 B: packet 0.540 / byte 0.621 ms; lengths uniform in [0, 2944]:
   // 0.728 / 0.644 (profiles/r02/sweeps/ragged_blocksums.json).
-  std::atomic<int> varlen_btile{1};
-  std::atomic<int> varlen_lds_pad{0};  // extra dynamic LDS per varlen encode tile (sweeps only)
+  RUDP_KNOB(varlen_btile, 1)
   // Varlen tile sum pass from 128-B block sums (VarlenArgs::tile_sums 2): 1M x
   // 1472 B 0.544 -> 0.527 ms, lengths uniform in [0, 2944] 0.808 -> 0.729
   // (profiles/r02/sweeps/ragged_blocksums.json).
-  std::atomic<int> varlen_tile_sums{2};
-  std::atomic<int> host_slots{3};     // *_host pipeline: device staging slots (2..8)
-  std::atomic<int> host_stage_mb{128};  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
+  RUDP_KNOB(varlen_tile_sums, 2)
+  RUDP_KNOB(host_slots, 3)     // *_host pipeline: device staging slots (2..8)
+  RUDP_KNOB(host_stage_mb, 128)  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
 };
+#undef RUDP_KNOB
+#if RUDP_TOOLS
 Tuning& tuning();
+#else
+inline const Tuning& tuning() {
+  static constexpr Tuning t{};
+  return t;
+}
+#endif
 
 // Tile geometry for a fast-path payload length (L % 16 == 0, 16 <= L <= 4096).
 void encode_tile_geometry(uint32_t L, uint32_t* T, uint32_t* glog);

@@ -1,11 +1,14 @@
-// Non-ABI experiment hooks (not declared in include/rudp.h): launch-policy
-// knobs for kernel sweeps, and a plain streaming copy used to measure the
-// device-to-device bandwidth ceiling next to the codec.
+// Non-ABI experiment hooks of the tools build (librudp_tools.so, RUDP_TOOLS=1;
+// not declared in include/rudp.h, not in librudp.so): launch-policy knobs for
+// kernel sweeps, tile timelines, wall-clock stamps, and plain streaming copies
+// that measure the device-to-device bandwidth ceiling next to the codec
+// (SURVEY.md §8d).
 #include <atomic>
 
 #include "codec_device.hpp"
 #include "internal.hpp"
 
+#if RUDP_TOOLS
 namespace rudp {
 
 Tuning& tuning() {
@@ -250,7 +253,7 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // (7: per-packet phase-1 loads, lost to the contiguous stream, removed); 8: host pipeline
 // slots; 9: host pipeline MiB per slot; 10: encode tile workgroup size;
 // 11: copy-out decode through an LDS tile; 12: verify-only decode through an LDS tile;
-// 13: encode stage ablation; 14: varlen vector kernels; 15: varlen lanes log2;
+// (13: encode stage ablation, removed with its kernel branches); 14: varlen vector kernels; 15: varlen lanes log2;
 // 16: varlen encode through LDS tiles (packed payloads); 17: most packets per
 // varlen tile; 18: varlen tile payload bytes at the hint; 20: register-streamed
 // encode; 21: its packets per workgroup (0 auto); 22: its load rounds in flight;
@@ -260,8 +263,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // varlen-encode phase 1 by LDS-DMA, measured no faster and removed); 29: encode phase 2 with prebuilt header chunks;
 // 30: encode header-table loads before phase 1; 31: fixed-stride UTF-8 validation
 // through LDS tiles; 32: dedup window pass by LDS hash table; 33: varlen decode
-// through LDS tiles; 34: decode tile outputs staged in LDS; 35: varlen encode tile
-// stage ablation (diagnostic); 36: varlen encode tile prebuilt header chunks;
+// through LDS tiles; 34: decode tile outputs staged in LDS; (35: varlen encode tile
+// stage ablation, removed); 36: varlen encode tile prebuilt header chunks;
 // 37: encode header chunks through an LDS scratch; 38: varlen decode tile LDS budget (%);
 // 39: varlen encode tile LDS budget (%); 40: decode tiles per CU cap; 41: packed-frame
 // UTF-8 validation through LDS tiles; 42: its LDS budget (%); 43: varlen tile
@@ -283,7 +286,7 @@ int rudpx_tune(int key, int value) {
             : key == 6 ? &t.encode_blocks_per_cu
             : key == 8 ? &t.host_slots : key == 9 ? &t.host_stage_mb
             : key == 10 ? &t.encode_block : key == 11 ? &t.decode_copy_tile
-            : key == 12 ? &t.decode_verify_tile : key == 13 ? &t.encode_ablate : key == 14 ? &t.varlen_vec : key == 15 ? &t.varlen_glog
+            : key == 12 ? &t.decode_verify_tile : key == 14 ? &t.varlen_vec : key == 15 ? &t.varlen_glog
             : key == 16 ? &t.varlen_tile : key == 17 ? &t.varlen_tile_maxT
             : key == 18 ? &t.varlen_tile_bytes : key == 23 ? &t.out_align64 : key == 24 ? &t.varlen_scan : key == 25 ? &t.encode_dma
             : key == 29 ? &t.encode_hchunk
@@ -292,7 +295,6 @@ int rudpx_tune(int key, int value) {
             : key == 32 ? &t.dedup_table
             : key == 33 ? &t.varlen_decode_tile
             : key == 34 ? &t.decode_stage_out
-            : key == 35 ? &t.varlen_ablate
             : key == 36 ? &t.varlen_hchunk
             : key == 37 ? &t.encode_hc_scratch
             : key == 38 ? &t.varlen_decode_cap_pct
@@ -309,7 +311,7 @@ int rudpx_tune(int key, int value) {
             : key == 49 ? &t.tile_xcd
             : key == 50 ? &t.varlen_small_fused
             : key == 51 ? &t.varlen_btile
-            : key == 52 ? &t.varlen_tile_sums : key == 53 ? &t.varlen_lds_pad : nullptr;
+            : key == 52 ? &t.varlen_tile_sums : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }
@@ -337,3 +339,4 @@ int rudpx_copy(const void* src, void* dst, uint64_t n16, uint32_t blocks, void* 
 }
 
 }  // extern "C"
+#endif  // RUDP_TOOLS

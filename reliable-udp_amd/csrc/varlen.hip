@@ -4,7 +4,7 @@
 // payload per datagram (utils/reliableUDP.py:11, :60).  A varlen batch is the
 // header table plus len[N] (+ optional payload_off[N]) over one payload
 // buffer.  Frame offsets are the exclusive scan of len[i] + H (scan.hip, a
-// three-pass reduce-then-scan; hipcub behind a tuning knob), so the frames
+// three-pass reduce-then-scan; hipcub in the tools build's sweeps), so the frames
 // come out packed back to back exactly as N calls of Packet.to_byte() would
 // be concatenated.
 //
@@ -15,11 +15,12 @@
 // kernels (16-byte aligned chunks, G lanes per packet from the caller's
 // mean-length hint) when the buffers are 16-byte aligned, byte-granular
 // kernels (8 lanes per packet) when not.  Numbers: DESIGN.md §3.
-#include <hipcub/hipcub.hpp>
-
 #include "codec_device.hpp"
 #include "internal.hpp"
 #include "scan_device.hpp"
+#if RUDP_TOOLS
+#include <hipcub/hipcub.hpp>
+#endif
 
 namespace rudp {
 
@@ -29,11 +30,13 @@ constexpr uint32_t kVarLanes = 8;
 // Uniform (a kernel argument), so this is one scalar load per wave.
 __device__ __forceinline__ bool call_failed(const uint32_t* status) { return status && *status; }
 
+#if RUDP_TOOLS
 struct FrameLen {
   const uint32_t* len;
   uint32_t H;
   __host__ __device__ uint64_t operator()(uint64_t i) const { return (uint64_t)len[i] + H; }
 };
+#endif
 
 template <int H>
 __global__ void __launch_bounds__(kBlock) encode_varlen_kernel(VarlenArgs a) {
@@ -364,7 +367,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   const uint64_t A = po0 & ~15ull;
   const uint64_t run = ((po_end + 15u) & ~15ull) - A;
   if (Tall > T || run > cap) {  // uniform over the workgroup
-    if (a.ablate & 4u) return;  // diagnostic (wrong output): overflowing tiles do nothing
     for (uint32_t q0 = 0; q0 < Tall; q0 += kBlock >> glog)  // (byte tiles may hold more than T packets)
       encode_varlen_packet<H>(a, p0 + q0 + q, q0 + q < Tall, g, glog);
     return;
@@ -422,7 +424,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
     const uint32_t Lq = fe - fs - H;
     const uint32_t d = shift + fs - q * H;  // LDS offset of the packet's first payload byte
-    if (Lq && !(a.ablate & 2u)) {  // ablate bit 2 (diagnostic, wrong output): no sum pass
+    if (Lq) {
       if (blk_sums) {
         // the 16 chunks of the blocks holding the payload's first and last
         // bytes (each masked to the payload), then the block sums between
@@ -578,12 +580,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
       continue;
     }
     uint64_t lo = 0, hi = 0;
-    if (a.ablate & 1u) {  // diagnostic (wrong output): one aligned LDS read, no frame walk
-      const u32x4 w = reinterpret_cast<const u32x4*>(lds_pay)[(x >> 4) + 1u];
-      lo = lo64(w);
-      hi = hi64(w);
-      r = Tv;
-    }
     // frames r, r+1, ... are back to back: each one starts where the last ended
     for (uint32_t fs = lds_fo[r < Tv ? r : 0]; r < Tv; ++r) {
       const uint32_t fe = lds_fo[r + 1];
@@ -1262,7 +1258,9 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
   const uint64_t p0 = tile * T;
   const uint32_t Tv = a.n - p0 < T ? (uint32_t)(a.n - p0) : T;
   uint64_t fo0, fo_end;
+#if RUDP_TOOLS
   const uint64_t t_start = a.trace ? (uint64_t)wall_clock64() : 0ull;  // diagnostics
+#endif
   if (FUSED) {
     __shared__ uint64_t s_pre[kBlock / 64], s_all[kBlock / 64];
     __shared__ uint32_t s_bits;
@@ -1309,7 +1307,9 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
     fo_end = p0 + T < a.n ? sums[tile + 1] : a.frame_off[a.n];
     if (call_failed(a.status)) return;
   }
+#if RUDP_TOOLS
   const uint64_t t_base = a.trace ? (uint64_t)wall_clock64() : 0ull;
+#endif
   const uint64_t po0 = fo0 - p0 * (uint64_t)H, po_end = fo_end - (p0 + Tv) * (uint64_t)H;
   const uint64_t A = po0 & ~15ull, OA = fo0 & ~15ull;
   const uint64_t prun = ((po_end + 15u) & ~15ull) - A;
@@ -1435,6 +1435,7 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
       for (uint32_t b = lo; b < hi; ++b) out[b] = img[b];
     }
   }
+#if RUDP_TOOLS
   if (a.trace) {  // diagnostics: {start, base known, end, XCC} per tile (tools/small_timeline.py)
     __syncthreads();
     if (tid == 0) {
@@ -1443,6 +1444,7 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
       rec[1] = make_u32x4((uint64_t)wall_clock64(), __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20));
     }
   }
+#endif
 }
 
 template <int H, uint32_t FPT>
@@ -1465,6 +1467,18 @@ int launch_small_fpt(const VarlenArgs& args, const uint64_t* sums, uint64_t nb, 
   return (int)hipGetLastError();
 }
 
+// 2 or 4 packets per thread (the measured choice by hint); 1 and 8 in the tools build's sweeps.
+template <int H>
+int launch_small_any(const VarlenArgs& args, const uint64_t* sums, uint64_t nb, const ScanCheck& chk, bool fused,
+                     hipStream_t stream) {
+#if RUDP_TOOLS
+  if (args.small_fpt == 1) return launch_small_fpt<H, 1>(args, sums, nb, chk, fused, stream);
+  if (args.small_fpt == 8) return launch_small_fpt<H, 8>(args, sums, nb, chk, fused, stream);
+#endif
+  return args.small_fpt == 2 ? launch_small_fpt<H, 2>(args, sums, nb, chk, fused, stream)
+                             : launch_small_fpt<H, 4>(args, sums, nb, chk, fused, stream);
+}
+
 int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int layout, hipStream_t stream) {
   if (args.n == 0) return 0;
   const uint32_t fpt = args.small_fpt;
@@ -1478,17 +1492,8 @@ int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int
   const bool fused = tuning().varlen_small_fused && nb <= kSmallFusedTiles;
   scan_block_sums(args.len, args.n, (uint32_t)layout, fpt, sums, chk, stream);
   if (!fused) scan_block_bases(sums, nb, const_cast<uint64_t*>(args.frame_off), args.n, (uint32_t)layout, chk, stream);
-  int rc;
-  if (layout == 7)
-    rc = fpt == 1 ? launch_small_fpt<7, 1>(args, sums, nb, chk, fused, stream)
-       : fpt == 2 ? launch_small_fpt<7, 2>(args, sums, nb, chk, fused, stream)
-       : fpt == 4 ? launch_small_fpt<7, 4>(args, sums, nb, chk, fused, stream)
-                  : launch_small_fpt<7, 8>(args, sums, nb, chk, fused, stream);
-  else
-    rc = fpt == 1 ? launch_small_fpt<5, 1>(args, sums, nb, chk, fused, stream)
-       : fpt == 2 ? launch_small_fpt<5, 2>(args, sums, nb, chk, fused, stream)
-       : fpt == 4 ? launch_small_fpt<5, 4>(args, sums, nb, chk, fused, stream)
-                  : launch_small_fpt<5, 8>(args, sums, nb, chk, fused, stream);
+  const int rc = layout == 7 ? launch_small_any<7>(args, sums, nb, chk, fused, stream)
+                             : launch_small_any<5>(args, sums, nb, chk, fused, stream);
   e = stream_free(sums, stream);
   return rc ? rc : (int)e;
 }
@@ -1590,12 +1595,15 @@ int launch_decode_small_fpt(const VarlenArgs& args, hipStream_t stream) {
 
 template <int H>
 int launch_decode_small(const VarlenArgs& args, hipStream_t stream) {
+#if RUDP_TOOLS  // 4 frames per thread is the measured choice; 1, 2 and 8 for sweeps
   switch (args.small_fpt) {
     case 1: return launch_decode_small_fpt<H, 1>(args, stream);
     case 2: return launch_decode_small_fpt<H, 2>(args, stream);
     case 8: return launch_decode_small_fpt<H, 8>(args, stream);
-    default: return launch_decode_small_fpt<H, 4>(args, stream);
+    default: break;
   }
+#endif
+  return launch_decode_small_fpt<H, 4>(args, stream);
 }
 
 // Dynamic LDS of one varlen encode tile whose arrays hold Tl packets.
@@ -1664,9 +1672,11 @@ int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
     const size_t per_cu = kLdsPerCu / lds;
     w = per_cu >= 7 ? 7 : per_cu == 6 ? 6 : 1;
   }
+#if RUDP_TOOLS
+  if (w == 8) return launch_varlen_tile_w<H, 8>(args, lds, blocks, stream);
+#endif
   return w == 6 ? launch_varlen_tile_w<H, 6>(args, lds, blocks, stream)
        : w == 7 ? launch_varlen_tile_w<H, 7>(args, lds, blocks, stream)
-       : w == 8 ? launch_varlen_tile_w<H, 8>(args, lds, blocks, stream)
                 : launch_varlen_tile_w<H, 1>(args, lds, blocks, stream);
 }
 
@@ -1808,12 +1818,10 @@ int launch_validate_utf8(const Utf8Args& args, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
-// frame_off[0..n] = exclusive scan of len[i] + H, frame_off[n] = total bytes.
-int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
-                       const ScanCheck& chk, hipStream_t stream, const SpanStarts& spans) {
-  // the device-side checks and the span starts live in the three-pass scan only
-  if (tuning().varlen_scan == 1 || chk.status || spans.rec)
-    return scan_frame_offsets_3pass(d_len, n, H, d_frame_off, chk, stream, spans);
+#if RUDP_TOOLS
+// The round-1 scan by hipcub (tools build, sweeps only): no device-side checks, no span starts.
+static int scan_frame_offsets_hipcub(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
+                                     hipStream_t stream) {
   hipcub::CountingInputIterator<uint64_t> idx(0);
   hipcub::TransformInputIterator<uint64_t, FrameLen, hipcub::CountingInputIterator<uint64_t>> it(
       idx, FrameLen{d_len, H});
@@ -1828,6 +1836,18 @@ int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* 
   if (e != hipSuccess) return (int)e;
   if (e2 != hipSuccess) return (int)e2;
   return (int)e3;
+}
+#endif
+
+// frame_off[0..n] = exclusive scan of len[i] + H, frame_off[n] = total bytes.
+int scan_frame_offsets(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
+                       const ScanCheck& chk, hipStream_t stream, const SpanStarts& spans) {
+#if RUDP_TOOLS
+  // the device-side checks and the span starts live in the three-pass scan only
+  if (tuning().varlen_scan != 1 && !chk.status && !spans.rec)
+    return scan_frame_offsets_hipcub(d_len, n, H, d_frame_off, stream);
+#endif
+  return scan_frame_offsets_3pass(d_len, n, H, d_frame_off, chk, stream, spans);
 }
 
 }  // namespace rudp

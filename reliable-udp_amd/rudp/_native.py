@@ -16,6 +16,10 @@ from pathlib import Path
 # RUDP_LIB names another build of the same ABI (A/B timing of two builds in one
 # GPU call, tools/ only); the default is the in-tree build.
 LIB_PATH = Path(os.environ.get("RUDP_LIB") or Path(__file__).resolve().parent / "librudp.so")
+# The diagnostics build of the same sources (RUDP_TOOLS=1): the same ABI plus the
+# rudpx_* sweep knobs, tile timelines and copy ceilings, for tools/ and the tests
+# of the non-default kernel forms.  Never loaded by the product path on its own.
+TOOLS_LIB_PATH = Path(os.environ.get("RUDP_TOOLS_LIB") or Path(__file__).resolve().parent / "librudp_tools.so")
 
 LAYOUT_RUDP5 = 5
 LAYOUT_RUDP7 = 7
@@ -58,7 +62,9 @@ class RudpError(RuntimeError):
 
 
 _lock = threading.Lock()
-_lib = None
+_lib = None        # the library the batch API calls (librudp.so unless tools_lib() switched it)
+_product = None
+_tools = None
 
 
 def _declare(lib: ctypes.CDLL) -> None:
@@ -92,24 +98,62 @@ def _declare(lib: ctypes.CDLL) -> None:
     lib.rudp_last_error.restype = ctypes.c_char_p
 
 
+def _load(path: Path) -> ctypes.CDLL:
+    if not path.exists():
+        raise RuntimeError(
+            f"{path} is missing: build it with "
+            "`python reliable-udp_amd/rudp/_build.py` (or __graft_entry__.build())")
+    import torch  # noqa: F401  -- bind to torch's HIP runtime first
+    handle = ctypes.CDLL(str(path))
+    _declare(handle)
+    if handle.rudp_abi_version() != ABI_VERSION:
+        raise RuntimeError(f"{path.name} ABI version mismatch; rebuild it")
+    return handle
+
+
 def lib() -> ctypes.CDLL:
-    """Load librudp.so once per process (raises if it was not built)."""
-    global _lib
+    """The library the batch API calls: librudp.so, loaded once per process
+    (raises if it was not built), unless tools_lib() made the diagnostics build
+    the active one."""
+    global _lib, _product
     if _lib is not None:
         return _lib
     with _lock:
+        if _product is None:
+            _product = _load(LIB_PATH)
         if _lib is None:
-            if not LIB_PATH.exists():
-                raise RuntimeError(
-                    f"{LIB_PATH} is missing: build it with "
-                    "`python reliable-udp_amd/rudp/_build.py` (or __graft_entry__.build())")
-            import torch  # noqa: F401  -- bind to torch's HIP runtime first
-            handle = ctypes.CDLL(str(LIB_PATH))
-            _declare(handle)
-            if handle.rudp_abi_version() != ABI_VERSION:
-                raise RuntimeError("librudp.so ABI version mismatch; rebuild it")
-            _lib = handle
+            _lib = _product
     return _lib
+
+
+def tools_lib(activate: bool = True) -> ctypes.CDLL:
+    """The diagnostics build librudp_tools.so (rudpx_tune, rudpx_encode_trace,
+    rudpx_stamp, rudpx_copy*).  ``activate``: the batch API calls it too until
+    use_product() (its knobs only act on calls made through it)."""
+    global _lib, _tools
+    with _lock:
+        if _tools is None:
+            h = _load(TOOLS_LIB_PATH)
+            P, I, U32, U64 = ctypes.c_void_p, ctypes.c_int, ctypes.c_uint32, ctypes.c_uint64
+            for name, args in {"rudpx_tune": [I, I], "rudpx_encode_trace": [P], "rudpx_stamp": [P, P],
+                               "rudpx_copy": [P, P, U64, U32, P], "rudpx_copy_vpt": [P, P, U64, I, I, P],
+                               "rudpx_copy_tile": [P, P, U64, U32, U32, P],
+                               "rudpx_copy_tile_dma": [P, P, U64, U32, U32, U32, I, P],
+                               "rudpx_copy_tile_pipe": [P, P, U64, U32, U32, U32, P]}.items():
+                fn = getattr(h, name)
+                fn.argtypes = args
+                fn.restype = I
+            _tools = h
+        if activate:
+            _lib = _tools
+    return _tools
+
+
+def use_product() -> None:
+    """Make librudp.so the library the batch API calls again."""
+    global _lib
+    with _lock:
+        _lib = _product
 
 
 def check(rc: int) -> None:

@@ -69,3 +69,12 @@ def split_by_lengths(buf, lengths):
 def golden_dedup():
     with np.load(GOLDEN / "dedup.npz") as z:
         return {k: z[k] for k in z.files}
+
+
+@pytest.fixture(autouse=True)
+def _product_library_after_each_test():
+    """Tests of the non-default kernel forms switch the batch API to the
+    diagnostics build (rudp._native.tools_lib()); every test ends on librudp.so."""
+    yield
+    from rudp import _native
+    _native.use_product()

@@ -23,11 +23,26 @@ def test_header_and_binding_agree():
     assert declared_functions() == set(_native.EXPORTS)
 
 
+def _dynamic_symbols(path):
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", str(path)], capture_output=True, text=True, check=True)
+    return {line.split()[-1] for line in out.stdout.splitlines() if line.strip()}
+
+
 def test_library_exports_every_declared_symbol():
     lib = _native.lib()
     for name in declared_functions():
         assert hasattr(lib, name), name
     assert lib.rudp_abi_version() == _native.ABI_VERSION
+
+
+def test_product_library_exports_only_the_abi():
+    """librudp.so carries the include/rudp.h ABI and nothing of the diagnostics
+    (no rudpx_* knobs, timelines or copy kernels); librudp_tools.so adds them."""
+    prod = {s for s in _dynamic_symbols(_native.LIB_PATH) if s.startswith(("rudp", "rudpx"))}
+    assert prod == declared_functions()
+    tools = {s for s in _dynamic_symbols(_native.TOOLS_LIB_PATH) if s.startswith("rudpx_")}
+    assert {"rudpx_tune", "rudpx_encode_trace", "rudpx_stamp", "rudpx_copy_vpt"} <= tools
 
 
 def test_batch_struct_layout():

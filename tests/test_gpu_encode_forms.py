@@ -16,7 +16,7 @@ pytestmark = pytest.mark.gpu
 
 
 def _lib():
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.rudpx_tune.restype = ctypes.c_int
     return lib

@@ -19,7 +19,7 @@ _KNOBS = {2: (0, 16, 32, 64, 128, 256), 23: (-1, 0, 1), 30: (-1, 0, 1, 2), 29: (
 
 
 def _lib():
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.rudpx_tune.restype = ctypes.c_int
     return lib

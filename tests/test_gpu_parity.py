@@ -246,7 +246,7 @@ def test_decode_paths_agree(cuda, L):
     """Every decode kernel (LDS tile, aligned chunks, register windows) gives the same answer."""
     import ctypes
     from rudp import _native
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     n = 3001
     seq, ack, flags, pay = synth.synth(0x77 + L, 0, n, L, ascii=False)
@@ -282,7 +282,7 @@ def test_encode_tile_sizes_agree(cuda, L):
     """Every encode tile size gives the oracle's frames (T < 16: tiles share boundary chunks)."""
     import ctypes
     from rudp import _native
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     for n in (1, 3, 4, 5, 9, 33, 1027):
         seq, ack, flags, pay = synth.synth(0x99 + L, n, n, L, ascii=False)
@@ -312,7 +312,7 @@ def test_encode_align64_vs_oracle(cuda, L):
     import ctypes
     import torch
     from rudp import _native
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     for n in (1, 5, 16, 17, 257, 1031):
         seq, ack, flags, pay = synth.synth(0x55 + L, n, n, L, ascii=False)
@@ -384,7 +384,7 @@ def test_host_pipeline_many_chunks(cuda, slots, stage_mb):
     through the slot ring in many chunks (ragged last chunk), H2D/kernel/D2H overlapped."""
     import ctypes
     from rudp import _native
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     old_slots, old_mb = lib.rudpx_tune(8, slots), lib.rudpx_tune(9, stage_mb)
     try:

@@ -163,7 +163,7 @@ def _dedup_form(table):
     import contextlib
     import ctypes
     from rudp import _native
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.rudpx_tune.restype = ctypes.c_int
 
@@ -281,7 +281,7 @@ def test_varlen_decode_kernels_vs_oracle(cuda, lo, hi, layout):
     import ctypes
     import torch
     from rudp import _native
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     rng = np.random.default_rng(lo * 7 + hi + layout)
     n = 1500 if hi < 2000 else 300
@@ -326,7 +326,7 @@ def test_varlen_encode_kernels_vs_oracle(cuda, lo, hi, layout):
     import ctypes
     import torch
     from rudp import _native
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     rng = np.random.default_rng(lo + 3 * hi + layout)
     n = 2000 if hi < 2000 else 120
@@ -381,7 +381,7 @@ def test_varlen_encode_tile_kernel_vs_oracle(cuda, dist, layout):
     import ctypes
     import torch
     from rudp import _native
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     rng = np.random.default_rng(sum(map(ord, dist)) * 10 + layout)
     n = 20011
@@ -504,7 +504,7 @@ def test_frame_offset_scans_agree(cuda, n):
     import ctypes
     import torch
     from rudp import _native
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     rng = np.random.default_rng(n)
     lens = rng.integers(0, 65536, n).astype(np.int32) if n < 10000 else \
@@ -531,7 +531,7 @@ def test_utf8_fixed_stride_tile_and_vector_kernels(cuda, L):
     16-B chunk and tile boundaries; both outcomes well represented)."""
     import ctypes
     from rudp import _native
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.rudpx_tune.restype = ctypes.c_int
     rng = np.random.default_rng(4321 + L)
@@ -586,7 +586,7 @@ def test_utf8_packed_tile_vs_python_decoder(cuda):
     import ctypes
     import torch
     from rudp import _native
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.rudpx_tune.restype = ctypes.c_int
     rng = np.random.default_rng(2468)
@@ -776,7 +776,7 @@ def test_small_frame_tiles_vs_oracle(cuda, fpt):
     import ctypes
     import torch
     from rudp import _native
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     rng = np.random.default_rng(70 + fpt)
     for n, lo, hi, burst in ((1, 0, 3, False), (255, 1, 1, False), (256 * fpt + 3, 0, 9, False),
@@ -828,7 +828,7 @@ def test_varlen_tile_forms_vs_oracle(cuda, dist):
     than a whole tile's LDS budget."""
     import ctypes
     from rudp import _native
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     rng = np.random.default_rng(sum(map(ord, dist)))
     n = 20011

@@ -22,7 +22,7 @@ import torch  # noqa: E402
 
 from rudp import _native, batch  # noqa: E402
 
-lib = _native.lib()
+lib = _native.tools_lib()
 lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
 GIB = float(1 << 30)
 

@@ -45,7 +45,7 @@ def main():
     out1 = torch.empty((M, F), dtype=torch.uint8, device=dev)
     tab16, pay16 = batch.synth_batch(16 * M, L, 0x5EED0005, device=dev)
     out16 = torch.empty((16 * M, F), dtype=torch.uint8, device=dev)
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_copy_vpt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
                                    ctypes.c_int, ctypes.c_void_p]
     stream = torch.cuda.current_stream().cuda_stream

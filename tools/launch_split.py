@@ -31,7 +31,7 @@ def main():
     ap.add_argument("--reps", type=int, default=9)
     ap.add_argument("--chunks", default="0,131072,262144,524288,1048576,2097152")
     args = ap.parse_args()
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     dev = torch.device("cuda", 0)
     L = 1472

@@ -49,7 +49,7 @@ def main():
     amdsmi.amdsmi_init()
     handles = amdsmi.amdsmi_get_processor_handles()
     dev = torch.device("cuda", 0)
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_copy_vpt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
                                    ctypes.c_int, ctypes.c_void_p]
     L, M = 1472, 1 << 20

@@ -4,7 +4,8 @@ usage: python tools/run_kernel.py --op encode|decode|roundtrip|encode_varlen|dec
           [--L 1472] [--n 1048576]
           [--layout rudp7] [--steps 20] [--ragged] [--tune 51=1,52=2]
 Prints the HIP-event time per launch so it can be set beside the profiler's
-kernel-trace average.
+kernel-trace average.  Runs librudp.so (the product) unless --tune is given,
+which needs the diagnostics build librudp_tools.so.
 """
 from __future__ import annotations
 
@@ -53,7 +54,8 @@ def main():
         sets.append((tab, pay, fr))
     import ctypes
     from rudp import _native
-    lib = _native.lib()
+    # the product library unless knobs are asked for (they live in the diagnostics build only)
+    lib = _native.tools_lib() if args.tune else _native.lib()
     for kv in filter(None, args.tune.split(",")):
         k, v = kv.split("=")
         lib.rudpx_tune(int(k), int(v))

@@ -38,7 +38,7 @@ def main():
     ap.add_argument("--n", type=int, default=1 << 20)
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
     lib.rudpx_encode_trace.argtypes = [ctypes.c_void_p]
     lib.rudpx_stamp.argtypes = [ctypes.c_void_p, ctypes.c_void_p]

@@ -34,7 +34,7 @@ def main():
                     help="also: a stamp kernel before every launch, the tile trace on")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_copy_vpt.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_int,
                                    ctypes.c_int, ctypes.c_void_p]
     L, M = args.L, 1 << 20

@@ -20,7 +20,7 @@ import torch  # noqa: E402
 
 from rudp import _native, batch  # noqa: E402
 
-lib = _native.lib()
+lib = _native.tools_lib()
 lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
 lib.rudpx_tune.restype = ctypes.c_int
 lib.rudpx_copy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32,

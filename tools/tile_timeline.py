@@ -96,7 +96,7 @@ def main():
     ap.add_argument("--tune", default="", help="rudpx_tune knobs for every shape, key=value[,key=value]")
     args = ap.parse_args()
     dev = torch.device("cuda", 0)
-    lib = _native.lib()
+    lib = _native.tools_lib()
     lib.rudpx_encode_trace.argtypes = [ctypes.c_void_p]
     lib.rudpx_stamp.argtypes = [ctypes.c_void_p, ctypes.c_void_p]
     stream = torch.cuda.current_stream().cuda_stream

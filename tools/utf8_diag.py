@@ -12,7 +12,7 @@ sys.path[:0] = [str(REPO), str(REPO / "reliable-udp_amd")]
 import torch
 from rudp import batch, _native
 import bench
-lib = _native.lib(); lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+lib = _native.tools_lib(); lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
 dev = torch.device("cuda", 0)
 w = bench.Workload(torch, batch, 1 << 20, 1472, "rudp7", 0, bench.SEEDS.get(1472, 0x5EED0004), dev)
 for i in range(3): w.encode(batch, i)
