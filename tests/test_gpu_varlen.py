@@ -937,7 +937,9 @@ def test_varlen_reuse_outputs_equal_fresh(cuda, L):
     bad = again.frame_off.clone()
     bad[17] = bad[18] + 1
     d3 = batch.unpack_batch_varlen(again.frames, bad, 5, csum=again.csum, reuse=d2, check=False)
-    assert int(d3.status.item()) == _native.ST_OFFSETS and int(d3.ok[16].item()) == _native.OK_BAD_OFFSETS
+    # frame 17 = [off[18] + 1, off[18]) is decreasing: rejected; frame 16 only grew (checksum)
+    assert int(d3.status.item()) == _native.ST_OFFSETS and int(d3.ok[17].item()) == _native.OK_BAD_OFFSETS
+    assert int((d3.ok == _native.OK_BAD_OFFSETS).sum().item()) == 1
     with pytest.raises(ValueError, match="non-decreasing"):
         d3.check()
     assert torch.equal(d3.ok[:16], torch.ones(16, dtype=torch.uint8, device=cuda))

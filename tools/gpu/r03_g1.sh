@@ -5,4 +5,5 @@ timeout -k 10 300 python -u tools/tile_timeline.py --L 64 --no-16m --sets 8 > gp
 timeout -k 10 300 python -u tools/tile_timeline.py --L 64 --no-16m --sets 8 --tune 5=1 > gpurun_out/tl64_xcd.json 2> gpurun_out/tl64_xcd.err
 bash tools/gpu/run.sh trace c3_kt tools/run_kernel.py --op encode --L 64 --steps 50
 bash tools/gpu/run.sh pmc c3 tools/run_kernel.py --op encode --L 64 --steps 20
+bash tools/gpu/run.sh bench r03a
 echo done
