@@ -612,6 +612,9 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
   }
   // Sum pass of the tile kernel: 2 = from 128-B block sums
   a.tile_sums = tuning().varlen_tile_sums == 2 ? 2u : 0u;
+#if RUDP_TOOLS
+  a.trace = tuning().encode_trace.load();  // tile-kernel phase timeline (tools/varlen_timeline.py)
+#endif
   // Tiles by payload bytes (checked calls, where the payload size is known on
   // the host): spans of S = budget - 2 * hint - 64 bytes, so a tile overflows its
   // LDS budget only through a packet over twice the hint; at most bt_slots

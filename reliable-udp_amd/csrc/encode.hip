@@ -167,20 +167,20 @@ __device__ __forceinline__ void encode_phase2_hc(const EncodeTileArgs& a, const 
 template <int H, bool NTL, bool NTS, int P1, int BLOCK = kBlock, bool DMA = false>
 __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  uint32_t tile = blockIdx.x;
+  if (a.xcd_swizzle) tile = xcd_tile(tile, a.num_tiles);  // each XCD streams its own slice
   uint64_t* lds_hdr = reinterpret_cast<uint64_t*>(lds);  // [T + 1]
   unsigned char* lds_pay = lds + a.hdr_bytes;            // guard + T*L + tail guard
 
   const uint32_t tid = threadIdx.x;
   const uint32_t L = a.L;
   const uint32_t T = a.T;
+  const uint64_t p0 = (uint64_t)tile * T;
   // a.glog is lanes-per-packet for 256-thread groups; wider (narrower) groups
   // give each packet more (fewer) lanes.  The launcher keeps T <= BLOCK.
   constexpr int kLogBlock = BLOCK == 64 ? 6 : BLOCK == 128 ? 7 : BLOCK == 512 ? 9 : BLOCK == 1024 ? 10 : 8;
   const uint32_t glog = (uint32_t)((int)a.glog + kLogBlock - 8);
   const uint32_t G = 1u << glog;
-  uint32_t tile = blockIdx.x;
-  if (a.xcd_swizzle) tile = xcd_tile(tile, a.num_tiles);  // each XCD streams its own slice
-  const uint64_t p0 = (uint64_t)tile * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
 #if RUDP_TOOLS
@@ -350,7 +350,7 @@ __global__ void __launch_bounds__(kBlock) encode_bytes_kernel(EncodeTileArgs a) 
 
 template <int H, bool NTL, bool NTS, int P1, int BLOCK = kBlock, bool DMA = false>
 int launch_tile(const EncodeTileArgs& args, hipStream_t stream) {
-  const uint64_t blocks = (args.n + args.T - 1) / args.T;
+  const uint64_t blocks = args.num_tiles;
   size_t lds = args.hdr_bytes + kLdsGuard + (size_t)args.T * args.L + 32;
   int per_cu = tuning().encode_blocks_per_cu;
   // Auto: cap resident tiles per CU by tile payload, so the concurrent HBM
@@ -368,9 +368,9 @@ int launch_tile(const EncodeTileArgs& args, hipStream_t stream) {
     const size_t want = ((size_t)(160 * 1024) / (size_t)per_cu) & ~size_t(15);
     if (want > lds) lds = want;
   }
+  const void* fn = reinterpret_cast<const void*>(&encode_tile_kernel<H, NTL, NTS, P1, BLOCK, DMA>);
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_tile_kernel<H, NTL, NTS, P1, BLOCK, DMA>),
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
   hipLaunchKernelGGL((encode_tile_kernel<H, NTL, NTS, P1, BLOCK, DMA>), dim3((uint32_t)blocks), dim3(BLOCK), lds,

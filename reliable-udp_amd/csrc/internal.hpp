@@ -305,6 +305,7 @@ struct Tuning {
   // Fixed-length encode: batches of more packets than this go out as several
   // launches of at most this many (0: one launch).
   RUDP_KNOB(encode_launch_packets, 0)
+
   // Varlen encode tiles by payload bytes (spans from the scan) instead of by
   // packet count: no tile overflows short of one packet past the budget's
   // slack.  0: packet tiles; 1: byte tiles when over 1/32 of the packet tiles

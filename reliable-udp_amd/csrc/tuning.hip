@@ -277,6 +277,9 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // 52: varlen tile sum pass (2 from 128-B block sums, 0 chunk by chunk).
 // (54: chunked / rotated XCD orders, measured within 2% and removed;
 // profiles/r02/headline/xcd_orders.json.)
+// (55, 56: a small-tile launch tail, and 57: persistent workgroups looping over the tiles,
+// for the 64-B encode: tail within +-2%, persistent 1-30% slower; removed;
+// profiles/r03/sweeps/encode64_*.json, encode_persistent_256_1024_1472.json.)
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();

@@ -304,6 +304,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   unsigned char* lds_pay = lds + vt_pay_off(Tl, cap, H, wide ? 1u : 0u);
 
   const uint32_t tid = threadIdx.x;
+#if RUDP_TOOLS
+  const uint64_t t_start = a.trace ? (uint64_t)wall_clock64() : 0ull;  // diagnostics: tile phases
+  uint64_t t_loaded = 0, t_summed = 0, t_mapped = 0;
+#endif
   // Both forms' loads go out together (one round trip): the form, the span
   // records, the packet tile's offsets.  Each form numbers its own tiles
   // (XCD-contiguous over its own count) and leaves the surplus workgroups,
@@ -414,6 +418,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     }
   }
   __syncthreads();
+#if RUDP_TOOLS
+  if (a.trace && tid == 0) t_loaded = (uint64_t)wall_clock64();
+#endif
 
   // ---- per-packet sums, header words, chunk -> frame map ------------------
   const uint32_t shift = kVTGuard + (uint32_t)(po0 & 15u);  // LDS offset of payload byte po0
@@ -462,6 +469,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     }
   }
   if (blk_sums) __syncthreads();  // the map overwrites the block sums
+#if RUDP_TOOLS
+  if (a.trace && tid == 0) t_summed = (uint64_t)wall_clock64();
+#endif
   if (q < Tv) {
     const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
     // map[k] = q for the output units k whose first byte lead + 16k lies in [fs, fe)
@@ -521,6 +531,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   // Fast phase 2 when every frame of the tile is at least kVHCMinFrame bytes:
   // then a chunk overlaps at most one header.
   const bool vfast = __syncthreads_and(q >= Tv || lds_fo[q + 1] - lds_fo[q] >= kVHCMinFrame) && a.vhc;
+#if RUDP_TOOLS
+  if (a.trace && tid == 0) t_mapped = (uint64_t)wall_clock64();
+#endif
 
   // ---- phase 2: aligned 16-B output chunks ---------------------------------
   unsigned char* out = a.frames + fo0;
@@ -615,6 +628,18 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
         out[x + b] = (unsigned char)(b < 8 ? lo >> (8 * b) : hi >> (8 * (b - 8)));
     }
   }
+#if RUDP_TOOLS
+  if (a.trace) {  // diagnostics: {start, loaded, summed, mapped, end, XCC, Tv | bt << 16 | vfast << 17, bytes}
+    __syncthreads();
+    if (tid == 0) {
+      u32x4* rec = reinterpret_cast<u32x4*>(a.trace + 8ull * blockIdx.x);
+      rec[0] = make_u32x4(t_start, t_loaded);
+      rec[1] = make_u32x4(t_summed, t_mapped);
+      rec[2] = make_u32x4((uint64_t)wall_clock64(), __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20));
+      rec[3] = make_u32x4((uint64_t)Tv | (bt ? 1ull << 16 : 0ull) | (vfast ? 1ull << 17 : 0ull), (uint64_t)nbytes);
+    }
+  }
+#endif
 }
 
 // Byte limit of a decode's frames: the caller's buffer size for checked

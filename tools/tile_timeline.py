@@ -110,8 +110,10 @@ def main():
         shapes["own_1M_early_table"] = (M, -1)
     if not args.no_16m:
         shapes["launch_16M"] = (16 * M, -1)
+    tune = {}
     for kv in filter(None, args.tune.split(",")):
         k, v = kv.split("=")
+        tune[int(k)] = int(v)
         lib.rudpx_tune(int(k), int(v))
     # packets per tile, as encode_tile_geometry (capi.hip) picks them
     T = 16
