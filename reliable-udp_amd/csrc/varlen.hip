@@ -218,13 +218,15 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_vec_kernel(VarlenArgs a)
 }
 
 // LDS layout of the varlen encode tile: header words u64[T], tile-relative
-// frame offsets u32[T + 1], the chunk -> frame map u8[] (first holding the
-// block-sum pass's u32 sums of the run's 128-B blocks), then the payload run
+// frame offsets u32[T + 1], the chunk -> frame map u8[] or u16[], the
+// block-sum pass's u32 sums of the run's 128-B blocks, then the payload run
 // (guard, cap bytes, guard).  Shared by the launcher (LDS size) and the kernel.
 constexpr uint32_t kVTGuard = 32;
 // The map holds one u8 (owner frame) per output chunk, or with the coded map
 // (vhc == 2) one u16: owner frame in bits 0-7, bit 15 = pure payload chunk,
-// else bit 8 = header chunk of the next frame and bit 9 = its slot.
+// else bit 8 = header chunk of the next frame and bit 9 = its slot; bit 14 =
+// the chunk touches a header of a frame under kVHCMinFrame bytes, which has
+// no prebuilt chunks: phase 2 walks its frames.
 __host__ __device__ inline uint32_t vt_map_bytes(uint32_t T, uint32_t cap, uint32_t H, uint32_t wide) {
   return (((cap + T * H) >> 4) + 4u) << (wide ? 1 : 0);
 }
@@ -233,9 +235,14 @@ __host__ __device__ inline uint32_t vt_map_bytes(uint32_t T, uint32_t cap, uint3
 // previous frame (the varlen tile's fast phase 2).
 constexpr uint32_t kVHCMinFrame = 32;
 
-// (the map's bytes hold the block sums, 4 B per 128 B of run, before it)
+// the block sums: one u32 per 128 B of run (own region, so the map can be
+// built while other packets' lanes still read them)
+__host__ __device__ inline uint32_t vt_blk_bytes(uint32_t cap) { return ((cap >> 7) + 4u) * 4u; }
+__host__ __device__ inline uint32_t vt_blk_off(uint32_t T, uint32_t cap, uint32_t H, uint32_t wide) {
+  return (8u * T + 4u * (T + 1u) + vt_map_bytes(T, cap, H, wide) + 3u) & ~3u;
+}
 __host__ __device__ inline uint32_t vt_pay_off(uint32_t T, uint32_t cap, uint32_t H, uint32_t wide) {
-  return (8u * T + 4u * (T + 1u) + vt_map_bytes(T, cap, H, wide) + 15u) & ~15u;
+  return (vt_blk_off(T, cap, H, wide) + vt_blk_bytes(cap) + 15u) & ~15u;
 }
 
 // The block-sum pass (tile_sums 2).  Summing a packet's payload chunk by
@@ -300,7 +307,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   const bool blk_sums = a.tile_sums == 2u;  // the block-sum pass
   uint8_t* lds_map = reinterpret_cast<uint8_t*>(lds_fo + Tl + 1u);
   uint16_t* lds_map16 = reinterpret_cast<uint16_t*>(lds_map);
-  uint32_t* lds_blk = reinterpret_cast<uint32_t*>(lds_map);  // (until the map is built)
+  uint32_t* lds_blk = reinterpret_cast<uint32_t*>(lds + vt_blk_off(Tl, cap, H, wide ? 1u : 0u));
   unsigned char* lds_pay = lds + vt_pay_off(Tl, cap, H, wide ? 1u : 0u);
 
   const uint32_t tid = threadIdx.x;
@@ -360,7 +367,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   // Header-table loads before phase 1: their latency overlaps its stream
   // instead of following the barrier.
   uint32_t t_seq = 0, t_ack = 0, t_flags = 0;
-  if (a.early_table && g == 0 && q < Tv) {
+  if (a.early_table && g < 2u && q < Tv) {  // (lanes 0 and 1 each build a header chunk)
     t_seq = a.seq_in[p0 + q];
     t_ack = a.ack_in[p0 + q];
     t_flags = a.flags_in[p0 + q];
@@ -468,10 +475,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
       }
     }
   }
-  if (blk_sums) __syncthreads();  // the map overwrites the block sums
 #if RUDP_TOOLS
-  if (a.trace && tid == 0) t_summed = (uint64_t)wall_clock64();
+  if (a.trace && tid == 0) t_summed = (uint64_t)wall_clock64();  // (thread 0's own sums done)
 #endif
+  // The map, in the same pass (the block sums have their own LDS region).
   if (q < Tv) {
     const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
     // map[k] = q for the output units k whose first byte lead + 16k lies in [fs, fe)
@@ -480,6 +487,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     if (wide) {
       // the chunk's class for the fast phase 2: pure payload of q, or one of
       // the prebuilt header chunks of q (chunk starts in q's header) or q + 1
+      // -- which exist only for frames of kVHCMinFrame bytes and up: a chunk
+      // over a shorter frame's header is left to the frame walk (bit 14)
       for (uint32_t k = klo + g; k < khi; k += G) {
         const uint32_t x = lead + 16u * k;
         const int k0 = (int)x - (int)fs;
@@ -491,6 +500,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
           const uint32_t fsp = nxt ? fe : fs;
           const int i0 = fsp >= lead ? (int)((fsp - lead) >> 4) : -1;
           e |= (nxt << 8) | ((uint32_t)((int)k - i0) & 1u) << 9;
+          const uint32_t hlen = nxt ? (q + 1u < Tv ? lds_fo[q + 2u] - fe : 0u) : fe - fs;
+          if (hlen < kVHCMinFrame) e |= 0x4000u;
         }
         lds_map16[k] = (uint16_t)e;
       }
@@ -499,28 +510,34 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     }
   }
   for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
-  if (g == 0 && q < Tv) {
+  // The header word and the frame's (up to) two header chunks: lanes 0 and 1
+  // of the packet build one chunk each (the leader both when G = 1).
+  const uint32_t hl = G >= 2u ? 2u : 1u;
+  if (g < hl && q < Tv) {
     const uint64_t p = p0 + q;
     const bool late = !early_tab;
     const uint32_t s = late ? a.seq_in[p] : t_seq, k = late ? a.ack_in[p] : t_ack,
                    f = late ? a.flags_in[p] : t_flags;
     const uint32_t c = packet_csum(sum, s, k, f);
     const uint64_t hw = pack_header<H>(s, k, f, c);
-    lds_hdr[q] = hw;
-    if (a.csum) a.csum[p] = (uint16_t)c;
+    if (g == 0) {
+      lds_hdr[q] = hw;
+      if (a.csum) a.csum[p] = (uint16_t)c;
+    }
     const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
     if (a.vhc && fe - fs >= kVHCMinFrame) {
       // This frame's header chunks (the full output chunks over [fs, fs + H))
-      // for phase 2's fast path.  Payloads are contiguous in LDS, so the 16
-      // payload bytes before this frame's payload are the previous frame's
-      // last 16 (frames of 32 B and up carry 25+ payload bytes).
+      // for phase 2's fast path.  Payloads are contiguous in LDS: the bytes of
+      // a slot-0 chunk before fs are the last payload bytes before this
+      // frame's (the map sends a chunk here only when they are the previous
+      // frame's payload, never its header).
       const uint32_t d = shift + fs - q * H;
       const u32x4 tail = window16_dw(reinterpret_cast<const uint32_t*>(lds_pay), d - 16u);
       const u32x4 head = window16_dw(reinterpret_cast<const uint32_t*>(lds_pay), d);
       const int i0 = fs >= lead ? (int)((fs - lead) >> 4) : -1;
       u32x4* hc = reinterpret_cast<u32x4*>(lds + a.hc_off) + 2u * q;
-      for (int sl = 0; sl < 2; ++sl) {
-        const int i = i0 + sl;
+      for (uint32_t sl = g; sl < 2u; sl += hl) {
+        const int i = i0 + (int)sl;
         const int X = (int)lead + 16 * i;
         if (X >= (int)(fs + H)) break;
         if (i >= 0 && (uint32_t)i < (nbytes > lead ? (nbytes - lead) >> 4 : 0u))
@@ -528,8 +545,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
       }
     }
   }
-  // Fast phase 2 when every frame of the tile is at least kVHCMinFrame bytes:
-  // then a chunk overlaps at most one header.
+  // u8 map: the fast phase 2 when every frame of the tile is at least
+  // kVHCMinFrame bytes (then a chunk overlaps at most one header); the coded
+  // map decides chunk by chunk.
   const bool vfast = __syncthreads_and(q >= Tv || lds_fo[q + 1] - lds_fo[q] >= kVHCMinFrame) && a.vhc;
 #if RUDP_TOOLS
   if (a.trace && tid == 0) t_mapped = (uint64_t)wall_clock64();
@@ -552,7 +570,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
       x = lead + 16u * i; hi_b = 16u;
       if (wide) {
         const uint32_t e = lds_map16[i];
-        if (vfast) {
+        if (!(e & 0x4000u)) {
           // pure payload: one LDS window at shift + x - (r + 1) H; otherwise a
           // prebuilt header chunk, no frame offsets needed
           const uint32_t rr = e & 0xFFu;

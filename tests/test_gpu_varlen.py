@@ -819,7 +819,7 @@ def test_small_frame_tiles_vs_oracle(cuda, fpt):
             assert np.array_equal(results[0], results[1]) and np.array_equal(results[0], results[2])
 
 
-@pytest.mark.parametrize("dist", ["ragged", "equal", "bursty", "tiny_runs", "zeros", "jumbo"])
+@pytest.mark.parametrize("dist", ["ragged", "equal", "bursty", "tiny_runs", "zeros", "jumbo", "threshold"])
 def test_varlen_tile_forms_vs_oracle(cuda, dist):
     """Varlen encode tile forms (key 51 packet / byte tiles / the device's choice;
     52 each sum pass) == the oracle, checksums included, for
@@ -846,6 +846,10 @@ def test_varlen_tile_forms_vs_oracle(cuda, dist):
     elif dist == "zeros":
         lens = rng.integers(0, 2945, n)
         lens[rng.random(n) < 0.3] = 0
+    elif dist == "threshold":  # frames around the 32-B prebuilt-header-chunk limit among MTU ones
+        lens = rng.integers(1300, 1600, n)
+        m = rng.random(n) < 0.35
+        lens[m] = rng.choice(np.array([0, 1, 9, 15, 16, 17, 23, 24, 25, 26, 27, 28, 40]), int(m.sum()))
     else:  # jumbo: a few packets over a whole tile's budget (~27 KB at a 1.5-KB hint)
         lens = rng.integers(1000, 2000, n)
         lens[rng.choice(n, 12, replace=False)] = rng.integers(30000, 60000, 12)
