@@ -627,10 +627,15 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
     const uint64_t h = in->payload_len ? in->payload_len : 1u;
     const uint64_t ptiles = (in->n + a.tile_T - 1u) / a.tile_T;
     const uint64_t S = a.tile_cap > 2u * h + 64u + h ? a.tile_cap - 2u * h - 64u : 0u;
-    uint64_t slots = 4;
-    while (S && slots < 256 && slots < 3u * S / (2u * h) + 2u) slots <<= 1;
-    if (S && (btile == 2 || varlen_btile_ok(a.tile_T, (uint32_t)slots, a.tile_cap, (uint32_t)layout, a.vhc, ptiles,
-                                           chk.payload_bytes / S + 1u))) {
+    // 1.5x a span's mean packet count + 2 (fewer, down to the mean + 2, where
+    // the slots' LDS would cost a tile per CU: each slot is 44 B, and at 1M x
+    // 1472 B 32 slots ran 4 tiles per CU instead of 5)
+    uint32_t slots = S ? (uint32_t)(3u * S / (2u * h) + 2u) : 4u;
+    if (slots < 4u) slots = 4u;
+    if (slots > 256u) slots = 256u;
+    const uint32_t min_slots = S ? (uint32_t)(S / h + 2u) : 4u;
+    if (S && (btile == 2 || varlen_btile_ok(a.tile_T, &slots, min_slots, a.tile_cap, (uint32_t)layout, a.vhc,
+                                           ptiles, chk.payload_bytes / S + 1u))) {
       spans.bytes = S;
       spans.count = chk.payload_bytes / S + 1u;
       void* buf = nullptr;

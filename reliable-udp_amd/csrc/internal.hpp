@@ -338,8 +338,8 @@ int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStr
 int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream_t stream);
 int launch_synth(const SynthArgs& args, hipStream_t stream);
 void varlen_tile_geometry(uint32_t len_hint, uint32_t* T, uint32_t* glog, uint32_t* cap);
-bool varlen_btile_ok(uint32_t tile_T, uint32_t bt_slots, uint32_t cap, uint32_t H, uint32_t vhc,
-                     uint64_t packet_tiles, uint64_t spans);
+bool varlen_btile_ok(uint32_t tile_T, uint32_t* bt_slots, uint32_t min_slots, uint32_t cap, uint32_t H,
+                     uint32_t vhc, uint64_t packet_tiles, uint64_t spans);
 int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream);
 int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream);
 int launch_validate_utf8(const Utf8Args& args, hipStream_t stream);

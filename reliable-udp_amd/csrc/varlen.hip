@@ -15,6 +15,9 @@
 // kernels (16-byte aligned chunks, G lanes per packet from the caller's
 // mean-length hint) when the buffers are 16-byte aligned, byte-granular
 // kernels (8 lanes per packet) when not.  Numbers: DESIGN.md §3.
+#include <mutex>
+#include <vector>
+
 #include "codec_device.hpp"
 #include "internal.hpp"
 #include "scan_device.hpp"
@@ -1656,19 +1659,67 @@ static size_t varlen_tile_lds(uint32_t Tl, uint32_t cap, uint32_t H, uint32_t vh
   return b;
 }
 
+// Tiles of the varlen encode kernel (waves-per-SIMD floor W) one CU holds at
+// `lds` bytes of dynamic LDS, from the runtime's occupancy calculation (its LDS
+// allocation granule and limit, the kernel's registers), cached per size: a
+// byte count over 160 KiB misjudged it (1M x 1472 B byte tiles at 31.8 KB ran
+// 4 per CU, not 5).
+template <int H, int W>
+static int vt_occupancy(size_t lds) {
+  static std::mutex mu;
+  static std::vector<std::pair<size_t, int>> cache;
+  std::lock_guard<std::mutex> lk(mu);
+  for (const auto& e : cache)
+    if (e.first == lds) return e.second;
+  const void* fn = reinterpret_cast<const void*>(&encode_varlen_tile_kernel<H, W>);
+  int nb = 0;
+  if (lds > 65536) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, (int)kBlock, lds) != hipSuccess || nb < 1)
+    nb = (int)((160u * 1024u) / lds);  // (no answer: the plain byte count)
+  cache.emplace_back(lds, nb);
+  return nb;
+}
+
+// The kernel's register budget to match its LDS occupancy: 94 VGPRs (5 waves
+// per SIMD) unconstrained, so tiles small enough for 6-7 per CU ask the
+// allocator for that many waves (a few spills in the per-packet fallback):
+// 1M x 512 B 0.259 -> 0.233 ms (W = 7), x 256 B 0.163 -> 0.153 (W = 6).  At 5
+// tiles per CU and fewer it stays unconstrained: spills cost ragged batches
+// whose tiles take the fallback (lengths uniform in [0, 2944] at W = 7: 0.80 ->
+// 1.00 ms; profiles/r01/sweeps/varlen_waves.json).
+template <int H>
+static int vt_waves(size_t lds) {
+  if (vt_occupancy<H, 7>(lds) >= 7) return 7;
+  if (vt_occupancy<H, 6>(lds) >= 6) return 6;
+  return 1;
+}
+
+template <int H>
+static int vt_tiles_per_cu(size_t lds) {
+  const int w = vt_waves<H>(lds);
+  return w == 7 ? vt_occupancy<H, 7>(lds) : w == 6 ? vt_occupancy<H, 6>(lds) : vt_occupancy<H, 1>(lds);
+}
+
 // Byte tiles of bt_slots packets as an alternative to packet tiles of tile_T:
 // only for packet tiles of 16 or fewer (hints from 1 KiB: below, ragged
 // lengths rarely overflow and byte tiles lost, lengths uniform in [0, 512]
 // 0.204 -> 0.248 ms), where their arrays leave the tiles per CU unchanged
-// (1M x 512 B: 64 slots would take 7 packet tiles per CU to 6, 8% slower) and
-// their grid is at most 5% larger (the surplus workgroups of the form not
-// taken still occupy LDS for a round trip: 4000-B hints, 50% slower).
-bool varlen_btile_ok(uint32_t tile_T, uint32_t bt_slots, uint32_t cap, uint32_t H, uint32_t vhc,
-                     uint64_t packet_tiles, uint64_t spans) {
-  constexpr size_t kLdsPerCu = 160u * 1024u;
+// (1M x 512 B: 64 slots would take 7 packet tiles per CU to 6, 8% slower) --
+// fewer slots, down to min_slots, when that keeps them so -- and their grid
+// is at most 5% larger (the surplus workgroups of the form not taken still
+// occupy LDS for a round trip: 4000-B hints, 50% slower).
+bool varlen_btile_ok(uint32_t tile_T, uint32_t* bt_slots, uint32_t min_slots, uint32_t cap, uint32_t H,
+                     uint32_t vhc, uint64_t packet_tiles, uint64_t spans) {
   if (tile_T > 16u) return false;
-  const uint32_t Tl = bt_slots > tile_T ? bt_slots : tile_T;
-  if (kLdsPerCu / varlen_tile_lds(Tl, cap, H, vhc) < kLdsPerCu / varlen_tile_lds(tile_T, cap, H, vhc)) return false;
+  auto per_cu = [&](uint32_t Tl) {
+    const size_t lds = varlen_tile_lds(Tl, cap, H, vhc);
+    return H == 7u ? vt_tiles_per_cu<7>(lds) : vt_tiles_per_cu<5>(lds);
+  };
+  const int want = per_cu(tile_T);
+  uint32_t slots = *bt_slots;
+  while (slots > tile_T && slots > min_slots && per_cu(slots) < want) --slots;
+  if ((slots > tile_T ? per_cu(slots) : want) < want) return false;
+  *bt_slots = slots;
   return spans * 20u <= packet_tiles * 21u;
 }
 
@@ -1693,9 +1744,8 @@ int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
   // The coded map costs 1 B more per output chunk.  Where that would leave
   // fewer than 4 tiles per CU (1M x 1024 B: 4 -> 3, 9% slower) the u8 map is
   // used instead (profiles/r01/sweeps/varlen_coded_map.json).
-  constexpr size_t kLdsPerCu = 160u * 1024u;
-  if (args.vhc == 2u && kLdsPerCu / varlen_tile_lds(Tl, args.tile_cap, H, 2u) < 4u &&
-      kLdsPerCu / varlen_tile_lds(Tl, args.tile_cap, H, 1u) >= 4u)
+  if (args.vhc == 2u && vt_tiles_per_cu<H>(varlen_tile_lds(Tl, args.tile_cap, H, 2u)) < 4 &&
+      vt_tiles_per_cu<H>(varlen_tile_lds(Tl, args.tile_cap, H, 1u)) >= 4)
     args.vhc = 1u;
   size_t lds = vt_pay_off(Tl, args.tile_cap, H, args.vhc == 2u ? 1u : 0u) + 2u * kVTGuard + args.tile_cap;
   if (args.vhc) {  // prebuilt header chunks [Tl][2] x 16 B after the payload run
@@ -1703,18 +1753,9 @@ int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
     args.hc_off = (uint32_t)lds;
     lds += 32u * Tl;
   }
-  // Register budget to match the LDS occupancy: the kernel needs 88 VGPRs (5
-  // waves per SIMD) unconstrained, so tiles small enough for 6-7 per CU ask
-  // the allocator for that many waves (a few spills in the per-packet
-  // fallback): 1M x 512 B 0.259 -> 0.233 ms (W = 7), x 256 B 0.163 -> 0.153
-  // (W = 6).  At 5 tiles per CU and fewer it stays unconstrained: spills cost
-  // ragged batches whose tiles take the fallback (lengths uniform in
-  // [0, 2944] at W = 7: 0.80 -> 1.00 ms; profiles/r01/sweeps/varlen_waves.json).
+  // register budget to match the LDS occupancy (vt_waves)
   int w = tuning().varlen_waves;
-  if (w < 0) {
-    const size_t per_cu = kLdsPerCu / lds;
-    w = per_cu >= 7 ? 7 : per_cu == 6 ? 6 : 1;
-  }
+  if (w < 0) w = vt_waves<H>(lds);
 #if RUDP_TOOLS
   if (w == 8) return launch_varlen_tile_w<H, 8>(args, lds, blocks, stream);
 #endif
