@@ -3,6 +3,6 @@
 set -e
 O=gpurun_out
 timeout -k 10 600 python -u -m pytest tests/test_gpu_varlen.py tests/test_gpu_fuzz.py -x -q --timeout 180 --timeout-method thread > $O/vt_tests.log 2>&1
-timeout -k 10 300 python -u tools/varlen_timeline.py > $O/vtl2.json 2> $O/vtl2.err
-bash tools/gpu/run.sh bench r03b --no-cpu-baseline
+timeout -k 10 300 python -u tools/varlen_timeline.py > $O/vtl3.json 2> $O/vtl3.err
+bash tools/gpu/run.sh bench r03c --no-cpu-baseline
 echo done
