@@ -317,6 +317,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
 #if RUDP_TOOLS
   const uint64_t t_start = a.trace ? (uint64_t)wall_clock64() : 0ull;  // diagnostics: tile phases
   uint64_t t_loaded = 0, t_summed = 0, t_mapped = 0;
+  __shared__ unsigned long long s_last[3];  // latest wave: sums, map, header chunks done
+  if (a.trace && tid < 3u) s_last[tid] = 0ull;
 #endif
   // Both forms' loads go out together (one round trip): the form, the span
   // records, the packet tile's offsets.  Each form numbers its own tiles
@@ -480,6 +482,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   }
 #if RUDP_TOOLS
   if (a.trace && tid == 0) t_summed = (uint64_t)wall_clock64();  // (thread 0's own sums done)
+  if (a.trace && (tid & 63u) == 0) atomicMax(&s_last[0], (unsigned long long)wall_clock64());
 #endif
   // The map, in the same pass (the block sums have their own LDS region).
   if (q < Tv) {
@@ -512,6 +515,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
       for (uint32_t k = klo + g; k < khi; k += G) lds_map[k] = (uint8_t)q;
     }
   }
+#if RUDP_TOOLS
+  if (a.trace && (tid & 63u) == 0) atomicMax(&s_last[1], (unsigned long long)wall_clock64());
+#endif
   for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
   // The header word and the frame's (up to) two header chunks: lanes 0 and 1
   // of the packet build one chunk each (the leader both when G = 1).
@@ -548,6 +554,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
       }
     }
   }
+#if RUDP_TOOLS
+  if (a.trace) atomicMax(&s_last[2], (unsigned long long)wall_clock64());  // (after its lanes' stores)
+#endif
   // u8 map: the fast phase 2 when every frame of the tile is at least
   // kVHCMinFrame bytes (then a chunk overlaps at most one header); the coded
   // map decides chunk by chunk.
@@ -650,14 +659,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     }
   }
 #if RUDP_TOOLS
-  if (a.trace) {  // diagnostics: {start, loaded, summed, mapped, end, XCC, Tv | bt << 16 | vfast << 17, bytes}
+  if (a.trace) {  // diagnostics: {start, loaded, summed, mapped, end, XCC, Tv | bt << 16 | vfast << 17, bytes,
+                  //               latest wave's sums, map, header chunks done, 0}
     __syncthreads();
     if (tid == 0) {
-      u32x4* rec = reinterpret_cast<u32x4*>(a.trace + 8ull * blockIdx.x);
+      u32x4* rec = reinterpret_cast<u32x4*>(a.trace + 12ull * blockIdx.x);
       rec[0] = make_u32x4(t_start, t_loaded);
       rec[1] = make_u32x4(t_summed, t_mapped);
       rec[2] = make_u32x4((uint64_t)wall_clock64(), __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20));
       rec[3] = make_u32x4((uint64_t)Tv | (bt ? 1ull << 16 : 0ull) | (vfast ? 1ull << 17 : 0ull), (uint64_t)nbytes);
+      rec[4] = make_u32x4(s_last[0], s_last[1]);
+      rec[5] = make_u32x4(s_last[2], 0ull);
     }
   }
 #endif

@@ -3,7 +3,8 @@
 Every workgroup that frames a tile records (rudpx_encode_trace, tools build):
 start, phase-1 loads landed, sums done, chunk map + header words done, end
 (100 MHz wall clock), its XCD, its packet count, whether it was a byte tile and
-took the fast phase 2, and its frame bytes.  For each shape and form this
+took the fast phase 2, its frame bytes, and when its last wave finished its
+sums, its map and its header chunks.  For each shape and form this
 prints per-phase percentiles (us), the span, resident tiles, and the share of
 tiles on the slow phase 2.
 
@@ -57,7 +58,12 @@ def analyse(rec):
            "median_resident": float(np.median(conc[:max(1, int(span))])),
            "packets_per_tile": pct(tv), "slow_phase2_share": float(1 - fast.mean()),
            "load_us": pct(d(t0, tl)), "sums_us": pct(d(tl, ts)), "map_hdr_us": pct(d(ts, tm)),
-           "phase2_us": pct(d(tm, te)), "tile_us": pct(d(t0, te))}
+           "phase2_us": pct(d(tm, te)), "tile_us": pct(d(t0, te)),
+           # from the phase-1 barrier to the LAST wave's sums / map / header chunks done
+           "last_wave_sums_us": pct(d(tl, rec[:, 8].astype(np.int64))),
+           "last_wave_map_us": pct(d(tl, rec[:, 9].astype(np.int64))),
+           "last_wave_hdr_us": pct(d(tl, rec[:, 10].astype(np.int64))),
+           "barrier_after_hdr_us": pct(d(rec[:, 10].astype(np.int64), tm))}
     for name, m in (("fast", fast == 1), ("slow", fast == 0)):
         if m.any():
             out[f"phase2_us_{name}"] = pct(d(tm, te)[m])
@@ -83,7 +89,7 @@ def main():
     out = {}
     for name, (t, flat, ln) in shapes.items():
         blocks = flat.numel() // 1000 + n // 8 + 16
-        buf = torch.zeros((blocks * 8,), dtype=torch.int64, device=dev)
+        buf = torch.zeros((blocks * 12,), dtype=torch.int64, device=dev)
         for form, key in (("packet_tiles", 0), ("byte_tiles", 2)):
             lib.rudpx_tune(51, key)
             res = batch.pack_batch_varlen(t, flat, ln, "rudp7")
@@ -105,7 +111,7 @@ def main():
                 batch.pack_batch_varlen(t, flat, ln, "rudp7", reuse=res, check=False)
                 lib.rudpx_encode_trace(None)
                 torch.cuda.synchronize()
-                rec = buf.view(-1, 8).cpu().numpy()
+                rec = buf.view(-1, 12).cpu().numpy()
                 if args.save:
                     np.save(Path(args.save) / f"vtile_{name}_{form}_{k}.npy", rec[rec[:, 0] != 0])
                 runs.append(analyse(rec))
