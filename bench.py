@@ -471,6 +471,9 @@ def legs(torch, batch, device, steps):
     # socket boundary: 1M one-character frames sendmmsg'd over loopback, recvmmsg'd into a
     # pinned ring and decoded on the GPU per received batch (rudp.netio)
     out["socket_e2e_1M_x_1char"] = socket_leg(torch, batch, device)
+    # the proxy's role with many datagrams in flight: the batched relay (recvmmsg with
+    # sources, GPU retransmission flags, sendmmsg) beside the per-datagram one
+    out["relay_1char"] = relay_leg(torch, batch, device)
     # device-to-device streaming-copy ceiling, same byte count as one encode's payload:
     # the fastest copy in tools/sweep.py (one dwordx4 per thread, nt loads and stores,
     # rudpx_copy_vpt) and, for reference, the grid-stride copy (rudpx_copy, 65536 blocks)
@@ -525,6 +528,61 @@ def socket_leg(torch, batch, device, n=1 << 20):
     return {"received": got, "verified": good, "batches": batches, "wall_s": dt,
             "Mpkt_s": got / dt / 1e6,
             "note": "loopback kernel UDP stack bound; sendmmsg/recvmmsg 1024 per call"}
+
+
+def relay_leg(torch, batch, device):
+    """Datagrams through rudp.relay.Relay in proxy.py's role (proxy.py:126-154):
+    a client blasts one-character frames (sendmmsg) at the relay, which forwards
+    them to a sink in the server's place; the sink counts what arrives.  Batched
+    relay over 256K datagrams, per-datagram relay over 32K; datagrams/s from the
+    first send to the last datagram at the sink, and the relay's counters (every
+    datagram distinct: no retransmissions).  Loopback UDP may drop under load;
+    the received counts say how many made it."""
+    import socket
+    import threading
+
+    import numpy as np
+    from rudp import netio
+    from rudp.relay import Relay
+    out = {}
+    for name, n, batched in (("batched", 1 << 18, True), ("per_datagram", 1 << 15, False)):
+        tab, pay = batch.synth_batch(n, 1, SEEDS[1472], device=device)
+        tab.seq.copy_(torch.arange(n, device=device).to(torch.int32).to(torch.uint16))  # distinct frames
+        enc = batch.pack_batch_varlen(tab, pay.view(-1), torch.ones(n, dtype=torch.int32, device=device), "rudp5")
+        frames, off = enc.frames.cpu().numpy(), enc.frame_off.cpu().numpy()
+        sink = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        sink.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 26)
+        sink.bind(("127.0.0.1", 0))
+        relay = Relay(sink.getsockname()[1], batched=batched, device=device if batched else None)
+        relay.sock.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 26)
+        relay.start()
+        tx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+        got = [0]
+        rbuf, roff = np.empty((1 << 16) * 64, np.uint8), np.empty((1 << 16) + 1, np.int64)
+
+        def drain():
+            while True:
+                k = netio.recv_batch(sink, rbuf, roff, slot_bytes=64, timeout_ms=500)
+                if k == 0:
+                    break
+                got[0] += k
+        t = threading.Thread(target=drain)
+        t.start()
+        t0 = time.perf_counter()
+        for a in range(0, n, 4096):  # paced in 4096-datagram bursts
+            b = min(n, a + 4096)
+            netio.send_batch(tx, frames, off[a:b + 1], "127.0.0.1", relay.port)
+        t.join()
+        dt = time.perf_counter() - t0 - 0.5  # minus the sink's final idle timeout
+        relay.stop()
+        tx.close()
+        sink.close()
+        out[name] = {"sent": n, "relayed_to_sink": got[0], "wall_s": dt, "Mpkt_s": got[0] / dt / 1e6,
+                     "relay_batches": relay.batches, "relay_stats": relay.stats}
+    out["note"] = ("client -> relay -> sink over loopback, 1-char frames in 4096-datagram sendmmsg bursts; "
+                   "batched: recvmmsg of up to 1024 with sources, one rudp_dedup_window launch per batch "
+                   "(500-deep history carried over), sendmmsg to per-datagram destinations")
+    return out
 
 
 def config1_loopback():
