@@ -29,7 +29,7 @@ from __future__ import annotations
 import socket
 import threading
 from collections import Counter, deque
-from typing import Callable, Dict, List
+from typing import Callable, Dict, List, Optional
 
 import numpy as np
 
@@ -41,12 +41,15 @@ class Relay(threading.Thread):
     """Forward between one client and the server at ``server_port``.
 
     ``drop(direction, index) -> bool`` decides per datagram ("c2s" / "s2c",
-    the datagram's index in that direction).  ``log`` keeps every datagram
-    seen per direction; ``stats`` mirrors proxy.py's live_stats counters.
+    the datagram's index in that direction; None: nothing is dropped).
+    ``log`` keeps every datagram seen per direction (``keep_log=False``: only
+    the per-direction counts, for throughput runs); ``stats`` mirrors
+    proxy.py's live_stats counters.
     """
 
-    def __init__(self, server_port: int, drop: Callable[[str, int], bool] = lambda d, i: False,
-                 host: str = "127.0.0.1", batched: bool = False, device=None, max_msgs: int = 1024):
+    def __init__(self, server_port: int, drop: Optional[Callable[[str, int], bool]] = None,
+                 host: str = "127.0.0.1", batched: bool = False, device=None, max_msgs: int = 1024,
+                 keep_log: bool = True):
         super().__init__(daemon=True)
         self.sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
         self.sock.bind((host, 0))
@@ -55,7 +58,9 @@ class Relay(threading.Thread):
         self.server = (host, server_port)
         self.client = None
         self.drop = drop
+        self.keep_log = keep_log
         self.log: Dict[str, List[bytes]] = {"c2s": [], "s2c": []}
+        self.seen = {"c2s": 0, "s2c": 0}  # datagrams per direction (the drop rule's index)
         self.stats = {f"{side}_{k}": 0 for side in ("client", "server")
                       for k in ("sent", "received", "dropped", "retransmitted")}
         self._history: deque = deque()
@@ -118,22 +123,31 @@ class Relay(threading.Thread):
         """Record and forward one received batch (the per-datagram loop's work, batched)."""
         from . import netio
         k = off.shape[0] - 1
-        dst = np.zeros(k, np.uint64)
-        dropped = np.zeros(k, bool)
         from_server = src == self._server_key
-        for i in range(k):
-            data = frames[off[i]:off[i + 1]].tobytes()
-            if from_server[i]:
-                direction = "s2c"
-            else:
-                direction = "c2s"
-                self.client = netio.key_addr(int(src[i]))
-                self._client_key = int(src[i])
-            index = len(self.log[direction])
-            self.log[direction].append(data)
-            dropped[i] = bool(self.drop(direction, index))
-            # a server datagram before any client one has nowhere to go (dst 0: not sent)
-            dst[i] = self._server_key if not from_server[i] else (self._client_key or 0)
+        n_s = int(from_server.sum())
+        first = {"s2c": self.seen["s2c"], "c2s": self.seen["c2s"]}
+        self.seen["s2c"] += n_s
+        self.seen["c2s"] += k - n_s
+        dropped = np.zeros(k, bool)
+        if self.keep_log or self.drop is not None:
+            idx = {"s2c": first["s2c"], "c2s": first["c2s"]}
+            for i in range(k):
+                direction = "s2c" if from_server[i] else "c2s"
+                if self.keep_log:
+                    self.log[direction].append(frames[off[i]:off[i + 1]].tobytes())
+                if self.drop is not None:
+                    dropped[i] = bool(self.drop(direction, idx[direction]))
+                idx[direction] += 1
+        # the client is the source of the latest client datagram (proxy.py:133-135):
+        # a server datagram goes to the client known when it arrived
+        pos = np.where(~from_server, np.arange(k), -1)
+        last = np.maximum.accumulate(pos)
+        prev = np.uint64(self._client_key or 0)
+        to_client = np.where(last >= 0, src[np.maximum(last, 0)], prev)
+        dst = np.where(from_server, to_client, np.uint64(self._server_key)).astype(np.uint64)
+        if n_s < k:
+            self._client_key = int(src[pos.max()])
+            self.client = netio.key_addr(self._client_key)
         dup = self._dup_flags(frames, off)
         # proxy.py:79-94, summed over the batch
         for side, m in (("server", from_server), ("client", ~from_server)):
@@ -142,6 +156,7 @@ class Relay(threading.Thread):
             self.stats[f"{side}_dropped"] += int((m & dropped).sum())
             self.stats[f"{other}_received"] += int((m & ~dropped).sum())
             self.stats[f"{side}_retransmitted"] += int((m & dup).sum())
+        # a server datagram before any client one has nowhere to go (dst 0: not sent)
         send = ~dropped & (dst != 0)
         if send.any():
             lens = np.diff(off)
@@ -175,9 +190,11 @@ class Relay(threading.Thread):
             if not from_server:
                 self.client = addr
             direction = "s2c" if from_server else "c2s"
-            index = len(self.log[direction])
-            self.log[direction].append(data)
-            dropped = bool(self.drop(direction, index))
+            index = self.seen[direction]
+            self.seen[direction] += 1
+            if self.keep_log:
+                self.log[direction].append(data)
+            dropped = bool(self.drop(direction, index)) if self.drop is not None else False
             self._record("server" if from_server else "client", data, dropped)
             if not dropped:
                 self.sock.sendto(data, self.client if from_server else self.server)
