@@ -1,0 +1,112 @@
+"""Interleaved A/B of one rudpx_tune knob (tools build) on the codec's BASELINE shapes.
+
+For every shape, each knob value's launches run in rotation (median of
+--reps rounds of --inner back-to-back calls, HIP events), and every value's
+output is compared byte for byte with the first value's.
+
+shapes: encode:L (fixed-length, 1M x L, rotating sets below 1 GiB), varlen:L
+(packed, equal lengths), ragged (lengths uniform in [0, 2944]), decode:L.
+
+usage: python tools/knob_ab.py --knob 58 --values 0,1 --shapes encode:1472,encode:64,varlen:1472,ragged
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import statistics
+import sys
+from pathlib import Path
+
+REPO = Path(__file__).resolve().parent.parent
+sys.path[:0] = [str(REPO), str(REPO / "reliable-udp_amd")]
+
+import torch  # noqa: E402
+
+from rudp import _native, batch  # noqa: E402
+
+
+def make_shape(spec, dev):
+    n = 1 << 20
+    kind, _, arg = spec.partition(":")
+    if kind in ("encode", "decode"):
+        L = int(arg)
+        nsets = max(1, min(8, math.ceil((1 << 30) / (n * (2 * L + 12)))))
+        sets = []
+        for _ in range(nsets):
+            tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
+            fr, _ = batch.pack_batch(tab, pay, 7)
+            sets.append((tab, pay, fr))
+        cur = [0]
+
+        def run():
+            tab, pay, fr = sets[cur[0] % len(sets)]
+            cur[0] += 1
+            if kind == "encode":
+                batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
+                return fr
+            return batch.unpack_batch(fr, 7).ok
+        return run
+    g = torch.Generator(device=dev).manual_seed(0x5EED0004)
+    if kind == "varlen":
+        L = int(arg)
+        tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
+        flat, lens = pay.view(-1), torch.full((n,), L, dtype=torch.int32, device=dev)
+    else:  # ragged
+        lens = torch.randint(0, 2945, (n,), dtype=torch.int32, device=dev, generator=g)
+        tab, _ = batch.synth_batch(n, 0, 0x5EED0004, device=dev)
+        flat = torch.randint(0, 256, (int(lens.sum().item()),), dtype=torch.uint8, device=dev, generator=g)
+    res = batch.pack_batch_varlen(tab, flat, lens, 7)
+
+    def run():
+        batch.pack_batch_varlen(tab, flat, lens, 7, reuse=res, check=False)
+        return res.frames
+    return run
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--knob", type=int, required=True)
+    ap.add_argument("--values", required=True)
+    ap.add_argument("--shapes", required=True)
+    ap.add_argument("--reps", type=int, default=9)
+    ap.add_argument("--inner", type=int, default=10)
+    args = ap.parse_args()
+    lib = _native.tools_lib()
+    dev = torch.device("cuda", 0)
+    values = [int(v) for v in args.values.split(",")]
+    default = lib.rudpx_tune(args.knob, values[0])
+    out = {"knob": args.knob, "values": values, "shapes": {}}
+    for spec in args.shapes.split(","):
+        run = make_shape(spec, dev)
+        ref = None
+        exact = {}
+        for v in values:
+            lib.rudpx_tune(args.knob, v)
+            got = run().clone()
+            torch.cuda.synchronize()
+            if ref is None:
+                ref = got
+            exact[v] = bool(torch.equal(got, ref))
+        times = {v: [] for v in values}
+        for _ in range(args.reps):
+            for v in values:
+                lib.rudpx_tune(args.knob, v)
+                run()
+                s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                s.record()
+                for _ in range(args.inner):
+                    run()
+                e.record()
+                e.synchronize()
+                times[v].append(s.elapsed_time(e) / args.inner)
+        out["shapes"][spec] = {"ms": {v: statistics.median(t) for v, t in times.items()}, "exact": exact}
+        print(spec, out["shapes"][spec], file=sys.stderr, flush=True)
+        del run
+        torch.cuda.empty_cache()
+    lib.rudpx_tune(args.knob, default)
+    print(json.dumps(out, indent=1))
+
+
+if __name__ == "__main__":
+    main()
