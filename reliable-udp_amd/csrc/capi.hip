@@ -149,7 +149,6 @@ EncodeTileArgs make_encode_args(const rudp_batch* in, uint8_t* frames, uint16_t*
     // measured equal or 0.4-1.3% faster from 64 to 1472 B;
     // profiles/r01/sweeps/align64_after_dma.json).
     a.out_align64 = al != 0 ? 1u : 0u;
-    a.win128 = tuning().lds_win128 ? 1u : 0u;
   }
   return a;
 }
@@ -613,7 +612,6 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
   }
   // Sum pass of the tile kernel: 2 = from 128-B block sums
   a.tile_sums = tuning().varlen_tile_sums == 2 ? 2u : 0u;
-  a.win128 = tuning().lds_win128 ? 1u : 0u;
 #if RUDP_TOOLS
   a.trace = tuning().encode_trace.load();  // tile-kernel phase timeline (tools/varlen_timeline.py)
 #endif

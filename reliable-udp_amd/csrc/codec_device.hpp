@@ -117,16 +117,6 @@ __device__ __forceinline__ u32x4 funnel32(u32x4 a, u32x4 b, uint32_t sh) {
   return r;
 }
 
-// The same window from two aligned 16-B LDS reads (ds_read_b128) and a byte
-// funnel: lanes reading consecutive chunks hit consecutive banks, where the
-// five dword reads of window16_dw at a 16-B lane stride are 4-way bank
-// conflicts.  base16 is 16-byte aligned and 16 bytes past the window are
-// readable.
-__device__ __forceinline__ u32x4 window16_b128(const unsigned char* base16, uint32_t byte_off) {
-  const u32x4* p = reinterpret_cast<const u32x4*>(base16) + (byte_off >> 4);
-  return funnel32(p[0], p[1], byte_off & 15u);
-}
-
 // 16 bytes at frames[off], off 16-byte aligned; bytes at or past `total`
 // read as zero (only the last packets of a batch take the byte path).
 __device__ __forceinline__ u32x4 load16_guarded(const unsigned char* frames, uint64_t off,

@@ -151,8 +151,7 @@ __device__ __forceinline__ void encode_phase2_hc(const EncodeTileArgs& a, const 
     const uint32_t ph = r < (uint32_t)H ? qq : qq + 1u;  // packet whose header the chunk holds
     u32x4 v;
     if ((r >= (uint32_t)H && r + 16u <= F) || ph >= Tv) {
-      const uint32_t off = kLdsGuard + qq * L + r - H;
-      v = a.win128 ? window16_b128(lds_pay, off) : window16_dw(pay_dw, off);
+      v = window16_dw(pay_dw, kLdsGuard + qq * L + r - H);
     } else {
       v = lds_hc[2u * ph + ((x - ((ph * F) & ~15u)) >> 4)];
     }

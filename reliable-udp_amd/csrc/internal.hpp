@@ -45,7 +45,6 @@ struct EncodeTileArgs {
   uint32_t hc_off;          // LDS byte offset of the header-chunk array [T + 1][2] x 16 B
   uint32_t hc_scratch;      // leaders build header chunks through a 48-B LDS scratch per packet
   uint32_t scr_off;         // LDS byte offset of that scratch [T][48 B]
-  uint32_t win128;          // phase-2 payload windows from aligned 16-B LDS reads (window16_b128)
 #if RUDP_TOOLS
   uint64_t* trace;          // diagnostics (rudpx_encode_trace): per tile {start, end, XCC, CU}
 #endif
@@ -147,7 +146,6 @@ struct VarlenArgs {
   uint32_t bt_slots;
   uint32_t tile_Tl;
   uint32_t tile_sums;             // tile sum pass: 2 from 128-B block sums, 0 chunk by chunk
-  uint32_t win128;                // tile phase 2: payload windows from aligned 16-B LDS reads
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -319,7 +317,6 @@ struct Tuning {
   // 1472 B 0.544 -> 0.527 ms, lengths uniform in [0, 2944] 0.808 -> 0.729
   // (profiles/r02/sweeps/ragged_blocksums.json).
   RUDP_KNOB(varlen_tile_sums, 2)
-  RUDP_KNOB(lds_win128, 0)     // encode phase-2 LDS windows: 1 aligned ds_read_b128 pairs, 0 dword reads
   RUDP_KNOB(host_slots, 3)     // *_host pipeline: device staging slots (2..8)
   RUDP_KNOB(host_stage_mb, 128)  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
 };

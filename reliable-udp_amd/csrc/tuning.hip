@@ -280,7 +280,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // (55, 56: a small-tile launch tail, and 57: persistent workgroups looping over the tiles,
 // for the 64-B encode: tail within +-2%, persistent 1-30% slower; removed;
 // profiles/r03/sweeps/encode64_*.json, encode_persistent_256_1024_1472.json.)
-// 58: encode / varlen-encode phase-2 LDS windows from aligned ds_read_b128 pairs (1) or dword reads (0).
+// (58: phase-2 LDS windows from aligned ds_read_b128 pairs: 20x fewer bank conflicts, same
+// kernel time; removed; profiles/r03/sq_counters_encode_tiles.json.)
 // Returns the old value.
 int rudpx_tune(int key, int value) {
   rudp::Tuning& t = rudp::tuning();
@@ -315,7 +316,7 @@ int rudpx_tune(int key, int value) {
             : key == 49 ? &t.tile_xcd
             : key == 50 ? &t.varlen_small_fused
             : key == 51 ? &t.varlen_btile
-            : key == 52 ? &t.varlen_tile_sums : key == 58 ? &t.lds_win128 : nullptr;
+            : key == 52 ? &t.varlen_tile_sums : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }

@@ -588,8 +588,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
           const uint32_t rr = e & 0xFFu;
           u32x4 v;
           if (e & 0x8000u)
-            v = a.win128 ? window16_b128(lds_pay, shift + x - (rr + 1u) * (uint32_t)H)
-                         : window16_dw(pay_dw, shift + x - (rr + 1u) * (uint32_t)H);
+            v = window16_dw(pay_dw, shift + x - (rr + 1u) * (uint32_t)H);
           else
             v = reinterpret_cast<const u32x4*>(lds + a.hc_off)[2u * (rr + ((e >> 8) & 1u)) + ((e >> 9) & 1u)];
           __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(out + x));
