@@ -219,11 +219,25 @@ int rudp_validate_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_n
  * get_hex(), so an empty datagram equals 00 00 00 00 00) one of frames
  * max(0, i - window) .. i-1.  window <= 4096 (the proxy uses 500).  To carry
  * history across batches, prepend the previous batch's last `window` frames.
- * Frames as in rudp_decode (fixed stride or n+1 offsets).
+ * Frames as in rudp_decode (fixed stride or n+1 offsets; with offsets
+ * frame_len is a typical-length hint that picks lanes per frame).
  */
 int rudp_dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
                       uint32_t frame_len, uint64_t n, uint32_t window, uint8_t* d_dup, int device,
                       void* hip_stream);
+
+/*
+ * rudp_dedup_window over packed frames with the argument check on the device
+ * (ABI 5; the sync-free form the Python layer uses): every frame checks its
+ * own pair of offsets against [0, frames_bytes]; a frame whose offsets are
+ * decreasing or past the buffer gets d_dup = RUDP_DUP_BAD_OFFSETS, none of its
+ * bytes is read, and it equals no other frame.  len_hint: the mean frame
+ * length (picks lanes per frame, never the result).
+ */
+#define RUDP_DUP_BAD_OFFSETS 2
+int rudp_dedup_window_checked(const uint8_t* d_frames, uint64_t frames_bytes, const uint64_t* d_frame_off,
+                              uint32_t len_hint, uint64_t n, uint32_t window, uint8_t* d_dup, int device,
+                              void* hip_stream);
 
 /*
  * Batched UDP socket I/O (host only, no device work): the reference moves one

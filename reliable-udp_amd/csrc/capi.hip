@@ -782,9 +782,9 @@ int rudp_validate_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_n
   return 0;
 }
 
-int rudp_dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
-                      uint32_t frame_len, uint64_t n, uint32_t window, uint8_t* d_dup, int device,
-                      void* hip_stream) {
+static int dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, uint32_t frame_len,
+                        uint64_t n, uint32_t window, uint8_t* d_dup, int device, void* hip_stream,
+                        bool checked, uint64_t frames_bytes) {
   if (window > dedup_max_window())
     return fail(RUDP_EINVAL, "window %u exceeds %u", window, dedup_max_window());
   if (n == 0) return 0;
@@ -801,6 +801,11 @@ int rudp_dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_nu
   a.F = frame_len;
   a.window = window;
   a.dup = d_dup;
+  // lanes per frame for the hash pass from the (typical) frame length: 1 for the
+  // reference's 6-9 B datagrams, 2 to 64 B, 4 to 256 B, 8 above
+  a.glog = frame_len <= 16u ? 0u : frame_len <= 64u ? 1u : frame_len <= 256u ? 2u : 3u;
+  a.lim_checked = checked ? 1u : 0u;
+  a.frames_lim = frames_bytes;
   void* scratch = nullptr;
   RUDP_HIP(stream_alloc(&scratch, n * sizeof(uint64_t), s));
   a.hash = (uint64_t*)scratch;
@@ -809,6 +814,19 @@ int rudp_dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_nu
   if (rc) return hip_fail((hipError_t)rc, "dedup launch");
   if (e != hipSuccess) return hip_fail(e, "hipFreeAsync");
   return 0;
+}
+
+int rudp_dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
+                      uint32_t frame_len, uint64_t n, uint32_t window, uint8_t* d_dup, int device,
+                      void* hip_stream) {
+  return dedup_window(d_frames, d_frame_off_or_null, frame_len, n, window, d_dup, device, hip_stream, false, 0);
+}
+
+int rudp_dedup_window_checked(const uint8_t* d_frames, uint64_t frames_bytes, const uint64_t* d_frame_off,
+                              uint32_t len_hint, uint64_t n, uint32_t window, uint8_t* d_dup, int device,
+                              void* hip_stream) {
+  if (!d_frame_off) return fail(RUDP_EINVAL, "rudp_dedup_window_checked: frame_off is NULL");
+  return dedup_window(d_frames, d_frame_off, len_hint, n, window, d_dup, device, hip_stream, true, frames_bytes);
 }
 
 int rudp_encode_host(const rudp_batch* h_in, uint8_t* h_frames, uint16_t* h_csum_or_null,

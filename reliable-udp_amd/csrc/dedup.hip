@@ -9,7 +9,8 @@
 // with == meaning equal get_hex(): equal bytes, except that an empty datagram
 // parses as the 40-bit zero header (utils/packet.py:16), i.e. equals 00 00 00 00 00.
 //
-//   pass 1  hash: G = 8 lanes per frame, h = sum over bytes of
+//   pass 1  hash: G lanes per frame (1 for the reference's 6-9 B datagrams,
+//           up to 8 from 256-B frames), h = sum over bytes of
 //           mix64(position << 8 | byte) (order-sensitive, associative, so the
 //           lanes can split the frame), plus the length.
 //   pass 2  window: each workgroup stages the hashes of its 256 frames and the
@@ -34,15 +35,24 @@ __device__ __forceinline__ uint64_t dmix(uint64_t z) {
   return z ^ (z >> 31);
 }
 
-// The bytes Packet(frame).get_hex() spells: the frame, or 5 zero bytes when it is empty.
-__device__ __forceinline__ void frame_span(const DedupArgs& a, uint64_t i, uint64_t* off, uint32_t* len) {
+// The bytes Packet(frame).get_hex() spells: the frame, or 5 zero bytes when it
+// is empty.  False (and an empty span) for a checked call's frame whose offsets
+// are decreasing or past the buffer: none of its bytes is read.
+__device__ __forceinline__ bool frame_span(const DedupArgs& a, uint64_t i, uint64_t* off, uint32_t* len) {
   if (a.frame_off) {
-    *off = a.frame_off[i];
-    *len = (uint32_t)(a.frame_off[i + 1] - *off);
+    const uint64_t fo = a.frame_off[i], fe = a.frame_off[i + 1];
+    if (a.lim_checked && (fo > fe || fe > a.frames_lim)) {
+      *off = 0;
+      *len = 0;
+      return false;
+    }
+    *off = fo;
+    *len = (uint32_t)(fe - fo);
   } else {
     *off = i * (uint64_t)a.F;
     *len = a.F;
   }
+  return true;
 }
 
 __device__ __forceinline__ uint32_t canon_byte(const DedupArgs& a, uint64_t off, uint32_t len, uint32_t k) {
@@ -50,20 +60,21 @@ __device__ __forceinline__ uint32_t canon_byte(const DedupArgs& a, uint64_t off,
 }
 
 __global__ void __launch_bounds__(kBlock) dedup_hash_kernel(DedupArgs a) {
-  const uint32_t g = threadIdx.x & (kDedupLanes - 1u);
-  const uint64_t i = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / kDedupLanes;
+  const uint32_t G = 1u << a.glog;
+  const uint32_t g = threadIdx.x & (G - 1u);
+  const uint64_t i = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) >> a.glog;
   const bool valid = i < a.n;
   uint64_t h = 0;
   uint32_t len = 0;
   if (valid) {
     uint64_t off;
-    frame_span(a, i, &off, &len);
+    const bool ok = frame_span(a, i, &off, &len);
     const uint32_t clen = len ? len : 5u;
-    for (uint32_t k = g; k < clen; k += kDedupLanes)
+    for (uint32_t k = g; ok && k < clen; k += G)
       h += dmix(((uint64_t)k << 8) | canon_byte(a, off, len, k));
     if (g == 0) h += dmix(0xFFFFFFFF00000000ull | clen);
   }
-  for (uint32_t m = kDedupLanes >> 1; m > 0; m >>= 1) {
+  for (uint32_t m = G >> 1; m > 0; m >>= 1) {
     const uint32_t lo = __shfl_xor((uint32_t)h, (int)m, 64);
     const uint32_t hi = __shfl_xor((uint32_t)(h >> 32), (int)m, 64);
     h += ((uint64_t)hi << 32) | lo;
@@ -74,8 +85,7 @@ __global__ void __launch_bounds__(kBlock) dedup_hash_kernel(DedupArgs a) {
 __device__ bool frames_equal(const DedupArgs& a, uint64_t i, uint64_t j) {
   uint64_t oi, oj;
   uint32_t li, lj;
-  frame_span(a, i, &oi, &li);
-  frame_span(a, j, &oj, &lj);
+  if (!frame_span(a, i, &oi, &li) || !frame_span(a, j, &oj, &lj)) return false;
   const uint32_t ci = li ? li : 5u, cj = lj ? lj : 5u;
   if (ci != cj) return false;
   // 16 bytes of each frame per step, all loads issued before the compares
@@ -108,7 +118,9 @@ __global__ void __launch_bounds__(kBlock) dedup_window_kernel(DedupArgs a) {
       break;
     }
   }
-  a.dup[i] = dup;
+  uint64_t o;
+  uint32_t l;
+  a.dup[i] = frame_span(a, i, &o, &l) ? dup : (uint8_t)RUDP_DUP_BAD_OFFSETS;
 }
 
 // Table form of pass 2: LDS = hashes [cnt] u64, chain links [cnt] i32, bucket
@@ -144,12 +156,14 @@ __global__ void __launch_bounds__(kBlock) dedup_table_kernel(DedupArgs a, uint32
       break;
     }
   }
-  a.dup[i] = dup;
+  uint64_t o;
+  uint32_t l;
+  a.dup[i] = frame_span(a, i, &o, &l) ? dup : (uint8_t)RUDP_DUP_BAD_OFFSETS;
 }
 
 int launch_dedup(const DedupArgs& args, hipStream_t stream) {
   if (args.n == 0) return 0;
-  const uint64_t hblocks = (args.n * kDedupLanes + kBlock - 1) / kBlock;
+  const uint64_t hblocks = ((args.n << args.glog) + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(dedup_hash_kernel, dim3((uint32_t)hblocks), dim3(kBlock), 0, stream, args);
   const uint64_t wblocks = (args.n + kBlock - 1) / kBlock;
   if (tuning().dedup_table) {

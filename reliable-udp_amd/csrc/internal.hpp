@@ -168,6 +168,9 @@ struct DedupArgs {
   uint64_t n;
   uint32_t F;
   uint32_t window;
+  uint32_t glog;              // hash pass: log2 lanes per frame (from the mean frame length)
+  uint32_t lim_checked;       // frames reach at most frames_lim bytes: a frame whose offsets are
+  uint64_t frames_lim;        // decreasing or past it gets dup = RUDP_DUP_BAD_OFFSETS, nothing read
   uint64_t* hash;             // scratch [n]
   uint8_t* dup;
 };

@@ -28,6 +28,7 @@ EINVAL, ENOMEM, ENOTSUP, EHIP_BASE = -22, -12, -95, -1000
 ABI_VERSION = 5
 # status bits of the sync-free varlen calls (RUDP_ST_*)
 ST_LEN, ST_PAYLOAD, ST_FRAMES_CAP, ST_OFFSETS = 1, 2, 4, 8
+DUP_BAD_OFFSETS = 2  # rudp_dedup_window_checked: a frame whose offsets were rejected
 
 # Every symbol include/rudp.h declares (checked by tests/test_abi.py).
 EXPORTS = (
@@ -36,7 +37,7 @@ EXPORTS = (
     "rudp_encode_varlen", "rudp_validate_utf8", "rudp_dedup_window",
     "rudp_udp_recv_batch", "rudp_udp_send_batch", "rudp_varlen_bounds", "rudp_frame_off_bounds",
     "rudp_encode_varlen_checked", "rudp_decode_varlen_checked", "rudp_frame_off_check",
-    "rudp_udp_recv_batch_from", "rudp_udp_send_batch_to",
+    "rudp_udp_recv_batch_from", "rudp_udp_send_batch_to", "rudp_dedup_window_checked",
 )
 
 
@@ -78,6 +79,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rudp_encode_varlen": [ctypes.POINTER(RudpBatch), P, P, P, I, I, P],
         "rudp_validate_utf8": [P, P, U32, U64, I, P, I, P],
         "rudp_dedup_window": [P, P, U32, U64, U32, P, I, P],
+        "rudp_dedup_window_checked": [P, U64, P, U32, U64, U32, P, I, P],
         "rudp_udp_recv_batch": [I, P, U64, U32, U32, P, I],
         "rudp_udp_send_batch": [I, P, P, U64, ctypes.c_char_p, ctypes.c_uint16],
         "rudp_udp_recv_batch_from": [I, P, U64, U32, U32, P, P, I],

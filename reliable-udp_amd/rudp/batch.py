@@ -719,13 +719,17 @@ def validate_utf8(frames, layout: Union[str, int] = "rudp7", *, frame_off=None, 
 PROXY_MAX_MEMORY = 500  # proxy.py:17
 
 
-def detect_retransmissions(frames, *, frame_off=None, window: int = PROXY_MAX_MEMORY, stream=None):
+def detect_retransmissions(frames, *, frame_off=None, window: int = PROXY_MAX_MEMORY, stream=None,
+                           check: bool = True):
     """u8 [N]: 1 where frame i equals one of the `window` frames before it.
 
     Batched form of the reference proxy's `packet in self.packets` check
     (proxy.py:90, with the 500-packet history of proxy.py:17, :92-94) and
     Packet.__eq__ semantics (utils/packet.py:83-86).  ``frames``: [N, F]
-    fixed-length, or 1-D with ``frame_off`` (N + 1 offsets).
+    fixed-length, or 1-D with ``frame_off`` (N + 1 offsets), checked on the
+    device (rudp_dedup_window_checked): a frame whose offsets are decreasing or
+    past ``frames`` gets 2 and is never read; ``check=True`` waits and raises
+    ValueError when there is one, ``check=False`` never waits.
     """
     import torch
     dev = frames.device
@@ -736,9 +740,19 @@ def detect_retransmissions(frames, *, frame_off=None, window: int = PROXY_MAX_ME
     else:
         _dev_check(frames, "frames", torch.uint8, 1, dev)
         _int_tensor(frame_off, "frame_off", dev, dtypes=(torch.int64,))
-        _check_offsets(frames, frame_off, stream)
-        n, F = frame_off.shape[0] - 1, 0
-        off_ptr = frame_off.data_ptr()
+        n = frame_off.shape[0] - 1
+        if n < 0:
+            raise ValueError("frame_off needs N + 1 entries")
+        dup = torch.empty((n,), dtype=torch.uint8, device=dev)
+        if n:
+            # mean frame length from the buffer size: picks lanes per frame
+            _native.check(_native.lib().rudp_dedup_window_checked(
+                frames.data_ptr() if frames.numel() else 16, frames.numel(), frame_off.data_ptr(),
+                min(frames.numel() // n, 0xFFFFFFFF), n, window, dup.data_ptr(), dev.index or 0,
+                _stream_ptr(stream, dev)))
+            if check and bool((dup == _native.DUP_BAD_OFFSETS).any()):
+                raise ValueError("frame_off must be non-decreasing offsets inside frames")
+        return dup
     dup = torch.empty((n,), dtype=torch.uint8, device=dev)
     if n:
         _native.check(_native.lib().rudp_dedup_window(

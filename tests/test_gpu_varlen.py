@@ -579,6 +579,34 @@ def test_dedup_table_heavy_repeats_and_collisions(cuda, window):
         assert got.tolist() == want, table
 
 
+@pytest.mark.parametrize("mean_len", [6, 40, 200, 1500])
+def test_dedup_lanes_per_frame_and_bad_offsets(cuda, mean_len):
+    """The hash pass takes 1-8 lanes per frame from the mean frame length: same
+    flags at every length; a frame whose offsets are decreasing or past the
+    buffer gets 2 (RUDP_DUP_BAD_OFFSETS), equals nothing, and check=True raises."""
+    rng = np.random.default_rng(mean_len)
+    pool = [bytes(rng.integers(0, 256, max(0, int(rng.normal(mean_len, mean_len / 4))), dtype=np.uint8))
+            for _ in range(300)]
+    seq = [pool[int(k)] for k in rng.integers(0, len(pool), 5000)]
+    off = np.concatenate([[0], np.cumsum([len(f) for f in seq])]).astype(np.int64)
+    flat = np.frombuffer(b"".join(seq) + b"\x00", np.uint8)[:-1]
+    canon = [f if f else bytes(5) for f in seq]
+    last, want = {}, []
+    for i, k in enumerate(canon):
+        want.append(int(k in last and last[k] >= i - 500))
+        last[k] = i
+    got = host(batch.detect_retransmissions(dev(flat, cuda), frame_off=dev(off, cuda), window=500))
+    assert got.tolist() == want
+    bad = off.copy()
+    bad[100] = bad[101] + 1           # frame 100 decreasing
+    bad[-1] = len(flat) + 7           # the last frame past the buffer
+    d = host(batch.detect_retransmissions(dev(flat, cuda), frame_off=dev(bad, cuda), window=500, check=False))
+    assert d[100] == _native.DUP_BAD_OFFSETS and d[-1] == _native.DUP_BAD_OFFSETS
+    assert int((d == _native.DUP_BAD_OFFSETS).sum()) == 2
+    with pytest.raises(ValueError, match="non-decreasing"):
+        batch.detect_retransmissions(dev(flat, cuda), frame_off=dev(bad, cuda), window=500)
+
+
 def test_utf8_packed_tile_vs_python_decoder(cuda):
     """Packed frames of 0.3-3 KB (mean-length hint >= 128 B: the LDS-tile
     validator; a low hint: every tile overflows its budget and checks its
