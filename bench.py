@@ -196,11 +196,22 @@ def digest_field(chk):
     return None if chk is None else f"{chk[1]}/{chk[0]}"
 
 
-def time_loop(torch, fn, steps, warmup):
-    """HIP-event time of `steps` back-to-back calls on the current stream (ms)."""
+def time_loop(torch, fn, steps, warmup, warm_ms=30.0):
+    """HIP-event time of `steps` back-to-back calls on the current stream (ms),
+    after `warmup` calls and at least `warm_ms` of back-to-back calls: after an
+    idle stretch (a host-side digest, a PCIe-bound leg) the first launches run
+    several percent slow (1M x 1024 B: 0.373 vs 0.351 ms right after the
+    headline's digest check; tools/c2_probe.py)."""
     for i in range(warmup):
         fn(i)
     torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    i = warmup
+    while (time.perf_counter() - t0) * 1e3 < warm_ms:
+        for _ in range(4):
+            fn(i)
+            i += 1
+        torch.cuda.synchronize()
     start = torch.cuda.Event(enable_timing=True)
     stop = torch.cuda.Event(enable_timing=True)
     start.record()
