@@ -8,6 +8,8 @@ shapes: encode:L (fixed-length, 1M x L, rotating sets below 1 GiB), varlen:L
 (packed, equal lengths), ragged (lengths uniform in [0, 2944]), decode:L.
 
 usage: python tools/knob_ab.py --knob 58 --values 0,1 --shapes encode:1472,encode:64,varlen:1472,ragged
+       python tools/knob_ab.py --variants "base:;t256b512:2=256,10=512" --shapes encode:64
+         (named variants of several knobs each; knobs a variant does not name keep their defaults)
 """
 from __future__ import annotations
 
@@ -66,23 +68,38 @@ def make_shape(spec, dev):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--knob", type=int, required=True)
-    ap.add_argument("--values", required=True)
+    ap.add_argument("--knob", type=int)
+    ap.add_argument("--values")
+    ap.add_argument("--variants", help="name:key=value,key=value;name:...")
     ap.add_argument("--shapes", required=True)
     ap.add_argument("--reps", type=int, default=9)
     ap.add_argument("--inner", type=int, default=10)
     args = ap.parse_args()
     lib = _native.tools_lib()
     dev = torch.device("cuda", 0)
-    values = [int(v) for v in args.values.split(",")]
-    default = lib.rudpx_tune(args.knob, values[0])
-    out = {"knob": args.knob, "values": values, "shapes": {}}
+    if args.variants:
+        variants = {}
+        for item in args.variants.split(";"):
+            name, _, kvs = item.partition(":")
+            variants[name] = {int(k): int(v) for k, v in (kv.split("=") for kv in kvs.split(",") if kv)}
+    else:
+        variants = {str(v): {args.knob: int(v)} for v in args.values.split(",")}
+    keys = sorted({k for kv in variants.values() for k in kv})
+    defaults = {k: lib.rudpx_tune(k, 0) for k in keys}
+    for k, v in defaults.items():
+        lib.rudpx_tune(k, v)
+
+    def apply(name):
+        for k in keys:
+            lib.rudpx_tune(k, variants[name].get(k, defaults[k]))
+    values = list(variants)
+    out = {"variants": variants, "shapes": {}}
     for spec in args.shapes.split(","):
         run = make_shape(spec, dev)
         ref = None
         exact = {}
         for v in values:
-            lib.rudpx_tune(args.knob, v)
+            apply(v)
             got = run().clone()
             torch.cuda.synchronize()
             if ref is None:
@@ -91,7 +108,7 @@ def main():
         times = {v: [] for v in values}
         for _ in range(args.reps):
             for v in values:
-                lib.rudpx_tune(args.knob, v)
+                apply(v)
                 run()
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
@@ -104,7 +121,8 @@ def main():
         print(spec, out["shapes"][spec], file=sys.stderr, flush=True)
         del run
         torch.cuda.empty_cache()
-    lib.rudpx_tune(args.knob, default)
+    for k, v in defaults.items():
+        lib.rudpx_tune(k, v)
     print(json.dumps(out, indent=1))
 
 
