@@ -399,6 +399,7 @@ int launch_tile_policy(const EncodeTileArgs& args, hipStream_t stream) {
   if (block > 256 && (uint64_t)(256u / args.T) * (uint32_t)(block / 256) > 64u) block = 256;
   const Tuning& t = tuning();
   if (t.encode_dma && block == 512) return launch_tile<H, true, true, 8, 512, true>(args, stream);
+  if (t.encode_dma && block == 128 && args.T <= 128) return launch_tile<H, true, true, 8, 128, true>(args, stream);
   if (t.encode_dma && block == 256) {
     if (t.encode_nt_load && t.encode_nt_store) return launch_tile<H, true, true, 8, kBlock, true>(args, stream);
     if (t.encode_nt_load) return launch_tile<H, true, false, 8, kBlock, true>(args, stream);
