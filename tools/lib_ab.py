@@ -30,6 +30,10 @@ def main():
     ap.add_argument("--libs", required=True)
     ap.add_argument("--L", default="1472,1024,64")
     ap.add_argument("--reps", type=int, default=11)
+    ap.add_argument("--op", default="encode", choices=["encode", "decode", "varlen"],
+                    help="decode: verify-only fixed-length rudp_decode of the encoded frames; varlen: "
+                         "rudp_encode_varlen_checked of packed payloads, --L lengths or 'ragged' "
+                         "(uniform in [0, 2944]); a 'u' suffix (1472u) times the unchecked rudp_encode_varlen")
     args = ap.parse_args()
     _native.lib()  # torch's HIP runtime first
     libs = {}
@@ -39,10 +43,27 @@ def main():
         h.rudp_encode.argtypes = [ctypes.POINTER(_native.RudpBatch), ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         h.rudp_encode.restype = ctypes.c_int
+        h.rudp_decode.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64, ctypes.c_void_p,
+                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                  ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        h.rudp_decode.restype = ctypes.c_int
+        h.rudp_encode_varlen_checked.argtypes = [ctypes.POINTER(_native.RudpBatch), ctypes.c_uint64, ctypes.c_void_p,
+                                                 ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                 ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        h.rudp_encode_varlen_checked.restype = ctypes.c_int
+        h.rudp_encode_varlen.argtypes = [ctypes.POINTER(_native.RudpBatch), ctypes.c_void_p, ctypes.c_void_p,
+                                         ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        h.rudp_encode_varlen.restype = ctypes.c_int
         libs[name] = h
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream().cuda_stream
     out = {}
+    if args.op == "varlen":
+        for spec in args.L.split(","):
+            out[spec] = varlen_ab(libs, spec, args.reps, dev, stream)
+            print(spec, out[spec], file=sys.stderr, flush=True)
+        print(json.dumps(out, indent=1))
+        return
     for L in (int(x) for x in args.L.split(",")):
         n = 1 << 20
         nsets = max(1, min(8, math.ceil((1 << 30) / (n * (2 * L + 12)))))
@@ -53,13 +74,25 @@ def main():
             b = _native.RudpBatch(n=n, payload_len=L, reserved=0, seq=tab.seq.data_ptr(), ack=tab.ack.data_ptr(),
                                   flags=tab.flags.data_ptr(), payload=pay.data_ptr(), len=None, payload_off=None)
             sets.append((tab, pay, fr, b))
+            libs[next(iter(libs))].rudp_encode(ctypes.byref(b), fr.data_ptr(), None, 7, 0, stream)
+        outs = [torch.empty((n,), dtype=dt, device=dev) for dt in (torch.uint16, torch.uint16, torch.uint8,
+                                                                     torch.uint8, torch.uint16)]
+
+        def call(h, fr, b):
+            if args.op == "encode":
+                return h.rudp_encode(ctypes.byref(b), fr.data_ptr(), None, 7, 0, stream)
+            return h.rudp_decode(fr.data_ptr(), None, L + 7, n, None, *[t.data_ptr() for t in outs], None, 7, 0,
+                                 stream)
         ref = None
         exact = {}
         for name, h in libs.items():
             _, _, fr, b = sets[0]
-            fr.zero_()
-            assert h.rudp_encode(ctypes.byref(b), fr.data_ptr(), None, 7, 0, stream) == 0
-            got = fr.clone()
+            if args.op == "encode":
+                fr.zero_()
+            for t in outs:
+                t.zero_()
+            assert call(h, fr, b) == 0
+            got = fr.clone() if args.op == "encode" else torch.cat([t.view(torch.uint8) for t in outs])
             ref = got if ref is None else ref
             exact[name] = bool(torch.equal(got, ref))
         times = {k: [] for k in libs}
@@ -67,12 +100,12 @@ def main():
             for name, h in libs.items():
                 for i in range(2):
                     _, _, fr, b = sets[i % nsets]
-                    h.rudp_encode(ctypes.byref(b), fr.data_ptr(), None, 7, 0, stream)
+                    call(h, fr, b)
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 for i in range(10):
                     _, _, fr, b = sets[i % nsets]
-                    h.rudp_encode(ctypes.byref(b), fr.data_ptr(), None, 7, 0, stream)
+                    call(h, fr, b)
                 e.record()
                 e.synchronize()
                 times[name].append(s.elapsed_time(e) / 10)
@@ -81,6 +114,55 @@ def main():
         del sets
         torch.cuda.empty_cache()
     print(json.dumps(out, indent=1))
+
+
+def varlen_ab(libs, spec, reps, dev, stream):
+    n = 1 << 20
+    g = torch.Generator(device=dev).manual_seed(0x5EED0004)
+    unchecked = spec.endswith("u")
+    spec = spec.rstrip("u")
+    if spec == "ragged":
+        lens = torch.randint(0, 2945, (n,), dtype=torch.int32, device=dev, generator=g)
+        hint = 1472
+    else:
+        hint = int(spec)
+        lens = torch.full((n,), hint, dtype=torch.int32, device=dev)
+    tab, _ = batch.synth_batch(n, 0, 0x5EED0004, device=dev)
+    pbytes = int(lens.sum().item())
+    pay = torch.randint(0, 256, (pbytes,), dtype=torch.uint8, device=dev, generator=g)
+    fcap = pbytes + 7 * n
+    frames = torch.empty((fcap,), dtype=torch.uint8, device=dev)
+    fo = torch.empty((n + 1,), dtype=torch.int64, device=dev)
+    st = torch.zeros((1,), dtype=torch.int32, device=dev)
+    b = _native.RudpBatch(n=n, payload_len=hint, reserved=0, seq=tab.seq.data_ptr(), ack=tab.ack.data_ptr(),
+                          flags=tab.flags.data_ptr(), payload=pay.data_ptr(), len=lens.data_ptr(), payload_off=None)
+
+    def call(h):
+        if unchecked:
+            return h.rudp_encode_varlen(ctypes.byref(b), frames.data_ptr(), fo.data_ptr(), None, 7, 0, stream)
+        return h.rudp_encode_varlen_checked(ctypes.byref(b), pbytes, frames.data_ptr(), fcap, fo.data_ptr(), None,
+                                            st.data_ptr(), 7, 0, stream)
+    ref, exact = None, {}
+    for name, h in libs.items():
+        frames.zero_()
+        assert call(h) == 0
+        assert int(st.item()) == 0
+        got = frames.clone()
+        ref = got if ref is None else ref
+        exact[name] = bool(torch.equal(got, ref))
+    times = {k: [] for k in libs}
+    for _ in range(reps):
+        for name, h in libs.items():
+            for _ in range(2):
+                call(h)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(10):
+                call(h)
+            e.record()
+            e.synchronize()
+            times[name].append(s.elapsed_time(e) / 10)
+    return {"ms": {k: statistics.median(v) for k, v in times.items()}, "exact": exact, "payload_bytes": pbytes}
 
 
 if __name__ == "__main__":
