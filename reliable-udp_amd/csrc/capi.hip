@@ -589,6 +589,9 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
   a.early_fo = tuning().varlen_early_fo ? 1u : 0u;
   a.xcd = tuning().tile_xcd ? 1u : 0u;
   a.status = chk.status;
+#if RUDP_TOOLS
+  a.diag = (uint32_t)tuning().varlen_diag;
+#endif
   // Small frames (hints under varlen_small bytes, packed, aligned): the scan's
   // last pass and the framing in one tile kernel (launch_encode_varlen_small).
   const int small_hint = tuning().varlen_small;
@@ -626,14 +629,18 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
   if (btile > 0 && chk.status && !in->payload_off && a.tile_T && aligned16(in->payload) && aligned16(d_frames)) {
     const uint64_t h = in->payload_len ? in->payload_len : 1u;
     const uint64_t ptiles = (in->n + a.tile_T - 1u) / a.tile_T;
-    const uint64_t S = a.tile_cap > 2u * h + 64u + h ? a.tile_cap - 2u * h - 64u : 0u;
+    uint64_t S = a.tile_cap > 2u * h + 64u + h ? a.tile_cap - 2u * h - 64u : 0u;
+    if (tuning().varlen_span_bytes > 0) S = (uint64_t)tuning().varlen_span_bytes;
     // 1.5x a span's mean packet count + 2 (fewer, down to the mean + 2, where
     // the slots' LDS would cost a tile per CU: each slot is 44 B, and at 1M x
     // 1472 B 32 slots ran 4 tiles per CU instead of 5)
     uint32_t slots = S ? (uint32_t)(3u * S / (2u * h) + 2u) : 4u;
     if (slots < 4u) slots = 4u;
     if (slots > 256u) slots = 256u;
-    const uint32_t min_slots = S ? (uint32_t)(S / h + 2u) : 4u;
+    uint32_t min_slots = S ? (uint32_t)(S / h + 2u) : 4u;
+#if RUDP_TOOLS
+    if (a.diag & 2u) slots = min_slots = a.tile_T;
+#endif
     if (S && (btile == 2 || varlen_btile_ok(a.tile_T, &slots, min_slots, a.tile_cap, (uint32_t)layout, a.vhc,
                                            ptiles, chk.payload_bytes / S + 1u))) {
       spans.bytes = S;

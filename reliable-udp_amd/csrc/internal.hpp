@@ -129,6 +129,7 @@ struct VarlenArgs {
   uint32_t lim_checked;           // decode: frames_lim bounds the frames (checked calls)
 #if RUDP_TOOLS
   uint64_t* trace;                // diagnostics (rudpx_encode_trace): small-frame encode timeline per tile
+  uint32_t diag;                  // diagnostics (rudpx_tune 61): varlen tile ablation bits
 #endif
   uint32_t small_fpt;             // decode small-frame tile: frames per thread (0: not used)
   uint32_t small_cap;             // its LDS run budget in bytes
@@ -320,6 +321,14 @@ struct Tuning {
   // 1472 B 0.544 -> 0.527 ms, lengths uniform in [0, 2944] 0.808 -> 0.729
   // (profiles/r02/sweeps/ragged_blocksums.json).
   RUDP_KNOB(varlen_tile_sums, 2)
+  // Varlen byte tiles: span bytes S (0 = budget - 2 * hint - 64); sweeps only.
+  RUDP_KNOB(varlen_span_bytes, 0)
+#if RUDP_TOOLS
+  // Varlen tile ablations (timing only, 1 = wrong output): 1 skip the edge
+  // units; 2 byte tiles with tile_T slots; 4 byte tiles without the packet
+  // form's loads (with varlen_btile 2).
+  RUDP_KNOB(varlen_diag, 0)
+#endif
   RUDP_KNOB(host_slots, 3)     // *_host pipeline: device staging slots (2..8)
   RUDP_KNOB(host_stage_mb, 128)  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
 };

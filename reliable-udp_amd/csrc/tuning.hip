@@ -316,7 +316,9 @@ int rudpx_tune(int key, int value) {
             : key == 49 ? &t.tile_xcd
             : key == 50 ? &t.varlen_small_fused
             : key == 51 ? &t.varlen_btile
-            : key == 52 ? &t.varlen_tile_sums : nullptr;
+            : key == 52 ? &t.varlen_tile_sums
+            : key == 59 ? &t.varlen_span_bytes
+            : key == 61 ? &t.varlen_diag : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }

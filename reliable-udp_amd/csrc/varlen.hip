@@ -329,13 +329,18 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   const uint32_t tile_p = b < ptiles ? (a.xcd ? xcd_tile(b, ptiles) : b) : ptiles - 1u;
   const uint64_t pp0 = (uint64_t)tile_p * a.tile_T;
   const uint32_t pTv = a.n - pp0 < a.tile_T ? (uint32_t)(a.n - pp0) : a.tile_T;
-  const uint64_t pfo0 = a.frame_off[pp0], pfo_end = a.frame_off[pp0 + pTv];
+#if RUDP_TOOLS
+  const bool no_pload = (a.diag & 4u) && a.span_rec;  // ablation: byte tiles without the packet form's loads
+#else
+  constexpr bool no_pload = false;
+#endif
+  const uint64_t pfo0 = no_pload ? 0ull : a.frame_off[pp0], pfo_end = no_pload ? 0ull : a.frame_off[pp0 + pTv];
   bool bt = false;
   SpanRec r0{}, r1{};
   const uint32_t spans = (uint32_t)a.span_count;
   const uint32_t tile_s = b < spans ? (a.xcd ? xcd_tile(b, spans) : b) : 0u;
   if (a.span_rec) {
-    bt = *a.tile_over >= a.bt_min_over;
+    bt = no_pload || *a.tile_over >= a.bt_min_over;
     if (b < spans) {
       r0 = a.span_rec[tile_s];
       r1 = a.span_rec[tile_s + 1];
@@ -576,6 +581,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   // lead + 16i; then the partial head [0, lead) and tail [lead + 16*nfull,
   // nbytes), written bytewise.
   for (uint32_t k = tid; k < nfull + 2u; k += kBlock) {
+#if RUDP_TOOLS
+    if ((a.diag & 1u) && k >= nfull) continue;  // ablation: the edge units not stored
+#endif
     uint32_t x, hi_b, r;
     if (k < nfull) {
       const uint32_t i = k + npre < nfull ? k + npre : k + npre - nfull;

@@ -74,6 +74,9 @@ def analyse(rec):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--save", default="")
+    ap.add_argument("--forms", default="packet_tiles:51=0;byte_tiles:51=2",
+                    help="name:key=value,...;... (rudpx_tune knobs per form; unnamed knobs keep their defaults)")
+    ap.add_argument("--shapes", default="equal_1472,ragged_0_2944")
     args = ap.parse_args()
     lib = _native.tools_lib()
     dev = torch.device("cuda", 0)
@@ -86,12 +89,23 @@ def main():
     tot = int(lens.sum().item())
     tab2, _ = batch.synth_batch(n, 0, 0x5EED0004, device=dev)
     shapes["ragged_0_2944"] = (tab2, torch.randint(0, 256, (tot,), dtype=torch.uint8, device=dev, generator=g), lens)
+    forms = {}
+    for item in args.forms.split(";"):
+        fname, _, kvs = item.partition(":")
+        forms[fname] = {int(k): int(v) for k, v in (kv.split("=") for kv in kvs.split(",") if kv)}
+    keys = sorted({k for kv in forms.values() for k in kv})
+    defaults = {k: lib.rudpx_tune(k, 0) for k in keys}
+    for k, v in defaults.items():
+        lib.rudpx_tune(k, v)
     out = {}
     for name, (t, flat, ln) in shapes.items():
+        if name not in args.shapes.split(","):
+            continue
         blocks = flat.numel() // 1000 + n // 8 + 16
         buf = torch.zeros((blocks * 12,), dtype=torch.int64, device=dev)
-        for form, key in (("packet_tiles", 0), ("byte_tiles", 2)):
-            lib.rudpx_tune(51, key)
+        for form, knobs in forms.items():
+            for k in keys:
+                lib.rudpx_tune(k, knobs.get(k, defaults[k]))
             res = batch.pack_batch_varlen(t, flat, ln, "rudp7")
             for _ in range(3):
                 batch.pack_batch_varlen(t, flat, ln, "rudp7", reuse=res, check=False)
@@ -119,7 +133,8 @@ def main():
             out[f"{name}/{form}"] = {"call_ms_median": statistics.median(ts), "traced": runs}
             print(f"{name}/{form} done", file=sys.stderr, flush=True)
         del buf
-    lib.rudpx_tune(51, 1)
+    for k, v in defaults.items():
+        lib.rudpx_tune(k, v)
     print(json.dumps(out, indent=1))
 
 
