@@ -261,6 +261,24 @@ def c5_strong_leg(torch, dist, batch, device, world, rank, layout, share_device,
             "scaling": "strong"}
 
 
+def copy_same_bytes(torch, device, alg_bytes, nsets, steps, encode_ms):
+    """Streaming copy (rudpx_copy_vpt: one dwordx4 per thread, nt loads and stores,
+    diagnostics build) moving alg_bytes per launch (half read, half written) over
+    nsets rotating buffer pairs: the HBM ceiling at the size of one encode launch."""
+    from rudp import _native
+    lib = _native.tools_lib(activate=False)
+    half = alg_bytes // 2 // 16 * 16
+    bufs = [(torch.empty(half, dtype=torch.uint8, device=device), torch.empty(half, dtype=torch.uint8, device=device))
+            for _ in range(nsets)]
+    stream = torch.cuda.current_stream().cuda_stream
+    ms = time_loop(torch, lambda i: lib.rudpx_copy_vpt(bufs[i % nsets][0].data_ptr(), bufs[i % nsets][1].data_ptr(),
+                                                       half // 16, 1, 1, stream), steps, 3) / steps
+    del bufs
+    gbs = 2 * half / (ms / 1e3) / 1e9
+    return {"copy_same_bytes_ms": ms, "copy_same_bytes_GBs": gbs,
+            "copy_same_bytes_frac_of_peak": gbs / HBM_PEAK_GBS, "frac_of_copy_same_bytes": ms / encode_ms}
+
+
 def legs(torch, batch, device, steps):
     out = {}
     for L, cfg_name in ((1024, "C2"), (64, "C3")):
@@ -274,6 +292,12 @@ def legs(torch, batch, device, steps):
             "buffer_sets": len(w.sets),
             "matches_reference": None if chk is None else chk[0] == chk[1] > 0,
             "chunks_matching_reference_digests": digest_field(chk)}
+        if L == 64:
+            # the streaming copy of the same bytes in the same number of rotating sets: at
+            # 147 MB per launch the ramp and tail of any HBM-bound launch are a visible part
+            # of it, so this (not 8 TB/s) is what the 64-B encode can reach
+            out["encode_1Mx64"].update(copy_same_bytes(torch, device, (1 << 20) * algorithmic_bytes_encode(L),
+                                                       len(w.sets), steps, ms))
         del w
     w = Workload(torch, batch, 1 << 20, 1472, "rudp7", 0, SEEDS[1472], device)
     for i in range(len(w.sets)):
