@@ -619,11 +619,15 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
   a.trace = tuning().encode_trace.load();  // tile-kernel phase timeline (tools/varlen_timeline.py)
 #endif
   // Tiles by payload bytes (checked calls, where the payload size is known on
-  // the host): spans of S = budget - 2 * hint - 64 bytes, so a tile overflows its
-  // LDS budget only through a packet over twice the hint; at most bt_slots
-  // packets per tile in LDS (more take the per-packet path).  The scan counts
-  // the packet tiles that would overflow, and the tile kernel takes byte tiles
-  // when they are bt_min_over or more (varlen_btile 1: 1/32 of the tiles).
+  // the host; hints from 1 KiB, varlen_btile_ok): spans of S = budget - 2 *
+  // hint - 64 bytes, so a byte tile overflows its LDS budget only through a
+  // packet over twice the hint; at most bt_slots packets per tile in LDS (more
+  // take the per-packet path).  The scan chooses per call: pass 1 counts the
+  // packet tiles likely to overflow, pass 2 picks byte tiles when they are
+  // 1/32 of the tiles or more, and pass 3 writes one record per workgroup in
+  // the chosen form, so every tile's first loads are two adjacent records
+  // (varlen_btile 1; 2: byte tiles always, 3: packet tiles through records;
+  // 0: packet tiles from frame_off).
   SpanStarts spans{};
   const int btile = tuning().varlen_btile;
   if (btile > 0 && chk.status && !in->payload_off && a.tile_T && aligned16(in->payload) && aligned16(d_frames)) {
@@ -641,22 +645,23 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
 #if RUDP_TOOLS
     if (a.diag & 2u) slots = min_slots = a.tile_T;
 #endif
-    if (S && (btile == 2 || varlen_btile_ok(a.tile_T, &slots, min_slots, a.tile_cap, (uint32_t)layout, a.vhc,
-                                           ptiles, chk.payload_bytes / S + 1u))) {
+    if (S && (btile == 2 || varlen_btile_ok(a.tile_T, &slots, min_slots, a.tile_cap, a.tile_cap, (uint32_t)layout,
+                                           a.vhc, ptiles, chk.payload_bytes / S + 1u))) {
       spans.bytes = S;
       spans.count = chk.payload_bytes / S + 1u;
-      void* buf = nullptr;
-      // records [count + 1], then the scan's overflow counter
-      RUDP_HIP(stream_alloc(&buf, (spans.count + 2u) * sizeof(SpanRec), s));
-      spans.rec = static_cast<SpanRec*>(buf);
-      spans.over = reinterpret_cast<uint32_t*>(spans.rec + spans.count + 1u);
+      spans.ptiles = ptiles;
+      spans.grid = ptiles > spans.count ? ptiles : spans.count;
+      spans.min_over = btile == 2 ? 0u : btile == 3 ? 0xFFFFFFFFu : (uint32_t)(ptiles / 32u + 1u);
       spans.tile_T = a.tile_T;
       spans.tile_cap = a.tile_cap;
+      void* buf = nullptr;
+      // records [grid + 1], then pass 2's choice
+      RUDP_HIP(stream_alloc(&buf, (spans.grid + 2u) * sizeof(SpanRec), s));
+      spans.rec = static_cast<SpanRec*>(buf);
+      spans.ctl = reinterpret_cast<uint32_t*>(spans.rec + spans.grid + 1u);
       a.span_rec = spans.rec;
-      a.span_count = spans.count;
-      a.tile_over = spans.over;
+      a.span_count = spans.grid;
       a.bt_slots = (uint32_t)slots;
-      a.bt_min_over = btile == 2 ? 0u : (uint32_t)(ptiles / 32u + 1u);
     }
   }
   rc = scan_frame_offsets(in->len, in->n, (uint32_t)layout, d_frame_off, chk, s, spans);

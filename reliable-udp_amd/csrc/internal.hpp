@@ -134,16 +134,15 @@ struct VarlenArgs {
   uint32_t small_fpt;             // decode small-frame tile: frames per thread (0: not used)
   uint32_t small_cap;             // its LDS run budget in bytes
   uint32_t xcd;                   // tile kernels: XCD-contiguous tile order (xcd_tile)
-  // Byte tiles (span_rec set): workgroup k may frame the packets whose payload
-  // starts in [k*S, (k+1)*S) (span_rec[k].p .. span_rec[k+1].p, from the scan)
-  // instead of packet tile k.  The launch picks per call on the device: byte
-  // tiles when the scan counted at least bt_min_over packet tiles over their
-  // LDS budget (*tile_over).  bt_slots is the most packets a byte tile holds
-  // in LDS; tile_Tl = max(tile_T, bt_slots) sizes the LDS arrays.
+  // Tile records (span_rec set, checked calls): workgroup t frames packets
+  // span_rec[t].p .. span_rec[t+1].p, whose frames start at span_rec[t].fo.
+  // The scan chose per call between packet tiles (tile_T packets each) and
+  // byte tiles (the packets whose payload starts in one span of S bytes) and
+  // wrote the chosen form's records; span_count = the grid (records - 1).
+  // bt_slots is the most packets a tile holds in LDS; tile_Tl = max(tile_T,
+  // bt_slots) sizes the LDS arrays.
   const struct SpanRec* span_rec;
   uint64_t span_count;
-  const uint32_t* tile_over;
-  uint32_t bt_min_over;
   uint32_t bt_slots;
   uint32_t tile_Tl;
   uint32_t tile_sums;             // tile sum pass: 2 from 128-B block sums, 0 chunk by chunk
@@ -312,10 +311,13 @@ struct Tuning {
 
   // Varlen encode tiles by payload bytes (spans from the scan) instead of by
   // packet count: no tile overflows short of one packet past the budget's
-  // slack.  0: packet tiles; 1: byte tiles when over 1/32 of the packet tiles
-  // would overflow (decided on the device per call); 2: byte tiles.  1M x
-  // 1472 B: packet 0.540 / byte 0.621 ms; lengths uniform in [0, 2944]:
-  // 0.728 / 0.644 (profiles/r02/sweeps/ragged_blocksums.json).
+  // slack.  1: the scan chooses per call (byte tiles when over 1/32 of the
+  // packet tiles would overflow) and writes the chosen form's tile records;
+  // 2: byte tiles always; 3: packet tiles through records; 0: packet tiles
+  // from frame_off (no records).  Round 2: packet 0.540 / byte 0.621 ms at 1M
+  // x 1472 B, lengths uniform in [0, 2944] 0.728 / 0.644
+  // (profiles/r02/sweeps/ragged_blocksums.json); round 3 (records instead of a
+  // choice read by every tile): profiles/r03/sweeps/varlen_records.json.
   RUDP_KNOB(varlen_btile, 1)
   // Varlen tile sum pass from 128-B block sums (VarlenArgs::tile_sums 2): 1M x
   // 1472 B 0.544 -> 0.527 ms, lengths uniform in [0, 2944] 0.808 -> 0.729
@@ -325,8 +327,7 @@ struct Tuning {
   RUDP_KNOB(varlen_span_bytes, 0)
 #if RUDP_TOOLS
   // Varlen tile ablations (timing only, 1 = wrong output): 1 skip the edge
-  // units; 2 byte tiles with tile_T slots; 4 byte tiles without the packet
-  // form's loads (with varlen_btile 2).
+  // units; 2 byte tiles with tile_T slots.
   RUDP_KNOB(varlen_diag, 0)
 #endif
   RUDP_KNOB(host_slots, 3)     // *_host pipeline: device staging slots (2..8)
@@ -350,8 +351,8 @@ int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStr
 int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream_t stream);
 int launch_synth(const SynthArgs& args, hipStream_t stream);
 void varlen_tile_geometry(uint32_t len_hint, uint32_t* T, uint32_t* glog, uint32_t* cap);
-bool varlen_btile_ok(uint32_t tile_T, uint32_t* bt_slots, uint32_t min_slots, uint32_t cap, uint32_t H,
-                     uint32_t vhc, uint64_t packet_tiles, uint64_t spans);
+bool varlen_btile_ok(uint32_t tile_T, uint32_t* bt_slots, uint32_t min_slots, uint32_t cap, uint32_t cap_packet,
+                     uint32_t H, uint32_t vhc, uint64_t packet_tiles, uint64_t spans);
 int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream);
 int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream);
 int launch_validate_utf8(const Utf8Args& args, hipStream_t stream);
@@ -383,9 +384,9 @@ struct ScanCheck {
 // blocks of kBlock * items packets (items 1, 2, 4 or 8; with the ScanCheck's
 // bits), then the exclusive block bases in place, frame_off[n] and the status.
 void scan_block_sums(const uint32_t* d_len, uint64_t n, uint32_t H, uint32_t items, uint64_t* sums,
-                     const ScanCheck& chk, hipStream_t stream);
+                     const ScanCheck& chk, hipStream_t stream, uint32_t over_T = 0, uint32_t over_cap = 0);
 void scan_block_bases(uint64_t* sums, uint64_t nb, uint64_t* d_frame_off, uint64_t n, uint32_t H,
-                      const ScanCheck& chk, hipStream_t stream, uint32_t* zero = nullptr);
+                      const ScanCheck& chk, hipStream_t stream, uint32_t* ctl = nullptr, uint32_t min_over = 0);
 // Small-frame varlen encode of packed payloads (varlen.hip): the scan's first
 // two passes, then one kernel per tile of kBlock * fpt packets that writes the
 // tile's offsets and assembles its frames in LDS.
@@ -396,11 +397,20 @@ int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int
 // adjacent records in one round trip.
 // With over set, the scan also counts into *over the tiles of tile_T packets
 // whose payload run (16-B aligned) exceeds tile_cap.
+// The varlen tile kernel's records (scan_apply_kernel): rec[0..grid] for
+// grid = max(packet tiles, spans) workgroups.  Pass 1 counts the packet tiles
+// of tile_T packets whose payload run (estimated as their length sum + 30)
+// exceeds tile_cap; pass 2 writes *ctl = 1 (byte tiles) when the count is at
+// least min_over, else 0; pass 3 writes the chosen form's records, the
+// unused workgroups' records spread evenly as empty ones (rec_index).
 struct SpanStarts {
-  SpanRec* rec;  // [count + 1], or null
-  uint64_t bytes;
-  uint64_t count;
-  uint32_t* over;
+  SpanRec* rec;  // [grid + 1], or null
+  uint64_t bytes;      // span size S
+  uint64_t count;      // spans: ceil over the payload bytes (+ 1)
+  uint64_t ptiles;     // packet tiles
+  uint64_t grid;       // max(ptiles, count)
+  uint32_t* ctl;       // pass 2's choice
+  uint32_t min_over;   // 0: byte tiles always; UINT32_MAX: packet tiles always
   uint32_t tile_T, tile_cap;
 };
 int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,

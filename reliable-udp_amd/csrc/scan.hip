@@ -28,12 +28,17 @@ constexpr uint32_t kScanBlockItems = kBlock * kScanItems;  // 2048 per block
 
 // ITEMS packets per thread: a block sums kBlock * ITEMS lengths (8 for the
 // offset scan; the small-frame encode uses its own tile size).
+// With over_T (ITEMS = 8 only): the block's packet tiles of over_T packets
+// whose length sum + 30 (a bound on their 16-B aligned payload run) exceeds
+// over_cap are counted into bits 44-55 of the sum.
 template <uint32_t ITEMS>
 __global__ void __launch_bounds__(kBlock) scan_block_sums_kernel(const uint32_t* len, uint64_t n,
                                                                  uint32_t H, uint64_t* sums,
-                                                                 ScanCheck chk) {
+                                                                 ScanCheck chk, uint32_t over_T,
+                                                                 uint32_t over_cap) {
   __shared__ uint64_t s_wave[kBlock / 64];
   __shared__ uint32_t s_bits;
+  __shared__ uint32_t s_l[ITEMS == 8 ? kBlock * ITEMS : 1];
   if (threadIdx.x == 0) s_bits = 0;
   const uint64_t base = (uint64_t)blockIdx.x * (kBlock * ITEMS);
   uint64_t acc = 0;
@@ -41,6 +46,7 @@ __global__ void __launch_bounds__(kBlock) scan_block_sums_kernel(const uint32_t*
 #pragma unroll
   for (uint32_t j = 0; j < ITEMS; ++j) {
     const uint64_t i = base + j * kBlock + threadIdx.x;
+    if (ITEMS == 8 && over_T) s_l[j * kBlock + threadIdx.x] = i < n ? len[i] : 0u;
     if (i < n) {
       const uint32_t l = len[i];
       acc += (uint64_t)l + H;
@@ -55,38 +61,56 @@ __global__ void __launch_bounds__(kBlock) scan_block_sums_kernel(const uint32_t*
     }
   }
   for (int m = 32; m > 0; m >>= 1) acc += __shfl_xor(acc, m, 64);
-  __syncthreads();  // s_bits initialised
+  __syncthreads();  // s_bits initialised, s_l stored
   if (bits) atomicOr(&s_bits, bits);
   if ((threadIdx.x & 63u) == 0) s_wave[threadIdx.x >> 6] = acc;
+  uint32_t over = 0;
+  if (ITEMS == 8 && over_T) {
+    const uint32_t tiles = kBlock * ITEMS / over_T;  // (over_T a power of two <= 256)
+    for (uint32_t t0 = 0; t0 < tiles; t0 += kBlock) {  // (uniform rounds)
+      const uint32_t t = t0 + threadIdx.x;
+      bool o = false;
+      if (t < tiles) {
+        uint64_t sum = 0;
+        for (uint32_t k = 0; k < over_T; ++k) sum += s_l[t * over_T + k];
+        o = sum + 30u > over_cap;
+      }
+      over += (uint32_t)__syncthreads_count(o);
+    }
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t t = 0;
     for (uint32_t w = 0; w < kBlock / 64; ++w) t += s_wave[w];
-    sums[blockIdx.x] = t | ((uint64_t)s_bits << kSumBitsShift);
+    sums[blockIdx.x] = t | ((uint64_t)over << kSumCountShift) | ((uint64_t)s_bits << kSumBitsShift);
   }
 }
 
 // One workgroup of 1024 threads: sums[b] <- sum_{c<b} sums[c]; frame_off[n] <- total;
 // with a ScanCheck, the call's status word.
+// With ctl: the varlen tile form, *ctl = 1 (byte tiles) when pass 1 counted at
+// least min_over likely overflowing packet tiles, else 0.
 __global__ void __launch_bounds__(1024) scan_block_bases_kernel(uint64_t* sums, uint64_t nb,
                                                                uint64_t* frame_off, uint64_t n,
-                                                               uint32_t H, ScanCheck chk, uint32_t* zero) {
+                                                               uint32_t H, ScanCheck chk, uint32_t* ctl,
+                                                               uint32_t min_over) {
   __shared__ uint64_t s_wave[1024 / 64];
-  __shared__ uint32_t s_bits;
-  if (threadIdx.x == 0) s_bits = 0;
-  if (zero && threadIdx.x == 0) *zero = 0;  // (pass 3's counter)
+  __shared__ uint32_t s_bits, s_over;
+  if (threadIdx.x == 0) s_bits = s_over = 0;
   const uint64_t per = (nb + 1023) / 1024;
   const uint64_t lo = threadIdx.x * per, hi = lo + per < nb ? lo + per : nb;
   uint64_t mine = 0;
-  uint32_t bits = 0;
+  uint32_t bits = 0, over = 0;
   for (uint64_t i = lo; i < hi; ++i) {
     const uint64_t v = sums[i];
     mine += v & kSumMask;
+    over += (uint32_t)(v >> kSumCountShift) & 0xFFFu;
     bits |= (uint32_t)(v >> kSumBitsShift);
   }
   uint64_t total = 0;
-  uint64_t run = block_exclusive_scan(mine, &total, s_wave);  // (its barriers order s_bits)
+  uint64_t run = block_exclusive_scan(mine, &total, s_wave);  // (its barriers order s_bits, s_over)
   if (bits) atomicOr(&s_bits, bits);
+  if (over) atomicAdd(&s_over, over);
   for (uint64_t i = lo; i < hi; ++i) {
     const uint64_t v = sums[i] & kSumMask;
     sums[i] = run;
@@ -94,6 +118,7 @@ __global__ void __launch_bounds__(1024) scan_block_bases_kernel(uint64_t* sums, 
   }
   __syncthreads();
   if (threadIdx.x == 0) {
+    if (ctl) *ctl = s_over >= min_over ? 1u : 0u;
     frame_off[n] = total;
     if (chk.status) {
       uint32_t st = s_bits;
@@ -104,11 +129,15 @@ __global__ void __launch_bounds__(1024) scan_block_bases_kernel(uint64_t* sums, 
   }
 }
 
-// With spans.rec: the packed payload splits into spans of S bytes, and
-// spans.rec[k] = {frame_off[p], p} for p the first packet whose payload starts
-// at or after k*S (n for spans after the last packet's start), k = 0 .. spans.count.
-// With spans.over: the tiles of spans.tile_T packets (which divides the
-// block's packets) whose run exceeds spans.tile_cap are counted into *over.
+// With spans.rec: the varlen tile kernel's records in the form pass 2 chose
+// (*spans.ctl).  Byte tiles: the packed payload splits into spans of S bytes,
+// and span t's record is {frame_off[p], p} for p the first packet whose payload
+// starts at or after t*S (n for spans after the last packet's start), t = 0 ..
+// spans.count.  Packet tiles: tile k's record is {frame_off[k T], k T}, k = 0
+// .. ptiles (the last {total, n}).  Tile k of nt goes to record index
+// k + floor(k (grid - nt) / nt), so the grid's workgroups the form does not
+// need are spread evenly (over the XCDs too); a skipped index repeats the
+// next tile's record, which makes its workgroup's tile empty.
 __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len, uint64_t n, uint32_t H,
                                                             const uint64_t* bases, uint64_t* frame_off,
                                                             SpanStarts spans) {
@@ -141,72 +170,74 @@ __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len,
     if (base + k < n) frame_off[base + k] = s_off[k];
   }
   if (spans.rec) {
-    const uint64_t S = spans.bytes, K = spans.count;
-    // x / S through the double reciprocal, corrected to the exact quotient
-    // (x < 2^53: the estimate is off by at most one); a u64 division per
-    // packet cost 10 us on 1M packets
-    const double inv = 1.0 / (double)S;
-    auto div_s = [&](uint64_t x) {
-      uint64_t d = (uint64_t)((double)x * inv);
-      if (d * S > x) --d;
-      if ((d + 1u) * S <= x) ++d;
-      return d;
+    const uint64_t G = spans.grid;
+    auto put = [&](uint64_t k, uint64_t nt, SpanRec r) {
+      const uint64_t e = G - nt;
+      const uint64_t ri = e ? k + k * e / nt : k;
+      const uint64_t r0 = k == 0 ? 0 : (e ? (k - 1) + (k - 1) * e / nt : k - 1) + 1;
+      for (uint64_t x = r0; x <= ri; ++x) spans.rec[x] = r;
     };
+    if (*spans.ctl) {  // byte tiles
+      const uint64_t S = spans.bytes, K = spans.count;
+      // x / S through the double reciprocal, corrected to the exact quotient
+      // (x < 2^53: the estimate is off by at most one); a u64 division per
+      // packet cost 10 us on 1M packets
+      const double inv = 1.0 / (double)S;
+      auto div_s = [&](uint64_t x) {
+        uint64_t d = (uint64_t)((double)x * inv);
+        if (d * S > x) --d;
+        if ((d + 1u) * S <= x) ++d;
+        return d;
+      };
 #pragma unroll
-    for (uint32_t j = 0; j < kScanItems; ++j) {
-      const uint32_t k = j * kBlock + threadIdx.x;
-      const uint64_t p = base + k;
-      if (p >= n) continue;
-      const uint64_t po = s_off[k] - p * H;  // packed payload offset of packet p
-      uint64_t lo = 0;
-      if (p > 0) {
-        const uint64_t prev_len = k > 0 ? s_len[k - 1] - H : len[p - 1];
-        lo = div_s(po - prev_len) + 1;  // spans after the one the previous packet starts in
+      for (uint32_t j = 0; j < kScanItems; ++j) {
+        const uint32_t k = j * kBlock + threadIdx.x;
+        const uint64_t p = base + k;
+        if (p >= n) continue;
+        const uint64_t po = s_off[k] - p * H;  // packed payload offset of packet p
+        uint64_t lo = 0;
+        if (p > 0) {
+          const uint64_t prev_len = k > 0 ? s_len[k - 1] - H : len[p - 1];
+          lo = div_s(po - prev_len) + 1;  // spans after the one the previous packet starts in
+        }
+        const uint64_t qpo = div_s(po);
+        const uint64_t hi = qpo < K ? qpo : K;
+        for (uint64_t t = lo; t <= hi; ++t) put(t, K, SpanRec{s_off[k], (uint32_t)p, 0u});
+        if (p == n - 1)
+          for (uint64_t t = (qpo + 1 > lo ? qpo + 1 : lo); t <= K; ++t)
+            put(t, K, SpanRec{s_off[k] + s_len[k], (uint32_t)n, 0u});
       }
-      const uint64_t qpo = div_s(po);
-      const uint64_t hi = qpo < K ? qpo : K;
-      for (uint64_t t = lo; t <= hi; ++t) spans.rec[t] = SpanRec{s_off[k], (uint32_t)p, 0u};
-      if (p == n - 1)
-        for (uint64_t t = (qpo + 1 > lo ? qpo + 1 : lo); t <= K; ++t)
-          spans.rec[t] = SpanRec{s_off[k] + s_len[k], (uint32_t)n, 0u};
-    }
-  }
-  if (spans.over) {
-    // tile k of this block: packets [k T, k T + T) (capped at n); its run
-    // from the 16-B aligned payload offsets at both ends
-    const uint32_t T = spans.tile_T, tiles = kScanBlockItems / T;
-    uint32_t c = 0;
-    for (uint32_t t0 = 0; t0 < tiles; t0 += kBlock) {  // (uniform rounds)
-      bool over = false;
-      const uint64_t k0 = (uint64_t)(t0 + threadIdx.x) * T;
-      if (t0 + threadIdx.x < tiles && base + k0 < n) {
-        const uint64_t k1 = base + k0 + T < n ? k0 + T : n - base;
-        const uint64_t f1 = k1 < kScanBlockItems ? s_off[k1] : s_off[k1 - 1] + s_len[k1 - 1];
-        const uint64_t pa = s_off[k0] - (base + k0) * H, pb = f1 - (base + k1) * H;
-        over = ((pb + 15u) & ~15ull) - (pa & ~15ull) > spans.tile_cap;
+    } else {  // packet tiles of spans.tile_T packets (a power of two dividing the block)
+      const uint32_t T = spans.tile_T, tiles = kScanBlockItems / T;
+      for (uint32_t i = threadIdx.x; i < tiles; i += kBlock) {
+        const uint64_t p = base + (uint64_t)i * T;
+        if (p < n) put(p / T, spans.ptiles, SpanRec{s_off[i * T], (uint32_t)p, 0u});
       }
-      c += (uint32_t)__syncthreads_count(over);
+      if (threadIdx.x == 0 && base + kScanBlockItems >= n) {  // the last block: the end record
+        const uint32_t kl = (uint32_t)(n - 1 - base);
+        put(spans.ptiles, spans.ptiles, SpanRec{s_off[kl] + s_len[kl], (uint32_t)n, 0u});
+      }
     }
-    if (threadIdx.x == 0 && c) atomicAdd(spans.over, c);
   }
 }
 
 void scan_block_sums(const uint32_t* d_len, uint64_t n, uint32_t H, uint32_t items, uint64_t* sums,
-                     const ScanCheck& chk, hipStream_t stream) {
+                     const ScanCheck& chk, hipStream_t stream, uint32_t over_T, uint32_t over_cap) {
   const uint64_t nb = (n + kBlock * items - 1) / (kBlock * items);
   const dim3 grid((uint32_t)nb), block(kBlock);
   switch (items) {
-    case 1: hipLaunchKernelGGL(scan_block_sums_kernel<1>, grid, block, 0, stream, d_len, n, H, sums, chk); break;
-    case 2: hipLaunchKernelGGL(scan_block_sums_kernel<2>, grid, block, 0, stream, d_len, n, H, sums, chk); break;
-    case 4: hipLaunchKernelGGL(scan_block_sums_kernel<4>, grid, block, 0, stream, d_len, n, H, sums, chk); break;
-    default: hipLaunchKernelGGL(scan_block_sums_kernel<8>, grid, block, 0, stream, d_len, n, H, sums, chk);
+    case 1: hipLaunchKernelGGL(scan_block_sums_kernel<1>, grid, block, 0, stream, d_len, n, H, sums, chk, 0u, 0u); break;
+    case 2: hipLaunchKernelGGL(scan_block_sums_kernel<2>, grid, block, 0, stream, d_len, n, H, sums, chk, 0u, 0u); break;
+    case 4: hipLaunchKernelGGL(scan_block_sums_kernel<4>, grid, block, 0, stream, d_len, n, H, sums, chk, 0u, 0u); break;
+    default: hipLaunchKernelGGL(scan_block_sums_kernel<8>, grid, block, 0, stream, d_len, n, H, sums, chk, over_T,
+                                over_cap);
   }
 }
 
 void scan_block_bases(uint64_t* sums, uint64_t nb, uint64_t* d_frame_off, uint64_t n, uint32_t H,
-                      const ScanCheck& chk, hipStream_t stream, uint32_t* zero) {
+                      const ScanCheck& chk, hipStream_t stream, uint32_t* ctl, uint32_t min_over) {
   hipLaunchKernelGGL(scan_block_bases_kernel, dim3(1), dim3(1024), 0, stream, sums, nb, d_frame_off, n, H, chk,
-                     zero);
+                     ctl, min_over);
 }
 
 int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint64_t* d_frame_off,
@@ -215,8 +246,8 @@ int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint
   uint64_t* sums = nullptr;
   hipError_t e = stream_alloc(reinterpret_cast<void**>(&sums), nb * sizeof(uint64_t), stream);
   if (e != hipSuccess) return (int)e;
-  scan_block_sums(d_len, n, H, kScanItems, sums, chk, stream);
-  scan_block_bases(sums, nb, d_frame_off, n, H, chk, stream, spans.over);
+  scan_block_sums(d_len, n, H, kScanItems, sums, chk, stream, spans.rec ? spans.tile_T : 0u, spans.tile_cap);
+  scan_block_bases(sums, nb, d_frame_off, n, H, chk, stream, spans.rec ? spans.ctl : nullptr, spans.min_over);
   hipLaunchKernelGGL(scan_apply_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, stream, d_len, n, H, sums,
                      d_frame_off, spans);
   e = hipGetLastError();

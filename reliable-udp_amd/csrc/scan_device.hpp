@@ -7,9 +7,11 @@
 namespace rudp {
 
 // Status bits of a block live above bit 56 of its pass-1 block sum (a sum of
-// at most 2048 x (2^32 - 1 + 7) fits in 44 bits).
+// at most 2048 x (2^32 - 1 + 7) fits in 44 bits); bits 44-55 hold the
+// varlen tile kernel's count of likely overflowing packet tiles (SpanStarts).
 constexpr int kSumBitsShift = 56;
-constexpr uint64_t kSumMask = (1ull << kSumBitsShift) - 1ull;
+constexpr int kSumCountShift = 44;
+constexpr uint64_t kSumMask = (1ull << kSumCountShift) - 1ull;
 
 // Exclusive scan of one u64 per thread over the block (all threads call it).
 __device__ inline uint64_t block_exclusive_scan(uint64_t x, uint64_t* total, uint64_t* s_wave) {

@@ -295,10 +295,10 @@ __device__ __forceinline__ uint32_t octet_sum(uint32_t x) {
 //            with the neighbour tiles are written bytewise.
 // A tile whose run exceeds tile_cap (lengths far above the caller's hint)
 // encodes its packets with the per-packet vector path instead.
-// Byte tiles (a.span_rec set and the scan's count of overflowing packet tiles
-// at least bt_min_over, read per launch): workgroup k frames the packets whose
-// payload starts in span k instead, their lanes per packet from their count.
-// The grid covers both forms.
+// Byte tiles (chosen by the scan per call, when enough packet tiles would
+// overflow): a workgroup frames the packets whose payload starts in one span
+// of S payload bytes instead, their lanes per packet from their count.  The
+// grid covers both forms; a tile learns its packets from the scan's records.
 // W: minimum waves per SIMD the register allocation must allow (1 = none).
 template <int H, int W>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))) encode_varlen_tile_kernel(VarlenArgs a) {
@@ -320,39 +320,20 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   __shared__ unsigned long long s_last[3];  // latest wave: sums, map, header chunks done
   if (a.trace && tid < 3u) s_last[tid] = 0ull;
 #endif
-  // Both forms' loads go out together (one round trip): the form, the span
-  // records, the packet tile's offsets.  Each form numbers its own tiles
-  // (XCD-contiguous over its own count) and leaves the surplus workgroups,
-  // the highest, idle: spread over the XCDs.
+  // Tile records (checked calls, a.span_rec): the scan chose the form for
+  // the whole call and wrote one record {frame_off[p], p} per workgroup for
+  // its first packet, so a tile's first loads are its two adjacent records
+  // whatever the form -- packet tiles of tile_T packets or byte tiles (the
+  // packets whose payload starts in one span of S bytes); the workgroups the
+  // chosen form does not need hold empty records spread over the grid.
+  // Unchecked calls: packet tiles from frame_off directly.
   const uint32_t b = blockIdx.x;
-  const uint32_t ptiles = (uint32_t)((a.n + a.tile_T - 1u) / a.tile_T);
-  const uint32_t tile_p = b < ptiles ? (a.xcd ? xcd_tile(b, ptiles) : b) : ptiles - 1u;
-  const uint64_t pp0 = (uint64_t)tile_p * a.tile_T;
-  const uint32_t pTv = a.n - pp0 < a.tile_T ? (uint32_t)(a.n - pp0) : a.tile_T;
-#if RUDP_TOOLS
-  const bool no_pload = (a.diag & 4u) && a.span_rec;  // ablation: byte tiles without the packet form's loads
-#else
-  constexpr bool no_pload = false;
-#endif
-  const uint64_t pfo0 = no_pload ? 0ull : a.frame_off[pp0], pfo_end = no_pload ? 0ull : a.frame_off[pp0 + pTv];
-  bool bt = false;
-  SpanRec r0{}, r1{};
-  const uint32_t spans = (uint32_t)a.span_count;
-  const uint32_t tile_s = b < spans ? (a.xcd ? xcd_tile(b, spans) : b) : 0u;
-  if (a.span_rec) {
-    bt = no_pload || *a.tile_over >= a.bt_min_over;
-    if (b < spans) {
-      r0 = a.span_rec[tile_s];
-      r1 = a.span_rec[tile_s + 1];
-    }
-  }
   uint64_t p0, fo0, fo_end;
   uint32_t Tv, Tall, T, glog;
-  if (bt) {
-    // the packets whose payload starts in span tile_s (clamped, so a rejected
-    // batch's unwritten records stay in range), their frame run from the same
-    // two records
-    if (b >= spans) return;
+  if (a.span_rec) {
+    const uint32_t t = a.xcd ? xcd_tile(b, gridDim.x) : b;
+    const SpanRec r0 = a.span_rec[t], r1 = a.span_rec[t + 1];
+    // (clamped, so a rejected batch's records stay in range)
     p0 = r0.p < a.n ? r0.p : a.n;
     const uint64_t p1 = r1.p < a.n ? (r1.p > p0 ? r1.p : p0) : a.n;
     Tall = (uint32_t)(p1 - p0);
@@ -365,12 +346,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     glog = 0;
     while (glog < 6u && (Tv << (glog + 1u)) <= kBlock) ++glog;
   } else {
+    const uint32_t ptiles = (uint32_t)((a.n + a.tile_T - 1u) / a.tile_T);
     if (b >= ptiles) return;
-    p0 = pp0;
+    p0 = (uint64_t)(a.xcd ? xcd_tile(b, ptiles) : b) * a.tile_T;
     T = a.tile_T;
-    Tv = Tall = pTv;
-    fo0 = pfo0;
-    fo_end = pfo_end;
+    Tv = Tall = a.n - p0 < a.tile_T ? (uint32_t)(a.n - p0) : a.tile_T;
+    fo0 = a.frame_off[p0];
+    fo_end = a.frame_off[p0 + Tv];
     glog = a.tile_glog;
   }
   const uint32_t G = 1u << glog, q = tid >> glog, g = tid & (G - 1u);
@@ -667,7 +649,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     }
   }
 #if RUDP_TOOLS
-  if (a.trace) {  // diagnostics: {start, loaded, summed, mapped, end, XCC, Tv | bt << 16 | vfast << 17, bytes,
+  if (a.trace) {  // diagnostics: {start, loaded, summed, mapped, end, XCC, Tv | records << 16 | vfast << 17, bytes,
                   //               latest wave's sums, map, header chunks done, 0}
     __syncthreads();
     if (tid == 0) {
@@ -675,7 +657,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
       rec[0] = make_u32x4(t_start, t_loaded);
       rec[1] = make_u32x4(t_summed, t_mapped);
       rec[2] = make_u32x4((uint64_t)wall_clock64(), __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20));
-      rec[3] = make_u32x4((uint64_t)Tv | (bt ? 1ull << 16 : 0ull) | (vfast ? 1ull << 17 : 0ull), (uint64_t)nbytes);
+      rec[3] = make_u32x4((uint64_t)Tv | (a.span_rec ? 1ull << 16 : 0ull) | (vfast ? 1ull << 17 : 0ull), (uint64_t)nbytes);
       rec[4] = make_u32x4(s_last[0], s_last[1]);
       rec[5] = make_u32x4(s_last[2], 0ull);
     }
@@ -1728,17 +1710,17 @@ static int vt_tiles_per_cu(size_t lds) {
 // fewer slots, down to min_slots, when that keeps them so -- and their grid
 // is at most 5% larger (the surplus workgroups of the form not taken still
 // occupy LDS for a round trip: 4000-B hints, 50% slower).
-bool varlen_btile_ok(uint32_t tile_T, uint32_t* bt_slots, uint32_t min_slots, uint32_t cap, uint32_t H,
-                     uint32_t vhc, uint64_t packet_tiles, uint64_t spans) {
+bool varlen_btile_ok(uint32_t tile_T, uint32_t* bt_slots, uint32_t min_slots, uint32_t cap, uint32_t cap_packet,
+                     uint32_t H, uint32_t vhc, uint64_t packet_tiles, uint64_t spans) {
   if (tile_T > 16u) return false;
-  auto per_cu = [&](uint32_t Tl) {
-    const size_t lds = varlen_tile_lds(Tl, cap, H, vhc);
+  auto per_cu = [&](uint32_t Tl, uint32_t c) {
+    const size_t lds = varlen_tile_lds(Tl, c, H, vhc);
     return H == 7u ? vt_tiles_per_cu<7>(lds) : vt_tiles_per_cu<5>(lds);
   };
-  const int want = per_cu(tile_T);
+  const int want = per_cu(tile_T, cap_packet);
   uint32_t slots = *bt_slots;
-  while (slots > tile_T && slots > min_slots && per_cu(slots) < want) --slots;
-  if ((slots > tile_T ? per_cu(slots) : want) < want) return false;
+  while (slots > tile_T && slots > min_slots && per_cu(slots, cap) < want) --slots;
+  if (per_cu(slots > tile_T ? slots : tile_T, cap) < want) return false;
   *bt_slots = slots;
   return spans * 20u <= packet_tiles * 21u;
 }

@@ -888,8 +888,11 @@ def test_varlen_tile_forms_vs_oracle(cuda, dist):
     tab = (dev(seq, cuda), dev(ack, cuda), dev(flags, cuda))
     for layout in (5, 7):
         want, off, cs = codec_np.encode_varlen(seq, ack, flags, pays, layout)
-        # (tile form: 1 auto / 2 byte tiles / 0 packet tiles, sum pass: 2 block sums / 0 chunks, XCD order)
-        for knobs in ((1, 2, 1), (2, 2, 1), (2, 2, 0), (2, 0, 1), (0, 2, 1), (0, 0, 1), (0, 2, 0)):
+        # (tile form: 1 the scan's choice / 2 byte tiles / 3 packet tiles through
+        # records / 0 packet tiles from frame_off, sum pass: 2 block sums / 0
+        # chunks, XCD order)
+        for knobs in ((1, 2, 1), (1, 0, 1), (1, 2, 0), (3, 2, 1), (2, 2, 1), (2, 2, 0), (2, 0, 1), (0, 2, 1),
+                      (0, 0, 1), (0, 2, 0)):
             old = [lib.rudpx_tune(key, v) for key, v in zip((51, 52, 49), knobs)]
             try:
                 r = batch.pack_batch_varlen(tab, dev(pay, cuda), dev(lens, cuda), layout, want_csum=True,
