@@ -28,27 +28,26 @@ constexpr uint32_t kScanBlockItems = kBlock * kScanItems;  // 2048 per block
 
 // ITEMS packets per thread: a block sums kBlock * ITEMS lengths (8 for the
 // offset scan; the small-frame encode uses its own tile size).
-// With over_T (ITEMS = 8 only): the block's packet tiles of over_T packets
-// whose length sum + 30 (a bound on their 16-B aligned payload run) exceeds
-// over_cap are counted into bits 44-55 of the sum.
+// With over_T (a power of two <= 64): the block's packet tiles of over_T
+// consecutive packets -- over_T consecutive lanes of one load -- whose length
+// sum + 30 (a bound on their 16-B aligned payload run) exceeds over_cap are
+// counted into bits 44-55 of the sum (at most 2048 tiles per block).
 template <uint32_t ITEMS>
 __global__ void __launch_bounds__(kBlock) scan_block_sums_kernel(const uint32_t* len, uint64_t n,
                                                                  uint32_t H, uint64_t* sums,
                                                                  ScanCheck chk, uint32_t over_T,
                                                                  uint32_t over_cap) {
   __shared__ uint64_t s_wave[kBlock / 64];
-  __shared__ uint32_t s_bits;
-  __shared__ uint32_t s_l[ITEMS == 8 ? kBlock * ITEMS : 1];
-  if (threadIdx.x == 0) s_bits = 0;
+  __shared__ uint32_t s_bits, s_over;
+  if (threadIdx.x == 0) s_bits = s_over = 0;
   const uint64_t base = (uint64_t)blockIdx.x * (kBlock * ITEMS);
   uint64_t acc = 0;
-  uint32_t bits = 0;
+  uint32_t bits = 0, over = 0;
 #pragma unroll
   for (uint32_t j = 0; j < ITEMS; ++j) {
     const uint64_t i = base + j * kBlock + threadIdx.x;
-    if (ITEMS == 8 && over_T) s_l[j * kBlock + threadIdx.x] = i < n ? len[i] : 0u;
+    const uint32_t l = i < n ? len[i] : 0u;
     if (i < n) {
-      const uint32_t l = len[i];
       acc += (uint64_t)l + H;
       if (chk.status) {
         if (l > kMaxPayload) bits |= RUDP_ST_LEN;
@@ -59,30 +58,25 @@ __global__ void __launch_bounds__(kBlock) scan_block_sums_kernel(const uint32_t*
         }
       }
     }
+    if (over_T) {  // (uniform)
+      uint64_t ts = l;
+      for (uint32_t m = 1; m < over_T; m <<= 1) ts += __shfl_xor(ts, (int)m, 64);
+      const bool o = (threadIdx.x & (over_T - 1u)) == 0 && i < n && ts + 30u > over_cap;
+      over += (uint32_t)__popcll(__ballot(o));
+    }
   }
   for (int m = 32; m > 0; m >>= 1) acc += __shfl_xor(acc, m, 64);
-  __syncthreads();  // s_bits initialised, s_l stored
+  __syncthreads();  // s_bits, s_over initialised
   if (bits) atomicOr(&s_bits, bits);
-  if ((threadIdx.x & 63u) == 0) s_wave[threadIdx.x >> 6] = acc;
-  uint32_t over = 0;
-  if (ITEMS == 8 && over_T) {
-    const uint32_t tiles = kBlock * ITEMS / over_T;  // (over_T a power of two <= 256)
-    for (uint32_t t0 = 0; t0 < tiles; t0 += kBlock) {  // (uniform rounds)
-      const uint32_t t = t0 + threadIdx.x;
-      bool o = false;
-      if (t < tiles) {
-        uint64_t sum = 0;
-        for (uint32_t k = 0; k < over_T; ++k) sum += s_l[t * over_T + k];
-        o = sum + 30u > over_cap;
-      }
-      over += (uint32_t)__syncthreads_count(o);
-    }
+  if ((threadIdx.x & 63u) == 0) {
+    s_wave[threadIdx.x >> 6] = acc;
+    if (over) atomicAdd(&s_over, over);  // (every lane holds its wave's count)
   }
   __syncthreads();
   if (threadIdx.x == 0) {
     uint64_t t = 0;
     for (uint32_t w = 0; w < kBlock / 64; ++w) t += s_wave[w];
-    sums[blockIdx.x] = t | ((uint64_t)over << kSumCountShift) | ((uint64_t)s_bits << kSumBitsShift);
+    sums[blockIdx.x] = t | ((uint64_t)s_over << kSumCountShift) | ((uint64_t)s_bits << kSumBitsShift);
   }
 }
 

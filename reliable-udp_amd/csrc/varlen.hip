@@ -1309,6 +1309,20 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
 #if RUDP_TOOLS
   const uint64_t t_start = a.trace ? (uint64_t)wall_clock64() : 0ull;  // diagnostics
 #endif
+  // The tile's lengths and header table (coalesced) go out first: they do not
+  // depend on the tile's base, so their round trip overlaps the base's.
+  uint32_t lv[FPT], sq[FPT], ak[FPT], fl[FPT];
+#pragma unroll
+  for (uint32_t j = 0; j < FPT; ++j) {
+    const uint32_t q = j * kBlock + tid;
+    lv[j] = sq[j] = ak[j] = fl[j] = 0;
+    if (q < Tv) {
+      lv[j] = a.len[p0 + q];
+      sq[j] = a.seq_in[p0 + q];
+      ak[j] = a.ack_in[p0 + q];
+      fl[j] = a.flags_in[p0 + q];
+    }
+  }
   if (FUSED) {
     __shared__ uint64_t s_pre[kBlock / 64], s_all[kBlock / 64];
     __shared__ uint32_t s_bits;
@@ -1364,22 +1378,8 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
   const uint64_t orun = ((fo_end + 15u) & ~15ull) - OA;
   const bool fits = prun <= cap && orun <= small_out_cap(T, cap, H);
 
-  // ---- loads: lengths, header table, payload run ---------------------------
+  // ---- loads: the payload run; lengths and header table to LDS -------------
   {
-    uint32_t lv[FPT], sq[FPT], ak[FPT], fl[FPT];
-#pragma unroll
-    for (uint32_t j = 0; j < FPT; ++j) {
-      const uint32_t q = j * kBlock + tid;
-      lv[j] = sq[j] = ak[j] = fl[j] = 0;
-      if (q < Tv) {
-        lv[j] = a.len[p0 + q];
-        if (fits) {
-          sq[j] = a.seq_in[p0 + q];
-          ak[j] = a.ack_in[p0 + q];
-          fl[j] = a.flags_in[p0 + q];
-        }
-      }
-    }
     if (fits) {
       const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + A);
       u32x4* dst = reinterpret_cast<u32x4*>(pay);
@@ -1438,11 +1438,13 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
   }
 
   // ---- frames into the LDS image of the output run ---------------------------
+  // (lane-strided: neighbouring lanes build neighbouring frames, so their LDS
+  // byte stores land a frame apart instead of FPT frames apart)
   const uint32_t lead = (uint32_t)(fo0 - OA);   // output bytes before fo0 in the first chunk
   const uint32_t pshift = (uint32_t)(po0 - A);  // LDS offset of payload byte po0
 #pragma unroll
   for (uint32_t i = 0; i < FPT; ++i) {
-    const uint32_t q = tid * FPT + i;
+    const uint32_t q = i * kBlock + tid;
     if (q < Tv) {
       const uint32_t Lq = s_len[q], fs = s_off[q];
       const unsigned char* src = pay + pshift + fs - q * (uint32_t)H;
