@@ -30,10 +30,12 @@ def main():
     ap.add_argument("--libs", required=True)
     ap.add_argument("--L", default="1472,1024,64")
     ap.add_argument("--reps", type=int, default=11)
-    ap.add_argument("--op", default="encode", choices=["encode", "decode", "varlen"],
+    ap.add_argument("--op", default="encode", choices=["encode", "decode", "varlen", "vdecode"],
                     help="decode: verify-only fixed-length rudp_decode of the encoded frames; varlen: "
                          "rudp_encode_varlen_checked of packed payloads, --L lengths or 'ragged' "
-                         "(uniform in [0, 2944]); a 'u' suffix (1472u) times the unchecked rudp_encode_varlen")
+                         "(uniform in [0, 2944]); a 'u' suffix (1472u) times the unchecked rudp_encode_varlen; "
+                         "vdecode: rudp_decode_varlen_checked (no status word) of such frames, rudp5 with the "
+                         "sideband checksums below 16-B payloads, else rudp7")
     args = ap.parse_args()
     _native.lib()  # torch's HIP runtime first
     libs = {}
@@ -54,13 +56,17 @@ def main():
         h.rudp_encode_varlen.argtypes = [ctypes.POINTER(_native.RudpBatch), ctypes.c_void_p, ctypes.c_void_p,
                                          ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         h.rudp_encode_varlen.restype = ctypes.c_int
+        h.rudp_decode_varlen_checked.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32,
+                                                 ctypes.c_uint64, ctypes.c_void_p] + [ctypes.c_void_p] * 6 + \
+                                                [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        h.rudp_decode_varlen_checked.restype = ctypes.c_int
         libs[name] = h
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream().cuda_stream
     out = {}
-    if args.op == "varlen":
+    if args.op in ("varlen", "vdecode"):
         for spec in args.L.split(","):
-            out[spec] = varlen_ab(libs, spec, args.reps, dev, stream)
+            out[spec] = (varlen_ab if args.op == "varlen" else vdecode_ab)(libs, spec, args.reps, dev, stream)
             print(spec, out[spec], file=sys.stderr, flush=True)
         print(json.dumps(out, indent=1))
         return
@@ -163,6 +169,50 @@ def varlen_ab(libs, spec, reps, dev, stream):
             e.synchronize()
             times[name].append(s.elapsed_time(e) / 10)
     return {"ms": {k: statistics.median(v) for k, v in times.items()}, "exact": exact, "payload_bytes": pbytes}
+
+
+def vdecode_ab(libs, spec, reps, dev, stream):
+    n = 1 << 20
+    g = torch.Generator(device=dev).manual_seed(0x5EED0004)
+    if spec == "ragged":
+        lens = torch.randint(0, 2945, (n,), dtype=torch.int32, device=dev, generator=g)
+        hint = 1472
+    else:
+        hint = int(spec)
+        lens = torch.full((n,), hint, dtype=torch.int32, device=dev)
+    layout = 5 if hint < 16 else 7
+    tab, _ = batch.synth_batch(n, 0, 0x5EED0004, device=dev)
+    pay = torch.randint(0, 256, (int(lens.sum().item()),), dtype=torch.uint8, device=dev, generator=g)
+    enc = batch.pack_batch_varlen(tab, pay, lens, layout, want_csum=layout == 5)
+    cs = enc.csum if layout == 5 else None
+    outs = [torch.empty((n,), dtype=dt, device=dev) for dt in (torch.uint16, torch.uint16, torch.uint8, torch.uint8,
+                                                                 torch.uint16)]
+
+    def call(h):
+        return h.rudp_decode_varlen_checked(enc.frames.data_ptr(), enc.frames.numel(), enc.frame_off.data_ptr(),
+                                            hint + layout, n, cs.data_ptr() if cs is not None else None,
+                                            *[t.data_ptr() for t in outs], None, layout, 0, stream)
+    ref, exact = None, {}
+    for name, h in libs.items():
+        for t in outs:
+            t.zero_()
+        assert call(h) == 0
+        got = torch.cat([t.view(torch.uint8) for t in outs])
+        ref = got if ref is None else ref
+        exact[name] = bool(torch.equal(got, ref))
+    times = {k: [] for k in libs}
+    for _ in range(reps):
+        for name, h in libs.items():
+            for _ in range(2):
+                call(h)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(10):
+                call(h)
+            e.record()
+            e.synchronize()
+            times[name].append(s.elapsed_time(e) / 10)
+    return {"ms": {k: statistics.median(v) for k, v in times.items()}, "exact": exact, "layout": layout}
 
 
 if __name__ == "__main__":
