@@ -243,14 +243,13 @@ int check_frame_offsets(const uint64_t* d_frame_off, uint64_t n, uint64_t frames
   uint64_t want = (n + 1 + kBlock * 8 - 1) / (kBlock * 8);
   const uint32_t blocks = (uint32_t)(want < 1 ? 1 : want > kBoundsBlocks ? kBoundsBlocks : want);
   uint32_t* partial = nullptr;
-  hipError_t e = stream_alloc(reinterpret_cast<void**>(&partial), blocks * sizeof(uint32_t), stream);
+  hipError_t e = stream_scratch(reinterpret_cast<void**>(&partial), blocks * sizeof(uint32_t), stream,
+                                kScratchBounds);
   if (e != hipSuccess) return (int)e;
   hipLaunchKernelGGL(off_check_kernel, dim3(blocks), dim3(kBlock), 0, stream, d_frame_off, n, frames_bytes,
                      partial);
   hipLaunchKernelGGL(off_check_final_kernel, dim3(1), dim3(kBlock), 0, stream, partial, blocks, d_status);
-  e = hipGetLastError();
-  hipError_t e2 = stream_free(partial, stream);
-  return (int)(e != hipSuccess ? e : e2);
+  return (int)hipGetLastError();
 }
 
 }  // namespace rudp

@@ -656,7 +656,7 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
       spans.tile_cap = a.tile_cap;
       void* buf = nullptr;
       // records [grid + 1], then pass 2's choice
-      RUDP_HIP(stream_alloc(&buf, (spans.grid + 2u) * sizeof(SpanRec), s));
+      RUDP_HIP(stream_scratch(&buf, (spans.grid + 2u) * sizeof(SpanRec), s, kScratchRecords));
       spans.rec = static_cast<SpanRec*>(buf);
       spans.ctl = reinterpret_cast<uint32_t*>(spans.rec + spans.grid + 1u);
       a.span_rec = spans.rec;
@@ -666,10 +666,6 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
   }
   rc = scan_frame_offsets(in->len, in->n, (uint32_t)layout, d_frame_off, chk, s, spans);
   if (!rc) rc = launch_encode_varlen(a, layout, s);
-  if (spans.rec) {
-    const hipError_t e = stream_free(spans.rec, s);
-    if (!rc && e != hipSuccess) return hip_fail(e, "hipFreeAsync");
-  }
   if (rc) return hip_fail((hipError_t)rc, "varlen encode");
   return 0;
 }
@@ -819,12 +815,10 @@ static int dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_
   a.lim_checked = checked ? 1u : 0u;
   a.frames_lim = frames_bytes;
   void* scratch = nullptr;
-  RUDP_HIP(stream_alloc(&scratch, n * sizeof(uint64_t), s));
+  RUDP_HIP(stream_scratch(&scratch, n * sizeof(uint64_t), s, kScratchHash));
   a.hash = (uint64_t*)scratch;
   rc = launch_dedup(a, s);
-  hipError_t e = stream_free(scratch, s);
   if (rc) return hip_fail((hipError_t)rc, "dedup launch");
-  if (e != hipSuccess) return hip_fail(e, "hipFreeAsync");
   return 0;
 }
 

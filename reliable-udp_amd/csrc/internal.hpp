@@ -362,6 +362,9 @@ uint32_t dedup_max_window();
 // that keeps its memory across synchronizes (device_pool.hip).
 hipError_t stream_alloc(void** ptr, size_t bytes, hipStream_t stream);
 hipError_t stream_free(void* ptr, hipStream_t stream);
+// A per-(host thread, device, stream, slot) temporary kept across calls (device_pool.hip).
+enum ScratchSlot { kScratchSums = 0, kScratchRecords = 1, kScratchHash = 2, kScratchBounds = 3 };
+hipError_t stream_scratch(void** ptr, size_t bytes, hipStream_t stream, int slot);
 
 struct Bounds {
   uint64_t min_len, max_len, sum_len;

@@ -238,16 +238,13 @@ int scan_frame_offsets_3pass(const uint32_t* d_len, uint64_t n, uint32_t H, uint
                              const ScanCheck& chk, hipStream_t stream, const SpanStarts& spans) {
   const uint64_t nb = (n + kScanBlockItems - 1) / kScanBlockItems;
   uint64_t* sums = nullptr;
-  hipError_t e = stream_alloc(reinterpret_cast<void**>(&sums), nb * sizeof(uint64_t), stream);
+  hipError_t e = stream_scratch(reinterpret_cast<void**>(&sums), nb * sizeof(uint64_t), stream, kScratchSums);
   if (e != hipSuccess) return (int)e;
   scan_block_sums(d_len, n, H, kScanItems, sums, chk, stream, spans.rec ? spans.tile_T : 0u, spans.tile_cap);
   scan_block_bases(sums, nb, d_frame_off, n, H, chk, stream, spans.rec ? spans.ctl : nullptr, spans.min_over);
   hipLaunchKernelGGL(scan_apply_kernel, dim3((uint32_t)nb), dim3(kBlock), 0, stream, d_len, n, H, sums,
                      d_frame_off, spans);
-  e = hipGetLastError();
-  hipError_t e2 = stream_free(sums, stream);
-  if (e != hipSuccess) return (int)e;
-  return (int)e2;
+  return (int)hipGetLastError();
 }
 
 }  // namespace rudp

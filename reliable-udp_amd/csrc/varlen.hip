@@ -1535,17 +1535,15 @@ int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int
   const uint64_t T = (uint64_t)kBlock * fpt;
   const uint64_t nb = (args.n + T - 1) / T;
   uint64_t* sums = nullptr;
-  hipError_t e = stream_alloc(reinterpret_cast<void**>(&sums), nb * sizeof(uint64_t), stream);
+  hipError_t e = stream_scratch(reinterpret_cast<void**>(&sums), nb * sizeof(uint64_t), stream, kScratchSums);
   if (e != hipSuccess) return (int)e;
   // pass 1, then either the framing kernel finds its own base (two launches)
   // or pass 2 runs between them (three)
   const bool fused = tuning().varlen_small_fused && nb <= kSmallFusedTiles;
   scan_block_sums(args.len, args.n, (uint32_t)layout, fpt, sums, chk, stream);
   if (!fused) scan_block_bases(sums, nb, const_cast<uint64_t*>(args.frame_off), args.n, (uint32_t)layout, chk, stream);
-  const int rc = layout == 7 ? launch_small_any<7>(args, sums, nb, chk, fused, stream)
-                             : launch_small_any<5>(args, sums, nb, chk, fused, stream);
-  e = stream_free(sums, stream);
-  return rc ? rc : (int)e;
+  return layout == 7 ? launch_small_any<7>(args, sums, nb, chk, fused, stream)
+                     : launch_small_any<5>(args, sums, nb, chk, fused, stream);
 }
 
 // Small-frame decode: a tile of T = 256 * FPT consecutive frames (the
