@@ -30,7 +30,10 @@
  *    calling thread is available from rudp_last_error().
  *  - Reentrant and thread-safe: the only global state is mutex-guarded
  *    per-device caches (the *_host staging pipeline, the stream-ordered
- *    scratch pool, the bounds scratch).  Every launch choice is fixed at its
+ *    scratch pool, the bounds scratch).  A call's device temporaries (scan
+ *    sums, tile records, dedup hashes) are kept per calling thread, device
+ *    and stream, reused by its next call on that stream (stream order keeps
+ *    them safe) and held until the process exits.  Every launch choice is fixed at its
  *    measured default; librudp.so exports exactly the functions below.  (The
  *    diagnostics build of the same sources, librudp_tools.so, adds non-ABI
  *    rudpx_* sweep knobs and timelines for tools/ and is not a product library.)
