@@ -74,8 +74,11 @@ def cpu_baseline(L: int, per_worker: int, workers: int):
         "unit": "GiB/s",
         "cores": workers,
         "kind": "port",
-        "sample": f"{workers} workers x {per_worker} packets x {L} B, rudp7 encode through "
-                  f"oracle/bitstring_packet.py (utils/packet.py algorithm), payload GiB/s",
+        "sample": f"{workers} workers x {per_worker} packets x {L} B: the reference's framing "
+                  f"(Packet(), set_header_field x4, set_payload, to_byte: utils/packet.py's bit-string "
+                  f"algorithm, oracle/bitstring_packet.py) of the rudp7 layout, payload GiB/s.  The "
+                  f"reference has no checksum: the checksum field's value is computed with numpy "
+                  f"before the clock and only the framing is timed",
         "single_core_value": single[0] / single[1] / GIB,
         "single_core_us_per_packet": single[1] / max(per_worker // 4, 256) * 1e6,
         "cpu_model": _cpu_model(),
@@ -226,10 +229,26 @@ C5_PACKETS = 1 << 24
 C5_SEED = 0x5EED0005   # tests/golden/make_golden.py CONFIGS["C5"]
 
 
-def c5_strong_leg(torch, dist, batch, device, world, rank, layout, share_device, steps=10):
+def over_ranks(torch, dist, world, share_device, device, wall_s, kernel_ms):
+    """The job's clock: MAX over ranks of the wall time (device tensors over RCCL,
+    CPU tensors over gloo), and every rank's HIP-event kernel time gathered, so
+    the roofline can be the slowest GPU's.  Returns (wall_max_s, [kernel_ms per rank])."""
+    if world == 1 and not dist.is_initialized():
+        return wall_s, [kernel_ms]
+    where = "cpu" if share_device else device
+    t = torch.tensor([wall_s], dtype=torch.float64, device=where)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    k = torch.tensor([kernel_ms], dtype=torch.float64, device=where)
+    ks = [torch.empty_like(k) for _ in range(dist.get_world_size())]
+    dist.all_gather(ks, k)
+    return float(t.item()), [float(x.item()) for x in ks]
+
+
+def c5_strong_leg(torch, dist, batch, device, world, rank, layout, share_device, steps=10, total=None):
     """BASELINE config 5: 16M x 1472 B packets sharded over the ranks by slicing
     (rank r frames packets [r*16M/N, (r+1)*16M/N)); whole-job payload GiB/s."""
-    first, n = rank_slice(rank, world, C5_PACKETS)
+    total = total or C5_PACKETS
+    first, n = rank_slice(rank, world, total)
     w = Workload(torch, batch, n, 1472, layout, first, C5_SEED, device, min_bytes=0)
     for i in range(2):
         w.encode(batch, i)
@@ -242,10 +261,7 @@ def c5_strong_leg(torch, dist, batch, device, world, rank, layout, share_device,
     torch.cuda.synchronize()
     dist.barrier()
     torch.cuda.synchronize()
-    t = torch.tensor([time.perf_counter() - t0], dtype=torch.float64,
-                     device="cpu" if share_device else device)
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall = float(t.item())
+    wall, _ = over_ranks(torch, dist, world, share_device, device, time.perf_counter() - t0, 0.0)
     # every rank's frames against the reference's chunk digests (outside the clock)
     chk = verify_c5(w, first, n)
     ok = torch.tensor([0 if chk is None else int(chk[0] == chk[1]), 0 if chk is None else chk[1]],
@@ -253,10 +269,10 @@ def c5_strong_leg(torch, dist, batch, device, world, rank, layout, share_device,
     dist.all_reduce(ok, op=dist.ReduceOp.SUM)
     del w
     torch.cuda.empty_cache()
-    return {"GiB_s": C5_PACKETS * 1472 * steps / wall / GIB, "ms": wall / steps * 1e3,
+    return {"GiB_s": total * 1472 * steps / wall / GIB, "ms": wall / steps * 1e3,
             "ranks_bit_exact_vs_reference": int(ok[0].item()),
             "chunks_matching_reference_digests": int(ok[1].item()),
-            "packets_total": C5_PACKETS, "packets_per_gpu": n, "n_gpus": world, "steps": steps,
+            "packets_total": total, "packets_per_gpu": n, "n_gpus": world, "steps": steps,
             "per_gpu_roofline_frac": n * algorithmic_bytes_encode(1472) / (wall / steps) / 1e9 / HBM_PEAK_GBS,
             "scaling": "strong"}
 
@@ -306,6 +322,26 @@ def legs(torch, batch, device, steps):
     out["decode_verify_1Mx1472"] = {
         "GiB_s": (1 << 20) * 1472 / (ms / 1e3) / GIB, "ms": ms,
         "roofline_frac": (1 << 20) * algorithmic_bytes_decode(1472) / (ms / 1e3) / 1e9 / HBM_PEAK_GBS}
+    # the reference's whole receive per datagram: parse + verify + get_payload()'s strict
+    # UTF-8 decode (utils/reliableUDP.py:118-123, utils/packet.py:73), in one pass
+    # (rudp_decode_utf8), beside the two-pass form (decode, then the validation kernel)
+    nsets = len(w.sets)
+    ms_u = time_loop(torch, lambda i: batch.unpack_batch(w.sets[i % nsets][2], "rudp7", utf8=True),
+                     steps, 3) / steps
+
+    def two_pass(i):
+        batch.unpack_batch(w.sets[i % nsets][2], "rudp7")
+        batch.validate_utf8(w.sets[i % nsets][2], "rudp7")
+    ms_2 = time_loop(torch, two_pass, steps, 3) / steps
+    du = batch.unpack_batch(w.sets[0][2], "rudp7", utf8=True)
+    out["decode_utf8_1Mx1472"] = {
+        "GiB_s": (1 << 20) * 1472 / (ms_u / 1e3) / GIB, "ms": ms_u,
+        "roofline_frac": (1 << 20) * (algorithmic_bytes_decode(1472) + 1) / (ms_u / 1e3) / 1e9 / HBM_PEAK_GBS,
+        "two_pass_ms": ms_2,
+        "all_valid_and_verified": bool((du.valid == 1).all()) and bool((du.ok == 1).all()),
+        "note": "rudp_decode_utf8: parse + verify + strict UTF-8 per frame in the decode tile kernel; "
+                "algorithmic bytes L + 7 read, 7 written; two_pass_ms = rudp_decode then rudp_validate_utf8"}
+    del du
 
     def rt(i):
         w.encode(batch, i)
@@ -425,6 +461,9 @@ def legs(torch, batch, device, steps):
         def d_reuse(i):
             last["d"] = batch.unpack_batch_varlen(frames, off, layout, csum=csum, check=False, reuse=last["d"])
 
+        def d_utf8(i):  # parse + verify + get_payload()'s strict UTF-8, one kernel
+            last["u"] = batch.unpack_batch_varlen(frames, off, layout, csum=csum, check=False, utf8=True)
+
         def e_abi(i):
             lib.rudp_encode_varlen_checked(ctypes.byref(rb), flat.numel(), f_out.data_ptr(), f_out.numel(),
                                            o_out.data_ptr(), c_out.data_ptr() if c_out is not None else None,
@@ -436,7 +475,7 @@ def legs(torch, batch, device, steps):
                                            csum.data_ptr() if csum is not None else None,
                                            *[t.data_ptr() for t in d_out], None, H,
                                            device.index or 0, sp)
-        fns = {"encode": e, "decode": d, "encode_reuse": e_reuse, "decode_reuse": d_reuse,
+        fns = {"encode": e, "decode": d, "encode_reuse": e_reuse, "decode_reuse": d_reuse, "decode_utf8": d_utf8,
                "encode_eager_check": lambda i: e(i, True),
                "decode_eager_check": lambda i: d(i, True), "encode_abi": e_abi, "decode_abi": d_abi}
         per = {k: [] for k in fns}
@@ -523,6 +562,10 @@ def legs(torch, batch, device, steps):
     out["proxy_dedup_1M_window500"] = {"Mpkt_s": n1 / ms_x / 1e3, "ms": ms_x, "ms_eager_check": ms_xe,
                                        "note": "rudp_dedup_window_checked through the Python entry, sync-free"}
     del tab1, pay1, lens1, flat1, enc
+    # the proxy-role caller's batch sizes (recvmmsg batches of <= 1024, proxy.py:126-154) and a
+    # large socket batch: per-call cost of the sync-free entries back to back, and the latency of
+    # one call waited for (launch + kernels + one synchronize)
+    out["small_batch_calls"] = small_batch_calls(torch, batch, device)
     # socket boundary: 1M one-character frames sendmmsg'd over loopback, recvmmsg'd into a
     # pinned ring and decoded on the GPU per received batch (rudp.netio)
     out["socket_e2e_1M_x_1char"] = socket_leg(torch, batch, device)
@@ -547,6 +590,50 @@ def legs(torch, batch, device, steps):
     out["d2d_copy_gridstride_GBs"] = 2 * a.numel() / (ms_gs / 1e3) / 1e9
     del w, a, b
     torch.cuda.empty_cache()
+    return out
+
+
+def small_batch_calls(torch, batch, device, sizes=(1024, 65536), reps=200):
+    """Per-call times at the batch sizes a reference caller produces: one-character
+    rudp5 datagrams (utils/reliableUDP.py:11), n per call.  ``us_per_call``: the
+    median of 5 runs of `reps` back-to-back sync-free calls on one stream (HIP
+    events, outputs reused); ``us_latency``: wall time of one call plus its
+    synchronize, median of `reps` (what a caller that waits for every batch sees)."""
+    out = {}
+    for n in sizes:
+        tab, pay = batch.synth_batch(n, 1, SEEDS[1472], device=device)
+        lens = torch.ones(n, dtype=torch.int32, device=device)
+        flat = pay.view(-1)
+        enc = batch.pack_batch_varlen(tab, flat, lens, "rudp5", want_csum=True)
+        last = {"e": enc, "d": batch.unpack_batch_varlen(enc.frames, enc.frame_off, "rudp5", csum=enc.csum),
+                "u": batch.unpack_batch_varlen(enc.frames, enc.frame_off, "rudp5", csum=enc.csum, utf8=True)}
+        ops = {
+            "encode": lambda: last.__setitem__("e", batch.pack_batch_varlen(
+                tab, flat, lens, "rudp5", want_csum=True, check=False, reuse=last["e"])),
+            "decode": lambda: last.__setitem__("d", batch.unpack_batch_varlen(
+                enc.frames, enc.frame_off, "rudp5", csum=enc.csum, check=False, reuse=last["d"])),
+            "decode_utf8": lambda: last.__setitem__("u", batch.unpack_batch_varlen(
+                enc.frames, enc.frame_off, "rudp5", csum=enc.csum, check=False, reuse=last["u"], utf8=True)),
+            "dedup_window500": lambda: batch.detect_retransmissions(enc.frames, frame_off=enc.frame_off,
+                                                                    window=500, check=False),
+        }
+        row = {}
+        for name, fn in ops.items():
+            per = sorted(time_loop(torch, lambda i: fn(), reps, 5) / reps * 1e3 for _ in range(5))
+            lat = []
+            for _ in range(reps):
+                t0 = time.perf_counter()
+                fn()
+                torch.cuda.synchronize()
+                lat.append((time.perf_counter() - t0) * 1e6)
+            lat.sort()
+            row[name] = {"us_per_call": per[2], "us_latency": lat[len(lat) // 2],
+                         "Mpkt_s_back_to_back": n / per[2]}
+        last["e"].check()
+        last["d"].check()
+        out[f"n{n}"] = row
+    out["note"] = ("1-char rudp5 datagrams; Python entries, sync-free, outputs reused; us_per_call: back-to-back "
+                   "calls on one stream (HIP events); us_latency: one call + torch.cuda.synchronize (wall)")
     return out
 
 
@@ -712,6 +799,11 @@ def main():
                     help="packets per CPU worker at 16 workers, scaled to keep the total (16 x 32768 x ~26 us: about 14 s of CPU work)")
     ap.add_argument("--share-device", action="store_true",
                     help="testing only: every rank uses cuda:0 and gloo (rehearse N>1 on one GPU)")
+    ap.add_argument("--dist", action="store_true",
+                    help="testing only: the N>1 code path (process group, collectives, C5 strong leg) "
+                         "also at N = 1, so the RCCL branch runs on a one-GPU box")
+    ap.add_argument("--c5-packets", type=int, default=0,
+                    help="testing only: packets of the C5 strong leg (default 16M)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -733,7 +825,8 @@ def main():
     dev_index = 0 if args.share_device else local_rank
     torch.cuda.set_device(dev_index)
     device = torch.device("cuda", dev_index)
-    if world > 1:
+    distributed = world > 1 or args.dist
+    if distributed:
         if args.share_device:
             dist.init_process_group("gloo")
         else:
@@ -742,7 +835,7 @@ def main():
     # which physical GPU each rank drives: index, PCI address and UUID, gathered to
     # rank 0 for the line; without --share-device every rank must hold its own GPU
     devices = [device_record(torch, rank, local_rank, dev_index)]
-    if world > 1:
+    if distributed:
         gathered = [None] * world
         dist.all_gather_object(gathered, devices[0])
         devices = gathered
@@ -760,7 +853,7 @@ def main():
     for i in range(args.warmup):
         w.encode(batch, i)
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     start = torch.cuda.Event(enable_timing=True)
@@ -771,33 +864,32 @@ def main():
         w.encode(batch, args.warmup + i)
     stop.record()
     torch.cuda.synchronize()
-    if world > 1:
+    if distributed:
         dist.barrier()
     torch.cuda.synchronize()
     wall = time.perf_counter() - t0
-    kernel_ms = start.elapsed_time(stop)
-    t = torch.tensor([wall], dtype=torch.float64,
-                     device="cpu" if args.share_device else device)
-    if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    wall_max = float(t.item())
+    # every rank's kernel time: the roofline is the slowest GPU's
+    wall_max, rank_kernel_ms = over_ranks(torch, dist, world, args.share_device, device, wall,
+                                          start.elapsed_time(stop))
+    kernel_ms = max(rank_kernel_ms)
 
     # the timed frames against the reference (BASELINE configs 2-4 by payload size), outside the clock
     head_chk = verify_digests(w, {1024: "C2", 64: "C3", 1472: "C4"}.get(L, ""), first, n)
     del w
     torch.cuda.empty_cache()
     extra = legs(torch, batch, device, max(10, args.steps // 2)) if (
-        rank == 0 and world == 1 and not args.no_legs) else None
-    if world > 1 and not args.no_legs and not args.total_packets:
+        rank == 0 and not distributed and not args.no_legs) else None
+    if distributed and not args.no_legs and not args.total_packets:
         # BASELINE config 5 beside the weak-scaling headline: 16M x 1472 B split
         # over the ranks (strong scaling), same barrier + max-over-ranks clock.
         extra = {"c5_16Mx1472_strong": c5_strong_leg(torch, dist, batch, device, world, rank,
-                                                      args.layout, args.share_device)}
+                                                      args.layout, args.share_device,
+                                                      total=args.c5_packets or None)}
 
     if rank == 0:
         # strong scaling: the ranks' slices add up to --total-packets (rank_slice)
         total_payload = (args.total_packets or world * n) * L * args.steps
-        per_launch_s = kernel_ms / 1e3 / args.steps
+        per_launch_s = kernel_ms / 1e3 / args.steps  # the slowest rank's
         achieved = n * algorithmic_bytes_encode(L) / per_launch_s / 1e9
         traffic, traffic_src = read_pmc_traffic(L, n)
         line = {
@@ -832,6 +924,8 @@ def main():
                 "traffic": traffic,
                 "algorithmic_bytes_per_launch": n * algorithmic_bytes_encode(L),
                 "kernel_ms_per_launch": per_launch_s * 1e3,
+                "kernel_ms_per_launch_by_rank": [k / args.steps for k in rank_kernel_ms],
+                "rank_note": "achieved/frac from the slowest rank's HIP-event kernel time",
                 "traffic_source": traffic_src,
             },
             "cpu_baseline": cpu,
@@ -843,7 +937,7 @@ def main():
                 line["roofline"]["measured_copy_ceiling_GBs"] = ceiling
                 line["roofline"]["frac_of_copy_ceiling"] = achieved / ceiling
         print(json.dumps(line), flush=True)
-    if world > 1:
+    if distributed:
         dist.destroy_process_group()
 
 

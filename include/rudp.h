@@ -30,10 +30,17 @@
  *    calling thread is available from rudp_last_error().
  *  - Reentrant and thread-safe: the only global state is mutex-guarded
  *    per-device caches (the *_host staging pipeline, the stream-ordered
- *    scratch pool, the bounds scratch).  A call's device temporaries (scan
- *    sums, tile records, dedup hashes) are kept per calling thread, device
- *    and stream, reused by its next call on that stream (stream order keeps
- *    them safe) and held until the process exits.  Every launch choice is fixed at its
+ *    scratch pool, the call temporaries).  A call's device temporaries (scan
+ *    sums, tile records, dedup hashes, offset-check partials) are kept per
+ *    (device, stream), shared by all host threads: a call holds its stream's
+ *    set while it enqueues (calls on one stream serialize on the host, as
+ *    they do on the GPU) and the next call on that stream reuses it (stream
+ *    order keeps them safe).  Nothing is held per host thread, so short-lived
+ *    threads leave nothing behind; at most 64 streams per device keep a set
+ *    (a 65th takes the least recently used one after a device synchronize),
+ *    and a temporary grown past 64 MiB is freed when its call ends.  Under
+ *    stream capture the temporaries are allocated and freed inside the graph.
+ *    Every launch choice is fixed at its
  *    measured default; librudp.so exports exactly the functions below.  (The
  *    diagnostics build of the same sources, librudp_tools.so, adds non-ABI
  *    rudpx_* sweep knobs and timelines for tools/ and is not a product library.)
@@ -47,7 +54,7 @@
 extern "C" {
 #endif
 
-#define RUDP_ABI_VERSION 5
+#define RUDP_ABI_VERSION 6
 
 /* Frame layouts: the value is the header length in bytes. */
 #define RUDP_LAYOUT_RUDP5 5 /* reference-exact 5-byte header, checksum sideband */
@@ -186,6 +193,32 @@ int rudp_decode_varlen_checked(const uint8_t* d_frames, uint64_t frames_bytes, c
                                void* hip_stream);
 int rudp_frame_off_check(const uint64_t* d_frame_off, uint64_t n, uint64_t frames_bytes, uint32_t* d_status,
                          int device, void* hip_stream);
+
+/*
+ * Decode and strict-UTF-8 check in one pass (ABI 6): the reference's receive
+ * parses every datagram AND decodes its payload (utils/reliableUDP.py:118-123:
+ * Packet(data) -> get_header_field ... -> get_payload, whose strict
+ * bytes.decode() is utils/packet.py:73).  As rudp_decode /
+ * rudp_decode_varlen_checked, plus d_valid_or_null: d_valid[i] = 1 when
+ * Packet(frame).get_payload() would return (an empty payload or a frame
+ * shorter than the header: None), 0 when it would raise UnicodeDecodeError
+ * -- rudp_validate_utf8's answer -- and 0 for a frame rejected for bad
+ * offsets (nothing of it is read).  The LDS-tile decode kernels (fixed-length
+ * frames whose 256/G-frame tile fits 64 KiB; packed frames of every hint)
+ * judge each payload from the bytes they already hold, so every frame leaves
+ * HBM once; other fixed-length shapes run the validation kernel after the
+ * decode.  d_valid_or_null NULL: exactly rudp_decode / rudp_decode_varlen_checked.
+ */
+int rudp_decode_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, uint32_t frame_len,
+                     uint64_t n, const uint16_t* d_csum_in_or_null, uint16_t* d_seq, uint16_t* d_ack,
+                     uint8_t* d_flags, uint8_t* d_ok, uint16_t* d_csum_out_or_null,
+                     uint8_t* d_payload_out_or_null, uint8_t* d_valid_or_null, int layout, int device,
+                     void* hip_stream);
+int rudp_decode_varlen_utf8(const uint8_t* d_frames, uint64_t frames_bytes, const uint64_t* d_frame_off,
+                            uint32_t len_hint, uint64_t n, const uint16_t* d_csum_in_or_null,
+                            uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags, uint8_t* d_ok,
+                            uint16_t* d_csum_out_or_null, uint8_t* d_valid_or_null, uint32_t* d_status,
+                            int layout, int device, void* hip_stream);
 
 /*
  * Bounds of a variable-length batch, computed on the device (argument checks

@@ -17,7 +17,7 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
                   const uint16_t* d_csum_in, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
                   uint8_t* d_ok, uint16_t* d_csum_out, uint8_t* d_payload_out, int layout,
                   int device, void* hip_stream, bool checked = false, uint32_t* status_out = nullptr,
-                  uint64_t frames_lim = 0);
+                  uint64_t frames_lim = 0, uint8_t* d_valid = nullptr);
 namespace {
 
 thread_local std::string g_last_error;
@@ -325,7 +325,8 @@ uint32_t decode_group_log2(uint32_t L) {
 int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t len_hint, uint64_t n,
                   const uint16_t* d_csum_in, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
                   uint8_t* d_ok, uint16_t* d_csum_out, uint8_t* d_payload_out, int layout,
-                  int device, void* hip_stream, bool checked, uint32_t* status_out, uint64_t frames_lim) {
+                  int device, void* hip_stream, bool checked, uint32_t* status_out, uint64_t frames_lim,
+                  uint8_t* d_valid) {
   if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
     return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
   if (d_payload_out)
@@ -346,6 +347,7 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
   a.flags = d_flags;
   a.ok = d_ok;
   a.csum_out = d_csum_out;
+  a.valid = d_valid;
   a.n = n;
   // Lanes per frame from the caller's typical frame length (0 = unknown:
   // tiny frames).  Two or more 16-byte chunks per lane, G in [2, 16].
@@ -452,9 +454,19 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, ui
                 uint64_t n, const uint16_t* d_csum_in_or_null, uint16_t* d_seq, uint16_t* d_ack,
                 uint8_t* d_flags, uint8_t* d_ok, uint16_t* d_csum_out_or_null,
                 uint8_t* d_payload_out_or_null, int layout, int device, void* hip_stream) {
+  return rudp_decode_utf8(d_frames, d_frame_off_or_null, frame_len, n, d_csum_in_or_null, d_seq, d_ack, d_flags,
+                          d_ok, d_csum_out_or_null, d_payload_out_or_null, nullptr, layout, device, hip_stream);
+}
+
+int rudp_decode_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, uint32_t frame_len,
+                     uint64_t n, const uint16_t* d_csum_in_or_null, uint16_t* d_seq, uint16_t* d_ack,
+                     uint8_t* d_flags, uint8_t* d_ok, uint16_t* d_csum_out_or_null,
+                     uint8_t* d_payload_out_or_null, uint8_t* d_valid_or_null, int layout, int device,
+                     void* hip_stream) {
   if (d_frame_off_or_null) {
     return decode_varlen(d_frames, d_frame_off_or_null, frame_len, n, d_csum_in_or_null, d_seq, d_ack, d_flags,
-                         d_ok, d_csum_out_or_null, d_payload_out_or_null, layout, device, hip_stream);
+                         d_ok, d_csum_out_or_null, d_payload_out_or_null, layout, device, hip_stream, false,
+                         nullptr, 0, d_valid_or_null);
   }
   int rc = validate_decode(d_frames, nullptr, frame_len, n, d_seq, d_ack, d_flags, d_ok, layout);
   if (rc || n == 0) return rc;
@@ -465,7 +477,8 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, ui
   a.stage_out = (tuning().decode_stage_out &&
                  ((reinterpret_cast<uintptr_t>(d_seq) | reinterpret_cast<uintptr_t>(d_ack) |
                    reinterpret_cast<uintptr_t>(d_flags) | reinterpret_cast<uintptr_t>(d_ok) |
-                   reinterpret_cast<uintptr_t>(d_csum_out_or_null)) & 3u) == 0) ? 1u : 0u;
+                   reinterpret_cast<uintptr_t>(d_csum_out_or_null) | reinterpret_cast<uintptr_t>(d_valid_or_null)) &
+                  3u) == 0) ? 1u : 0u;
   a.xcd = (tuning().tile_xcd && frame_len >= 128u) ? 1u : 0u;
   a.frames = d_frames;
   a.csum_in = d_csum_in_or_null;
@@ -501,8 +514,24 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, ui
         forced <= 4 && (size_t)(256u >> forced) * frame_len + 48 <= 65536)
       a.glog = (uint32_t)forced;
   }
+  // The tile kernels check each payload's UTF-8 in the same pass; the other
+  // forms (frames past a 64 KiB tile, copy-out by register windows, any other
+  // shape) leave it to the validation kernels, a second read of the frames.
+  const bool fused = path == DecodePath::kCopyTile || path == DecodePath::kVerifyTile;
+  a.valid = fused ? d_valid_or_null : nullptr;
   rc = launch_decode(a, layout, path, (hipStream_t)hip_stream);
   if (rc) return hip_fail((hipError_t)rc, "decode launch");
+  if (d_valid_or_null && !fused) {
+    Utf8Args u{};
+    u.frames = d_frames;
+    u.n = n;
+    u.F = frame_len;
+    u.H = (uint32_t)layout;
+    u.valid = d_valid_or_null;
+    u.xcd = tuning().tile_xcd ? 1u : 0u;
+    rc = launch_validate_utf8(u, (hipStream_t)hip_stream);
+    if (rc) return hip_fail((hipError_t)rc, "utf8 validation launch");
+  }
   return 0;
 }
 
@@ -552,6 +581,7 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
   int rc = dev_scope.set(device);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)hip_stream;
+  ScratchCall call(s);  // the scan's sums and the tile records, until the last launch
   VarlenArgs a{};
   a.payload = in->payload;
   a.len = in->len;
@@ -701,6 +731,15 @@ int rudp_decode_varlen_checked(const uint8_t* d_frames, uint64_t frames_bytes, c
                                uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags, uint8_t* d_ok,
                                uint16_t* d_csum_out_or_null, uint32_t* d_status, int layout, int device,
                                void* hip_stream) {
+  return rudp_decode_varlen_utf8(d_frames, frames_bytes, d_frame_off, len_hint, n, d_csum_in_or_null, d_seq, d_ack,
+                                 d_flags, d_ok, d_csum_out_or_null, nullptr, d_status, layout, device, hip_stream);
+}
+
+int rudp_decode_varlen_utf8(const uint8_t* d_frames, uint64_t frames_bytes, const uint64_t* d_frame_off,
+                            uint32_t len_hint, uint64_t n, const uint16_t* d_csum_in_or_null,
+                            uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags, uint8_t* d_ok,
+                            uint16_t* d_csum_out_or_null, uint8_t* d_valid_or_null, uint32_t* d_status,
+                            int layout, int device, void* hip_stream) {
   if (!d_frame_off) return fail(RUDP_EINVAL, "rudp_decode_varlen_checked: frame_off is NULL");
   if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
     return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
@@ -716,7 +755,8 @@ int rudp_decode_varlen_checked(const uint8_t* d_frames, uint64_t frames_bytes, c
   }
   if (n == 0) return 0;
   return decode_varlen(d_frames, d_frame_off, len_hint, n, d_csum_in_or_null, d_seq, d_ack, d_flags, d_ok,
-                       d_csum_out_or_null, nullptr, layout, device, hip_stream, true, d_status, frames_bytes);
+                       d_csum_out_or_null, nullptr, layout, device, hip_stream, true, d_status, frames_bytes,
+                       d_valid_or_null);
 }
 
 int rudp_frame_off_check(const uint64_t* d_frame_off, uint64_t n, uint64_t frames_bytes, uint32_t* d_status,
@@ -725,6 +765,7 @@ int rudp_frame_off_check(const uint64_t* d_frame_off, uint64_t n, uint64_t frame
   DeviceScope dev_scope;
   int rc = dev_scope.set(device);
   if (rc) return rc;
+  ScratchCall call((hipStream_t)hip_stream);  // the check's partials
   rc = check_frame_offsets(d_frame_off, n, frames_bytes, d_status, (hipStream_t)hip_stream);
   if (rc) return hip_fail((hipError_t)rc, "frame offset check");
   return 0;
@@ -802,6 +843,7 @@ static int dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_
   int rc = dev_scope.set(device);
   if (rc) return rc;
   hipStream_t s = (hipStream_t)hip_stream;
+  ScratchCall call(s);  // the hash scratch, until the table pass is enqueued
   DedupArgs a{};
   a.frames = d_frames;
   a.frame_off = d_frame_off_or_null;
@@ -814,9 +856,13 @@ static int dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_
   a.glog = frame_len <= 16u ? 0u : frame_len <= 64u ? 1u : frame_len <= 256u ? 2u : 3u;
   a.lim_checked = checked ? 1u : 0u;
   a.frames_lim = frames_bytes;
-  void* scratch = nullptr;
-  RUDP_HIP(stream_scratch(&scratch, n * sizeof(uint64_t), s, kScratchHash));
-  a.hash = (uint64_t*)scratch;
+  // packed frames of the reference's sizes: one launch, nothing in HBM but the flags
+  if (d_frame_off_or_null && aligned16(d_frames)) a.small_cap = dedup_small_cap(frame_len, window);
+  if (!a.small_cap) {
+    void* scratch = nullptr;
+    RUDP_HIP(stream_scratch(&scratch, n * sizeof(uint64_t), s, kScratchHash));
+    a.hash = (uint64_t*)scratch;
+  }
   rc = launch_dedup(a, s);
   if (rc) return hip_fail((hipError_t)rc, "dedup launch");
   return 0;

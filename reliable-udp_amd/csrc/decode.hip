@@ -17,6 +17,7 @@
 // decode_vec_kernel (register windows); any other shape the byte kernel.
 #include "codec_device.hpp"
 #include "internal.hpp"
+#include "utf8_device.hpp"
 
 namespace rudp {
 
@@ -187,7 +188,11 @@ __global__ void __launch_bounds__(kBlock) decode_verify_kernel(DecodeArgs a) {
 // v_alignbyte) and sum the LE u16 halves; the group leader parses the header
 // out of LDS.  Copy-out streams the same windows to payload_out as one
 // contiguous run per tile.
-template <int H, bool COPY>
+// U8: each payload's strict UTF-8 check in the same pass (a.valid; the
+// reference decodes every payload, utils/reliableUDP.py:121 ->
+// utils/packet.py:73): the windows' high bits are OR'ed as they are summed,
+// and only a frame with a high bit runs the byte checks over its LDS chunks.
+template <int H, bool COPY, bool U8>
 __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const uint32_t tid = threadIdx.x;
@@ -232,13 +237,18 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
   }
   __syncthreads();
   const uint32_t* dw = reinterpret_cast<const uint32_t*>(lds);
-  uint32_t sum = 0;
+  uint32_t sum = 0, hib = 0;
   const uint64_t p = p0 + q;
   const uint32_t V = L >> 4;
   if (q < Tv) {
     const uint32_t pay = q * F + H;  // LDS byte offset of the payload
-    for (uint32_t v = g; v < V; v += G) sum += le16_sum(window16_dw(dw, pay + 16u * v));
+    for (uint32_t v = g; v < V; v += G) {
+      const u32x4 w = window16_dw(dw, pay + 16u * v);
+      sum += le16_sum(w);
+      if (U8) hib |= w.x | w.y | w.z | w.w;
+    }
   }
+
   if (COPY) {
     // The tile's payload_out range is contiguous (Tv*L bytes, 16-B aligned):
     // store it as one stream, lane t taking vectors t, t+256, ... so every
@@ -268,7 +278,17 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
       }
     }
   }
-  for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
+  for (uint32_t m = G >> 1; m > 0; m >>= 1) {
+    sum += __shfl_xor(sum, (int)m, 64);
+    if (U8) hib |= (uint32_t)__shfl_xor((int)hib, (int)m, 64);
+  }
+  uint32_t u8bad = 0;
+  if (U8 && __any((hib & 0x80808080u) != 0)) {  // the byte checks, for frames with a high bit
+    if ((hib & 0x80808080u) && q < Tv)
+      u8bad = utf8_check_frame(q * F + H, q * F + F, g, G, [&](uint64_t c) { return tile[c]; },
+                               [&](uint64_t x) { return x ? dw[(x >> 2) - 1u] : 0u; });
+    u8bad = group_or(u8bad, G);
+  }
   if (!a.stage_out) {
     if (g == 0 && q < Tv) {
       const u32x4 h = window16_dw(dw, q * F);
@@ -277,6 +297,7 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
       const uint32_t flags = h.y & 0xFFu;
       const uint32_t inband = (((h.y >> 8) & 0xFFu) << 8) | ((h.y >> 16) & 0xFFu);
       finish_packet<H, true>(a, p, sum, seq, ack, flags, H == 5 ? want_cs : inband);
+      if (U8) a.valid[p] = u8bad ? 0 : 1;
     }
     return;
   }
@@ -289,6 +310,7 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
   uint16_t* s_cs = s_ack + T;
   uint8_t* s_flags = reinterpret_cast<uint8_t*>(s_cs + T);
   uint8_t* s_ok = s_flags + T;
+  uint8_t* s_valid = s_ok + T;  // U8
   if (g == 0 && q < Tv) {
     const u32x4 h = window16_dw(dw, q * F);
     const uint32_t seq = ((h.x & 0xFFu) << 8) | ((h.x >> 8) & 0xFFu);
@@ -305,6 +327,7 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
     s_cs[q] = (uint16_t)c;
     s_flags[q] = (uint8_t)flags;
     s_ok[q] = ok;
+    if (U8) s_valid[q] = u8bad ? 0 : 1;
   }
   __syncthreads();
   if (Tv == T) {  // T % 16 == 0 and p0 % 16 == 0: every array slice is dword aligned
@@ -314,6 +337,7 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
     const uint32_t* l_cs = reinterpret_cast<const uint32_t*>(s_cs);
     const uint32_t* l_fl = reinterpret_cast<const uint32_t*>(s_flags);
     const uint32_t* l_ok = reinterpret_cast<const uint32_t*>(s_ok);
+    const uint32_t* l_valid = reinterpret_cast<const uint32_t*>(s_valid);
     for (uint32_t i = tid; i < w16; i += kBlock) {
       reinterpret_cast<uint32_t*>(a.seq + p0)[i] = l_seq[i];
       reinterpret_cast<uint32_t*>(a.ack + p0)[i] = l_ack[i];
@@ -322,6 +346,7 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
     for (uint32_t i = tid; i < w8; i += kBlock) {
       reinterpret_cast<uint32_t*>(a.flags + p0)[i] = l_fl[i];
       reinterpret_cast<uint32_t*>(a.ok + p0)[i] = l_ok[i];
+      if (U8) reinterpret_cast<uint32_t*>(a.valid + p0)[i] = l_valid[i];
     }
   } else {
     for (uint32_t i = tid; i < Tv; i += kBlock) {
@@ -330,6 +355,7 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
       if (a.csum_out) a.csum_out[p0 + i] = s_cs[i];
       a.flags[p0 + i] = s_flags[i];
       a.ok[p0 + i] = s_ok[i];
+      if (U8) a.valid[p0 + i] = s_valid[i];
     }
   }
 }
@@ -376,6 +402,23 @@ __global__ void __launch_bounds__(kBlock) decode_bytes_kernel(DecodeArgs a) {
   }
 }
 
+template <int H, bool COPY, bool U8>
+static int launch_decode_tile(const DecodeArgs& args, size_t lds, uint64_t blocks, hipStream_t stream) {
+  if (lds > 65536) {
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_tile_kernel<H, COPY, U8>),
+                                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  hipLaunchKernelGGL((decode_tile_kernel<H, COPY, U8>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
+  return (int)hipGetLastError();
+}
+
+template <int H, bool COPY>
+static int launch_decode_tile_u8(const DecodeArgs& args, size_t lds, uint64_t blocks, hipStream_t stream) {
+  return args.valid ? launch_decode_tile<H, COPY, true>(args, lds, blocks, stream)
+                    : launch_decode_tile<H, COPY, false>(args, lds, blocks, stream);
+}
+
 int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream_t stream) {
   if (args.n == 0) return 0;
   if (path != DecodePath::kBytes) {
@@ -383,7 +426,7 @@ int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream
     const uint64_t blocks = (args.n + per_block - 1) / per_block;
     if (path == DecodePath::kCopyTile || path == DecodePath::kVerifyTile) {
       size_t lds = ((size_t)per_block * args.F + 32 + 15) & ~size_t(15);
-      if (args.stage_out) lds += 8u * per_block;  // staged outputs
+      if (args.stage_out) lds += (args.valid ? 9u : 8u) * per_block;  // staged outputs
       // Resident tiles per CU: verify-only wants every tile it can get; the
       // copy-out (read + write, like encode) runs best at 5 for tiles over
       // 14 KiB (1M x 1024 B 0.348 -> 0.340 ms, x 1472 B 0.518 -> 0.515; verify
@@ -394,24 +437,13 @@ int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream
         const size_t want = ((size_t)(160 * 1024) / (size_t)per_cu) & ~size_t(15);
         if (want > lds) lds = want;
       }
-      if (lds > 65536) {
-        const void* fn = path == DecodePath::kCopyTile
-            ? (layout == 7 ? reinterpret_cast<const void*>(&decode_tile_kernel<7, true>)
-                           : reinterpret_cast<const void*>(&decode_tile_kernel<5, true>))
-            : (layout == 7 ? reinterpret_cast<const void*>(&decode_tile_kernel<7, false>)
-                           : reinterpret_cast<const void*>(&decode_tile_kernel<5, false>));
-        const hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-        if (e != hipSuccess) return (int)e;
-      }
-      const dim3 grid((uint32_t)blocks), block(kBlock);
-      if (path == DecodePath::kCopyTile) {
-        if (layout == 7) hipLaunchKernelGGL((decode_tile_kernel<7, true>), grid, block, lds, stream, args);
-        else hipLaunchKernelGGL((decode_tile_kernel<5, true>), grid, block, lds, stream, args);
-      } else {
-        if (layout == 7) hipLaunchKernelGGL((decode_tile_kernel<7, false>), grid, block, lds, stream, args);
-        else hipLaunchKernelGGL((decode_tile_kernel<5, false>), grid, block, lds, stream, args);
-      }
-    } else if (path == DecodePath::kVerify) {
+      if (path == DecodePath::kCopyTile)
+        return layout == 7 ? launch_decode_tile_u8<7, true>(args, lds, blocks, stream)
+                           : launch_decode_tile_u8<5, true>(args, lds, blocks, stream);
+      return layout == 7 ? launch_decode_tile_u8<7, false>(args, lds, blocks, stream)
+                         : launch_decode_tile_u8<5, false>(args, lds, blocks, stream);
+    }
+    if (path == DecodePath::kVerify) {
       if (layout == 7)
         hipLaunchKernelGGL(decode_verify_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
       else

@@ -21,6 +21,17 @@
 //           answer).  Expected O(1) per frame instead of `window` compares.
 //           The scan form (every frame compares its whole window) stays
 //           behind rudpx_tune key 32 = 0.
+//
+// Small frames (the reference's 6-9 B datagrams; mean length up to
+// kDedupSmallLen, window up to kDedupSmallWin) take one launch instead:
+// dedup_small_kernel.  A workgroup owns T = 256 * FPT consecutive frames and
+// stages their offsets and bytes, and those of the `window` frames before
+// them, in LDS (one contiguous run, coalesced; the halo is its neighbour
+// workgroup's run, an L2 hit under the XCD-contiguous tile order), hashes all
+// of them from LDS (32-bit, an invalid frame hashes to 0), chains them into
+// an LDS table and confirms every hit from LDS.  No hash scratch in HBM and
+// each offset read once: the round-3 two-pass chain moved 3.8x the algorithmic
+// bytes (8-B hashes written, then re-read per workgroup with their halo).
 #include "codec_device.hpp"
 #include "internal.hpp"
 
@@ -161,8 +172,191 @@ __global__ void __launch_bounds__(kBlock) dedup_table_kernel(DedupArgs a, uint32
   a.dup[i] = frame_span(a, i, &o, &l) ? dup : (uint8_t)RUDP_DUP_BAD_OFFSETS;
 }
 
+// ---- small frames: one launch -------------------------------------------------
+constexpr uint32_t kDedupSmallWin = 1024;  // most window the one-launch form stages
+constexpr uint32_t kDedupSmallLen = 16;    // mean frame length (bytes) it is used up to
+
+// 32-bit hash of a frame's canonical bytes (FNV-1a, then the murmur3 finalizer
+// with the length): equal frames hash equal; 0 is kept for invalid frames.
+template <class ByteF>
+__device__ __forceinline__ uint32_t small_hash(uint32_t len, ByteF byte) {
+  const uint32_t cl = len ? len : 5u;
+  uint32_t h = 0x811C9DC5u;
+  for (uint32_t k = 0; k < cl; ++k) h = (h ^ (len ? byte(k) : 0u)) * 0x01000193u;
+  h ^= cl * 0x9E3779B1u;
+  h ^= h >> 16;
+  h *= 0x85EBCA6Bu;
+  h ^= h >> 13;
+  h *= 0xC2B2AE35u;
+  h ^= h >> 16;
+  return h ? h : 1u;
+}
+
+// The tile's work once its entries' spans are known: `span(e, &off, &len)`
+// gives entry e's bytes (false: offsets rejected, equal to nothing) and
+// `byte(off, k)` one of them; entries [0, C) are frames lo .. lo + C - 1, the
+// tile's own frames entries [own0, C).
+template <class SpanF, class ByteF>
+__device__ __forceinline__ void dedup_tile(const DedupArgs& a, uint64_t lo, uint32_t C, uint32_t own0,
+                                           uint32_t* lh, int16_t* nxt, int* head, uint32_t nb, SpanF span,
+                                           ByteF byte) {
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t b = tid; b < nb; b += kBlock) head[b] = -1;
+  for (uint32_t e = tid; e < C; e += kBlock) {
+    uint64_t off;
+    uint32_t len;
+    lh[e] = span(e, &off, &len) ? small_hash(len, [&](uint32_t k) { return byte(off, k); }) : 0u;
+  }
+  __syncthreads();
+  for (uint32_t e = tid; e < C; e += kBlock)
+    if (lh[e]) nxt[e] = (int16_t)atomicExch(&head[lh[e] & (nb - 1u)], (int)e);
+  __syncthreads();
+  for (uint32_t e = own0 + tid; e < C; e += kBlock) {  // lane-strided: coalesced flags
+    const uint64_t i = lo + e;
+    const uint32_t h = lh[e];
+    uint8_t dup = RUDP_DUP_BAD_OFFSETS;
+    if (h) {
+      dup = 0;
+      const uint32_t emin = (uint32_t)((i > a.window ? i - a.window : 0) - lo);
+      uint64_t oi;
+      uint32_t li;
+      span(e, &oi, &li);
+      const uint32_t ci = li ? li : 5u;
+      for (int c = head[h & (nb - 1u)]; c >= 0 && !dup; c = nxt[c]) {
+        const uint32_t u = (uint32_t)c;
+        if (u < emin || u >= e || lh[u] != h) continue;
+        uint64_t ou;
+        uint32_t lu;
+        span(u, &ou, &lu);
+        if ((lu ? lu : 5u) != ci) continue;
+        uint32_t diff = 0;
+        for (uint32_t k = 0; k < ci && !diff; ++k)
+          diff = (li ? byte(oi, k) : 0u) ^ (lu ? byte(ou, k) : 0u);
+        dup = diff ? 0 : 1;
+      }
+    }
+    a.dup[i] = dup;
+  }
+}
+
+// LDS of the one-launch form: offsets u32 [cmax + 1] | hashes u32 [cmax] |
+// chain links i16 [cmax] | bucket heads i32 [nb] | the run [cap].
+__host__ __device__ inline uint32_t dedup_small_lds(uint32_t cmax, uint32_t nb, uint32_t cap) {
+  return 4u * ((cmax + 1u + 3u) & ~3u) + 4u * cmax + 2u * ((cmax + 1u) & ~1u) + 4u * nb + cap;
+}
+
+// Offsets and run vectors a thread stages (loads all issued before any is used).
+constexpr uint32_t kDedupOffPer = 9;    // (T + kDedupSmallWin + 1) / kBlock, FPT = 4
+constexpr uint32_t kDedupVecPer = 11;   // the largest budget / 16 / kBlock
+
+template <uint32_t FPT>
+__global__ void __launch_bounds__(kBlock) dedup_small_kernel(DedupArgs a, uint32_t nb, uint32_t cap) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds_raw[];
+  constexpr uint32_t T = kBlock * FPT;
+  static_assert(T + kDedupSmallWin + 1 <= kDedupOffPer * kBlock, "offsets per thread");
+  const uint32_t W = a.window;
+  const uint32_t tid = threadIdx.x;
+  const uint64_t p0 = (uint64_t)xcd_tile(blockIdx.x, gridDim.x) * T;
+  const uint64_t p1 = p0 + T < a.n ? p0 + T : a.n;
+  const uint64_t lo = p0 > W ? p0 - W : 0;
+  const uint32_t C = (uint32_t)(p1 - lo), own0 = (uint32_t)(p0 - lo);
+  const uint32_t cmax = T + W;
+  uint32_t* s_off = reinterpret_cast<uint32_t*>(lds_raw);                 // [cmax + 1]
+  uint32_t* lh = s_off + ((cmax + 1u + 3u) & ~3u);                        // [cmax]
+  int16_t* nxt = reinterpret_cast<int16_t*>(lh + cmax);                  // [cmax]
+  int* head = reinterpret_cast<int*>(nxt + ((cmax + 1u) & ~1u));         // [nb]
+  unsigned char* img = reinterpret_cast<unsigned char*>(head + nb);      // the run [cap]
+  // first round trip: the tile's offsets, and its outer two (every lane) for the run
+  uint64_t o[kDedupOffPer];
+#pragma unroll
+  for (uint32_t j = 0; j < kDedupOffPer; ++j) {
+    const uint32_t e = j * kBlock + tid;
+    o[j] = e <= C ? a.frame_off[lo + e] : 0;
+  }
+  const uint64_t lim = a.lim_checked ? a.frames_lim : a.frame_off[a.n];
+  const uint64_t f_lo = a.frame_off[lo], f_hi = a.frame_off[p1];
+  const uint64_t A = f_lo & ~15ull;
+  const uint64_t run = ((f_hi + 15u) & ~15ull) - A;
+  // The tile's run is staged when its outer offsets are in order, inside the
+  // buffer and within budget, and every inner offset falls inside it (else a
+  // frame could be valid yet reach outside the run): otherwise the same work
+  // straight from HBM.
+  bool staged = f_lo <= f_hi && f_hi <= lim && run <= cap;
+  uint32_t outside = 0;
+  if (staged) {
+    // second round trip: the run, every vector load issued before the offsets are stored
+    const uint32_t nvec = (uint32_t)(run >> 4);
+    const uint64_t whole = lim > A ? (lim - A) >> 4 : 0;
+    u32x4 r[kDedupVecPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kDedupVecPer; ++j) {
+      const uint32_t v = j * kBlock + tid;
+      if (v < nvec)
+        r[j] = v < whole ? __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(a.frames + A) + v)
+                         : load16_guarded(a.frames, A + 16ull * v, lim);
+    }
+#pragma unroll
+    for (uint32_t j = 0; j < kDedupOffPer; ++j) {
+      const uint32_t e = j * kBlock + tid;
+      if (e <= C) {
+        const bool in = o[j] >= f_lo && o[j] <= f_hi;
+        outside |= in ? 0u : 1u;
+        s_off[e] = in ? (uint32_t)(o[j] - A) : 0u;
+      }
+    }
+    u32x4* dst = reinterpret_cast<u32x4*>(img);
+#pragma unroll
+    for (uint32_t j = 0; j < kDedupVecPer; ++j) {
+      const uint32_t v = j * kBlock + tid;
+      if (v < nvec) dst[v] = r[j];
+    }
+  }
+  staged = !__syncthreads_or((int)(!staged || outside));
+  if (staged) {
+    const uint32_t rlim = (uint32_t)(f_hi - A);
+    dedup_tile(
+        a, lo, C, own0, lh, nxt, head, nb,
+        [&](uint32_t e, uint64_t* off, uint32_t* len) {
+          const uint32_t fs = s_off[e], fe = s_off[e + 1];
+          *off = fs;
+          *len = fe - fs;
+          return fs <= fe && fe <= rlim;  // (inner offsets in order: the checked rule)
+        },
+        [&](uint64_t off, uint32_t k) { return (uint32_t)img[off + k]; });
+  } else {
+    dedup_tile(
+        a, lo, C, own0, lh, nxt, head, nb,
+        [&](uint32_t e, uint64_t* off, uint32_t* len) {
+          // (an unchecked caller's offsets are valid by contract; checking them
+          // anyway keeps a bad one from reading past the buffer)
+          const uint64_t fo = a.frame_off[lo + e], fe = a.frame_off[lo + e + 1];
+          const bool ok = fo <= fe && fe <= lim;
+          *off = ok ? fo : 0;
+          *len = ok ? (uint32_t)(fe - fo) : 0u;
+          return ok;
+        },
+        [&](uint64_t off, uint32_t k) { return (uint32_t)a.frames[off + k]; });
+  }
+}
+
 int launch_dedup(const DedupArgs& args, hipStream_t stream) {
   if (args.n == 0) return 0;
+  if (args.small_cap) {
+    constexpr uint32_t FPT = 4, T = kBlock * FPT;
+    const uint32_t cmax = T + args.window;
+    uint32_t nb = 256;  // buckets: chains of 1-2 entries
+    while (2u * nb < cmax) nb <<= 1;
+    const size_t lds = dedup_small_lds(cmax, nb, args.small_cap);
+    if (lds > 65536) {
+      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dedup_small_kernel<FPT>),
+                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (e != hipSuccess) return (int)e;
+    }
+    const uint64_t blocks = (args.n + T - 1) / T;
+    hipLaunchKernelGGL((dedup_small_kernel<FPT>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args, nb,
+                       args.small_cap);
+    return (int)hipGetLastError();
+  }
   const uint64_t hblocks = ((args.n << args.glog) + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(dedup_hash_kernel, dim3((uint32_t)hblocks), dim3(kBlock), 0, stream, args);
   const uint64_t wblocks = (args.n + kBlock - 1) / kBlock;
@@ -185,5 +379,15 @@ int launch_dedup(const DedupArgs& args, hipStream_t stream) {
 }
 
 uint32_t dedup_max_window() { return kMaxWindow; }
+
+uint32_t dedup_small_cap(uint32_t mean_len, uint32_t window) {
+  if (!tuning().dedup_small || !tuning().dedup_table || window > kDedupSmallWin || mean_len > kDedupSmallLen)
+    return 0;
+  // the tile's and its window's frames at 1.25x the mean length (a burst past it
+  // takes the same work from HBM inside the launch)
+  const uint64_t C = (uint64_t)kBlock * 4u + window;
+  const uint64_t cap = (C * (mean_len ? mean_len : 1u) * 5u / 4u + 256u + 15u) & ~15ull;
+  return cap <= 16ull * kDedupVecPer * kBlock ? (uint32_t)cap : 0u;
+}
 
 }  // namespace rudp

@@ -53,49 +53,156 @@ hipError_t stream_alloc(void** ptr, size_t bytes, hipStream_t stream) {
 
 hipError_t stream_free(void* ptr, hipStream_t stream) { return hipFreeAsync(ptr, stream); }
 
-// Per-call temporaries without an allocation per call: every host thread
-// keeps one buffer per (device, stream, slot), grown when a call needs more
-// (the old one freed in stream order).  Only this thread enqueues work on
-// its buffers, and only on that stream, so the stream's order protects them:
-// a call's kernels run after the previous call's on the same stream.  (A
-// destroyed stream's handle is released only after its pending work, so a
-// new stream with the same handle finds its buffers idle.)  hipFreeAsync
-// cost 3.9 us of host time per call (rocprofv3 --hip-trace, 1M one-character
-// datagrams), as long as a kernel launch.
+// Per-call temporaries without an allocation per call: one scratch set per
+// (device, stream), shared by every host thread, with one buffer per slot
+// grown when a call needs more (the old one freed in stream order).  A call
+// holds its set's mutex (ScratchCall) from its first scratch request until
+// its last kernel is enqueued, so the kernels of calls on one stream never
+// interleave on it and the stream's order protects the buffers: a call's
+// kernels run after the previous call's.  Nothing is owned by a host thread,
+// so threads that come and go (a thread per request, a worker pool that
+// recycles its workers: proxy.py:127, :154) leave nothing behind.  (A
+// destroyed stream's handle is released only after its pending work, so a new
+// stream with the same handle finds the set idle.)  At most kMaxSets sets per
+// device: a call on a new stream past that takes the least recently used set
+// after a device synchronize (its buffers then idle), so a caller that makes
+// a stream per call keeps a bounded footprint.  A buffer grown past kKeepBytes
+// is given back when its call ends.  While the stream is being captured into
+// a graph the call's temporaries are allocated and freed inside the capture
+// (stream_alloc / stream_free), never cached.  hipFreeAsync cost 3.9 us of
+// host time per call (rocprofv3 --hip-trace, 1M one-character datagrams), as
+// long as a kernel launch, which is why a call does not allocate.
 namespace {
-struct Scratch {
-  int device;
-  hipStream_t stream;
-  int slot;
-  void* ptr;
-  size_t cap;
+constexpr int kSlots = 4;
+constexpr size_t kMaxSets = 64;
+constexpr size_t kKeepBytes = size_t(64) << 20;
+
+struct ScratchSet {
+  std::mutex mu;  // held by the ScratchCall that enqueues work on these buffers
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint64_t last_use = 0;
+  void* ptr[kSlots] = {};
+  size_t cap[kSlots] = {};
 };
-thread_local std::vector<Scratch> t_scratch;
+
+struct DeviceSets {
+  std::mutex mu;
+  std::vector<ScratchSet*> sets;  // never deleted: a set is re-keyed, not freed
+  uint64_t clock = 0;
+};
+
+std::mutex g_sets_mu;
+std::vector<DeviceSets*> g_sets;
+
+DeviceSets* device_sets(int device) {
+  std::lock_guard<std::mutex> lk(g_sets_mu);
+  if ((int)g_sets.size() <= device) g_sets.resize(device + 1, nullptr);
+  if (!g_sets[device]) g_sets[device] = new DeviceSets();  // lives for the process
+  return g_sets[device];
+}
+
+thread_local ScratchCall* t_call = nullptr;  // the call this thread is making, if any
 }  // namespace
 
+// The set of (device, stream), locked for the caller: found, made (up to
+// kMaxSets), or the least recently used one re-keyed once it is idle.
+static ScratchSet* lock_set(int device, hipStream_t stream) {
+  DeviceSets* ds = device_sets(device);
+  for (;;) {
+    ScratchSet* set = nullptr;
+    {
+      std::lock_guard<std::mutex> lk(ds->mu);
+      for (ScratchSet* s : ds->sets)
+        if (s->stream == stream) set = s;
+      if (!set && ds->sets.size() < kMaxSets) {
+        set = new ScratchSet();
+        set->device = device;
+        set->stream = stream;
+        ds->sets.push_back(set);
+      }
+      if (!set) {  // past kMaxSets streams: the least recently used set, once idle
+        set = ds->sets[0];
+        for (ScratchSet* s : ds->sets)
+          if (s->last_use < set->last_use) set = s;
+        std::lock_guard<std::mutex> sl(set->mu);  // no call is enqueueing on it
+        (void)hipDeviceSynchronize();             // and nothing it enqueued is still running
+        set->stream = stream;
+      }
+      set->last_use = ++ds->clock;
+    }
+    set->mu.lock();
+    if (set->stream == stream) return set;
+    set->mu.unlock();  // re-keyed by an eviction between the lookup and the lock: look again
+  }
+}
+
+ScratchCall::ScratchCall(hipStream_t stream) : stream_(stream) {
+  if (t_call) return;  // nested in a call already holding its set (same thread)
+  if (hipGetDevice(&device_) != hipSuccess) return;
+  hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+  capture_ = stream && hipStreamIsCapturing(stream, &st) == hipSuccess && st != hipStreamCaptureStatusNone;
+  t_call = this;
+  outer_ = true;
+  if (!capture_) set_ = lock_set(device_, stream);
+}
+
+ScratchCall::~ScratchCall() {
+  if (!outer_) return;
+  t_call = nullptr;
+  for (int i = 0; i < nfree_; ++i) (void)stream_free(free_[i], stream_);  // capture: inside the graph
+  if (!set_) return;
+  ScratchSet* set = static_cast<ScratchSet*>(set_);
+  for (int k = 0; k < kSlots; ++k) {
+    if (set->cap[k] > kKeepBytes) {  // a one-off giant call does not pin its scratch
+      (void)stream_free(set->ptr[k], stream_);
+      set->ptr[k] = nullptr;
+      set->cap[k] = 0;
+    }
+  }
+  set->mu.unlock();
+}
+
 hipError_t stream_scratch(void** ptr, size_t bytes, hipStream_t stream, int slot) {
-  int device = 0;
-  hipError_t e = hipGetDevice(&device);
-  if (e != hipSuccess) return e;
-  Scratch* hit = nullptr;
-  for (auto& sc : t_scratch)
-    if (sc.device == device && sc.stream == stream && sc.slot == slot) hit = &sc;
-  if (hit && hit->cap >= bytes) {
-    *ptr = hit->ptr;
+  ScratchCall* call = t_call;
+  if (!call || call->stream_ != stream || slot < 0 || slot >= kSlots) return hipErrorInvalidValue;
+  const size_t cap = ((bytes ? bytes : 1) + 65535u) & ~size_t(65535);
+  if (call->capture_ || !call->set_) {
+    if (call->nfree_ >= ScratchCall::kMaxFree) return hipErrorInvalidValue;
+    hipError_t e = stream_alloc(ptr, cap, stream);
+    if (e == hipSuccess) call->free_[call->nfree_++] = *ptr;
+    return e;
+  }
+  ScratchSet* set = static_cast<ScratchSet*>(call->set_);
+  if (set->cap[slot] >= bytes && set->ptr[slot]) {
+    *ptr = set->ptr[slot];
     return hipSuccess;
   }
-  const size_t cap = ((bytes ? bytes : 1) + 65535u) & ~size_t(65535);
   void* p = nullptr;
-  if ((e = stream_alloc(&p, cap, stream)) != hipSuccess) return e;
-  if (hit) {
-    (void)stream_free(hit->ptr, stream);  // after the calls already enqueued on this stream
-    hit->ptr = p;
-    hit->cap = cap;
-  } else {
-    t_scratch.push_back(Scratch{device, stream, slot, p, cap});
-  }
+  hipError_t e = stream_alloc(&p, cap, stream);
+  if (e != hipSuccess) return e;
+  if (set->ptr[slot]) (void)stream_free(set->ptr[slot], stream);  // after the calls already enqueued
+  set->ptr[slot] = p;
+  set->cap[slot] = cap;
   *ptr = p;
   return hipSuccess;
+}
+
+size_t scratch_sets(int device) {
+  DeviceSets* ds = device_sets(device);
+  std::lock_guard<std::mutex> lk(ds->mu);
+  return ds->sets.size();
+}
+
+hipError_t pool_used_bytes(int device, uint64_t* used) {
+  *used = 0;
+  hipMemPool_t pool = nullptr;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    if ((int)g_pools.size() > device) pool = g_pools[device];
+  }
+  if (!pool) return hipSuccess;
+  return hipMemPoolGetAttribute(pool, hipMemPoolAttrUsedMemCurrent, used);
 }
 
 }  // namespace rudp

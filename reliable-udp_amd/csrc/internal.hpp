@@ -59,6 +59,7 @@ struct DecodeArgs {
   uint8_t* ok;
   uint16_t* csum_out;       // may be null
   unsigned char* payload_out;  // may be null
+  uint8_t* valid;           // tile kernels: strict UTF-8 of each payload in the same pass, or null
   uint64_t n;
   uint32_t F;               // frame bytes
   uint32_t glog;            // log2(lanes per packet)
@@ -103,6 +104,7 @@ struct VarlenArgs {
   uint8_t* flags;
   uint8_t* ok;
   uint16_t* csum_out;
+  uint8_t* valid;                 // decode: strict UTF-8 of each payload in the same pass, or null
   uint64_t n;
   uint32_t glog;                  // log2 lanes per packet (vector kernels); kNoVec = byte kernels
   // encode tile kernel (packed payload): packets per tile (power of two, 4..256),
@@ -171,8 +173,9 @@ struct DedupArgs {
   uint32_t glog;              // hash pass: log2 lanes per frame (from the mean frame length)
   uint32_t lim_checked;       // frames reach at most frames_lim bytes: a frame whose offsets are
   uint64_t frames_lim;        // decreasing or past it gets dup = RUDP_DUP_BAD_OFFSETS, nothing read
-  uint64_t* hash;             // scratch [n]
+  uint64_t* hash;             // scratch [n] (two-pass form)
   uint8_t* dup;
+  uint32_t small_cap;         // > 0: the one-launch small-frame form, LDS run budget in bytes
 };
 
 constexpr uint32_t kTileMaxPayload = 4096;
@@ -276,6 +279,7 @@ struct Tuning {
   RUDP_KNOB(varlen_encode_cap_pct, 110)
   RUDP_KNOB(varlen_decode_tile, 1)  // varlen decode through LDS tiles for hints >= 128 B (2: any hint; 0: never)
   RUDP_KNOB(dedup_table, 1)    // dedup window pass by LDS hash table (0: every frame scans its window)
+  RUDP_KNOB(dedup_small, 1)    // packed small frames: dedup in one launch (dedup_small_kernel; 0: two passes)
   RUDP_KNOB(utf8_tile, 1)
   // Packed-frame UTF-8 validation through LDS tiles (hints >= 128 B) and its
   // LDS budget in % of the hinted run: 1M x 1479 B ASCII frames 0.287 ->
@@ -358,13 +362,40 @@ int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream)
 int launch_validate_utf8(const Utf8Args& args, hipStream_t stream);
 int launch_dedup(const DedupArgs& args, hipStream_t stream);
 uint32_t dedup_max_window();
+// The one-launch dedup's LDS run budget for packed frames of this mean length
+// and window, or 0 when the two-pass form is used.
+uint32_t dedup_small_cap(uint32_t mean_len, uint32_t window);
 // Stream-ordered temporaries from a library-owned pool of the current device
 // that keeps its memory across synchronizes (device_pool.hip).
 hipError_t stream_alloc(void** ptr, size_t bytes, hipStream_t stream);
 hipError_t stream_free(void* ptr, hipStream_t stream);
-// A per-(host thread, device, stream, slot) temporary kept across calls (device_pool.hip).
+// A per-(device, stream, slot) temporary kept across calls (device_pool.hip),
+// valid while the ScratchCall that covers the call is alive: every entry
+// point that asks for scratch makes one on its stream before its first
+// request and keeps it until its last kernel is enqueued.
 enum ScratchSlot { kScratchSums = 0, kScratchRecords = 1, kScratchHash = 2, kScratchBounds = 3 };
+class ScratchCall {
+ public:
+  explicit ScratchCall(hipStream_t stream);
+  ~ScratchCall();
+  ScratchCall(const ScratchCall&) = delete;
+  ScratchCall& operator=(const ScratchCall&) = delete;
+
+ private:
+  friend hipError_t stream_scratch(void** ptr, size_t bytes, hipStream_t stream, int slot);
+  static constexpr int kMaxFree = 4;
+  hipStream_t stream_ = nullptr;
+  int device_ = 0;
+  bool outer_ = false;    // the outermost call on this thread (a nested one is a no-op)
+  bool capture_ = false;  // the stream is being captured: temporaries live inside the graph
+  void* set_ = nullptr;   // the (device, stream) scratch set this call holds
+  void* free_[kMaxFree] = {};
+  int nfree_ = 0;
+};
 hipError_t stream_scratch(void** ptr, size_t bytes, hipStream_t stream, int slot);
+// Diagnostics (tools build): scratch sets held for a device, bytes in use in its pool.
+size_t scratch_sets(int device);
+hipError_t pool_used_bytes(int device, uint64_t* used);
 
 struct Bounds {
   uint64_t min_len, max_len, sum_len;

@@ -274,7 +274,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // 49: XCD-contiguous tile order in the decode / varlen / UTF-8 tile kernels;
 // 50: small-frame encode finds its tile bases itself (no pass-2 launch);
 // 51: varlen byte tiles (0 never, 1 when the scan counts overflowing packet tiles, 2 always);
-// 52: varlen tile sum pass (2 from 128-B block sums, 0 chunk by chunk).
+// 52: varlen tile sum pass (2 from 128-B block sums, 0 chunk by chunk);
+// 62: packed small-frame dedup in one launch (dedup_small_kernel; 0: two passes).
 // (54: chunked / rotated XCD orders, measured within 2% and removed;
 // profiles/r02/headline/xcd_orders.json.)
 // (55, 56: a small-tile launch tail, and 57: persistent workgroups looping over the tiles,
@@ -318,7 +319,8 @@ int rudpx_tune(int key, int value) {
             : key == 51 ? &t.varlen_btile
             : key == 52 ? &t.varlen_tile_sums
             : key == 59 ? &t.varlen_span_bytes
-            : key == 61 ? &t.varlen_diag : nullptr;
+            : key == 61 ? &t.varlen_diag
+            : key == 62 ? &t.dedup_small : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }
@@ -343,6 +345,14 @@ int rudpx_copy(const void* src, void* dst, uint64_t n16, uint32_t blocks, void* 
   hipLaunchKernelGGL(rudp::copy_kernel, dim3(blocks), dim3(rudp::kBlock), 0, (hipStream_t)stream,
                      (const rudp::u32x4*)src, (rudp::u32x4*)dst, n16);
   return (int)hipGetLastError();
+}
+
+// The library's call-temporary footprint on `device`: out[0] = bytes in use in
+// its stream-ordered pool (hipMemPoolAttrUsedMemCurrent), out[1] = scratch
+// sets held (one per stream that made a call needing temporaries).
+int rudpx_scratch_stats(int device, uint64_t* out) {
+  out[1] = (uint64_t)rudp::scratch_sets(device);
+  return (int)rudp::pool_used_bytes(device, &out[0]);
 }
 
 }  // extern "C"

@@ -21,6 +21,7 @@
 #include "codec_device.hpp"
 #include "internal.hpp"
 #include "scan_device.hpp"
+#include "utf8_device.hpp"
 #if RUDP_TOOLS
 #include <hipcub/hipcub.hpp>
 #endif
@@ -678,10 +679,14 @@ __device__ __forceinline__ void decode_varlen_reject(const VarlenArgs& a, uint64
   a.flags[p] = 0;
   a.ok[p] = RUDP_OK_BAD_OFFSETS;
   if (a.csum_out) a.csum_out[p] = 0;
+  if (a.valid) a.valid[p] = 0;  // nothing of it was read, so nothing is vouched for
   if (a.status_out) atomicOr(a.status_out, RUDP_ST_OFFSETS);
 }
 
-template <int H>
+// U8: the payload's strict UTF-8 check in the same pass (a.valid).  Here the
+// lanes judge contiguous slices of the payload (utf8_slice), byte-granular as
+// the sum loop is.
+template <int H, bool U8>
 __global__ void __launch_bounds__(kBlock) decode_varlen_kernel(VarlenArgs a) {
   const uint32_t g = threadIdx.x & (kVarLanes - 1u);
   const uint64_t p = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / kVarLanes;
@@ -699,12 +704,18 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_kernel(VarlenArgs a) {
       sum += ((j - H) & 1u) ? (b << 8) : b;
     }
   }
+  uint32_t u8bad = 0;
+  if (U8) {
+    if (valid && F > (uint32_t)H) u8bad = utf8_slice(a.frames, fo + H, F - H, g, kVarLanes);
+    for (uint32_t m = kVarLanes >> 1; m > 0; m >>= 1) u8bad |= __shfl_xor(u8bad, (int)m, 64);
+  }
   for (uint32_t m = kVarLanes >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
   if (valid && g == 0) {
     if (bad) {
       decode_varlen_reject(a, p);
       return;
     }
+    if (U8) a.valid[p] = u8bad ? 0 : 1;
     uint32_t b[7] = {0, 0, 0, 0, 0, 0, 0};
 #pragma unroll
     for (uint32_t i = 0; i < 7; ++i)
@@ -732,11 +743,12 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_kernel(VarlenArgs a) {
   }
 }
 
-// The group leader's part of a varlen decode: `sum` is the whole frame's
-// big-endian word sum, `h` its first 16 bytes (little-endian packed).
+// The group leader's part of a varlen decode: `payload_sum` is the frame's
+// big-endian word sum over its payload bytes only (the callers mask the
+// header out as they sum), `h` its first 16 bytes (little-endian packed).
 template <int H>
 __device__ __forceinline__ void decode_varlen_finish(const VarlenArgs& a, uint64_t p, uint32_t F,
-                                                     uint32_t sum, u32x4 h) {
+                                                     uint32_t payload_sum, u32x4 h) {
   const uint32_t b0 = h.x & 0xFFu, b1 = (h.x >> 8) & 0xFFu, b2 = (h.x >> 16) & 0xFFu,
                  b3 = h.x >> 24, b4 = h.y & 0xFFu, b5 = (h.y >> 8) & 0xFFu,
                  b6 = (h.y >> 16) & 0xFFu;
@@ -752,9 +764,6 @@ __device__ __forceinline__ void decode_varlen_finish(const VarlenArgs& a, uint64
   }
   const uint32_t seq = (b0 << 8) | b1, ack = (b2 << 8) | b3, flags = b4;
   const uint32_t inband = (b5 << 8) | b6;
-  // the whole-frame sum holds seq, ack, flags<<8 and (rudp7) the checksum
-  // bytes at positions 5 (low) and 6 (high): take them back out
-  const uint32_t payload_sum = sum - seq - ack - (flags << 8) - (H == 7 ? (b5 | (b6 << 8)) : 0u);
   const uint32_t c = packet_csum(payload_sum, seq, ack, flags);
   uint8_t ok;
   if (H == 7) ok = c == inband ? 1 : 0;
@@ -768,15 +777,18 @@ __device__ __forceinline__ void decode_varlen_finish(const VarlenArgs& a, uint64
 
 // Vectorized varlen decode (frames buffer 16-byte aligned): G lanes per
 // frame load the ALIGNED 16-byte chunks overlapping [off[p], off[p+1]) once
-// each, mask the two boundary chunks to the frame, and sum bytes at even and
-// odd global offsets separately.  A byte at frame position k = x - off[p] is
-// the high byte of its big-endian word iff k is even, i.e. iff x and off[p]
-// have the same parity, which picks the weighting per frame (the fixed-stride
-// decode_verify_kernel's trick with the frame start in place of p*F).  The
-// header comes from the group's first two chunks; the header fields' share of
-// the exact integer sum is taken back out before the fold.  G is chosen on the
-// host from the batch's mean frame length; any G >= 2 gives the same answer.
-template <int H>
+// each, mask the chunks at the frame's edges to its payload bytes, and sum
+// bytes at even and odd global offsets separately.  A byte at frame position
+// k = x - off[p] is the high byte of its big-endian word iff k is even, i.e.
+// iff x and off[p] have the same parity, which picks the weighting per frame
+// (the fixed-stride decode_verify_kernel's trick with the frame start in
+// place of p*F).  The header comes from the group's first two chunks.  G is
+// chosen on the host from the batch's mean frame length; any G >= 2 gives the
+// same answer.
+// U8: the payload's strict UTF-8 check in the same pass: the (masked) payload
+// words' high bits are OR'ed as they are summed, and only a frame that holds
+// one runs the byte checks (utf8_check_frame, its chunks again, from L2).
+template <int H, bool U8>
 __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_t p, bool valid, uint32_t g,
                                                     uint32_t glog) {
   const uint32_t tid = threadIdx.x;
@@ -790,26 +802,31 @@ __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_
   const uint32_t nchunks = fend > fstart ? (uint32_t)(((fend - 1) >> 4) - c_lo + 1) : 0u;
 
   uint32_t even_sum = 0, odd_sum = 0;  // byte sums at even / odd global offsets
+  uint32_t hib = 0;                     // U8: high bits of the payload bytes
+  const uint64_t ps = fstart + H;       // payload start
   u32x4 first = {0u, 0u, 0u, 0u};
-  for (uint32_t i0 = g; i0 < nchunks; i0 += 8u * G) {
+  // loads in flight per lane: 8, or 6 with the UTF-8 check (its registers keep the
+  // tile kernels that inline this at 6 waves per SIMD)
+  constexpr int P = U8 ? 6 : 8;
+  for (uint32_t i0 = g; i0 < nchunks; i0 += (uint32_t)P * G) {
     uint32_t even = 0, odd = 0;  // at most 32 dwords per round: packed halves cannot overflow
-    u32x4 v[8];
+    u32x4 v[P];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < P; ++u) {
       const uint32_t i = i0 + (uint32_t)u * G;
       if (i < nchunks) v[u] = load16_guarded(a.frames, (c_lo + i) << 4, total);
     }
     if (i0 == g) first = v[0];
 #pragma unroll
-    for (int u = 0; u < 8; ++u) {
+    for (int u = 0; u < P; ++u) {
       const uint32_t i = i0 + (uint32_t)u * G;
       if (i < nchunks) {
         u32x4 w = v[u];
-        if (i == 0 || i + 1 == nchunks) {  // boundary chunk: keep this frame's bytes only
+        if (i <= 1 || i + 1 == nchunks) {  // chunks at the frame's edges: its payload bytes only
           const int64_t cb = (int64_t)((c_lo + i) << 4);
-          const int lo = (int)((int64_t)fstart - cb), hi = (int)((int64_t)fend - cb);
-          w = make_u32x4(lo64(w) & byte_mask(lo, hi), hi64(w) & byte_mask(lo - 8, hi - 8));
+          w = keep_bytes(w, (int)((int64_t)ps - cb), (int)((int64_t)fend - cb));
         }
+        if (U8) hib |= w.x | w.y | w.z | w.w;
         even += (w.x & 0x00FF00FFu) + (w.y & 0x00FF00FFu) + (w.z & 0x00FF00FFu) + (w.w & 0x00FF00FFu);
         odd += ((w.x >> 8) & 0x00FF00FFu) + ((w.y >> 8) & 0x00FF00FFu) +
                ((w.z >> 8) & 0x00FF00FFu) + ((w.w >> 8) & 0x00FF00FFu);
@@ -820,7 +837,19 @@ __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_
   }
   // even global offsets are high bytes iff the frame starts at an even offset
   uint32_t sum = (fstart & 1u) ? (even_sum + (odd_sum << 8)) : ((even_sum << 8) + odd_sum);
-  for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
+  for (uint32_t m = G >> 1; m > 0; m >>= 1) {
+    sum += __shfl_xor(sum, (int)m, 64);
+    if (U8) hib |= (uint32_t)__shfl_xor((int)hib, (int)m, 64);
+  }
+  uint32_t u8bad = 0;
+  if (U8 && __any((hib & 0x80808080u) != 0)) {  // the byte checks, for frames with a high bit
+    if ((hib & 0x80808080u) && valid && !bad)
+      u8bad = utf8_check_frame(ps, fend, g, G, [&](uint64_t c) { return load16_guarded(a.frames, c << 4, total); },
+                               [&](uint64_t x) {
+                                 return x >= 4 ? *reinterpret_cast<const uint32_t*>(a.frames + x - 4) : 0u;
+                               });
+    u8bad = group_or(u8bad, G);
+  }
   const int src = (int)((tid & 63u) + 1u);
   u32x4 next;
   next.x = __shfl(first.x, src, 64);
@@ -832,14 +861,15 @@ __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_
     decode_varlen_reject(a, p);
     return;
   }
+  if (U8) a.valid[p] = u8bad ? 0 : 1;
   decode_varlen_finish<H>(a, p, (uint32_t)(fend - fstart), sum, funnel32(first, next, (uint32_t)(fstart & 15u)));
 }
 
-template <int H>
+template <int H, bool U8>
 __global__ void __launch_bounds__(kBlock) decode_varlen_vec_kernel(VarlenArgs a) {
   const uint32_t glog = a.glog;
   const uint64_t p = (uint64_t)blockIdx.x * (kBlock >> glog) + (threadIdx.x >> glog);
-  decode_varlen_frame<H>(a, p, p < a.n, threadIdx.x & ((1u << glog) - 1u), glog);
+  decode_varlen_frame<H, U8>(a, p, p < a.n, threadIdx.x & ((1u << glog) - 1u), glog);
 }
 
 // Varlen decode through an LDS tile (the fixed-length decode tile's shape):
@@ -847,11 +877,11 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_vec_kernel(VarlenArgs a)
 // contiguous run [frame_off[p0], frame_off[p0 + T]).  Phase 1 streams the run
 // into LDS as a copy (every wave-instruction 1 KiB contiguous) and puts the
 // tile's frame offsets there; phase 2 gives G lanes to each frame, which sum
-// its aligned LDS chunks by address parity (as decode_varlen_vec_kernel does
-// from HBM), and the leader parses the header from LDS.  A tile whose run
+// its payload's aligned LDS chunks by address parity (as decode_varlen_vec_kernel
+// does from HBM), and the leader parses the header from LDS.  A tile whose run
 // exceeds tile_cap (lengths far above the hint) decodes its frames with the
 // per-frame vector path inside the same launch.
-template <int H>
+template <int H, bool U8>
 __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const uint32_t tid = threadIdx.x;
@@ -867,11 +897,12 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
   const uint64_t A = fo0 & ~15ull;
   const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
   if (fo0 > fo_end || fo_end > total || run > a.tile_cap) {  // uniform over the workgroup
-    decode_varlen_frame<H>(a, p0 + q, q < Tv, g, glog);
+    decode_varlen_frame<H, U8>(a, p0 + q, q < Tv, g, glog);
     return;
   }
-  // tile-relative offsets; one outside the run reads as 0xFFFFFFFF (its frames are rejected)
-  auto rel = [&](uint64_t o) { return o - A <= run ? (uint32_t)(o - A) : 0xFFFFFFFFu; };
+  // tile-relative offsets; one outside [A, fo_end] reads as 0xFFFFFFFF
+  const uint64_t span_end = fo_end - A;
+  auto rel = [&](uint64_t o) { return o - A <= span_end ? (uint32_t)(o - A) : 0xFFFFFFFFu; };
   {
     // T = 256 / G <= 128 frames: one offset per lane, loaded before the run (early_fo)
     const uint32_t fo_r = a.early_fo && tid <= Tv ? rel(a.frame_off[p0 + tid]) : 0u;
@@ -900,23 +931,27 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
   __syncthreads();
   if (q >= Tv) return;
   {
+    // A pair out of order, or an offset outside the tile's run: the frame may
+    // still be valid (its own pair in order and inside the buffer is all the
+    // rule asks) but reach past the staged bytes, so it decodes from HBM, where
+    // the rule is applied to its true offsets.  Uniform over the frame's lanes.
     const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
-    if (fs > fe || fe > (uint32_t)(fo_end - A)) {  // uniform over the frame's lanes
-      if (g == 0) decode_varlen_reject(a, p0 + q);
+    if (fs > fe || fe > (uint32_t)span_end) {
+      decode_varlen_frame<H, U8>(a, p0 + q, true, g, glog);
       return;
     }
   }
   const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
   const u32x4* img16 = reinterpret_cast<const u32x4*>(img);
   uint32_t even_sum = 0, odd_sum = 0;  // byte sums at even / odd offsets (A is even)
-  if (fe > fs) {
-    const uint32_t c0 = fs >> 4, c1 = (fe - 1u) >> 4;
+  uint32_t hib = 0;                     // U8: high bits of the payload bytes
+  const uint32_t ps = fs + (uint32_t)H;
+  if (fe > ps) {  // the payload's chunks, the edge ones masked to it
+    const uint32_t c0 = ps >> 4, c1 = (fe - 1u) >> 4;
     for (uint32_t c = c0 + g; c <= c1; c += G) {
       u32x4 w = img16[c];
-      if (c == c0 || c == c1) {  // keep this frame's bytes only
-        const int lo = (int)fs - (int)(c << 4), hi = (int)fe - (int)(c << 4);
-        w = make_u32x4(lo64(w) & byte_mask(lo, hi), hi64(w) & byte_mask(lo - 8, hi - 8));
-      }
+      if (c == c0 || c == c1) w = keep_bytes(w, (int)ps - (int)(c << 4), (int)fe - (int)(c << 4));
+      if (U8) hib |= w.x | w.y | w.z | w.w;
       const uint32_t e = (w.x & 0x00FF00FFu) + (w.y & 0x00FF00FFu) + (w.z & 0x00FF00FFu) + (w.w & 0x00FF00FFu);
       const uint32_t o = ((w.x >> 8) & 0x00FF00FFu) + ((w.y >> 8) & 0x00FF00FFu) +
                          ((w.z >> 8) & 0x00FF00FFu) + ((w.w >> 8) & 0x00FF00FFu);
@@ -926,48 +961,36 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
   }
   // even offsets are high bytes iff the frame starts at an even offset
   uint32_t sum = (fs & 1u) ? (even_sum + (odd_sum << 8)) : ((even_sum << 8) + odd_sum);
-  for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
+  for (uint32_t m = G >> 1; m > 0; m >>= 1) {
+    sum += __shfl_xor(sum, (int)m, 64);
+    if (U8) hib |= (uint32_t)__shfl_xor((int)hib, (int)m, 64);
+  }
+  if (U8) {  // a frame with a high bit in its payload: the byte checks, from LDS
+    uint32_t u8bad = 0;
+    if (__any((hib & 0x80808080u) != 0)) {
+      if (hib & 0x80808080u) {
+        const uint32_t* idw = reinterpret_cast<const uint32_t*>(img);  // kVTGuard bytes before it
+        u8bad = utf8_check_frame(ps, fe, g, G, [&](uint64_t c) { return img16[c]; },
+                                 [&](uint64_t x) { return idw[(int64_t)(x >> 2) - 1]; });
+      }
+      u8bad = group_or(u8bad, G);
+    }
+    if (g == 0) a.valid[p0 + q] = u8bad ? 0 : 1;
+  }
   if (g == 0)
     decode_varlen_finish<H>(a, p0 + q, fe - fs,
                             sum, window16_dw(reinterpret_cast<const uint32_t*>(img), fs));
 }
 
-// Strict UTF-8 (RFC 3629, as CPython's bytes.decode() accepts it, i.e. what
-// utils/packet.py:73 enforces): no overlongs (C0, C1, E0 80-9F, F0 80-8F), no
-// surrogates (ED A0-BF), nothing above U+10FFFF (F4 90+, F5-FF), no stray or
-// missing continuation bytes.  Byte-parallel: every byte is judged from itself and the three bytes before it, so the
-// payload splits over G lanes with no carried state (the approach of SIMD
-// UTF-8 validators): byte c at payload index i, with p1 p2 p3 the bytes at
-// i-1, i-2, i-3 (0 before the payload start):
-//   c is a continuation byte  <=>  p1 is a 2/3/4-byte lead, or p2 a 3/4-byte
-//                                  lead, or p3 a 4-byte lead ("expected")
-//   C0 C1 F5..FF never appear; after E0 / ED / F0 / F4 the next byte lies in
-//   A0-BF / 80-9F / 90-BF / 80-8F; and nothing is still expected at the end.
-__device__ __forceinline__ uint32_t utf8_need(uint32_t b) {  // continuation bytes a lead asks for
-  return b >= 0xF0 ? 3u : b >= 0xE0 ? 2u : b >= 0xC0 ? 1u : 0u;
-}
-
-__device__ __forceinline__ bool utf8_byte_ok(uint32_t c, uint32_t p1, uint32_t p2, uint32_t p3) {
-  const bool cont = (c & 0xC0u) == 0x80u;
-  const bool expected = utf8_need(p1) >= 1 || utf8_need(p2) >= 2 || utf8_need(p3) >= 3;
-  // p1..p3 that are themselves continuation bytes ask for nothing (need() of 80-BF is 0)
-  if (cont != expected) return false;
-  if (c == 0xC0 || c == 0xC1 || c >= 0xF5) return false;
-  if (p1 == 0xE0 && c < 0xA0) return false;
-  if (p1 == 0xED && c > 0x9F) return false;
-  if (p1 == 0xF0 && c < 0x90) return false;
-  if (p1 == 0xF4 && c > 0x8F) return false;
-  return true;
-}
-
+// Strict UTF-8 validation kernels (the checks themselves: utf8_device.hpp).
 __global__ void __launch_bounds__(kBlock) validate_utf8_par_kernel(Utf8Args a) {
   if (call_failed(a.status)) return;
   const uint32_t g = threadIdx.x & (kVarLanes - 1u);
   const uint64_t p = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / kVarLanes;
   const bool valid_p = p < a.n;
   uint32_t bad = 0;
-  uint64_t fo = 0, fe = 0;
   if (valid_p) {
+    uint64_t fo, fe;
     if (a.frame_off) {
       fo = a.frame_off[p];
       fe = a.frame_off[p + 1];
@@ -976,25 +999,7 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_par_kernel(Utf8Args a) {
       fe = fo + a.F;
     }
     const uint64_t s = fo + a.H;  // payload start
-    if (s < fe) {
-      const uint64_t len = fe - s;
-      // lane g judges a contiguous slice of ceil(len / G) bytes
-      const uint64_t per = (len + kVarLanes - 1) / kVarLanes;
-      const uint64_t b0 = g * per, b1 = b0 + per < len ? b0 + per : len;
-      uint32_t p3 = b0 >= 3 ? a.frames[s + b0 - 3] : 0u;
-      uint32_t p2 = b0 >= 2 ? a.frames[s + b0 - 2] : 0u;
-      uint32_t p1 = b0 >= 1 ? a.frames[s + b0 - 1] : 0u;
-      for (uint64_t i = b0; i < b1; ++i) {
-        const uint32_t c = a.frames[s + i];
-        bad |= utf8_byte_ok(c, p1, p2, p3) ? 0u : 1u;
-        p3 = p2;
-        p2 = p1;
-        p1 = c;
-      }
-      if (b1 == len && b0 < b1) {  // last slice: nothing may still be expected
-        bad |= (utf8_need(p1) >= 1 || utf8_need(p2) >= 2 || utf8_need(p3) >= 3) ? 1u : 0u;
-      }
-    }
+    if (s < fe) bad = utf8_slice(a.frames, s, fe - s, g, kVarLanes);
   }
   for (uint32_t m = kVarLanes >> 1; m > 0; m >>= 1) bad |= __shfl_xor(bad, (int)m, 64);
   if (valid_p && g == 0) a.valid[p] = bad ? 0 : 1;
@@ -1006,11 +1011,6 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_par_kernel(Utf8Args a) {
 // predecessor bytes), bytes outside [payload start, frame end) count as
 // absent (0).  An all-ASCII chunk whose predecessors hold no lead byte is
 // valid without the per-byte walk: the common case for text payloads.
-
-__device__ __forceinline__ uint32_t byte_of(u32x4 v, int k) {
-  const uint32_t w = k < 4 ? v.x : k < 8 ? v.y : k < 12 ? v.z : v.w;
-  return (w >> (8 * (k & 3))) & 0xFFu;
-}
 
 __global__ void __launch_bounds__(kBlock) validate_utf8_vec_kernel(Utf8Args a) {
   if (call_failed(a.status)) return;
@@ -1103,49 +1103,12 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_vec_kernel(Utf8Args a) {
         p1 = cb;
       }
       if (i + 1 == nch)  // the frame's last chunk: nothing may still be expected
-        bad |= (utf8_need(p1) >= 1 || utf8_need(p2) >= 2 || utf8_need(p3) >= 3) ? 1u : 0u;
+        bad |= utf8_pending(p1, p2, p3) ? 1u : 0u;
     }
     carry = vv[U - 1].w;
   }
   for (uint32_t m = G >> 1; m > 0; m >>= 1) bad |= __shfl_xor(bad, (int)m, 64);
   if (valid_p && g == 0) a.valid[p] = bad ? 0 : 1;
-}
-
-// Strict UTF-8 check of one frame's payload bytes [s, fe) by G lanes (lane g
-// takes aligned chunks c_lo + g, + G, ...): `chunk(c)` returns aligned chunk c
-// and `prev(x)` the dword of bytes x-4 .. x-1 (x a multiple of 16; only bytes
-// at or past s are used).  Returns nonzero if this lane saw an invalid byte.
-template <class Chunk, class Prev>
-__device__ __forceinline__ uint32_t utf8_check_frame(uint64_t s, uint64_t fe, uint32_t g, uint32_t G,
-                                                     Chunk chunk, Prev prev_dw) {
-  uint32_t bad = 0;
-  if (fe <= s) return 0;
-  const uint64_t c_lo = s >> 4, c_hi = (fe - 1u) >> 4;
-  for (uint64_t c = c_lo + g; c <= c_hi; c += G) {
-    const uint64_t x = c << 4;
-    const u32x4 v = chunk(c);
-    const uint32_t prev = prev_dw(x);
-    uint32_t p3 = x >= s + 3 ? (prev >> 8) & 0xFFu : 0u;
-    uint32_t p2 = x >= s + 2 ? (prev >> 16) & 0xFFu : 0u;
-    uint32_t p1 = x >= s + 1 ? prev >> 24 : 0u;
-    const int lo_b = (int)((int64_t)s - (int64_t)x), hi_b = (int)((int64_t)fe - (int64_t)x);
-    const uint64_t pl = lo64(v) & byte_mask(lo_b, hi_b), ph = hi64(v) & byte_mask(lo_b - 8, hi_b - 8);
-    if (((pl | ph) & 0x8080808080808080ull) == 0 && p1 < 0xC0 && p2 < 0xC0 && p3 < 0xC0) continue;
-    if (bad) continue;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const uint64_t y = x + (uint64_t)k;
-      if (y < s || y >= fe) continue;
-      const uint32_t cb = byte_of(v, k);
-      bad |= utf8_byte_ok(cb, p1, p2, p3) ? 0u : 1u;
-      p3 = p2;
-      p2 = p1;
-      p1 = cb;
-    }
-    if (c == c_hi)  // the frame's last chunk: nothing may still be expected
-      bad |= (utf8_need(p1) >= 1 || utf8_need(p2) >= 2 || utf8_need(p3) >= 3) ? 1u : 0u;
-  }
-  return bad;
 }
 
 // Fixed-stride frames through an LDS tile (frames 16-B aligned, H < F,
@@ -1551,7 +1514,33 @@ int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int
 // stream into LDS, then each lane parses FPT frames (lane-strided, so the
 // per-frame outputs leave as coalesced stores), summing a frame's LDS dwords
 // by address parity.  A run over the LDS budget decodes per frame (G = 1).
-template <int H, uint32_t FPT>
+// One frame by one lane, straight from HBM, byte by byte: the checked rule
+// on its true offsets (the small-frame tile's frames whose offsets fall
+// outside its staged run; rare).
+template <int H, bool U8>
+__device__ __noinline__ void decode_varlen_frame_lane(const VarlenArgs& a, uint64_t p) {
+  const uint64_t fo = a.frame_off[p], fe = a.frame_off[p + 1];
+  if (fo > fe || fe > frames_limit(a)) {
+    decode_varlen_reject(a, p);
+    return;
+  }
+  const uint32_t F = (uint32_t)(fe - fo);
+  uint32_t sum = 0;
+  for (uint32_t j = (uint32_t)H; j < F; ++j) sum += ((j - H) & 1u) ? (uint32_t)a.frames[fo + j] << 8 : a.frames[fo + j];
+  uint32_t d[4] = {0, 0, 0, 0};
+  for (uint32_t i = 0; i < 7 && i < F; ++i) d[i >> 2] |= (uint32_t)a.frames[fo + i] << (8 * (i & 3));
+  u32x4 h;
+  h.x = d[0];
+  h.y = d[1];
+  h.z = 0;
+  h.w = 0;
+  if (U8)
+    a.valid[p] = F > (uint32_t)H && utf8_check_bytes((uint32_t)H, F, [&](uint32_t i) { return (uint32_t)a.frames[fo + i]; })
+                     ? 0 : 1;
+  decode_varlen_finish<H>(a, p, F, sum, h);
+}
+
+template <int H, uint32_t FPT, bool U8>
 __global__ void __launch_bounds__(kBlock) decode_varlen_small_kernel(VarlenArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   constexpr uint32_t T = kBlock * FPT;
@@ -1568,7 +1557,7 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_small_kernel(VarlenArgs 
 #pragma unroll
     for (uint32_t j = 0; j < 2u * FPT; ++j) {  // (the header comes from the pair's two first chunks)
       const uint32_t q = j * (kBlock / 2u) + (tid >> 1);
-      decode_varlen_frame<H>(a, p0 + q, q < Tv, tid & 1u, 1u);
+      decode_varlen_frame<H, U8>(a, p0 + q, q < Tv, tid & 1u, 1u);
     }
     return;
   }
@@ -1578,7 +1567,7 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_small_kernel(VarlenArgs 
     for (uint32_t j = 0; j < FPT; ++j) {
       const uint32_t q = j * kBlock + tid;
       const uint64_t o = q <= Tv ? a.frame_off[p0 + q] : A;
-      fo_r[j] = o - A <= run ? (uint32_t)(o - A) : 0xFFFFFFFFu;  // outside the run: its frames are rejected
+      fo_r[j] = o - A <= fo_end - A ? (uint32_t)(o - A) : 0xFFFFFFFFu;  // outside [A, fo_end]
     }
     if (tid == 0) fo_last = (uint32_t)(fo_end - A);
     const uint32_t nvec = (uint32_t)(run >> 4);
@@ -1604,54 +1593,62 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_small_kernel(VarlenArgs 
     const uint32_t q = j * kBlock + tid;
     if (q >= Tv) continue;
     const uint32_t fs = s_fo[q], fe = s_fo[q + 1];
-    if (fs > fe || fe > lim) {
-      decode_varlen_reject(a, p0 + q);
+    if (fs > fe || fe > lim) {  // out of order or outside the run: this lane, from HBM (see the tile kernel)
+      decode_varlen_frame_lane<H, U8>(a, p0 + q);
       continue;
     }
     uint32_t ev = 0, od = 0;  // byte sums at even / odd offsets (A is even)
-    if (fe > fs) {
-      const uint32_t w0 = fs >> 2, w1 = (fe - 1u) >> 2;
+    uint32_t hib = 0;         // U8: high bits of the payload bytes
+    const uint32_t ps = fs + (uint32_t)H;
+    if (fe > ps) {  // the payload's dwords, the edge ones masked to it
+      const uint32_t w0 = ps >> 2, w1 = (fe - 1u) >> 2;
       for (uint32_t w = w0; w <= w1; ++w) {
         uint32_t v = dw[w];
-        if (w == w0 || w == w1) {  // keep this frame's bytes only
-          const int lo = (int)fs - (int)(4u * w), hi = (int)fe - (int)(4u * w);
+        if (w == w0 || w == w1) {
+          const int lo = (int)ps - (int)(4u * w), hi = (int)fe - (int)(4u * w);
           v &= (uint32_t)byte_mask(lo, hi < 4 ? hi : 4);
         }
+        if (U8) hib |= v;
         ev += (v & 0xFFu) + ((v >> 16) & 0xFFu);
         od += ((v >> 8) & 0xFFu) + (v >> 24);
       }
+    }
+    if (U8) {
+      const unsigned char* ib = img;
+      a.valid[p0 + q] = (hib & 0x80808080u) && utf8_check_bytes(ps, fe, [&](uint32_t i) { return (uint32_t)ib[i]; })
+                            ? 0 : 1;
     }
     const uint32_t sum = (fs & 1u) ? (ev + (od << 8)) : ((ev << 8) + od);
     decode_varlen_finish<H>(a, p0 + q, fe - fs, sum, window16_dw(dw, fs));
   }
 }
 
-template <int H, uint32_t FPT>
+template <int H, uint32_t FPT, bool U8>
 int launch_decode_small_fpt(const VarlenArgs& args, hipStream_t stream) {
   constexpr uint32_t T = kBlock * FPT;
   const size_t lds = ((4u * (T + 1u) + 15u) & ~15u) + (size_t)args.small_cap + 32u;
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_varlen_small_kernel<H, FPT>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_varlen_small_kernel<H, FPT, U8>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
   const uint64_t blocks = (args.n + T - 1) / T;
-  hipLaunchKernelGGL((decode_varlen_small_kernel<H, FPT>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream,
+  hipLaunchKernelGGL((decode_varlen_small_kernel<H, FPT, U8>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream,
                      args);
   return (int)hipGetLastError();
 }
 
-template <int H>
+template <int H, bool U8>
 int launch_decode_small(const VarlenArgs& args, hipStream_t stream) {
 #if RUDP_TOOLS  // 4 frames per thread is the measured choice; 1, 2 and 8 for sweeps
   switch (args.small_fpt) {
-    case 1: return launch_decode_small_fpt<H, 1>(args, stream);
-    case 2: return launch_decode_small_fpt<H, 2>(args, stream);
-    case 8: return launch_decode_small_fpt<H, 8>(args, stream);
+    case 1: return launch_decode_small_fpt<H, 1, U8>(args, stream);
+    case 2: return launch_decode_small_fpt<H, 2, U8>(args, stream);
+    case 8: return launch_decode_small_fpt<H, 8, U8>(args, stream);
     default: break;
   }
 #endif
-  return launch_decode_small_fpt<H, 4>(args, stream);
+  return launch_decode_small_fpt<H, 4, U8>(args, stream);
 }
 
 // Dynamic LDS of one varlen encode tile whose arrays hold Tl packets.
@@ -1815,10 +1812,13 @@ int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream)
   return (int)hipGetLastError();
 }
 
-int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream) {
-  if (args.n == 0) return 0;
+// Every varlen decode form validates the payload's UTF-8 in the same pass when
+// args.valid is set (U8): the reference's receive decodes every payload
+// (utils/reliableUDP.py:121, get_payload's strict decode at utils/packet.py:73).
+template <int H, bool U8>
+static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
   if (args.small_fpt && args.glog != kNoVec && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0)
-    return layout == 7 ? launch_decode_small<7>(args, stream) : launch_decode_small<5>(args, stream);
+    return launch_decode_small<H, U8>(args, stream);
   if (args.glog != kNoVec && args.tile_cap && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0) {
     const uint32_t T = kBlock >> args.glog;
     const size_t lds = ((((T + 1u) * 4u) + 15u) & ~15u) + kVTGuard + args.tile_cap + 32u;
@@ -1827,27 +1827,25 @@ int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream)
       // 76 VGPRs (6 waves per SIMD).  Asking the allocator for 7 or 8 waves
       // spills and was slower at every size (1M x 1479 B 0.265 -> 0.306 ms;
       // profiles/r01/sweeps/varlen_decode_waves.json).
-      if (layout == 7)
-        hipLaunchKernelGGL(decode_varlen_tile_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
-      else
-        hipLaunchKernelGGL(decode_varlen_tile_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
+      hipLaunchKernelGGL((decode_varlen_tile_kernel<H, U8>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
       return (int)hipGetLastError();
     }
   }
   if (args.glog != kNoVec && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0) {
     const uint64_t blocks = (args.n + (kBlock >> args.glog) - 1) / (kBlock >> args.glog);
-    if (layout == 7)
-      hipLaunchKernelGGL(decode_varlen_vec_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
-    else
-      hipLaunchKernelGGL(decode_varlen_vec_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+    hipLaunchKernelGGL((decode_varlen_vec_kernel<H, U8>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
     return (int)hipGetLastError();
   }
   const uint64_t blocks = (args.n * kVarLanes + kBlock - 1) / kBlock;
-  if (layout == 7)
-    hipLaunchKernelGGL(decode_varlen_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
-  else
-    hipLaunchKernelGGL(decode_varlen_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+  hipLaunchKernelGGL((decode_varlen_kernel<H, U8>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
   return (int)hipGetLastError();
+}
+
+int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream) {
+  if (args.n == 0) return 0;
+  if (args.valid)
+    return layout == 7 ? launch_decode_varlen_t<7, true>(args, stream) : launch_decode_varlen_t<5, true>(args, stream);
+  return layout == 7 ? launch_decode_varlen_t<7, false>(args, stream) : launch_decode_varlen_t<5, false>(args, stream);
 }
 
 int launch_validate_utf8(const Utf8Args& args, hipStream_t stream) {

@@ -25,7 +25,7 @@ LAYOUT_RUDP5 = 5
 LAYOUT_RUDP7 = 7
 OK_BAD_CSUM, OK_GOOD, OK_SHORT, OK_UNVERIFIED, OK_BAD_OFFSETS = 0, 1, 2, 3, 4
 EINVAL, ENOMEM, ENOTSUP, EHIP_BASE = -22, -12, -95, -1000
-ABI_VERSION = 5
+ABI_VERSION = 6
 # status bits of the sync-free varlen calls (RUDP_ST_*)
 ST_LEN, ST_PAYLOAD, ST_FRAMES_CAP, ST_OFFSETS = 1, 2, 4, 8
 DUP_BAD_OFFSETS = 2  # rudp_dedup_window_checked: a frame whose offsets were rejected
@@ -38,6 +38,7 @@ EXPORTS = (
     "rudp_udp_recv_batch", "rudp_udp_send_batch", "rudp_varlen_bounds", "rudp_frame_off_bounds",
     "rudp_encode_varlen_checked", "rudp_decode_varlen_checked", "rudp_frame_off_check",
     "rudp_udp_recv_batch_from", "rudp_udp_send_batch_to", "rudp_dedup_window_checked",
+    "rudp_decode_utf8", "rudp_decode_varlen_utf8",
 )
 
 
@@ -88,6 +89,8 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rudp_frame_off_bounds": [P, U64, P, I, P],
         "rudp_encode_varlen_checked": [ctypes.POINTER(RudpBatch), U64, P, U64, P, P, P, I, I, P],
         "rudp_decode_varlen_checked": [P, U64, P, U32, U64, P, P, P, P, P, P, P, I, I, P],
+        "rudp_decode_utf8": [P, P, U32, U64, P, P, P, P, P, P, P, P, I, I, P],
+        "rudp_decode_varlen_utf8": [P, U64, P, U32, U64, P, P, P, P, P, P, P, P, I, I, P],
         "rudp_frame_off_check": [P, U64, U64, P, I, P],
         "rudp_device_count": [ctypes.POINTER(ctypes.c_int)],
         "rudp_abi_version": [],
@@ -141,7 +144,8 @@ def tools_lib(activate: bool = True) -> ctypes.CDLL:
                                "rudpx_copy": [P, P, U64, U32, P], "rudpx_copy_vpt": [P, P, U64, I, I, P],
                                "rudpx_copy_tile": [P, P, U64, U32, U32, P],
                                "rudpx_copy_tile_dma": [P, P, U64, U32, U32, U32, I, P],
-                               "rudpx_copy_tile_pipe": [P, P, U64, U32, U32, U32, P]}.items():
+                               "rudpx_copy_tile_pipe": [P, P, U64, U32, U32, U32, P],
+                               "rudpx_scratch_stats": [I, P]}.items():
                 fn = getattr(h, name)
                 fn.argtypes = args
                 fn.restype = I

@@ -124,6 +124,7 @@ class DecodedBatch(NamedTuple):
     csum: Any        # recomputed checksum per packet
     payload: Any     # [N, L] view into frames (zero-copy) or a copy
     status: Any = None  # sync-free varlen decode: device u32[1], RUDP_ST_* (0 = valid)
+    valid: Any = None   # utf8=True: u8 [N], 1 where get_payload() would return, 0 where it raises
 
     def check(self) -> "DecodedBatch":
         """Raise ValueError if the device rejected the batch (reads ``status``:
@@ -209,7 +210,7 @@ def _pack_device(tab: HeaderTable, payloads, H: int, out, csum_out, want_csum, s
     return out, csum_out
 
 
-def _unpack_device(frames, H: int, csum, copy_payload: bool, stream):
+def _unpack_device(frames, H: int, csum, copy_payload: bool, stream, utf8: bool = False):
     import torch
     dev = frames.device
     if dev.type != "cuda":
@@ -227,16 +228,18 @@ def _unpack_device(frames, H: int, csum, copy_payload: bool, stream):
         if csum.shape[0] != n:
             raise ValueError(f"csum has {csum.shape[0]} entries for {n} frames")
     pay = torch.empty((n, L), dtype=torch.uint8, device=dev) if copy_payload else None
+    valid = torch.empty((n,), dtype=torch.uint8, device=dev) if utf8 else None
     if n:
-        _native.check(_native.lib().rudp_decode(
+        _native.check(_native.lib().rudp_decode_utf8(
             frames.data_ptr() if F else None, None, F, n, csum.data_ptr() if csum is not None else None,
             seq.data_ptr(), ack.data_ptr(), flags.data_ptr(), ok.data_ptr(), cs.data_ptr(),
-            pay.data_ptr() if (pay is not None and L) else None, H,
+            pay.data_ptr() if (pay is not None and L) else None,
+            valid.data_ptr() if valid is not None else None, H,
             dev.index if dev.index is not None else torch.cuda.current_device(),
             _stream_ptr(stream, dev)))
     if pay is None:
         pay = frames[:, H:] if F >= H else frames[:, :0]
-    return DecodedBatch(seq, ack, flags, ok, cs, pay)
+    return DecodedBatch(seq, ack, flags, ok, cs, pay, None, valid)
 
 
 # ------------------------------------------------------------------ host path
@@ -328,17 +331,23 @@ def pack_batch(headers, payloads, layout: Union[str, int] = "rudp7", *, out=None
 
 
 def unpack_batch(frames, layout: Union[str, int] = "rudp7", *, csum=None,
-                 copy_payload: bool = False, stream=None, device: int = 0) -> DecodedBatch:
+                 copy_payload: bool = False, stream=None, device: int = 0, utf8: bool = False) -> DecodedBatch:
     """Parse + verify a batch of fixed-length frames ``[N, F]``.
 
     ``csum`` (rudp5 only): sideband checksums to verify against.  The payload
     is returned as a zero-copy view ``frames[:, H:]`` unless ``copy_payload``.
+    ``utf8`` (device tensors): also ``valid``, u8 [N], 1 where
+    Packet(frame).get_payload() would return and 0 where its strict UTF-8
+    decode would raise (utils/packet.py:68-73), judged in the same pass over
+    the frames (rudp_decode_utf8).
     """
     H = layout_header_len(layout)
     if H == 7 and csum is not None:
         raise ValueError("rudp7 carries its checksum in-band; csum= is for rudp5")
     if _is_torch(frames):
-        return _unpack_device(frames, H, csum, copy_payload, stream)
+        return _unpack_device(frames, H, csum, copy_payload, stream, utf8)
+    if utf8:
+        raise ValueError("utf8=True needs device tensors (use validate_utf8 on the host-staged result)")
     return _unpack_host(frames, H, csum, copy_payload, device)
 
 
@@ -430,34 +439,20 @@ class VarlenFrames:
         return self
 
 
-class _RejectedFrames:
-    """Status of a sync-free variable-length decode, read from its ``ok`` array
-    on demand: RUDP_ST_OFFSETS when a frame was rejected for bad offsets
-    (ok == RUDP_OK_BAD_OFFSETS), else 0.  The decode keeps no status word of its
-    own, so a call is its one kernel (rudp_decode_varlen_checked, d_status NULL)."""
-
-    __slots__ = ("_ok",)
-
-    def __init__(self, ok):
-        self._ok = ok
-
-    def item(self) -> int:
-        return _native.ST_OFFSETS if bool((self._ok == _native.OK_BAD_OFFSETS).any()) else 0
-
-
 class VarlenDecoded:
     """Result of ``unpack_batch_varlen``, with the fields of ``DecodedBatch``:
     seq, ack (u16 [N]), flags, ok (u8 [N]), csum (u16 [N]), payload
-    (``PayloadSpans``) and status.  The five output arrays share one device
-    allocation and are cut out of it on first access.  Iterates as
-    (seq, ack, flags, ok, csum, payload, status)."""
+    (``PayloadSpans``), status and valid (u8 [N] with ``utf8=True``, else
+    None).  The output arrays share one device allocation and are cut out of
+    it on first access.  Iterates as (seq, ack, flags, ok, csum, payload,
+    status)."""
 
-    __slots__ = ("_buf", "_n", "payload", "_v")
+    __slots__ = ("_buf", "_n", "payload", "_v", "_utf8")
 
-    def __init__(self, buf, n: int, payload):
-        self._buf, self._n, self.payload, self._v = buf, n, payload, {}
+    def __init__(self, buf, n: int, payload, utf8: bool = False):
+        self._buf, self._n, self.payload, self._v, self._utf8 = buf, n, payload, {}, utf8
 
-    # one allocation: seq | ack | csum (u16 [n] each) | flags | ok (u8 [n] each)
+    # one allocation: seq | ack | csum (u16 [n] each) | flags | ok | valid (u8 [n] each)
     def _cut(self, name, at, nbytes, dtype):
         v = self._v.get(name)
         if v is None:
@@ -491,8 +486,22 @@ class VarlenDecoded:
         return self._cut("ok", 7 * self._n, self._n, None)
 
     @property
+    def valid(self):
+        return self._cut("valid", 8 * self._n, self._n, None) if self._utf8 else None
+
+    @property
     def status(self):
-        return _RejectedFrames(self.ok)
+        """Device int32 [1]: RUDP_ST_OFFSETS when a frame was rejected for bad
+        offsets (ok == RUDP_OK_BAD_OFFSETS), else 0, as ``VarlenFrames.status``.
+        The decode keeps no status word of its own (a call is its one kernel,
+        rudp_decode_varlen_checked with d_status NULL), so this is built from
+        ``ok`` on first access: one device reduction, no synchronization."""
+        v = self._v.get("status")
+        if v is None:
+            import torch
+            v = ((self.ok == _native.OK_BAD_OFFSETS).any().to(torch.int32) * _native.ST_OFFSETS).reshape(1)
+            self._v["status"] = v
+        return v
 
     def __iter__(self):
         return iter((self.seq, self.ack, self.flags, self.ok, self.csum, self.payload, self.status))
@@ -643,8 +652,8 @@ def _check_offsets(frames, frame_off, stream=None) -> int:
 
 
 def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *, csum=None,
-                        stream=None, check: bool = True, reuse: Optional["VarlenDecoded"] = None
-                        ) -> "VarlenDecoded":
+                        stream=None, check: bool = True, reuse: Optional["VarlenDecoded"] = None,
+                        utf8: bool = False) -> "VarlenDecoded":
     """Parse + verify frames packed back to back (offsets as pack_batch_varlen returns).
 
     The payload is zero-copy: ``payload`` is the pair ``(start, end)`` of int64
@@ -655,7 +664,10 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
     ``check=True`` waits and raises ValueError when there is one;
     ``check=False`` never waits, and the result's ``check()`` raises later.
     ``reuse``: an earlier result for the same N whose output buffer takes this
-    call's outputs (no allocation).
+    call's outputs (no allocation).  ``utf8``: also ``valid`` (u8 [N]: 1 where
+    Packet(frame).get_payload() would return, 0 where its strict UTF-8 decode
+    would raise, utils/packet.py:68-73; 0 for a rejected frame), judged by the
+    decode kernel from the bytes it already holds (rudp_decode_varlen_utf8).
     """
     import torch
     H = layout_header_len(layout)
@@ -674,21 +686,24 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
     # one allocation for every output: seq | ack | csum (u16) | flags | ok (u8), cut
     # into views only when the caller reads them (per-view slicing was most of the
     # entry's host time at small batches)
+    per = 9 if utf8 else 8
     if reuse is not None:
-        if not isinstance(reuse, VarlenDecoded) or reuse._n != n or reuse._buf.device != dev:
-            raise ValueError("reuse= must be an earlier unpack_batch_varlen result for the same N and device")
+        if not isinstance(reuse, VarlenDecoded) or reuse._n != n or reuse._buf.device != dev \
+                or reuse._utf8 != utf8:
+            raise ValueError("reuse= must be an earlier unpack_batch_varlen result for the same N, device "
+                             "and utf8 choice")
         buf = reuse._buf
     else:
-        buf = frames.new_empty(8 * n)  # (u8 on dev, checked above)
+        buf = frames.new_empty(per * n)  # (u8 on dev, checked above)
     base = buf.data_ptr()
     # mean frame length from the buffer size: a hint that picks lanes / tiles per frame
     hint = min(frames.numel() // n, 0xFFFFFFFF) if n else 0
     # no status word: a rejected frame is ok == RUDP_OK_BAD_OFFSETS (check() reads that)
-    _native.check(_native.lib().rudp_decode_varlen_checked(
+    _native.check(_native.lib().rudp_decode_varlen_utf8(
         frames.data_ptr() if frames.numel() else 16, frames.numel(), frame_off.data_ptr(), hint, n,
         csum.data_ptr() if csum is not None else None, base, base + 2 * n, base + 6 * n, base + 7 * n,
-        base + 4 * n, None, H, dev.index or 0, _stream_ptr(stream, dev)))
-    res = VarlenDecoded(buf, n, PayloadSpans(frame_off, H))
+        base + 4 * n, base + 8 * n if utf8 else None, None, H, dev.index or 0, _stream_ptr(stream, dev)))
+    res = VarlenDecoded(buf, n, PayloadSpans(frame_off, H), utf8)
     return res.check() if check else res
 
 

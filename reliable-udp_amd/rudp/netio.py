@@ -135,6 +135,12 @@ class BatchReceiver:
         # each datagram's source (addr_key), for callers that route by it (the relay)
         self._src = [np.empty((max_msgs,), dtype=np.uint64) for _ in range(slots)] if with_sources else None
         self._copied = [None] * slots   # event behind the last H2D copy out of each slot
+        # a caller that still reads a slot on the host after recv() returns (the relay's
+        # sender thread) holds it; recv() hands a slot to the socket only once released
+        import threading
+        self._free = [threading.Event() for _ in range(slots)]
+        for ev in self._free:
+            ev.set()
         self._slot = -1
         self.count = 0
 
@@ -154,8 +160,18 @@ class BatchReceiver:
             raise RuntimeError("BatchReceiver(with_sources=True) keeps the sources")
         return self._src[self._slot][:self.count]
 
+    def hold(self) -> int:
+        """Keep the last batch's slot from the socket until ``release(slot)``
+        (a host reader of it on another thread).  Returns the slot."""
+        self._free[self._slot].clear()
+        return self._slot
+
+    def release(self, slot: int) -> None:
+        self._free[slot].set()
+
     def recv(self, timeout_ms: int = -1) -> int:
         k = (self._slot + 1) % len(self._frames_t)
+        self._free[k].wait()
         if self._copied[k] is not None:
             self._copied[k].synchronize()  # that slot's H2D copy has left the pinned buffer
             self._copied[k] = None
@@ -168,13 +184,34 @@ class BatchReceiver:
     def frame(self, i: int) -> bytes:
         return bytes(self.frames[self.frame_off[i]:self.frame_off[i + 1]])
 
-    def decode(self, layout="rudp5", device=None, csum=None, stream=None, check=False):
+    def copy_frames_to(self, dst, stream=None) -> int:
+        """Enqueue the H2D copy of the last batch's packed frames into ``dst``
+        (a u8 device tensor with room for them) on ``stream`` (default: this
+        receiver's); the slot goes back to the socket only once it has run.
+        Returns the byte count.  (For callers that place the frames themselves,
+        e.g. behind a device-resident history: rudp.relay.)"""
+        import torch
+        s = stream if stream is not None else self.stream
+        k, n = self._slot, self.count
+        total = int(self._off_t[k][n])
+        if total:
+            with torch.cuda.stream(s):
+                dst[:total].copy_(self._frames_t[k][:total], non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record(s)
+                self._copied[k] = ev
+        return total
+
+    def decode(self, layout="rudp5", device=None, csum=None, stream=None, check=False, utf8=False):
         """H2D of the received frames, then parse + verify them on the device.
 
         Returns ``(VarlenDecoded, d_frames, d_frame_off)``; the device buffers are
         fresh (the caller owns them; the payload spans index ``d_frames``).
         ``check=True`` also waits for the device's offset check and raises on
         bad offsets (recvmmsg writes valid ones, so the default is not to wait).
+        ``utf8=True``: the result's ``valid`` says, per datagram, whether the
+        reference's receive (utils/reliableUDP.py:121, get_payload) would decode
+        its payload, judged in the same kernel as the parse.
         """
         import torch
         if device is not None and torch.device(device) != self.device:
@@ -193,7 +230,7 @@ class BatchReceiver:
             ev = torch.cuda.Event()
             ev.record(s)
             self._copied[k] = ev
-            dec = _batch.unpack_batch_varlen(d_frames, d_off, layout, csum=csum, stream=s, check=False)
+            dec = _batch.unpack_batch_varlen(d_frames, d_off, layout, csum=csum, stream=s, check=False, utf8=utf8)
         cur = torch.cuda.current_stream(self.device)
         cur.wait_stream(s)
         # allocated on `s`, used on the caller's stream from here on

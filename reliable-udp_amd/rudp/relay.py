@@ -17,12 +17,20 @@ bytes.  O(1) per datagram instead of up to 500 __eq__ calls.
 
 ``Relay(..., batched=True)`` is the batched form:
 every recvmmsg takes up to ``max_msgs`` datagrams with their source addresses
-(rudp_udp_recv_batch_from); the retransmission flags of the whole batch come
-from one GPU launch of rudp_dedup_window over the last MAX_MEMORY datagrams
-of the earlier batches followed by this batch (the history carried across
-batches), and the datagrams that are not dropped leave in one sendmmsg with
-per-datagram destinations (rudp_udp_send_batch_to).  Same forwarding, log and
-counters as the per-datagram loop.
+into a pinned receive ring (rudp.netio.BatchReceiver, rudp_udp_recv_batch_from),
+and the datagrams that are not dropped leave in one sendmmsg with
+per-datagram destinations (rudp_udp_send_batch_to), on a forwarding thread
+of their own so the kernel's per-datagram send cost overlaps the next
+recvmmsg (the receive slot stays held until its datagrams are sent; one
+thread, so each direction keeps its order).  The retransmission flags
+of a batch come from one GPU launch of rudp_dedup_window over the last
+MAX_MEMORY datagrams of the earlier batches followed by this batch: the
+history stays on the device (two arenas used in turn, the kept tail copied
+device to device), every size it needs is known on the host, and the flags
+are summed into device counters, so the loop never waits for the GPU; the
+counters are read when ``stats`` is.  Forwarding does not depend on the flags
+(the proxy only counts retransmissions, proxy.py:90-91).  Same forwarding, log
+and counters as the per-datagram loop.
 """
 from __future__ import annotations
 
@@ -61,8 +69,8 @@ class Relay(threading.Thread):
         self.keep_log = keep_log
         self.log: Dict[str, List[bytes]] = {"c2s": [], "s2c": []}
         self.seen = {"c2s": 0, "s2c": 0}  # datagrams per direction (the drop rule's index)
-        self.stats = {f"{side}_{k}": 0 for side in ("client", "server")
-                      for k in ("sent", "received", "dropped", "retransmitted")}
+        self._stats = {f"{side}_{k}": 0 for side in ("client", "server")
+                       for k in ("sent", "received", "dropped", "retransmitted")}
         self._history: deque = deque()
         self._seen: Counter = Counter()
         self.stop_event = threading.Event()
@@ -75,52 +83,101 @@ class Relay(threading.Thread):
             from .netio import addr_key
             self._server_key = addr_key(host, server_port)
             self._client_key = None
-            # the last MAX_MEMORY datagrams (both directions), packed, for the next batch's check
-            self._hist_frames = np.zeros(0, np.uint8)
-            self._hist_off = np.zeros(1, np.int64)
+            self._stream = torch.cuda.Stream(self._device)
+            cap_frames = (MAX_MEMORY + max_msgs) * SLOT_BYTES + 16
+            # the last MAX_MEMORY datagrams (both directions) live at the front of one
+            # of two device arenas, the next batch is appended behind them
+            self._arena = [torch.empty(cap_frames, dtype=torch.uint8, device=self._device) for _ in range(2)]
+            self._cur = 0
+            self._hist_len = np.zeros(0, np.int64)  # their lengths (host): every offset is known here
+            self._d_dup = torch.empty(MAX_MEMORY + max_msgs, dtype=torch.uint8, device=self._device)
+            self._d_acc = torch.zeros(2, dtype=torch.int64, device=self._device)  # client, server
+            # pinned staging of each batch's offsets and sides, reused after its copy has run
+            self._pin = [(torch.empty(MAX_MEMORY + max_msgs + 1, dtype=torch.int64, pin_memory=True),
+                          torch.empty(max_msgs, dtype=torch.int64, pin_memory=True), None) for _ in range(4)]
+            self._pin_i = 0
+
+    @property
+    def stats(self) -> Dict[str, int]:
+        """proxy.py's live_stats counters.  Batched: the GPU's retransmission counts
+        are folded in here (one synchronization with the relay's stream)."""
+        if self.batched:
+            self._stream.synchronize()
+            acc = self._d_acc.cpu().tolist()
+            return {**self._stats, "client_retransmitted": acc[0], "server_retransmitted": acc[1]}
+        return dict(self._stats)
 
     @property
     def retransmitted(self) -> int:
-        return self.stats["client_retransmitted"] + self.stats["server_retransmitted"]
+        st = self.stats
+        return st["client_retransmitted"] + st["server_retransmitted"]
 
     def _record(self, source: str, data: bytes, dropped: bool) -> None:
         # proxy.py:79-94
         other = "client" if source == "server" else "server"
         key = data if data else bytes(5)  # Packet(b"") is the 40-bit zero header
-        self.stats[f"{source}_sent"] += 1
-        self.stats[f"{source}_dropped" if dropped else f"{other}_received"] += 1
+        self._stats[f"{source}_sent"] += 1
+        self._stats[f"{source}_dropped" if dropped else f"{other}_received"] += 1
         if self._seen[key]:
-            self.stats[f"{source}_retransmitted"] += 1
+            self._stats[f"{source}_retransmitted"] += 1
         self._history.append(key)
         self._seen[key] += 1
         if len(self._history) > MAX_MEMORY:
             old = self._history.popleft()
             self._seen[old] -= 1
 
-    def _dup_flags(self, frames: np.ndarray, off: np.ndarray) -> np.ndarray:
-        """Retransmission flags of a batch (frames[off[i]:off[i+1]], i < k) against the
-        carried history and the batch's own earlier datagrams: one GPU launch of the
-        proxy's `Packet(data) in self.packets` (proxy.py:90), window MAX_MEMORY."""
+    def _count_retransmissions(self, stage, off: np.ndarray, from_server: np.ndarray) -> None:
+        """Enqueue the batch's retransmission check (the proxy's `Packet(data) in
+        self.packets`, proxy.py:90, window MAX_MEMORY) on the relay's stream:
+        ``stage(dst, stream)`` puts the batch's packed frames into ``dst`` on the
+        device.  One rudp_dedup_window launch over the carried history and the
+        batch, its flags summed per side into the device counters, the history's
+        new tail copied to the other arena.  Nothing here waits for the device."""
         import torch
         from . import batch
         k = off.shape[0] - 1
-        h = self._hist_off.shape[0] - 1
-        body = frames[off[0]:off[k]]
-        # one spare byte keeps the buffer non-empty when every datagram is empty
-        allf = np.concatenate([self._hist_frames, body, np.zeros(1, np.uint8)])
-        allo = np.concatenate([self._hist_off, self._hist_off[-1] + (off[1:] - off[0])])
-        d_frames = torch.from_numpy(allf).to(self._device)
-        d_off = torch.from_numpy(allo).to(self._device)
-        dup = batch.detect_retransmissions(d_frames, frame_off=d_off, window=MAX_MEMORY).cpu().numpy()[h:]
-        # carry the last MAX_MEMORY datagrams into the next batch
-        keep = min(MAX_MEMORY, h + k)
-        first = h + k - keep
-        self._hist_frames = allf[allo[first]:allo[-1]].copy()
-        self._hist_off = allo[first:] - allo[first]
-        return dup.astype(bool)
+        h = self._hist_len.shape[0]
+        lens = np.diff(off)
+        allen = np.concatenate([self._hist_len, lens])
+        allo = np.concatenate([[0], np.cumsum(allen)]).astype(np.int64)
+        hb = int(allo[h])
+        po, ps, ev = self._pin[self._pin_i]
+        if ev is not None:
+            ev.synchronize()  # this staging slot's last copies have run (four batches ago)
+        po[:h + k + 1].numpy()[:] = allo
+        ps[:k].numpy()[:] = from_server
+        s = self._stream
+        arena = self._arena[self._cur]
+        with torch.cuda.stream(s):
+            stage(arena[hb:], s)
+            d_off = po[:h + k + 1].to(self._device, non_blocking=True)
+            d_side = ps[:k].to(self._device, non_blocking=True)
+            ev = torch.cuda.Event()
+            ev.record(s)
+            self._pin[self._pin_i] = (po, ps, ev)
+            self._pin_i = (self._pin_i + 1) % len(self._pin)
+            # (one spare byte keeps the frames buffer non-empty when every datagram is empty)
+            dup = batch.detect_retransmissions(arena[:int(allo[-1]) + 1], frame_off=d_off, window=MAX_MEMORY,
+                                               stream=s, check=False)
+            self._d_acc.index_add_(0, d_side, dup[h:].to(torch.int64))
+            # carry the last MAX_MEMORY datagrams into the next batch, in the other arena
+            keep = min(MAX_MEMORY, h + k)
+            first = h + k - keep
+            nxt = self._arena[1 - self._cur]
+            nb = int(allo[-1] - allo[first])
+            if nb:
+                nxt[:nb].copy_(arena[int(allo[first]):int(allo[-1])])
+            for t in (d_off, d_side, dup):
+                t.record_stream(s)
+        self._cur = 1 - self._cur
+        self._hist_len = allen[first:].copy()
 
-    def _relay_batch(self, frames: np.ndarray, off: np.ndarray, src: np.ndarray) -> None:
-        """Record and forward one received batch (the per-datagram loop's work, batched)."""
+    def _relay_batch(self, frames: np.ndarray, off: np.ndarray, src: np.ndarray, rx=None, send_q=None) -> None:
+        """Record and forward one received batch (the per-datagram loop's work,
+        batched).  ``rx``: the BatchReceiver whose last batch this is (its pinned
+        slot is copied to the device asynchronously); else ``frames`` is copied
+        from wherever it lives.  ``send_q``: hand the sendmmsg to the forwarding
+        thread (holding rx's slot until it has run); else send here."""
         from . import netio
         k = off.shape[0] - 1
         from_server = src == self._server_key
@@ -148,34 +205,73 @@ class Relay(threading.Thread):
         if n_s < k:
             self._client_key = int(src[pos.max()])
             self.client = netio.key_addr(self._client_key)
-        dup = self._dup_flags(frames, off)
-        # proxy.py:79-94, summed over the batch
+        if rx is not None:
+            stage = lambda dst, s: rx.copy_frames_to(dst, s)  # noqa: E731
+        else:
+            def stage(dst, s):
+                import torch
+                body = np.ascontiguousarray(frames[off[0]:off[k]])
+                if body.size:  # a pageable source: torch stages it (the host waits for the copy)
+                    dst[:body.size].copy_(torch.from_numpy(body), non_blocking=True)
+        self._count_retransmissions(stage, off - off[0], from_server.astype(np.int64))
+        # proxy.py:79-94 (retransmissions: on the device, _count_retransmissions)
         for side, m in (("server", from_server), ("client", ~from_server)):
             other = "client" if side == "server" else "server"
-            self.stats[f"{side}_sent"] += int(m.sum())
-            self.stats[f"{side}_dropped"] += int((m & dropped).sum())
-            self.stats[f"{other}_received"] += int((m & ~dropped).sum())
-            self.stats[f"{side}_retransmitted"] += int((m & dup).sum())
+            self._stats[f"{side}_sent"] += int(m.sum())
+            self._stats[f"{side}_dropped"] += int((m & dropped).sum())
+            self._stats[f"{other}_received"] += int((m & ~dropped).sum())
         # a server datagram before any client one has nowhere to go (dst 0: not sent)
         send = ~dropped & (dst != 0)
-        if send.any():
+        if send.all():
+            out, out_off, out_dst = frames, off - off[0] if off[0] else off, dst
+        elif send.any():
             lens = np.diff(off)
             body = frames[off[0]:off[k]]
             out = body[np.repeat(send, lens)] if body.size else body
             out_off = np.concatenate([[0], np.cumsum(lens[send])]).astype(np.int64)
-            netio.send_batch_to(self.sock, out, out_off, dst[send])
+            out_dst = dst[send]
+        else:
+            out = None
+        if out is not None:
+            if send_q is not None:
+                send_q.put((out, out_off, out_dst, rx.hold() if rx is not None else None))
+            else:
+                netio.send_batch_to(self.sock, out, out_off, out_dst)
         self.batches += 1
 
-    def _run_batched(self) -> None:
+    def _forward(self, q, rx) -> None:
+        """The forwarding thread: sendmmsg each batch handed over, in order, then
+        give its receive slot back."""
         from . import netio
-        frames = np.empty(self._max_msgs * SLOT_BYTES, np.uint8)
-        off = np.empty(self._max_msgs + 1, np.int64)
-        src = np.empty(self._max_msgs, np.uint64)
-        while not self.stop_event.is_set():
-            k = netio.recv_batch(self.sock, frames, off, slot_bytes=SLOT_BYTES, max_msgs=self._max_msgs,
-                                 timeout_ms=50, sources=src)
-            if k:
-                self._relay_batch(frames, off[:k + 1], src[:k])
+        while True:
+            item = q.get()
+            if item is None:
+                return
+            out, out_off, out_dst, slot = item
+            try:
+                netio.send_batch_to(self.sock, out, out_off, out_dst)
+            except OSError:
+                pass  # the socket closed under a stopping relay
+            finally:
+                if slot is not None:
+                    rx.release(slot)
+
+    def _run_batched(self) -> None:
+        import queue
+        from . import netio
+        rx = netio.BatchReceiver(self.sock, max_msgs=self._max_msgs, slot_bytes=SLOT_BYTES, slots=4,
+                                 device=self._device, stream=self._stream, with_sources=True)
+        q: "queue.Queue" = queue.Queue()
+        fwd = threading.Thread(target=self._forward, args=(q, rx), daemon=True)
+        fwd.start()
+        try:
+            while not self.stop_event.is_set():
+                k = rx.recv(timeout_ms=50)
+                if k:
+                    self._relay_batch(rx.frames, rx.frame_off[:k + 1], rx.sources, rx=rx, send_q=q)
+        finally:
+            q.put(None)
+            fwd.join()
 
     def run(self) -> None:
         if self.batched:

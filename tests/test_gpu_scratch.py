@@ -1,0 +1,139 @@
+"""Call temporaries (scan sums, tile records, dedup hashes, offset-check
+partials) kept per (device, stream) by librudp, not per host thread.
+
+The reference proxy parses datagrams on ThreadPoolExecutor workers
+(proxy.py:127, :154); a caller with short-lived threads, or one that makes a
+stream per call, must not grow the library's device footprint.  Measured
+through the diagnostics build's rudpx_scratch_stats (its pool's
+hipMemPoolAttrUsedMemCurrent and the number of scratch sets).
+"""
+import ctypes
+import threading
+
+import numpy as np
+import pytest
+
+from oracle import codec_np, synth
+from rudp import _native, batch
+
+pytestmark = pytest.mark.gpu
+
+
+def _stats(lib):
+    out = (ctypes.c_uint64 * 2)()
+    _native.check(lib.rudpx_scratch_stats(0, out))
+    return int(out[0]), int(out[1])
+
+
+def _work(cuda, n, seed, own_stream, errors):
+    """One request's worth: varlen encode (scan + tiles), decode, dedup; checked."""
+    import torch
+    try:
+        s = torch.cuda.Stream(device=cuda) if own_stream else torch.cuda.current_stream(cuda)
+        rng = np.random.default_rng(seed)
+        lens = rng.integers(0, 300 if seed % 2 else 3, n).astype(np.int32)
+        pay = rng.integers(0, 128, int(lens.sum()), dtype=np.uint8)
+        seq, ack, flags, _ = synth.synth(seed, 0, n, 0)
+        with torch.cuda.stream(s):
+            tab = tuple(torch.from_numpy(a).to(cuda) for a in (seq, ack, flags))
+            res = batch.pack_batch_varlen(tab, torch.from_numpy(pay).to(cuda),
+                                          torch.from_numpy(lens).to(cuda), "rudp7")
+            dec = batch.unpack_batch_varlen(res.frames, res.frame_off, "rudp7", utf8=True)
+            dup = batch.detect_retransmissions(res.frames, frame_off=res.frame_off, window=500)
+            s.synchronize()
+        pays = [bytes(pay[o:o + k]) for o, k in zip(np.concatenate([[0], np.cumsum(lens)[:-1]]), lens)]
+        want, off, _ = codec_np.encode_varlen(seq, ack, flags, pays, 7)
+        assert np.array_equal(res.frames.cpu().numpy(), want)
+        assert bool((dec.ok == 1).all()) and bool((dec.valid == 1).all())
+        assert int(dup.sum().item()) >= 0
+    except BaseException as e:  # noqa: BLE001 -- reported by the main thread
+        errors.append(e)
+
+
+def _wave(cuda, k, n, base_seed):
+    errors = []
+    threads = [threading.Thread(target=_work, args=(cuda, n, base_seed + i, i % 4 == 0, errors))
+               for i in range(k)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    if errors:
+        raise errors[0]
+
+
+def test_short_lived_threads_keep_footprint_bounded(cuda):
+    """Two waves of 64 short-lived threads (a quarter on streams of their own):
+    every result correct, and the second wave adds no memory and no sets."""
+    import torch
+    lib = _native.tools_lib()
+    _wave(cuda, 64, 3000, 1000)
+    torch.cuda.synchronize()
+    used1, sets1 = _stats(lib)
+    _wave(cuda, 64, 3000, 2000)
+    torch.cuda.synchronize()
+    used2, sets2 = _stats(lib)
+    assert 0 < sets1 <= 64 and sets2 <= 64
+    # new streams may map onto released handles or new sets, never past the cap,
+    # and the pool does not grow by a thread's worth per thread
+    assert used2 <= used1 + 16 * (1 << 20), (used1, used2)
+
+
+def test_stream_per_call_is_capped(cuda):
+    """A caller that makes a fresh stream per call (80 live streams at once):
+    at most 64 scratch sets, results still exact (an evicted set is reused
+    only after the device is idle)."""
+    import torch
+    lib = _native.tools_lib()
+    n = 2000
+    seq, ack, flags, _ = synth.synth(5, 0, n, 0)
+    lens = np.full(n, 40, np.int32)
+    pay = np.random.default_rng(5).integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    want, off, _ = codec_np.encode_varlen(seq, ack, flags, [bytes(pay[40 * i:40 * i + 40]) for i in range(n)], 7)
+    tab = tuple(torch.from_numpy(a).to(cuda) for a in (seq, ack, flags))
+    d_pay, d_len = torch.from_numpy(pay).to(cuda), torch.from_numpy(lens).to(cuda)
+    streams = [torch.cuda.Stream(device=cuda) for _ in range(80)]
+    outs = []
+    for s in streams:
+        s.wait_stream(torch.cuda.current_stream(cuda))
+        with torch.cuda.stream(s):
+            outs.append(batch.pack_batch_varlen(tab, d_pay, d_len, "rudp7", check=False))
+    torch.cuda.synchronize()
+    for r in outs:
+        r.check()
+        assert np.array_equal(r.frames.cpu().numpy(), want)
+    assert _stats(lib)[1] <= 64
+
+
+def test_scratch_under_graph_capture(cuda):
+    """A varlen encode captured into a HIP graph allocates its temporaries inside
+    the capture; replays give the same frames, and eager calls on the capture
+    stream afterwards still do (no pointer the graph owns is cached)."""
+    import torch
+    n = 5000
+    rng = np.random.default_rng(77)
+    lens = rng.integers(0, 200, n).astype(np.int32)
+    pay = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    seq, ack, flags, _ = synth.synth(77, 0, n, 0)
+    pays = [bytes(pay[o:o + k]) for o, k in zip(np.concatenate([[0], np.cumsum(lens)[:-1]]), lens)]
+    want, _, _ = codec_np.encode_varlen(seq, ack, flags, pays, 7)
+    tab = tuple(torch.from_numpy(a).to(cuda) for a in (seq, ack, flags))
+    d_pay, d_len = torch.from_numpy(pay).to(cuda), torch.from_numpy(lens).to(cuda)
+    s = torch.cuda.Stream(device=cuda)
+    s.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(s):
+        warm = batch.pack_batch_varlen(tab, d_pay, d_len, "rudp7", check=False)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    with torch.cuda.graph(g, stream=s):
+        cap = batch.pack_batch_varlen(tab, d_pay, d_len, "rudp7", check=False)
+    for _ in range(3):
+        g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(cap.frames.cpu().numpy(), want)
+    with torch.cuda.stream(s):
+        again = batch.pack_batch_varlen(tab, d_pay, d_len, "rudp7", check=False)
+        g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(again.frames.cpu().numpy(), want)
+    assert np.array_equal(warm.frames.cpu().numpy(), want)

@@ -5,7 +5,9 @@ For every shape, each knob value's launches run in rotation (median of
 output is compared byte for byte with the first value's.
 
 shapes: encode:L (fixed-length, 1M x L, rotating sets below 1 GiB), varlen:L
-(packed, equal lengths), ragged (lengths uniform in [0, 2944]), decode:L.
+(packed, equal lengths), ragged (lengths uniform in [0, 2944]), decode:L,
+vdec:L (varlen decode, equal lengths; vdec:L+u with the UTF-8 check), rdec (varlen
+decode, ragged ASCII lengths; rdec:+u), dedup (1M one-character datagrams, window 500).
 
 usage: python tools/knob_ab.py --knob 58 --values 0,1 --shapes encode:1472,encode:64,varlen:1472,ragged
        python tools/knob_ab.py --variants "base:;t256b512:2=256,10=512" --shapes encode:64
@@ -50,6 +52,30 @@ def make_shape(spec, dev):
             return batch.unpack_batch(fr, 7).ok
         return run
     g = torch.Generator(device=dev).manual_seed(0x5EED0004)
+    if kind == "dedup":  # the proxy's check over 1M one-character rudp5 datagrams, window 500
+        tab, pay = batch.synth_batch(n, 1, 0x5EED0004, device=dev)
+        res = batch.pack_batch_varlen(tab, pay.view(-1), torch.ones(n, dtype=torch.int32, device=dev), 5)
+
+        def run():
+            return batch.detect_retransmissions(res.frames, frame_off=res.frame_off, window=500, check=False)
+        return run
+    if kind in ("vdec", "rdec"):  # varlen decode (vdec:L equal lengths, rdec: lengths uniform in [0, 2944])
+        if kind == "vdec":
+            L = int(arg.split("+")[0])
+            tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
+            flat, lens = pay.view(-1), torch.full((n,), L, dtype=torch.int32, device=dev)
+        else:
+            lens = torch.randint(0, 2945, (n,), dtype=torch.int32, device=dev, generator=g)
+            tab, _ = batch.synth_batch(n, 0, 0x5EED0004, device=dev)
+            flat = torch.randint(0, 128, (int(lens.sum().item()),), dtype=torch.uint8, device=dev, generator=g)
+        res = batch.pack_batch_varlen(tab, flat, lens, 7)
+        utf8 = spec.endswith("+u")
+        dec = batch.unpack_batch_varlen(res.frames, res.frame_off, 7, utf8=utf8)
+
+        def run():
+            batch.unpack_batch_varlen(res.frames, res.frame_off, 7, reuse=dec, check=False, utf8=utf8)
+            return dec._buf
+        return run
     if kind == "varlen":
         L = int(arg)
         tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)

@@ -1,9 +1,9 @@
-"""Turn tools/gpu/r03_prof2.sh's rocprofv3 output (gpurun_out/p2_*) into
-profiles/r03/<leg>_summary.json + _kernel_stats.csv (tools/prof_summary.py),
+"""Turn tools/gpu/profile_legs.sh's rocprofv3 output (gpurun_out/<prefix>_*) into
+profiles/<round>/<leg>_summary.json + _kernel_stats.csv (tools/prof_summary.py),
 one per timed bench leg, with the run's own HIP-event time per call beside
 the trace's per-dispatch median.
 
-usage: python tools/r03_summaries.py [--out gpurun_out]
+usage: python tools/leg_summaries.py --prefix p4 --round r04 [--out gpurun_out] [leg ...]
 """
 from __future__ import annotations
 
@@ -21,18 +21,23 @@ LEGS = {
     "enc1024": ("encode_1Mx1024", "encode_tile_kernel", 1 << 20, 1024, 2060),
     "enc64": ("encode_1Mx64", "encode_tile_kernel", 1 << 20, 64, 140),
     "dec1472": ("decode_verify_1Mx1472", "decode_tile_kernel", 1 << 20, 1472, 1485),
+    # parse + verify + strict UTF-8 in one pass: the valid flag is one more byte written
+    "decu8_1472": ("decode_utf8_1Mx1472", "decode_tile_kernel", 1 << 20, 1472, 1486),
     "enc16M": ("encode_16Mx1472", "encode_tile_kernel", 1 << 24, 1472, 2956),
     "venc1472": ("encode_varlen_1Mx1472", "scan_block_sums_kernel<8u>,scan_block_bases_kernel,scan_apply_kernel,"
                  "encode_varlen_tile_kernel", 1 << 20, 1472, 2968),
     "vdec1472": ("decode_varlen_1Mx1472", "decode_varlen_tile_kernel", 1 << 20, 1472, 1495),
+    "vdecu8_1472": ("decode_varlen_utf8_1Mx1472", "decode_varlen_tile_kernel", 1 << 20, 1472, 1496),
     "vencrag": ("encode_varlen_ragged_0_2944", "scan_block_sums_kernel<8u>,scan_block_bases_kernel,"
                 "scan_apply_kernel,encode_varlen_tile_kernel", 1 << 20, 1473, None),
     "vdecrag": ("decode_varlen_ragged_0_2944", "decode_varlen_tile_kernel", 1 << 20, 1473, None),
+    "vdecu8rag": ("decode_varlen_utf8_ragged_0_2944", "decode_varlen_tile_kernel", 1 << 20, 1473, None),
     "utf8": ("utf8_validate_1Mx1472", "validate_utf8_tile_kernel", 1 << 20, 1472, 1480),
-    "dedup": ("proxy_dedup_1M_window500", "dedup_hash_kernel,dedup_table_kernel", 1 << 20, 1, 15),
+    "dedup": ("proxy_dedup_1M_window500", "dedup_small_kernel", 1 << 20, 1, 15),
     "venc1c": ("encode_varlen_small_1Mx1char", "scan_block_sums_kernel<4u>,encode_varlen_small_kernel",
                1 << 20, 1, 26),
     "vdec1c": ("decode_varlen_small_1Mx1char", "decode_varlen_small_kernel", 1 << 20, 1, 24),
+    "vdecu8_1c": ("decode_varlen_utf8_small_1Mx1char", "decode_varlen_small_kernel", 1 << 20, 1, 25),
 }
 
 
@@ -47,20 +52,26 @@ def event_ms(log: Path):
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", type=Path, default=REPO / "gpurun_out")
+    ap.add_argument("--prefix", required=True)
+    ap.add_argument("--round", required=True)
+    ap.add_argument("legs", nargs="*")
     args = ap.parse_args()
     for tag, (name, kernels, n, L, per_unit) in LEGS.items():
-        kt = args.out / f"p2_{tag}_kt"
+        if args.legs and tag not in args.legs:
+            continue
+        P = args.prefix
+        kt = args.out / f"{P}_{tag}_kt"
         if not kt.exists():
             print(f"skip {tag}: no {kt}", file=sys.stderr)
             continue
-        ms, pay = event_ms(args.out / f"p2_{tag}_kt.log")
+        ms, pay = event_ms(args.out / f"{P}_{tag}_kt.log")
         if per_unit is None:  # ragged (mean 1473.1 B): as the equal-length legs, per the run's payload bytes
             # encode: read L + len 4 + table 5, write L + 7 + frame_off 8; decode: read L + 7 + frame_off 8,
             # write seq/ack/flags/ok/csum 8
-            per_unit = 2 * pay / n + 24 if tag.startswith("venc") else pay / n + 23
-        cmd = [sys.executable, str(REPO / "tools/prof_summary.py"), "--round", "r03", "--tag", name,
-               "--kt", str(kt), "--fetch", str(args.out / f"p2_{tag}_fetch"),
-               "--write", str(args.out / f"p2_{tag}_write"), "--kernel", kernels, "--n", str(n), "--L", str(L),
+            per_unit = 2 * pay / n + 24 if tag.startswith("venc") else pay / n + (24 if "u8" in tag else 23)
+        cmd = [sys.executable, str(REPO / "tools/prof_summary.py"), "--round", args.round, "--tag", name,
+               "--kt", str(kt), "--fetch", str(args.out / f"{P}_{tag}_fetch"),
+               "--write", str(args.out / f"{P}_{tag}_write"), "--kernel", kernels, "--n", str(n), "--L", str(L),
                "--alg-bytes-per-unit", str(per_unit)]
         if ms is not None:
             cmd += ["--event-ms", str(ms)]

@@ -37,6 +37,8 @@ def main():
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--ragged", action="store_true",
                     help="varlen ops: lengths uniform in [0, 2L] (mean L) instead of all L")
+    ap.add_argument("--utf8", action="store_true",
+                    help="decode ops: strict UTF-8 of each payload in the same pass (rudp_decode_utf8)")
     ap.add_argument("--tune", default="",
                     help="rudpx_tune knobs to set first, as key=value[,key=value...]")
     ap.add_argument("--gap-ms", type=float, default=0.0,
@@ -84,7 +86,7 @@ def main():
                 flat = pay.view(-1)
             res = batch.pack_batch_varlen(tab, flat, lens, "rudp5" if args.op == "dedup" else args.layout)
             dec = batch.unpack_batch_varlen(res.frames, res.frame_off, "rudp5" if args.op == "dedup" else args.layout,
-                                            csum=res.csum)
+                                            csum=res.csum, utf8=args.utf8)
             vsets.append((tab, flat, lens, res, dec))
 
     def step(i):
@@ -98,13 +100,13 @@ def main():
                 batch.detect_retransmissions(res.frames, frame_off=res.frame_off, window=500)
             else:
                 batch.unpack_batch_varlen(res.frames, res.frame_off, args.layout, csum=res.csum, reuse=dec,
-                                          check=False)
+                                          check=False, utf8=args.utf8)
             return
         tab, pay, fr = sets[i % nsets]
         if args.op in ("encode", "roundtrip"):
             batch.pack_batch(tab, pay, args.layout, out=fr, want_csum=False)
         if args.op in ("decode", "roundtrip"):
-            batch.unpack_batch(fr, args.layout)
+            batch.unpack_batch(fr, args.layout, utf8=args.utf8)
         if args.op == "decode_copy":
             decode_copy(tab, pay, fr)
         if args.op == "utf8":
@@ -133,7 +135,7 @@ def main():
     e.record()
     e.synchronize()
     payload_bytes = int(vsets[0][1].numel()) if vsets else args.n * args.L
-    print(json.dumps({"op": args.op, "L": args.L, "n": args.n, "layout": args.layout, "tune": args.tune,
+    print(json.dumps({"op": args.op, "utf8": args.utf8, "L": args.L, "n": args.n, "layout": args.layout, "tune": args.tune,
                       "ragged": args.ragged, "payload_bytes": payload_bytes,
                       "buffer_sets": nsets, "ms_per_launch": s.elapsed_time(e) / args.steps}))
 
