@@ -342,6 +342,26 @@ def legs(torch, batch, device, steps):
         "note": "rudp_decode_utf8: parse + verify + strict UTF-8 per frame in the decode tile kernel; "
                 "algorithmic bytes L + 7 read, 7 written; two_pass_ms = rudp_decode then rudp_validate_utf8"}
     del du
+    # the same on valid multi-byte text (every chunk takes the table check): a 1472-B
+    # payload of 1-4 byte characters, framed for every packet
+    text = ("é中😀aßЖ€𝄞" * 200).encode()[:1472]
+    while True:
+        try:
+            text.decode()
+            break
+        except UnicodeDecodeError:
+            text = text[:-1]
+    text += b"x" * (1472 - len(text))
+    row = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(device)
+    tab_t = w.sets[0][0]
+    fr_t = batch.pack_batch(tab_t, row.expand(1 << 20, 1472).contiguous(), "rudp7")[0]
+    ms_t = time_loop(torch, lambda i: batch.unpack_batch(fr_t, "rudp7", utf8=True), steps, 3) / steps
+    dt = batch.unpack_batch(fr_t, "rudp7", utf8=True)
+    out["decode_utf8_1Mx1472_multibyte_text"] = {
+        "ms": ms_t, "roofline_frac": (1 << 20) * (algorithmic_bytes_decode(1472) + 1) / (ms_t / 1e3) / 1e9
+        / HBM_PEAK_GBS, "all_valid_and_verified": bool((dt.valid == 1).all()) and bool((dt.ok == 1).all()),
+        "note": "payload: valid UTF-8 of 1-4 byte characters (no all-ASCII chunk), one frame buffer"}
+    del fr_t, dt, row
 
     def rt(i):
         w.encode(batch, i)
@@ -672,61 +692,91 @@ def socket_leg(torch, batch, device, n=1 << 20):
             "note": "loopback kernel UDP stack bound; sendmmsg/recvmmsg 1024 per call"}
 
 
-def relay_leg(torch, batch, device):
-    """Datagrams through rudp.relay.Relay in proxy.py's role (proxy.py:126-154):
-    a client blasts one-character frames (sendmmsg) at the relay, which forwards
-    them to a sink in the server's place; the sink counts what arrives.  Batched
-    relay over 256K datagrams, per-datagram relay over 32K; datagrams/s from the
-    first send to the last datagram at the sink, and the relay's counters (every
-    datagram distinct: no retransmissions).  Loopback UDP may drop under load;
-    the received counts say how many made it."""
+def relay_peer(peer_dir: str) -> None:
+    """The relay leg's client and server ends, in a process of their own (as
+    client.py and server.py are the reference's own processes around proxy.py):
+    bind a sink, report its port, read the relay's port, blast the frames in
+    4096-datagram sendmmsg bursts (at most 32K datagrams in flight) and count
+    what reaches the sink.  Prints one JSON line.  No GPU work."""
     import socket
     import threading
 
     import numpy as np
     from rudp import netio
+    frames = np.load(Path(peer_dir) / "frames.npy")
+    off = np.load(Path(peer_dir) / "off.npy")
+    n = off.shape[0] - 1
+    sink = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    sink.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 26)
+    sink.bind(("127.0.0.1", 0))
+    print(f"SINK {sink.getsockname()[1]}", flush=True)
+    relay_port = int(sys.stdin.readline().split()[1])
+    tx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
+    got = [0]
+    rbuf, roff = np.empty((1 << 16) * 64, np.uint8), np.empty((1 << 16) + 1, np.int64)
+
+    def drain():
+        while True:
+            k = netio.recv_batch(sink, rbuf, roff, slot_bytes=64, timeout_ms=500)
+            if k == 0:
+                break
+            got[0] += k
+    t = threading.Thread(target=drain)
+    t.start()
+    t0 = time.perf_counter()
+    for a in range(0, n, 4096):
+        while a - got[0] > 32768 and t.is_alive():
+            time.sleep(20e-6)
+        b = min(n, a + 4096)
+        netio.send_batch(tx, frames, off[a:b + 1], "127.0.0.1", relay_port)
+    t.join()
+    dt = time.perf_counter() - t0 - 0.5  # minus the sink's final idle timeout
+    print(json.dumps({"got": got[0], "wall_s": dt}), flush=True)
+
+
+def relay_leg(torch, batch, device):
+    """Datagrams through rudp.relay.Relay in proxy.py's role (proxy.py:126-154):
+    a client blasts one-character frames (sendmmsg) at the relay, which forwards
+    them to a sink in the server's place; the sink counts what arrives.  The
+    client and sink run in a child process (relay_peer), the relay here, as the
+    reference runs client.py, proxy.py and server.py as processes of their own.
+    Batched relay over 256K datagrams, per-datagram relay over 32K; datagrams/s
+    from the first send to the last datagram at the sink, and the relay's
+    counters (every datagram distinct: no retransmissions).  Loopback UDP may
+    drop under load; the received counts say how many made it."""
+    import socket
+    import subprocess
+    import tempfile
+
+    import numpy as np
     from rudp.relay import Relay
     out = {}
     for name, n, batched in (("batched", 1 << 18, True), ("per_datagram", 1 << 15, False)):
         tab, pay = batch.synth_batch(n, 1, SEEDS[1472], device=device)
         tab.seq.copy_(torch.arange(n, device=device).to(torch.int32).to(torch.uint16))  # distinct frames
         enc = batch.pack_batch_varlen(tab, pay.view(-1), torch.ones(n, dtype=torch.int32, device=device), "rudp5")
-        frames, off = enc.frames.cpu().numpy(), enc.frame_off.cpu().numpy()
-        sink = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
-        sink.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 26)
-        sink.bind(("127.0.0.1", 0))
-        relay = Relay(sink.getsockname()[1], batched=batched, device=device if batched else None, keep_log=False)
-        relay.sock.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 26)
-        relay.start()
-        tx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
-        got = [0]
-        rbuf, roff = np.empty((1 << 16) * 64, np.uint8), np.empty((1 << 16) + 1, np.int64)
-
-        def drain():
-            while True:
-                k = netio.recv_batch(sink, rbuf, roff, slot_bytes=64, timeout_ms=500)
-                if k == 0:
-                    break
-                got[0] += k
-        t = threading.Thread(target=drain)
-        t.start()
-        t0 = time.perf_counter()
-        for a in range(0, n, 4096):  # 4096-datagram bursts, at most 32K in flight
-            while a - got[0] > 32768 and t.is_alive():
-                time.sleep(20e-6)
-            b = min(n, a + 4096)
-            netio.send_batch(tx, frames, off[a:b + 1], "127.0.0.1", relay.port)
-        t.join()
-        dt = time.perf_counter() - t0 - 0.5  # minus the sink's final idle timeout
-        relay.stop()
-        tx.close()
-        sink.close()
-        out[name] = {"sent": n, "relayed_to_sink": got[0], "wall_s": dt, "Mpkt_s": got[0] / dt / 1e6,
-                     "relay_batches": relay.batches, "relay_stats": relay.stats}
-    out["note"] = ("client -> relay -> sink over loopback, 1-char frames in 4096-datagram sendmmsg bursts "
-                   "(at most 32K datagrams in flight); relay without its datagram log; "
-                   "batched: recvmmsg of up to 1024 with sources, one rudp_dedup_window launch per batch "
-                   "(500-deep history carried over), sendmmsg to per-datagram destinations")
+        with tempfile.TemporaryDirectory() as tmp:
+            np.save(Path(tmp) / "frames.npy", enc.frames.cpu().numpy())
+            np.save(Path(tmp) / "off.npy", enc.frame_off.cpu().numpy())
+            peer = subprocess.Popen([sys.executable, str(Path(__file__).resolve()), "--relay-peer", tmp],
+                                    stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True)
+            sink_port = int(peer.stdout.readline().split()[1])
+            relay = Relay(sink_port, batched=batched, device=device if batched else None, keep_log=False)
+            relay.sock.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 26)
+            relay.start()
+            peer.stdin.write(f"RELAY {relay.port}\n")
+            peer.stdin.flush()
+            res = json.loads(peer.stdout.readline())
+            peer.wait(timeout=60)
+            relay.stop()
+        out[name] = {"sent": n, "relayed_to_sink": res["got"], "wall_s": res["wall_s"],
+                     "Mpkt_s": res["got"] / res["wall_s"] / 1e6, "relay_batches": relay.batches,
+                     "relay_stats": relay.stats}
+    out["note"] = ("client + sink in a child process -> relay (this process) -> sink over loopback, 1-char "
+                   "frames in 4096-datagram sendmmsg bursts (at most 32K datagrams in flight); relay without "
+                   "its datagram log; batched: recvmmsg of up to 1024 with sources into a pinned ring, "
+                   "librudp's dedup stream (500-deep history on the device, no wait per batch), sendmmsg to "
+                   "per-datagram destinations on a forwarding thread")
     return out
 
 
@@ -804,7 +854,11 @@ def main():
                          "also at N = 1, so the RCCL branch runs on a one-GPU box")
     ap.add_argument("--c5-packets", type=int, default=0,
                     help="testing only: packets of the C5 strong leg (default 16M)")
+    ap.add_argument("--relay-peer", metavar="DIR", help=argparse.SUPPRESS)  # relay_leg's child process
     args = ap.parse_args()
+    if args.relay_peer:
+        relay_peer(args.relay_peer)
+        return
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))

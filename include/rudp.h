@@ -50,6 +50,15 @@
 
 #include <stdint.h>
 
+/* Every entry point is exported; librudp is built with hidden default
+ * visibility, so nothing else of it (kernels' host stubs, internal C++) can
+ * interpose on another library's symbols or be interposed on. */
+#if defined(__GNUC__)
+#define RUDP_API __attribute__((visibility("default")))
+#else
+#define RUDP_API
+#endif
+
 #ifdef __cplusplus
 extern "C" {
 #endif
@@ -124,7 +133,7 @@ typedef struct rudp_batch {
  * d_frames and payload are 16-byte aligned; any other shape runs a
  * byte-granular kernel with identical results.
  */
-int rudp_encode(const rudp_batch* in, uint8_t* d_frames, uint16_t* d_csum_or_null,
+RUDP_API int rudp_encode(const rudp_batch* in, uint8_t* d_frames, uint16_t* d_csum_or_null,
                 int layout, int device, void* hip_stream);
 
 /*
@@ -144,7 +153,7 @@ int rudp_encode(const rudp_batch* in, uint8_t* d_frames, uint16_t* d_csum_or_nul
  * Frames shorter than the header get d_ok = RUDP_OK_SHORT and the fields
  * that are present (truncated as utils/packet.py:31 slices them), 0 otherwise.
  */
-int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
+RUDP_API int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
                 uint32_t frame_len, uint64_t n, const uint16_t* d_csum_in_or_null,
                 uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags, uint8_t* d_ok,
                 uint16_t* d_csum_out_or_null, uint8_t* d_payload_out_or_null,
@@ -158,7 +167,7 @@ int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
  * bytes); d_frames must hold sum(len) + n*layout bytes.  The concatenated
  * frames equal N calls of Packet(...).to_byte() back to back.
  */
-int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_frame_off,
+RUDP_API int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_frame_off,
                        uint16_t* d_csum_or_null, int layout, int device, void* hip_stream);
 
 /*
@@ -183,15 +192,15 @@ int rudp_encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fram
  * rudp_frame_off_check: only the offset check, for callers that run their own
  *   kernels on the frames afterwards.
  */
-int rudp_encode_varlen_checked(const rudp_batch* in, uint64_t payload_bytes, uint8_t* d_frames,
+RUDP_API int rudp_encode_varlen_checked(const rudp_batch* in, uint64_t payload_bytes, uint8_t* d_frames,
                                uint64_t frames_cap, uint64_t* d_frame_off, uint16_t* d_csum_or_null,
                                uint32_t* d_status, int layout, int device, void* hip_stream);
-int rudp_decode_varlen_checked(const uint8_t* d_frames, uint64_t frames_bytes, const uint64_t* d_frame_off,
+RUDP_API int rudp_decode_varlen_checked(const uint8_t* d_frames, uint64_t frames_bytes, const uint64_t* d_frame_off,
                                uint32_t len_hint, uint64_t n, const uint16_t* d_csum_in_or_null,
                                uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags, uint8_t* d_ok,
                                uint16_t* d_csum_out_or_null, uint32_t* d_status, int layout, int device,
                                void* hip_stream);
-int rudp_frame_off_check(const uint64_t* d_frame_off, uint64_t n, uint64_t frames_bytes, uint32_t* d_status,
+RUDP_API int rudp_frame_off_check(const uint64_t* d_frame_off, uint64_t n, uint64_t frames_bytes, uint32_t* d_status,
                          int device, void* hip_stream);
 
 /*
@@ -209,12 +218,12 @@ int rudp_frame_off_check(const uint64_t* d_frame_off, uint64_t n, uint64_t frame
  * HBM once; other fixed-length shapes run the validation kernel after the
  * decode.  d_valid_or_null NULL: exactly rudp_decode / rudp_decode_varlen_checked.
  */
-int rudp_decode_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, uint32_t frame_len,
+RUDP_API int rudp_decode_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null, uint32_t frame_len,
                      uint64_t n, const uint16_t* d_csum_in_or_null, uint16_t* d_seq, uint16_t* d_ack,
                      uint8_t* d_flags, uint8_t* d_ok, uint16_t* d_csum_out_or_null,
                      uint8_t* d_payload_out_or_null, uint8_t* d_valid_or_null, int layout, int device,
                      void* hip_stream);
-int rudp_decode_varlen_utf8(const uint8_t* d_frames, uint64_t frames_bytes, const uint64_t* d_frame_off,
+RUDP_API int rudp_decode_varlen_utf8(const uint8_t* d_frames, uint64_t frames_bytes, const uint64_t* d_frame_off,
                             uint32_t len_hint, uint64_t n, const uint16_t* d_csum_in_or_null,
                             uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags, uint8_t* d_ok,
                             uint16_t* d_csum_out_or_null, uint8_t* d_valid_or_null, uint32_t* d_status,
@@ -231,9 +240,9 @@ int rudp_decode_varlen_utf8(const uint8_t* d_frames, uint64_t frames_bytes, cons
  * the number of i < n with d_frame_off[i+1] < d_frame_off[i] (0 = valid
  * offsets for rudp_decode; min and max are then the first and last).
  */
-int rudp_varlen_bounds(const uint32_t* d_len, const int64_t* d_payload_off_or_null, uint64_t n,
+RUDP_API int rudp_varlen_bounds(const uint32_t* d_len, const int64_t* d_payload_off_or_null, uint64_t n,
                        int64_t* h_out, int device, void* hip_stream);
-int rudp_frame_off_bounds(const int64_t* d_frame_off, uint64_t n, int64_t* h_out, int device,
+RUDP_API int rudp_frame_off_bounds(const int64_t* d_frame_off, uint64_t n, int64_t* h_out, int device,
                           void* hip_stream);
 
 /*
@@ -243,7 +252,7 @@ int rudp_frame_off_bounds(const int64_t* d_frame_off, uint64_t n, int64_t* h_out
  * UnicodeDecodeError.  Frames as in rudp_decode (fixed stride or offsets;
  * with offsets frame_len is a typical-length hint, as there).
  */
-int rudp_validate_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
+RUDP_API int rudp_validate_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
                        uint32_t frame_len, uint64_t n, int layout, uint8_t* d_valid, int device,
                        void* hip_stream);
 
@@ -258,7 +267,7 @@ int rudp_validate_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_n
  * Frames as in rudp_decode (fixed stride or n+1 offsets; with offsets
  * frame_len is a typical-length hint that picks lanes per frame).
  */
-int rudp_dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
+RUDP_API int rudp_dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
                       uint32_t frame_len, uint64_t n, uint32_t window, uint8_t* d_dup, int device,
                       void* hip_stream);
 
@@ -271,9 +280,32 @@ int rudp_dedup_window(const uint8_t* d_frames, const uint64_t* d_frame_off_or_nu
  * length (picks lanes per frame, never the result).
  */
 #define RUDP_DUP_BAD_OFFSETS 2
-int rudp_dedup_window_checked(const uint8_t* d_frames, uint64_t frames_bytes, const uint64_t* d_frame_off,
+RUDP_API int rudp_dedup_window_checked(const uint8_t* d_frames, uint64_t frames_bytes, const uint64_t* d_frame_off,
                               uint32_t len_hint, uint64_t n, uint32_t window, uint8_t* d_dup, int device,
                               void* hip_stream);
+
+/*
+ * The proxy's retransmission count over a datagram stream (ABI 6; proxy.py:79-94:
+ * every datagram is checked against the last Proxy.MAX_MEMORY = 500 of both
+ * directions, proxy.py:17, :90-94, and counted per side).  The history stays
+ * on the device between batches and nothing here waits for the GPU:
+ * rudp_dedup_stream_push copies a batch of host frames (packed, n + 1
+ * offsets; any host memory, the caller may reuse it once the call returns)
+ * behind the history, flags it with rudp_dedup_window_checked's rule, adds
+ * the flags to per-side counters (h_side_or_null[i] = 0 or 1; NULL: all 0),
+ * optionally copies the batch's flags to d_dup_or_null (n bytes, device), and
+ * keeps the last `window` datagrams, all on the stream given at creation.
+ * rudp_dedup_stream_counts synchronizes and returns the two counters.
+ * window <= 4096; a batch holds at most max_batch datagrams of at most
+ * max_frame bytes each.  One stream object per thread at a time.
+ */
+typedef struct rudp_dedup_stream rudp_dedup_stream;
+RUDP_API int rudp_dedup_stream_create(uint32_t window, uint32_t max_batch, uint32_t max_frame, int device,
+                                      void* hip_stream, rudp_dedup_stream** out);
+RUDP_API int rudp_dedup_stream_push(rudp_dedup_stream* st, const uint8_t* h_frames, const uint64_t* h_frame_off,
+                                    uint64_t n, const uint8_t* h_side_or_null, uint8_t* d_dup_or_null);
+RUDP_API int rudp_dedup_stream_counts(rudp_dedup_stream* st, uint64_t* h_counts);
+RUDP_API int rudp_dedup_stream_destroy(rudp_dedup_stream* st);
 
 /*
  * Batched UDP socket I/O (host only, no device work): the reference moves one
@@ -291,9 +323,9 @@ int rudp_dedup_window_checked(const uint8_t* d_frames, uint64_t frames_bytes, co
  * rudp_udp_send_batch: sends frames [h_frame_off[i], h_frame_off[i+1]) for
  * i < n to ip:port.  Returns the count sent or a negative errno.
  */
-int rudp_udp_recv_batch(int fd, uint8_t* h_frames, uint64_t cap_bytes, uint32_t slot_bytes,
+RUDP_API int rudp_udp_recv_batch(int fd, uint8_t* h_frames, uint64_t cap_bytes, uint32_t slot_bytes,
                         uint32_t max_msgs, uint64_t* h_frame_off, int timeout_ms);
-int rudp_udp_send_batch(int fd, const uint8_t* h_frames, const uint64_t* h_frame_off, uint64_t n,
+RUDP_API int rudp_udp_send_batch(int fd, const uint8_t* h_frames, const uint64_t* h_frame_off, uint64_t n,
                         const char* ip, uint16_t port);
 
 /*
@@ -305,10 +337,10 @@ int rudp_udp_send_batch(int fd, const uint8_t* h_frames, const uint64_t* h_frame
  * rudp_udp_send_batch_to: sends frame i to h_dst[i] (per_datagram != 0) or
  *   every frame to h_dst[0].  Returns the count sent or a negative errno.
  */
-int rudp_udp_recv_batch_from(int fd, uint8_t* h_frames, uint64_t cap_bytes, uint32_t slot_bytes,
+RUDP_API int rudp_udp_recv_batch_from(int fd, uint8_t* h_frames, uint64_t cap_bytes, uint32_t slot_bytes,
                              uint32_t max_msgs, uint64_t* h_frame_off, uint64_t* h_src_or_null,
                              int timeout_ms);
-int rudp_udp_send_batch_to(int fd, const uint8_t* h_frames, const uint64_t* h_frame_off, uint64_t n,
+RUDP_API int rudp_udp_send_batch_to(int fd, const uint8_t* h_frames, const uint64_t* h_frame_off, uint64_t n,
                            const uint64_t* h_dst, int per_datagram);
 
 /*
@@ -318,9 +350,9 @@ int rudp_udp_send_batch_to(int fd, const uint8_t* h_frames, const uint64_t* h_fr
  * real boundary, a UDP socket buffer in host memory (utils/reliableUDP.py:61,
  * :67, :118).
  */
-int rudp_encode_host(const rudp_batch* h_in, uint8_t* h_frames, uint16_t* h_csum_or_null,
+RUDP_API int rudp_encode_host(const rudp_batch* h_in, uint8_t* h_frames, uint16_t* h_csum_or_null,
                      int layout, int device);
-int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
+RUDP_API int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
                      const uint16_t* h_csum_in_or_null, uint16_t* h_seq, uint16_t* h_ack,
                      uint8_t* h_flags, uint8_t* h_ok, uint16_t* h_csum_out_or_null,
                      uint8_t* h_payload_out_or_null, int layout, int device);
@@ -333,13 +365,13 @@ int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
  *   payload bytes from splitmix64, masked to 0x00-0x7F when ascii != 0.
  * The same definition is restated on the CPU in oracle/synth.py.
  */
-int rudp_synth(uint64_t seed, uint64_t first_index, uint64_t n, uint32_t payload_len,
+RUDP_API int rudp_synth(uint64_t seed, uint64_t first_index, uint64_t n, uint32_t payload_len,
                int ascii, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
                uint8_t* d_payload, int device, void* hip_stream);
 
-int rudp_device_count(int* count);
-const char* rudp_last_error(void);
-int rudp_abi_version(void);
+RUDP_API int rudp_device_count(int* count);
+RUDP_API const char* rudp_last_error(void);
+RUDP_API int rudp_abi_version(void);
 
 #ifdef __cplusplus
 }

@@ -14,7 +14,7 @@
 #include "codec_device.hpp"
 #include "internal.hpp"
 
-namespace rudp {
+namespace RUDP_NS {
 
 constexpr uint32_t kBoundsBlocks = 256;
 

@@ -5,6 +5,7 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <deque>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -12,7 +13,7 @@
 #include "../../include/rudp.h"
 #include "internal.hpp"
 
-namespace rudp {
+namespace RUDP_NS {
 int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t len_hint, uint64_t n,
                   const uint16_t* d_csum_in, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
                   uint8_t* d_ok, uint16_t* d_csum_out, uint8_t* d_payload_out, int layout,
@@ -382,6 +383,8 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
   }
   a.early_fo = tuning().varlen_early_fo ? 1u : 0u;
   a.xcd = tuning().tile_xcd ? 1u : 0u;
+  // decode tile sums from 128-B block sums (the encode tile's scheme)
+  a.tile_sums = tuning().varlen_decode_blocks ? 2u : 0u;
   // Small frames (payload hint under varlen_small bytes): tiles of 256 * fpt
   // frames with the per-frame outputs lane-strided (decode_varlen_small_kernel).
   {
@@ -406,7 +409,7 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
 
 }  // namespace rudp
 
-using namespace rudp;
+using namespace RUDP_NS;
 
 extern "C" {
 
@@ -968,6 +971,195 @@ int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
     return 0;
   };
   return run_pipeline(pp, n, cn, h2d, kern, d2h);
+}
+
+// ---- the proxy's retransmission count over a stream of batches ----------------
+struct rudp_dedup_stream {
+  static constexpr int kStages = 4;
+  int device = 0;
+  hipStream_t stream = nullptr;
+  uint32_t window = 0, max_batch = 0, max_frame = 0;
+  uint8_t* arena[2] = {nullptr, nullptr};  // history, then the batch behind it; used in turn
+  int cur = 0;
+  uint64_t* d_off = nullptr;               // [window + max_batch + 1]
+  uint8_t* d_dup = nullptr;                // [window + max_batch]
+  uint8_t* d_side = nullptr;               // [max_batch]
+  uint64_t* d_counts = nullptr;            // [2]
+  struct Stage {                           // pinned staging of one push, reused after its copies ran
+    uint8_t* frames = nullptr;
+    uint64_t* off = nullptr;
+    uint8_t* side = nullptr;
+    uint64_t* counts = nullptr;
+    hipEvent_t done = nullptr;
+    bool used = false;
+  } stage[kStages];
+  int si = 0;
+  std::deque<uint32_t> hist;               // lengths of the kept datagrams (host: every offset is known here)
+  uint64_t hist_bytes = 0;
+};
+
+namespace {
+void dedup_stream_free(rudp_dedup_stream* st) {
+  if (!st) return;
+  if (st->stream) (void)hipStreamSynchronize(st->stream);
+  for (uint8_t* a : st->arena) (void)hipFree(a);
+  (void)hipFree(st->d_off);
+  (void)hipFree(st->d_dup);
+  (void)hipFree(st->d_side);
+  (void)hipFree(st->d_counts);
+  for (auto& g : st->stage) {
+    (void)hipHostFree(g.frames);
+    (void)hipHostFree(g.off);
+    (void)hipHostFree(g.side);
+    (void)hipHostFree(g.counts);
+    if (g.done) (void)hipEventDestroy(g.done);
+  }
+  delete st;
+}
+}  // namespace
+
+int rudp_dedup_stream_create(uint32_t window, uint32_t max_batch, uint32_t max_frame, int device, void* hip_stream,
+                             rudp_dedup_stream** out) {
+  if (!out) return fail(RUDP_EINVAL, "rudp_dedup_stream_create: out is NULL");
+  *out = nullptr;
+  if (window > dedup_max_window()) return fail(RUDP_EINVAL, "window %u exceeds %u", window, dedup_max_window());
+  if (max_batch == 0 || max_batch > (1u << 24) || max_frame > 65535u + 7u)
+    return fail(RUDP_EINVAL, "rudp_dedup_stream_create: max_batch in [1, 2^24], max_frame <= 65542");
+  DeviceScope dev_scope;
+  int rc = dev_scope.set(device);
+  if (rc) return rc;
+  rudp_dedup_stream* st = new rudp_dedup_stream();
+  st->device = device;
+  st->stream = (hipStream_t)hip_stream;
+  st->window = window;
+  st->max_batch = max_batch;
+  st->max_frame = max_frame;
+  const uint64_t entries = (uint64_t)window + max_batch;
+  const size_t arena = (size_t)(entries * (max_frame ? max_frame : 1u) + 16u);
+  const size_t batch_bytes = (size_t)max_batch * max_frame + 16u;
+  hipError_t e = hipSuccess;
+  for (auto& a : st->arena)
+    if (e == hipSuccess) e = hipMalloc(&a, arena);
+  if (e == hipSuccess) e = hipMalloc(&st->d_off, (entries + 1) * sizeof(uint64_t));
+  if (e == hipSuccess) e = hipMalloc(&st->d_dup, entries);
+  if (e == hipSuccess) e = hipMalloc(&st->d_side, max_batch);
+  if (e == hipSuccess) e = hipMalloc(&st->d_counts, 2 * sizeof(uint64_t));
+  if (e == hipSuccess) e = hipMemsetAsync(st->d_counts, 0, 2 * sizeof(uint64_t), st->stream);
+  for (auto& g : st->stage) {
+    if (e == hipSuccess) e = hipHostMalloc(&g.frames, batch_bytes, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc(&g.off, (entries + 1) * sizeof(uint64_t), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc(&g.side, max_batch, hipHostMallocDefault);
+    if (e == hipSuccess) e = hipHostMalloc(&g.counts, 2 * sizeof(uint64_t), hipHostMallocDefault);
+    if (e == hipSuccess) e = hipEventCreateWithFlags(&g.done, hipEventDisableTiming);
+  }
+  if (e != hipSuccess) {
+    dedup_stream_free(st);
+    return hip_fail(e, "rudp_dedup_stream_create");
+  }
+  *out = st;
+  return 0;
+}
+
+int rudp_dedup_stream_push(rudp_dedup_stream* st, const uint8_t* h_frames, const uint64_t* h_frame_off, uint64_t n,
+                           const uint8_t* h_side_or_null, uint8_t* d_dup_or_null) {
+  if (!st || (!h_frame_off && n)) return fail(RUDP_EINVAL, "rudp_dedup_stream_push: NULL argument");
+  if (n == 0) return 0;
+  if (n > st->max_batch) return fail(RUDP_EINVAL, "batch of %llu exceeds max_batch %u", (unsigned long long)n,
+                                     st->max_batch);
+  for (uint64_t i = 0; i < n; ++i)
+    if (h_frame_off[i + 1] < h_frame_off[i] || h_frame_off[i + 1] - h_frame_off[i] > st->max_frame)
+      return fail(RUDP_EINVAL, "rudp_dedup_stream_push: offsets decreasing or a frame over max_frame");
+  const uint64_t bb = h_frame_off[n] - h_frame_off[0];
+  if (bb && !h_frames) return fail(RUDP_EINVAL, "rudp_dedup_stream_push: frames is NULL");
+  DeviceScope dev_scope;
+  int rc = dev_scope.set(st->device);
+  if (rc) return rc;
+  hipStream_t s = st->stream;
+  auto& g = st->stage[st->si];
+  st->si = (st->si + 1) % rudp_dedup_stream::kStages;
+  if (g.used) RUDP_HIP(hipEventSynchronize(g.done));  // its copies (kStages pushes ago) have run
+  g.used = true;
+  // the history's offsets, then the batch's behind them, all known on the host
+  const uint64_t h = st->hist.size(), hb = st->hist_bytes;
+  uint64_t o = 0, k = 0;
+  for (const uint32_t len : st->hist) {
+    g.off[k++] = o;
+    o += len;
+  }
+  for (uint64_t i = 0; i <= n; ++i) g.off[h + i] = hb + (h_frame_off[i] - h_frame_off[0]);
+  if (bb) memcpy(g.frames, h_frames + h_frame_off[0], bb);
+  if (h_side_or_null) {
+    for (uint64_t i = 0; i < n; ++i) g.side[i] = h_side_or_null[i] ? 1 : 0;
+  }
+  uint8_t* arena = st->arena[st->cur];
+  if (bb) RUDP_HIP(hipMemcpyAsync(arena + hb, g.frames, bb, hipMemcpyHostToDevice, s));
+  RUDP_HIP(hipMemcpyAsync(st->d_off, g.off, (h + n + 1) * sizeof(uint64_t), hipMemcpyHostToDevice, s));
+  if (h_side_or_null) RUDP_HIP(hipMemcpyAsync(st->d_side, g.side, n, hipMemcpyHostToDevice, s));
+  RUDP_HIP(hipEventRecord(g.done, s));
+  // one dedup launch over history + batch (the checked rule; packed, 16-B aligned arena)
+  {
+    ScratchCall call(s);
+    DedupArgs a{};
+    a.frames = arena;
+    a.frame_off = st->d_off;
+    a.n = h + n;
+    a.window = st->window;
+    a.dup = st->d_dup;
+    const uint64_t total = hb + bb;
+    const uint32_t mean = (uint32_t)(total / (h + n));
+    a.F = mean;
+    a.glog = mean <= 16u ? 0u : mean <= 64u ? 1u : mean <= 256u ? 2u : 3u;
+    a.lim_checked = 1;
+    a.frames_lim = total;
+    a.small_cap = dedup_small_cap(mean, st->window);
+    if (!a.small_cap) {
+      void* scratch = nullptr;
+      RUDP_HIP(stream_scratch(&scratch, (h + n) * sizeof(uint64_t), s, kScratchHash));
+      a.hash = (uint64_t*)scratch;
+    }
+    rc = launch_dedup(a, s);
+    if (rc) return hip_fail((hipError_t)rc, "dedup launch");
+  }
+  rc = launch_dedup_count(st->d_dup + h, h_side_or_null ? st->d_side : nullptr, n, st->d_counts, s);
+  if (rc) return hip_fail((hipError_t)rc, "dedup count launch");
+  if (d_dup_or_null) RUDP_HIP(hipMemcpyAsync(d_dup_or_null, st->d_dup + h, n, hipMemcpyDeviceToDevice, s));
+  // keep the last `window` datagrams, at the front of the other arena
+  for (uint64_t i = 0; i < n; ++i) {
+    const uint32_t len = (uint32_t)(h_frame_off[i + 1] - h_frame_off[i]);
+    st->hist.push_back(len);
+    st->hist_bytes += len;
+  }
+  uint64_t first_off = 0;
+  while (st->hist.size() > st->window) {
+    first_off += st->hist.front();
+    st->hist_bytes -= st->hist.front();
+    st->hist.pop_front();
+  }
+  if (st->hist_bytes)
+    RUDP_HIP(hipMemcpyAsync(st->arena[1 - st->cur], arena + first_off, st->hist_bytes, hipMemcpyDeviceToDevice, s));
+  st->cur = 1 - st->cur;
+  return 0;
+}
+
+int rudp_dedup_stream_counts(rudp_dedup_stream* st, uint64_t* h_counts) {
+  if (!st || !h_counts) return fail(RUDP_EINVAL, "rudp_dedup_stream_counts: NULL argument");
+  DeviceScope dev_scope;
+  int rc = dev_scope.set(st->device);
+  if (rc) return rc;
+  uint64_t* pin = st->stage[0].counts;
+  RUDP_HIP(hipMemcpyAsync(pin, st->d_counts, 2 * sizeof(uint64_t), hipMemcpyDeviceToHost, st->stream));
+  RUDP_HIP(hipStreamSynchronize(st->stream));
+  h_counts[0] = pin[0];
+  h_counts[1] = pin[1];
+  return 0;
+}
+
+int rudp_dedup_stream_destroy(rudp_dedup_stream* st) {
+  if (!st) return 0;
+  DeviceScope dev_scope;
+  (void)dev_scope.set(st->device);
+  dedup_stream_free(st);
+  return 0;
 }
 
 }  // extern "C"

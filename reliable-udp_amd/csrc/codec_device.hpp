@@ -9,10 +9,20 @@
 // little-endian dword load gives for free, no byte swap anywhere.  The
 // header words are seq, ack and flags<<8 (the checksum field counts as 0).
 #pragma once
+// The diagnostics build (RUDP_TOOLS) puts every internal name in a namespace
+// of its own, so its kernels and functions (whose argument structs differ
+// from the product's) can never bind to the product library's in one process.
+#ifndef RUDP_NS
+#if defined(RUDP_TOOLS) && RUDP_TOOLS
+#define RUDP_NS rudp_tools
+#else
+#define RUDP_NS rudp
+#endif
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-namespace rudp {
+namespace RUDP_NS {
 
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
 

@@ -19,7 +19,7 @@
 #include "internal.hpp"
 #include "utf8_device.hpp"
 
-namespace rudp {
+namespace RUDP_NS {
 
 __device__ __forceinline__ u32x4 window16_global(const unsigned char* frames, uint64_t off,
                                                  uint64_t total) {

@@ -35,7 +35,7 @@
 #include "codec_device.hpp"
 #include "internal.hpp"
 
-namespace rudp {
+namespace RUDP_NS {
 
 constexpr uint32_t kDedupLanes = 8;
 constexpr uint32_t kMaxWindow = 4096;
@@ -379,6 +379,41 @@ int launch_dedup(const DedupArgs& args, hipStream_t stream) {
 }
 
 uint32_t dedup_max_window() { return kMaxWindow; }
+
+// Retransmission counts of a batch by side: counts[side[i]] += (dup[i] == 1)
+// (proxy.py:90-91: client_/server_retransmitted).  Per block in LDS, then one
+// atomic per side per block.
+__global__ void __launch_bounds__(kBlock) dedup_count_kernel(const uint8_t* dup, const uint8_t* side, uint64_t n,
+                                                             unsigned long long* counts) {
+  __shared__ unsigned int s_c[2];
+  if (threadIdx.x < 2) s_c[threadIdx.x] = 0;
+  __syncthreads();
+  unsigned int c0 = 0, c1 = 0;
+  for (uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x; i < n; i += (uint64_t)gridDim.x * kBlock) {
+    const unsigned int d = dup[i] == 1 ? 1u : 0u;
+    if (side && side[i]) c1 += d;
+    else c0 += d;
+  }
+  for (int m = 32; m > 0; m >>= 1) {
+    c0 += (unsigned int)__shfl_xor((int)c0, m, 64);
+    c1 += (unsigned int)__shfl_xor((int)c1, m, 64);
+  }
+  if ((threadIdx.x & 63u) == 0) {
+    if (c0) atomicAdd(&s_c[0], c0);
+    if (c1) atomicAdd(&s_c[1], c1);
+  }
+  __syncthreads();
+  if (threadIdx.x < 2 && s_c[threadIdx.x]) atomicAdd(&counts[threadIdx.x], (unsigned long long)s_c[threadIdx.x]);
+}
+
+int launch_dedup_count(const uint8_t* dup, const uint8_t* side, uint64_t n, uint64_t* counts, hipStream_t stream) {
+  if (n == 0) return 0;
+  uint64_t blocks = (n + kBlock - 1) / kBlock;
+  if (blocks > 1024) blocks = 1024;
+  hipLaunchKernelGGL(dedup_count_kernel, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, dup, side, n,
+                     reinterpret_cast<unsigned long long*>(counts));
+  return (int)hipGetLastError();
+}
 
 uint32_t dedup_small_cap(uint32_t mean_len, uint32_t window) {
   if (!tuning().dedup_small || !tuning().dedup_table || window > kDedupSmallWin || mean_len > kDedupSmallLen)

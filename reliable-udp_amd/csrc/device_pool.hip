@@ -13,7 +13,7 @@
 
 #include "internal.hpp"
 
-namespace rudp {
+namespace RUDP_NS {
 
 namespace {
 std::mutex g_pool_mu;

@@ -27,7 +27,7 @@
 #include "codec_device.hpp"
 #include "internal.hpp"
 
-namespace rudp {
+namespace RUDP_NS {
 
 constexpr int kLdsGuard = 16;  // bytes before the payload tile (negative offsets)
 

@@ -9,6 +9,16 @@
 //                     value a runtime knob), rudpx_encode_trace (tile timelines),
 //                     rudpx_stamp and the streaming-copy ceilings (tuning.hip).
 #pragma once
+// The diagnostics build (RUDP_TOOLS) puts every internal name in a namespace
+// of its own, so its kernels and functions (whose argument structs differ
+// from the product's) can never bind to the product library's in one process.
+#ifndef RUDP_NS
+#if defined(RUDP_TOOLS) && RUDP_TOOLS
+#define RUDP_NS rudp_tools
+#else
+#define RUDP_NS rudp
+#endif
+#endif
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -20,7 +30,7 @@
 #define RUDP_TOOLS 0
 #endif
 
-namespace rudp {
+namespace RUDP_NS {
 
 struct EncodeTileArgs {
   const unsigned char* payload;
@@ -279,7 +289,12 @@ struct Tuning {
   RUDP_KNOB(varlen_encode_cap_pct, 110)
   RUDP_KNOB(varlen_decode_tile, 1)  // varlen decode through LDS tiles for hints >= 128 B (2: any hint; 0: never)
   RUDP_KNOB(dedup_table, 1)    // dedup window pass by LDS hash table (0: every frame scans its window)
-  RUDP_KNOB(dedup_small, 1)    // packed small frames: dedup in one launch (dedup_small_kernel; 0: two passes)
+  RUDP_KNOB(dedup_small, 1)
+  // Varlen decode tile frame sums from 128-B block sums taken in phase 1 (the
+  // encode tile's scheme): lengths uniform in [0, 2944] 0.288 -> 0.278 ms, but
+  // equal 1472-B lengths 0.246 -> 0.268 (the block sums' DPP work sits in the
+  // streaming phase), so off (profiles/r04/sweeps/varlen_decode_blocks.json).
+  RUDP_KNOB(varlen_decode_blocks, 0)    // packed small frames: dedup in one launch (dedup_small_kernel; 0: two passes)
   RUDP_KNOB(utf8_tile, 1)
   // Packed-frame UTF-8 validation through LDS tiles (hints >= 128 B) and its
   // LDS budget in % of the hinted run: 1M x 1479 B ASCII frames 0.287 ->
@@ -365,6 +380,8 @@ uint32_t dedup_max_window();
 // The one-launch dedup's LDS run budget for packed frames of this mean length
 // and window, or 0 when the two-pass form is used.
 uint32_t dedup_small_cap(uint32_t mean_len, uint32_t window);
+// counts[side[i]] += (dup[i] == 1) for i < n (side null: all side 0), on `stream`.
+int launch_dedup_count(const uint8_t* dup, const uint8_t* side, uint64_t n, uint64_t* counts, hipStream_t stream);
 // Stream-ordered temporaries from a library-owned pool of the current device
 // that keeps its memory across synchronizes (device_pool.hip).
 hipError_t stream_alloc(void** ptr, size_t bytes, hipStream_t stream);

@@ -20,7 +20,7 @@
 #include "internal.hpp"
 #include "scan_device.hpp"
 
-namespace rudp {
+namespace RUDP_NS {
 
 constexpr uint32_t kScanItems = 8;                     // per thread
 constexpr uint32_t kScanBlockItems = kBlock * kScanItems;  // 2048 per block

@@ -4,7 +4,9 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
-namespace rudp {
+#include "codec_device.hpp"  // RUDP_NS
+
+namespace RUDP_NS {
 
 // Status bits of a block live above bit 56 of its pass-1 block sum (a sum of
 // at most 2048 x (2^32 - 1 + 7) fits in 44 bits); bits 44-55 hold the

@@ -14,7 +14,7 @@
 #include "codec_device.hpp"
 #include "internal.hpp"
 
-namespace rudp {
+namespace RUDP_NS {
 
 __device__ __forceinline__ uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;

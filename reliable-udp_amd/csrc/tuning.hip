@@ -9,7 +9,7 @@
 #include "internal.hpp"
 
 #if RUDP_TOOLS
-namespace rudp {
+namespace RUDP_NS {
 
 Tuning& tuning() {
   static Tuning t;
@@ -171,66 +171,66 @@ __global__ void stamp_kernel(uint64_t* dst) {
 extern "C" {
 
 // Persistent pipelined tiled copy (diagnostic): `blocks` workgroups.
-int rudpx_copy_tile_pipe(const void* src, void* dst, uint64_t n16, uint32_t tile16, uint32_t blocks,
+RUDP_API int rudpx_copy_tile_pipe(const void* src, void* dst, uint64_t n16, uint32_t tile16, uint32_t blocks,
                          uint32_t lds_bytes, void* stream) {
-  if (tile16 == 0 || tile16 > 8u * rudp::kBlock || blocks == 0) return -22;
+  if (tile16 == 0 || tile16 > 8u * RUDP_NS::kBlock || blocks == 0) return -22;
   size_t lds = (size_t)tile16 * 16;
   if (lds_bytes > lds) lds = lds_bytes;
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&rudp::copy_tile_pipe_kernel),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&RUDP_NS::copy_tile_pipe_kernel),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL(rudp::copy_tile_pipe_kernel, dim3(blocks), dim3(rudp::kBlock), lds,
-                     (hipStream_t)stream, (const rudp::u32x4*)src, (rudp::u32x4*)dst, n16, tile16);
+  hipLaunchKernelGGL(RUDP_NS::copy_tile_pipe_kernel, dim3(blocks), dim3(RUDP_NS::kBlock), lds,
+                     (hipStream_t)stream, (const RUDP_NS::u32x4*)src, (RUDP_NS::u32x4*)dst, n16, tile16);
   return (int)hipGetLastError();
 }
 
 // LDS-DMA tiled copy (diagnostic).  pipe = 0: one tile per block; pipe = 1:
 // `blocks` persistent blocks, double-buffered.  lds_bytes >= 2*tile16*16 sets occupancy.
-int rudpx_copy_tile_dma(const void* src, void* dst, uint64_t n16, uint32_t tile16, uint32_t blocks,
+RUDP_API int rudpx_copy_tile_dma(const void* src, void* dst, uint64_t n16, uint32_t tile16, uint32_t blocks,
                         uint32_t lds_bytes, int pipe, void* stream) {
   if (tile16 == 0 || tile16 > 4096u) return -22;
   const uint64_t ntiles = (n16 + tile16 - 1) / tile16;
   size_t lds = (size_t)tile16 * 16 * (pipe ? 2 : 1);
   if (lds_bytes > lds) lds = lds_bytes;
-  const void* fn = pipe ? reinterpret_cast<const void*>(&rudp::copy_tile_dma_kernel<true>)
-                        : reinterpret_cast<const void*>(&rudp::copy_tile_dma_kernel<false>);
+  const void* fn = pipe ? reinterpret_cast<const void*>(&RUDP_NS::copy_tile_dma_kernel<true>)
+                        : reinterpret_cast<const void*>(&RUDP_NS::copy_tile_dma_kernel<false>);
   if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
   const uint32_t grid = pipe ? (uint32_t)(blocks < ntiles ? blocks : ntiles) : (uint32_t)ntiles;
   if (pipe)
-    hipLaunchKernelGGL(rudp::copy_tile_dma_kernel<true>, dim3(grid), dim3(rudp::kBlock), lds,
-                       (hipStream_t)stream, (const rudp::u32x4*)src, (rudp::u32x4*)dst, n16, tile16);
+    hipLaunchKernelGGL(RUDP_NS::copy_tile_dma_kernel<true>, dim3(grid), dim3(RUDP_NS::kBlock), lds,
+                       (hipStream_t)stream, (const RUDP_NS::u32x4*)src, (RUDP_NS::u32x4*)dst, n16, tile16);
   else
-    hipLaunchKernelGGL(rudp::copy_tile_dma_kernel<false>, dim3(grid), dim3(rudp::kBlock), lds,
-                       (hipStream_t)stream, (const rudp::u32x4*)src, (rudp::u32x4*)dst, n16, tile16);
+    hipLaunchKernelGGL(RUDP_NS::copy_tile_dma_kernel<false>, dim3(grid), dim3(RUDP_NS::kBlock), lds,
+                       (hipStream_t)stream, (const RUDP_NS::u32x4*)src, (RUDP_NS::u32x4*)dst, n16, tile16);
   return (int)hipGetLastError();
 }
 
 // LDS-staged tile copy (diagnostic); lds_bytes >= tile16*16 sets occupancy.
-int rudpx_copy_tile(const void* src, void* dst, uint64_t n16, uint32_t tile16, uint32_t lds_bytes,
+RUDP_API int rudpx_copy_tile(const void* src, void* dst, uint64_t n16, uint32_t tile16, uint32_t lds_bytes,
                     void* stream) {
   const uint64_t blocks = (n16 + tile16 - 1) / tile16;
   size_t lds = (size_t)tile16 * 16;
   if (lds_bytes > lds) lds = lds_bytes;
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&rudp::copy_tile_kernel),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&RUDP_NS::copy_tile_kernel),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL(rudp::copy_tile_kernel, dim3((uint32_t)blocks), dim3(rudp::kBlock), lds,
-                     (hipStream_t)stream, (const rudp::u32x4*)src, (rudp::u32x4*)dst, n16, tile16);
+  hipLaunchKernelGGL(RUDP_NS::copy_tile_kernel, dim3((uint32_t)blocks), dim3(RUDP_NS::kBlock), lds,
+                     (hipStream_t)stream, (const RUDP_NS::u32x4*)src, (RUDP_NS::u32x4*)dst, n16, tile16);
   return (int)hipGetLastError();
 }
 
 // Copy with VPT (1, 2, 4, 8, 16) vectors per thread, loads before stores;
 // policy 1 = non-temporal, 0 = default.
-int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy, void* stream) {
+RUDP_API int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy, void* stream) {
   hipStream_t s = (hipStream_t)stream;
-  using namespace rudp;
+  using namespace RUDP_NS;
   switch (vpt * 2 + (policy ? 1 : 0)) {
     case 2: return launch_copy_vpt<1, 0>(src, dst, n16, s);
     case 3: return launch_copy_vpt<1, 1>(src, dst, n16, s);
@@ -275,7 +275,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // 50: small-frame encode finds its tile bases itself (no pass-2 launch);
 // 51: varlen byte tiles (0 never, 1 when the scan counts overflowing packet tiles, 2 always);
 // 52: varlen tile sum pass (2 from 128-B block sums, 0 chunk by chunk);
-// 62: packed small-frame dedup in one launch (dedup_small_kernel; 0: two passes).
+// 62: packed small-frame dedup in one launch (dedup_small_kernel; 0: two passes);
+// 63: varlen decode tile frame sums from 128-B block sums (0: chunk by chunk).
 // (54: chunked / rotated XCD orders, measured within 2% and removed;
 // profiles/r02/headline/xcd_orders.json.)
 // (55, 56: a small-tile launch tail, and 57: persistent workgroups looping over the tiles,
@@ -284,8 +285,8 @@ int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, int policy
 // (58: phase-2 LDS windows from aligned ds_read_b128 pairs: 20x fewer bank conflicts, same
 // kernel time; removed; profiles/r03/sq_counters_encode_tiles.json.)
 // Returns the old value.
-int rudpx_tune(int key, int value) {
-  rudp::Tuning& t = rudp::tuning();
+RUDP_API int rudpx_tune(int key, int value) {
+  RUDP_NS::Tuning& t = RUDP_NS::tuning();
   std::atomic<int>* slot = key == 0 ? &t.encode_nt_load : key == 1 ? &t.encode_nt_store
             : key == 2 ? &t.encode_tile : key == 3 ? &t.encode_p1
             : key == 4 ? &t.decode_glog : key == 5 ? &t.encode_xcd_swizzle
@@ -320,7 +321,8 @@ int rudpx_tune(int key, int value) {
             : key == 52 ? &t.varlen_tile_sums
             : key == 59 ? &t.varlen_span_bytes
             : key == 61 ? &t.varlen_diag
-            : key == 62 ? &t.dedup_small : nullptr;
+            : key == 62 ? &t.dedup_small
+            : key == 63 ? &t.varlen_decode_blocks : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }
@@ -329,30 +331,30 @@ int rudpx_tune(int key, int value) {
 // {start, end (100 MHz wall clock), XCC id, CU id, phase-1 loads landed, sums
 // done} as 6 u64 at buf[6 * tile], and every small-frame encode tile {start,
 // base known, end, XCC id} at buf[4 * tile].  Not thread-safe; tools only.
-int rudpx_encode_trace(uint64_t* buf) {
-  rudp::tuning().encode_trace.store(buf);
+RUDP_API int rudpx_encode_trace(uint64_t* buf) {
+  RUDP_NS::tuning().encode_trace.store(buf);
   return 0;
 }
 
 // Writes the wall clock at dst[0] (dst 16-B aligned) when the stream gets there.
-int rudpx_stamp(uint64_t* dst, void* stream) {
-  hipLaunchKernelGGL(rudp::stamp_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, dst);
+RUDP_API int rudpx_stamp(uint64_t* dst, void* stream) {
+  hipLaunchKernelGGL(RUDP_NS::stamp_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream, dst);
   return (int)hipGetLastError();
 }
 
 // Copy n16 16-byte vectors (both pointers 16-byte aligned) with `blocks` workgroups.
-int rudpx_copy(const void* src, void* dst, uint64_t n16, uint32_t blocks, void* stream) {
-  hipLaunchKernelGGL(rudp::copy_kernel, dim3(blocks), dim3(rudp::kBlock), 0, (hipStream_t)stream,
-                     (const rudp::u32x4*)src, (rudp::u32x4*)dst, n16);
+RUDP_API int rudpx_copy(const void* src, void* dst, uint64_t n16, uint32_t blocks, void* stream) {
+  hipLaunchKernelGGL(RUDP_NS::copy_kernel, dim3(blocks), dim3(RUDP_NS::kBlock), 0, (hipStream_t)stream,
+                     (const RUDP_NS::u32x4*)src, (RUDP_NS::u32x4*)dst, n16);
   return (int)hipGetLastError();
 }
 
 // The library's call-temporary footprint on `device`: out[0] = bytes in use in
 // its stream-ordered pool (hipMemPoolAttrUsedMemCurrent), out[1] = scratch
 // sets held (one per stream that made a call needing temporaries).
-int rudpx_scratch_stats(int device, uint64_t* out) {
-  out[1] = (uint64_t)rudp::scratch_sets(device);
-  return (int)rudp::pool_used_bytes(device, &out[0]);
+RUDP_API int rudpx_scratch_stats(int device, uint64_t* out) {
+  out[1] = (uint64_t)RUDP_NS::scratch_sets(device);
+  return (int)RUDP_NS::pool_used_bytes(device, &out[0]);
 }
 
 }  // extern "C"

@@ -19,7 +19,7 @@
 #pragma once
 #include "codec_device.hpp"
 
-namespace rudp {
+namespace RUDP_NS {
 
 __device__ __forceinline__ uint32_t utf8_need(uint32_t b) {  // continuation bytes a lead asks for
   return b >= 0xF0 ? 3u : b >= 0xE0 ? 2u : b >= 0xC0 ? 1u : 0u;
@@ -61,37 +61,69 @@ __device__ __forceinline__ uint32_t group_or(uint32_t bits, uint32_t G) {
   return bits;
 }
 
+// 16-entry byte table lookup for the four bytes of `idx` (each 0..15):
+// two v_perm_b32 over the table's halves, the half picked by bit 3.
+__device__ __forceinline__ uint32_t lookup16(uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3, uint32_t idx) {
+  const uint32_t sel = idx & 0x07070707u;
+  const uint32_t lo = __builtin_amdgcn_perm(t1, t0, sel), hi = __builtin_amdgcn_perm(t3, t2, sel);
+  const uint32_t b = idx & 0x08080808u;
+  const uint32_t m = (b << 5) - (b >> 3);  // 0xFF in every byte whose bit 3 is set (no multiply)
+  return (hi & m) | (lo & ~m);
+}
+
+// Bytes of `x` that are >= 0xE0 (p2 must be followed by two continuations) or,
+// for `four`, >= 0xF0: bit 7 of each such byte.
+__device__ __forceinline__ uint32_t at_least_e0(uint32_t x) { return x & (x << 1) & (x << 2) & 0x80808080u; }
+__device__ __forceinline__ uint32_t at_least_f0(uint32_t x) { return at_least_e0(x) & (x << 3); }
+
+// Error bits of four bytes `cur` given the four before them, `prev` (SWAR form
+// of the lookup validator of Keiser & Lemire, "Validating UTF-8 in less than
+// one instruction per byte"): every byte is checked against the byte before
+// it through three 16-entry tables of the nibbles (too short, too long,
+// overlong 2/3/4, surrogate, too large, two continuations), and against the
+// two and three before it for the continuations a 3- or 4-byte lead asks for.
+// Nonzero iff some byte of `cur` breaks strict UTF-8 given its predecessors.
+__device__ __forceinline__ uint32_t utf8_dword_errors(uint32_t cur, uint32_t prev) {
+  const uint32_t p1 = __builtin_amdgcn_alignbyte(cur, prev, 3);
+  const uint32_t p2 = __builtin_amdgcn_alignbyte(cur, prev, 2);
+  const uint32_t p3 = __builtin_amdgcn_alignbyte(cur, prev, 1);
+  // tables: byte 1's high nibble, byte 1's low nibble, byte 2's high nibble
+  // (bits: 0 too short, 1 too long, 2 overlong 3, 3 too large, 4 surrogate,
+  // 5 overlong 2, 6 too large 1000 / overlong 4, 7 two continuations)
+  const uint32_t sc = lookup16(0x02020202u, 0x02020202u, 0x80808080u, 0x49150121u, (p1 >> 4) & 0x0F0F0F0Fu) &
+                      lookup16(0x8383A3E7u, 0xCBCBCB8Bu, 0xCBCBCBCBu, 0xCBCBDBCBu, p1 & 0x0F0F0F0Fu) &
+                      lookup16(0x01010101u, 0x01010101u, 0xBABAAEE6u, 0x01010101u, (cur >> 4) & 0x0F0F0F0Fu);
+  const uint32_t must23 = at_least_e0(p2) | at_least_f0(p3);
+  return must23 ^ sc;
+}
+
 // Strict UTF-8 check of one frame's payload bytes [s, fe) by G lanes (lane g
 // takes aligned chunks c_lo + g, + G, ...): `chunk(c)` returns aligned chunk c
 // and `prev(x)` the dword of bytes x-4 .. x-1 (x a multiple of 16; only bytes
-// at or past s are used).  Returns nonzero if this lane saw an invalid byte.
+// at or past s are used).  Bytes outside [s, fe) count as 0 (ASCII): a
+// sequence cut by the payload's end then fails on the 0 after it, and a chunk
+// that ends the payload exactly checks what its last bytes still expect.  An
+// all-ASCII chunk with no lead byte just before it is valid outright.
+// Returns nonzero if this lane saw an invalid byte (it stops there).
 template <class Chunk, class Prev>
 __device__ __forceinline__ uint32_t utf8_check_frame(uint64_t s, uint64_t fe, uint32_t g, uint32_t G,
                                                      Chunk chunk, Prev prev_dw) {
   uint32_t bad = 0;
   if (fe <= s) return 0;
   const uint64_t c_lo = s >> 4, c_hi = (fe - 1u) >> 4;
-  for (uint64_t c = c_lo + g; c <= c_hi && !bad; c += G) {  // a lane stops at its first invalid byte
+  for (uint64_t c = c_lo + g; c <= c_hi && !bad; c += G) {  // a lane stops at its first invalid chunk
     const uint64_t x = c << 4;
-    const u32x4 v = chunk(c);
-    const uint32_t prev = prev_dw(x);
-    uint32_t p3 = x >= s + 3 ? (prev >> 8) & 0xFFu : 0u;
-    uint32_t p2 = x >= s + 2 ? (prev >> 16) & 0xFFu : 0u;
-    uint32_t p1 = x >= s + 1 ? prev >> 24 : 0u;
     const int lo_b = (int)((int64_t)s - (int64_t)x), hi_b = (int)((int64_t)fe - (int64_t)x);
-    if (!high_bits(keep_bytes(v, lo_b, hi_b)) && p1 < 0xC0 && p2 < 0xC0 && p3 < 0xC0) continue;
-#pragma unroll
-    for (int k = 0; k < 16; ++k) {
-      const uint64_t y = x + (uint64_t)k;
-      if (y < s || y >= fe) continue;
-      const uint32_t cb = byte_of(v, k);
-      bad |= utf8_byte_ok(cb, p1, p2, p3) ? 0u : 1u;
-      p3 = p2;
-      p2 = p1;
-      p1 = cb;
-    }
-    if (c == c_hi)  // the frame's last chunk: nothing may still be expected
-      bad |= utf8_pending(p1, p2, p3) ? 1u : 0u;
+    const u32x4 v = keep_bytes(chunk(c), lo_b, hi_b);
+    // the three bytes before the chunk that belong to the payload (bytes 1-3 of the dword)
+    const uint32_t prev = prev_dw(x) & (uint32_t)byte_mask(lo_b + 4, 4);
+    // ASCII, and no lead byte (11xxxxxx) just before: nothing to check
+    if (!high_bits(v) && !(prev & (prev << 1) & 0x80808000u)) continue;
+    uint32_t err = utf8_dword_errors(v.x, prev) | utf8_dword_errors(v.y, v.x) | utf8_dword_errors(v.z, v.y) |
+                   utf8_dword_errors(v.w, v.z);
+    if (c == c_hi && hi_b >= 16)  // the payload ends with this chunk: nothing may still be expected
+      err |= utf8_pending(v.w >> 24, (v.w >> 16) & 0xFFu, (v.w >> 8) & 0xFFu) ? 1u : 0u;
+    bad = err ? 1u : 0u;
   }
   return bad;
 }

@@ -15,6 +15,7 @@
 // kernels (16-byte aligned chunks, G lanes per packet from the caller's
 // mean-length hint) when the buffers are 16-byte aligned, byte-granular
 // kernels (8 lanes per packet) when not.  Numbers: DESIGN.md §3.
+#include <map>
 #include <mutex>
 #include <vector>
 
@@ -26,7 +27,7 @@
 #include <hipcub/hipcub.hpp>
 #endif
 
-namespace rudp {
+namespace RUDP_NS {
 
 constexpr uint32_t kVarLanes = 8;
 
@@ -881,6 +882,27 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_vec_kernel(VarlenArgs a)
 // does from HBM), and the leader parses the header from LDS.  A tile whose run
 // exceeds tile_cap (lengths far above the hint) decodes its frames with the
 // per-frame vector path inside the same launch.
+// Block sums (a.tile_sums == 2, the encode tile's scheme): phase 1 also takes
+// the even/odd byte sums of every whole 128-B block of the run from the
+// registers it streams through (and, U8, whether the block holds a high
+// bit), so a frame's G lanes read the 16 chunks of its two edge blocks and
+// one word per block between: work per frame nearly independent of its
+// length, where chunk by chunk a tile of ragged lengths waits for its longest
+// frame.
+__host__ __device__ inline uint32_t dvt_blk_off(uint32_t T, uint32_t cap) {
+  return (((((T + 1u) * 4u) + 15u) & ~15u) + kVTGuard + cap + 32u + 15u) & ~15u;
+}
+__host__ __device__ inline uint32_t dvt_lds_bytes(uint32_t T, uint32_t cap, bool blk) {
+  return blk ? dvt_blk_off(T, cap) + ((cap >> 7) + 4u) * 4u : ((((T + 1u) * 4u) + 15u) & ~15u) + kVTGuard + cap + 32u;
+}
+// OR over 8 consecutive lanes (all 8 active).
+__device__ __forceinline__ uint32_t octet_or(uint32_t x) {
+  x |= dpp_u32<0xB1>(x);
+  x |= dpp_u32<0x4E>(x);
+  x |= dpp_u32<0x141>(x);
+  return x;
+}
+
 template <int H, bool U8>
 __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
@@ -889,6 +911,8 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
   const uint32_t q = tid >> glog, g = tid & (G - 1u);
   uint32_t* lds_fo = reinterpret_cast<uint32_t*>(lds);                       // [T + 1]
   unsigned char* img = lds + ((((T + 1u) * 4u) + 15u) & ~15u) + kVTGuard;   // the run
+  const bool blk = a.tile_sums == 2u;
+  uint32_t* lds_blk = reinterpret_cast<uint32_t*>(lds + dvt_blk_off(T, a.tile_cap));  // [cap / 128 + 4]
   const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
@@ -920,6 +944,13 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
       for (uint32_t u = 0; u < P; ++u) {
         const uint32_t v = v0 + u * kBlock;
         if (v < nvec) dst[v] = r[u];
+        // block sums from the registers: whole 128-B blocks only (uniform per 8
+        // lanes; a partial last block is only ever an edge block of a frame)
+        if (blk && (v | 7u) < nvec) {
+          uint32_t eo = octet_sum(eo_sum(lo64(r[u]), hi64(r[u])));  // e, o at most 16320 each
+          if (U8 && octet_or(high_bits(r[u]))) eo |= 0x8000u;      // the block holds a high bit
+          if ((tid & 7u) == 0) lds_blk[v >> 3] = eo;
+        }
       }
     }
     if (a.early_fo) {
@@ -946,7 +977,27 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
   uint32_t even_sum = 0, odd_sum = 0;  // byte sums at even / odd offsets (A is even)
   uint32_t hib = 0;                     // U8: high bits of the payload bytes
   const uint32_t ps = fs + (uint32_t)H;
-  if (fe > ps) {  // the payload's chunks, the edge ones masked to it
+  if (blk && fe > ps) {
+    // the 16 chunks of the blocks holding the payload's first and last bytes
+    // (each masked to the payload), then the block words between
+    const uint32_t j0 = ps >> 7, j1 = (fe - 1u) >> 7;
+    for (uint32_t c = g; c < 16u; c += G) {
+      const uint32_t cx = ((c < 8u ? j0 : j1) << 7) + ((c & 7u) << 4);
+      if ((c < 8u || j1 != j0) && cx < fe && cx + 16u > ps) {
+        const u32x4 w = keep_bytes(img16[cx >> 4], (int)ps - (int)cx, (int)fe - (int)cx);
+        const uint32_t eo = eo_sum(lo64(w), hi64(w));
+        even_sum += eo & 0xFFFFu;
+        odd_sum += eo >> 16;
+        if (U8) hib |= w.x | w.y | w.z | w.w;
+      }
+    }
+    for (uint32_t j = j0 + 1u + g; j < j1; j += G) {
+      const uint32_t bs = lds_blk[j];
+      even_sum += bs & 0x7FFFu;
+      odd_sum += bs >> 16;
+      if (U8) hib |= (bs & 0x8000u) ? 0x80u : 0u;
+    }
+  } else if (fe > ps) {  // the payload's chunks, the edge ones masked to it
     const uint32_t c0 = ps >> 4, c1 = (fe - 1u) >> 4;
     for (uint32_t c = c0 + g; c <= c1; c += G) {
       u32x4 w = img16[c];
@@ -1518,7 +1569,7 @@ int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int
 // on its true offsets (the small-frame tile's frames whose offsets fall
 // outside its staged run; rare).
 template <int H, bool U8>
-__device__ __noinline__ void decode_varlen_frame_lane(const VarlenArgs& a, uint64_t p) {
+__device__ __forceinline__ void decode_varlen_frame_lane(const VarlenArgs& a, uint64_t p) {
   const uint64_t fo = a.frame_off[p], fe = a.frame_off[p + 1];
   if (fo > fe || fe > frames_limit(a)) {
     decode_varlen_reject(a, p);
@@ -1588,13 +1639,14 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_small_kernel(VarlenArgs 
   __syncthreads();
   const uint32_t* dw = reinterpret_cast<const uint32_t*>(img);
   const uint32_t lim = (uint32_t)(fo_end - A);
+  uint32_t fallback = 0;  // this lane's frames whose offsets leave the run (see the tile kernel)
 #pragma unroll
   for (uint32_t j = 0; j < FPT; ++j) {
     const uint32_t q = j * kBlock + tid;
     if (q >= Tv) continue;
     const uint32_t fs = s_fo[q], fe = s_fo[q + 1];
-    if (fs > fe || fe > lim) {  // out of order or outside the run: this lane, from HBM (see the tile kernel)
-      decode_varlen_frame_lane<H, U8>(a, p0 + q);
+    if (fs > fe || fe > lim) {  // out of order or outside the run: after the loop, from HBM
+      fallback |= 1u << j;
       continue;
     }
     uint32_t ev = 0, od = 0;  // byte sums at even / odd offsets (A is even)
@@ -1621,6 +1673,9 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_small_kernel(VarlenArgs 
     const uint32_t sum = (fs & 1u) ? (ev + (od << 8)) : ((ev << 8) + od);
     decode_varlen_finish<H>(a, p0 + q, fe - fs, sum, window16_dw(dw, fs));
   }
+#pragma unroll 1
+  for (uint32_t j = 0; j < FPT; ++j)  // one lane per such frame, straight from HBM (rare)
+    if (fallback & (1u << j)) decode_varlen_frame_lane<H, U8>(a, p0 + j * kBlock + tid);
 }
 
 template <int H, uint32_t FPT, bool U8>
@@ -1660,22 +1715,36 @@ static size_t varlen_tile_lds(uint32_t Tl, uint32_t cap, uint32_t H, uint32_t vh
 
 // Tiles of the varlen encode kernel (waves-per-SIMD floor W) one CU holds at
 // `lds` bytes of dynamic LDS, from the runtime's occupancy calculation (its LDS
-// allocation granule and limit, the kernel's registers), cached per size: a
-// byte count over 160 KiB misjudged it (1M x 1472 B byte tiles at 31.8 KB ran
-// 4 per CU, not 5).
+// allocation granule and limit, the kernel's registers), cached per (device,
+// size): a byte count over 160 KiB misjudged it (1M x 1472 B byte tiles at
+// 31.8 KB ran 4 per CU, not 5).  Every launch asks; a thread's last answer is
+// kept thread-locally, so only a new size takes the shared map's lock.
 template <int H, int W>
 static int vt_occupancy(size_t lds) {
+  int device = 0;
+  (void)hipGetDevice(&device);
+  const uint64_t key = ((uint64_t)(uint32_t)device << 40) | (uint64_t)lds;
+  thread_local uint64_t last_key = ~0ull;
+  thread_local int last_nb = 0;
+  if (key == last_key) return last_nb;
   static std::mutex mu;
-  static std::vector<std::pair<size_t, int>> cache;
-  std::lock_guard<std::mutex> lk(mu);
-  for (const auto& e : cache)
-    if (e.first == lds) return e.second;
-  const void* fn = reinterpret_cast<const void*>(&encode_varlen_tile_kernel<H, W>);
+  static std::map<uint64_t, int> cache;
   int nb = 0;
-  if (lds > 65536) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, (int)kBlock, lds) != hipSuccess || nb < 1)
-    nb = (int)((160u * 1024u) / lds);  // (no answer: the plain byte count)
-  cache.emplace_back(lds, nb);
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    const auto it = cache.find(key);
+    if (it != cache.end()) {
+      nb = it->second;
+    } else {
+      const void* fn = reinterpret_cast<const void*>(&encode_varlen_tile_kernel<H, W>);
+      if (lds > 65536) (void)hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+      if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, (int)kBlock, lds) != hipSuccess || nb < 1)
+        nb = (int)((160u * 1024u) / lds);  // (no answer: the plain byte count)
+      cache.emplace(key, nb);
+    }
+  }
+  last_key = key;
+  last_nb = nb;
   return nb;
 }
 
@@ -1821,7 +1890,7 @@ static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
     return launch_decode_small<H, U8>(args, stream);
   if (args.glog != kNoVec && args.tile_cap && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0) {
     const uint32_t T = kBlock >> args.glog;
-    const size_t lds = ((((T + 1u) * 4u) + 15u) & ~15u) + kVTGuard + args.tile_cap + 32u;
+    const size_t lds = dvt_lds_bytes(T, args.tile_cap, args.tile_sums == 2u);
     if (lds <= 65536) {
       const uint64_t blocks = (args.n + T - 1) / T;
       // 76 VGPRs (6 waves per SIMD).  Asking the allocator for 7 or 8 waves

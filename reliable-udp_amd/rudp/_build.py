@@ -47,15 +47,18 @@ def _newest_header() -> float:
 def _build_one(lib: Path, objdir: Path, defines, force: bool, verbose: bool, hipcc: str, hdr_time: float,
                pool: ThreadPoolExecutor):
     objdir.mkdir(parents=True, exist_ok=True)
+    # host code hidden by default: only the RUDP_API entry points leave the .so, so the
+    # product and diagnostics builds (same C++ names, different struct layouts) can
+    # never interpose on each other, even under RTLD_GLOBAL or a profiler's preload
     flags = [f"--offload-arch={ARCH}", "-O3", "-std=c++17", "-fPIC", "-Wall",
-             "-mcode-object-version=5", f"-I{INCLUDE}", *defines]
+             "-mcode-object-version=5", "-Xarch_host", "-fvisibility=hidden", f"-I{INCLUDE}", *defines]
 
     def compile_one(src: str) -> Path:
         s = CSRC / src
         o = objdir / (Path(src).stem + ".o")
         if force or not o.exists() or o.stat().st_mtime < max(s.stat().st_mtime, hdr_time):
             if s.suffix == ".cpp":  # host-only C++ (no HIP): plain g++
-                cmd = [shutil.which("g++") or "g++", "-O2", "-std=c++17", "-fPIC", "-Wall",
+                cmd = [shutil.which("g++") or "g++", "-O2", "-std=c++17", "-fPIC", "-Wall", "-fvisibility=hidden",
                        f"-I{INCLUDE}", *defines, "-c", str(s), "-o", str(o)]
             else:
                 cmd = [hipcc, *flags, "-c", str(s), "-o", str(o)]

@@ -39,6 +39,7 @@ EXPORTS = (
     "rudp_encode_varlen_checked", "rudp_decode_varlen_checked", "rudp_frame_off_check",
     "rudp_udp_recv_batch_from", "rudp_udp_send_batch_to", "rudp_dedup_window_checked",
     "rudp_decode_utf8", "rudp_decode_varlen_utf8",
+    "rudp_dedup_stream_create", "rudp_dedup_stream_push", "rudp_dedup_stream_counts", "rudp_dedup_stream_destroy",
 )
 
 
@@ -92,6 +93,10 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rudp_decode_utf8": [P, P, U32, U64, P, P, P, P, P, P, P, P, I, I, P],
         "rudp_decode_varlen_utf8": [P, U64, P, U32, U64, P, P, P, P, P, P, P, P, I, I, P],
         "rudp_frame_off_check": [P, U64, U64, P, I, P],
+        "rudp_dedup_stream_create": [U32, U32, U32, I, P, ctypes.POINTER(ctypes.c_void_p)],
+        "rudp_dedup_stream_push": [P, P, P, U64, P, P],
+        "rudp_dedup_stream_counts": [P, P],
+        "rudp_dedup_stream_destroy": [P],
         "rudp_device_count": [ctypes.POINTER(ctypes.c_int)],
         "rudp_abi_version": [],
     }

@@ -184,23 +184,6 @@ class BatchReceiver:
     def frame(self, i: int) -> bytes:
         return bytes(self.frames[self.frame_off[i]:self.frame_off[i + 1]])
 
-    def copy_frames_to(self, dst, stream=None) -> int:
-        """Enqueue the H2D copy of the last batch's packed frames into ``dst``
-        (a u8 device tensor with room for them) on ``stream`` (default: this
-        receiver's); the slot goes back to the socket only once it has run.
-        Returns the byte count.  (For callers that place the frames themselves,
-        e.g. behind a device-resident history: rudp.relay.)"""
-        import torch
-        s = stream if stream is not None else self.stream
-        k, n = self._slot, self.count
-        total = int(self._off_t[k][n])
-        if total:
-            with torch.cuda.stream(s):
-                dst[:total].copy_(self._frames_t[k][:total], non_blocking=True)
-                ev = torch.cuda.Event()
-                ev.record(s)
-                self._copied[k] = ev
-        return total
 
     def decode(self, layout="rudp5", device=None, csum=None, stream=None, check=False, utf8=False):
         """H2D of the received frames, then parse + verify them on the device.

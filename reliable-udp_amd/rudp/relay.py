@@ -22,18 +22,18 @@ and the datagrams that are not dropped leave in one sendmmsg with
 per-datagram destinations (rudp_udp_send_batch_to), on a forwarding thread
 of their own so the kernel's per-datagram send cost overlaps the next
 recvmmsg (the receive slot stays held until its datagrams are sent; one
-thread, so each direction keeps its order).  The retransmission flags
-of a batch come from one GPU launch of rudp_dedup_window over the last
-MAX_MEMORY datagrams of the earlier batches followed by this batch: the
-history stays on the device (two arenas used in turn, the kept tail copied
-device to device), every size it needs is known on the host, and the flags
-are summed into device counters, so the loop never waits for the GPU; the
-counters are read when ``stats`` is.  Forwarding does not depend on the flags
-(the proxy only counts retransmissions, proxy.py:90-91).  Same forwarding, log
-and counters as the per-datagram loop.
+thread, so each direction keeps its order).  The retransmission flags of a
+batch come from librudp's dedup stream (rudp_dedup_stream_push): one GPU
+launch of rudp_dedup_window's rule over the last MAX_MEMORY datagrams of the
+earlier batches followed by this batch, the history kept on the device, the
+flags summed into per-side device counters, all enqueued from C with no wait
+for the GPU; the counters are read when ``stats`` is.  Forwarding does not
+depend on the flags (the proxy only counts retransmissions, proxy.py:90-91).
+Same forwarding, log and counters as the per-datagram loop.
 """
 from __future__ import annotations
 
+import ctypes
 import socket
 import threading
 from collections import Counter, deque
@@ -84,27 +84,28 @@ class Relay(threading.Thread):
             self._server_key = addr_key(host, server_port)
             self._client_key = None
             self._stream = torch.cuda.Stream(self._device)
-            cap_frames = (MAX_MEMORY + max_msgs) * SLOT_BYTES + 16
-            # the last MAX_MEMORY datagrams (both directions) live at the front of one
-            # of two device arenas, the next batch is appended behind them
-            self._arena = [torch.empty(cap_frames, dtype=torch.uint8, device=self._device) for _ in range(2)]
-            self._cur = 0
-            self._hist_len = np.zeros(0, np.int64)  # their lengths (host): every offset is known here
-            self._d_dup = torch.empty(MAX_MEMORY + max_msgs, dtype=torch.uint8, device=self._device)
-            self._d_acc = torch.zeros(2, dtype=torch.int64, device=self._device)  # client, server
-            # pinned staging of each batch's offsets and sides, reused after its copy has run
-            self._pin = [(torch.empty(MAX_MEMORY + max_msgs + 1, dtype=torch.int64, pin_memory=True),
-                          torch.empty(max_msgs, dtype=torch.int64, pin_memory=True), None) for _ in range(4)]
-            self._pin_i = 0
+            from . import _native
+            h = ctypes.c_void_p()
+            _native.check(_native.lib().rudp_dedup_stream_create(
+                MAX_MEMORY, max_msgs, SLOT_BYTES, self._device.index or 0, self._stream.cuda_stream, ctypes.byref(h)))
+            self._dstream = h
+
+    def __del__(self):
+        h = getattr(self, "_dstream", None)
+        if h is not None and h.value:
+            from . import _native
+            _native.lib().rudp_dedup_stream_destroy(h)
+            self._dstream = None
 
     @property
     def stats(self) -> Dict[str, int]:
         """proxy.py's live_stats counters.  Batched: the GPU's retransmission counts
         are folded in here (one synchronization with the relay's stream)."""
         if self.batched:
-            self._stream.synchronize()
-            acc = self._d_acc.cpu().tolist()
-            return {**self._stats, "client_retransmitted": acc[0], "server_retransmitted": acc[1]}
+            from . import _native
+            acc = (ctypes.c_uint64 * 2)()
+            _native.check(_native.lib().rudp_dedup_stream_counts(self._dstream, acc))
+            return {**self._stats, "client_retransmitted": int(acc[0]), "server_retransmitted": int(acc[1])}
         return dict(self._stats)
 
     @property
@@ -126,51 +127,17 @@ class Relay(threading.Thread):
             old = self._history.popleft()
             self._seen[old] -= 1
 
-    def _count_retransmissions(self, stage, off: np.ndarray, from_server: np.ndarray) -> None:
+    def _count_retransmissions(self, frames: np.ndarray, off: np.ndarray, side: np.ndarray) -> None:
         """Enqueue the batch's retransmission check (the proxy's `Packet(data) in
-        self.packets`, proxy.py:90, window MAX_MEMORY) on the relay's stream:
-        ``stage(dst, stream)`` puts the batch's packed frames into ``dst`` on the
-        device.  One rudp_dedup_window launch over the carried history and the
-        batch, its flags summed per side into the device counters, the history's
-        new tail copied to the other arena.  Nothing here waits for the device."""
-        import torch
-        from . import batch
+        self.packets`, proxy.py:90, window MAX_MEMORY) and its per-side count
+        (side 1: from the server) through librudp's dedup stream; frames are
+        copied out of ``frames`` before the call returns, nothing waits for the GPU."""
+        from . import _native
         k = off.shape[0] - 1
-        h = self._hist_len.shape[0]
-        lens = np.diff(off)
-        allen = np.concatenate([self._hist_len, lens])
-        allo = np.concatenate([[0], np.cumsum(allen)]).astype(np.int64)
-        hb = int(allo[h])
-        po, ps, ev = self._pin[self._pin_i]
-        if ev is not None:
-            ev.synchronize()  # this staging slot's last copies have run (four batches ago)
-        po[:h + k + 1].numpy()[:] = allo
-        ps[:k].numpy()[:] = from_server
-        s = self._stream
-        arena = self._arena[self._cur]
-        with torch.cuda.stream(s):
-            stage(arena[hb:], s)
-            d_off = po[:h + k + 1].to(self._device, non_blocking=True)
-            d_side = ps[:k].to(self._device, non_blocking=True)
-            ev = torch.cuda.Event()
-            ev.record(s)
-            self._pin[self._pin_i] = (po, ps, ev)
-            self._pin_i = (self._pin_i + 1) % len(self._pin)
-            # (one spare byte keeps the frames buffer non-empty when every datagram is empty)
-            dup = batch.detect_retransmissions(arena[:int(allo[-1]) + 1], frame_off=d_off, window=MAX_MEMORY,
-                                               stream=s, check=False)
-            self._d_acc.index_add_(0, d_side, dup[h:].to(torch.int64))
-            # carry the last MAX_MEMORY datagrams into the next batch, in the other arena
-            keep = min(MAX_MEMORY, h + k)
-            first = h + k - keep
-            nxt = self._arena[1 - self._cur]
-            nb = int(allo[-1] - allo[first])
-            if nb:
-                nxt[:nb].copy_(arena[int(allo[first]):int(allo[-1])])
-            for t in (d_off, d_side, dup):
-                t.record_stream(s)
-        self._cur = 1 - self._cur
-        self._hist_len = allen[first:].copy()
+        off = np.ascontiguousarray(off, dtype=np.uint64)
+        side = np.ascontiguousarray(side, dtype=np.uint8)
+        _native.check(_native.lib().rudp_dedup_stream_push(
+            self._dstream, frames.ctypes.data if frames.size else None, off.ctypes.data, k, side.ctypes.data, None))
 
     def _relay_batch(self, frames: np.ndarray, off: np.ndarray, src: np.ndarray, rx=None, send_q=None) -> None:
         """Record and forward one received batch (the per-datagram loop's work,
@@ -205,15 +172,7 @@ class Relay(threading.Thread):
         if n_s < k:
             self._client_key = int(src[pos.max()])
             self.client = netio.key_addr(self._client_key)
-        if rx is not None:
-            stage = lambda dst, s: rx.copy_frames_to(dst, s)  # noqa: E731
-        else:
-            def stage(dst, s):
-                import torch
-                body = np.ascontiguousarray(frames[off[0]:off[k]])
-                if body.size:  # a pageable source: torch stages it (the host waits for the copy)
-                    dst[:body.size].copy_(torch.from_numpy(body), non_blocking=True)
-        self._count_retransmissions(stage, off - off[0], from_server.astype(np.int64))
+        self._count_retransmissions(frames, off, from_server)
         # proxy.py:79-94 (retransmissions: on the device, _count_retransmissions)
         for side, m in (("server", from_server), ("client", ~from_server)):
             other = "client" if side == "server" else "server"

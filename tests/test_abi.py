@@ -16,7 +16,7 @@ from rudp import batch
 
 def declared_functions():
     text = (REPO / "include" / "rudp.h").read_text()
-    return set(re.findall(r"^(?:int|const char\*)\s+(rudp_\w+)\s*\(", text, flags=re.M))
+    return set(re.findall(r"^RUDP_API\s+(?:int|const char\*)\s+(rudp_\w+)\s*\(", text, flags=re.M))
 
 
 def test_header_and_binding_agree():
@@ -43,6 +43,26 @@ def test_product_library_exports_only_the_abi():
     assert prod == declared_functions()
     tools = {s for s in _dynamic_symbols(_native.TOOLS_LIB_PATH) if s.startswith("rudpx_")}
     assert {"rudpx_tune", "rudpx_encode_trace", "rudpx_stamp", "rudpx_copy_vpt"} <= tools
+
+
+def test_internals_stay_inside_each_library():
+    """Both builds hide everything but their entry points; what the HIP runtime
+    needs exported (kernel handles) lives in a namespace per build (rudp::,
+    rudp_tools::), so the product and diagnostics libraries in one process can
+    never bind to each other's kernels or functions (their argument structs
+    differ), whatever the load flags."""
+    prod = _dynamic_symbols(_native.LIB_PATH)
+    tools = _dynamic_symbols(_native.TOOLS_LIB_PATH)
+    assert not any("rudp_tools" in s for s in prod)
+    assert not any(s.startswith("_ZN4rudp") and not s.startswith("_ZN10rudp_tools") for s in tools)
+    internal = {s for s in prod if s.startswith("_ZN4rudp")}
+    assert not (internal & tools)
+    # functions: the entry points only (no internal C++ function of librudp is exported)
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", str(_native.LIB_PATH)], capture_output=True, text=True,
+                         check=True).stdout
+    funcs = {ln.split()[-1] for ln in out.splitlines() if ln.split()[1:2] == ["T"]}
+    assert funcs == declared_functions()
 
 
 def test_batch_struct_layout():

@@ -333,3 +333,71 @@ def test_dedup_small_and_two_pass_forms_agree(cuda):
                                                        check=False))
                 assert g2[1000] == _native.DUP_BAD_OFFSETS and g2[-1] == _native.DUP_BAD_OFFSETS, (window, form)
                 assert int((g2 == _native.DUP_BAD_OFFSETS).sum()) == 2
+
+
+@pytest.mark.parametrize("H", [5, 7])
+def test_fused_multibyte_text_every_corruption_offset(cuda, H):
+    """Valid multi-byte text (2-, 3- and 4-byte characters across every 16-B
+    chunk boundary) takes the table check on every chunk: all valid; then one
+    byte per frame replaced at every payload offset, with bytes that make each
+    error class (stray continuation, truncated lead, overlong, surrogate, past
+    U+10FFFF): the answer equals Python's strict decoder, fixed-length tiles
+    and packed tiles alike."""
+    import torch
+    text = ("é中😀aßЖ€𝄞" * 200).encode()
+    L = 1472
+    body = text[:L]
+    while True:  # cut on a character boundary, pad with ASCII
+        try:
+            body.decode()
+            break
+        except UnicodeDecodeError:
+            body = body[:-1]
+    body = body + b"x" * (L - len(body))
+    subs = [0x80, 0xBF, 0xC0, 0xC1, 0xE0, 0xED, 0xF0, 0xF4, 0xF5, 0xFF, 0x41]
+    rows = [body]
+    for k in range(L):
+        b = bytearray(body)
+        b[k] = subs[k % len(subs)]
+        rows.append(bytes(b))
+    hdr = b"\x12\x34\x00\x00\x80" + (b"\xbe\xef" if H == 7 else b"")
+    fr = np.frombuffer(b"".join(hdr + r for r in rows), np.uint8).reshape(len(rows), L + H)
+    off = np.arange(len(rows) + 1, dtype=np.int64) * (L + H)
+    want = codec_np.utf8_valid(fr.reshape(-1), off, H)
+    assert want[0] == 1 and 0 < want.mean() < 1
+    got = batch.unpack_batch(dev(fr, cuda), H, utf8=True)
+    assert np.array_equal(host(got.valid), want)
+    for hint in (0, 200, 1600):
+        g = _varlen_decode(dev(fr.reshape(-1), cuda), fr.size, dev(off, cuda), len(rows), hint, H, True)
+        assert np.array_equal(g["valid"], want), hint
+    assert bool((batch.validate_utf8(dev(fr, cuda), H) == torch.from_numpy(want).to(cuda)).all())
+
+
+@pytest.mark.parametrize("blocks", [1, 0])
+def test_varlen_tile_block_sums_and_chunk_sums_agree(cuda, blocks):
+    """The varlen decode tile's two sum forms (128-B block sums from phase 1,
+    rudpx_tune 63 = 1, the default; chunk by chunk, 0) on ragged frames of
+    0-3000 B with near-UTF-8 bodies, the fused check on and off: equal to the
+    oracle's fields and Python's strict decoder."""
+    import ctypes
+    lib = _native.tools_lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    old = lib.rudpx_tune(63, blocks)
+    try:
+        rng = np.random.default_rng(63 + blocks)
+        for H in (5, 7):
+            hdr = b"\x12\x34\x00\x00\x80" + (b"\xbe\xef" if H == 7 else b"")
+            frames = []
+            for b in _near_utf8(rng, 3000):
+                L = int(rng.integers(0, 3000))
+                frames.append(hdr + ((b or b"A") * (L // max(1, len(b)) + 1))[:L])
+            flat, off = _pack(frames)
+            want = codec_np.decode_varlen(flat, off, H)
+            want_v = codec_np.utf8_valid(flat, off, H)
+            for hint in (200, 1600, 3000):
+                got = _varlen_decode(dev(flat, cuda), len(flat), dev(off, cuda), len(frames), hint, H, True)
+                for k, w in zip(("seq", "ack", "flags", "ok", "csum"), want):
+                    assert np.array_equal(got[k], w), (k, H, hint)
+                assert np.array_equal(got["valid"], want_v), (H, hint)
+    finally:
+        lib.rudpx_tune(63, old)
