@@ -702,7 +702,8 @@ def relay_peer(peer_dir: str) -> None:
     import threading
 
     import numpy as np
-    from rudp import netio
+    from rudp import _native, netio
+    _native.lib()  # load librudp (and torch, which it binds to) before any clock starts
     frames = np.load(Path(peer_dir) / "frames.npy")
     off = np.load(Path(peer_dir) / "off.npy")
     n = off.shape[0] - 1

@@ -6,7 +6,7 @@
 // fresh mapping: the Python varlen entry points sync once per call for their
 // bounds checks, and the 8 MB dedup scratch of a 1M-datagram batch cost about
 // 230 us per call that way (detect_retransmissions 462 -> 236 us with this
-// pool, tools/dedup_overhead.py).  This pool keeps what it has (threshold =
+// pool, round-2 probe tools/dedup_overhead.py, in git history).  This pool keeps what it has (threshold =
 // max) and leaves the process's default pool alone.
 #include <mutex>
 #include <vector>

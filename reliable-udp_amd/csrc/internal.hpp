@@ -300,7 +300,7 @@ struct Tuning {
   // LDS budget in % of the hinted run: 1M x 1479 B ASCII frames 0.287 ->
   // 0.279 ms, lengths uniform in [0, 2944] 0.373 -> 0.370 at 130% (110%:
   // more tiles overflow to the HBM path on ragged lengths; 150%: fewer tiles
-  // per CU; tools/utf8_varlen_sweep.py, profiles/r01/sweeps/utf8_varlen_tile.json).
+  // per CU; round-1 tools/utf8_varlen_sweep.py (git history), profiles/r01/sweeps/utf8_varlen_tile.json).
   RUDP_KNOB(utf8_vtile, 1)
   RUDP_KNOB(utf8_vtile_cap_pct, 130)      // fixed-stride UTF-8 validation through LDS tiles (0: per-frame vector kernel)
   // Varlen tile kernels load the tile's frame offsets into registers before
@@ -324,6 +324,7 @@ struct Tuning {
   RUDP_KNOB(varlen_small, 16)
   RUDP_KNOB(varlen_small_fpt, 0)  // 0: 4 for hints up to 4 B, 2 above (profiles/r02/sweeps/small.json)
   RUDP_KNOB(varlen_small_fused, 1)  // the framing kernel finds its own base (no pass-2 launch)
+  RUDP_KNOB(varlen_small_single, 1)  // a checked call that is one small-frame tile: one launch, no pass 1
   // Fixed-length encode: batches of more packets than this go out as several
   // launches of at most this many (0: one launch).
   RUDP_KNOB(encode_launch_packets, 0)

@@ -276,7 +276,8 @@ RUDP_API int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, i
 // 51: varlen byte tiles (0 never, 1 when the scan counts overflowing packet tiles, 2 always);
 // 52: varlen tile sum pass (2 from 128-B block sums, 0 chunk by chunk);
 // 62: packed small-frame dedup in one launch (dedup_small_kernel; 0: two passes);
-// 63: varlen decode tile frame sums from 128-B block sums (0: chunk by chunk).
+// 63: varlen decode tile frame sums from 128-B block sums (0: chunk by chunk);
+// 64: a checked small-frame encode of one tile in one launch (no pass 1).
 // (54: chunked / rotated XCD orders, measured within 2% and removed;
 // profiles/r02/headline/xcd_orders.json.)
 // (55, 56: a small-tile launch tail, and 57: persistent workgroups looping over the tiles,
@@ -322,7 +323,8 @@ RUDP_API int rudpx_tune(int key, int value) {
             : key == 59 ? &t.varlen_span_bytes
             : key == 61 ? &t.varlen_diag
             : key == 62 ? &t.dedup_small
-            : key == 63 ? &t.varlen_decode_blocks : nullptr;
+            : key == 63 ? &t.varlen_decode_blocks
+            : key == 64 ? &t.varlen_small_single : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }

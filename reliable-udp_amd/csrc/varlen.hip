@@ -1297,11 +1297,18 @@ __host__ __device__ inline uint32_t small_out_cap(uint32_t T, uint32_t cap, uint
 // status from all of them -- nb <= kSmallFusedTiles, so that is a few KiB of
 // L2 reads per block -- instead of a one-workgroup pass between the two
 // launches.  Otherwise `sums` are pass 2's exclusive bases.
+// SINGLE (a checked call of packed payloads that is one tile, e.g. a
+// recvmmsg batch of <= 1024 datagrams): no pass 1 at all.  The tile's base
+// is 0 and its payload run is the whole payload buffer, whose size the call
+// states, so the run loads before the scan; the block scan's total then gives
+// frame_off[n] and the checks pass 1 would have made.  One launch per call.
 constexpr uint64_t kSmallFusedTiles = 2048;
+enum SmallMode { kSmallBases = 0, kSmallFused = 1, kSmallSingle = 2 };
 
-template <int H, uint32_t FPT, bool FUSED>
+template <int H, uint32_t FPT, int MODE>
 __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs a, const uint64_t* sums,
                                                                      uint64_t nb, ScanCheck chk) {
+  constexpr bool FUSED = MODE == kSmallFused, SINGLE = MODE == kSmallSingle;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   constexpr uint32_t T = kBlock * FPT;
   const uint32_t tid = threadIdx.x;
@@ -1378,6 +1385,9 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
     if (chk.status && st) return;  // uniform: every block computes the same status
     fo0 = pre;
     fo_end = pre + (sums[tile] & kSumMask);
+  } else if (SINGLE) {
+    fo0 = 0;
+    fo_end = 0;  // from the scan below
   } else {
     fo0 = sums[tile];
     fo_end = p0 + T < a.n ? sums[tile + 1] : a.frame_off[a.n];
@@ -1386,11 +1396,12 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
 #if RUDP_TOOLS
   const uint64_t t_base = a.trace ? (uint64_t)wall_clock64() : 0ull;
 #endif
-  const uint64_t po0 = fo0 - p0 * (uint64_t)H, po_end = fo_end - (p0 + Tv) * (uint64_t)H;
+  const uint64_t po0 = fo0 - p0 * (uint64_t)H;
+  const uint64_t po_end = SINGLE ? chk.payload_bytes : fo_end - (p0 + Tv) * (uint64_t)H;
   const uint64_t A = po0 & ~15ull, OA = fo0 & ~15ull;
   const uint64_t prun = ((po_end + 15u) & ~15ull) - A;
-  const uint64_t orun = ((fo_end + 15u) & ~15ull) - OA;
-  const bool fits = prun <= cap && orun <= small_out_cap(T, cap, H);
+  uint64_t orun = ((fo_end + 15u) & ~15ull) - OA;
+  bool fits = prun <= cap && (SINGLE || orun <= small_out_cap(T, cap, H));
 
   // ---- loads: the payload run; lengths and header table to LDS -------------
   {
@@ -1434,6 +1445,22 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
       const uint32_t q = tid * FPT + i;
       s_off[q] = run;
       run += q < Tv ? s_len[q] + (uint32_t)H : 0u;
+    }
+    if (SINGLE) {  // the checks pass 1 would have made, and frame_off[n]
+      uint32_t big = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < FPT; ++j) big |= lv[j] > kMaxPayload ? 1u : 0u;
+      uint32_t st = __syncthreads_or((int)big) ? RUDP_ST_LEN : 0u;
+      if (total - a.n * (uint64_t)H != chk.payload_bytes) st |= RUDP_ST_PAYLOAD;
+      if (total > chk.frames_cap) st |= RUDP_ST_FRAMES_CAP;
+      if (tid == 0) {
+        const_cast<uint64_t*>(a.frame_off)[a.n] = total;
+        if (chk.status) *chk.status = st;
+      }
+      if (st) return;  // uniform
+      fo_end = total;
+      orun = ((fo_end + 15u) & ~15ull) - OA;
+      fits = fits && orun <= small_out_cap(T, cap, H);
     }
   }
   __syncthreads();
@@ -1516,17 +1543,22 @@ int launch_small_fpt(const VarlenArgs& args, const uint64_t* sums, uint64_t nb, 
                      bool fused, hipStream_t stream) {
   constexpr uint32_t T = kBlock * FPT;
   const size_t lds = small_lds_off_out(T, args.small_cap) + small_out_cap(T, args.small_cap, H) + 32u;
-  const void* fn = fused ? reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT, true>)
-                         : reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT, false>);
+  const int mode = sums == nullptr ? kSmallSingle : fused ? kSmallFused : kSmallBases;
+  const void* fn = mode == kSmallSingle ? reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT, kSmallSingle>)
+                 : mode == kSmallFused  ? reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT, kSmallFused>)
+                                        : reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT, kSmallBases>);
   if (lds > 65536) {
     hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
-  if (fused)
-    hipLaunchKernelGGL((encode_varlen_small_kernel<H, FPT, true>), dim3((uint32_t)nb), dim3(kBlock), lds, stream,
+  if (mode == kSmallSingle)
+    hipLaunchKernelGGL((encode_varlen_small_kernel<H, FPT, kSmallSingle>), dim3(1), dim3(kBlock), lds, stream,
                        args, sums, nb, chk);
+  else if (mode == kSmallFused)
+    hipLaunchKernelGGL((encode_varlen_small_kernel<H, FPT, kSmallFused>), dim3((uint32_t)nb), dim3(kBlock), lds,
+                       stream, args, sums, nb, chk);
   else
-    hipLaunchKernelGGL((encode_varlen_small_kernel<H, FPT, false>), dim3((uint32_t)nb), dim3(kBlock), lds,
+    hipLaunchKernelGGL((encode_varlen_small_kernel<H, FPT, kSmallBases>), dim3((uint32_t)nb), dim3(kBlock), lds,
                        stream, args, sums, nb, chk);
   return (int)hipGetLastError();
 }
@@ -1548,6 +1580,10 @@ int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int
   const uint32_t fpt = args.small_fpt;
   const uint64_t T = (uint64_t)kBlock * fpt;
   const uint64_t nb = (args.n + T - 1) / T;
+  // one tile of a checked call (packed payloads: the small path's only form): one launch, no pass 1
+  if (nb == 1 && chk.status && tuning().varlen_small_single)
+    return layout == 7 ? launch_small_any<7>(args, nullptr, 1, chk, false, stream)
+                       : launch_small_any<5>(args, nullptr, 1, chk, false, stream);
   uint64_t* sums = nullptr;
   hipError_t e = stream_scratch(reinterpret_cast<void**>(&sums), nb * sizeof(uint64_t), stream, kScratchSums);
   if (e != hipSuccess) return (int)e;

@@ -401,3 +401,45 @@ def test_varlen_tile_block_sums_and_chunk_sums_agree(cuda, blocks):
                 assert np.array_equal(got["valid"], want_v), (H, hint)
     finally:
         lib.rudpx_tune(63, old)
+
+
+@pytest.mark.parametrize("single", [1, 0])
+def test_small_encode_one_tile_batches(cuda, single):
+    """A checked small-frame encode of at most 1024 packets (a recvmmsg batch)
+    runs as one launch with no scan pass (rudpx_tune 64 = 1, the default):
+    frames, offsets and checksums equal the oracle's for 1..1024 packets of
+    1-4 byte payloads, and every argument check still reports (lengths past
+    65535, a payload size that disagrees, a frame buffer too small)."""
+    import ctypes
+    import torch
+    from oracle import synth
+    lib = _native.tools_lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    old = lib.rudpx_tune(64, single)
+    try:
+        rng = np.random.default_rng(64 + single)
+        for n in (1, 7, 255, 1000, 1024):
+            lens = rng.integers(1, 5, n).astype(np.int32)
+            pay = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+            seq, ack, flags, _ = synth.synth(n, 0, n, 0)
+            tab = (dev(seq, cuda), dev(ack, cuda), dev(flags, cuda))
+            pays = [bytes(pay[o:o + k]) for o, k in zip(np.concatenate([[0], np.cumsum(lens)[:-1]]), lens)]
+            for H in (5, 7):
+                want, off, cs = codec_np.encode_varlen(seq, ack, flags, pays, H)
+                res = batch.pack_batch_varlen(tab, dev(pay, cuda), dev(lens, cuda), H, want_csum=True)
+                assert np.array_equal(host(res.frames), want), (n, H)
+                assert np.array_equal(host(res.frame_off), off) and np.array_equal(host(res.csum), cs), (n, H)
+        n = 600
+        lens = np.ones(n, np.int32)
+        z16, z8 = dev(np.zeros(n, np.uint16), cuda), dev(np.zeros(n, np.uint8), cuda)
+        with pytest.raises(ValueError, match="sum"):
+            batch.pack_batch_varlen((z16, z16, z8), dev(np.zeros(n + 1, np.uint8), cuda), dev(lens, cuda))
+        big = lens.copy()
+        big[17] = 70000
+        with pytest.raises(ValueError, match="65535"):
+            batch.pack_batch_varlen((z16, z16, z8), dev(np.zeros(n, np.uint8), cuda), dev(big, cuda))
+        with pytest.raises(ValueError, match="too small"):
+            batch.pack_batch_varlen((z16, z16, z8), dev(np.zeros(n, np.uint8), cuda), dev(lens, cuda),
+                                    out=torch.empty(n * 6 - 1, dtype=torch.uint8, device=cuda))
+    finally:
+        lib.rudpx_tune(64, old)

@@ -1,6 +1,8 @@
 """Per-kernel median / mean durations of rocprofv3 kernel traces under gpurun_out/.
 
 usage: python tools/trace_stats.py TAG [TAG ...]   (directories gpurun_out/TAG/run_kernel_trace.csv)
+       python tools/trace_stats.py --counters TAG_sq [...]   (gpurun_out/TAG_sq/run_counter_collection.csv:
+                                                            per kernel, the median of each counter over dispatches)
 Prints, per tag, each kernel with at least --min dispatches and the run's HIP-event
 ms_per_launch from gpurun_out/TAG.log (tools/run_kernel.py's line).
 """
@@ -23,11 +25,30 @@ def kernel_durations(tag: str) -> dict:
     return by
 
 
+def counters(tag: str) -> dict:
+    """{kernel: {counter: median over dispatches}} of a --pmc run (values summed over a dispatch's rows)."""
+    per = {}
+    with open(OUT / tag / "run_counter_collection.csv") as f:
+        for r in csv.DictReader(f):
+            key = (r["Kernel_Name"], r["Dispatch_Id"])
+            per.setdefault(key, {}).setdefault(r["Counter_Name"], 0.0)
+            per[key][r["Counter_Name"]] += float(r["Counter_Value"])
+    by = {}
+    for (k, _), cs in per.items():
+        for c, v in cs.items():
+            by.setdefault(k, {}).setdefault(c, []).append(v)
+    return {k: {c: st.median(v) for c, v in cs.items()} for k, cs in by.items()}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("tags", nargs="+")
     ap.add_argument("--min", type=int, default=20)
+    ap.add_argument("--counters", action="store_true")
     args = ap.parse_args()
+    if args.counters:
+        print(json.dumps({t: counters(t) for t in args.tags}, indent=1))
+        return
     for tag in args.tags:
         line = ""
         log = OUT / f"{tag}.log"
