@@ -289,12 +289,12 @@ struct Tuning {
   RUDP_KNOB(varlen_encode_cap_pct, 110)
   RUDP_KNOB(varlen_decode_tile, 1)  // varlen decode through LDS tiles for hints >= 128 B (2: any hint; 0: never)
   RUDP_KNOB(dedup_table, 1)    // dedup window pass by LDS hash table (0: every frame scans its window)
-  RUDP_KNOB(dedup_small, 1)
+  RUDP_KNOB(dedup_small, 1)  // packed small frames: dedup in one launch (dedup_small_kernel; 0: two passes)
   // Varlen decode tile frame sums from 128-B block sums taken in phase 1 (the
   // encode tile's scheme): lengths uniform in [0, 2944] 0.288 -> 0.278 ms, but
   // equal 1472-B lengths 0.246 -> 0.268 (the block sums' DPP work sits in the
   // streaming phase), so off (profiles/r04/sweeps/varlen_decode_blocks.json).
-  RUDP_KNOB(varlen_decode_blocks, 0)    // packed small frames: dedup in one launch (dedup_small_kernel; 0: two passes)
+  RUDP_KNOB(varlen_decode_blocks, 0)
   RUDP_KNOB(utf8_tile, 1)
   // Packed-frame UTF-8 validation through LDS tiles (hints >= 128 B) and its
   // LDS budget in % of the hinted run: 1M x 1479 B ASCII frames 0.287 ->

@@ -7,7 +7,8 @@ output is compared byte for byte with the first value's.
 shapes: encode:L (fixed-length, 1M x L, rotating sets below 1 GiB), varlen:L
 (packed, equal lengths), ragged (lengths uniform in [0, 2944]), decode:L,
 vdec:L (varlen decode, equal lengths; vdec:L+u with the UTF-8 check), rdec (varlen
-decode, ragged ASCII lengths; rdec:+u), dedup (1M one-character datagrams, window 500).
+decode, ragged ASCII lengths; rdec:+u; rdec:sort sorts each run of 16 lengths,
+rdec:perm makes each run of 16 a permutation of one even spread), dedup (1M one-character datagrams, window 500).
 
 usage: python tools/knob_ab.py --knob 58 --values 0,1 --shapes encode:1472,encode:64,varlen:1472,ragged
        python tools/knob_ab.py --variants "base:;t256b512:2=256,10=512" --shapes encode:64
@@ -66,6 +67,12 @@ def make_shape(spec, dev):
             flat, lens = pay.view(-1), torch.full((n,), L, dtype=torch.int32, device=dev)
         else:
             lens = torch.randint(0, 2945, (n,), dtype=torch.int32, device=dev, generator=g)
+            if arg.startswith("sort"):  # sorted within each run of 16 frames: same tile runs, even waves
+                lens = lens.view(-1, 16).sort(dim=1).values.reshape(-1).contiguous()
+            elif arg.startswith("perm"):  # every run of 16 a permutation of one spread: equal tile runs
+                base = (torch.arange(16, device=dev, dtype=torch.int32) * 2944 + 1472) // 16
+                idx = torch.rand((n // 16, 16), device=dev, generator=g).argsort(dim=1)
+                lens = base[idx].reshape(-1).to(torch.int32).contiguous()
             tab, _ = batch.synth_batch(n, 0, 0x5EED0004, device=dev)
             flat = torch.randint(0, 128, (int(lens.sum().item()),), dtype=torch.uint8, device=dev, generator=g)
         res = batch.pack_batch_varlen(tab, flat, lens, 7)
