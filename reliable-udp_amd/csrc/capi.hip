@@ -5,8 +5,10 @@
 #include <stdio.h>
 #include <string.h>
 
+#include <atomic>
 #include <deque>
 #include <mutex>
+#include <optional>
 #include <string>
 #include <vector>
 
@@ -402,6 +404,27 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
   a.status_out = status_out;
   a.frames_lim = frames_lim;
   a.lim_checked = checked ? 1u : 0u;
+  // Checked calls with MTU-scale hints: byte spans (decode_varlen_span_kernel)
+  // instead of frame tiles; the span index lives in this stream's scratch.
+  const uint64_t S = (uint64_t)tuning().varlen_decode_span_bytes & ~15ull;
+  const uint64_t span_cap = (S + 2u * (uint64_t)len_hint + 64u + 15u) & ~15ull;
+  const uint64_t nt = S ? frames_lim / S + 1u : 0u;
+  const bool span = checked && tuning().varlen_decode_span && a.glog != kNoVec && !a.small_fpt &&
+                    len_hint >= 256u && S >= 4096u && n < 0xFFFFFFFFull && nt < 0x7FFFFFFFull &&
+                    decode_span_fits(span_cap) && (reinterpret_cast<uintptr_t>(d_frames) & 15u) == 0;
+  std::optional<ScratchCall> call;
+  if (span) {
+    call.emplace((hipStream_t)hip_stream);
+    void* buf = nullptr;
+    RUDP_HIP(stream_scratch(&buf, (nt + 2u) * sizeof(SpanRec), (hipStream_t)hip_stream, kScratchRecords));
+    static std::atomic<uint32_t> epoch{0};
+    a.span_rec = static_cast<const SpanRec*>(buf);
+    a.span_count = nt;
+    a.span_flag = reinterpret_cast<const uint32_t*>(static_cast<SpanRec*>(buf) + nt + 1u);
+    a.span_epoch = epoch.fetch_add(1u) + 1u;
+    a.span_S = (uint32_t)S;
+    a.tile_cap = (uint32_t)span_cap;
+  }
   rc = launch_decode_varlen(a, layout, (hipStream_t)hip_stream);
   if (rc) return hip_fail((hipError_t)rc, "varlen decode launch");
   return 0;

@@ -47,6 +47,18 @@ __device__ __forceinline__ uint32_t fold16(uint32_t s) {
   return s;
 }
 
+// A partial word sum of any size brought to at most 0x1FFFE with its value
+// mod 0xFFFF and its zero-ness kept (2^16 = 1 mod 0xFFFF): a checksum folded
+// from such parts equals the one folded from the exact total.  The decode
+// paths that take frames of any length (untrusted offsets) fold before sums
+// could pass 2^32.
+__device__ __forceinline__ uint32_t fold_keep(uint64_t s) {
+  s = (s & 0xFFFFFFFFull) + (s >> 32);
+  s = (s & 0xFFFFull) + (s >> 16);
+  s = (s & 0xFFFFull) + (s >> 16);
+  return (uint32_t)s;
+}
+
 // Sum of the eight little-endian u16 halves of a 16-byte vector.
 __device__ __forceinline__ uint32_t le16_sum(u32x4 v) {
   uint32_t lo = (v.x & 0xFFFFu) + (v.y & 0xFFFFu) + (v.z & 0xFFFFu) + (v.w & 0xFFFFu);

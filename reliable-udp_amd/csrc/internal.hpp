@@ -158,6 +158,13 @@ struct VarlenArgs {
   uint32_t bt_slots;
   uint32_t tile_Tl;
   uint32_t tile_sums;             // tile sum pass: 2 from 128-B block sums, 0 chunk by chunk
+  // Decode by byte spans (checked calls): span_rec[k] = the first frame that
+  // starts at or past k * span_S (decode_span_index_kernel); *span_flag ==
+  // span_epoch when the offsets are not in order inside the buffer, and the
+  // decode then checks frame by frame.
+  const uint32_t* span_flag;
+  uint32_t span_epoch;
+  uint32_t span_S;
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -325,6 +332,11 @@ struct Tuning {
   RUDP_KNOB(varlen_small_fpt, 0)  // 0: 4 for hints up to 4 B, 2 above (profiles/r02/sweeps/small.json)
   RUDP_KNOB(varlen_small_fused, 1)  // the framing kernel finds its own base (no pass-2 launch)
   RUDP_KNOB(varlen_small_single, 1)  // a checked call that is one small-frame tile: one launch, no pass 1
+  // Checked varlen decode by byte spans: a workgroup decodes the frames that
+  // start in one span of varlen_decode_span_bytes, its lanes over the bytes
+  // (not over frames), after an index pass over the offsets (0: frame tiles).
+  RUDP_KNOB(varlen_decode_span, 0)
+  RUDP_KNOB(varlen_decode_span_bytes, 24576)
   // Fixed-length encode: batches of more packets than this go out as several
   // launches of at most this many (0: one launch).
   RUDP_KNOB(encode_launch_packets, 0)
@@ -375,6 +387,8 @@ bool varlen_btile_ok(uint32_t tile_T, uint32_t* bt_slots, uint32_t min_slots, ui
                      uint32_t H, uint32_t vhc, uint64_t packet_tiles, uint64_t spans);
 int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream);
 int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream);
+// The span decode's LDS (run budget `cap` plus its arrays) fits a workgroup.
+bool decode_span_fits(uint64_t cap);
 int launch_validate_utf8(const Utf8Args& args, hipStream_t stream);
 int launch_dedup(const DedupArgs& args, hipStream_t stream);
 uint32_t dedup_max_window();

@@ -324,7 +324,9 @@ RUDP_API int rudpx_tune(int key, int value) {
             : key == 61 ? &t.varlen_diag
             : key == 62 ? &t.dedup_small
             : key == 63 ? &t.varlen_decode_blocks
-            : key == 64 ? &t.varlen_small_single : nullptr;
+            : key == 64 ? &t.varlen_small_single
+            : key == 65 ? &t.varlen_decode_span
+            : key == 66 ? &t.varlen_decode_span_bytes : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }

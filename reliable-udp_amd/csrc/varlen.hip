@@ -692,19 +692,20 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_kernel(VarlenArgs a) {
   const uint32_t g = threadIdx.x & (kVarLanes - 1u);
   const uint64_t p = ((uint64_t)blockIdx.x * kBlock + threadIdx.x) / kVarLanes;
   const bool valid = p < a.n;
-  uint32_t sum = 0, F = 0;
+  uint64_t acc = 0, F = 0;  // (frames of any length: the sum is folded before the lanes add)
   uint64_t fo = 0;
   bool bad = false;
   if (valid) {
     fo = a.frame_off[p];
     const uint64_t fe = a.frame_off[p + 1];
     bad = fo > fe || fe > frames_limit(a);
-    F = bad ? 0u : (uint32_t)(fe - fo);
-    for (uint32_t j = (uint32_t)H + g; j < F; j += kVarLanes) {
+    F = bad ? 0u : fe - fo;
+    for (uint64_t j = (uint64_t)H + g; j < F; j += kVarLanes) {
       const uint32_t b = a.frames[fo + j];
-      sum += ((j - H) & 1u) ? (b << 8) : b;
+      acc += ((j - H) & 1u) ? (b << 8) : b;
     }
   }
+  uint32_t sum = fold_keep(acc);
   uint32_t u8bad = 0;
   if (U8) {
     if (valid && F > (uint32_t)H) u8bad = utf8_slice(a.frames, fo + H, F - H, g, kVarLanes);
@@ -722,7 +723,7 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_kernel(VarlenArgs a) {
     for (uint32_t i = 0; i < 7; ++i)
       if (i < F) b[i] = a.frames[fo + i];
     uint32_t seq = (b[0] << 8) | b[1], ack = (b[2] << 8) | b[3];
-    if (F < (uint32_t)H) {  // short frame: fields truncated as utils/packet.py:31 slices them
+    if (F < (uint64_t)H) {  // short frame: fields truncated as utils/packet.py:31 slices them
       if (F < 2) seq = b[0];
       if (F < 4) ack = b[2];
       a.seq[p] = (uint16_t)seq;
@@ -789,7 +790,7 @@ __device__ __forceinline__ void decode_varlen_finish(const VarlenArgs& a, uint64
 // U8: the payload's strict UTF-8 check in the same pass: the (masked) payload
 // words' high bits are OR'ed as they are summed, and only a frame that holds
 // one runs the byte checks (utf8_check_frame, its chunks again, from L2).
-template <int H, bool U8>
+template <int H, bool U8, int PL = 0>
 __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_t p, bool valid, uint32_t g,
                                                     uint32_t glog) {
   const uint32_t tid = threadIdx.x;
@@ -807,8 +808,8 @@ __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_
   const uint64_t ps = fstart + H;       // payload start
   u32x4 first = {0u, 0u, 0u, 0u};
   // loads in flight per lane: 8, or 6 with the UTF-8 check (its registers keep the
-  // tile kernels that inline this at 6 waves per SIMD)
-  constexpr int P = U8 ? 6 : 8;
+  // tile kernels that inline this at 6 waves per SIMD); PL: the caller's choice
+  constexpr int P = PL ? PL : (U8 ? 6 : 8);
   for (uint32_t i0 = g; i0 < nchunks; i0 += (uint32_t)P * G) {
     uint32_t even = 0, odd = 0;  // at most 32 dwords per round: packed halves cannot overflow
     u32x4 v[P];
@@ -833,9 +834,12 @@ __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_
                ((w.z >> 8) & 0x00FF00FFu) + ((w.w >> 8) & 0x00FF00FFu);
       }
     }
-    even_sum += (even & 0xFFFFu) + (even >> 16);
-    odd_sum += (odd & 0xFFFFu) + (odd >> 16);
+    // (folded as they go: a frame may be of any length)
+    even_sum = fold_keep(even_sum) + (even & 0xFFFFu) + (even >> 16);
+    odd_sum = fold_keep(odd_sum) + (odd & 0xFFFFu) + (odd >> 16);
   }
+  even_sum = fold_keep(even_sum);
+  odd_sum = fold_keep(odd_sum);
   // even global offsets are high bytes iff the frame starts at an even offset
   uint32_t sum = (fstart & 1u) ? (even_sum + (odd_sum << 8)) : ((even_sum << 8) + odd_sum);
   for (uint32_t m = G >> 1; m > 0; m >>= 1) {
@@ -863,7 +867,9 @@ __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_
     return;
   }
   if (U8) a.valid[p] = u8bad ? 0 : 1;
-  decode_varlen_finish<H>(a, p, (uint32_t)(fend - fstart), sum, funnel32(first, next, (uint32_t)(fstart & 15u)));
+  const uint64_t F = fend - fstart;
+  decode_varlen_finish<H>(a, p, F < 0xFFFFFFFFull ? (uint32_t)F : 0xFFFFFFFFu, sum,
+                          funnel32(first, next, (uint32_t)(fstart & 15u)));
 }
 
 template <int H, bool U8>
@@ -1031,6 +1037,203 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
   if (g == 0)
     decode_varlen_finish<H>(a, p0 + q, fe - fs,
                             sum, window16_dw(reinterpret_cast<const uint32_t*>(img), fs));
+}
+
+// ---------------------------------------------------------------------------
+// Varlen decode by byte spans (checked calls, a.span_rec set).
+//
+// Frame tiles (decode_varlen_tile_kernel) hold T frames each: with ragged
+// lengths their runs spread (16 frames of U[0, 2944] B: 23.5 KiB +- 3.4 KiB),
+// a quarter overflow the LDS budget into the per-frame path, and the G lanes
+// of a frame sum its chunks while the wave waits for its longest frame.  Here
+// workgroup k decodes the frames that START in bytes [k S, (k + 1) S) of the
+// buffer (decode_span_index_kernel found them), so every run is S plus at
+// most its last frame, and the lanes split the run's chunks evenly: lane l
+// sums chunks [l kc, (l + 1) kc) whatever frames they hold.  A frame's
+// payload sum is then the difference of two prefix sums of the run, at its
+// payload start and end: a lane records the prefix at every boundary inside
+// its chunks, a scan over the lanes makes those prefixes absolute, and the
+// frame's leader subtracts.  Offsets not in order, or past the buffer: the
+// index pass raises span_flag, and the launch decodes frame by frame (every
+// pair checked, decode_varlen_frame).
+constexpr uint32_t kSpanNF = 128;  // frames of one span held in LDS (more: per-frame path)
+
+// one record per span (and one past the last): first frame starting at or
+// past k S, and its offset.  Thread i <= n writes the spans whose first frame
+// is i; threads past n write the spans past the last offset.
+__global__ void __launch_bounds__(kBlock) decode_span_index_kernel(const uint64_t* fo, uint64_t n, uint64_t lim,
+                                                                   uint32_t S, uint32_t nt, SpanRec* rec,
+                                                                   uint32_t* flag, uint32_t epoch) {
+  const uint64_t i = (uint64_t)blockIdx.x * kBlock + threadIdx.x;
+  if (i <= n) {
+    const uint64_t x = fo[i];
+    const uint64_t xp = i ? fo[i - 1] : 0u;
+    if (x > lim || xp > x) {
+      *flag = epoch;
+      return;
+    }
+    const uint64_t k1 = x / S;
+    for (uint64_t k = i ? xp / S + 1u : 0u; k <= k1; ++k) rec[k] = SpanRec{x, (uint32_t)i, 0u};
+  } else if (i <= n + 1u + nt) {
+    const uint64_t k = i - n - 1u;
+    const uint64_t x = fo[n];
+    if (x <= lim && k > x / S) rec[k] = SpanRec{x, (uint32_t)n, 0u};
+  }
+}
+
+__host__ __device__ inline uint32_t dsp_img_off() {
+  // fo u32[NF + 1] | boundary prefixes u32[2 NF] | U8 flags u8[NF] | wave sums u64[4] | guard | run
+  return ((((((kSpanNF + 1u) * 4u + 15u) & ~15u) + 8u * kSpanNF + kSpanNF + 32u) + 15u) & ~15u) + kVTGuard;
+}
+__host__ __device__ inline uint32_t dsp_lds_bytes(uint32_t cap) { return dsp_img_off() + cap + 32u; }
+
+template <int H, bool U8>
+__global__ void __launch_bounds__(kBlock) decode_varlen_span_kernel(VarlenArgs a) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  const uint32_t tid = threadIdx.x;
+  const uint32_t glog = a.glog, G = 1u << glog, T = kBlock >> glog;
+  const uint32_t q = tid >> glog, g = tid & (G - 1u);
+  const uint32_t nt = (uint32_t)a.span_count;
+  if (*a.span_flag == a.span_epoch) {  // offsets out of order or past the buffer: frame by frame
+    const uint64_t p = (uint64_t)blockIdx.x * T + q;
+    if ((uint64_t)blockIdx.x * T < a.n) decode_varlen_frame<H, U8, 4>(a, p, p < a.n, g, glog);
+    return;
+  }
+  if (blockIdx.x >= nt) return;
+  const uint32_t k = a.xcd ? xcd_tile(blockIdx.x, nt) : blockIdx.x;
+  const SpanRec r0 = a.span_rec[k], r1 = a.span_rec[k + 1];
+  const uint32_t nf = r1.p - r0.p;
+  if (nf == 0) return;
+  const uint64_t f0 = r0.p;
+  const uint64_t A = r0.fo & ~15ull;
+  const uint64_t run = ((r1.fo + 15u) & ~15ull) - A;
+  if (nf > kSpanNF || run > a.tile_cap) {  // uniform: the span's frames one by one from HBM
+    for (uint32_t base = 0; base < nf; base += T)
+      decode_varlen_frame<H, U8, 4>(a, f0 + base + q, base + q < nf, g, glog);
+    return;
+  }
+  uint32_t* lds_fo = reinterpret_cast<uint32_t*>(lds);                                       // [nf + 1]
+  uint32_t* lds_pre = reinterpret_cast<uint32_t*>(lds + (((kSpanNF + 1u) * 4u + 15u) & ~15u));  // [2 nf]
+  unsigned char* lds_hi = reinterpret_cast<unsigned char*>(lds_pre + 2u * kSpanNF);           // [nf]
+  uint64_t* lds_wsum = reinterpret_cast<uint64_t*>((reinterpret_cast<uintptr_t>(lds_hi + kSpanNF) + 7u) & ~(uintptr_t)7u);
+  unsigned char* img = lds + dsp_img_off();
+  const uint64_t total = frames_limit(a);
+  {
+    const uint32_t fo_r = tid <= nf ? (uint32_t)(a.frame_off[f0 + tid] - A) : 0u;
+    const uint32_t nvec = (uint32_t)(run >> 4);
+    u32x4* dst = reinterpret_cast<u32x4*>(img);
+    constexpr uint32_t P = 8;
+    for (uint32_t v0 = tid; v0 < nvec; v0 += P * kBlock) {
+      u32x4 r[P];
+#pragma unroll
+      for (uint32_t u = 0; u < P; ++u) {
+        const uint32_t v = v0 + u * kBlock;
+        if (v < nvec) r[u] = load16_guarded(a.frames, A + 16ull * v, total);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < P; ++u) {
+        const uint32_t v = v0 + u * kBlock;
+        if (v < nvec) dst[v] = r[u];
+      }
+    }
+    if (tid <= nf) lds_fo[tid] = fo_r;
+    if (U8 && tid < nf) lds_hi[tid] = 0;
+  }
+  __syncthreads();
+  const u32x4* img16 = reinterpret_cast<const u32x4*>(img);
+  const uint32_t nvec = (uint32_t)(run >> 4);
+  // lane tid's chunks; together the lanes cover one chunk past the run, so
+  // every boundary (at most 16 nvec) lies inside some lane's bytes
+  const uint32_t kc = nvec / kBlock + 1u;
+  const uint32_t c_begin = tid * kc;
+  const uint32_t pos0 = c_begin << 4;
+  // boundary b: payload start of frame b / 2 (even b) or its end (odd b)
+  auto bpos = [&](uint32_t b) -> uint32_t {
+    if (b >= 2u * nf) return 0xFFFFFFFFu;
+    const uint32_t i = b >> 1, fe = lds_fo[i + 1u];
+    if (b & 1u) return fe;
+    const uint32_t ps = lds_fo[i] + (uint32_t)H;
+    return ps < fe ? ps : fe;
+  };
+  uint32_t lo = 0, hi = nf;  // the first frame ending at or past pos0
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (lds_fo[mid + 1u] >= pos0) hi = mid;
+    else lo = mid + 1u;
+  }
+  uint32_t b = 2u * lo;
+  if (bpos(b) < pos0) ++b;
+  const uint32_t b_first = b;
+  uint32_t nb = bpos(b);
+  uint32_t acc = 0;  // even | odd << 16 byte sums of the lane's chunks so far (at most kc * 2040 each)
+  for (uint32_t c = c_begin; c < c_begin + kc; ++c) {
+    const uint32_t cb = c << 4;
+    const u32x4 w = c < nvec ? img16[c] : make_u32x4(0ull, 0ull);
+    const uint32_t hb = U8 ? high_bits(w) : 0u;
+    uint32_t seg = 0;  // chunk-relative start of the piece before the next boundary
+    while (nb < cb + 16u) {
+      const uint32_t m = nb - cb;
+      const u32x4 head = keep_bytes(w, 0, (int)m);
+      if (U8 && hb && (b & 1u) && m > seg && high_bits(keep_bytes(head, (int)seg, 16))) lds_hi[b >> 1] = 1;
+      lds_pre[b] = acc + eo_sum(lo64(head), hi64(head));
+      seg = m;
+      ++b;
+      nb = bpos(b);
+    }
+    if (U8 && hb && (b & 1u) && high_bits(keep_bytes(w, (int)seg, 16))) lds_hi[b >> 1] = 1;
+    acc += eo_sum(lo64(w), hi64(w));
+  }
+  // exclusive scan of the lanes' (even, odd) sums over the workgroup
+  const uint32_t lane = tid & 63u, wave = tid >> 6;
+  uint32_t se = acc & 0xFFFFu, so = acc >> 16;
+  for (uint32_t d = 1; d < 64u; d <<= 1) {
+    const uint32_t te = (uint32_t)__shfl_up((int)se, d, 64), to = (uint32_t)__shfl_up((int)so, d, 64);
+    if (lane >= d) {
+      se += te;
+      so += to;
+    }
+  }
+  if (lane == 63u) lds_wsum[wave] = (uint64_t)se | ((uint64_t)so << 32);
+  se -= acc & 0xFFFFu;
+  so -= acc >> 16;
+  __syncthreads();
+  for (uint32_t w = 0; w < wave; ++w) {
+    const uint64_t ws = lds_wsum[w];
+    se += (uint32_t)ws;
+    so += (uint32_t)(ws >> 32);
+  }
+  // this lane's boundaries: absolute prefixes, weighted by their frame's
+  // start parity (even offsets are high bytes iff the frame starts even)
+  for (uint32_t s = b_first; s < b; ++s) {
+    const uint32_t loc = lds_pre[s];
+    const uint32_t e = se + (loc & 0xFFFFu), o = so + (loc >> 16);
+    lds_pre[s] = (lds_fo[s >> 1] & 1u) ? e + (o << 8) : (e << 8) + o;
+  }
+  __syncthreads();
+  if (U8) {  // frames with a high bit in their payload: the byte checks, G lanes each, from LDS
+    const uint32_t* idw = reinterpret_cast<const uint32_t*>(img);  // kVTGuard bytes before it
+    for (uint32_t base = 0; base < nf; base += T) {
+      const uint32_t i = base + q;
+      const bool flagged = i < nf && lds_hi[i];
+      if (__any(flagged)) {
+        uint32_t bad = 0;
+        if (flagged) {
+          const uint32_t fs = lds_fo[i], fe = lds_fo[i + 1u];
+          const uint32_t ps = fs + (uint32_t)H < fe ? fs + (uint32_t)H : fe;
+          bad = utf8_check_frame(ps, fe, g, G, [&](uint64_t c) { return img16[c]; },
+                                 [&](uint64_t x) { return idw[(int64_t)(x >> 2) - 1]; });
+        }
+        bad = group_or(bad, G);
+        if (flagged && g == 0) a.valid[f0 + i] = bad ? 0 : 1;
+      }
+    }
+  }
+  if (tid < nf) {
+    const uint32_t fs = lds_fo[tid], fe = lds_fo[tid + 1u];
+    if (U8 && !lds_hi[tid]) a.valid[f0 + tid] = 1;
+    decode_varlen_finish<H>(a, f0 + tid, fe - fs, lds_pre[2u * tid + 1u] - lds_pre[2u * tid],
+                            window16_dw(reinterpret_cast<const uint32_t*>(img), fs));
+  }
 }
 
 // Strict UTF-8 validation kernels (the checks themselves: utf8_device.hpp).
@@ -1611,9 +1814,11 @@ __device__ __forceinline__ void decode_varlen_frame_lane(const VarlenArgs& a, ui
     decode_varlen_reject(a, p);
     return;
   }
-  const uint32_t F = (uint32_t)(fe - fo);
-  uint32_t sum = 0;
-  for (uint32_t j = (uint32_t)H; j < F; ++j) sum += ((j - H) & 1u) ? (uint32_t)a.frames[fo + j] << 8 : a.frames[fo + j];
+  const uint64_t F64 = fe - fo;
+  const uint32_t F = F64 < 0xFFFFFFFFull ? (uint32_t)F64 : 0xFFFFFFFFu;
+  uint64_t acc = 0;
+  for (uint64_t j = (uint64_t)H; j < F64; ++j) acc += ((j - H) & 1u) ? (uint32_t)a.frames[fo + j] << 8 : a.frames[fo + j];
+  const uint32_t sum = fold_keep(acc);
   uint32_t d[4] = {0, 0, 0, 0};
   for (uint32_t i = 0; i < 7 && i < F; ++i) d[i >> 2] |= (uint32_t)a.frames[fo + i] << (8 * (i & 3));
   u32x4 h;
@@ -1922,6 +2127,19 @@ int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream)
 // (utils/reliableUDP.py:121, get_payload's strict decode at utils/packet.py:73).
 template <int H, bool U8>
 static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
+  if (args.span_rec) {  // byte spans: the index pass, then one workgroup per span (or per T frames)
+    const uint32_t nt = (uint32_t)args.span_count;
+    const uint64_t idx_threads = args.n + 2u + nt;
+    hipLaunchKernelGGL(decode_span_index_kernel, dim3((uint32_t)((idx_threads + kBlock - 1) / kBlock)), dim3(kBlock),
+                       0, stream, args.frame_off, args.n, args.frames_lim, args.span_S, nt,
+                       const_cast<SpanRec*>(args.span_rec), const_cast<uint32_t*>(args.span_flag), args.span_epoch);
+    const uint32_t T = kBlock >> args.glog;
+    const uint64_t frame_blocks = (args.n + T - 1) / T;
+    const uint64_t blocks = frame_blocks > nt ? frame_blocks : nt;
+    hipLaunchKernelGGL((decode_varlen_span_kernel<H, U8>), dim3((uint32_t)blocks), dim3(kBlock),
+                       dsp_lds_bytes(args.tile_cap), stream, args);
+    return (int)hipGetLastError();
+  }
   if (args.small_fpt && args.glog != kNoVec && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0)
     return launch_decode_small<H, U8>(args, stream);
   if (args.glog != kNoVec && args.tile_cap && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0) {
@@ -1945,6 +2163,8 @@ static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
   hipLaunchKernelGGL((decode_varlen_kernel<H, U8>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
   return (int)hipGetLastError();
 }
+
+bool decode_span_fits(uint64_t cap) { return cap < 65536u && dsp_lds_bytes((uint32_t)cap) <= 65536u; }
 
 int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream) {
   if (args.n == 0) return 0;
