@@ -404,6 +404,9 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
   a.status_out = status_out;
   a.frames_lim = frames_lim;
   a.lim_checked = checked ? 1u : 0u;
+#if RUDP_TOOLS
+  a.diag = (uint32_t)tuning().varlen_diag;
+#endif
   // Checked calls with MTU-scale hints: byte spans (decode_varlen_span_kernel)
   // instead of frame tiles; the span index lives in this stream's scratch.
   const uint64_t S = (uint64_t)tuning().varlen_decode_span_bytes & ~15ull;
@@ -671,6 +674,7 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
   }
   // Sum pass of the tile kernel: 2 = from 128-B block sums
   a.tile_sums = tuning().varlen_tile_sums == 2 ? 2u : 0u;
+  a.map_bal = tuning().varlen_map_bal ? 1u : 0u;
 #if RUDP_TOOLS
   a.trace = tuning().encode_trace.load();  // tile-kernel phase timeline (tools/varlen_timeline.py)
 #endif

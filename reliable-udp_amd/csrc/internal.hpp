@@ -165,6 +165,7 @@ struct VarlenArgs {
   const uint32_t* span_flag;
   uint32_t span_epoch;
   uint32_t span_S;
+  uint32_t map_bal;               // encode tile: chunk map built by output units, not by frames
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -337,6 +338,9 @@ struct Tuning {
   // (not over frames), after an index pass over the offsets (0: frame tiles).
   RUDP_KNOB(varlen_decode_span, 0)
   RUDP_KNOB(varlen_decode_span_bytes, 24576)
+  // Varlen encode tile: the chunk -> frame map built by output units spread
+  // evenly over the lanes (1) instead of G lanes per frame (0).
+  RUDP_KNOB(varlen_map_bal, 0)
   // Fixed-length encode: batches of more packets than this go out as several
   // launches of at most this many (0: one launch).
   RUDP_KNOB(encode_launch_packets, 0)

@@ -326,7 +326,8 @@ RUDP_API int rudpx_tune(int key, int value) {
             : key == 63 ? &t.varlen_decode_blocks
             : key == 64 ? &t.varlen_small_single
             : key == 65 ? &t.varlen_decode_span
-            : key == 66 ? &t.varlen_decode_span_bytes : nullptr;
+            : key == 66 ? &t.varlen_decode_span_bytes
+            : key == 67 ? &t.varlen_map_bal : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }

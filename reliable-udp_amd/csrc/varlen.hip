@@ -474,35 +474,63 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
   if (a.trace && (tid & 63u) == 0) atomicMax(&s_last[0], (unsigned long long)wall_clock64());
 #endif
   // The map, in the same pass (the block sums have their own LDS region).
-  if (q < Tv) {
+  // map[k] = the frame r whose bytes [fs, fe) hold output unit k's first byte
+  // lead + 16k; with the coded map also the chunk's class for the fast phase
+  // 2: pure payload of r, or one of the prebuilt header chunks of r (chunk
+  // starts in r's header) or r + 1 -- which exist only for frames of
+  // kVHCMinFrame bytes and up: a chunk over a shorter frame's header is left
+  // to the frame walk (bit 14).
+  auto map_entry = [&](uint32_t k, uint32_t r, uint32_t fs, uint32_t fe) {
+    if (!wide) {
+      lds_map[k] = (uint8_t)r;
+      return;
+    }
+    const uint32_t x = lead + 16u * k;
+    const int k0 = (int)x - (int)fs;
+    uint32_t e = r;
+    if (k0 >= H && x + 16u <= fe) {
+      e |= 0x8000u;
+    } else {
+      const uint32_t nxt = k0 >= H ? 1u : 0u;
+      const uint32_t fsp = nxt ? fe : fs;
+      const int i0 = fsp >= lead ? (int)((fsp - lead) >> 4) : -1;
+      e |= (nxt << 8) | ((uint32_t)((int)k - i0) & 1u) << 9;
+      const uint32_t hlen = nxt ? (r + 1u < Tv ? lds_fo[r + 2u] - fe : 0u) : fe - fs;
+      if (hlen < kVHCMinFrame) e |= 0x4000u;
+    }
+    lds_map16[k] = (uint16_t)e;
+  };
+  if (a.map_bal) {
+    // by units: lane tid takes units [tid kc, (tid + 1) kc) whatever frames
+    // they fall in, so a tile of ragged lengths does not wait for its longest
+    // frame's G lanes (a frame's units are its length / 16)
+    const uint32_t K = nbytes > lead ? (nbytes - lead + 15u) >> 4 : 0u;
+    const uint32_t kc = K / kBlock + 1u;
+    uint32_t k = tid * kc;
+    const uint32_t kend = k + kc < K ? k + kc : K;
+    if (k < kend) {
+      uint32_t x = lead + 16u * k;
+      uint32_t lo = 0, hi = Tv - 1u;  // the first frame ending past x
+      while (lo < hi) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (lds_fo[mid + 1u] > x) hi = mid;
+        else lo = mid + 1u;
+      }
+      uint32_t r = lo, fs = lds_fo[r], fe = lds_fo[r + 1u];
+      for (; k < kend; ++k, x += 16u) {
+        while (x >= fe) {
+          ++r;
+          fs = fe;
+          fe = lds_fo[r + 1u];
+        }
+        map_entry(k, r, fs, fe);
+      }
+    }
+  } else if (q < Tv) {
     const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
-    // map[k] = q for the output units k whose first byte lead + 16k lies in [fs, fe)
     const uint32_t klo = fs > lead ? (fs - lead + 15u) >> 4 : 0u;
     const uint32_t khi = fe > lead ? (fe - lead + 15u) >> 4 : 0u;
-    if (wide) {
-      // the chunk's class for the fast phase 2: pure payload of q, or one of
-      // the prebuilt header chunks of q (chunk starts in q's header) or q + 1
-      // -- which exist only for frames of kVHCMinFrame bytes and up: a chunk
-      // over a shorter frame's header is left to the frame walk (bit 14)
-      for (uint32_t k = klo + g; k < khi; k += G) {
-        const uint32_t x = lead + 16u * k;
-        const int k0 = (int)x - (int)fs;
-        uint32_t e = q;
-        if (k0 >= H && x + 16u <= fe) {
-          e |= 0x8000u;
-        } else {
-          const uint32_t nxt = k0 >= H ? 1u : 0u;
-          const uint32_t fsp = nxt ? fe : fs;
-          const int i0 = fsp >= lead ? (int)((fsp - lead) >> 4) : -1;
-          e |= (nxt << 8) | ((uint32_t)((int)k - i0) & 1u) << 9;
-          const uint32_t hlen = nxt ? (q + 1u < Tv ? lds_fo[q + 2u] - fe : 0u) : fe - fs;
-          if (hlen < kVHCMinFrame) e |= 0x4000u;
-        }
-        lds_map16[k] = (uint16_t)e;
-      }
-    } else {
-      for (uint32_t k = klo + g; k < khi; k += G) lds_map[k] = (uint8_t)q;
-    }
+    for (uint32_t k = klo + g; k < khi; k += G) map_entry(k, q, fs, fe);
   }
 #if RUDP_TOOLS
   if (a.trace && (tid & 63u) == 0) atomicMax(&s_last[1], (unsigned long long)wall_clock64());
@@ -1081,9 +1109,12 @@ __global__ void __launch_bounds__(kBlock) decode_span_index_kernel(const uint64_
   }
 }
 
+__host__ __device__ inline uint32_t dsp_pre_off() { return (((kSpanNF + 1u) * 4u) + 15u) & ~15u; }
 __host__ __device__ inline uint32_t dsp_img_off() {
-  // fo u32[NF + 1] | boundary prefixes u32[2 NF] | U8 flags u8[NF] | wave sums u64[4] | guard | run
-  return ((((((kSpanNF + 1u) * 4u + 15u) & ~15u) + 8u * kSpanNF + kSpanNF + 32u) + 15u) & ~15u) + kVTGuard;
+  // fo u32[NF + 1] | boundary prefixes u32[2 NF] | their high-byte counts u16[2 NF] |
+  // wave sums u64[4] | wave counts u32[4] | lane prefixes u64[256] | lane counts u16[256] | guard | run
+  return ((dsp_pre_off() + 8u * kSpanNF + 4u * kSpanNF + 32u + 16u + 8u * kBlock + 2u * kBlock + 15u) & ~15u) +
+         kVTGuard;
 }
 __host__ __device__ inline uint32_t dsp_lds_bytes(uint32_t cap) { return dsp_img_off() + cap + 32u; }
 
@@ -1094,14 +1125,16 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_span_kernel(VarlenArgs a
   const uint32_t glog = a.glog, G = 1u << glog, T = kBlock >> glog;
   const uint32_t q = tid >> glog, g = tid & (G - 1u);
   const uint32_t nt = (uint32_t)a.span_count;
-  if (*a.span_flag == a.span_epoch) {  // offsets out of order or past the buffer: frame by frame
+  // the flag and the span's two records in one round trip
+  const uint32_t k = blockIdx.x >= nt ? 0u : a.xcd ? xcd_tile(blockIdx.x, nt) : blockIdx.x;
+  const uint32_t flag = *a.span_flag;
+  const SpanRec r0 = a.span_rec[k], r1 = a.span_rec[k + 1];
+  if (flag == a.span_epoch) {  // offsets out of order or past the buffer: frame by frame
     const uint64_t p = (uint64_t)blockIdx.x * T + q;
     if ((uint64_t)blockIdx.x * T < a.n) decode_varlen_frame<H, U8, 4>(a, p, p < a.n, g, glog);
     return;
   }
   if (blockIdx.x >= nt) return;
-  const uint32_t k = a.xcd ? xcd_tile(blockIdx.x, nt) : blockIdx.x;
-  const SpanRec r0 = a.span_rec[k], r1 = a.span_rec[k + 1];
   const uint32_t nf = r1.p - r0.p;
   if (nf == 0) return;
   const uint64_t f0 = r0.p;
@@ -1112,12 +1145,27 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_span_kernel(VarlenArgs a
       decode_varlen_frame<H, U8, 4>(a, f0 + base + q, base + q < nf, g, glog);
     return;
   }
-  uint32_t* lds_fo = reinterpret_cast<uint32_t*>(lds);                                       // [nf + 1]
-  uint32_t* lds_pre = reinterpret_cast<uint32_t*>(lds + (((kSpanNF + 1u) * 4u + 15u) & ~15u));  // [2 nf]
-  unsigned char* lds_hi = reinterpret_cast<unsigned char*>(lds_pre + 2u * kSpanNF);           // [nf]
-  uint64_t* lds_wsum = reinterpret_cast<uint64_t*>((reinterpret_cast<uintptr_t>(lds_hi + kSpanNF) + 7u) & ~(uintptr_t)7u);
+  uint32_t* lds_fo = reinterpret_cast<uint32_t*>(lds);                                      // [nf + 1]
+  uint32_t* lds_pre = reinterpret_cast<uint32_t*>(lds + dsp_pre_off());                         // [2 nf]
+  uint16_t* lds_ph = reinterpret_cast<uint16_t*>(lds_pre + 2u * kSpanNF);                      // [2 nf]
+  uint64_t* lds_wsum = reinterpret_cast<uint64_t*>(lds_ph + 2u * kSpanNF);                     // [4]
+  uint32_t* lds_whc = reinterpret_cast<uint32_t*>(lds_wsum + 4);                               // [4]
+  uint64_t* lds_lex = reinterpret_cast<uint64_t*>(lds_whc + 4);                                // [256]
+  uint16_t* lds_lhc = reinterpret_cast<uint16_t*>(lds_lex + kBlock);                           // [256]
   unsigned char* img = lds + dsp_img_off();
   const uint64_t total = frames_limit(a);
+#if RUDP_TOOLS
+  if (a.diag & 64u) {  // ablation: the loads only
+    const uint32_t nvec = (uint32_t)(run >> 4);
+    u32x4 x = make_u32x4(0ull, 0ull);
+    for (uint32_t v = tid; v < nvec; v += kBlock) {
+      const u32x4 r = load16_guarded(a.frames, A + 16ull * v, total);
+      x.x ^= r.x;
+    }
+    if (x.x == 0x12345678u) a.ok[f0] = 9;
+    return;
+  }
+#endif
   {
     const uint32_t fo_r = tid <= nf ? (uint32_t)(a.frame_off[f0 + tid] - A) : 0u;
     const uint32_t nvec = (uint32_t)(run >> 4);
@@ -1137,84 +1185,98 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_span_kernel(VarlenArgs a
       }
     }
     if (tid <= nf) lds_fo[tid] = fo_r;
-    if (U8 && tid < nf) lds_hi[tid] = 0;
   }
   __syncthreads();
   const u32x4* img16 = reinterpret_cast<const u32x4*>(img);
   const uint32_t nvec = (uint32_t)(run >> 4);
-  // lane tid's chunks; together the lanes cover one chunk past the run, so
-  // every boundary (at most 16 nvec) lies inside some lane's bytes
-  const uint32_t kc = nvec / kBlock + 1u;
+  // Lane tid sums chunks [tid kc, (tid + 1) kc) of the run, whatever frames
+  // they hold (the lanes cover one chunk past the run, so every boundary, at
+  // most 16 nvec, lies in some lane's chunks; kc odd: the 16 lanes of an LDS
+  // pass read 16 different bank groups).  U8: it also counts bytes >= 0x80.
+  const uint32_t kc = (nvec / kBlock + 1u) | 1u;
   const uint32_t c_begin = tid * kc;
-  const uint32_t pos0 = c_begin << 4;
-  // boundary b: payload start of frame b / 2 (even b) or its end (odd b)
-  auto bpos = [&](uint32_t b) -> uint32_t {
-    if (b >= 2u * nf) return 0xFFFFFFFFu;
-    const uint32_t i = b >> 1, fe = lds_fo[i + 1u];
-    if (b & 1u) return fe;
-    const uint32_t ps = lds_fo[i] + (uint32_t)H;
-    return ps < fe ? ps : fe;
+  const uint32_t c_end = c_begin + kc < nvec ? c_begin + kc : nvec;
+  auto hcount = [](const u32x4& w) {
+    return (uint32_t)(__builtin_popcount(w.x & 0x80808080u) + __builtin_popcount(w.y & 0x80808080u) +
+                      __builtin_popcount(w.z & 0x80808080u) + __builtin_popcount(w.w & 0x80808080u));
   };
-  uint32_t lo = 0, hi = nf;  // the first frame ending at or past pos0
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (lds_fo[mid + 1u] >= pos0) hi = mid;
-    else lo = mid + 1u;
-  }
-  uint32_t b = 2u * lo;
-  if (bpos(b) < pos0) ++b;
-  const uint32_t b_first = b;
-  uint32_t nb = bpos(b);
-  uint32_t acc = 0;  // even | odd << 16 byte sums of the lane's chunks so far (at most kc * 2040 each)
-  for (uint32_t c = c_begin; c < c_begin + kc; ++c) {
-    const uint32_t cb = c << 4;
-    const u32x4 w = c < nvec ? img16[c] : make_u32x4(0ull, 0ull);
-    const uint32_t hb = U8 ? high_bits(w) : 0u;
-    uint32_t seg = 0;  // chunk-relative start of the piece before the next boundary
-    while (nb < cb + 16u) {
-      const uint32_t m = nb - cb;
-      const u32x4 head = keep_bytes(w, 0, (int)m);
-      if (U8 && hb && (b & 1u) && m > seg && high_bits(keep_bytes(head, (int)seg, 16))) lds_hi[b >> 1] = 1;
-      lds_pre[b] = acc + eo_sum(lo64(head), hi64(head));
-      seg = m;
-      ++b;
-      nb = bpos(b);
-    }
-    if (U8 && hb && (b & 1u) && high_bits(keep_bytes(w, (int)seg, 16))) lds_hi[b >> 1] = 1;
-    acc += eo_sum(lo64(w), hi64(w));
-  }
-  // exclusive scan of the lanes' (even, odd) sums over the workgroup
-  const uint32_t lane = tid & 63u, wave = tid >> 6;
-  uint32_t se = acc & 0xFFFFu, so = acc >> 16;
-  for (uint32_t d = 1; d < 64u; d <<= 1) {
-    const uint32_t te = (uint32_t)__shfl_up((int)se, d, 64), to = (uint32_t)__shfl_up((int)so, d, 64);
-    if (lane >= d) {
-      se += te;
-      so += to;
+  uint32_t acc = 0, hc = 0;  // even | odd << 16 byte sums (each at most kc * 2040), high bytes
+#if RUDP_TOOLS
+  const uint32_t c_stop = (a.diag & 16u) ? c_begin : c_end;  // ablation: no sums
+#else
+  const uint32_t c_stop = c_end;
+#endif
+  for (uint32_t c0 = c_begin; c0 < c_stop; c0 += 4u) {
+    u32x4 w[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4u; ++u) w[u] = c0 + u < c_stop ? img16[c0 + u] : make_u32x4(0ull, 0ull);
+#pragma unroll
+    for (uint32_t u = 0; u < 4u; ++u) {
+      acc += eo_sum(lo64(w[u]), hi64(w[u]));
+      if (U8) hc += hcount(w[u]);
     }
   }
-  if (lane == 63u) lds_wsum[wave] = (uint64_t)se | ((uint64_t)so << 32);
-  se -= acc & 0xFFFFu;
-  so -= acc >> 16;
-  __syncthreads();
-  for (uint32_t w = 0; w < wave; ++w) {
-    const uint64_t ws = lds_wsum[w];
-    se += (uint32_t)ws;
-    so += (uint32_t)(ws >> 32);
+  // each lane's exclusive prefix within its wave, and the four wave totals
+  {
+    const uint32_t lane = tid & 63u, wave = tid >> 6;
+    uint32_t se = acc & 0xFFFFu, so = acc >> 16, sh = hc;
+    for (uint32_t d = 1; d < 64u; d <<= 1) {
+      const uint32_t te = (uint32_t)__shfl_up((int)se, d, 64), to = (uint32_t)__shfl_up((int)so, d, 64);
+      const uint32_t th = U8 ? (uint32_t)__shfl_up((int)sh, d, 64) : 0u;
+      if (lane >= d) {
+        se += te;
+        so += to;
+        sh += th;
+      }
+    }
+    if (lane == 63u) {
+      lds_wsum[wave] = (uint64_t)se | ((uint64_t)so << 32);
+      if (U8) lds_whc[wave] = sh;
+    }
+    lds_lex[tid] = (uint64_t)(se - (acc & 0xFFFFu)) | ((uint64_t)(so - (acc >> 16)) << 32);
+    if (U8) lds_lhc[tid] = (uint16_t)(sh - hc);  // (at most 63 * 16 kc)
   }
-  // this lane's boundaries: absolute prefixes, weighted by their frame's
-  // start parity (even offsets are high bytes iff the frame starts even)
-  for (uint32_t s = b_first; s < b; ++s) {
-    const uint32_t loc = lds_pre[s];
-    const uint32_t e = se + (loc & 0xFFFFu), o = so + (loc >> 16);
-    lds_pre[s] = (lds_fo[s >> 1] & 1u) ? e + (o << 8) : (e << 8) + o;
+  __syncthreads();
+  // Boundary b = tid: payload start of frame b / 2 (even b) or its end (odd
+  // b).  The run's sums before it = its lane's prefix + that lane's chunks up
+  // to it (at most kc reads, issued four at a time), weighted by the frame's
+  // start parity (even offsets are high bytes iff the frame starts even).
+  if (tid < 2u * nf) {
+    const uint32_t i = tid >> 1, fs = lds_fo[i], fe = lds_fo[i + 1u];
+    const uint32_t x = (tid & 1u) ? fe : (fs + (uint32_t)H < fe ? fs + (uint32_t)H : fe);
+    const uint32_t cx = x >> 4, L = cx / kc;
+    uint32_t loc = 0, lh = 0;
+    for (uint32_t c0 = L * kc; c0 <= cx; c0 += 4u) {
+      u32x4 w[4];
+#pragma unroll
+      for (uint32_t u = 0; u < 4u; ++u) {
+        const uint32_t c = c0 + u;
+        w[u] = c <= cx && c < nvec ? img16[c] : make_u32x4(0ull, 0ull);
+      }
+#pragma unroll
+      for (uint32_t u = 0; u < 4u; ++u) {
+        const uint32_t c = c0 + u;
+        const u32x4 v = c == cx ? keep_bytes(w[u], 0, (int)(x & 15u)) : w[u];
+        loc += eo_sum(lo64(v), hi64(v));
+        if (U8) lh += hcount(v);
+      }
+    }
+    uint64_t p = lds_lex[L];
+    uint32_t ph = U8 ? lds_lhc[L] : 0u;
+    for (uint32_t w = 0; w < (L >> 6); ++w) {
+      p += lds_wsum[w];
+      if (U8) ph += lds_whc[w];
+    }
+    const uint32_t e = (uint32_t)p + (loc & 0xFFFFu), o = (uint32_t)(p >> 32) + (loc >> 16);
+    lds_pre[tid] = (fs & 1u) ? e + (o << 8) : (e << 8) + o;
+    if (U8) lds_ph[tid] = (uint16_t)(ph + lh);
   }
   __syncthreads();
-  if (U8) {  // frames with a high bit in their payload: the byte checks, G lanes each, from LDS
+  if (U8) {  // frames with a byte >= 0x80 in their payload: the byte checks, G lanes each, from LDS
     const uint32_t* idw = reinterpret_cast<const uint32_t*>(img);  // kVTGuard bytes before it
     for (uint32_t base = 0; base < nf; base += T) {
       const uint32_t i = base + q;
-      const bool flagged = i < nf && lds_hi[i];
+      const bool flagged = i < nf && lds_ph[2u * i + 1u] != lds_ph[2u * i];
       if (__any(flagged)) {
         uint32_t bad = 0;
         if (flagged) {
@@ -1228,9 +1290,12 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_span_kernel(VarlenArgs a
       }
     }
   }
+#if RUDP_TOOLS
+  if (a.diag & 32u) return;  // ablation: no leaders' work
+#endif
   if (tid < nf) {
     const uint32_t fs = lds_fo[tid], fe = lds_fo[tid + 1u];
-    if (U8 && !lds_hi[tid]) a.valid[f0 + tid] = 1;
+    if (U8 && lds_ph[2u * tid + 1u] == lds_ph[2u * tid]) a.valid[f0 + tid] = 1;
     decode_varlen_finish<H>(a, f0 + tid, fe - fs, lds_pre[2u * tid + 1u] - lds_pre[2u * tid],
                             window16_dw(reinterpret_cast<const uint32_t*>(img), fs));
   }

@@ -211,3 +211,33 @@ def test_huge_frames_fold_like_the_reference(cuda, H):
     torch.cuda.synchronize()
     for k in out:
         assert np.array_equal(out[k].cpu().numpy(), want[k]), (k, "byte kernel")
+
+
+@pytest.mark.parametrize("bal", [1, 0])
+def test_encode_chunk_map_by_units(cuda, bal):
+    """The varlen encode tile's chunk map built by output units spread over the
+    lanes (rudpx_tune 67 = 1) or by G lanes per frame (0): ragged payloads of
+    0-2944 B with runs of empty and short ones (the coded map's header-chunk
+    classes and the frame walk), equal to the oracle's frames byte for byte."""
+    import torch
+    from oracle import synth
+    from rudp import batch
+    rng = np.random.default_rng(6900 + bal)
+    n = 30000
+    lens = rng.integers(0, 2945, n).astype(np.int32)
+    lens[1000:1400] = rng.integers(0, 40, 400)
+    lens[5000:5100] = 0
+    pay = rng.integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    seq, ack, flags, _ = synth.synth(bal + 5, 0, n, 0)
+    pays = [bytes(pay[o:o + k]) for o, k in zip(np.concatenate([[0], np.cumsum(lens)[:-1]]), lens)]
+    want, want_off, _ = codec_np.encode_varlen(seq, ack, flags, pays, 7)
+    lib = _native.tools_lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    old = lib.rudpx_tune(67, bal)
+    try:
+        tab = tuple(torch.from_numpy(a).to(cuda) for a in (seq, ack, flags))
+        res = batch.pack_batch_varlen(tab, torch.from_numpy(pay).to(cuda), torch.from_numpy(lens).to(cuda), "rudp7")
+        assert np.array_equal(res.frames.cpu().numpy(), want)
+        assert np.array_equal(res.frame_off.cpu().numpy(), want_off)
+    finally:
+        lib.rudpx_tune(67, old)
