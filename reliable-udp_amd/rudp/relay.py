@@ -57,7 +57,7 @@ class Relay(threading.Thread):
 
     def __init__(self, server_port: int, drop: Optional[Callable[[str, int], bool]] = None,
                  host: str = "127.0.0.1", batched: bool = False, device=None, max_msgs: int = 1024,
-                 keep_log: bool = True):
+                 keep_log: bool = True, forwarders: int = 1):
         super().__init__(daemon=True)
         self.sock = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
         self.sock.bind((host, 0))
@@ -76,6 +76,13 @@ class Relay(threading.Thread):
         self.stop_event = threading.Event()
         self.batched = batched
         self.batches = 0
+        # Batched: sendmmsg threads (batches leave in the order the threads
+        # reach the kernel, as the reference's executor workers send them,
+        # proxy.py:127, :154).  One is the default: the hop costs ~1.2 us per
+        # datagram in the kernel's send path of the one socket, and 2 or 3
+        # threads on it measured no faster (0.64-0.79 vs 0.78 M/s,
+        # profiles/r04/sweeps/relay_forwarders.json).
+        self.forwarders = max(1, int(forwarders))
         if batched:
             import torch
             self._device = torch.device(device) if device is not None else torch.device("cuda", 0)
@@ -218,19 +225,22 @@ class Relay(threading.Thread):
     def _run_batched(self) -> None:
         import queue
         from . import netio
-        rx = netio.BatchReceiver(self.sock, max_msgs=self._max_msgs, slot_bytes=SLOT_BYTES, slots=4,
+        rx = netio.BatchReceiver(self.sock, max_msgs=self._max_msgs, slot_bytes=SLOT_BYTES, slots=2 + 2 * self.forwarders,
                                  device=self._device, stream=self._stream, with_sources=True)
         q: "queue.Queue" = queue.Queue()
-        fwd = threading.Thread(target=self._forward, args=(q, rx), daemon=True)
-        fwd.start()
+        fwd = [threading.Thread(target=self._forward, args=(q, rx), daemon=True) for _ in range(self.forwarders)]
+        for t in fwd:
+            t.start()
         try:
             while not self.stop_event.is_set():
                 k = rx.recv(timeout_ms=50)
                 if k:
                     self._relay_batch(rx.frames, rx.frame_off[:k + 1], rx.sources, rx=rx, send_q=q)
         finally:
-            q.put(None)
-            fwd.join()
+            for _ in fwd:
+                q.put(None)
+            for t in fwd:
+                t.join()
 
     def run(self) -> None:
         if self.batched:

@@ -7,7 +7,7 @@ bookkeeping and the GPU enqueue), the forwarding thread's sendmmsg, and the
 sink's recvmmsg.  Prints one JSON line: seconds and calls per phase, and the
 datagrams/s.
 
-usage: python tools/relay_probe.py [--n 262144] [--max-msgs 1024]
+usage: python tools/relay_probe.py [--n 262144] [--max-msgs 1024] [--switch 0.0002]
 """
 from __future__ import annotations
 
@@ -46,7 +46,11 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--n", type=int, default=1 << 18)
     ap.add_argument("--max-msgs", type=int, default=1024)
+    ap.add_argument("--forwarders", type=int, default=2)
+    ap.add_argument("--switch", type=float, default=0.0, help="sys.setswitchinterval (s); 0 keeps the default")
     args = ap.parse_args()
+    if args.switch > 0:
+        sys.setswitchinterval(args.switch)
     dev = torch.device("cuda", 0)
     n = args.n
     tab, pay = batch.synth_batch(n, 1, 0x5EED0004, device=dev)
@@ -61,7 +65,8 @@ def main():
     sink = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
     sink.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 26)
     sink.bind(("127.0.0.1", 0))
-    r = relay.Relay(sink.getsockname()[1], batched=True, device=dev, keep_log=False, max_msgs=args.max_msgs)
+    r = relay.Relay(sink.getsockname()[1], batched=True, device=dev, keep_log=False, max_msgs=args.max_msgs,
+                    forwarders=args.forwarders)
     r.sock.setsockopt(socket.SOL_SOCKET, socket.SO_RCVBUF, 1 << 26)
     r.start()
     tx = socket.socket(socket.AF_INET, socket.SOCK_DGRAM)
@@ -86,7 +91,7 @@ def main():
     t.join()
     dt = time.perf_counter() - t0 - 0.5
     r.stop()
-    print(json.dumps({"n": n, "relayed": got[0], "wall_s": dt, "Mpkt_s": got[0] / dt / 1e6,
+    print(json.dumps({"n": n, "switch_s": sys.getswitchinterval(), "forwarders": args.forwarders, "relayed": got[0], "wall_s": dt, "Mpkt_s": got[0] / dt / 1e6,
                       "batches": r.batches, "phases_s_calls": {k: [round(v[0], 4), v[1]] for k, v in T.items()}}))
 
 
