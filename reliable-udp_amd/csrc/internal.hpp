@@ -166,6 +166,7 @@ struct VarlenArgs {
   uint32_t span_epoch;
   uint32_t span_S;
   uint32_t map_bal;               // encode tile: chunk map built by output units, not by frames
+  uint32_t dec_nt;                // decode tile: threads per workgroup (256, or 128: two-wave tiles)
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -341,6 +342,8 @@ struct Tuning {
   // Varlen encode tile: the chunk -> frame map built by output units spread
   // evenly over the lanes (1) instead of G lanes per frame (0).
   RUDP_KNOB(varlen_map_bal, 0)
+  // Varlen decode tile workgroup size: 256 (T = 256 / G frames) or 128.
+  RUDP_KNOB(varlen_decode_nt, 256)
   // Fixed-length encode: batches of more packets than this go out as several
   // launches of at most this many (0: one launch).
   RUDP_KNOB(encode_launch_packets, 0)

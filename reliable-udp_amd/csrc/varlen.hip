@@ -937,11 +937,11 @@ __device__ __forceinline__ uint32_t octet_or(uint32_t x) {
   return x;
 }
 
-template <int H, bool U8>
-__global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a) {
+template <int H, bool U8, uint32_t NT = kBlock>
+__global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const uint32_t tid = threadIdx.x;
-  const uint32_t glog = a.glog, G = 1u << glog, T = kBlock >> glog;
+  const uint32_t glog = a.glog, G = 1u << glog, T = NT >> glog;
   const uint32_t q = tid >> glog, g = tid & (G - 1u);
   uint32_t* lds_fo = reinterpret_cast<uint32_t*>(lds);                       // [T + 1]
   unsigned char* img = lds + ((((T + 1u) * 4u) + 15u) & ~15u) + kVTGuard;   // the run
@@ -955,7 +955,7 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
   const uint64_t A = fo0 & ~15ull;
   const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
   if (fo0 > fo_end || fo_end > total || run > a.tile_cap) {  // uniform over the workgroup
-    decode_varlen_frame<H, U8>(a, p0 + q, q < Tv, g, glog);
+    decode_varlen_frame<H, U8, 6>(a, p0 + q, q < Tv, g, glog);
     return;
   }
   // tile-relative offsets; one outside [A, fo_end] reads as 0xFFFFFFFF
@@ -967,16 +967,16 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
     const uint32_t nvec = (uint32_t)(run >> 4);
     u32x4* dst = reinterpret_cast<u32x4*>(img);
     constexpr uint32_t P = 8;
-    for (uint32_t v0 = tid; v0 < nvec; v0 += P * kBlock) {
+    for (uint32_t v0 = tid; v0 < nvec; v0 += P * NT) {
       u32x4 r[P];
 #pragma unroll
       for (uint32_t u = 0; u < P; ++u) {
-        const uint32_t v = v0 + u * kBlock;
+        const uint32_t v = v0 + u * NT;
         if (v < nvec) r[u] = load16_guarded(a.frames, A + 16ull * v, total);
       }
 #pragma unroll
       for (uint32_t u = 0; u < P; ++u) {
-        const uint32_t v = v0 + u * kBlock;
+        const uint32_t v = v0 + u * NT;
         if (v < nvec) dst[v] = r[u];
         // block sums from the registers: whole 128-B blocks only (uniform per 8
         // lanes; a partial last block is only ever an edge block of a frame)
@@ -990,7 +990,7 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
     if (a.early_fo) {
       if (tid <= Tv) lds_fo[tid] = fo_r;
     } else {
-      for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = rel(a.frame_off[p0 + i]);
+      for (uint32_t i = tid; i <= Tv; i += NT) lds_fo[i] = rel(a.frame_off[p0 + i]);
     }
   }
   __syncthreads();
@@ -1002,7 +1002,7 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_tile_kernel(VarlenArgs a
     // the rule is applied to its true offsets.  Uniform over the frame's lanes.
     const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
     if (fs > fe || fe > (uint32_t)span_end) {
-      decode_varlen_frame<H, U8>(a, p0 + q, true, g, glog);
+      decode_varlen_frame<H, U8, 6>(a, p0 + q, true, g, glog);
       return;
     }
   }
@@ -2215,6 +2215,12 @@ static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
       // 76 VGPRs (6 waves per SIMD).  Asking the allocator for 7 or 8 waves
       // spills and was slower at every size (1M x 1479 B 0.265 -> 0.306 ms;
       // profiles/r01/sweeps/varlen_decode_waves.json).
+      if (args.dec_nt == 128u) {  // two-wave tiles: a tile's LDS waits for the slower of two waves, not four
+        const uint64_t b128 = (args.n + (128u >> args.glog) - 1) / (128u >> args.glog);
+        hipLaunchKernelGGL((decode_varlen_tile_kernel<H, U8, 128u>), dim3((uint32_t)b128), dim3(128), lds, stream,
+                           args);
+        return (int)hipGetLastError();
+      }
       hipLaunchKernelGGL((decode_varlen_tile_kernel<H, U8>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
       return (int)hipGetLastError();
     }
