@@ -381,6 +381,7 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
     }
     const uint64_t pct = (uint64_t)tuning().varlen_decode_cap_pct;
     a.dec_nt = tuning().varlen_decode_nt == 128 ? 128u : 256u;
+    a.dec_r4 = tuning().varlen_decode_r4 ? 1u : 0u;
     const uint64_t cap = (((a.dec_nt >> lg) * hint * pct / 100u + 256u) + 15u) & ~15ull;
     a.tile_cap = cap <= 49152u ? (uint32_t)cap : 0u;
   }

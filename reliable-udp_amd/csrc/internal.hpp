@@ -167,6 +167,7 @@ struct VarlenArgs {
   uint32_t span_S;
   uint32_t map_bal;               // encode tile: chunk map built by output units, not by frames
   uint32_t dec_nt;                // decode tile: threads per workgroup (256, or 128: two-wave tiles)
+  uint32_t dec_r4;                // decode tile: payload chunks read four at a time
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -344,6 +345,9 @@ struct Tuning {
   RUDP_KNOB(varlen_map_bal, 0)
   // Varlen decode tile workgroup size: 256 (T = 256 / G frames) or 128.
   RUDP_KNOB(varlen_decode_nt, 256)
+  // Varlen decode tile: a lane's payload chunks read four at a time (1) or
+  // one at a time (0).
+  RUDP_KNOB(varlen_decode_r4, 0)
   // Fixed-length encode: batches of more packets than this go out as several
   // launches of at most this many (0: one launch).
   RUDP_KNOB(encode_launch_packets, 0)

@@ -937,7 +937,10 @@ __device__ __forceinline__ uint32_t octet_or(uint32_t x) {
   return x;
 }
 
-template <int H, bool U8, uint32_t NT = kBlock>
+// R4: a lane reads its payload chunks four at a time (one LDS wait per four
+// instead of one per chunk: the longest frame's chain of LDS round trips is
+// what a wave of ragged lengths waits for).
+template <int H, bool U8, uint32_t NT = kBlock, bool R4 = false>
 __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const uint32_t tid = threadIdx.x;
@@ -994,77 +997,90 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
     }
   }
   __syncthreads();
-  if (q >= Tv) return;
-  {
+  const uint32_t glog2 = glog, G2 = G, q2 = q, g2 = g;
+  const u32x4* img16 = reinterpret_cast<const u32x4*>(img);
+  auto frame = [&](const uint32_t q) {
+    const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
     // A pair out of order, or an offset outside the tile's run: the frame may
     // still be valid (its own pair in order and inside the buffer is all the
     // rule asks) but reach past the staged bytes, so it decodes from HBM, where
     // the rule is applied to its true offsets.  Uniform over the frame's lanes.
-    const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
     if (fs > fe || fe > (uint32_t)span_end) {
-      decode_varlen_frame<H, U8, 6>(a, p0 + q, true, g, glog);
+      decode_varlen_frame<H, U8, 6>(a, p0 + q, true, g2, glog2);
       return;
     }
-  }
-  const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
-  const u32x4* img16 = reinterpret_cast<const u32x4*>(img);
-  uint32_t even_sum = 0, odd_sum = 0;  // byte sums at even / odd offsets (A is even)
-  uint32_t hib = 0;                     // U8: high bits of the payload bytes
-  const uint32_t ps = fs + (uint32_t)H;
-  if (blk && fe > ps) {
-    // the 16 chunks of the blocks holding the payload's first and last bytes
-    // (each masked to the payload), then the block words between
-    const uint32_t j0 = ps >> 7, j1 = (fe - 1u) >> 7;
-    for (uint32_t c = g; c < 16u; c += G) {
-      const uint32_t cx = ((c < 8u ? j0 : j1) << 7) + ((c & 7u) << 4);
-      if ((c < 8u || j1 != j0) && cx < fe && cx + 16u > ps) {
-        const u32x4 w = keep_bytes(img16[cx >> 4], (int)ps - (int)cx, (int)fe - (int)cx);
-        const uint32_t eo = eo_sum(lo64(w), hi64(w));
-        even_sum += eo & 0xFFFFu;
-        odd_sum += eo >> 16;
+    uint32_t even_sum = 0, odd_sum = 0;  // byte sums at even / odd offsets (A is even)
+    uint32_t hib = 0;                     // U8: high bits of the payload bytes
+    const uint32_t ps = fs + (uint32_t)H;
+    if (blk && fe > ps) {
+      // the 16 chunks of the blocks holding the payload's first and last bytes
+      // (each masked to the payload), then the block words between
+      const uint32_t j0 = ps >> 7, j1 = (fe - 1u) >> 7;
+      for (uint32_t c = g2; c < 16u; c += G2) {
+        const uint32_t cx = ((c < 8u ? j0 : j1) << 7) + ((c & 7u) << 4);
+        if ((c < 8u || j1 != j0) && cx < fe && cx + 16u > ps) {
+          const u32x4 w = keep_bytes(img16[cx >> 4], (int)ps - (int)cx, (int)fe - (int)cx);
+          const uint32_t eo = eo_sum(lo64(w), hi64(w));
+          even_sum += eo & 0xFFFFu;
+          odd_sum += eo >> 16;
+          if (U8) hib |= w.x | w.y | w.z | w.w;
+        }
+      }
+      for (uint32_t j = j0 + 1u + g2; j < j1; j += G2) {
+        const uint32_t bs = lds_blk[j];
+        even_sum += bs & 0x7FFFu;
+        odd_sum += bs >> 16;
+        if (U8) hib |= (bs & 0x8000u) ? 0x80u : 0u;
+      }
+    } else if (fe > ps) {  // the payload's chunks, the edge ones masked to it
+      const uint32_t c0 = ps >> 4, c1 = (fe - 1u) >> 4;
+      auto add = [&](u32x4 w, uint32_t c) {
+        if (c == c0 || c == c1) w = keep_bytes(w, (int)ps - (int)(c << 4), (int)fe - (int)(c << 4));
         if (U8) hib |= w.x | w.y | w.z | w.w;
+        const uint32_t e = (w.x & 0x00FF00FFu) + (w.y & 0x00FF00FFu) + (w.z & 0x00FF00FFu) + (w.w & 0x00FF00FFu);
+        const uint32_t o = ((w.x >> 8) & 0x00FF00FFu) + ((w.y >> 8) & 0x00FF00FFu) +
+                           ((w.z >> 8) & 0x00FF00FFu) + ((w.w >> 8) & 0x00FF00FFu);
+        even_sum += (e & 0xFFFFu) + (e >> 16);
+        odd_sum += (o & 0xFFFFu) + (o >> 16);
+      };
+      if (R4) {
+        for (uint32_t c = c0 + g2; c <= c1; c += 4u * G2) {
+          u32x4 w[4];
+#pragma unroll
+          for (uint32_t u = 0; u < 4u; ++u) {
+            const uint32_t cu = c + u * G2;
+            w[u] = cu <= c1 ? img16[cu] : make_u32x4(0ull, 0ull);
+          }
+#pragma unroll
+          for (uint32_t u = 0; u < 4u; ++u)
+            if (c + u * G2 <= c1) add(w[u], c + u * G2);
+        }
+      } else {
+        for (uint32_t c = c0 + g2; c <= c1; c += G2) add(img16[c], c);
       }
     }
-    for (uint32_t j = j0 + 1u + g; j < j1; j += G) {
-      const uint32_t bs = lds_blk[j];
-      even_sum += bs & 0x7FFFu;
-      odd_sum += bs >> 16;
-      if (U8) hib |= (bs & 0x8000u) ? 0x80u : 0u;
+    // even offsets are high bytes iff the frame starts at an even offset
+    uint32_t sum = (fs & 1u) ? (even_sum + (odd_sum << 8)) : ((even_sum << 8) + odd_sum);
+    for (uint32_t m = G2 >> 1; m > 0; m >>= 1) {
+      sum += __shfl_xor(sum, (int)m, 64);
+      if (U8) hib |= (uint32_t)__shfl_xor((int)hib, (int)m, 64);
     }
-  } else if (fe > ps) {  // the payload's chunks, the edge ones masked to it
-    const uint32_t c0 = ps >> 4, c1 = (fe - 1u) >> 4;
-    for (uint32_t c = c0 + g; c <= c1; c += G) {
-      u32x4 w = img16[c];
-      if (c == c0 || c == c1) w = keep_bytes(w, (int)ps - (int)(c << 4), (int)fe - (int)(c << 4));
-      if (U8) hib |= w.x | w.y | w.z | w.w;
-      const uint32_t e = (w.x & 0x00FF00FFu) + (w.y & 0x00FF00FFu) + (w.z & 0x00FF00FFu) + (w.w & 0x00FF00FFu);
-      const uint32_t o = ((w.x >> 8) & 0x00FF00FFu) + ((w.y >> 8) & 0x00FF00FFu) +
-                         ((w.z >> 8) & 0x00FF00FFu) + ((w.w >> 8) & 0x00FF00FFu);
-      even_sum += (e & 0xFFFFu) + (e >> 16);
-      odd_sum += (o & 0xFFFFu) + (o >> 16);
-    }
-  }
-  // even offsets are high bytes iff the frame starts at an even offset
-  uint32_t sum = (fs & 1u) ? (even_sum + (odd_sum << 8)) : ((even_sum << 8) + odd_sum);
-  for (uint32_t m = G >> 1; m > 0; m >>= 1) {
-    sum += __shfl_xor(sum, (int)m, 64);
-    if (U8) hib |= (uint32_t)__shfl_xor((int)hib, (int)m, 64);
-  }
-  if (U8) {  // a frame with a high bit in its payload: the byte checks, from LDS
-    uint32_t u8bad = 0;
-    if (__any((hib & 0x80808080u) != 0)) {
-      if (hib & 0x80808080u) {
-        const uint32_t* idw = reinterpret_cast<const uint32_t*>(img);  // kVTGuard bytes before it
-        u8bad = utf8_check_frame(ps, fe, g, G, [&](uint64_t c) { return img16[c]; },
-                                 [&](uint64_t x) { return idw[(int64_t)(x >> 2) - 1]; });
+    if (U8) {  // a frame with a high bit in its payload: the byte checks, from LDS
+      uint32_t u8bad = 0;
+      if (__any((hib & 0x80808080u) != 0)) {
+        if (hib & 0x80808080u) {
+          const uint32_t* idw = reinterpret_cast<const uint32_t*>(img);  // kVTGuard bytes before it
+          u8bad = utf8_check_frame(ps, fe, g2, G2, [&](uint64_t c) { return img16[c]; },
+                                   [&](uint64_t x) { return idw[(int64_t)(x >> 2) - 1]; });
+        }
+        u8bad = group_or(u8bad, G2);
       }
-      u8bad = group_or(u8bad, G);
+      if (g2 == 0) a.valid[p0 + q] = u8bad ? 0 : 1;
     }
-    if (g == 0) a.valid[p0 + q] = u8bad ? 0 : 1;
-  }
-  if (g == 0)
-    decode_varlen_finish<H>(a, p0 + q, fe - fs,
-                            sum, window16_dw(reinterpret_cast<const uint32_t*>(img), fs));
+    if (g2 == 0)
+      decode_varlen_finish<H>(a, p0 + q, fe - fs, sum, window16_dw(reinterpret_cast<const uint32_t*>(img), fs));
+  };
+  if (q2 < Tv) frame(q2);
 }
 
 // ---------------------------------------------------------------------------
@@ -2215,6 +2231,11 @@ static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
       // 76 VGPRs (6 waves per SIMD).  Asking the allocator for 7 or 8 waves
       // spills and was slower at every size (1M x 1479 B 0.265 -> 0.306 ms;
       // profiles/r01/sweeps/varlen_decode_waves.json).
+      if (args.dec_r4) {
+        hipLaunchKernelGGL((decode_varlen_tile_kernel<H, U8, kBlock, true>), dim3((uint32_t)blocks), dim3(kBlock),
+                           lds, stream, args);
+        return (int)hipGetLastError();
+      }
       if (args.dec_nt == 128u) {  // two-wave tiles: a tile's LDS waits for the slower of two waves, not four
         const uint64_t b128 = (args.n + (128u >> args.glog) - 1) / (128u >> args.glog);
         hipLaunchKernelGGL((decode_varlen_tile_kernel<H, U8, 128u>), dim3((uint32_t)b128), dim3(128), lds, stream,

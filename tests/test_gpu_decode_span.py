@@ -241,3 +241,30 @@ def test_encode_chunk_map_by_units(cuda, bal):
         assert np.array_equal(res.frame_off.cpu().numpy(), want_off)
     finally:
         lib.rudpx_tune(67, old)
+
+
+@pytest.mark.parametrize("r4", [1, 0])
+@pytest.mark.parametrize("H", [5, 7])
+def test_decode_tile_chunk_reads(cuda, r4, H):
+    """The varlen decode tile's payload chunks read four at a time per lane
+    (rudpx_tune 69 = 1) or one at a time (0): ragged, short, empty and out-of-order
+    frames at the hints that pick 16, 8, 4 and 2 lanes per frame, equal to
+    the oracle (fields, checksums, UTF-8 verdicts, rejections)."""
+    lib = _native.tools_lib()
+    lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
+    old = lib.rudpx_tune(69, r4)
+    try:
+        rng = np.random.default_rng(6900 + 10 * r4 + H)
+        lens = list(rng.integers(0, 2945, 6000))
+        lens[100:400] = list(rng.integers(0, 30, 300))
+        frames = _frames(rng, lens, H)
+        off = _offsets(frames)
+        off[3001] = off[3002] + 2          # a decreasing pair inside a tile
+        flat = np.frombuffer(b"".join(frames), np.uint8)
+        want, _ = _want(flat, off, H, len(flat))
+        for hint in (200, 700, 1472, 3000):
+            got, _ = _decode(cuda, flat, off, len(frames), hint, H, True)
+            for k in want:
+                assert np.array_equal(got[k], want[k]), (k, hint, r4)
+    finally:
+        lib.rudpx_tune(69, old)
