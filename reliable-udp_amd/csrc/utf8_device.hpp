@@ -61,40 +61,53 @@ __device__ __forceinline__ uint32_t group_or(uint32_t bits, uint32_t G) {
   return bits;
 }
 
-// 16-entry byte table lookup for the four bytes of `idx` (each 0..15):
-// two v_perm_b32 over the table's halves, the half picked by bit 3.
-__device__ __forceinline__ uint32_t lookup16(uint32_t t0, uint32_t t1, uint32_t t2, uint32_t t3, uint32_t idx) {
-  const uint32_t sel = idx & 0x07070707u;
-  const uint32_t lo = __builtin_amdgcn_perm(t1, t0, sel), hi = __builtin_amdgcn_perm(t3, t2, sel);
-  const uint32_t b = idx & 0x08080808u;
-  const uint32_t m = (b << 5) - (b >> 3);  // 0xFF in every byte whose bit 3 is set (no multiply)
-  return (hi & m) | (lo & ~m);
+// Per-dword inputs of the table check, computed once per dword and shared by
+// the dword's own check and the next one's (which needs the bytes before
+// it): the low / high nibbles' table selectors (bits 0-2) and their bit-3
+// blend masks (0xFF per byte whose nibble is 8-15), and bit 7 of every byte
+// >= 0xE0 / >= 0xF0 (a 3- / 4-byte lead).
+struct Utf8Pre {
+  uint32_t sel_lo, m_lo, sel_hi, m_hi, e0, f0;
+};
+__device__ __forceinline__ Utf8Pre utf8_pre(uint32_t x) {
+  Utf8Pre p;
+  p.sel_lo = x & 0x07070707u;
+  const uint32_t bl = x & 0x08080808u;
+  p.m_lo = (bl << 5) - (bl >> 3);  // 0xFF in every byte whose bit 3 is set (no multiply)
+  p.sel_hi = (x >> 4) & 0x07070707u;
+  const uint32_t bh = x & 0x80808080u;
+  p.m_hi = (bh << 1) - (bh >> 7);  // the same for bit 7
+  const uint32_t e = x & (x << 1) & (x << 2) & 0x80808080u;
+  p.e0 = e;
+  p.f0 = e & (x << 3);
+  return p;
 }
 
-// Bytes of `x` that are >= 0xE0 (p2 must be followed by two continuations) or,
-// for `four`, >= 0xF0: bit 7 of each such byte.
-__device__ __forceinline__ uint32_t at_least_e0(uint32_t x) { return x & (x << 1) & (x << 2) & 0x80808080u; }
-__device__ __forceinline__ uint32_t at_least_f0(uint32_t x) { return at_least_e0(x) & (x << 3); }
-
-// Error bits of four bytes `cur` given the four before them, `prev` (SWAR form
-// of the lookup validator of Keiser & Lemire, "Validating UTF-8 in less than
-// one instruction per byte"): every byte is checked against the byte before
-// it through three 16-entry tables of the nibbles (too short, too long,
-// overlong 2/3/4, surrogate, too large, two continuations), and against the
-// two and three before it for the continuations a 3- or 4-byte lead asks for.
-// Nonzero iff some byte of `cur` breaks strict UTF-8 given its predecessors.
-__device__ __forceinline__ uint32_t utf8_dword_errors(uint32_t cur, uint32_t prev) {
-  const uint32_t p1 = __builtin_amdgcn_alignbyte(cur, prev, 3);
-  const uint32_t p2 = __builtin_amdgcn_alignbyte(cur, prev, 2);
-  const uint32_t p3 = __builtin_amdgcn_alignbyte(cur, prev, 1);
-  // tables: byte 1's high nibble, byte 1's low nibble, byte 2's high nibble
-  // (bits: 0 too short, 1 too long, 2 overlong 3, 3 too large, 4 surrogate,
-  // 5 overlong 2, 6 too large 1000 / overlong 4, 7 two continuations)
-  const uint32_t sc = lookup16(0x02020202u, 0x02020202u, 0x80808080u, 0x49150121u, (p1 >> 4) & 0x0F0F0F0Fu) &
-                      lookup16(0x8383A3E7u, 0xCBCBCB8Bu, 0xCBCBCBCBu, 0xCBCBDBCBu, p1 & 0x0F0F0F0Fu) &
-                      lookup16(0x01010101u, 0x01010101u, 0xBABAAEE6u, 0x01010101u, (cur >> 4) & 0x0F0F0F0Fu);
-  const uint32_t must23 = at_least_e0(p2) | at_least_f0(p3);
-  return must23 ^ sc;
+// Error bits of the four bytes of a dword (`c`: utf8_pre of it) given the four
+// before it (`p`), the SWAR form of the lookup validator of Keiser & Lemire
+// ("Validating UTF-8 in less than one instruction per byte"): every byte is
+// checked against the byte before it through three 16-entry tables of the
+// nibbles (too short, too long, overlong 2/3/4, surrogate, too large, two
+// continuations), two v_perm_b32 per table over its halves and a v_bfi by
+// bit 3 (one perm where a half is constant), and against the two and three
+// before it for the continuations a 3- or 4-byte lead asks for.  Nonzero iff
+// some byte breaks strict UTF-8 given its predecessors.
+__device__ __forceinline__ uint32_t utf8_dword_errors(const Utf8Pre& c, const Utf8Pre& p) {
+  // table bits: 0 too short, 1 too long, 2 overlong 3, 3 too large, 4 surrogate,
+  // 5 overlong 2, 6 too large 1000 / overlong 4, 7 two continuations
+  const uint32_t s1 = __builtin_amdgcn_alignbyte(c.sel_hi, p.sel_hi, 3);  // byte 1 = the byte before
+  const uint32_t m1 = __builtin_amdgcn_alignbyte(c.m_hi, p.m_hi, 3);
+  const uint32_t sl = __builtin_amdgcn_alignbyte(c.sel_lo, p.sel_lo, 3);
+  const uint32_t ml = __builtin_amdgcn_alignbyte(c.m_lo, p.m_lo, 3);
+  // byte 1's high nibble: 0-7 all 0x02 (too long), 8-15 from the second half
+  const uint32_t t1 = (m1 & __builtin_amdgcn_perm(0x49150121u, 0x80808080u, s1)) | (~m1 & 0x02020202u);
+  // byte 1's low nibble: all 16 entries
+  const uint32_t t2 = (ml & __builtin_amdgcn_perm(0xCBCBDBCBu, 0xCBCBCBCBu, sl)) |
+                      (~ml & __builtin_amdgcn_perm(0xCBCBCB8Bu, 0x8383A3E7u, sl));
+  // byte 2's (this byte's) high nibble: 0-7 and 12-15 all 0x01 (too short)
+  const uint32_t t3 = (c.m_hi & __builtin_amdgcn_perm(0x01010101u, 0xBABAAEE6u, c.sel_hi)) | (~c.m_hi & 0x01010101u);
+  const uint32_t must23 = __builtin_amdgcn_alignbyte(c.e0, p.e0, 2) | __builtin_amdgcn_alignbyte(c.f0, p.f0, 1);
+  return must23 ^ (t1 & t2 & t3);
 }
 
 // Strict UTF-8 check of one frame's payload bytes [s, fe) by G lanes (lane g
@@ -114,13 +127,19 @@ __device__ __forceinline__ uint32_t utf8_check_frame(uint64_t s, uint64_t fe, ui
   for (uint64_t c = c_lo + g; c <= c_hi && !bad; c += G) {  // a lane stops at its first invalid chunk
     const uint64_t x = c << 4;
     const int lo_b = (int)((int64_t)s - (int64_t)x), hi_b = (int)((int64_t)fe - (int64_t)x);
-    const u32x4 v = keep_bytes(chunk(c), lo_b, hi_b);
+    // an inner chunk (it and the four bytes before it all payload) needs no masks
+    const bool inner = lo_b <= -4 && hi_b >= 16;
+    const u32x4 raw = chunk(c);
+    const u32x4 v = inner ? raw : keep_bytes(raw, lo_b, hi_b);
     // the three bytes before the chunk that belong to the payload (bytes 1-3 of the dword)
-    const uint32_t prev = prev_dw(x) & (uint32_t)byte_mask(lo_b + 4, 4);
+    const uint32_t pd = prev_dw(x);
+    const uint32_t prev = inner ? pd : pd & (uint32_t)byte_mask(lo_b + 4, 4);
     // ASCII, and no lead byte (11xxxxxx) just before: nothing to check
     if (!high_bits(v) && !(prev & (prev << 1) & 0x80808000u)) continue;
-    uint32_t err = utf8_dword_errors(v.x, prev) | utf8_dword_errors(v.y, v.x) | utf8_dword_errors(v.z, v.y) |
-                   utf8_dword_errors(v.w, v.z);
+    const Utf8Pre q0 = utf8_pre(prev), q1 = utf8_pre(v.x), q2 = utf8_pre(v.y), q3 = utf8_pre(v.z),
+                  q4 = utf8_pre(v.w);
+    uint32_t err = utf8_dword_errors(q1, q0) | utf8_dword_errors(q2, q1) | utf8_dword_errors(q3, q2) |
+                   utf8_dword_errors(q4, q3);
     if (c == c_hi && hi_b >= 16)  // the payload ends with this chunk: nothing may still be expected
       err |= utf8_pending(v.w >> 24, (v.w >> 16) & 0xFFu, (v.w >> 8) & 0xFFu) ? 1u : 0u;
     bad = err ? 1u : 0u;

@@ -30,12 +30,13 @@ def main():
     ap.add_argument("--libs", required=True)
     ap.add_argument("--L", default="1472,1024,64")
     ap.add_argument("--reps", type=int, default=11)
-    ap.add_argument("--op", default="encode", choices=["encode", "decode", "varlen", "vdecode"],
+    ap.add_argument("--op", default="encode", choices=["encode", "decode", "varlen", "vdecode", "u8text"],
                     help="decode: verify-only fixed-length rudp_decode of the encoded frames; varlen: "
                          "rudp_encode_varlen_checked of packed payloads, --L lengths or 'ragged' "
                          "(uniform in [0, 2944]); a 'u' suffix (1472u) times the unchecked rudp_encode_varlen; "
                          "vdecode: rudp_decode_varlen_checked (no status word) of such frames, rudp5 with the "
-                         "sideband checksums below 16-B payloads, else rudp7")
+                         "sideband checksums below 16-B payloads, else rudp7; u8text: rudp_decode_utf8 of "
+                         "frames whose payload is valid multi-byte UTF-8 text (1-4 byte characters)")
     args = ap.parse_args()
     _native.lib()  # torch's HIP runtime first
     libs = {}
@@ -49,6 +50,9 @@ def main():
                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         h.rudp_decode.restype = ctypes.c_int
+        h.rudp_decode_utf8.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64] + \
+            [ctypes.c_void_p] * 8 + [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+        h.rudp_decode_utf8.restype = ctypes.c_int
         h.rudp_encode_varlen_checked.argtypes = [ctypes.POINTER(_native.RudpBatch), ctypes.c_uint64, ctypes.c_void_p,
                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                  ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
@@ -76,6 +80,16 @@ def main():
         sets = []
         for _ in range(nsets):
             tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
+            if args.op == "u8text":
+                text = ("é中😀aßЖ€𝄞" * (L // 8 + 8)).encode()[:L]
+                while True:
+                    try:
+                        text.decode()
+                        break
+                    except UnicodeDecodeError:
+                        text = text[:-1]
+                text += b"x" * (L - len(text))
+                pay = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(dev).expand(n, L).contiguous()
             fr = torch.empty((n, L + 7), dtype=torch.uint8, device=dev)
             b = _native.RudpBatch(n=n, payload_len=L, reserved=0, seq=tab.seq.data_ptr(), ack=tab.ack.data_ptr(),
                                   flags=tab.flags.data_ptr(), payload=pay.data_ptr(), len=None, payload_off=None)
@@ -83,10 +97,14 @@ def main():
             libs[next(iter(libs))].rudp_encode(ctypes.byref(b), fr.data_ptr(), None, 7, 0, stream)
         outs = [torch.empty((n,), dtype=dt, device=dev) for dt in (torch.uint16, torch.uint16, torch.uint8,
                                                                      torch.uint8, torch.uint16)]
+        valid = torch.empty((n,), dtype=torch.uint8, device=dev)
 
         def call(h, fr, b):
             if args.op == "encode":
                 return h.rudp_encode(ctypes.byref(b), fr.data_ptr(), None, 7, 0, stream)
+            if args.op == "u8text":
+                return h.rudp_decode_utf8(fr.data_ptr(), None, L + 7, n, None, *[t.data_ptr() for t in outs], None,
+                                          valid.data_ptr(), 7, 0, stream)
             return h.rudp_decode(fr.data_ptr(), None, L + 7, n, None, *[t.data_ptr() for t in outs], None, 7, 0,
                                  stream)
         ref = None
@@ -98,7 +116,7 @@ def main():
             for t in outs:
                 t.zero_()
             assert call(h, fr, b) == 0
-            got = fr.clone() if args.op == "encode" else torch.cat([t.view(torch.uint8) for t in outs])
+            got = fr.clone() if args.op == "encode" else torch.cat([t.view(torch.uint8) for t in outs] + [valid])
             ref = got if ref is None else ref
             exact[name] = bool(torch.equal(got, ref))
         times = {k: [] for k in libs}
