@@ -111,7 +111,7 @@ __device__ __forceinline__ uint32_t utf8_dword_errors(const Utf8Pre& c, const Ut
 }
 
 // Strict UTF-8 check of one frame's payload bytes [s, fe) by G lanes (lane g
-// takes aligned chunks c_lo + g, + G, ...): `chunk(c)` returns aligned chunk c
+// takes aligned chunk pairs from c_lo + 2g, every 2G): `chunk(c)` returns aligned chunk c
 // and `prev(x)` the dword of bytes x-4 .. x-1 (x a multiple of 16; only bytes
 // at or past s are used).  Bytes outside [s, fe) count as 0 (ASCII): a
 // sequence cut by the payload's end then fails on the 0 after it, and a chunk
@@ -124,25 +124,44 @@ __device__ __forceinline__ uint32_t utf8_check_frame(uint64_t s, uint64_t fe, ui
   uint32_t bad = 0;
   if (fe <= s) return 0;
   const uint64_t c_lo = s >> 4, c_hi = (fe - 1u) >> 4;
-  for (uint64_t c = c_lo + g; c <= c_hi && !bad; c += G) {  // a lane stops at its first invalid chunk
-    const uint64_t x = c << 4;
-    const int lo_b = (int)((int64_t)s - (int64_t)x), hi_b = (int)((int64_t)fe - (int64_t)x);
-    // an inner chunk (it and the four bytes before it all payload) needs no masks
-    const bool inner = lo_b <= -4 && hi_b >= 16;
-    const u32x4 raw = chunk(c);
-    const u32x4 v = inner ? raw : keep_bytes(raw, lo_b, hi_b);
-    // the three bytes before the chunk that belong to the payload (bytes 1-3 of the dword)
-    const uint32_t pd = prev_dw(x);
-    const uint32_t prev = inner ? pd : pd & (uint32_t)byte_mask(lo_b + 4, 4);
-    // ASCII, and no lead byte (11xxxxxx) just before: nothing to check
-    if (!high_bits(v) && !(prev & (prev << 1) & 0x80808000u)) continue;
-    const Utf8Pre q0 = utf8_pre(prev), q1 = utf8_pre(v.x), q2 = utf8_pre(v.y), q3 = utf8_pre(v.z),
-                  q4 = utf8_pre(v.w);
-    uint32_t err = utf8_dword_errors(q1, q0) | utf8_dword_errors(q2, q1) | utf8_dword_errors(q3, q2) |
-                   utf8_dword_errors(q4, q3);
-    if (c == c_hi && hi_b >= 16)  // the payload ends with this chunk: nothing may still be expected
-      err |= utf8_pending(v.w >> 24, (v.w >> 16) & 0xFFu, (v.w >> 8) & 0xFFu) ? 1u : 0u;
-    bad = err ? 1u : 0u;
+  // lane g takes chunk pairs (c_lo + 2g, + 1), (+ 2G, + 2G + 1), ...: the second
+  // chunk's "bytes before" are the first's last dword, already at hand
+  for (uint64_t c0 = c_lo + 2u * g; c0 <= c_hi && !bad; c0 += 2u * (uint64_t)G) {  // stops at its first invalid chunk
+    uint32_t last = 0;  // the previous chunk's last dword (masked to the payload)
+    Utf8Pre q_last;
+    bool have_q = false;
+#pragma unroll
+    for (uint32_t k = 0; k < 2u; ++k) {
+      const uint64_t c = c0 + k;
+      if (c > c_hi || bad) break;
+      const uint64_t x = c << 4;
+      const int lo_b = (int)((int64_t)s - (int64_t)x), hi_b = (int)((int64_t)fe - (int64_t)x);
+      // an inner chunk (it and the four bytes before it all payload) needs no masks
+      const bool inner = lo_b <= -4 && hi_b >= 16;
+      const u32x4 raw = chunk(c);
+      const u32x4 v = inner ? raw : keep_bytes(raw, lo_b, hi_b);
+      // the bytes before the chunk that belong to the payload (bytes 1-3 of the dword)
+      uint32_t prev = last;
+      if (k == 0) {
+        const uint32_t pd = prev_dw(x);
+        prev = inner ? pd : pd & (uint32_t)byte_mask(lo_b + 4, 4);
+      }
+      last = v.w;
+      // ASCII, and no lead byte (11xxxxxx) just before: nothing to check
+      if (!high_bits(v) && !(prev & (prev << 1) & 0x80808000u)) {
+        have_q = false;
+        continue;
+      }
+      const Utf8Pre q0 = have_q ? q_last : utf8_pre(prev), q1 = utf8_pre(v.x), q2 = utf8_pre(v.y),
+                    q3 = utf8_pre(v.z), q4 = utf8_pre(v.w);
+      uint32_t err = utf8_dword_errors(q1, q0) | utf8_dword_errors(q2, q1) | utf8_dword_errors(q3, q2) |
+                     utf8_dword_errors(q4, q3);
+      if (c == c_hi && hi_b >= 16)  // the payload ends with this chunk: nothing may still be expected
+        err |= utf8_pending(v.w >> 24, (v.w >> 16) & 0xFFu, (v.w >> 8) & 0xFFu) ? 1u : 0u;
+      bad = err ? 1u : 0u;
+      q_last = q4;
+      have_q = true;
+    }
   }
   return bad;
 }

@@ -1914,7 +1914,7 @@ __device__ __forceinline__ void decode_varlen_frame_lane(const VarlenArgs& a, ui
 }
 
 template <int H, uint32_t FPT, bool U8>
-__global__ void __launch_bounds__(kBlock) decode_varlen_small_kernel(VarlenArgs a) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) decode_varlen_small_kernel(VarlenArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   constexpr uint32_t T = kBlock * FPT;
   const uint32_t tid = threadIdx.x;
@@ -1930,7 +1930,7 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_small_kernel(VarlenArgs 
 #pragma unroll
     for (uint32_t j = 0; j < 2u * FPT; ++j) {  // (the header comes from the pair's two first chunks)
       const uint32_t q = j * (kBlock / 2u) + (tid >> 1);
-      decode_varlen_frame<H, U8>(a, p0 + q, q < Tv, tid & 1u, 1u);
+      decode_varlen_frame<H, U8, 4>(a, p0 + q, q < Tv, tid & 1u, 1u);
     }
     return;
   }
