@@ -69,14 +69,15 @@ __device__ __forceinline__ uint32_t group_or(uint32_t bits, uint32_t G) {
 struct Utf8Pre {
   uint32_t sel_lo, m_lo, sel_hi, m_hi, e0, f0;
 };
+// Every byte of y replaced by 0xFF if its bit 7 is set, else 0: v_perm_b32's
+// selectors 8-11 replicate the sign bits of bytes 1, 3, 5, 7 of {y, y << 8}.
+__device__ __forceinline__ uint32_t sign_bytes(uint32_t y) { return __builtin_amdgcn_perm(y, y << 8, 0x0B090A08u); }
 __device__ __forceinline__ Utf8Pre utf8_pre(uint32_t x) {
   Utf8Pre p;
   p.sel_lo = x & 0x07070707u;
-  const uint32_t bl = x & 0x08080808u;
-  p.m_lo = (bl << 5) - (bl >> 3);  // 0xFF in every byte whose bit 3 is set (no multiply)
+  p.m_lo = sign_bytes(x << 4);  // bit 3 of each byte
   p.sel_hi = (x >> 4) & 0x07070707u;
-  const uint32_t bh = x & 0x80808080u;
-  p.m_hi = (bh << 1) - (bh >> 7);  // the same for bit 7
+  p.m_hi = sign_bytes(x);       // bit 7
   const uint32_t e = x & (x << 1) & (x << 2) & 0x80808080u;
   p.e0 = e;
   p.f0 = e & (x << 3);
