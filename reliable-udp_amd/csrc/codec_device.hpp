@@ -40,6 +40,34 @@ __device__ __forceinline__ uint32_t xcd_tile(uint32_t b, uint32_t nt) {
   return x * per + (x < rem ? x : rem) + k;
 }
 
+// Reductions over a lane group of G lanes (G a power of two, groups aligned
+// to G lanes, every lane of the group active): DPP row operations up to 16
+// lanes -- quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror, each
+// pairing a lane with one in the other half of its 2/4/8/16 -- instead of a
+// ds_bpermute round trip per step; the 32- and 64-lane steps stay shuffles.
+template <int CTRL>
+__device__ __forceinline__ uint32_t dpp_row(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, CTRL, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t group_sum(uint32_t x, uint32_t G) {
+  if (G >= 2u) x += dpp_row<0xB1>(x);
+  if (G >= 4u) x += dpp_row<0x4E>(x);
+  if (G >= 8u) x += dpp_row<0x141>(x);
+  if (G >= 16u) x += dpp_row<0x140>(x);
+  if (G >= 32u) x += (uint32_t)__shfl_xor((int)x, 16, 64);
+  if (G >= 64u) x += (uint32_t)__shfl_xor((int)x, 32, 64);
+  return x;
+}
+__device__ __forceinline__ uint32_t group_or_rows(uint32_t x, uint32_t G) {
+  if (G >= 2u) x |= dpp_row<0xB1>(x);
+  if (G >= 4u) x |= dpp_row<0x4E>(x);
+  if (G >= 8u) x |= dpp_row<0x141>(x);
+  if (G >= 16u) x |= dpp_row<0x140>(x);
+  if (G >= 32u) x |= (uint32_t)__shfl_xor((int)x, 16, 64);
+  if (G >= 64u) x |= (uint32_t)__shfl_xor((int)x, 32, 64);
+  return x;
+}
+
 // End-around-carry fold of a 32-bit partial sum to 16 bits.
 __device__ __forceinline__ uint32_t fold16(uint32_t s) {
   s = (s & 0xFFFFu) + (s >> 16);

@@ -278,10 +278,8 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
       }
     }
   }
-  for (uint32_t m = G >> 1; m > 0; m >>= 1) {
-    sum += __shfl_xor(sum, (int)m, 64);
-    if (U8) hib |= (uint32_t)__shfl_xor((int)hib, (int)m, 64);
-  }
+  sum = group_sum(sum, G);
+  if (U8) hib = group_or_rows(hib, G);
   uint32_t u8bad = 0;
   if (U8 && __any((hib & 0x80808080u) != 0)) {  // the byte checks, for frames with a high bit
     if ((hib & 0x80808080u) && q < Tv)

@@ -250,7 +250,7 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
       for (uint32_t v = g; v < V; v += G) sum += le16_sum(mine[v]);
     }
   }
-  for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
+  sum = group_sum(sum, G);
   if (g == 0 && q < Tv) {
     const uint64_t p = p0 + q;
     const bool late = a.early_table != 1u && !dma_tab;

@@ -55,11 +55,9 @@ __device__ __forceinline__ u32x4 keep_bytes(u32x4 w, int lo, int hi) {
 
 __device__ __forceinline__ uint32_t high_bits(u32x4 w) { return (w.x | w.y | w.z | w.w) & 0x80808080u; }
 
-// OR of `bits` over the G lanes of this lane's group (G a power of two <= 64).
-__device__ __forceinline__ uint32_t group_or(uint32_t bits, uint32_t G) {
-  for (uint32_t m = G >> 1; m > 0; m >>= 1) bits |= (uint32_t)__shfl_xor((int)bits, (int)m, 64);
-  return bits;
-}
+// OR of `bits` over the G lanes of this lane's group (G a power of two <= 64,
+// every lane of the group active): DPP rows, codec_device.hpp.
+__device__ __forceinline__ uint32_t group_or(uint32_t bits, uint32_t G) { return group_or_rows(bits, G); }
 
 // Per-dword inputs of the table check, computed once per dword and shared by
 // the dword's own check and the next one's (which needs the bytes before

@@ -870,10 +870,8 @@ __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_
   odd_sum = fold_keep(odd_sum);
   // even global offsets are high bytes iff the frame starts at an even offset
   uint32_t sum = (fstart & 1u) ? (even_sum + (odd_sum << 8)) : ((even_sum << 8) + odd_sum);
-  for (uint32_t m = G >> 1; m > 0; m >>= 1) {
-    sum += __shfl_xor(sum, (int)m, 64);
-    if (U8) hib |= (uint32_t)__shfl_xor((int)hib, (int)m, 64);
-  }
+  sum = group_sum(sum, G);
+  if (U8) hib = group_or_rows(hib, G);
   uint32_t u8bad = 0;
   if (U8 && __any((hib & 0x80808080u) != 0)) {  // the byte checks, for frames with a high bit
     if ((hib & 0x80808080u) && valid && !bad)
@@ -1061,10 +1059,8 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
     }
     // even offsets are high bytes iff the frame starts at an even offset
     uint32_t sum = (fs & 1u) ? (even_sum + (odd_sum << 8)) : ((even_sum << 8) + odd_sum);
-    for (uint32_t m = G2 >> 1; m > 0; m >>= 1) {
-      sum += __shfl_xor(sum, (int)m, 64);
-      if (U8) hib |= (uint32_t)__shfl_xor((int)hib, (int)m, 64);
-    }
+    sum = group_sum(sum, G2);
+    if (U8) hib = group_or_rows(hib, G2);
     if (U8) {  // a frame with a high bit in its payload: the byte checks, from LDS
       uint32_t u8bad = 0;
       if (__any((hib & 0x80808080u) != 0)) {
