@@ -1007,6 +1007,9 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
       decode_varlen_frame<H, U8, 6>(a, p0 + q, true, g2, glog2);
       return;
     }
+    // the leader's header window, read now so its LDS round trip overlaps the sums
+    u32x4 hdr = make_u32x4(0ull, 0ull);
+    if (g2 == 0) hdr = window16_dw(reinterpret_cast<const uint32_t*>(img), fs);
     uint32_t even_sum = 0, odd_sum = 0;  // byte sums at even / odd offsets (A is even)
     uint32_t hib = 0;                     // U8: high bits of the payload bytes
     const uint32_t ps = fs + (uint32_t)H;
@@ -1074,7 +1077,7 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
       if (g2 == 0) a.valid[p0 + q] = u8bad ? 0 : 1;
     }
     if (g2 == 0)
-      decode_varlen_finish<H>(a, p0 + q, fe - fs, sum, window16_dw(reinterpret_cast<const uint32_t*>(img), fs));
+      decode_varlen_finish<H>(a, p0 + q, fe - fs, sum, hdr);
   };
   if (q2 < Tv) frame(q2);
 }
