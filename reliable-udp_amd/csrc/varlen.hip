@@ -185,7 +185,7 @@ __device__ __forceinline__ void encode_varlen_packet(const VarlenArgs& a, uint64
       sum += payload_le16_sum(hlo[i], hhi[i], k0 - H);
     }
   }
-  for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
+  sum = group_sum(sum, G);
   if (!valid) return;
   const uint32_t s = a.seq_in[p], k = a.ack_in[p], f = a.flags_in[p];
   const uint32_t c = packet_csum(sum, s, k, f);
@@ -535,7 +535,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
 #if RUDP_TOOLS
   if (a.trace && (tid & 63u) == 0) atomicMax(&s_last[1], (unsigned long long)wall_clock64());
 #endif
-  for (uint32_t m = G >> 1; m > 0; m >>= 1) sum += __shfl_xor(sum, (int)m, 64);
+  sum = group_sum(sum, G);
   // The header word and the frame's (up to) two header chunks: lanes 0 and 1
   // of the packet build one chunk each (the leader both when G = 1).
   const uint32_t hl = G >= 2u ? 2u : 1u;
