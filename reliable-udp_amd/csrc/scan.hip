@@ -137,7 +137,7 @@ __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len,
                                                             SpanStarts spans) {
   __shared__ uint32_t s_len[kScanBlockItems];
   __shared__ uint64_t s_off[kScanBlockItems];
-  __shared__ uint64_t s_wave[kBlock / 64];
+  __shared__ uint32_t s_wave32[kBlock / 64];
   const uint64_t base = (uint64_t)blockIdx.x * kScanBlockItems;
   // coalesced load of the block's lengths, then each thread takes 8 in a row
 #pragma unroll
@@ -146,11 +146,11 @@ __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len,
     s_len[k] = base + k < n ? len[base + k] + H : 0u;
   }
   __syncthreads();
-  uint64_t mine = 0;
+  uint32_t mine = 0;
 #pragma unroll
   for (uint32_t j = 0; j < kScanItems; ++j) mine += s_len[threadIdx.x * kScanItems + j];
-  uint64_t total = 0;
-  uint64_t run = bases[blockIdx.x] + block_exclusive_scan(mine, &total, s_wave);
+  uint32_t total = 0;  // (at most kScanBlockItems * (65535 + H) for lengths that passed pass 1)
+  uint64_t run = bases[blockIdx.x] + block_exclusive_scan32(mine, &total, s_wave32);
 #pragma unroll
   for (uint32_t j = 0; j < kScanItems; ++j) {
     const uint32_t k = threadIdx.x * kScanItems + j;

@@ -1604,7 +1604,7 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
   uint8_t* s_flags = reinterpret_cast<uint8_t*>(s_cs + T);
   unsigned char* pay = lds + small_lds_off_pay(T);
   unsigned char* img = lds + small_lds_off_out(T, cap);
-  __shared__ uint64_t s_wave[kBlock / 64];
+  __shared__ uint32_t s_wave32[kBlock / 64];
 
   const uint64_t tile = a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x;
   const uint64_t p0 = tile * T;
@@ -1721,8 +1721,8 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
       const uint32_t q = tid * FPT + i;
       mine += q < Tv ? s_len[q] + (uint32_t)H : 0u;
     }
-    uint64_t total = 0;
-    uint32_t run = (uint32_t)block_exclusive_scan(mine, &total, s_wave);
+    uint32_t total = 0;  // (at most 256 * FPT * 65542)
+    uint32_t run = block_exclusive_scan32(mine, &total, s_wave32);
 #pragma unroll
     for (uint32_t i = 0; i < FPT; ++i) {
       const uint32_t q = tid * FPT + i;
