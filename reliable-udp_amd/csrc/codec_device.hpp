@@ -68,6 +68,27 @@ __device__ __forceinline__ uint32_t group_or_rows(uint32_t x, uint32_t G) {
   return x;
 }
 
+// Sum of a u64 over the whole wave: the 16-lane steps by DPP on the two
+// halves (carry added by hand), the 32- and 64-lane steps as shuffles.
+template <int CTRL>
+__device__ __forceinline__ void add64_rows(uint32_t& lo, uint32_t& hi) {
+  const uint32_t l2 = dpp_row<CTRL>(lo), h2 = dpp_row<CTRL>(hi);
+  const uint32_t s = lo + l2;
+  hi = hi + h2 + (s < lo ? 1u : 0u);
+  lo = s;
+}
+__device__ __forceinline__ uint64_t wave_sum64(uint64_t x) {
+  uint32_t lo = (uint32_t)x, hi = (uint32_t)(x >> 32);
+  add64_rows<0xB1>(lo, hi);
+  add64_rows<0x4E>(lo, hi);
+  add64_rows<0x141>(lo, hi);
+  add64_rows<0x140>(lo, hi);
+  uint64_t v = (uint64_t)lo | ((uint64_t)hi << 32);
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
 // End-around-carry fold of a 32-bit partial sum to 16 bits.
 __device__ __forceinline__ uint32_t fold16(uint32_t s) {
   s = (s & 0xFFFFu) + (s >> 16);

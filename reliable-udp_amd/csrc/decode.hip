@@ -237,6 +237,9 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
   }
   __syncthreads();
   const uint32_t* dw = reinterpret_cast<const uint32_t*>(lds);
+  // the leader's header window, read now so its LDS round trip overlaps the sums
+  u32x4 hdr = make_u32x4(0ull, 0ull);
+  if (g == 0 && q < Tv) hdr = window16_dw(dw, q * F);
   uint32_t sum = 0, hib = 0;
   const uint64_t p = p0 + q;
   const uint32_t V = L >> 4;
@@ -289,7 +292,7 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
   }
   if (!a.stage_out) {
     if (g == 0 && q < Tv) {
-      const u32x4 h = window16_dw(dw, q * F);
+      const u32x4 h = hdr;
       const uint32_t seq = ((h.x & 0xFFu) << 8) | ((h.x >> 8) & 0xFFu);
       const uint32_t ack = (((h.x >> 16) & 0xFFu) << 8) | (h.x >> 24);
       const uint32_t flags = h.y & 0xFFu;
@@ -310,7 +313,7 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
   uint8_t* s_ok = s_flags + T;
   uint8_t* s_valid = s_ok + T;  // U8
   if (g == 0 && q < Tv) {
-    const u32x4 h = window16_dw(dw, q * F);
+    const u32x4 h = hdr;
     const uint32_t seq = ((h.x & 0xFFu) << 8) | ((h.x >> 8) & 0xFFu);
     const uint32_t ack = (((h.x >> 16) & 0xFFu) << 8) | (h.x >> 24);
     const uint32_t flags = h.y & 0xFFu;

@@ -58,14 +58,13 @@ __global__ void __launch_bounds__(kBlock) scan_block_sums_kernel(const uint32_t*
         }
       }
     }
-    if (over_T) {  // (uniform)
-      uint64_t ts = l;
-      for (uint32_t m = 1; m < over_T; m <<= 1) ts += __shfl_xor(ts, (int)m, 64);
+    if (over_T) {  // (uniform; lengths clamped: any over 65535 fails the call anyway)
+      const uint32_t ts = group_sum(l < 0x10000u ? l : 0x10000u, over_T);
       const bool o = (threadIdx.x & (over_T - 1u)) == 0 && i < n && ts + 30u > over_cap;
       over += (uint32_t)__popcll(__ballot(o));
     }
   }
-  for (int m = 32; m > 0; m >>= 1) acc += __shfl_xor(acc, m, 64);
+  acc = wave_sum64(acc);
   __syncthreads();  // s_bits, s_over initialised
   if (bits) atomicOr(&s_bits, bits);
   if ((threadIdx.x & 63u) == 0) {
