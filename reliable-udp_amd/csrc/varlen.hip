@@ -1929,7 +1929,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
 #pragma unroll
     for (uint32_t j = 0; j < 2u * FPT; ++j) {  // (the header comes from the pair's two first chunks)
       const uint32_t q = j * (kBlock / 2u) + (tid >> 1);
-      decode_varlen_frame<H, U8, 4>(a, p0 + q, q < Tv, tid & 1u, 1u);
+      decode_varlen_frame<H, U8, U8 ? 4 : 0>(a, p0 + q, q < Tv, tid & 1u, 1u);
     }
     return;
   }
