@@ -32,7 +32,10 @@
 // an LDS table and confirms every hit from LDS.  No hash scratch in HBM and
 // each offset read once: the round-3 two-pass chain moved 3.8x the algorithmic
 // bytes (8-B hashes written, then re-read per workgroup with their halo).
+#include <type_traits>
+
 #include "codec_device.hpp"
+
 #include "internal.hpp"
 
 namespace RUDP_NS {
@@ -342,20 +345,25 @@ __global__ void __launch_bounds__(kBlock) dedup_small_kernel(DedupArgs a, uint32
 int launch_dedup(const DedupArgs& args, hipStream_t stream) {
   if (args.n == 0) return 0;
   if (args.small_cap) {
-    constexpr uint32_t FPT = 4, T = kBlock * FPT;
-    const uint32_t cmax = T + args.window;
-    uint32_t nb = 256;  // buckets: chains of 1-2 entries
-    while (2u * nb < cmax) nb <<= 1;
-    const size_t lds = dedup_small_lds(cmax, nb, args.small_cap);
-    if (lds > 65536) {
-      hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dedup_small_kernel<FPT>),
-                                         hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-      if (e != hipSuccess) return (int)e;
-    }
-    const uint64_t blocks = (args.n + T - 1) / T;
-    hipLaunchKernelGGL((dedup_small_kernel<FPT>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args, nb,
-                       args.small_cap);
-    return (int)hipGetLastError();
+    auto launch = [&](auto fpt) -> int {
+      constexpr uint32_t FPT = decltype(fpt)::value, T = kBlock * FPT;
+      const uint32_t cmax = T + args.window;
+      uint32_t nb = 256;  // buckets: chains of 1-2 entries
+      while (2u * nb < cmax) nb <<= 1;
+      const size_t lds = dedup_small_lds(cmax, nb, args.small_cap);
+      if (lds > 65536) {
+        hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&dedup_small_kernel<FPT>),
+                                           hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+        if (e != hipSuccess) return (int)e;
+      }
+      const uint64_t blocks = (args.n + T - 1) / T;
+      hipLaunchKernelGGL((dedup_small_kernel<FPT>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args, nb,
+                         args.small_cap);
+      return (int)hipGetLastError();
+    };
+    // 1024-frame tiles; 512 (rudpx_tune 70 = 2) for the A/B
+    if (tuning().dedup_small_fpt == 2) return launch(std::integral_constant<uint32_t, 2>{});
+    return launch(std::integral_constant<uint32_t, 4>{});
   }
   const uint64_t hblocks = ((args.n << args.glog) + kBlock - 1) / kBlock;
   hipLaunchKernelGGL(dedup_hash_kernel, dim3((uint32_t)hblocks), dim3(kBlock), 0, stream, args);

@@ -348,6 +348,7 @@ struct Tuning {
   // Varlen decode tile: a lane's payload chunks read four at a time (1) or
   // one at a time (0).
   RUDP_KNOB(varlen_decode_r4, 0)
+  RUDP_KNOB(dedup_small_fpt, 4)  // one-launch dedup: frames per thread (4: 1024-frame tiles, 2: 512)
   // Fixed-length encode: batches of more packets than this go out as several
   // launches of at most this many (0: one launch).
   RUDP_KNOB(encode_launch_packets, 0)

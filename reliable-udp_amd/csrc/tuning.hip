@@ -329,7 +329,8 @@ RUDP_API int rudpx_tune(int key, int value) {
             : key == 66 ? &t.varlen_decode_span_bytes
             : key == 67 ? &t.varlen_map_bal
             : key == 68 ? &t.varlen_decode_nt
-            : key == 69 ? &t.varlen_decode_r4 : nullptr;
+            : key == 69 ? &t.varlen_decode_r4
+            : key == 70 ? &t.dedup_small_fpt : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }
