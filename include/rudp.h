@@ -63,7 +63,7 @@
 extern "C" {
 #endif
 
-#define RUDP_ABI_VERSION 6
+#define RUDP_ABI_VERSION 7
 
 /* Frame layouts: the value is the header length in bytes. */
 #define RUDP_LAYOUT_RUDP5 5 /* reference-exact 5-byte header, checksum sideband */
@@ -348,14 +348,46 @@ RUDP_API int rudp_udp_send_batch_to(int fd, const uint8_t* h_frames, const uint6
  * Staged through a ring of device slots in chunks, with H2D, kernel and D2H
  * on three streams chained by events so the three overlap.  Synchronous.  These model the reference's
  * real boundary, a UDP socket buffer in host memory (utils/reliableUDP.py:61,
- * :67, :118).
+ * :67, :118).  Pinned (page-locked) host buffers copy at the link's rate;
+ * pageable ones through the runtime's bounce buffers, at about half of it.
+ *
+ * rudp_decode_host (ABI 7: h_valid_or_null added): rudp_decode_utf8 of
+ *   fixed-length frames in host memory -- the reference's receive, Packet(data)
+ *   + get_header_field + get_payload() per datagram (utils/reliableUDP.py:118-121,
+ *   utils/packet.py:16, :29-40, :68-73) -- with h_valid_or_null[i] its strict
+ *   UTF-8 answer, judged in the decode pass (NULL: not computed).
+ * rudp_decode_varlen_host (ABI 7): rudp_decode_varlen_utf8 of packed frames
+ *   in host memory (a recvmmsg batch: frame i = h_frames[h_frame_off[i],
+ *   h_frame_off[i + 1]), frames_bytes = size of h_frames), with every frame's
+ *   offsets checked against frames_bytes as there (a rejected frame gets
+ *   h_ok = RUDP_OK_BAD_OFFSETS and h_valid = 0, and *h_status_or_null =
+ *   RUDP_ST_OFFSETS); the payload is zero-copy (frame i's bytes from
+ *   layout on).  len_hint: the typical frame length (0: frames_bytes / n).
+ *   Each chunk stages the byte range its offsets span: one valid frame over
+ *   host_stage bytes (128 MiB) is refused with RUDP_ENOTSUP.
+ * rudp_encode_varlen_host (ABI 7): rudp_encode_varlen of packed payloads in
+ *   host memory (h_in->payload_off must be NULL; h_in->payload_len is a hint
+ *   of the typical length) to packed frames in host memory -- the send side,
+ *   Packet() + set_header_field + set_payload + to_byte() per datagram
+ *   (utils/reliableUDP.py:53-61, utils/packet.py:43-65, :76-81).
+ *   h_frame_off receives n + 1 offsets (the exclusive scan of len[i] +
+ *   layout).  Every length (<= 65535) and frames_cap (>= sum(len) + n *
+ *   layout) is checked before any work is enqueued: a bad batch returns
+ *   RUDP_EINVAL and writes nothing.
  */
 RUDP_API int rudp_encode_host(const rudp_batch* h_in, uint8_t* h_frames, uint16_t* h_csum_or_null,
                      int layout, int device);
 RUDP_API int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
                      const uint16_t* h_csum_in_or_null, uint16_t* h_seq, uint16_t* h_ack,
                      uint8_t* h_flags, uint8_t* h_ok, uint16_t* h_csum_out_or_null,
-                     uint8_t* h_payload_out_or_null, int layout, int device);
+                     uint8_t* h_payload_out_or_null, uint8_t* h_valid_or_null, int layout, int device);
+RUDP_API int rudp_decode_varlen_host(const uint8_t* h_frames, uint64_t frames_bytes, const uint64_t* h_frame_off,
+                                     uint32_t len_hint, uint64_t n, const uint16_t* h_csum_in_or_null,
+                                     uint16_t* h_seq, uint16_t* h_ack, uint8_t* h_flags, uint8_t* h_ok,
+                                     uint16_t* h_csum_out_or_null, uint8_t* h_valid_or_null,
+                                     uint32_t* h_status_or_null, int layout, int device);
+RUDP_API int rudp_encode_varlen_host(const rudp_batch* h_in, uint8_t* h_frames, uint64_t frames_cap,
+                                     uint64_t* h_frame_off, uint16_t* h_csum_or_null, int layout, int device);
 
 /*
  * Deterministic synthetic batch, generated on the device:

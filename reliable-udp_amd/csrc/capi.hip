@@ -242,10 +242,23 @@ int pipeline_reserve(Pipeline* pp, int slots, size_t bytes) {
 
 size_t up256(size_t x) { return (x + 255u) & ~size_t(255); }
 
-// Packets per chunk for a given per-packet staging footprint.
-uint64_t chunk_packets(uint64_t n, uint64_t bytes_per_packet) {
+size_t stage_bytes() {
   const int mb = tuning().host_stage_mb;
-  uint64_t cn = ((uint64_t)(mb > 0 ? mb : 32) << 20) / (bytes_per_packet ? bytes_per_packet : 1);
+  return (size_t)(mb > 0 ? mb : 32) << 20;
+}
+
+// Packets per chunk for a given per-packet staging footprint: a slot's worth,
+// and for a batch over 4 MiB at most 1/host_min_chunks of it, so that even a
+// batch of small frames has copies in both directions overlapping a kernel.
+uint64_t chunk_packets(uint64_t n, uint64_t bytes_per_packet) {
+  const uint64_t bpp = bytes_per_packet ? bytes_per_packet : 1;
+  uint64_t cn = stage_bytes() / bpp;
+  const int kc = tuning().host_min_chunks;
+  const uint64_t k = (uint64_t)(kc > 1 ? kc : 1);
+  if (n * bpp > (4u << 20) && k > 1) {
+    const uint64_t part = (n + k - 1) / k;
+    if (part < cn) cn = part;
+  }
   if (cn < 64) cn = 64;
   return cn > n ? n : cn;
 }
@@ -255,17 +268,22 @@ int pipeline_slots() {
   return s < 2 ? 2 : s > kMaxSlots ? kMaxSlots : s;
 }
 
-// Drive chunks [0, n) in steps of cn through the pipeline.  The three
-// callbacks enqueue chunk work on the stream they are given.  Returns only
-// after all three streams have drained, on success and on every error path:
-// earlier chunks' copies into the caller's host arrays must not outlive the
-// call (the caller may free those arrays as soon as it returns).
-template <class H2D, class KERN, class D2H>
-int run_pipeline(Pipeline* pp, uint64_t n, uint64_t cn, H2D h2d, KERN kern, D2H d2h) {
+// Drive chunks through the pipeline: `plan(p0)` returns the packets of the
+// chunk that starts at packet p0 (> 0, or a negative error code), and the
+// three callbacks enqueue that chunk's work on the stream they are given (all
+// four run on this thread, one chunk at a time, so a plan's extra state lives
+// until the chunk's callbacks have run).  Returns only after all three streams
+// have drained, on success and on every error path: earlier chunks' copies
+// into the caller's host arrays must not outlive the call (the caller may
+// free those arrays as soon as it returns).
+template <class PLAN, class H2D, class KERN, class D2H>
+int run_pipeline_planned(Pipeline* pp, uint64_t n, PLAN plan, H2D h2d, KERN kern, D2H d2h) {
   const int S = pp->slots;
   auto enqueue = [&]() -> int {
-    for (uint64_t p0 = 0, k = 0; p0 < n; p0 += cn, ++k) {
-      const uint64_t m = (n - p0) < cn ? (n - p0) : cn;
+    for (uint64_t p0 = 0, k = 0; p0 < n; ++k) {
+      const int64_t mm = plan(p0);
+      if (mm <= 0) return mm < 0 ? (int)mm : fail(RUDP_EINVAL, "pipeline: empty chunk");
+      const uint64_t m = (uint64_t)mm;
       const int s = (int)(k % (uint64_t)S);
       char* base = (char*)pp->dbuf[s];
       if (k >= (uint64_t)S) RUDP_HIP(hipStreamWaitEvent(pp->h2d, pp->slot_free[s], 0));
@@ -278,6 +296,7 @@ int run_pipeline(Pipeline* pp, uint64_t n, uint64_t cn, H2D h2d, KERN kern, D2H 
       RUDP_HIP(hipStreamWaitEvent(pp->d2h, pp->out_ready[s], 0));
       if ((rc = d2h(base, p0, m, pp->d2h))) return rc;
       RUDP_HIP(hipEventRecord(pp->slot_free[s], pp->d2h));
+      p0 += m;
     }
     return 0;
   };
@@ -290,6 +309,13 @@ int run_pipeline(Pipeline* pp, uint64_t n, uint64_t cn, H2D h2d, KERN kern, D2H 
   if (e2 != hipSuccess) return hip_fail(e2, "pipeline kernel stream");
   if (e3 != hipSuccess) return hip_fail(e3, "pipeline D2H stream");
   return 0;
+}
+
+// Chunks of a fixed cn packets.
+template <class H2D, class KERN, class D2H>
+int run_pipeline(Pipeline* pp, uint64_t n, uint64_t cn, H2D h2d, KERN kern, D2H d2h) {
+  return run_pipeline_planned(
+      pp, n, [&](uint64_t p0) -> int64_t { return (int64_t)(n - p0 < cn ? n - p0 : cn); }, h2d, kern, d2h);
 }
 
 }  // namespace
@@ -409,8 +435,10 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
 #if RUDP_TOOLS
   a.diag = (uint32_t)tuning().varlen_diag;
 #endif
+#if RUDP_TOOLS
   // Checked calls with MTU-scale hints: byte spans (decode_varlen_span_kernel)
-  // instead of frame tiles; the span index lives in this stream's scratch.
+  // instead of frame tiles; the span index lives in this stream's scratch
+  // (measured slower than the frame tiles, DESIGN §7: diagnostics build only).
   const uint64_t S = (uint64_t)tuning().varlen_decode_span_bytes & ~15ull;
   const uint64_t span_cap = (S + 2u * (uint64_t)len_hint + 64u + 15u) & ~15ull;
   const uint64_t nt = S ? frames_lim / S + 1u : 0u;
@@ -430,9 +458,16 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
     a.span_S = (uint32_t)S;
     a.tile_cap = (uint32_t)span_cap;
   }
+#endif
   rc = launch_decode_varlen(a, layout, (hipStream_t)hip_stream);
   if (rc) return hip_fail((hipError_t)rc, "varlen decode launch");
   return 0;
+}
+
+// Adds a chunk's base to the frame offsets its encode wrote from 0.
+__global__ void __launch_bounds__(256) add_base_kernel(uint64_t* off, uint64_t n1, uint64_t base) {
+  const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
+  if (i < n1) off[i] += base;
 }
 
 }  // namespace rudp
@@ -959,7 +994,7 @@ int rudp_encode_host(const rudp_batch* h_in, uint8_t* h_frames, uint16_t* h_csum
 int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
                      const uint16_t* h_csum_in_or_null, uint16_t* h_seq, uint16_t* h_ack,
                      uint8_t* h_flags, uint8_t* h_ok, uint16_t* h_csum_out_or_null,
-                     uint8_t* h_payload_out_or_null, int layout, int device) {
+                     uint8_t* h_payload_out_or_null, uint8_t* h_valid_or_null, int layout, int device) {
   int rc = validate_decode(h_frames, nullptr, frame_len, n, h_seq, h_ack, h_flags, h_ok, layout);
   if (rc || n == 0) return rc;
   DeviceScope dev_scope;
@@ -967,12 +1002,13 @@ int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
   const uint64_t F = frame_len;
   const uint64_t L = F > (uint64_t)layout ? F - (uint64_t)layout : 0;
   uint8_t* h_pay = L ? h_payload_out_or_null : nullptr;
-  const uint64_t cn = chunk_packets(n, F + (h_pay ? L : 0) + 10);
-  // Slot layout: frames | payload | seq | ack | flags | ok | csum_in | csum_out.
+  uint8_t* h_val = h_valid_or_null;
+  const uint64_t cn = chunk_packets(n, F + (h_pay ? L : 0) + 10 + (h_val ? 1 : 0));
+  // Slot layout: frames | payload | seq | ack | flags | ok | csum_in | csum_out | valid.
   const size_t o_fr = 0, o_pay = up256(cn * F), o_seq = o_pay + up256(h_pay ? cn * L : 0),
                o_ack = o_seq + up256(cn * 2), o_fl = o_ack + up256(cn * 2),
                o_ok = o_fl + up256(cn), o_ci = o_ok + up256(cn), o_co = o_ci + up256(cn * 2),
-               slot = o_co + up256(cn * 2);
+               o_va = o_co + up256(cn * 2), slot = o_va + up256(h_val ? cn : 0);
   Pipeline* pp = pipeline_for(device);
   std::lock_guard<std::mutex> lk(pp->mu);
   if ((rc = pipeline_reserve(pp, pipeline_slots(), slot))) return rc;
@@ -983,11 +1019,12 @@ int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
     return 0;
   };
   auto kern = [&](char* base, uint64_t, uint64_t m, hipStream_t s) -> int {
-    return rudp_decode((const uint8_t*)(base + o_fr), nullptr, frame_len, m,
-                       h_csum_in_or_null ? (const uint16_t*)(base + o_ci) : nullptr,
-                       (uint16_t*)(base + o_seq), (uint16_t*)(base + o_ack), (uint8_t*)(base + o_fl),
-                       (uint8_t*)(base + o_ok), h_csum_out_or_null ? (uint16_t*)(base + o_co) : nullptr,
-                       h_pay ? (uint8_t*)(base + o_pay) : nullptr, layout, device, s);
+    return rudp_decode_utf8((const uint8_t*)(base + o_fr), nullptr, frame_len, m,
+                            h_csum_in_or_null ? (const uint16_t*)(base + o_ci) : nullptr,
+                            (uint16_t*)(base + o_seq), (uint16_t*)(base + o_ack), (uint8_t*)(base + o_fl),
+                            (uint8_t*)(base + o_ok), h_csum_out_or_null ? (uint16_t*)(base + o_co) : nullptr,
+                            h_pay ? (uint8_t*)(base + o_pay) : nullptr, h_val ? (uint8_t*)(base + o_va) : nullptr,
+                            layout, device, s);
   };
   auto d2h = [&](char* base, uint64_t p0, uint64_t m, hipStream_t s) -> int {
     RUDP_HIP(hipMemcpyAsync(h_seq + p0, base + o_seq, m * 2, hipMemcpyDeviceToHost, s));
@@ -997,9 +1034,230 @@ int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
     if (h_csum_out_or_null)
       RUDP_HIP(hipMemcpyAsync(h_csum_out_or_null + p0, base + o_co, m * 2, hipMemcpyDeviceToHost, s));
     if (h_pay) RUDP_HIP(hipMemcpyAsync(h_pay + p0 * L, base + o_pay, m * L, hipMemcpyDeviceToHost, s));
+    if (h_val) RUDP_HIP(hipMemcpyAsync(h_val + p0, base + o_va, m, hipMemcpyDeviceToHost, s));
     return 0;
   };
   return run_pipeline(pp, n, cn, h2d, kern, d2h);
+}
+
+// Packed payloads in host memory to packed frames in host memory (the send
+// side's socket buffer, utils/reliableUDP.py:53-61 per datagram).  A pre-pass
+// over the lengths (sum and maximum, per chunk) checks every length and the
+// frame buffer's capacity before anything is enqueued, and cuts the batch
+// into chunks whose payload bytes fit a slot; each chunk is one checked
+// device encode (its offsets from 0) plus one add of its base, so the
+// offsets that come back are the batch's own.
+int rudp_encode_varlen_host(const rudp_batch* h_in, uint8_t* h_frames, uint64_t frames_cap, uint64_t* h_frame_off,
+                            uint16_t* h_csum_or_null, int layout, int device) {
+  if (!h_in) return fail(RUDP_EINVAL, "rudp_encode_varlen_host: batch is NULL");
+  if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
+    return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
+  if (!h_frame_off) return fail(RUDP_EINVAL, "rudp_encode_varlen_host: frame_off is NULL");
+  const uint64_t n = h_in->n;
+  if (n == 0) {
+    h_frame_off[0] = 0;
+    return 0;
+  }
+  if (h_in->payload_off)
+    return fail(RUDP_ENOTSUP, "rudp_encode_varlen_host: packed payloads only (payload_off must be NULL)");
+  if (!h_in->len || !h_in->seq || !h_in->ack || !h_in->flags || !h_frames)
+    return fail(RUDP_EINVAL, "rudp_encode_varlen_host: NULL buffer for a non-empty batch");
+  if (n > 0x7FFFFFFFull) return fail(RUDP_EINVAL, "rudp_encode_varlen_host: at most 2^31-1 packets per call");
+  const uint64_t H = (uint64_t)layout;
+  const uint64_t bmax = stage_bytes();
+  const uint64_t hint = h_in->payload_len ? h_in->payload_len : 1u;
+  uint64_t cn = chunk_packets(n, 2u * hint + H + 13u);
+  if (cn > (1u << 22)) cn = 1u << 22;
+  // the plan: chunk k = packets [start[k], start[k + 1]) with pay[k] payload bytes
+  std::vector<uint64_t> start{0}, pay;
+  uint64_t total = 0;
+  for (uint64_t p0 = 0; p0 < n;) {
+    uint64_t m = n - p0 < cn ? n - p0 : cn;
+    for (;;) {
+      uint64_t sum = 0;
+      uint32_t mx = 0;
+      const uint32_t* l = h_in->len + p0;
+      for (uint64_t i = 0; i < m; ++i) {
+        sum += l[i];
+        mx = l[i] > mx ? l[i] : mx;
+      }
+      if (mx > 65535u)
+        return fail(RUDP_EINVAL, "rudp_encode_varlen_host: a length over 65535 in packets [%llu, %llu)",
+                    (unsigned long long)p0, (unsigned long long)(p0 + m));
+      if (sum <= bmax || m == 1) {
+        pay.push_back(sum);
+        total += sum;
+        p0 += m;
+        start.push_back(p0);
+        break;
+      }
+      m /= 2;
+    }
+  }
+  if (total && !h_in->payload) return fail(RUDP_EINVAL, "rudp_encode_varlen_host: payload is NULL");
+  if (total + n * H > frames_cap)
+    return fail(RUDP_EINVAL, "rudp_encode_varlen_host: %llu frame bytes exceed frames_cap %llu",
+                (unsigned long long)(total + n * H), (unsigned long long)frames_cap);
+  DeviceScope dev_scope;
+  int rc = dev_scope.set(device);
+  if (rc) return rc;
+  const size_t o_pay = 0, o_fr = up256(bmax), o_len = o_fr + up256(bmax + cn * H + 64u),
+               o_seq = o_len + up256(cn * 4), o_ack = o_seq + up256(cn * 2), o_fl = o_ack + up256(cn * 2),
+               o_cs = o_fl + up256(cn), o_off = o_cs + up256(cn * 2), o_st = o_off + up256((cn + 1) * 8),
+               slot = o_st + 256;
+  Pipeline* pp = pipeline_for(device);
+  std::lock_guard<std::mutex> lk(pp->mu);
+  if ((rc = pipeline_reserve(pp, pipeline_slots(), slot))) return rc;
+  size_t k = 0;
+  uint64_t pbase = 0;  // payload bytes before the current chunk
+  auto plan = [&](uint64_t p0) -> int64_t {
+    if (k > 0) pbase += pay[k - 1];
+    (void)p0;
+    const uint64_t m = start[k + 1] - start[k];
+    ++k;
+    return (int64_t)m;
+  };
+  auto h2d = [&](char* base, uint64_t p0, uint64_t m, hipStream_t s) -> int {
+    const uint64_t pb = pay[k - 1];
+    if (pb) RUDP_HIP(hipMemcpyAsync(base + o_pay, h_in->payload + pbase, pb, hipMemcpyHostToDevice, s));
+    RUDP_HIP(hipMemcpyAsync(base + o_len, h_in->len + p0, m * 4, hipMemcpyHostToDevice, s));
+    RUDP_HIP(hipMemcpyAsync(base + o_seq, h_in->seq + p0, m * 2, hipMemcpyHostToDevice, s));
+    RUDP_HIP(hipMemcpyAsync(base + o_ack, h_in->ack + p0, m * 2, hipMemcpyHostToDevice, s));
+    RUDP_HIP(hipMemcpyAsync(base + o_fl, h_in->flags + p0, m, hipMemcpyHostToDevice, s));
+    return 0;
+  };
+  auto kern = [&](char* base, uint64_t p0, uint64_t m, hipStream_t s) -> int {
+    const uint64_t pb = pay[k - 1];
+    rudp_batch sub{};
+    sub.n = m;
+    sub.payload_len = (uint32_t)(pb / m < 65535u ? pb / m : 65535u);  // the chunk's mean: picks the tiles
+    sub.seq = (const uint16_t*)(base + o_seq);
+    sub.ack = (const uint16_t*)(base + o_ack);
+    sub.flags = (const uint8_t*)(base + o_fl);
+    sub.payload = (const uint8_t*)(base + o_pay);
+    sub.len = (const uint32_t*)(base + o_len);
+    int r = rudp_encode_varlen_checked(&sub, pb, (uint8_t*)(base + o_fr), pb + m * H + 64u, (uint64_t*)(base + o_off),
+                                       h_csum_or_null ? (uint16_t*)(base + o_cs) : nullptr, (uint32_t*)(base + o_st),
+                                       layout, device, s);
+    if (r) return r;
+    const uint64_t fbase = pbase + p0 * H;
+    if (fbase) {
+      hipLaunchKernelGGL(add_base_kernel, dim3((uint32_t)((m + 256u) / 256u)), dim3(256), 0, s,
+                         (uint64_t*)(base + o_off), m + 1, fbase);
+      RUDP_HIP(hipGetLastError());
+    }
+    return 0;
+  };
+  auto d2h = [&](char* base, uint64_t p0, uint64_t m, hipStream_t s) -> int {
+    const uint64_t fb = pay[k - 1] + m * H;
+    RUDP_HIP(hipMemcpyAsync(h_frames + pbase + p0 * H, base + o_fr, fb, hipMemcpyDeviceToHost, s));
+    // offsets [p0, p0 + m): the chunk's last entry is the next chunk's first
+    const uint64_t last = start[k] == n ? m + 1 : m;
+    RUDP_HIP(hipMemcpyAsync(h_frame_off + p0, base + o_off, last * 8, hipMemcpyDeviceToHost, s));
+    if (h_csum_or_null) RUDP_HIP(hipMemcpyAsync(h_csum_or_null + p0, base + o_cs, m * 2, hipMemcpyDeviceToHost, s));
+    return 0;
+  };
+  return run_pipeline_planned(pp, n, plan, h2d, kern, d2h);
+}
+
+// Packed frames in host memory (a recvmmsg batch): chunks of consecutive
+// frames, each staged as the byte range its offsets span.  The plan scans a
+// chunk's n + 1 offsets for their least and greatest value at or below
+// frames_bytes (the only ones any kernel reads at: a frame with an offset
+// past frames_bytes or out of order is rejected before any of its bytes is
+// read), copies that range, 16-B aligned, to the slot and hands the decode a
+// frames pointer moved back by the range's start, so the caller's own
+// offsets index the slot unchanged and the device applies the checked rule
+// to them against frames_bytes: the result is rudp_decode_varlen_utf8's on
+// the same bytes.  A chunk whose range outgrows the slot is halved (a
+// ragged batch, offsets out of order) down to one frame; one valid frame
+// larger than the slot is refused.
+int rudp_decode_varlen_host(const uint8_t* h_frames, uint64_t frames_bytes, const uint64_t* h_frame_off,
+                            uint32_t len_hint, uint64_t n, const uint16_t* h_csum_in_or_null, uint16_t* h_seq,
+                            uint16_t* h_ack, uint8_t* h_flags, uint8_t* h_ok, uint16_t* h_csum_out_or_null,
+                            uint8_t* h_valid_or_null, uint32_t* h_status_or_null, int layout, int device) {
+  if (h_status_or_null) *h_status_or_null = 0;
+  if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
+    return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
+  if (n == 0) return 0;
+  if (!h_frame_off || !h_seq || !h_ack || !h_flags || !h_ok || (frames_bytes && !h_frames))
+    return fail(RUDP_EINVAL, "rudp_decode_varlen_host: NULL buffer for a non-empty batch");
+  if (n > 0x7FFFFFFFull) return fail(RUDP_EINVAL, "rudp_decode_varlen_host: at most 2^31-1 frames per call");
+  DeviceScope dev_scope;
+  int rc = dev_scope.set(device);
+  if (rc) return rc;
+  const uint64_t hint = len_hint ? len_hint : (frames_bytes / n ? frames_bytes / n : 1u);
+  const uint64_t bmax = stage_bytes();  // frame bytes a slot holds
+  // frames per chunk: 3/4 of a slot's bytes at the hint (room for ragged
+  // lengths), at least host_min_chunks chunks for a batch over 4 MiB
+  uint64_t cn = chunk_packets(n, hint * 4u / 3u + 1u);
+  if (cn > (1u << 22)) cn = 1u << 22;
+  // (64 guard bytes before and after the staged range: the UTF-8 check reads the
+  // dword before a payload chunk, the tile kernels whole 16-B chunks)
+  const size_t o_fr = 64, o_off = up256(o_fr + bmax + 64u), o_ci = o_off + up256((cn + 1) * 8), o_seq = o_ci + up256(cn * 2),
+               o_ack = o_seq + up256(cn * 2), o_co = o_ack + up256(cn * 2), o_fl = o_co + up256(cn * 2),
+               o_ok = o_fl + up256(cn), o_va = o_ok + up256(cn), slot = o_va + up256(h_valid_or_null ? cn : 0);
+  Pipeline* pp = pipeline_for(device);
+  std::lock_guard<std::mutex> lk(pp->mu);
+  if ((rc = pipeline_reserve(pp, pipeline_slots(), slot))) return rc;
+  uint64_t a0 = 0, a1 = 0;  // the current chunk's staged range [a0, a1), a0 16-B aligned
+  auto plan = [&](uint64_t p0) -> int64_t {
+    uint64_t m = n - p0 < cn ? n - p0 : cn;
+    for (;;) {
+      uint64_t lo = ~0ull, hi = 0;
+      const uint64_t* o = h_frame_off + p0;
+      for (uint64_t i = 0; i <= m; ++i) {
+        const uint64_t x = o[i];
+        if (x <= frames_bytes) {
+          lo = x < lo ? x : lo;
+          hi = x > hi ? x : hi;
+        }
+      }
+      if (lo > hi) lo = hi = 0;  // no offset inside the buffer: every frame is rejected unread
+      const uint64_t b0 = lo & ~15ull;
+      uint64_t b1 = (hi + 15u) & ~15ull;
+      if (b1 > frames_bytes) b1 = frames_bytes;
+      if (b1 - b0 <= bmax) {
+        a0 = b0;
+        a1 = b1 > b0 ? b1 : b0;
+        return (int64_t)m;
+      }
+      if (m == 1)
+        return fail(RUDP_ENOTSUP, "rudp_decode_varlen_host: frame %llu spans %llu bytes, over the %zu-byte staging slot",
+                    (unsigned long long)p0, (unsigned long long)(b1 - b0), (size_t)bmax);
+      m /= 2;
+    }
+  };
+  auto h2d = [&](char* base, uint64_t p0, uint64_t m, hipStream_t s) -> int {
+    if (a1 > a0) RUDP_HIP(hipMemcpyAsync(base + o_fr, h_frames + a0, a1 - a0, hipMemcpyHostToDevice, s));
+    RUDP_HIP(hipMemcpyAsync(base + o_off, h_frame_off + p0, (m + 1) * 8, hipMemcpyHostToDevice, s));
+    if (h_csum_in_or_null)
+      RUDP_HIP(hipMemcpyAsync(base + o_ci, h_csum_in_or_null + p0, m * 2, hipMemcpyHostToDevice, s));
+    return 0;
+  };
+  auto kern = [&](char* base, uint64_t, uint64_t m, hipStream_t s) -> int {
+    // frame bytes at offset x (a0 <= x < a1) sit at base + (x - a0)
+    const uint8_t* frames = reinterpret_cast<const uint8_t*>(base + o_fr) - a0;
+    return decode_varlen(frames, (const uint64_t*)(base + o_off), (uint32_t)(hint < 0xFFFFFFFFull ? hint : 0xFFFFFFFFu),
+                         m, h_csum_in_or_null ? (const uint16_t*)(base + o_ci) : nullptr, (uint16_t*)(base + o_seq),
+                         (uint16_t*)(base + o_ack), (uint8_t*)(base + o_fl), (uint8_t*)(base + o_ok),
+                         h_csum_out_or_null ? (uint16_t*)(base + o_co) : nullptr, nullptr, layout, device, s, true,
+                         nullptr, frames_bytes, h_valid_or_null ? (uint8_t*)(base + o_va) : nullptr);
+  };
+  auto d2h = [&](char* base, uint64_t p0, uint64_t m, hipStream_t s) -> int {
+    RUDP_HIP(hipMemcpyAsync(h_seq + p0, base + o_seq, m * 2, hipMemcpyDeviceToHost, s));
+    RUDP_HIP(hipMemcpyAsync(h_ack + p0, base + o_ack, m * 2, hipMemcpyDeviceToHost, s));
+    RUDP_HIP(hipMemcpyAsync(h_flags + p0, base + o_fl, m, hipMemcpyDeviceToHost, s));
+    RUDP_HIP(hipMemcpyAsync(h_ok + p0, base + o_ok, m, hipMemcpyDeviceToHost, s));
+    if (h_csum_out_or_null)
+      RUDP_HIP(hipMemcpyAsync(h_csum_out_or_null + p0, base + o_co, m * 2, hipMemcpyDeviceToHost, s));
+    if (h_valid_or_null) RUDP_HIP(hipMemcpyAsync(h_valid_or_null + p0, base + o_va, m, hipMemcpyDeviceToHost, s));
+    return 0;
+  };
+  rc = run_pipeline_planned(pp, n, plan, h2d, kern, d2h);
+  if (rc) return rc;
+  if (h_status_or_null && memchr(h_ok, RUDP_OK_BAD_OFFSETS, n)) *h_status_or_null = RUDP_ST_OFFSETS;
+  return 0;
 }
 
 // ---- the proxy's retransmission count over a stream of batches ----------------

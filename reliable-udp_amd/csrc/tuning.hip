@@ -277,7 +277,8 @@ RUDP_API int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, i
 // 52: varlen tile sum pass (2 from 128-B block sums, 0 chunk by chunk);
 // 62: packed small-frame dedup in one launch (dedup_small_kernel; 0: two passes);
 // 63: varlen decode tile frame sums from 128-B block sums (0: chunk by chunk);
-// 64: a checked small-frame encode of one tile in one launch (no pass 1).
+// 64: a checked small-frame encode of one tile in one launch (no pass 1);
+// 71: *_host pipeline: least chunks for a batch over 4 MiB (copy / kernel overlap).
 // (54: chunked / rotated XCD orders, measured within 2% and removed;
 // profiles/r02/headline/xcd_orders.json.)
 // (55, 56: a small-tile launch tail, and 57: persistent workgroups looping over the tiles,
@@ -330,7 +331,8 @@ RUDP_API int rudpx_tune(int key, int value) {
             : key == 67 ? &t.varlen_map_bal
             : key == 68 ? &t.varlen_decode_nt
             : key == 69 ? &t.varlen_decode_r4
-            : key == 70 ? &t.dedup_small_fpt : nullptr;
+            : key == 70 ? &t.dedup_small_fpt
+            : key == 71 ? &t.host_min_chunks : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }

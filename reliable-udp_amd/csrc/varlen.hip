@@ -500,7 +500,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     }
     lds_map16[k] = (uint16_t)e;
   };
-  if (a.map_bal) {
+  if (RUDP_TOOLS && a.map_bal) {  // (measured slower at equal lengths: diagnostics build only)
     // by units: lane tid takes units [tid kc, (tid + 1) kc) whatever frames
     // they fall in, so a tile of ragged lengths does not wait for its longest
     // frame's G lanes (a frame's units are its length / 16)
@@ -946,7 +946,7 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   const uint32_t q = tid >> glog, g = tid & (G - 1u);
   uint32_t* lds_fo = reinterpret_cast<uint32_t*>(lds);                       // [T + 1]
   unsigned char* img = lds + ((((T + 1u) * 4u) + 15u) & ~15u) + kVTGuard;   // the run
-  const bool blk = a.tile_sums == 2u;
+  const bool blk = RUDP_TOOLS && a.tile_sums == 2u;  // (measured slower: diagnostics build only)
   uint32_t* lds_blk = reinterpret_cast<uint32_t*>(lds + dvt_blk_off(T, a.tile_cap));  // [cap / 128 + 4]
   const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint64_t left = a.n - p0;
@@ -1099,6 +1099,7 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
 // frame's leader subtracts.  Offsets not in order, or past the buffer: the
 // index pass raises span_flag, and the launch decodes frame by frame (every
 // pair checked, decode_varlen_frame).
+#if RUDP_TOOLS  // measured slower than the frame tiles: the diagnostics build only
 constexpr uint32_t kSpanNF = 128;  // frames of one span held in LDS (more: per-frame path)
 
 // one record per span (and one past the last): first frame starting at or
@@ -1315,6 +1316,7 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_span_kernel(VarlenArgs a
                             window16_dw(reinterpret_cast<const uint32_t*>(img), fs));
   }
 }
+#endif  // RUDP_TOOLS
 
 // Strict UTF-8 validation kernels (the checks themselves: utf8_device.hpp).
 __global__ void __launch_bounds__(kBlock) validate_utf8_par_kernel(Utf8Args a) {
@@ -2207,6 +2209,7 @@ int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream)
 // (utils/reliableUDP.py:121, get_payload's strict decode at utils/packet.py:73).
 template <int H, bool U8>
 static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
+#if RUDP_TOOLS  // byte spans (measured slower; the diagnostics build only)
   if (args.span_rec) {  // byte spans: the index pass, then one workgroup per span (or per T frames)
     const uint32_t nt = (uint32_t)args.span_count;
     const uint64_t idx_threads = args.n + 2u + nt;
@@ -2220,6 +2223,7 @@ static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
                        dsp_lds_bytes(args.tile_cap), stream, args);
     return (int)hipGetLastError();
   }
+#endif
   if (args.small_fpt && args.glog != kNoVec && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0)
     return launch_decode_small<H, U8>(args, stream);
   if (args.glog != kNoVec && args.tile_cap && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0) {
@@ -2230,6 +2234,7 @@ static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
       // 76 VGPRs (6 waves per SIMD).  Asking the allocator for 7 or 8 waves
       // spills and was slower at every size (1M x 1479 B 0.265 -> 0.306 ms;
       // profiles/r01/sweeps/varlen_decode_waves.json).
+#if RUDP_TOOLS  // chunks read four at a time and two-wave tiles: measured slower
       if (args.dec_r4) {
         hipLaunchKernelGGL((decode_varlen_tile_kernel<H, U8, kBlock, true>), dim3((uint32_t)blocks), dim3(kBlock),
                            lds, stream, args);
@@ -2241,6 +2246,7 @@ static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
                            args);
         return (int)hipGetLastError();
       }
+#endif
       hipLaunchKernelGGL((decode_varlen_tile_kernel<H, U8>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
       return (int)hipGetLastError();
     }
@@ -2255,7 +2261,9 @@ static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
   return (int)hipGetLastError();
 }
 
+#if RUDP_TOOLS
 bool decode_span_fits(uint64_t cap) { return cap < 65536u && dsp_lds_bytes((uint32_t)cap) <= 65536u; }
+#endif
 
 int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream) {
   if (args.n == 0) return 0;

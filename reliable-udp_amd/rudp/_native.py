@@ -25,7 +25,7 @@ LAYOUT_RUDP5 = 5
 LAYOUT_RUDP7 = 7
 OK_BAD_CSUM, OK_GOOD, OK_SHORT, OK_UNVERIFIED, OK_BAD_OFFSETS = 0, 1, 2, 3, 4
 EINVAL, ENOMEM, ENOTSUP, EHIP_BASE = -22, -12, -95, -1000
-ABI_VERSION = 6
+ABI_VERSION = 7
 # status bits of the sync-free varlen calls (RUDP_ST_*)
 ST_LEN, ST_PAYLOAD, ST_FRAMES_CAP, ST_OFFSETS = 1, 2, 4, 8
 DUP_BAD_OFFSETS = 2  # rudp_dedup_window_checked: a frame whose offsets were rejected
@@ -40,6 +40,7 @@ EXPORTS = (
     "rudp_udp_recv_batch_from", "rudp_udp_send_batch_to", "rudp_dedup_window_checked",
     "rudp_decode_utf8", "rudp_decode_varlen_utf8",
     "rudp_dedup_stream_create", "rudp_dedup_stream_push", "rudp_dedup_stream_counts", "rudp_dedup_stream_destroy",
+    "rudp_decode_varlen_host", "rudp_encode_varlen_host",
 )
 
 
@@ -76,7 +77,9 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rudp_encode": [ctypes.POINTER(RudpBatch), P, P, I, I, P],
         "rudp_decode": [P, P, U32, U64, P, P, P, P, P, P, P, I, I, P],
         "rudp_encode_host": [ctypes.POINTER(RudpBatch), P, P, I, I],
-        "rudp_decode_host": [P, U32, U64, P, P, P, P, P, P, P, I, I],
+        "rudp_decode_host": [P, U32, U64, P, P, P, P, P, P, P, P, I, I],
+        "rudp_decode_varlen_host": [P, U64, P, U32, U64, P, P, P, P, P, P, P, P, I, I],
+        "rudp_encode_varlen_host": [ctypes.POINTER(RudpBatch), P, U64, P, P, I, I],
         "rudp_synth": [U64, U64, U64, U32, I, P, P, P, P, I, P],
         "rudp_encode_varlen": [ctypes.POINTER(RudpBatch), P, P, P, I, I, P],
         "rudp_validate_utf8": [P, P, U32, U64, I, P, I, P],

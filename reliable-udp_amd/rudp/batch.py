@@ -285,7 +285,7 @@ def _pack_host(tab: HeaderTable, payloads, H, want_csum, device, out=None, csum_
     return frames, csum
 
 
-def _unpack_host(frames, H, csum, copy_payload, device):
+def _unpack_host(frames, H, csum, copy_payload, device, utf8=False):
     frames = _host_arr(frames, "frames", np.uint8, 2)
     n, F = frames.shape
     L = max(F - H, 0)
@@ -299,13 +299,15 @@ def _unpack_host(frames, H, csum, copy_payload, device):
         if csum.shape[0] != n:
             raise ValueError(f"csum has {csum.shape[0]} entries for {n} frames")
     pay = np.empty((n, L), np.uint8) if copy_payload else None
+    valid = np.empty((n,), np.uint8) if utf8 else None
     if n:
         _native.check(_native.lib().rudp_decode_host(
             _ptr(frames), F, n, _ptr(csum) if csum is not None else None, _ptr(seq), _ptr(ack),
-            _ptr(flags), _ptr(ok), _ptr(cs), _ptr(pay) if pay is not None else None, H, device))
+            _ptr(flags), _ptr(ok), _ptr(cs), _ptr(pay) if pay is not None else None,
+            _ptr(valid) if valid is not None else None, H, device))
     if pay is None:
         pay = frames[:, H:] if F >= H else frames[:, :0]
-    return DecodedBatch(seq, ack, flags, ok, cs, pay)
+    return DecodedBatch(seq, ack, flags, ok, cs, pay, None, valid)
 
 
 # ------------------------------------------------------------------ public API
@@ -336,19 +338,17 @@ def unpack_batch(frames, layout: Union[str, int] = "rudp7", *, csum=None,
 
     ``csum`` (rudp5 only): sideband checksums to verify against.  The payload
     is returned as a zero-copy view ``frames[:, H:]`` unless ``copy_payload``.
-    ``utf8`` (device tensors): also ``valid``, u8 [N], 1 where
-    Packet(frame).get_payload() would return and 0 where its strict UTF-8
-    decode would raise (utils/packet.py:68-73), judged in the same pass over
-    the frames (rudp_decode_utf8).
+    ``utf8``: also ``valid``, u8 [N], 1 where Packet(frame).get_payload()
+    would return and 0 where its strict UTF-8 decode would raise
+    (utils/packet.py:68-73), judged in the same pass over the frames
+    (rudp_decode_utf8; numpy frames: rudp_decode_host, staged through the GPU).
     """
     H = layout_header_len(layout)
     if H == 7 and csum is not None:
         raise ValueError("rudp7 carries its checksum in-band; csum= is for rudp5")
     if _is_torch(frames):
         return _unpack_device(frames, H, csum, copy_payload, stream, utf8)
-    if utf8:
-        raise ValueError("utf8=True needs device tensors (use validate_utf8 on the host-staged result)")
-    return _unpack_host(frames, H, csum, copy_payload, device)
+    return _unpack_host(frames, H, csum, copy_payload, device, utf8)
 
 
 def synth_batch(n: int, payload_len: int, seed: int, *, first_index: int = 0, ascii: bool = True,
@@ -540,9 +540,63 @@ def _int_tensor(t, name, device, n=None, dtypes=None):
         raise ValueError(f"{name} has {t.shape[0]} entries, expected {n}")
 
 
+class HostVarlenFrames(NamedTuple):
+    """Result of ``pack_batch_varlen`` on numpy arrays (host memory, staged
+    through the GPU by rudp_encode_varlen_host): frames (u8, back to back),
+    frame_off (int64 [N + 1]), csum (u16 [N] or None), status (always 0: the
+    batch was checked before any work, and a bad one raised)."""
+    frames: Any
+    frame_off: Any
+    csum: Any
+    status: int = 0
+
+    def check(self) -> "HostVarlenFrames":
+        return self
+
+
+def _pack_varlen_host(tab: HeaderTable, payload, lengths, H, payload_off, want_csum, out, device):
+    if payload_off is not None:
+        raise ValueError("host-memory varlen encode takes packed payloads (payload_off=None)")
+    payload = _host_arr(payload, "payload", np.uint8, 1)
+    lengths = np.ascontiguousarray(lengths)
+    if lengths.dtype not in (np.int32, np.uint32) or lengths.ndim != 1:
+        raise TypeError("lengths must be a 1-D int32/uint32 array")
+    n = lengths.shape[0]
+    seq = _host_arr(tab.seq, "seq", np.uint16, 1)
+    ack = _host_arr(tab.ack, "ack", np.uint16, 1)
+    flags = _host_arr(tab.flags, "flags", np.uint8, 1)
+    for name, a in (("seq", seq), ("ack", ack), ("flags", flags)):
+        if a.shape[0] != n:
+            raise ValueError(f"{name} has {a.shape[0]} entries for {n} packets")
+    if n and (int(lengths.min()) < 0 or int(lengths.max()) > 65535):
+        raise ValueError("lengths must lie in [0, 65535]")
+    if int(lengths.sum(dtype=np.int64)) != payload.size:
+        raise ValueError("packed payloads: sum(lengths) must equal payload.numel(); "
+                         "gathered payloads: payload_off + lengths must stay inside payload")
+    need = payload.size + n * H
+    if out is not None:
+        if not isinstance(out, np.ndarray) or out.dtype != np.uint8 or out.ndim != 1 \
+                or not out.flags["C_CONTIGUOUS"] or not out.flags["WRITEABLE"]:
+            raise ValueError("out must be a writeable C-contiguous 1-D uint8 array")
+        if out.size < need:
+            raise ValueError("out is too small for the frames (sum(lengths) + N * header bytes)")
+        frames = out
+    else:
+        frames = np.empty((need,), np.uint8)
+    off = np.empty((n + 1,), np.int64)
+    csum = np.empty((n,), np.uint16) if want_csum else None
+    b = _native.RudpBatch(n=n, payload_len=min(payload.size // n, 65535) if n else 0, reserved=0,
+                          seq=_ptr(seq), ack=_ptr(ack), flags=_ptr(flags), payload=_ptr(payload),
+                          len=_ptr(lengths.view(np.uint32)), payload_off=None)
+    _native.check(_native.lib().rudp_encode_varlen_host(
+        ctypes.byref(b), _ptr(frames), frames.size, off.ctypes.data, _ptr(csum) if csum is not None else None,
+        H, device))
+    return HostVarlenFrames(frames, off, csum, 0)
+
+
 def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp7", *,
                       payload_off=None, want_csum: Optional[bool] = None, stream=None, out=None,
-                      check: bool = True, reuse: Optional[VarlenFrames] = None) -> VarlenFrames:
+                      check: bool = True, reuse: Optional[VarlenFrames] = None, device: int = 0) -> VarlenFrames:
     """Frame + checksum a variable-length batch on a HIP device.
 
     ``payload``: u8 1-D tensor holding the payload bytes; ``lengths``: int32
@@ -563,10 +617,19 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
     payloads, from one device read of the lengths' sum.  ``reuse``: an earlier
     result of this call for the same N and csum choice, whose buffers take this
     call's outputs (no allocation; the earlier result's contents are replaced).
+
+    numpy arrays (packed payloads in host memory, a send buffer): staged
+    through GPU ``device`` by rudp_encode_varlen_host, synchronously; the
+    lengths are checked before any work (ValueError) and the result is a
+    ``HostVarlenFrames`` of numpy arrays.
     """
-    import torch
     H = layout_header_len(layout)
     tab = _as_table(headers)
+    if want_csum is None:
+        want_csum = H == 5
+    if not _is_torch(payload):
+        return _pack_varlen_host(tab, payload, lengths, H, payload_off, want_csum, out, device)
+    import torch
     dev = payload.device
     if dev.type != "cuda":
         raise ValueError("varlen batches run on a HIP device")
@@ -605,8 +668,6 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
             raise ValueError("lengths must lie in [0, 65535]")
         if omin < 0 or oend > payload.numel():
             raise ValueError("payload_off + lengths must stay inside payload")
-    if want_csum is None:
-        want_csum = H == 5
     f_at, cs_bytes = VarlenFrames.layout(n, want_csum)
     if reuse is not None:
         # the caller's earlier result of the same shape: its buffer takes this call's outputs
@@ -651,9 +712,37 @@ def _check_offsets(frames, frame_off, stream=None) -> int:
     return min((last - first) // n, 0xFFFFFFFF)
 
 
+def _unpack_varlen_host(frames, frame_off, H, csum, check, utf8, device, len_hint=0):
+    frames = _host_arr(frames, "frames", np.uint8, 1)
+    frame_off = np.ascontiguousarray(frame_off)
+    if frame_off.dtype not in (np.int64, np.uint64) or frame_off.ndim != 1:
+        raise TypeError("frame_off must be a 1-D int64 array")
+    n = frame_off.shape[0] - 1
+    if n < 0:
+        raise ValueError("frame_off needs N + 1 entries")
+    if csum is not None:
+        csum = _host_arr(csum, "csum", np.uint16, 1)
+        if csum.shape[0] != n:
+            raise ValueError(f"csum has {csum.shape[0]} entries for {n} frames")
+    seq, ack, cs = (np.empty((n,), np.uint16) for _ in range(3))
+    flags, ok = np.empty((n,), np.uint8), np.empty((n,), np.uint8)
+    valid = np.empty((n,), np.uint8) if utf8 else None
+    status = np.zeros((1,), np.uint32)
+    if n:
+        # (negative int64 offsets read as huge u64 ones: past the buffer, so rejected)
+        _native.check(_native.lib().rudp_decode_varlen_host(
+            _ptr(frames), frames.size, frame_off.ctypes.data, min(len_hint or frames.size // n, 0xFFFFFFFF), n,
+            _ptr(csum) if csum is not None else None, _ptr(seq), _ptr(ack), _ptr(flags), _ptr(ok), _ptr(cs),
+            _ptr(valid) if valid is not None else None, status.ctypes.data, H, device))
+    off = frame_off.astype(np.int64, copy=False)
+    pay = (np.minimum(off[:-1] + H, off[1:]), off[1:])
+    res = DecodedBatch(seq, ack, flags, ok, cs, pay, status, valid)
+    return res.check() if check else res
+
+
 def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *, csum=None,
                         stream=None, check: bool = True, reuse: Optional["VarlenDecoded"] = None,
-                        utf8: bool = False) -> "VarlenDecoded":
+                        utf8: bool = False, device: int = 0) -> "VarlenDecoded":
     """Parse + verify frames packed back to back (offsets as pack_batch_varlen returns).
 
     The payload is zero-copy: ``payload`` is the pair ``(start, end)`` of int64
@@ -668,11 +757,20 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
     Packet(frame).get_payload() would return, 0 where its strict UTF-8 decode
     would raise, utils/packet.py:68-73; 0 for a rejected frame), judged by the
     decode kernel from the bytes it already holds (rudp_decode_varlen_utf8).
+
+    numpy arrays (a receive buffer in host memory): staged through GPU
+    ``device`` by rudp_decode_varlen_host, synchronously, with the same
+    per-frame offset rule; the result is a ``DecodedBatch`` of numpy arrays
+    (payload: the pair (start, end) of int64 arrays, status u32 [1]).
     """
-    import torch
     H = layout_header_len(layout)
     if H == 7 and csum is not None:
         raise ValueError("rudp7 carries its checksum in-band; csum= is for rudp5")
+    if not _is_torch(frames):
+        if reuse is not None:
+            raise ValueError("reuse= is for device batches")
+        return _unpack_varlen_host(frames, frame_off, H, csum, check, utf8, device)
+    import torch
     dev = frames.device
     _dev_check(frames, "frames", torch.uint8, 1, dev)
     _int_tensor(frame_off, "frame_off", dev, dtypes=(torch.int64,))

@@ -130,3 +130,57 @@ def test_python_api_validation():
         batch.unpack_batch(np.zeros((3, 20), np.uint8), "rudp7", csum=seq)
     assert batch.make_flags(syn=1, fin=1) == 0xA0
     assert batch.make_flags(ack=1, offset=0x3F) == 0x5F
+
+
+def _code_object_kernels(path):
+    """Kernel names of the gfx950 code objects in a library's offload bundles
+    (one per translation unit in .hip_fatbin: __CLANG_OFFLOAD_BUNDLE__, entry
+    count, then per entry offset / size / triple), read from each code
+    object's symbol table by llvm-readelf: names ending in .kd are kernel
+    descriptors."""
+    import struct
+    import subprocess
+    import tempfile
+    data = path.read_bytes()
+    magic = b"__CLANG_OFFLOAD_BUNDLE__"
+    objs, at = [], data.find(magic)
+    while at >= 0:
+        (count,) = struct.unpack_from("<Q", data, at + len(magic))
+        pos = at + len(magic) + 8
+        for _ in range(count):
+            off, size, tlen = struct.unpack_from("<QQQ", data, pos)
+            triple = data[pos + 24:pos + 24 + tlen].decode()
+            pos += 24 + tlen
+            if "gfx950" in triple and size:
+                objs.append(data[at + off:at + off + size])
+        at = data.find(magic, at + 1)
+    assert objs, "no gfx950 code object"
+    readelf = next((p for p in ("/opt/rocm/lib/llvm/bin/llvm-readelf", "/opt/rocm/llvm/bin/llvm-readelf")
+                    if __import__("os").path.exists(p)), None)
+    if readelf is None:
+        pytest.skip("llvm-readelf not found")
+    names = set()
+    for co in objs:
+        with tempfile.NamedTemporaryFile(suffix=".co") as f:
+            f.write(co)
+            f.flush()
+            out = subprocess.run([readelf, "--syms", "--wide", f.name], capture_output=True, text=True,
+                                 check=True).stdout
+        names |= {ln.split()[-1][:-3] for ln in out.splitlines() if ln.split() and ln.split()[-1].endswith(".kd")}
+    return names
+
+
+def test_product_code_object_ships_only_measured_forms():
+    """Kernel forms measured slower than the defaults live in the
+    diagnostics build only: the byte-span decode (index pass and span kernel),
+    the decode tile reading four chunks at a time (R4) and the two-wave
+    (128-thread) decode tiles.  librudp.so's code object has none of them;
+    librudp_tools.so keeps them for the A/B tools and their tests."""
+    prod = _code_object_kernels(_native.LIB_PATH)
+    assert any("decode_varlen_tile_kernel" in k for k in prod)
+    losing = [k for k in prod if "decode_span_index_kernel" in k or "decode_varlen_span_kernel" in k
+              or re.search(r"decode_varlen_tile_kernelILi[57]ELb[01]ELj(128ELb0|256ELb1)E", k)]
+    assert not losing, losing
+    tools = _code_object_kernels(_native.TOOLS_LIB_PATH)
+    assert any("decode_varlen_span_kernel" in k for k in tools)
+    assert any(re.search(r"decode_varlen_tile_kernelILi7ELb0ELj128ELb0E", k) for k in tools)

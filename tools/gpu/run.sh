@@ -8,6 +8,7 @@
 #   bash tools/gpu/run.sh trace TAG PROG [args]            # rocprofv3 kernel trace + stats
 #   bash tools/gpu/run.sh pmc TAG PROG [args]              # FETCH_SIZE and WRITE_SIZE, one pass each
 #   bash tools/gpu/run.sh pmcsq TAG PROG [args]            # 8 SQ counters (wave cycles, waits, VALU/LDS) in one pass
+#   bash tools/gpu/run.sh pmcvalu TAG PROG [args]          # VALU-busy view: 8 SQ + 2 GRBM counters in one pass
 #   bash tools/gpu/run.sh sweep TAG [tools/sweep.py args]  # interleaved A/B sweep
 #   bash tools/gpu/run.sh py TAG SCRIPT [args]             # any python tool, output to TAG.log
 #
@@ -42,6 +43,11 @@ case "$step" in
     timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
       SQ_INSTS_VALU SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE -f csv -d "$O/${tag}_sq" -o run \
       -- python3 "$@" > "$O/${tag}_sq.log" 2>&1 ;;
+  pmcvalu)
+    tag=$1; shift
+    timeout -s KILL 300 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY \
+      SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_WAVES GRBM_GUI_ACTIVE GRBM_COUNT -f csv -d "$O/${tag}_valu" -o run \
+      -- python3 "$@" > "$O/${tag}_valu.log" 2>&1 ;;
   sweep)
     tag=$1; shift
     timeout -k 10 500 python -u tools/sweep.py "$@" > "$O/sweep_$tag.json" 2> "$O/sweep_$tag.err" ;;

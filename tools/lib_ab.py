@@ -50,9 +50,10 @@ def main():
                                   ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                   ctypes.c_void_p, ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         h.rudp_decode.restype = ctypes.c_int
-        h.rudp_decode_utf8.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64] + \
-            [ctypes.c_void_p] * 8 + [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
-        h.rudp_decode_utf8.restype = ctypes.c_int
+        if hasattr(h, "rudp_decode_utf8"):  # ABI 6 on (older trees lack it)
+            h.rudp_decode_utf8.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64] + \
+                [ctypes.c_void_p] * 8 + [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+            h.rudp_decode_utf8.restype = ctypes.c_int
         h.rudp_encode_varlen_checked.argtypes = [ctypes.POINTER(_native.RudpBatch), ctypes.c_uint64, ctypes.c_void_p,
                                                  ctypes.c_uint64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                                  ctypes.c_int, ctypes.c_int, ctypes.c_void_p]

@@ -24,6 +24,20 @@ import torch  # noqa: E402
 from rudp import batch  # noqa: E402
 
 
+def text_payloads(n, L, dev):
+    """n copies of one L-byte payload of valid 1-4 byte UTF-8 characters, as bench.py's
+    decode_utf8_1Mx1472_multibyte_text leg frames them."""
+    text = ("\u00e9\u4e2d\U0001f600a\u00df\u0416\u20ac\U0001d11e" * (L // 8 + 8)).encode()[:L]
+    while True:
+        try:
+            text.decode()
+            break
+        except UnicodeDecodeError:
+            text = text[:-1]
+    text += b"x" * (L - len(text))
+    return torch.frombuffer(bytearray(text), dtype=torch.uint8).to(dev).expand(n, L).contiguous()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--op", choices=["encode", "decode", "decode_copy", "roundtrip", "encode_varlen",
@@ -39,6 +53,9 @@ def main():
                     help="varlen ops: lengths uniform in [0, 2L] (mean L) instead of all L")
     ap.add_argument("--utf8", action="store_true",
                     help="decode ops: strict UTF-8 of each payload in the same pass (rudp_decode_utf8)")
+    ap.add_argument("--text", action="store_true",
+                    help="fixed-length ops: every payload valid multi-byte UTF-8 text of 1-4 byte "
+                         "characters (bench leg decode_utf8_1Mx1472_multibyte_text)")
     ap.add_argument("--tune", default="",
                     help="rudpx_tune knobs to set first, as key=value[,key=value...]")
     ap.add_argument("--gap-ms", type=float, default=0.0,
@@ -52,6 +69,8 @@ def main():
     sets = []
     for _ in range(nsets):
         tab, pay = batch.synth_batch(args.n, args.L, 0x5EED0004, device=dev)
+        if args.text:
+            pay = text_payloads(args.n, args.L, dev)
         fr, _ = batch.pack_batch(tab, pay, args.layout)
         sets.append((tab, pay, fr))
     import ctypes
@@ -135,7 +154,7 @@ def main():
     e.record()
     e.synchronize()
     payload_bytes = int(vsets[0][1].numel()) if vsets else args.n * args.L
-    print(json.dumps({"op": args.op, "utf8": args.utf8, "L": args.L, "n": args.n, "layout": args.layout, "tune": args.tune,
+    print(json.dumps({"op": args.op, "utf8": args.utf8, "text": args.text, "L": args.L, "n": args.n, "layout": args.layout, "tune": args.tune,
                       "ragged": args.ragged, "payload_bytes": payload_bytes,
                       "buffer_sets": nsets, "ms_per_launch": s.elapsed_time(e) / args.steps}))
 
