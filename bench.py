@@ -409,7 +409,9 @@ def legs(torch, batch, device, steps):
         "GiB_s": n * L / dt / GIB, "ms": dt * 1e3,
         "pcie_GBs_each_way": n * (L + 6) / dt / 1e9,
         "note": "pinned host in/out, rudp_encode_host (H2D, kernel, D2H on two streams)"}
-    del hp, hs, ha, hf, hout
+    del hp, hs, ha, hf
+    out.update(e2e_host_decode_legs(torch, batch, hout.numpy(), n, L))
+    del hout
     # BASELINE config 5's shape on one GPU: 16M x 1472 B (23.6 GB in, 23.7 GB out)
     torch.cuda.empty_cache()
     w16 = Workload(torch, batch, C5_PACKETS, 1472, "rudp7", 0, C5_SEED, device, min_bytes=0)
@@ -613,13 +615,81 @@ def legs(torch, batch, device, steps):
     return out
 
 
+def e2e_host_decode_legs(torch, batch, frames, n, L, reps=3):
+    """The receive side from host memory (north_star: the path starts and ends in a
+    socket buffer), through the Python entries: the frames in pinned host memory,
+    staged through the GPU by the *_host pipeline, outputs back in host arrays.
+    1M x 1472 B rudp7 frames: parse + verify + get_payload()'s strict UTF-8
+    (rudp_decode_host with h_valid; utils/reliableUDP.py:118-121, utils/packet.py:73);
+    1M one-character rudp5 datagrams packed back to back (a recvmmsg batch): the
+    same through rudp_decode_varlen_host, and their encode from packed host
+    payloads (rudp_encode_varlen_host)."""
+    import numpy as np
+    out = {}
+    d = batch.unpack_batch(frames, "rudp7", utf8=True)  # first call: slots, pinned staging, warm
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        d = batch.unpack_batch(frames, "rudp7", utf8=True)
+    dt = (time.perf_counter() - t0) / reps
+    out["e2e_host_decode_utf8_1Mx1472"] = {
+        "GiB_s": n * L / dt / GIB, "ms": dt * 1e3, "pcie_GBs_h2d": n * (L + 7) / dt / 1e9,
+        "all_valid_and_verified": bool((d.valid == 1).all()) and bool((d.ok == 1).all()),
+        "note": "pinned host frames -> unpack_batch(numpy, utf8=True): rudp_decode_host (H2D, fused "
+                "decode + strict UTF-8 kernel, D2H of seq/ack/flags/ok/csum/valid on three streams), "
+                "outputs into numpy arrays the entry allocates"}
+    del d
+    # 1M one-character datagrams: packed frames + offsets in pinned host memory
+    m = 1 << 20
+    pin = lambda k, dt: torch.empty(k, dtype=dt, pin_memory=True).numpy()  # noqa: E731
+    rng = np.random.default_rng(0x5EED0004)
+    seq = pin(m, torch.uint16)
+    seq[:] = np.arange(m, dtype=np.uint16)
+    ack, flg = pin(m, torch.uint16), pin(m, torch.uint8)
+    ack[:] = rng.integers(0, 1 << 16, m, dtype=np.uint16)
+    flg[:] = 0x40
+    pay = pin(m, torch.uint8)
+    pay[:] = rng.integers(0x20, 0x7F, m, dtype=np.uint8)
+    lens = pin(m, torch.int32)
+    lens[:] = 1
+    enc = batch.pack_batch_varlen((seq, ack, flg), pay, lens, "rudp5", want_csum=True)
+    fr, fo, cs = pin(enc.frames.size, torch.uint8), pin(m + 1, torch.int64), pin(m, torch.uint16)
+    fr[:], fo[:], cs[:] = enc.frames, enc.frame_off, enc.csum
+    te = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        enc = batch.pack_batch_varlen((seq, ack, flg), pay, lens, "rudp5", want_csum=True, out=fr)
+        te.append(time.perf_counter() - t0)
+    dv = batch.unpack_batch_varlen(fr, fo, "rudp5", csum=cs, utf8=True)
+    td = []
+    for _ in range(reps):
+        t0 = time.perf_counter()
+        dv = batch.unpack_batch_varlen(fr, fo, "rudp5", csum=cs, utf8=True)
+        td.append(time.perf_counter() - t0)
+    ok = bool((dv.ok == 1).all()) and bool((dv.valid == 1).all()) and bool(np.array_equal(dv.seq, seq))
+    te, td = sorted(te)[len(te) // 2], sorted(td)[len(td) // 2]
+    out["e2e_host_varlen_1M_x_1char"] = {
+        "decode_utf8_Mpkt_s": m / td / 1e6, "decode_ms": td * 1e3,
+        "encode_Mpkt_s": m / te / 1e6, "encode_ms": te * 1e3,
+        "decoded_all_valid_and_verified": ok,
+        "note": "pinned host buffers: unpack_batch_varlen(numpy, csum, utf8=True) = rudp_decode_varlen_host "
+                "(6 B frames + 8 B offsets + 2 B sideband checksum per datagram up, 10 B of fields down); "
+                "pack_batch_varlen(numpy, out=pinned) = rudp_encode_varlen_host (10 B up, 6 B frame + 8 B "
+                "offset + 2 B checksum down); medians of 3 calls"}
+    return out
+
+
 def small_batch_calls(torch, batch, device, sizes=(1024, 65536), reps=200):
     """Per-call times at the batch sizes a reference caller produces: one-character
     rudp5 datagrams (utils/reliableUDP.py:11), n per call.  ``us_per_call``: the
     median of 5 runs of `reps` back-to-back sync-free calls on one stream (HIP
-    events, outputs reused); ``us_latency``: wall time of one call plus its
-    synchronize, median of `reps` (what a caller that waits for every batch sees)."""
-    out = {}
+    events, outputs reused).  ``us_latency``: wall time of one call plus its
+    synchronize (what a caller that waits for every batch sees), median of `reps`
+    rounds in which every size and op (and ``floor``: a one-element torch add, the
+    box's launch + synchronize floor) takes one turn, so drift of the host or GPU
+    state over the leg falls on all of them alike; ``us_latency_event``: the same
+    call waited for by an event recorded behind it instead of a device-wide
+    synchronize."""
+    ops, lasts = {}, []
     for n in sizes:
         tab, pay = batch.synth_batch(n, 1, SEEDS[1472], device=device)
         lens = torch.ones(n, dtype=torch.int32, device=device)
@@ -627,33 +697,55 @@ def small_batch_calls(torch, batch, device, sizes=(1024, 65536), reps=200):
         enc = batch.pack_batch_varlen(tab, flat, lens, "rudp5", want_csum=True)
         last = {"e": enc, "d": batch.unpack_batch_varlen(enc.frames, enc.frame_off, "rudp5", csum=enc.csum),
                 "u": batch.unpack_batch_varlen(enc.frames, enc.frame_off, "rudp5", csum=enc.csum, utf8=True)}
-        ops = {
-            "encode": lambda: last.__setitem__("e", batch.pack_batch_varlen(
-                tab, flat, lens, "rudp5", want_csum=True, check=False, reuse=last["e"])),
-            "decode": lambda: last.__setitem__("d", batch.unpack_batch_varlen(
-                enc.frames, enc.frame_off, "rudp5", csum=enc.csum, check=False, reuse=last["d"])),
-            "decode_utf8": lambda: last.__setitem__("u", batch.unpack_batch_varlen(
-                enc.frames, enc.frame_off, "rudp5", csum=enc.csum, check=False, reuse=last["u"], utf8=True)),
-            "dedup_window500": lambda: batch.detect_retransmissions(enc.frames, frame_off=enc.frame_off,
-                                                                    window=500, check=False),
-        }
-        row = {}
-        for name, fn in ops.items():
+        lasts.append(last)
+
+        def mk(last=last, tab=tab, flat=flat, lens=lens, enc=enc):
+            return {
+                "encode": lambda: last.__setitem__("e", batch.pack_batch_varlen(
+                    tab, flat, lens, "rudp5", want_csum=True, check=False, reuse=last["e"])),
+                "decode": lambda: last.__setitem__("d", batch.unpack_batch_varlen(
+                    enc.frames, enc.frame_off, "rudp5", csum=enc.csum, check=False, reuse=last["d"])),
+                "decode_utf8": lambda: last.__setitem__("u", batch.unpack_batch_varlen(
+                    enc.frames, enc.frame_off, "rudp5", csum=enc.csum, check=False, reuse=last["u"], utf8=True)),
+                "dedup_window500": lambda: batch.detect_retransmissions(enc.frames, frame_off=enc.frame_off,
+                                                                        window=500, check=False),
+            }
+        ops[n] = mk()
+    one = torch.zeros(1, device=device)
+    floor = lambda: one.add_(1)  # noqa: E731
+    out = {f"n{n}": {} for n in sizes}
+    for n in sizes:
+        for name, fn in ops[n].items():
             per = sorted(time_loop(torch, lambda i: fn(), reps, 5) / reps * 1e3 for _ in range(5))
-            lat = []
-            for _ in range(reps):
-                t0 = time.perf_counter()
-                fn()
-                torch.cuda.synchronize()
-                lat.append((time.perf_counter() - t0) * 1e6)
-            lat.sort()
-            row[name] = {"us_per_call": per[2], "us_latency": lat[len(lat) // 2],
-                         "Mpkt_s_back_to_back": n / per[2]}
+            out[f"n{n}"][name] = {"us_per_call": per[2], "Mpkt_s_back_to_back": n / per[2]}
+    turns = [("floor", None, floor)] + [(name, n, fn) for n in sizes for name, fn in ops[n].items()]
+    lat = {(name, n): [] for name, n, _ in turns}
+    lat_ev = {(name, n): [] for name, n, _ in turns}
+    ev = torch.cuda.Event()
+    for _ in range(reps):
+        for name, n, fn in turns:
+            t0 = time.perf_counter()
+            fn()
+            torch.cuda.synchronize()
+            lat[(name, n)].append((time.perf_counter() - t0) * 1e6)
+            t0 = time.perf_counter()
+            fn()
+            ev.record()
+            ev.synchronize()
+            lat_ev[(name, n)].append((time.perf_counter() - t0) * 1e6)
+    med = lambda v: sorted(v)[len(v) // 2]  # noqa: E731
+    for name, n, _ in turns:
+        row = out.setdefault("floor", {}) if n is None else out[f"n{n}"].setdefault(name, {})
+        row.update({"us_latency": med(lat[(name, n)]), "us_latency_p10_p90": [sorted(lat[(name, n)])[reps // 10],
+                                                                             sorted(lat[(name, n)])[reps * 9 // 10]],
+                    "us_latency_event": med(lat_ev[(name, n)])})
+    for last in lasts:
         last["e"].check()
         last["d"].check()
-        out[f"n{n}"] = row
     out["note"] = ("1-char rudp5 datagrams; Python entries, sync-free, outputs reused; us_per_call: back-to-back "
-                   "calls on one stream (HIP events); us_latency: one call + torch.cuda.synchronize (wall)")
+                   "calls on one stream (HIP events); us_latency: one call + torch.cuda.synchronize (wall), "
+                   "every size and op (and the floor: a one-element torch add) taking turns each round; "
+                   "us_latency_event: the call + an event recorded behind it, waited for")
     return out
 
 

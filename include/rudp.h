@@ -297,7 +297,9 @@ RUDP_API int rudp_dedup_window_checked(const uint8_t* d_frames, uint64_t frames_
  * keeps the last `window` datagrams, all on the stream given at creation.
  * rudp_dedup_stream_counts synchronizes and returns the two counters.
  * window <= 4096; a batch holds at most max_batch datagrams of at most
- * max_frame bytes each.  One stream object per thread at a time.
+ * max_frame bytes each.  Thread-safe: push and counts may come from different
+ * threads (a relay thread pushing, another reading its counters); the object
+ * serializes them.  destroy must be the object's last call.
  */
 typedef struct rudp_dedup_stream rudp_dedup_stream;
 RUDP_API int rudp_dedup_stream_create(uint32_t window, uint32_t max_batch, uint32_t max_frame, int device,

@@ -1263,6 +1263,7 @@ int rudp_decode_varlen_host(const uint8_t* h_frames, uint64_t frames_bytes, cons
 // ---- the proxy's retransmission count over a stream of batches ----------------
 struct rudp_dedup_stream {
   static constexpr int kStages = 4;
+  std::mutex mu;  // push and counts from any threads, one at a time (the relay's thread and a stats reader)
   int device = 0;
   hipStream_t stream = nullptr;
   uint32_t window = 0, max_batch = 0, max_frame = 0;
@@ -1353,6 +1354,7 @@ int rudp_dedup_stream_push(rudp_dedup_stream* st, const uint8_t* h_frames, const
   if (n == 0) return 0;
   if (n > st->max_batch) return fail(RUDP_EINVAL, "batch of %llu exceeds max_batch %u", (unsigned long long)n,
                                      st->max_batch);
+  std::lock_guard<std::mutex> lk(st->mu);
   for (uint64_t i = 0; i < n; ++i)
     if (h_frame_off[i + 1] < h_frame_off[i] || h_frame_off[i + 1] - h_frame_off[i] > st->max_frame)
       return fail(RUDP_EINVAL, "rudp_dedup_stream_push: offsets decreasing or a frame over max_frame");
@@ -1430,6 +1432,7 @@ int rudp_dedup_stream_push(rudp_dedup_stream* st, const uint8_t* h_frames, const
 
 int rudp_dedup_stream_counts(rudp_dedup_stream* st, uint64_t* h_counts) {
   if (!st || !h_counts) return fail(RUDP_EINVAL, "rudp_dedup_stream_counts: NULL argument");
+  std::lock_guard<std::mutex> lk(st->mu);  // (its pinned read-back buffer is the object's, shared with push)
   DeviceScope dev_scope;
   int rc = dev_scope.set(st->device);
   if (rc) return rc;
@@ -1443,6 +1446,7 @@ int rudp_dedup_stream_counts(rudp_dedup_stream* st, uint64_t* h_counts) {
 
 int rudp_dedup_stream_destroy(rudp_dedup_stream* st) {
   if (!st) return 0;
+  { std::lock_guard<std::mutex> lk(st->mu); }  // a push or counts still running on another thread ends first
   DeviceScope dev_scope;
   (void)dev_scope.set(st->device);
   dedup_stream_free(st);

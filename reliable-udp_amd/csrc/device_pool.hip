@@ -8,6 +8,7 @@
 // 230 us per call that way (detect_retransmissions 462 -> 236 us with this
 // pool, round-2 probe tools/dedup_overhead.py, in git history).  This pool keeps what it has (threshold =
 // max) and leaves the process's default pool alone.
+#include <algorithm>
 #include <mutex>
 #include <vector>
 
@@ -64,10 +65,15 @@ hipError_t stream_free(void* ptr, hipStream_t stream) { return hipFreeAsync(ptr,
 // recycles its workers: proxy.py:127, :154) leave nothing behind.  (A
 // destroyed stream's handle is released only after its pending work, so a new
 // stream with the same handle finds the set idle.)  At most kMaxSets sets per
-// device: a call on a new stream past that takes the least recently used set
-// after a device synchronize (its buffers then idle), so a caller that makes
-// a stream per call keeps a bounded footprint.  A buffer grown past kKeepBytes
-// is given back when its call ends.  While the stream is being captured into
+// device.  Once a device has that many, every call records an event behind
+// its work as it ends, and a call on a new stream takes the least recently
+// used set whose last call's event has fired (hipEventQuery: nothing waits,
+// no device-wide synchronize that another thread's graph capture would
+// refuse, and no lock is held across a wait); when no set is provably idle
+// the call gets uncached temporaries (allocated and freed in stream order, as
+// under capture), so a caller that makes a stream per call keeps a bounded
+// footprint and never reuses a buffer still in use.  A buffer grown past
+// kKeepBytes is given back when its call ends.  While the stream is being captured into
 // a graph the call's temporaries are allocated and freed inside the capture
 // (stream_alloc / stream_free), never cached.  hipFreeAsync cost 3.9 us of
 // host time per call (rocprofv3 --hip-trace, 1M one-character datagrams), as
@@ -77,19 +83,24 @@ constexpr int kSlots = 4;
 constexpr size_t kMaxSets = 64;
 constexpr size_t kKeepBytes = size_t(64) << 20;
 
+struct DeviceSets;
+
 struct ScratchSet {
   std::mutex mu;  // held by the ScratchCall that enqueues work on these buffers
-  int device = 0;
+  DeviceSets* owner = nullptr;
   hipStream_t stream = nullptr;
   uint64_t last_use = 0;
   void* ptr[kSlots] = {};
   size_t cap[kSlots] = {};
+  hipEvent_t done = nullptr;  // recorded behind the last call's work (once the device is full)
+  bool done_valid = false;    // done marks the end of everything enqueued on these buffers
 };
 
 struct DeviceSets {
   std::mutex mu;
   std::vector<ScratchSet*> sets;  // never deleted: a set is re-keyed, not freed
   uint64_t clock = 0;
+  std::atomic<bool> full{false};  // kMaxSets reached: calls record their end events
 };
 
 std::mutex g_sets_mu;
@@ -106,7 +117,8 @@ thread_local ScratchCall* t_call = nullptr;  // the call this thread is making, 
 }  // namespace
 
 // The set of (device, stream), locked for the caller: found, made (up to
-// kMaxSets), or the least recently used one re-keyed once it is idle.
+// kMaxSets), or the least recently used set that is provably idle, re-keyed;
+// nullptr when there is none (the call then uses uncached temporaries).
 static ScratchSet* lock_set(int device, hipStream_t stream) {
   DeviceSets* ds = device_sets(device);
   for (;;) {
@@ -117,17 +129,28 @@ static ScratchSet* lock_set(int device, hipStream_t stream) {
         if (s->stream == stream) set = s;
       if (!set && ds->sets.size() < kMaxSets) {
         set = new ScratchSet();
-        set->device = device;
+        set->owner = ds;
         set->stream = stream;
         ds->sets.push_back(set);
+        if (ds->sets.size() == kMaxSets) ds->full.store(true);
       }
-      if (!set) {  // past kMaxSets streams: the least recently used set, once idle
-        set = ds->sets[0];
-        for (ScratchSet* s : ds->sets)
-          if (s->last_use < set->last_use) set = s;
-        std::lock_guard<std::mutex> sl(set->mu);  // no call is enqueueing on it
-        (void)hipDeviceSynchronize();             // and nothing it enqueued is still running
-        set->stream = stream;
+      if (!set) {
+        // past kMaxSets streams: sets in least recently used order, the first
+        // with no call enqueueing (try_lock) whose last call's work is done
+        std::vector<ScratchSet*> order(ds->sets);
+        std::sort(order.begin(), order.end(),
+                  [](const ScratchSet* a, const ScratchSet* b) { return a->last_use < b->last_use; });
+        for (ScratchSet* s : order) {
+          if (!s->done_valid || !s->mu.try_lock()) continue;
+          if (s->done_valid && hipEventQuery(s->done) == hipSuccess) {
+            s->stream = stream;
+            s->done_valid = false;
+            s->last_use = ++ds->clock;
+            return s;  // locked
+          }
+          s->mu.unlock();
+        }
+        return nullptr;  // none provably idle: uncached temporaries for this call
       }
       set->last_use = ++ds->clock;
     }
@@ -159,6 +182,12 @@ ScratchCall::~ScratchCall() {
       set->ptr[k] = nullptr;
       set->cap[k] = 0;
     }
+  }
+  // once sets may be taken by other streams, mark where this call's work ends
+  set->done_valid = false;
+  if (set->owner->full.load(std::memory_order_relaxed)) {
+    if (!set->done && hipEventCreateWithFlags(&set->done, hipEventDisableTiming) != hipSuccess) set->done = nullptr;
+    set->done_valid = set->done && hipEventRecord(set->done, stream_) == hipSuccess;
   }
   set->mu.unlock();
 }

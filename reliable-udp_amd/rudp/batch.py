@@ -447,10 +447,11 @@ class VarlenDecoded:
     it on first access.  Iterates as (seq, ack, flags, ok, csum, payload,
     status)."""
 
-    __slots__ = ("_buf", "_n", "payload", "_v", "_utf8")
+    __slots__ = ("_buf", "_n", "payload", "_v", "_utf8", "_stream")
 
-    def __init__(self, buf, n: int, payload, utf8: bool = False):
+    def __init__(self, buf, n: int, payload, utf8: bool = False, stream=None):
         self._buf, self._n, self.payload, self._v, self._utf8 = buf, n, payload, {}, utf8
+        self._stream = stream  # the stream the decode was enqueued on (None: the current one)
 
     # one allocation: seq | ack | csum (u16 [n] each) | flags | ok | valid (u8 [n] each)
     def _cut(self, name, at, nbytes, dtype):
@@ -495,11 +496,20 @@ class VarlenDecoded:
         offsets (ok == RUDP_OK_BAD_OFFSETS), else 0, as ``VarlenFrames.status``.
         The decode keeps no status word of its own (a call is its one kernel,
         rudp_decode_varlen_checked with d_status NULL), so this is built from
-        ``ok`` on first access: one device reduction, no synchronization."""
+        ``ok`` on first access: one device reduction, no synchronization, on
+        the stream the decode ran on (so it reads ``ok`` after the decode wrote
+        it), with the caller's current stream then made to wait for it."""
         v = self._v.get("status")
         if v is None:
             import torch
-            v = ((self.ok == _native.OK_BAD_OFFSETS).any().to(torch.int32) * _native.ST_OFFSETS).reshape(1)
+            if self._stream is None:
+                v = ((self.ok == _native.OK_BAD_OFFSETS).any().to(torch.int32) * _native.ST_OFFSETS).reshape(1)
+            else:
+                cur = torch.cuda.current_stream(self._buf.device)
+                with torch.cuda.stream(self._stream):
+                    v = ((self.ok == _native.OK_BAD_OFFSETS).any().to(torch.int32) * _native.ST_OFFSETS).reshape(1)
+                cur.wait_stream(self._stream)
+                v.record_stream(cur)
             self._v["status"] = v
         return v
 
@@ -801,7 +811,7 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
         frames.data_ptr() if frames.numel() else 16, frames.numel(), frame_off.data_ptr(), hint, n,
         csum.data_ptr() if csum is not None else None, base, base + 2 * n, base + 6 * n, base + 7 * n,
         base + 4 * n, base + 8 * n if utf8 else None, None, H, dev.index or 0, _stream_ptr(stream, dev)))
-    res = VarlenDecoded(buf, n, PayloadSpans(frame_off, H), utf8)
+    res = VarlenDecoded(buf, n, PayloadSpans(frame_off, H), utf8, stream)
     return res.check() if check else res
 
 

@@ -170,8 +170,13 @@ class BatchReceiver:
         self._free[slot].set()
 
     def recv(self, timeout_ms: int = -1) -> int:
+        """Receive the next batch into the next slot; returns its datagram count,
+        0 when nothing arrived within ``timeout_ms`` (-1: wait forever) -- also
+        when the next slot is still held (``hold()``) for longer than that, so a
+        caller polling with a timeout (the relay's loop) always gets control back."""
         k = (self._slot + 1) % len(self._frames_t)
-        self._free[k].wait()
+        if not self._free[k].wait(None if timeout_ms < 0 else timeout_ms / 1e3):
+            return 0
         if self._copied[k] is not None:
             self._copied[k].synchronize()  # that slot's H2D copy has left the pinned buffer
             self._copied[k] = None

@@ -74,6 +74,7 @@ class Relay(threading.Thread):
         self._history: deque = deque()
         self._seen: Counter = Counter()
         self.stop_event = threading.Event()
+        self.errors: List[BaseException] = []  # forwarding-thread failures (the relay keeps going)
         self.batched = batched
         self.batches = 0
         # Batched: sendmmsg threads (batches leave in the order the threads
@@ -189,7 +190,7 @@ class Relay(threading.Thread):
         # a server datagram before any client one has nowhere to go (dst 0: not sent)
         send = ~dropped & (dst != 0)
         if send.all():
-            out, out_off, out_dst = frames, off - off[0] if off[0] else off, dst
+            out, out_off, out_dst = frames, off, dst  # (offsets into frames, as sendmmsg reads them)
         elif send.any():
             lens = np.diff(off)
             body = frames[off[0]:off[k]]
@@ -216,8 +217,11 @@ class Relay(threading.Thread):
             out, out_off, out_dst, slot = item
             try:
                 netio.send_batch_to(self.sock, out, out_off, out_dst)
-            except OSError:
-                pass  # the socket closed under a stopping relay
+            except OSError as e:
+                if not self.stop_event.is_set():  # (a socket closed under a stopping relay is expected)
+                    self.errors.append(e)         # anything else: kept for the caller, the relay goes on
+            except BaseException as e:  # noqa: BLE001 -- recorded; the slot is still given back
+                self.errors.append(e)
             finally:
                 if slot is not None:
                     rx.release(slot)

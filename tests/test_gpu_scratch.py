@@ -137,3 +137,72 @@ def test_scratch_under_graph_capture(cuda):
     torch.cuda.synchronize()
     assert np.array_equal(again.frames.cpu().numpy(), want)
     assert np.array_equal(warm.frames.cpu().numpy(), want)
+
+
+def test_eviction_while_another_thread_captures(cuda):
+    """with every scratch set taken (64 streams), a call on a new
+    stream must not synchronize the device while another thread holds a graph
+    capture open (torch.cuda.graph's default global mode refuses or breaks on
+    that).  Sets are taken over only when their last call's end event has
+    fired, else the call gets uncached temporaries; the capture stays valid
+    and every result is exact."""
+    import torch
+    lib = _native.tools_lib()  # the batch API runs the diagnostics build: its sets are the ones counted
+    n = 3000
+    seq, ack, flags, _ = synth.synth(9, 0, n, 0)
+    lens = np.full(n, 24, np.int32)
+    pay = np.random.default_rng(9).integers(0, 256, int(lens.sum()), dtype=np.uint8)
+    want, _, _ = codec_np.encode_varlen(seq, ack, flags, [bytes(pay[24 * i:24 * i + 24]) for i in range(n)], 7)
+    tab = tuple(torch.from_numpy(a).to(cuda) for a in (seq, ack, flags))
+    d_pay, d_len = torch.from_numpy(pay).to(cuda), torch.from_numpy(lens).to(cuda)
+    # fill the device's sets (earlier tests may have made some) and warm outputs to reuse
+    streams = [torch.cuda.Stream(device=cuda) for _ in range(72)]
+    warm = []
+    for s in streams:
+        s.wait_stream(torch.cuda.current_stream(cuda))
+        with torch.cuda.stream(s):
+            warm.append(batch.pack_batch_varlen(tab, d_pay, d_len, "rudp7", check=False))
+    torch.cuda.synchronize()
+    assert _stats(lib)[1] == 64
+    cap_stream = torch.cuda.Stream(device=cuda)
+    cap_stream.wait_stream(torch.cuda.current_stream(cuda))
+    with torch.cuda.stream(cap_stream):
+        cap_warm = batch.pack_batch_varlen(tab, d_pay, d_len, "rudp7", check=False)
+    torch.cuda.synchronize()
+    g = torch.cuda.CUDAGraph()
+    inside, done, errors, cap = threading.Event(), threading.Event(), [], {}
+
+    def capture():
+        try:
+            with torch.cuda.graph(g, stream=cap_stream):
+                cap["r"] = batch.pack_batch_varlen(tab, d_pay, d_len, "rudp7", check=False, reuse=cap_warm)
+                inside.set()
+                done.wait(60)
+        except BaseException as e:  # noqa: BLE001
+            errors.append(e)
+            inside.set()
+
+    t = threading.Thread(target=capture)
+    t.start()
+    inside.wait(60)
+    # new streams while the capture is open: each needs a set (eviction path)
+    late = [torch.cuda.Stream(device=cuda) for _ in range(8)]
+    outs = []
+    try:
+        for k, s in enumerate(late):
+            with torch.cuda.stream(s):
+                outs.append(batch.pack_batch_varlen(tab, d_pay, d_len, "rudp7", check=False, reuse=warm[k]))
+    finally:
+        done.set()
+        t.join()
+    if errors:
+        raise errors[0]
+    torch.cuda.synchronize()
+    for r in outs:
+        r.check()
+        assert np.array_equal(r.frames.cpu().numpy(), want)
+    for _ in range(2):
+        g.replay()
+    torch.cuda.synchronize()
+    assert np.array_equal(cap["r"].frames.cpu().numpy(), want)
+    assert _stats(lib)[1] <= 64

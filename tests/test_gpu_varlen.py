@@ -978,3 +978,24 @@ def test_varlen_reuse_outputs_equal_fresh(cuda, L):
     with pytest.raises(ValueError, match="non-decreasing"):
         d3.check()
     assert torch.equal(d3.ok[:16], torch.ones(16, dtype=torch.uint8, device=cuda))
+
+
+def test_varlen_decode_status_on_side_stream(cuda):
+    """a decode enqueued on a side stream behind long work, checked from
+    the caller's current stream: the status is reduced on the decode's stream, so
+    check() sees the rejected frame (it read ok[] before the kernel wrote it when
+    the reduction ran on the current stream)."""
+    import torch
+    n = 4096
+    frames = torch.zeros(n * 8, dtype=torch.uint8, device=cuda)
+    off = torch.arange(0, n * 8 + 1, 8, dtype=torch.int64, device=cuda)
+    off[100] = 10 ** 9  # frames 99 and 100 reach past the buffer
+    side = torch.cuda.Stream(device=cuda)
+    side.wait_stream(torch.cuda.current_stream(cuda))
+    for _ in range(3):
+        with torch.cuda.stream(side):
+            torch.cuda._sleep(50_000_000)  # ~20 ms of GPU time before the decode on `side`
+        d = batch.unpack_batch_varlen(frames, off, "rudp7", stream=side, check=False)
+        with pytest.raises(ValueError, match="non-decreasing"):
+            d.check()
+    torch.cuda.synchronize()

@@ -125,9 +125,16 @@ def main():
     def apply(name):
         for k in keys:
             lib.rudpx_tune(k, variants[name].get(k, defaults[k]))
+
+    def restore():
+        for k, v in defaults.items():
+            lib.rudpx_tune(k, v)
     values = list(variants)
     out = {"variants": variants, "shapes": {}}
     for spec in args.shapes.split(","):
+        # every shape's inputs (frames, offsets a decode shape encodes first) are built
+        # under the default knobs, whatever variant timed the shape before
+        restore()
         run = make_shape(spec, dev)
         ref = None
         exact = {}
@@ -154,8 +161,7 @@ def main():
         print(spec, out["shapes"][spec], file=sys.stderr, flush=True)
         del run
         torch.cuda.empty_cache()
-    for k, v in defaults.items():
-        lib.rudpx_tune(k, v)
+    restore()
     print(json.dumps(out, indent=1))
 
 
