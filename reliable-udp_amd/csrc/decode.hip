@@ -284,11 +284,24 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
   sum = group_sum(sum, G);
   if (U8) hib = group_or_rows(hib, G);
   uint32_t u8bad = 0;
-  if (U8 && __any((hib & 0x80808080u) != 0)) {  // the byte checks, for frames with a high bit
-    if ((hib & 0x80808080u) && q < Tv)
-      u8bad = utf8_check_frame(q * F + H, q * F + F, g, G, [&](uint64_t c) { return tile[c]; },
-                               [&](uint64_t x) { return x ? dw[(x >> 2) - 1u] : 0u; });
-    u8bad = group_or(u8bad, G);
+  if (U8 && __any((hib & 0x80808080u) != 0)) {  // the byte checks, for waves whose frames hold a high bit
+    if (G >= 2u) {
+      // the wave's 64 / G frames are contiguous in the tile: one stream over them, every
+      // lane a contiguous run of chunks (utf8_stream_frames), frames ORed over the wave
+      const uint32_t fpw = 64u >> glog, wq0 = (tid >> 6) * fpw;
+      const uint32_t nf = Tv > wq0 ? (Tv - wq0 < fpw ? Tv - wq0 : fpw) : 0u;
+      uint64_t bits = nf ? utf8_stream_frames(wq0 * F, nf, F, H, tid & 63u, [&](uint32_t c) { return tile[c]; },
+                                              [&](uint32_t i) { return dw[i]; })
+                         : 0ull;
+      const uint32_t lo = group_or_rows((uint32_t)bits, 64u), hi = group_or_rows((uint32_t)(bits >> 32), 64u);
+      const uint32_t b = q - wq0 + 1u;  // this frame's bit
+      u8bad = ((b < 32u ? lo >> b : hi >> (b - 32u)) & 1u);
+    } else {
+      if ((hib & 0x80808080u) && q < Tv)
+        u8bad = utf8_check_frame(q * F + H, q * F + F, g, G, [&](uint64_t c) { return tile[c]; },
+                                 [&](uint64_t x) { return x ? dw[(x >> 2) - 1u] : 0u; });
+      u8bad = group_or(u8bad, G);
+    }
   }
   if (!a.stage_out) {
     if (g == 0 && q < Tv) {

@@ -443,3 +443,36 @@ def test_small_encode_one_tile_batches(cuda, single):
                                     out=torch.empty(n * 6 - 1, dtype=torch.uint8, device=cuda))
     finally:
         lib.rudpx_tune(64, old)
+
+
+@pytest.mark.parametrize("L", [32, 48, 64, 96, 160, 1472])
+@pytest.mark.parametrize("H", [5, 7])
+def test_fixed_fused_sequences_across_frame_edges(cuda, L, H):
+    """The fixed-length tile judges a wave's frames as one stream: payloads of
+    valid multi-byte text cut at random points (a sequence left open at the
+    payload's end, continuations at its start), lone lead / continuation bytes
+    at the first and last payload bytes, and a ragged last tile (waves with
+    fewer or no frames), against Python's strict decoder."""
+    rng = np.random.default_rng(7000 + 10 * L + H)
+    n = 3 * 256 + 37
+    text = ("é中😀aßЖ€𝄞" * (L // 4 + 8)).encode()
+    bodies = []
+    for i in range(n):
+        s = int(rng.integers(0, 12))
+        b = bytearray(text[s:s + L])
+        kind = i % 5
+        if kind == 1:
+            b[-1] = int(rng.choice([0xC3, 0xE4, 0xF0, 0xF4]))   # a lead left open at the end
+        elif kind == 2:
+            b[0] = int(rng.choice([0x80, 0xA0, 0xBF]))          # a continuation first
+        elif kind == 3:
+            b[int(rng.integers(0, L))] = int(rng.integers(0x80, 0x100))
+        bodies.append(bytes(b))
+    hdr = b"\xe4\xb8\x00\xf0\x80" + (b"\xc3\xa9" if H == 7 else b"")  # header bytes that look like UTF-8
+    fr = np.frombuffer(b"".join(hdr + x for x in bodies), np.uint8).reshape(n, L + H)
+    off = np.arange(n + 1, dtype=np.int64) * (L + H)
+    want = codec_np.utf8_valid(fr.reshape(-1), off, H)
+    assert 0.1 < want.mean() < 0.9
+    for copy in (False, True):
+        got = batch.unpack_batch(dev(fr, cuda), H, copy_payload=copy, utf8=True)
+        assert np.array_equal(host(got.valid), want), copy

@@ -19,6 +19,29 @@ from rudp import _native, batch
 pytestmark = pytest.mark.gpu
 
 
+class _RawStreams:
+    """Distinct HIP streams (hipStreamCreate), as torch ExternalStreams: torch.cuda.Stream()
+    hands out its pool's 32 streams round robin, so it cannot make 65+ distinct ones."""
+
+    def __init__(self, k, cuda):
+        import torch
+        self.hip = ctypes.CDLL("libamdhip64.so")
+        self.hip.hipStreamCreate.argtypes = [ctypes.POINTER(ctypes.c_void_p)]
+        self.hip.hipStreamDestroy.argtypes = [ctypes.c_void_p]
+        self.raw = []
+        for _ in range(k):
+            h = ctypes.c_void_p()
+            assert self.hip.hipStreamCreate(ctypes.byref(h)) == 0
+            self.raw.append(h)
+        self.streams = [torch.cuda.ExternalStream(h.value, device=cuda) for h in self.raw]
+
+    def close(self):
+        import torch
+        torch.cuda.synchronize()
+        for h in self.raw:
+            self.hip.hipStreamDestroy(h)
+
+
 def _stats(lib):
     out = (ctypes.c_uint64 * 2)()
     _native.check(lib.rudpx_scratch_stats(0, out))
@@ -92,17 +115,20 @@ def test_stream_per_call_is_capped(cuda):
     want, off, _ = codec_np.encode_varlen(seq, ack, flags, [bytes(pay[40 * i:40 * i + 40]) for i in range(n)], 7)
     tab = tuple(torch.from_numpy(a).to(cuda) for a in (seq, ack, flags))
     d_pay, d_len = torch.from_numpy(pay).to(cuda), torch.from_numpy(lens).to(cuda)
-    streams = [torch.cuda.Stream(device=cuda) for _ in range(80)]
+    raw = _RawStreams(80, cuda)
     outs = []
-    for s in streams:
-        s.wait_stream(torch.cuda.current_stream(cuda))
-        with torch.cuda.stream(s):
-            outs.append(batch.pack_batch_varlen(tab, d_pay, d_len, "rudp7", check=False))
-    torch.cuda.synchronize()
-    for r in outs:
-        r.check()
-        assert np.array_equal(r.frames.cpu().numpy(), want)
-    assert _stats(lib)[1] <= 64
+    try:
+        for s in raw.streams:
+            s.wait_stream(torch.cuda.current_stream(cuda))
+            with torch.cuda.stream(s):
+                outs.append(batch.pack_batch_varlen(tab, d_pay, d_len, "rudp7", check=False))
+        torch.cuda.synchronize()
+        for r in outs:
+            r.check()
+            assert np.array_equal(r.frames.cpu().numpy(), want)
+        assert _stats(lib)[1] <= 64
+    finally:
+        raw.close()
 
 
 def test_scratch_under_graph_capture(cuda):
@@ -156,7 +182,8 @@ def test_eviction_while_another_thread_captures(cuda):
     tab = tuple(torch.from_numpy(a).to(cuda) for a in (seq, ack, flags))
     d_pay, d_len = torch.from_numpy(pay).to(cuda), torch.from_numpy(lens).to(cuda)
     # fill the device's sets (earlier tests may have made some) and warm outputs to reuse
-    streams = [torch.cuda.Stream(device=cuda) for _ in range(72)]
+    raw = _RawStreams(80, cuda)
+    streams, late = raw.streams[:72], raw.streams[72:]
     warm = []
     for s in streams:
         s.wait_stream(torch.cuda.current_stream(cuda))
@@ -186,7 +213,6 @@ def test_eviction_while_another_thread_captures(cuda):
     t.start()
     inside.wait(60)
     # new streams while the capture is open: each needs a set (eviction path)
-    late = [torch.cuda.Stream(device=cuda) for _ in range(8)]
     outs = []
     try:
         for k, s in enumerate(late):
@@ -206,3 +232,4 @@ def test_eviction_while_another_thread_captures(cuda):
     torch.cuda.synchronize()
     assert np.array_equal(cap["r"].frames.cpu().numpy(), want)
     assert _stats(lib)[1] <= 64
+    raw.close()

@@ -30,13 +30,14 @@ def main():
     ap.add_argument("--libs", required=True)
     ap.add_argument("--L", default="1472,1024,64")
     ap.add_argument("--reps", type=int, default=11)
-    ap.add_argument("--op", default="encode", choices=["encode", "decode", "varlen", "vdecode", "u8text"],
+    ap.add_argument("--op", default="encode", choices=["encode", "decode", "varlen", "vdecode", "u8text", "u8ascii"],
                     help="decode: verify-only fixed-length rudp_decode of the encoded frames; varlen: "
                          "rudp_encode_varlen_checked of packed payloads, --L lengths or 'ragged' "
                          "(uniform in [0, 2944]); a 'u' suffix (1472u) times the unchecked rudp_encode_varlen; "
                          "vdecode: rudp_decode_varlen_checked (no status word) of such frames, rudp5 with the "
                          "sideband checksums below 16-B payloads, else rudp7; u8text: rudp_decode_utf8 of "
-                         "frames whose payload is valid multi-byte UTF-8 text (1-4 byte characters)")
+                         "frames whose payload is valid multi-byte UTF-8 text (1-4 byte characters); u8ascii: "
+                         "rudp_decode_utf8 of the ASCII synthetic frames")
     args = ap.parse_args()
     _native.lib()  # torch's HIP runtime first
     libs = {}
@@ -103,7 +104,7 @@ def main():
         def call(h, fr, b):
             if args.op == "encode":
                 return h.rudp_encode(ctypes.byref(b), fr.data_ptr(), None, 7, 0, stream)
-            if args.op == "u8text":
+            if args.op in ("u8text", "u8ascii"):
                 return h.rudp_decode_utf8(fr.data_ptr(), None, L + 7, n, None, *[t.data_ptr() for t in outs], None,
                                           valid.data_ptr(), 7, 0, stream)
             return h.rudp_decode(fr.data_ptr(), None, L + 7, n, None, *[t.data_ptr() for t in outs], None, 7, 0,
