@@ -455,11 +455,19 @@ def test_fixed_fused_sequences_across_frame_edges(cuda, L, H):
     fewer or no frames), against Python's strict decoder."""
     rng = np.random.default_rng(7000 + 10 * L + H)
     n = 3 * 256 + 37
-    text = ("é中😀aßЖ€𝄞" * (L // 4 + 8)).encode()
+    chars = "é中😀aßЖ€𝄞"
     bodies = []
     for i in range(n):
-        s = int(rng.integers(0, 12))
-        b = bytearray(text[s:s + L])
+        s = int(rng.integers(0, len(chars)))
+        t = (chars[s:] + chars * (L // 4 + 2)).encode()
+        cut = L
+        while True:  # the longest prefix of at most L bytes that ends on a character boundary
+            try:
+                t[:cut].decode()
+                break
+            except UnicodeDecodeError:
+                cut -= 1
+        b = bytearray(t[:cut] + b"x" * (L - cut))
         kind = i % 5
         if kind == 1:
             b[-1] = int(rng.choice([0xC3, 0xE4, 0xF0, 0xF4]))   # a lead left open at the end
