@@ -414,7 +414,10 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
   a.early_fo = tuning().varlen_early_fo ? 1u : 0u;
   a.xcd = tuning().tile_xcd ? 1u : 0u;
   // decode tile sums from 128-B block sums (the encode tile's scheme)
-  a.tile_sums = tuning().varlen_decode_blocks ? 2u : 0u;
+  {
+    const int vb = tuning().varlen_decode_blocks;
+    a.tile_sums = vb == 2 ? 2u : vb == 1 ? 1u : 0u;
+  }
   // Small frames (payload hint under varlen_small bytes): tiles of 256 * fpt
   // frames with the per-frame outputs lane-strided (decode_varlen_small_kernel).
   {

@@ -68,6 +68,17 @@ __device__ __forceinline__ uint32_t group_or_rows(uint32_t x, uint32_t G) {
   return x;
 }
 
+// Maximum of a u32 over the whole wave (DPP row steps, then two shuffles).
+__device__ __forceinline__ uint32_t wave_max(uint32_t x) {
+  x = max(x, dpp_row<0xB1>(x));
+  x = max(x, dpp_row<0x4E>(x));
+  x = max(x, dpp_row<0x141>(x));
+  x = max(x, dpp_row<0x140>(x));
+  x = max(x, (uint32_t)__shfl_xor((int)x, 16, 64));
+  x = max(x, (uint32_t)__shfl_xor((int)x, 32, 64));
+  return x;
+}
+
 // Sum of a u64 over the whole wave: the 16-lane steps by DPP on the two
 // halves (carry added by hand), the 32- and 64-lane steps as shuffles.
 template <int CTRL>

@@ -157,7 +157,7 @@ struct VarlenArgs {
   uint64_t span_count;
   uint32_t bt_slots;
   uint32_t tile_Tl;
-  uint32_t tile_sums;             // tile sum pass: 2 from 128-B block sums, 0 chunk by chunk
+  uint32_t tile_sums;             // tile sum pass: 2 from 128-B block sums, 0 chunk by chunk (decode: 1 per tile)
   // Decode by byte spans (checked calls): span_rec[k] = the first frame that
   // starts at or past k * span_S (decode_span_index_kernel); *span_flag ==
   // span_epoch when the offsets are not in order inside the buffer, and the
@@ -303,8 +303,10 @@ struct Tuning {
   // Varlen decode tile frame sums from 128-B block sums taken in phase 1 (the
   // encode tile's scheme): lengths uniform in [0, 2944] 0.288 -> 0.278 ms, but
   // equal 1472-B lengths 0.246 -> 0.268 (the block sums' DPP work sits in the
-  // streaming phase), so off (profiles/r04/sweeps/varlen_decode_blocks.json).
-  RUDP_KNOB(varlen_decode_blocks, 0)
+  // streaming phase; profiles/r04/sweeps/varlen_decode_blocks.json).  1: per
+  // tile, for tiles whose longest frame is over 1.25x their mean (every wave
+  // reads the tile's offsets: uniform without a barrier); 2: every tile; 0: none.
+  RUDP_KNOB(varlen_decode_blocks, 1)
   RUDP_KNOB(utf8_tile, 1)
   // Packed-frame UTF-8 validation through LDS tiles (hints >= 128 B) and its
   // LDS budget in % of the hinted run: 1M x 1479 B ASCII frames 0.287 ->

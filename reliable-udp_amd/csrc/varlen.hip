@@ -946,12 +946,26 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   const uint32_t q = tid >> glog, g = tid & (G - 1u);
   uint32_t* lds_fo = reinterpret_cast<uint32_t*>(lds);                       // [T + 1]
   unsigned char* img = lds + ((((T + 1u) * 4u) + 15u) & ~15u) + kVTGuard;   // the run
-  const bool blk = RUDP_TOOLS && a.tile_sums == 2u;  // (measured slower: diagnostics build only)
   uint32_t* lds_blk = reinterpret_cast<uint32_t*>(lds + dvt_blk_off(T, a.tile_cap));  // [cap / 128 + 4]
   const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
   const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
+  // Block sums for every tile (tile_sums 2), or (1) for a tile of uneven frames:
+  // every wave reads the tile's T + 1 <= 64 offsets itself (the same lines as
+  // wave 0's early ones), so the choice is the same in all four without a
+  // barrier; a longest frame over 1.25x the tile's mean takes block sums (the
+  // lane groups of a ragged tile then have about equal work), an even tile
+  // keeps the chunk sums (no DPP work in its streaming phase).
+  bool blk = a.tile_sums == 2u;
+  if (a.tile_sums == 1u && T < 64u) {
+    const uint32_t l = tid & 63u;
+    const uint64_t o = l <= Tv ? a.frame_off[p0 + l] : 0ull;
+    const uint64_t on = (uint64_t)__shfl_down((long long)o, 1, 64);
+    uint32_t len = l < Tv ? (on - o < 0xFFFFFFFFull ? (uint32_t)(on - o) : 0xFFFFFFFFu) : 0u;
+    len = wave_max(len);
+    blk = (uint64_t)len * Tv * 4u > (fo_end - fo0) * 5u;
+  }
   const uint64_t total = frames_limit(a);
   const uint64_t A = fo0 & ~15ull;
   const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
@@ -2228,7 +2242,7 @@ static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
     return launch_decode_small<H, U8>(args, stream);
   if (args.glog != kNoVec && args.tile_cap && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0) {
     const uint32_t T = kBlock >> args.glog;
-    const size_t lds = dvt_lds_bytes(T, args.tile_cap, args.tile_sums == 2u);
+    const size_t lds = dvt_lds_bytes(T, args.tile_cap, args.tile_sums != 0u);
     if (lds <= 65536) {
       const uint64_t blocks = (args.n + T - 1) / T;
       // 76 VGPRs (6 waves per SIMD).  Asking the allocator for 7 or 8 waves
