@@ -167,11 +167,15 @@ def test_scratch_under_graph_capture(cuda):
 
 def test_eviction_while_another_thread_captures(cuda):
     """with every scratch set taken (64 streams), a call on a new
-    stream must not synchronize the device while another thread holds a graph
-    capture open (torch.cuda.graph's default global mode refuses or breaks on
-    that).  Sets are taken over only when their last call's end event has
-    fired, else the call gets uncached temporaries; the capture stays valid
-    and every result is exact."""
+    stream must neither synchronize the device while another thread holds a
+    graph capture open (torch.cuda.graph's default global mode refuses that,
+    or breaks the capture) nor reuse a set whose work may still run.  Sets are
+    taken over only when their last call's end event has fired, else the call
+    allocates its temporaries in stream order.  Under another thread's
+    global-mode capture the HIP runtime refuses those queries and allocations
+    (hipErrorStreamCaptureUnsupported): such a call fails cleanly with that
+    error, the capture stays valid and replays exactly, and once the capture
+    has ended every call succeeds with exact results."""
     import torch
     lib = _native.tools_lib()  # the batch API runs the diagnostics build: its sets are the ones counted
     n = 3000
@@ -181,16 +185,24 @@ def test_eviction_while_another_thread_captures(cuda):
     want, _, _ = codec_np.encode_varlen(seq, ack, flags, [bytes(pay[24 * i:24 * i + 24]) for i in range(n)], 7)
     tab = tuple(torch.from_numpy(a).to(cuda) for a in (seq, ack, flags))
     d_pay, d_len = torch.from_numpy(pay).to(cuda), torch.from_numpy(lens).to(cuda)
-    # fill the device's sets (earlier tests may have made some) and warm outputs to reuse
+    # fill the device's sets (earlier tests may have made some); a second round on
+    # them after the device is full records their end events
     raw = _RawStreams(80, cuda)
     streams, late = raw.streams[:72], raw.streams[72:]
     warm = []
-    for s in streams:
-        s.wait_stream(torch.cuda.current_stream(cuda))
-        with torch.cuda.stream(s):
-            warm.append(batch.pack_batch_varlen(tab, d_pay, d_len, "rudp7", check=False))
+    for rnd in range(2):
+        for k, s in enumerate(streams):
+            s.wait_stream(torch.cuda.current_stream(cuda))
+            with torch.cuda.stream(s):
+                r = batch.pack_batch_varlen(tab, d_pay, d_len, "rudp7", check=False,
+                                            reuse=warm[k] if rnd else None)
+                if not rnd:
+                    warm.append(r)
     torch.cuda.synchronize()
     assert _stats(lib)[1] == 64
+    for r in warm:
+        r.check()
+        assert np.array_equal(r.frames.cpu().numpy(), want)
     cap_stream = torch.cuda.Stream(device=cuda)
     cap_stream.wait_stream(torch.cuda.current_stream(cuda))
     with torch.cuda.stream(cap_stream):
@@ -212,12 +224,16 @@ def test_eviction_while_another_thread_captures(cuda):
     t = threading.Thread(target=capture)
     t.start()
     inside.wait(60)
-    # new streams while the capture is open: each needs a set (eviction path)
-    outs = []
+    # new streams while the capture is open: each needs a set (the eviction path)
+    outs, refused = [], 0
     try:
         for k, s in enumerate(late):
             with torch.cuda.stream(s):
-                outs.append(batch.pack_batch_varlen(tab, d_pay, d_len, "rudp7", check=False, reuse=warm[k]))
+                try:
+                    outs.append(batch.pack_batch_varlen(tab, d_pay, d_len, "rudp7", check=False, reuse=warm[k]))
+                except _native.RudpError as e:
+                    assert "capturing" in str(e) or "capture" in str(e), e
+                    refused += 1
     finally:
         done.set()
         t.join()
@@ -231,5 +247,12 @@ def test_eviction_while_another_thread_captures(cuda):
         g.replay()
     torch.cuda.synchronize()
     assert np.array_equal(cap["r"].frames.cpu().numpy(), want)
+    # after the capture: every new stream's call goes through
+    for k, s in enumerate(late):
+        with torch.cuda.stream(s):
+            r = batch.pack_batch_varlen(tab, d_pay, d_len, "rudp7", check=False, reuse=warm[k])
+        torch.cuda.synchronize()
+        r.check()
+        assert np.array_equal(r.frames.cpu().numpy(), want)
     assert _stats(lib)[1] <= 64
     raw.close()
