@@ -67,10 +67,12 @@ hipError_t stream_free(void* ptr, hipStream_t stream) { return hipFreeAsync(ptr,
 // stream with the same handle finds the set idle.)  At most kMaxSets sets per
 // device.  Once a device has that many, every call records an event behind
 // its work as it ends, and a call on a new stream takes the least recently
-// used set whose last call's event has fired (hipEventQuery: nothing waits,
-// no device-wide synchronize that another thread's graph capture would
-// refuse, and no lock is held across a wait); when no set is provably idle
-// the call gets uncached temporaries (allocated and freed in stream order, as
+// used set that has such an event, making its own stream wait for that event
+// (hipStreamWaitEvent: stream order, no host wait, no query and no
+// device-wide synchronize -- none of which the runtime allows while another
+// thread holds a global-mode graph capture -- and no lock held across a
+// wait); when no set has one (a set idle since before the device filled) the
+// call gets uncached temporaries (allocated and freed in stream order, as
 // under capture), so a caller that makes a stream per call keeps a bounded
 // footprint and never reuses a buffer still in use.  A buffer grown past
 // kKeepBytes is given back when its call ends.  While the stream is being captured into
@@ -142,7 +144,10 @@ static ScratchSet* lock_set(int device, hipStream_t stream) {
                   [](const ScratchSet* a, const ScratchSet* b) { return a->last_use < b->last_use; });
         for (ScratchSet* s : order) {
           if (!s->done_valid || !s->mu.try_lock()) continue;
-          if (s->done_valid && hipEventQuery(s->done) == hipSuccess) {
+          // the new stream waits, in stream order, for everything enqueued on
+          // these buffers (no host wait, no query: neither is allowed while
+          // another thread holds a global-mode graph capture)
+          if (s->done_valid && hipStreamWaitEvent(stream, s->done, 0) == hipSuccess) {
             s->stream = stream;
             s->done_valid = false;
             s->last_use = ++ds->clock;
@@ -150,7 +155,7 @@ static ScratchSet* lock_set(int device, hipStream_t stream) {
           }
           s->mu.unlock();
         }
-        return nullptr;  // none provably idle: uncached temporaries for this call
+        return nullptr;  // none with a known end: uncached temporaries for this call
       }
       set->last_use = ++ds->clock;
     }
