@@ -290,6 +290,15 @@ __global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
       // lane a contiguous run of chunks (utf8_stream_frames), frames ORed over the wave
       const uint32_t fpw = 64u >> glog, wq0 = (tid >> 6) * fpw;
       const uint32_t nf = Tv > wq0 ? (Tv - wq0 < fpw ? Tv - wq0 : fpw) : 0u;
+      // this wave's frames' header bytes read as 0 in the stream: zeroed in LDS
+      // (its leaders read their headers above; LDS keeps one wave's accesses
+      // in order, and no other wave reads these bytes but as discarded window
+      // edges)
+      if (q < Tv)
+        for (uint32_t b = g; b < (uint32_t)H; b += G) lds[q * F + b] = 0;
+      __builtin_amdgcn_wave_barrier();
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
       uint64_t bits = nf ? utf8_stream_frames(wq0 * F, nf, F, H, tid & 63u, [&](uint32_t c) { return tile[c]; },
                                               [&](uint32_t i) { return dw[i]; })
                          : 0ull;

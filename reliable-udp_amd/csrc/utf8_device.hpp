@@ -170,86 +170,53 @@ __device__ __forceinline__ uint32_t utf8_check_frame(uint64_t s, uint64_t fe, ui
 // one wave as ONE stream (the fixed-length decode tile: a wave's frames are
 // contiguous): lane l takes a contiguous run of the aligned 16-B chunks that
 // cover [R0, R1 = R0 + nf F] plus the chunk holding byte R1, so no lane walks
-// a frame's edges or pairs its chunks.  Header bytes, and bytes outside the
-// frames, count as 0 (ASCII): a payload can then neither borrow a lead byte
-// from the header before it nor leave a sequence open into the next header
-// (the 0 there fails as "too short", as the byte after a payload does in
-// utf8_check_frame).  An error at a header byte is that pending sequence of
-// the frame before; any other belongs to its own frame.  Returns this lane's
-// frames found invalid as bit (frame + 1) of a u64 (frame -1, bit 0: the
-// bytes before R0, never an error); the caller ORs it over the wave.
-// `chunk(c)` returns aligned chunk c, `dw(i)` the LDS dword i.  F >= H + 16.
+// a frame's edges or pairs its chunks.  The caller has zeroed the frames'
+// header bytes in LDS (the wave's own frames; its leaders read their headers
+// before): a payload can then neither borrow a lead byte from the header
+// before it nor leave a sequence open into the next frame (the 0 there fails
+// as "too short", as the byte after a payload does in utf8_check_frame).
+// Bytes at and past R1 (the next wave's frames) read as 0; bytes before R0
+// (the frame before, another wave's) are judged but their errors, like those
+// at a header byte, belong to the frame before -- here frame -1, ignored --
+// and the H zeros of frame 0's header cut any sequence from them.  Errors are
+// looked up only in a chunk that has some (valid text: never): a chunk spans
+// at most two frames' bytes (F >= H + 16), so its first and last error bytes
+// name every frame it finds invalid.  Returns them as bit (frame + 1) of a
+// u64 (bit 0: frame -1); the caller ORs it over the wave.  `chunk(c)`
+// returns aligned chunk c, `dw(i)` the LDS dword i.
 template <class Chunk, class Dword>
 __device__ __forceinline__ uint64_t utf8_stream_frames(uint32_t R0, uint32_t nf, uint32_t F, uint32_t H,
                                                        uint32_t lane, Chunk chunk, Dword dw) {
   const uint32_t R1 = R0 + nf * F;
-  const uint32_t cA = R0 >> 4, N = (R1 >> 4) - cA + 1u;
+  const uint32_t cA = R0 >> 4, cEnd = R1 >> 4, N = cEnd - cA + 1u;
   const uint32_t k0 = lane * N / 64u, k1 = (lane + 1u) * N / 64u;
   if (k0 >= k1) return 0ull;
-  const int iF = (int)F, iH = (int)H, inf = (int)nf;
-  // frame j and position pos of the first byte of chunk cA + k0 (j = -1 before R0)
-  const int d = (int)((cA + k0) << 4) - (int)R0;
-  int j = d >= 0 ? d / iF : -1;
-  int pos = d - j * iF;
-  // keep mask of a chunk at (pos, j): the payload bytes of frames 0..nf-1
-  auto keep = [&](int p, int jj, uint64_t& mlo, uint64_t& mhi) {
-    const int a1 = iH - p > 0 ? iH - p : 0, b1 = iF - p < 16 ? iF - p : 16;  // frame jj's payload part
-    const int a2 = iF - p + iH;                                               // frame jj + 1's payload from here
-    const bool in1 = jj >= 0 && jj < inf, in2 = jj + 1 >= 0 && jj + 1 < inf && iF - p < 16;
-    mlo = (in1 ? byte_mask(a1, b1) : 0ull) | (in2 ? byte_mask(a2, 16) : 0ull);
-    mhi = (in1 ? byte_mask(a1 - 8, b1 - 8) : 0ull) | (in2 ? byte_mask(a2 - 8, 8) : 0ull);
-  };
-  // the dword before this lane's first chunk, masked as its chunk is
-  uint32_t prev = 0;
-  if (cA + k0 > 0) {
-    int pp = pos - 16, jp = j;
-    if (pp < 0) {
-      pp += iF;
-      --jp;
-    }
-    uint64_t mlo, mhi;
-    keep(pp, jp, mlo, mhi);
-    prev = dw(((cA + k0) << 2) - 1u) & (uint32_t)(mhi >> 32);
-  }
+  uint32_t prev = cA + k0 > 0 ? dw(((cA + k0) << 2) - 1u) : 0u;
   Utf8Pre q_last = utf8_pre(prev);
   uint64_t bits = 0;
   for (uint32_t k = k0; k < k1; ++k) {
-    u32x4 v = chunk(cA + k);
-    int sp = 16, fa = j;  // errors at bytes < sp belong to frame fa, the rest to fa + 1
-    if (!(pos >= iH && pos + 16 <= iF && j >= 0 && j < inf)) {  // a header, a frame edge or outside
-      uint64_t mlo, mhi;
-      keep(pos, j, mlo, mhi);
-      v = make_u32x4(lo64(v) & mlo, hi64(v) & mhi);
-      if (pos < iH) {
-        sp = iH - pos;
-        fa = j - 1;
-      } else {
-        sp = iF - pos + iH < 16 ? iF - pos + iH : 16;
-      }
-    }
+    const uint32_t c = cA + k;
+    u32x4 v = chunk(c);
+    if (c == cEnd) v = keep_bytes(v, 0, (int)(R1 & 15u));  // the next wave's bytes read as 0
     // ASCII with no lead byte just before: nothing to check
     if (high_bits(v) || (prev & (prev << 1) & 0x80808000u)) {
       const Utf8Pre q1 = utf8_pre(v.x), q2 = utf8_pre(v.y), q3 = utf8_pre(v.z), q4 = utf8_pre(v.w);
       const uint32_t e0 = utf8_dword_errors(q1, q_last), e1 = utf8_dword_errors(q2, q1),
                      e2 = utf8_dword_errors(q3, q2), e3 = utf8_dword_errors(q4, q3);
       q_last = q4;
-      if (sp >= 16) {
-        if (e0 | e1 | e2 | e3) bits |= 1ull << (fa + 1);
-      } else {
-        const uint64_t elo = (uint64_t)e0 | ((uint64_t)e1 << 32), ehi = (uint64_t)e2 | ((uint64_t)e3 << 32);
-        const uint64_t alo = byte_mask(0, sp), ahi = byte_mask(-8, sp - 8);
-        if ((elo & alo) | (ehi & ahi)) bits |= 1ull << (fa + 1);
-        if ((elo & ~alo) | (ehi & ~ahi)) bits |= 1ull << (fa + 2);
+      if (e0 | e1 | e2 | e3) {  // which frames: the first and the last error byte's
+        const uint64_t lo = (uint64_t)e0 | ((uint64_t)e1 << 32), hi = (uint64_t)e2 | ((uint64_t)e3 << 32);
+        const int bf = lo ? (int)(__builtin_ctzll(lo) >> 3) : 8 + (int)(__builtin_ctzll(hi) >> 3);
+        const int bl = hi ? 15 - (int)(__builtin_clzll(hi) >> 3) : 7 - (int)(__builtin_clzll(lo) >> 3);
+        // byte x of the stream (relative to R0) belongs to frame floor((x - H) / F)
+        const int x0 = (int)(c << 4) - (int)R0 - (int)H;
+        const int f0 = x0 + bf >= 0 ? (x0 + bf) / (int)F : -1, f1 = x0 + bl >= 0 ? (x0 + bl) / (int)F : -1;
+        bits |= (1ull << (f0 + 1)) | (1ull << (f1 + 1));
       }
     } else {
       q_last = utf8_pre(v.w);
     }
     prev = v.w;
-    pos += 16;
-    if (pos >= iF) {
-      pos -= iF;
-      ++j;
-    }
   }
   return bits;
 }

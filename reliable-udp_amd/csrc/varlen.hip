@@ -527,10 +527,32 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
       }
     }
   } else if (q < Tv) {
+    // (the class test hoisted out of the loop, as round 3 had it: through
+    // map_entry, ragged lengths ran 0.607 -> 0.632 ms, profiles/r05/sweeps/
+    // varlen_encode_bisect.json)
     const uint32_t fs = lds_fo[q], fe = lds_fo[q + 1];
     const uint32_t klo = fs > lead ? (fs - lead + 15u) >> 4 : 0u;
     const uint32_t khi = fe > lead ? (fe - lead + 15u) >> 4 : 0u;
-    for (uint32_t k = klo + g; k < khi; k += G) map_entry(k, q, fs, fe);
+    if (wide) {
+      for (uint32_t k = klo + g; k < khi; k += G) {
+        const uint32_t x = lead + 16u * k;
+        const int k0 = (int)x - (int)fs;
+        uint32_t e = q;
+        if (k0 >= H && x + 16u <= fe) {
+          e |= 0x8000u;
+        } else {
+          const uint32_t nxt = k0 >= H ? 1u : 0u;
+          const uint32_t fsp = nxt ? fe : fs;
+          const int i0 = fsp >= lead ? (int)((fsp - lead) >> 4) : -1;
+          e |= (nxt << 8) | ((uint32_t)((int)k - i0) & 1u) << 9;
+          const uint32_t hlen = nxt ? (q + 1u < Tv ? lds_fo[q + 2u] - fe : 0u) : fe - fs;
+          if (hlen < kVHCMinFrame) e |= 0x4000u;
+        }
+        lds_map16[k] = (uint16_t)e;
+      }
+    } else {
+      for (uint32_t k = klo + g; k < khi; k += G) lds_map[k] = (uint8_t)q;
+    }
   }
 #if RUDP_TOOLS
   if (a.trace && (tid & 63u) == 0) atomicMax(&s_last[1], (unsigned long long)wall_clock64());
@@ -957,15 +979,12 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   // barrier; a longest frame over 1.25x the tile's mean takes block sums (the
   // lane groups of a ragged tile then have about equal work), an even tile
   // keeps the chunk sums (no DPP work in its streaming phase).
+  // (the offsets load with the tile's first ones; the choice is made once the
+  // run's first loads are in flight, so it costs the staging no round trip)
   bool blk = a.tile_sums == 2u;
-  if (a.tile_sums == 1u && T < 64u) {
-    const uint32_t l = tid & 63u;
-    const uint64_t o = l <= Tv ? a.frame_off[p0 + l] : 0ull;
-    const uint64_t on = (uint64_t)__shfl_down((long long)o, 1, 64);
-    uint32_t len = l < Tv ? (on - o < 0xFFFFFFFFull ? (uint32_t)(on - o) : 0xFFFFFFFFu) : 0u;
-    len = wave_max(len);
-    blk = (uint64_t)len * Tv * 4u > (fo_end - fo0) * 5u;
-  }
+  const bool adapt = a.tile_sums == 1u && T < 64u;
+  uint64_t o_adapt = 0;
+  if (adapt && (tid & 63u) <= Tv) o_adapt = a.frame_off[p0 + (tid & 63u)];
   const uint64_t total = frames_limit(a);
   const uint64_t A = fo0 & ~15ull;
   const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
@@ -982,12 +1001,20 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
     const uint32_t nvec = (uint32_t)(run >> 4);
     u32x4* dst = reinterpret_cast<u32x4*>(img);
     constexpr uint32_t P = 8;
+    const bool decide = adapt && nvec >= NT;  // (every lane then runs the first round)
     for (uint32_t v0 = tid; v0 < nvec; v0 += P * NT) {
       u32x4 r[P];
 #pragma unroll
       for (uint32_t u = 0; u < P; ++u) {
         const uint32_t v = v0 + u * NT;
         if (v < nvec) r[u] = load16_guarded(a.frames, A + 16ull * v, total);
+      }
+      if (decide && v0 == tid) {  // first round: the tile's longest frame against its mean
+        const uint64_t on = (uint64_t)__shfl_down((long long)o_adapt, 1, 64);
+        const uint32_t l = tid & 63u;
+        uint32_t len = l < Tv ? (on - o_adapt < 0xFFFFFFFFull ? (uint32_t)(on - o_adapt) : 0xFFFFFFFFu) : 0u;
+        len = wave_max(len);
+        blk = (uint64_t)len * Tv * 4u > (fo_end - fo0) * 5u;
       }
 #pragma unroll
       for (uint32_t u = 0; u < P; ++u) {
