@@ -193,7 +193,7 @@ __global__ void __launch_bounds__(kBlock) decode_verify_kernel(DecodeArgs a) {
 // utils/packet.py:73): the windows' high bits are OR'ed as they are summed,
 // and only a frame with a high bit runs the byte checks over its LDS chunks.
 template <int H, bool COPY, bool U8>
-__global__ void __launch_bounds__(kBlock) decode_tile_kernel(DecodeArgs a) {
+__global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 ? 8 : 1))) decode_tile_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const uint32_t tid = threadIdx.x;
   const uint32_t glog = a.glog;

@@ -968,7 +968,6 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   const uint32_t q = tid >> glog, g = tid & (G - 1u);
   uint32_t* lds_fo = reinterpret_cast<uint32_t*>(lds);                       // [T + 1]
   unsigned char* img = lds + ((((T + 1u) * 4u) + 15u) & ~15u) + kVTGuard;   // the run
-  uint32_t* lds_blk = reinterpret_cast<uint32_t*>(lds + dvt_blk_off(T, a.tile_cap));  // [cap / 128 + 4]
   const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
@@ -992,6 +991,13 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
     decode_varlen_frame<H, U8, 6>(a, p0 + q, q < Tv, g, glog);
     return;
   }
+  // The block words: tile_sums 2, a region of their own after the run's budget;
+  // per tile (1), right after the run inside its budget (no LDS beyond the chunk
+  // form's, which would cost a tile per CU at MTU hints: 27.1 vs 26.3 KB), for
+  // tiles that leave room for them.
+  uint32_t* lds_blk = reinterpret_cast<uint32_t*>(
+      a.tile_sums == 2u ? lds + dvt_blk_off(T, a.tile_cap) : img + run + 16u);  // [run / 128 + 2]
+  const bool blk_room = run + 16u + (run >> 5) + 8u <= a.tile_cap;
   // tile-relative offsets; one outside [A, fo_end] reads as 0xFFFFFFFF
   const uint64_t span_end = fo_end - A;
   auto rel = [&](uint64_t o) { return o - A <= span_end ? (uint32_t)(o - A) : 0xFFFFFFFFu; };
@@ -1014,7 +1020,7 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
         const uint32_t l = tid & 63u;
         uint32_t len = l < Tv ? (on - o_adapt < 0xFFFFFFFFull ? (uint32_t)(on - o_adapt) : 0xFFFFFFFFu) : 0u;
         len = wave_max(len);
-        blk = (uint64_t)len * Tv * 4u > (fo_end - fo0) * 5u;
+        blk = blk_room && (uint64_t)len * Tv * 4u > (fo_end - fo0) * 5u;
       }
 #pragma unroll
       for (uint32_t u = 0; u < P; ++u) {
@@ -2269,7 +2275,7 @@ static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
     return launch_decode_small<H, U8>(args, stream);
   if (args.glog != kNoVec && args.tile_cap && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0) {
     const uint32_t T = kBlock >> args.glog;
-    const size_t lds = dvt_lds_bytes(T, args.tile_cap, args.tile_sums != 0u);
+    const size_t lds = dvt_lds_bytes(T, args.tile_cap, args.tile_sums == 2u);
     if (lds <= 65536) {
       const uint64_t blocks = (args.n + T - 1) / T;
       // 76 VGPRs (6 waves per SIMD).  Asking the allocator for 7 or 8 waves
