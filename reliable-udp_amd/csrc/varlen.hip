@@ -978,12 +978,10 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   // barrier; a longest frame over 1.25x the tile's mean takes block sums (the
   // lane groups of a ragged tile then have about equal work), an even tile
   // keeps the chunk sums (no DPP work in its streaming phase).
-  // (the offsets load with the tile's first ones; the choice is made once the
-  // run's first loads are in flight, so it costs the staging no round trip)
+  // (the choice is made once the run's first loads are in flight: it costs the
+  // staging no round trip)
   bool blk = a.tile_sums == 2u;
-  const bool adapt = a.tile_sums == 1u && T < 64u;
-  uint64_t o_adapt = 0;
-  if (adapt && (tid & 63u) <= Tv) o_adapt = a.frame_off[p0 + (tid & 63u)];
+  const bool adapt = a.tile_sums == 1u && Tv == 16u;  // (16-frame tiles: MTU-scale hints)
   const uint64_t total = frames_limit(a);
   const uint64_t A = fo0 & ~15ull;
   const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
@@ -1008,19 +1006,27 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
     u32x4* dst = reinterpret_cast<u32x4*>(img);
     constexpr uint32_t P = 8;
     const bool decide = adapt && nvec >= NT;  // (every lane then runs the first round)
-    for (uint32_t v0 = tid; v0 < nvec; v0 += P * NT) {
+    auto stage = [&](uint32_t v0, bool first) {
       u32x4 r[P];
 #pragma unroll
       for (uint32_t u = 0; u < P; ++u) {
         const uint32_t v = v0 + u * NT;
         if (v < nvec) r[u] = load16_guarded(a.frames, A + 16ull * v, total);
       }
-      if (decide && v0 == tid) {  // first round: the tile's longest frame against its mean
-        const uint64_t on = (uint64_t)__shfl_down((long long)o_adapt, 1, 64);
-        const uint32_t l = tid & 63u;
-        uint32_t len = l < Tv ? (on - o_adapt < 0xFFFFFFFFull ? (uint32_t)(on - o_adapt) : 0xFFFFFFFFu) : 0u;
-        len = wave_max(len);
-        blk = blk_room && (uint64_t)len * Tv * 4u > (fo_end - fo0) * 5u;
+      if (first && decide) {
+        // the tile's longest frame against its mean, from its 17 offsets by
+        // scalar loads (one round trip) and scalar max, while the run's first
+        // loads are in flight
+        uint32_t mx = 0;
+        const uint64_t* o = a.frame_off + p0;
+        uint64_t prev_o = o[0];
+#pragma unroll
+        for (uint32_t i = 1; i <= 16u; ++i) {
+          const uint64_t d = o[i] - prev_o;
+          mx = d > mx ? (d < 0xFFFFFFFFull ? (uint32_t)d : 0xFFFFFFFFu) : mx;
+          prev_o = o[i];
+        }
+        blk = blk_room && (uint64_t)mx * 16u * 4u > (fo_end - fo0) * 5u;
       }
 #pragma unroll
       for (uint32_t u = 0; u < P; ++u) {
@@ -1034,7 +1040,13 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
           if ((tid & 7u) == 0) lds_blk[v >> 3] = eo;
         }
       }
+    };
+    uint32_t v0 = tid;
+    if (v0 < nvec) {
+      stage(v0, true);
+      v0 += P * NT;
     }
+    for (; v0 < nvec; v0 += P * NT) stage(v0, false);
     if (a.early_fo) {
       if (tid <= Tv) lds_fo[tid] = fo_r;
     } else {
