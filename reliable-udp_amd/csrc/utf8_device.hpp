@@ -194,10 +194,7 @@ __device__ __forceinline__ uint64_t utf8_stream_frames(uint32_t R0, uint32_t nf,
   uint32_t prev = cA + k0 > 0 ? dw(((cA + k0) << 2) - 1u) : 0u;
   Utf8Pre q_last = utf8_pre(prev);
   uint64_t bits = 0;
-  for (uint32_t k = k0; k < k1; ++k) {
-    const uint32_t c = cA + k;
-    u32x4 v = chunk(c);
-    if (c == cEnd) v = keep_bytes(v, 0, (int)(R1 & 15u));  // the next wave's bytes read as 0
+  auto body = [&](uint32_t c, u32x4 v) {
     // ASCII with no lead byte just before: nothing to check
     if (high_bits(v) || (prev & (prev << 1) & 0x80808000u)) {
       const Utf8Pre q1 = utf8_pre(v.x), q2 = utf8_pre(v.y), q3 = utf8_pre(v.z), q4 = utf8_pre(v.w);
@@ -217,7 +214,14 @@ __device__ __forceinline__ uint64_t utf8_stream_frames(uint32_t R0, uint32_t nf,
       q_last = utf8_pre(v.w);
     }
     prev = v.w;
-  }
+  };
+  for (uint32_t k = k0; k + 1u < k1; ++k) body(cA + k, chunk(cA + k));
+  // the lane's last chunk; the next wave's bytes read as 0 (only in the chunk
+  // holding R1, the last of the last lane's run)
+  const uint32_t cl = cA + k1 - 1u;
+  u32x4 v = chunk(cl);
+  if (cl == cEnd) v = keep_bytes(v, 0, (int)(R1 & 15u));
+  body(cl, v);
   return bits;
 }
 
