@@ -982,6 +982,11 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   // staging no round trip)
   bool blk = a.tile_sums == 2u;
   const bool adapt = a.tile_sums == 1u && Tv == 16u;  // (16-frame tiles: MTU-scale hints)
+  uint32_t len_adapt = 0;
+  if (adapt && (tid & 63u) < 16u) {
+    const uint64_t d = a.frame_off[p0 + (tid & 63u) + 1u] - a.frame_off[p0 + (tid & 63u)];
+    len_adapt = d < 0xFFFFFFFFull ? (uint32_t)d : 0xFFFFFFFFu;
+  }
   const uint64_t total = frames_limit(a);
   const uint64_t A = fo0 & ~15ull;
   const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
@@ -1014,18 +1019,15 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
         if (v < nvec) r[u] = load16_guarded(a.frames, A + 16ull * v, total);
       }
       if (first && decide) {
-        // the tile's longest frame against its mean, from its 17 offsets by
-        // scalar loads (one round trip) and scalar max, while the run's first
-        // loads are in flight
-        uint32_t mx = 0;
-        const uint64_t* o = a.frame_off + p0;
-        uint64_t prev_o = o[0];
-#pragma unroll
-        for (uint32_t i = 1; i <= 16u; ++i) {
-          const uint64_t d = o[i] - prev_o;
-          mx = d > mx ? (d < 0xFFFFFFFFull ? (uint32_t)d : 0xFFFFFFFFu) : mx;
-          prev_o = o[i];
-        }
+        // the tile's longest frame against its mean: lane i < 16 of every wave
+        // holds frame i's length (its two offsets, loaded with the tile's first
+        // ones), a DPP max over the row, the first lane's value for the wave
+        uint32_t mx = len_adapt;
+        mx = max(mx, dpp_row<0xB1>(mx));
+        mx = max(mx, dpp_row<0x4E>(mx));
+        mx = max(mx, dpp_row<0x141>(mx));
+        mx = max(mx, dpp_row<0x140>(mx));
+        mx = (uint32_t)__builtin_amdgcn_readfirstlane((int)mx);
         blk = blk_room && (uint64_t)mx * 16u * 4u > (fo_end - fo0) * 5u;
       }
 #pragma unroll
