@@ -305,8 +305,11 @@ struct Tuning {
   // equal 1472-B lengths 0.246 -> 0.268 (the block sums' DPP work sits in the
   // streaming phase; profiles/r04/sweeps/varlen_decode_blocks.json).  1: per
   // tile, for tiles whose longest frame is over 1.25x their mean (every wave
-  // reads the tile's offsets: uniform without a barrier); 2: every tile; 0: none.
-  RUDP_KNOB(varlen_decode_blocks, 1)
+  // reads the tile's lengths: uniform without a barrier): ragged 0.279 ->
+  // 0.264 ms, but equal lengths 0.235 -> 0.252 (round 5,
+  // profiles/r05/sweeps/varlen_decode_adaptive_blocks.json); 2: every tile;
+  // 0: none (the product's form; 1 and 2 exist in the diagnostics build only).
+  RUDP_KNOB(varlen_decode_blocks, 0)
   RUDP_KNOB(utf8_tile, 1)
   // Packed-frame UTF-8 validation through LDS tiles (hints >= 128 B) and its
   // LDS budget in % of the hinted run: 1M x 1479 B ASCII frames 0.287 ->

@@ -980,8 +980,10 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   // keeps the chunk sums (no DPP work in its streaming phase).
   // (the choice is made once the run's first loads are in flight: it costs the
   // staging no round trip)
-  bool blk = a.tile_sums == 2u;
-  const bool adapt = a.tile_sums == 1u && Tv == 16u;  // (16-frame tiles: MTU-scale hints)
+  // (both forms measured slower than chunk sums where lengths are equal, the per-tile
+  // choice too: diagnostics build only; profiles/r05/sweeps/varlen_decode_adaptive_blocks.json)
+  bool blk = RUDP_TOOLS && a.tile_sums == 2u;
+  const bool adapt = RUDP_TOOLS && a.tile_sums == 1u && Tv == 16u;  // (16-frame tiles: MTU-scale hints)
   uint32_t len_adapt = 0;
   if (adapt && (tid & 63u) < 16u) {
     const uint64_t d = a.frame_off[p0 + (tid & 63u) + 1u] - a.frame_off[p0 + (tid & 63u)];
