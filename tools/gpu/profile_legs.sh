@@ -12,6 +12,7 @@ declare -A LEG=(
   [enc64]="--op encode --L 64 --steps 80"
   [dec1472]="--op decode --L 1472 --steps 40"
   [decu8_1472]="--op decode --utf8 --L 1472 --steps 40"
+  [decu8text]="--op decode --utf8 --text --L 1472 --steps 40"
   [enc16M]="--op encode --L 1472 --n 16777216 --steps 8"
   [venc1472]="--op encode_varlen --L 1472 --steps 40"
   [vdec1472]="--op decode_varlen --L 1472 --steps 40"
@@ -26,7 +27,7 @@ declare -A LEG=(
   [vdecu8_1c]="--op decode_varlen --utf8 --L 1 --layout rudp5 --steps 80"
 )
 legs=("$@")
-[ ${#legs[@]} -eq 0 ] && legs=(enc1472 enc1024 enc64 dec1472 decu8_1472 enc16M venc1472 vdec1472 vdecu8_1472 \
+[ ${#legs[@]} -eq 0 ] && legs=(enc1472 enc1024 enc64 dec1472 decu8_1472 decu8text enc16M venc1472 vdec1472 vdecu8_1472 \
                                vencrag vdecrag vdecu8rag utf8 dedup venc1c vdec1c vdecu8_1c)
 for leg in "${legs[@]}"; do
   bash tools/gpu/run.sh trace ${P}_${leg}_kt $R ${LEG[$leg]}

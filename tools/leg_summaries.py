@@ -23,6 +23,8 @@ LEGS = {
     "dec1472": ("decode_verify_1Mx1472", "decode_tile_kernel", 1 << 20, 1472, 1485),
     # parse + verify + strict UTF-8 in one pass: the valid flag is one more byte written
     "decu8_1472": ("decode_utf8_1Mx1472", "decode_tile_kernel", 1 << 20, 1472, 1486),
+    # the same on valid multi-byte text (every chunk through the table check)
+    "decu8text": ("decode_utf8_1Mx1472_multibyte_text", "decode_tile_kernel", 1 << 20, 1472, 1486),
     "enc16M": ("encode_16Mx1472", "encode_tile_kernel", 1 << 24, 1472, 2956),
     "venc1472": ("encode_varlen_1Mx1472", "scan_block_sums_kernel<8u>,scan_block_bases_kernel,scan_apply_kernel,"
                  "encode_varlen_tile_kernel", 1 << 20, 1472, 2968),
