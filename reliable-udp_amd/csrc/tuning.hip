@@ -332,7 +332,8 @@ RUDP_API int rudpx_tune(int key, int value) {
             : key == 68 ? &t.varlen_decode_nt
             : key == 69 ? &t.varlen_decode_r4
             : key == 70 ? &t.dedup_small_fpt
-            : key == 71 ? &t.host_min_chunks : nullptr;
+            : key == 71 ? &t.host_min_chunks
+            : key == 72 ? &t.decode_stagger : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }

@@ -4,7 +4,8 @@ For every shape, each knob value's launches run in rotation (median of
 --reps rounds of --inner back-to-back calls, HIP events), and every value's
 output is compared byte for byte with the first value's.
 
-shapes: encode:L (fixed-length, 1M x L, rotating sets below 1 GiB), varlen:L
+shapes: encode:L (fixed-length, 1M x L, rotating sets below 1 GiB), decode:L, u8:L (decode + UTF-8),
+u8text:L (the same on valid multi-byte text), varlen:L
 (packed, equal lengths), ragged (lengths uniform in [0, 2944]), decode:L,
 vdec:L (varlen decode, equal lengths; vdec:L+u with the UTF-8 check), rdec (varlen
 decode, ragged ASCII lengths; rdec:+u; rdec:sort sorts each run of 16 lengths,
@@ -34,12 +35,15 @@ from rudp import _native, batch  # noqa: E402
 def make_shape(spec, dev):
     n = 1 << 20
     kind, _, arg = spec.partition(":")
-    if kind in ("encode", "decode"):
+    if kind in ("encode", "decode", "u8", "u8text"):
         L = int(arg)
         nsets = max(1, min(8, math.ceil((1 << 30) / (n * (2 * L + 12)))))
         sets = []
         for _ in range(nsets):
             tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
+            if kind == "u8text":  # valid multi-byte text in every payload (bench decode_utf8_*_multibyte_text)
+                from run_kernel import text_payloads
+                pay = text_payloads(n, L, dev)
             fr, _ = batch.pack_batch(tab, pay, 7)
             sets.append((tab, pay, fr))
         cur = [0]
@@ -50,6 +54,9 @@ def make_shape(spec, dev):
             if kind == "encode":
                 batch.pack_batch(tab, pay, 7, out=fr, want_csum=False)
                 return fr
+            if kind.startswith("u8"):  # decode + strict UTF-8 in one pass
+                d = batch.unpack_batch(fr, 7, utf8=True)
+                return torch.cat([d.ok, d.valid])
             return batch.unpack_batch(fr, 7).ok
         return run
     g = torch.Generator(device=dev).manual_seed(0x5EED0004)
