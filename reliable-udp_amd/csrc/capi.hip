@@ -588,7 +588,6 @@ int rudp_decode_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_nul
   // shape) leave it to the validation kernels, a second read of the frames.
   const bool fused = path == DecodePath::kCopyTile || path == DecodePath::kVerifyTile;
   a.valid = fused ? d_valid_or_null : nullptr;
-  a.stagger = a.valid ? (uint32_t)tuning().decode_stagger : 0u;
   rc = launch_decode(a, layout, path, (hipStream_t)hip_stream);
   if (rc) return hip_fail((hipError_t)rc, "decode launch");
   if (d_valid_or_null && !fused) {

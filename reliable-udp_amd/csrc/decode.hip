@@ -201,10 +201,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
   const uint32_t T = kBlock >> glog;
   const uint32_t q = tid >> glog;
   const uint32_t g = tid & (G - 1u);
-  // (experiment: the workgroups of odd 256-block layers of the first round start
-  // later, so a CU's resident tiles do not all load and then all check at once)
-  if (U8 && a.stagger && blockIdx.x < 1536u && ((blockIdx.x >> 8) & 1u))
-    for (uint32_t i = 0; i < a.stagger; ++i) __builtin_amdgcn_s_sleep(127);
   const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;

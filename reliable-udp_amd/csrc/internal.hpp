@@ -76,7 +76,6 @@ struct DecodeArgs {
   uint32_t align64;         // tile kernel: wave loads/stores start on 64-B sector boundaries
   uint32_t stage_out;       // tile kernel: outputs staged in LDS, written as dwords (pointers 4-B aligned)
   uint32_t xcd;             // tile kernel: XCD-contiguous tile order (xcd_tile)
-  uint32_t stagger;         // tile kernel: s_sleep rounds (x 127 x 64 cycles) for workgroups in odd 256-block layers
 };
 
 struct SynthArgs {

@@ -279,6 +279,9 @@ RUDP_API int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, i
 // 63: varlen decode tile frame sums from 128-B block sums (0: chunk by chunk);
 // 64: a checked small-frame encode of one tile in one launch (no pass 1);
 // 71: *_host pipeline: least chunks for a batch over 4 MiB (copy / kernel overlap).
+// (72: a first-round stagger of half the fused decode tiles' workgroups (s_sleep),
+// 0.539 -> 0.540-0.543 ms on multi-byte text, ASCII 0.229 -> 0.231-0.233: removed;
+// profiles/r05/sweeps/utf8_decode_stagger.json.)
 // (54: chunked / rotated XCD orders, measured within 2% and removed;
 // profiles/r02/headline/xcd_orders.json.)
 // (55, 56: a small-tile launch tail, and 57: persistent workgroups looping over the tiles,
@@ -332,8 +335,7 @@ RUDP_API int rudpx_tune(int key, int value) {
             : key == 68 ? &t.varlen_decode_nt
             : key == 69 ? &t.varlen_decode_r4
             : key == 70 ? &t.dedup_small_fpt
-            : key == 71 ? &t.host_min_chunks
-            : key == 72 ? &t.decode_stagger : nullptr;
+            : key == 71 ? &t.host_min_chunks : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }
