@@ -79,8 +79,11 @@ class PayloadSpans:
     @property
     def start(self):
         if self._start is None:
-            import torch
-            self._start = torch.minimum(self._frame_off[:-1] + self._H, self._frame_off[1:])
+            if isinstance(self._frame_off, np.ndarray):  # a host-memory decode's offsets
+                self._start = np.minimum(self._frame_off[:-1] + self._H, self._frame_off[1:])
+            else:
+                import torch
+                self._start = torch.minimum(self._frame_off[:-1] + self._H, self._frame_off[1:])
         return self._start
 
     @property
@@ -744,8 +747,8 @@ def _unpack_varlen_host(frames, frame_off, H, csum, check, utf8, device, len_hin
             _ptr(frames), frames.size, frame_off.ctypes.data, min(len_hint or frames.size // n, 0xFFFFFFFF), n,
             _ptr(csum) if csum is not None else None, _ptr(seq), _ptr(ack), _ptr(flags), _ptr(ok), _ptr(cs),
             _ptr(valid) if valid is not None else None, status.ctypes.data, H, device))
-    off = frame_off.astype(np.int64, copy=False)
-    pay = (np.minimum(off[:-1] + H, off[1:]), off[1:])
+    # payload spans computed on first use (two passes over N offsets: ~1 ms per 1M frames)
+    pay = PayloadSpans(frame_off.view(np.int64) if frame_off.dtype == np.uint64 else frame_off, H)
     res = DecodedBatch(seq, ack, flags, ok, cs, pay, status, valid)
     return res.check() if check else res
 
@@ -771,7 +774,7 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
     numpy arrays (a receive buffer in host memory): staged through GPU
     ``device`` by rudp_decode_varlen_host, synchronously, with the same
     per-frame offset rule; the result is a ``DecodedBatch`` of numpy arrays
-    (payload: the pair (start, end) of int64 arrays, status u32 [1]).
+    (payload: ``PayloadSpans`` of int64 arrays, status u32 [1]).
     """
     H = layout_header_len(layout)
     if H == 7 and csum is not None:
