@@ -373,9 +373,10 @@ RUDP_API int rudp_udp_send_batch_to(int fd, const uint8_t* h_frames, const uint6
  *   Packet() + set_header_field + set_payload + to_byte() per datagram
  *   (utils/reliableUDP.py:53-61, utils/packet.py:43-65, :76-81).
  *   h_frame_off receives n + 1 offsets (the exclusive scan of len[i] +
- *   layout).  Every length (<= 65535) and frames_cap (>= sum(len) + n *
- *   layout) is checked before any work is enqueued: a bad batch returns
- *   RUDP_EINVAL and writes nothing.
+ *   layout).  Every length (<= 65535), sum(len) == payload_bytes (the size
+ *   of h_in->payload) and frames_cap (>= sum(len) + n * layout) are checked
+ *   before any work is enqueued: a bad batch returns RUDP_EINVAL and writes
+ *   nothing.
  */
 RUDP_API int rudp_encode_host(const rudp_batch* h_in, uint8_t* h_frames, uint16_t* h_csum_or_null,
                      int layout, int device);
@@ -388,8 +389,9 @@ RUDP_API int rudp_decode_varlen_host(const uint8_t* h_frames, uint64_t frames_by
                                      uint16_t* h_seq, uint16_t* h_ack, uint8_t* h_flags, uint8_t* h_ok,
                                      uint16_t* h_csum_out_or_null, uint8_t* h_valid_or_null,
                                      uint32_t* h_status_or_null, int layout, int device);
-RUDP_API int rudp_encode_varlen_host(const rudp_batch* h_in, uint8_t* h_frames, uint64_t frames_cap,
-                                     uint64_t* h_frame_off, uint16_t* h_csum_or_null, int layout, int device);
+RUDP_API int rudp_encode_varlen_host(const rudp_batch* h_in, uint64_t payload_bytes, uint8_t* h_frames,
+                                     uint64_t frames_cap, uint64_t* h_frame_off, uint16_t* h_csum_or_null,
+                                     int layout, int device);
 
 /*
  * Deterministic synthetic batch, generated on the device:

@@ -268,6 +268,42 @@ int pipeline_slots() {
   return s < 2 ? 2 : s > kMaxSlots ? kMaxSlots : s;
 }
 
+// The host passes over a batch's offsets / lengths that plan its chunks run on
+// the caller's thread, ahead of the chunk's copies (for one-character frames a
+// scalar pass took as long as the chunk's copies): built for AVX-512 and AVX2
+// as well, picked at load time by the CPU.
+void offsets_range(const uint64_t* o, uint64_t cnt, uint64_t lim, uint64_t* plo, uint64_t* phi);
+void lengths_sum_max(const uint32_t* l, uint64_t m, uint64_t* psum, uint32_t* pmax);
+#if !defined(__HIP_DEVICE_COMPILE__)
+// least and greatest of o[0, cnt) at or below lim (lo = ~0, hi = 0 when none is)
+__attribute__((target_clones("avx512f", "avx2", "default"))) void offsets_range(const uint64_t* o, uint64_t cnt,
+                                                                              uint64_t lim, uint64_t* plo,
+                                                                              uint64_t* phi) {
+  uint64_t lo = ~0ull, hi = 0;
+  for (uint64_t i = 0; i < cnt; ++i) {
+    const uint64_t x = o[i];
+    const bool in = x <= lim;
+    const uint64_t a = in ? x : ~0ull, b = in ? x : 0;
+    lo = a < lo ? a : lo;
+    hi = b > hi ? b : hi;
+  }
+  *plo = lo;
+  *phi = hi;
+}
+
+__attribute__((target_clones("avx512f", "avx2", "default"))) void lengths_sum_max(const uint32_t* l, uint64_t m,
+                                                                                uint64_t* psum, uint32_t* pmax) {
+  uint64_t sum = 0;
+  uint32_t mx = 0;
+  for (uint64_t i = 0; i < m; ++i) {
+    sum += l[i];
+    mx = l[i] > mx ? l[i] : mx;
+  }
+  *psum = sum;
+  *pmax = mx;
+}
+#endif
+
 // Drive chunks through the pipeline: `plan(p0)` returns the packets of the
 // chunk that starts at packet p0 (> 0, or a negative error code), and the
 // three callbacks enqueue that chunk's work on the stream they are given (all
@@ -1050,8 +1086,8 @@ int rudp_decode_host(const uint8_t* h_frames, uint32_t frame_len, uint64_t n,
 // into chunks whose payload bytes fit a slot; each chunk is one checked
 // device encode (its offsets from 0) plus one add of its base, so the
 // offsets that come back are the batch's own.
-int rudp_encode_varlen_host(const rudp_batch* h_in, uint8_t* h_frames, uint64_t frames_cap, uint64_t* h_frame_off,
-                            uint16_t* h_csum_or_null, int layout, int device) {
+int rudp_encode_varlen_host(const rudp_batch* h_in, uint64_t payload_bytes, uint8_t* h_frames, uint64_t frames_cap,
+                            uint64_t* h_frame_off, uint16_t* h_csum_or_null, int layout, int device) {
   if (!h_in) return fail(RUDP_EINVAL, "rudp_encode_varlen_host: batch is NULL");
   if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
     return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
@@ -1079,13 +1115,9 @@ int rudp_encode_varlen_host(const rudp_batch* h_in, uint8_t* h_frames, uint64_t 
     for (;;) {
       uint64_t sum = 0;
       uint32_t mx = 0;
-      const uint32_t* l = h_in->len + p0;
-      for (uint64_t i = 0; i < m; ++i) {
-        sum += l[i];
-        mx = l[i] > mx ? l[i] : mx;
-      }
+      lengths_sum_max(h_in->len + p0, m, &sum, &mx);
       if (mx > 65535u)
-        return fail(RUDP_EINVAL, "rudp_encode_varlen_host: a length over 65535 in packets [%llu, %llu)",
+        return fail(RUDP_EINVAL, "lengths must lie in [0, 65535] (packets [%llu, %llu))",
                     (unsigned long long)p0, (unsigned long long)(p0 + m));
       if (sum <= bmax || m == 1) {
         pay.push_back(sum);
@@ -1097,9 +1129,12 @@ int rudp_encode_varlen_host(const rudp_batch* h_in, uint8_t* h_frames, uint64_t 
       m /= 2;
     }
   }
+  if (total != payload_bytes)
+    return fail(RUDP_EINVAL, "packed payloads: sum(lengths) must equal payload.numel() (%llu vs %llu)",
+                (unsigned long long)total, (unsigned long long)payload_bytes);
   if (total && !h_in->payload) return fail(RUDP_EINVAL, "rudp_encode_varlen_host: payload is NULL");
   if (total + n * H > frames_cap)
-    return fail(RUDP_EINVAL, "rudp_encode_varlen_host: %llu frame bytes exceed frames_cap %llu",
+    return fail(RUDP_EINVAL, "out is too small for the frames (sum(lengths) + N * header bytes = %llu > %llu)",
                 (unsigned long long)(total + n * H), (unsigned long long)frames_cap);
   DeviceScope dev_scope;
   int rc = dev_scope.set(device);
@@ -1208,14 +1243,7 @@ int rudp_decode_varlen_host(const uint8_t* h_frames, uint64_t frames_bytes, cons
     uint64_t m = n - p0 < cn ? n - p0 : cn;
     for (;;) {
       uint64_t lo = ~0ull, hi = 0;
-      const uint64_t* o = h_frame_off + p0;
-      for (uint64_t i = 0; i <= m; ++i) {
-        const uint64_t x = o[i];
-        if (x <= frames_bytes) {
-          lo = x < lo ? x : lo;
-          hi = x > hi ? x : hi;
-        }
-      }
+      offsets_range(h_frame_off + p0, m + 1, frames_bytes, &lo, &hi);
       if (lo > hi) lo = hi = 0;  // no offset inside the buffer: every frame is rejected unread
       const uint64_t b0 = lo & ~15ull;
       uint64_t b1 = (hi + 15u) & ~15ull;

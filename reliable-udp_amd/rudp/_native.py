@@ -79,7 +79,7 @@ def _declare(lib: ctypes.CDLL) -> None:
         "rudp_encode_host": [ctypes.POINTER(RudpBatch), P, P, I, I],
         "rudp_decode_host": [P, U32, U64, P, P, P, P, P, P, P, P, I, I],
         "rudp_decode_varlen_host": [P, U64, P, U32, U64, P, P, P, P, P, P, P, P, I, I],
-        "rudp_encode_varlen_host": [ctypes.POINTER(RudpBatch), P, U64, P, P, I, I],
+        "rudp_encode_varlen_host": [ctypes.POINTER(RudpBatch), U64, P, U64, P, P, I, I],
         "rudp_synth": [U64, U64, U64, U32, I, P, P, P, P, I, P],
         "rudp_encode_varlen": [ctypes.POINTER(RudpBatch), P, P, P, I, I, P],
         "rudp_validate_utf8": [P, P, U32, U64, I, P, I, P],

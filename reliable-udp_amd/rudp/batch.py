@@ -144,6 +144,19 @@ def _is_torch(x) -> bool:
     return isinstance(x, torch.Tensor)
 
 
+_PIN_DT = {np.uint8: "uint8", np.uint16: "uint16", np.int64: "int64"}
+
+
+def _pinned_out(n: int, dtype) -> np.ndarray:
+    """A per-packet output array of a *_host call: page-locked, from torch's
+    caching host allocator (a repeated call of the same size reuses the block),
+    so the pipeline's D2H lands at the link's rate instead of faulting fresh
+    pageable pages in.  Only the small per-packet arrays come from here; frames
+    and payloads are the caller's or plain numpy."""
+    import torch
+    return torch.empty((n,), dtype=getattr(torch, _PIN_DT[dtype]), pin_memory=True).numpy()
+
+
 def _as_table(headers) -> HeaderTable:
     if isinstance(headers, HeaderTable):
         return headers
@@ -280,7 +293,7 @@ def _pack_host(tab: HeaderTable, payloads, H, want_csum, device, out=None, csum_
     if csum_out is not None:
         csum = _host_out(csum_out, "csum_out", np.uint16, (n,))
     else:
-        csum = np.empty((n,), dtype=np.uint16) if want_csum else None
+        csum = _pinned_out(n, np.uint16) if want_csum else None
     b = _native.RudpBatch(n=n, payload_len=L, reserved=0, seq=_ptr(seq), ack=_ptr(ack),
                           flags=_ptr(flags), payload=_ptr(payloads), len=None, payload_off=None)
     _native.check(_native.lib().rudp_encode_host(
@@ -292,17 +305,17 @@ def _unpack_host(frames, H, csum, copy_payload, device, utf8=False):
     frames = _host_arr(frames, "frames", np.uint8, 2)
     n, F = frames.shape
     L = max(F - H, 0)
-    seq = np.empty((n,), np.uint16)
-    ack = np.empty((n,), np.uint16)
-    flags = np.empty((n,), np.uint8)
-    ok = np.empty((n,), np.uint8)
-    cs = np.empty((n,), np.uint16)
+    seq = _pinned_out(n, np.uint16)
+    ack = _pinned_out(n, np.uint16)
+    flags = _pinned_out(n, np.uint8)
+    ok = _pinned_out(n, np.uint8)
+    cs = _pinned_out(n, np.uint16)
     if csum is not None:
         csum = _host_arr(csum, "csum", np.uint16, 1)
         if csum.shape[0] != n:
             raise ValueError(f"csum has {csum.shape[0]} entries for {n} frames")
     pay = np.empty((n, L), np.uint8) if copy_payload else None
-    valid = np.empty((n,), np.uint8) if utf8 else None
+    valid = _pinned_out(n, np.uint8) if utf8 else None
     if n:
         _native.check(_native.lib().rudp_decode_host(
             _ptr(frames), F, n, _ptr(csum) if csum is not None else None, _ptr(seq), _ptr(ack),
@@ -581,29 +594,23 @@ def _pack_varlen_host(tab: HeaderTable, payload, lengths, H, payload_off, want_c
     for name, a in (("seq", seq), ("ack", ack), ("flags", flags)):
         if a.shape[0] != n:
             raise ValueError(f"{name} has {a.shape[0]} entries for {n} packets")
-    if n and (int(lengths.min()) < 0 or int(lengths.max()) > 65535):
-        raise ValueError("lengths must lie in [0, 65535]")
-    if int(lengths.sum(dtype=np.int64)) != payload.size:
-        raise ValueError("packed payloads: sum(lengths) must equal payload.numel(); "
-                         "gathered payloads: payload_off + lengths must stay inside payload")
-    need = payload.size + n * H
+    # (the lengths, their sum against the payload and the capacity are checked by the
+    # C entry before any work: a bad batch raises ValueError and nothing is written)
     if out is not None:
         if not isinstance(out, np.ndarray) or out.dtype != np.uint8 or out.ndim != 1 \
                 or not out.flags["C_CONTIGUOUS"] or not out.flags["WRITEABLE"]:
             raise ValueError("out must be a writeable C-contiguous 1-D uint8 array")
-        if out.size < need:
-            raise ValueError("out is too small for the frames (sum(lengths) + N * header bytes)")
         frames = out
     else:
-        frames = np.empty((need,), np.uint8)
-    off = np.empty((n + 1,), np.int64)
-    csum = np.empty((n,), np.uint16) if want_csum else None
+        frames = np.empty((payload.size + n * H,), np.uint8)
+    off = _pinned_out(n + 1, np.int64)
+    csum = _pinned_out(n, np.uint16) if want_csum else None
     b = _native.RudpBatch(n=n, payload_len=min(payload.size // n, 65535) if n else 0, reserved=0,
                           seq=_ptr(seq), ack=_ptr(ack), flags=_ptr(flags), payload=_ptr(payload),
                           len=_ptr(lengths.view(np.uint32)), payload_off=None)
     _native.check(_native.lib().rudp_encode_varlen_host(
-        ctypes.byref(b), _ptr(frames), frames.size, off.ctypes.data, _ptr(csum) if csum is not None else None,
-        H, device))
+        ctypes.byref(b), payload.size, _ptr(frames) if frames.size else 16, frames.size, off.ctypes.data,
+        _ptr(csum) if csum is not None else None, H, device))
     return HostVarlenFrames(frames, off, csum, 0)
 
 
@@ -725,7 +732,7 @@ def _check_offsets(frames, frame_off, stream=None) -> int:
     return min((last - first) // n, 0xFFFFFFFF)
 
 
-def _unpack_varlen_host(frames, frame_off, H, csum, check, utf8, device, len_hint=0):
+def _unpack_varlen_host(frames, frame_off, H, csum, check, utf8, device, len_hint=0, reuse=None):
     frames = _host_arr(frames, "frames", np.uint8, 1)
     frame_off = np.ascontiguousarray(frame_off)
     if frame_off.dtype not in (np.int64, np.uint64) or frame_off.ndim != 1:
@@ -737,10 +744,19 @@ def _unpack_varlen_host(frames, frame_off, H, csum, check, utf8, device, len_hin
         csum = _host_arr(csum, "csum", np.uint16, 1)
         if csum.shape[0] != n:
             raise ValueError(f"csum has {csum.shape[0]} entries for {n} frames")
-    seq, ack, cs = (np.empty((n,), np.uint16) for _ in range(3))
-    flags, ok = np.empty((n,), np.uint8), np.empty((n,), np.uint8)
-    valid = np.empty((n,), np.uint8) if utf8 else None
-    status = np.zeros((1,), np.uint32)
+    if reuse is not None:
+        # an earlier host result of the same N and utf8 choice: its arrays take this call's outputs
+        if not isinstance(reuse, DecodedBatch) or not isinstance(reuse.seq, np.ndarray) or reuse.seq.shape != (n,) \
+                or (reuse.valid is not None) != utf8:
+            raise ValueError("reuse= must be an earlier host unpack_batch_varlen result for the same N and utf8 choice")
+        seq, ack, cs, flags, ok, valid = reuse.seq, reuse.ack, reuse.csum, reuse.flags, reuse.ok, reuse.valid
+        status = reuse.status
+        status[0] = 0
+    else:
+        seq, ack, cs = (_pinned_out(n, np.uint16) for _ in range(3))
+        flags, ok = _pinned_out(n, np.uint8), _pinned_out(n, np.uint8)
+        valid = _pinned_out(n, np.uint8) if utf8 else None
+        status = np.zeros((1,), np.uint32)
     if n:
         # (negative int64 offsets read as huge u64 ones: past the buffer, so rejected)
         _native.check(_native.lib().rudp_decode_varlen_host(
@@ -774,15 +790,15 @@ def unpack_batch_varlen(frames, frame_off, layout: Union[str, int] = "rudp7", *,
     numpy arrays (a receive buffer in host memory): staged through GPU
     ``device`` by rudp_decode_varlen_host, synchronously, with the same
     per-frame offset rule; the result is a ``DecodedBatch`` of numpy arrays
-    (payload: ``PayloadSpans`` of int64 arrays, status u32 [1]).
+    (payload: ``PayloadSpans`` of int64 arrays, status u32 [1]); ``reuse``: an
+    earlier such result whose arrays take this call's outputs (a receive loop
+    keeps its buffers; pinned ones copy back at the link's rate).
     """
     H = layout_header_len(layout)
     if H == 7 and csum is not None:
         raise ValueError("rudp7 carries its checksum in-band; csum= is for rudp5")
     if not _is_torch(frames):
-        if reuse is not None:
-            raise ValueError("reuse= is for device batches")
-        return _unpack_varlen_host(frames, frame_off, H, csum, check, utf8, device)
+        return _unpack_varlen_host(frames, frame_off, H, csum, check, utf8, device, reuse=reuse)
     import torch
     dev = frames.device
     _dev_check(frames, "frames", torch.uint8, 1, dev)

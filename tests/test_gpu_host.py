@@ -216,6 +216,22 @@ def test_varlen_host_decode_frame_over_slot(cuda):
             batch.unpack_batch_varlen(big, off, 7)
 
 
+def test_varlen_host_decode_reuse(cuda, golden_varlen):
+    """reuse= an earlier host result: its arrays take the outputs, same answers."""
+    g = golden_varlen
+    flat = g["frames7"]
+    off = np.concatenate([[0], np.cumsum(g["lengths"].astype(np.int64) + 7)]).astype(np.int64)
+    d1 = batch.unpack_batch_varlen(flat, off, 7, utf8=True)
+    keep = {k: np.array(getattr(d1, k), copy=True) for k in ("seq", "ack", "flags", "ok", "csum", "valid")}
+    d1.ok[:] = 9
+    d2 = batch.unpack_batch_varlen(flat, off, 7, utf8=True, reuse=d1)
+    assert d2.ok is d1.ok
+    for k, v in keep.items():
+        assert np.array_equal(getattr(d2, k), v), k
+    with pytest.raises(ValueError, match="reuse"):
+        batch.unpack_batch_varlen(flat, off, 7, reuse=d1)  # utf8 choice differs
+
+
 def test_varlen_host_decode_empty(cuda):
     d = batch.unpack_batch_varlen(np.zeros(0, np.uint8), np.zeros(1, np.int64), 7, utf8=True)
     assert d.ok.shape == (0,) and d.valid.shape == (0,)
@@ -264,6 +280,11 @@ def test_varlen_host_encode_rejects(cuda):
                           flags=tab[2].ctypes.data, payload=np.zeros(70006, np.uint8).ctypes.data,
                           len=lens.ctypes.data, payload_off=None)
     fr, fo = np.zeros(80000, np.uint8), np.zeros(n + 1, np.uint64)
-    assert _native.lib().rudp_encode_varlen_host(ctypes.byref(b), fr.ctypes.data, fr.size, fo.ctypes.data, None,
-                                                 7, 0) == _native.EINVAL
+    assert _native.lib().rudp_encode_varlen_host(ctypes.byref(b), 70006, fr.ctypes.data, fr.size, fo.ctypes.data,
+                                                 None, 7, 0) == _native.EINVAL
+    assert b"65535" in _native.lib().rudp_last_error()
+    lens[3] = 100  # a sum that is not the payload's size: refused before any read of it
+    assert _native.lib().rudp_encode_varlen_host(ctypes.byref(b), 70006, fr.ctypes.data, fr.size, fo.ctypes.data,
+                                                 None, 7, 0) == _native.EINVAL
+    assert b"sum" in _native.lib().rudp_last_error()
     assert not fr.any()

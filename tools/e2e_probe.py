@@ -1,6 +1,7 @@
 """Where the host-memory (*_host) calls spend their time: the raw C-ABI call
 with pinned outputs, the same with pageable outputs, and the Python entry
-(which allocates its outputs), for 1M one-character rudp5 datagrams (decode
+(which allocates its per-packet outputs from torch's caching pinned allocator,
+or takes them from reuse=), for 1M one-character rudp5 datagrams (decode
 and encode, packed) and 1M x 1472 B rudp7 frames (decode + UTF-8).
 
 usage: python tools/e2e_probe.py [--reps 5]
@@ -70,13 +71,16 @@ def main():
         "raw_pinned_out_ms": med(dec_raw(outs_p), args.reps),
         "raw_pageable_out_ms": med(dec_raw(outs_u), args.reps),
         "python_entry_ms": med(lambda: batch.unpack_batch_varlen(fr, fo, "rudp5", csum=cs, utf8=True), args.reps)}
+    prev = batch.unpack_batch_varlen(fr, fo, "rudp5", csum=cs, utf8=True)
+    out["decode_varlen_1M_1char"]["python_entry_reuse_ms"] = med(
+        lambda: batch.unpack_batch_varlen(fr, fo, "rudp5", csum=cs, utf8=True, reuse=prev), args.reps)
     fo_out = pinned(m + 1, torch.int64)
     cs_out = pinned(m, torch.uint16)
     b = _native.RudpBatch(n=m, payload_len=1, reserved=0, seq=seq.ctypes.data, ack=ack.ctypes.data,
                           flags=flg.ctypes.data, payload=pay.ctypes.data, len=lens.ctypes.data, payload_off=None)
     out["encode_varlen_1M_1char"] = {
         "raw_pinned_out_ms": med(lambda: _native.check(lib.rudp_encode_varlen_host(
-            ctypes.byref(b), fr.ctypes.data, fr.size, fo_out.ctypes.data, cs_out.ctypes.data, 5, 0)), args.reps),
+            ctypes.byref(b), m, fr.ctypes.data, fr.size, fo_out.ctypes.data, cs_out.ctypes.data, 5, 0)), args.reps),
         "python_entry_ms": med(lambda: batch.pack_batch_varlen((seq, ack, flg), pay, lens, "rudp5", want_csum=True,
                                                                out=fr), args.reps)}
     del fr, fo, cs
