@@ -195,12 +195,14 @@ __device__ __forceinline__ uint64_t utf8_stream_frames(uint32_t R0, uint32_t nf,
   Utf8Pre q_last = utf8_pre(prev);
   uint64_t bits = 0;
   auto body = [&](uint32_t c, u32x4 v) {
+    // the chunk's last dword is the next one's "bytes before" either way: its
+    // inputs once, ahead of the branch (not again inside it)
+    const Utf8Pre q4 = utf8_pre(v.w);
     // ASCII with no lead byte just before: nothing to check
     if (high_bits(v) || (prev & (prev << 1) & 0x80808000u)) {
-      const Utf8Pre q1 = utf8_pre(v.x), q2 = utf8_pre(v.y), q3 = utf8_pre(v.z), q4 = utf8_pre(v.w);
+      const Utf8Pre q1 = utf8_pre(v.x), q2 = utf8_pre(v.y), q3 = utf8_pre(v.z);
       const uint32_t e0 = utf8_dword_errors(q1, q_last), e1 = utf8_dword_errors(q2, q1),
                      e2 = utf8_dword_errors(q3, q2), e3 = utf8_dword_errors(q4, q3);
-      q_last = q4;
       if (e0 | e1 | e2 | e3) {  // which frames: the first and the last error byte's
         const uint64_t lo = (uint64_t)e0 | ((uint64_t)e1 << 32), hi = (uint64_t)e2 | ((uint64_t)e3 << 32);
         const int bf = lo ? (int)(__builtin_ctzll(lo) >> 3) : 8 + (int)(__builtin_ctzll(hi) >> 3);
@@ -210,12 +212,19 @@ __device__ __forceinline__ uint64_t utf8_stream_frames(uint32_t R0, uint32_t nf,
         const int f0 = x0 + bf >= 0 ? (x0 + bf) / (int)F : -1, f1 = x0 + bl >= 0 ? (x0 + bl) / (int)F : -1;
         bits |= (1ull << (f0 + 1)) | (1ull << (f1 + 1));
       }
-    } else {
-      q_last = utf8_pre(v.w);
     }
+    q_last = q4;
     prev = v.w;
   };
-  for (uint32_t k = k0; k + 1u < k1; ++k) body(cA + k, chunk(cA + k));
+  // two chunks an iteration: the loop-carried inputs rotate through registers
+  // once per pair instead of being copied back after every chunk
+  uint32_t k = k0;
+  for (; k + 2u < k1; k += 2u) {
+    const u32x4 v0 = chunk(cA + k), v1 = chunk(cA + k + 1u);
+    body(cA + k, v0);
+    body(cA + k + 1u, v1);
+  }
+  if (k + 1u < k1) body(cA + k, chunk(cA + k));
   // the lane's last chunk; the next wave's bytes read as 0 (only in the chunk
   // holding R1, the last of the last lane's run)
   const uint32_t cl = cA + k1 - 1u;
