@@ -60,53 +60,54 @@ __device__ __forceinline__ uint32_t high_bits(u32x4 w) { return (w.x | w.y | w.z
 __device__ __forceinline__ uint32_t group_or(uint32_t bits, uint32_t G) { return group_or_rows(bits, G); }
 
 // Per-dword inputs of the table check, computed once per dword and shared by
-// the dword's own check and the next one's (which needs the bytes before
-// it): the low / high nibbles' table selectors (bits 0-2) and their bit-3
-// blend masks (0xFF per byte whose nibble is 8-15), and bit 7 of every byte
-// >= 0xE0 / >= 0xF0 (a 3- / 4-byte lead).
+// the dword's own check and the next one's (which needs the bytes before it).
+// The three nibble tables are looked up on the dword's OWN bytes (a table is
+// bytewise, so looking up the bytes and then shifting the results by one byte
+// equals shifting the bytes and looking them up): t1 / t2 = the "byte before"
+// tables of its high / low nibbles, t3 = the "this byte" table of its high
+// nibble, and ef = 0x80 per byte >= 0xE0 (a 3- or 4-byte lead), | 0x40 if >=
+// 0xF0 (a 4-byte lead).  A table has 16 entries: v_perm_b32 looks up the
+// nibble's bits 0-2 in 8 bytes, and a v_bfi by bit 3 (a mask of 0xFF per byte
+// whose nibble is 8-15) picks the half; one perm where a half is constant.
 struct Utf8Pre {
-  uint32_t sel_lo, m_lo, sel_hi, m_hi, e0, f0;
+  uint32_t t1, t2, t3, ef;
 };
 // Every byte of y replaced by 0xFF if its bit 7 is set, else 0: v_perm_b32's
 // selectors 8-11 replicate the sign bits of bytes 1, 3, 5, 7 of {y, y << 8}.
 __device__ __forceinline__ uint32_t sign_bytes(uint32_t y) { return __builtin_amdgcn_perm(y, y << 8, 0x0B090A08u); }
+__device__ __forceinline__ uint32_t blend(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
 __device__ __forceinline__ Utf8Pre utf8_pre(uint32_t x) {
+  const uint32_t sel_lo = x & 0x07070707u, m_lo = sign_bytes(x << 4);  // bit 3 of each byte
+  const uint32_t sel_hi = (x >> 4) & 0x07070707u, m_hi = sign_bytes(x);  // bit 7
+  // table bits: 0 too short, 1 too long, 2 overlong 3, 3 too large, 4 surrogate,
+  // 5 overlong 2, 6 too large 1000 / overlong 4, 7 two continuations
   Utf8Pre p;
-  p.sel_lo = x & 0x07070707u;
-  p.m_lo = sign_bytes(x << 4);  // bit 3 of each byte
-  p.sel_hi = (x >> 4) & 0x07070707u;
-  p.m_hi = sign_bytes(x);       // bit 7
-  const uint32_t e = x & (x << 1) & (x << 2) & 0x80808080u;
-  p.e0 = e;
-  p.f0 = e & (x << 3);
+  // as the byte before, its high nibble: 0-7 all 0x02 (too long), 8-15 from the second half
+  p.t1 = blend(m_hi, __builtin_amdgcn_perm(0x49150121u, 0x80808080u, sel_hi), 0x02020202u);
+  // as the byte before, its low nibble: all 16 entries
+  p.t2 = blend(m_lo, __builtin_amdgcn_perm(0xCBCBDBCBu, 0xCBCBCBCBu, sel_lo),
+               __builtin_amdgcn_perm(0xCBCBCB8Bu, 0x8383A3E7u, sel_lo));
+  // as this byte, its high nibble: 0-7 and 12-15 all 0x01 (too short)
+  p.t3 = blend(m_hi, __builtin_amdgcn_perm(0x01010101u, 0xBABAAEE6u, sel_hi), 0x01010101u);
+  // leads: nibble 14 -> 0x80, 15 -> 0xC0 (selectors 6, 7: bytes 2, 3 of the first operand)
+  p.ef = m_hi & __builtin_amdgcn_perm(0xC0800000u, 0u, sel_hi);
   return p;
 }
 
 // Error bits of the four bytes of a dword (`c`: utf8_pre of it) given the four
 // before it (`p`), the SWAR form of the lookup validator of Keiser & Lemire
 // ("Validating UTF-8 in less than one instruction per byte"): every byte is
-// checked against the byte before it through three 16-entry tables of the
-// nibbles (too short, too long, overlong 2/3/4, surrogate, too large, two
-// continuations), two v_perm_b32 per table over its halves and a v_bfi by
-// bit 3 (one perm where a half is constant), and against the two and three
-// before it for the continuations a 3- or 4-byte lead asks for.  Nonzero iff
-// some byte breaks strict UTF-8 given its predecessors.
+// checked against the byte before it through the three nibble tables, and
+// against the two and three before it for the continuations a 3- or 4-byte
+// lead asks for.  Nonzero iff some byte breaks strict UTF-8 given its
+// predecessors.
 __device__ __forceinline__ uint32_t utf8_dword_errors(const Utf8Pre& c, const Utf8Pre& p) {
-  // table bits: 0 too short, 1 too long, 2 overlong 3, 3 too large, 4 surrogate,
-  // 5 overlong 2, 6 too large 1000 / overlong 4, 7 two continuations
-  const uint32_t s1 = __builtin_amdgcn_alignbyte(c.sel_hi, p.sel_hi, 3);  // byte 1 = the byte before
-  const uint32_t m1 = __builtin_amdgcn_alignbyte(c.m_hi, p.m_hi, 3);
-  const uint32_t sl = __builtin_amdgcn_alignbyte(c.sel_lo, p.sel_lo, 3);
-  const uint32_t ml = __builtin_amdgcn_alignbyte(c.m_lo, p.m_lo, 3);
-  // byte 1's high nibble: 0-7 all 0x02 (too long), 8-15 from the second half
-  const uint32_t t1 = (m1 & __builtin_amdgcn_perm(0x49150121u, 0x80808080u, s1)) | (~m1 & 0x02020202u);
-  // byte 1's low nibble: all 16 entries
-  const uint32_t t2 = (ml & __builtin_amdgcn_perm(0xCBCBDBCBu, 0xCBCBCBCBu, sl)) |
-                      (~ml & __builtin_amdgcn_perm(0xCBCBCB8Bu, 0x8383A3E7u, sl));
-  // byte 2's (this byte's) high nibble: 0-7 and 12-15 all 0x01 (too short)
-  const uint32_t t3 = (c.m_hi & __builtin_amdgcn_perm(0x01010101u, 0xBABAAEE6u, c.sel_hi)) | (~c.m_hi & 0x01010101u);
-  const uint32_t must23 = __builtin_amdgcn_alignbyte(c.e0, p.e0, 2) | __builtin_amdgcn_alignbyte(c.f0, p.f0, 1);
-  return must23 ^ (t1 & t2 & t3);
+  const uint32_t t1 = __builtin_amdgcn_alignbyte(c.t1, p.t1, 3);  // byte i: the byte before's tables
+  const uint32_t t2 = __builtin_amdgcn_alignbyte(c.t2, p.t2, 3);
+  // a continuation is owed from 2 bytes after a 3/4-byte lead and 3 after a 4-byte lead
+  const uint32_t must23 = (__builtin_amdgcn_alignbyte(c.ef, p.ef, 2) | (__builtin_amdgcn_alignbyte(c.ef, p.ef, 1) << 1)) &
+                          0x80808080u;
+  return must23 ^ (t1 & t2 & c.t3);
 }
 
 // Strict UTF-8 check of one frame's payload bytes [s, fe) by G lanes (lane g
