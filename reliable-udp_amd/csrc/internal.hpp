@@ -381,8 +381,8 @@ struct Tuning {
 #endif
   RUDP_KNOB(host_slots, 3)     // *_host pipeline: device staging slots (2..8)
   RUDP_KNOB(host_stage_mb, 128)  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
-  RUDP_KNOB(host_min_chunks, 4)
-  RUDP_KNOB(decode_stagger, 0)   // fused decode tile: first-round stagger (s_sleep rounds) of half the workgroups  // *_host pipeline: batches over 4 MiB go as at least this many chunks (copy overlap)
+  RUDP_KNOB(host_min_chunks, 4)  // *_host pipeline: batches over 4 MiB go as at least this many chunks (copy overlap)
+
 };
 #undef RUDP_KNOB
 #if RUDP_TOOLS
