@@ -61,21 +61,35 @@ __device__ __forceinline__ uint32_t group_or(uint32_t bits, uint32_t G) { return
 
 // Per-dword inputs of the table check, computed once per dword and shared by
 // the dword's own check and the next one's (which needs the bytes before it).
-// The three nibble tables are looked up on the dword's OWN bytes (a table is
+// The nibble tables are looked up on the dword's OWN bytes (a table is
 // bytewise, so looking up the bytes and then shifting the results by one byte
-// equals shifting the bytes and looking them up): t1 / t2 = the "byte before"
-// tables of its high / low nibbles, t3 = the "this byte" table of its high
-// nibble, and ef = 0x80 per byte >= 0xE0 (a 3- or 4-byte lead), | 0x40 if >=
-// 0xF0 (a 4-byte lead).  A table has 16 entries: v_perm_b32 looks up the
-// nibble's bits 0-2 in 8 bytes, and a v_bfi by bit 3 (a mask of 0xFF per byte
-// whose nibble is 8-15) picks the half; one perm where a half is constant.
+// equals shifting the bytes and looking them up): t12 = the "byte before"
+// tables of its high and low nibbles, ANDed (they only ever meet ANDed), t3 =
+// the "this byte" table of its high nibble, and ef = 0x80 per byte >= 0xE0
+// (a 3- or 4-byte lead), | 0x40 if >= 0xF0 (a 4-byte lead).  A table has 16
+// entries: v_perm_b32 looks up the nibble's bits 0-2 in 8 bytes, and a blend
+// by bit 3 (a mask of 0xFF per byte whose nibble is 8-15) picks the half; one
+// perm where a half is constant.
 struct Utf8Pre {
-  uint32_t t1, t2, t3, ef;
+  uint32_t t12, t3, ef;
 };
 // Every byte of y replaced by 0xFF if its bit 7 is set, else 0: v_perm_b32's
 // selectors 8-11 replicate the sign bits of bytes 1, 3, 5, 7 of {y, y << 8}.
 __device__ __forceinline__ uint32_t sign_bytes(uint32_t y) { return __builtin_amdgcn_perm(y, y << 8, 0x0B090A08u); }
-__device__ __forceinline__ uint32_t blend(uint32_t m, uint32_t a, uint32_t b) { return (m & a) | (~m & b); }
+// v_bitop3_b32 (gfx950; truth table indexed by s0 s1 s2 as bits 2 1 0): it
+// issues faster than v_bfi_b32 / v_or3_b32 (profiles/r05/sweeps/valu_issue_rates.json)
+__device__ __forceinline__ uint32_t blend(uint32_t m, uint32_t a, uint32_t b) {
+  return __builtin_amdgcn_bitop3_b32(m, a, b, 0xCA);  // (m & a) | (~m & b)
+}
+__device__ __forceinline__ uint32_t or_and(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xA8);  // (a | b) & c
+}
+__device__ __forceinline__ uint32_t and_xor(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x6A);  // (a & b) ^ c
+}
+__device__ __forceinline__ uint32_t or3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0xFE);  // a | b | c
+}
 __device__ __forceinline__ Utf8Pre utf8_pre(uint32_t x) {
   const uint32_t sel_lo = x & 0x07070707u, m_lo = sign_bytes(x << 4);  // bit 3 of each byte
   const uint32_t sel_hi = (x >> 4) & 0x07070707u, m_hi = sign_bytes(x);  // bit 7
@@ -83,10 +97,11 @@ __device__ __forceinline__ Utf8Pre utf8_pre(uint32_t x) {
   // 5 overlong 2, 6 too large 1000 / overlong 4, 7 two continuations
   Utf8Pre p;
   // as the byte before, its high nibble: 0-7 all 0x02 (too long), 8-15 from the second half
-  p.t1 = blend(m_hi, __builtin_amdgcn_perm(0x49150121u, 0x80808080u, sel_hi), 0x02020202u);
+  const uint32_t t1 = blend(m_hi, __builtin_amdgcn_perm(0x49150121u, 0x80808080u, sel_hi), 0x02020202u);
   // as the byte before, its low nibble: all 16 entries
-  p.t2 = blend(m_lo, __builtin_amdgcn_perm(0xCBCBDBCBu, 0xCBCBCBCBu, sel_lo),
-               __builtin_amdgcn_perm(0xCBCBCB8Bu, 0x8383A3E7u, sel_lo));
+  const uint32_t t2 = blend(m_lo, __builtin_amdgcn_perm(0xCBCBDBCBu, 0xCBCBCBCBu, sel_lo),
+                            __builtin_amdgcn_perm(0xCBCBCB8Bu, 0x8383A3E7u, sel_lo));
+  p.t12 = t1 & t2;
   // as this byte, its high nibble: 0-7 and 12-15 all 0x01 (too short)
   p.t3 = blend(m_hi, __builtin_amdgcn_perm(0x01010101u, 0xBABAAEE6u, sel_hi), 0x01010101u);
   // leads: nibble 14 -> 0x80, 15 -> 0xC0 (selectors 6, 7: bytes 2, 3 of the first operand)
@@ -102,12 +117,11 @@ __device__ __forceinline__ Utf8Pre utf8_pre(uint32_t x) {
 // lead asks for.  Nonzero iff some byte breaks strict UTF-8 given its
 // predecessors.
 __device__ __forceinline__ uint32_t utf8_dword_errors(const Utf8Pre& c, const Utf8Pre& p) {
-  const uint32_t t1 = __builtin_amdgcn_alignbyte(c.t1, p.t1, 3);  // byte i: the byte before's tables
-  const uint32_t t2 = __builtin_amdgcn_alignbyte(c.t2, p.t2, 3);
+  const uint32_t t12 = __builtin_amdgcn_alignbyte(c.t12, p.t12, 3);  // byte i: the byte before's tables
   // a continuation is owed from 2 bytes after a 3/4-byte lead and 3 after a 4-byte lead
-  const uint32_t must23 = (__builtin_amdgcn_alignbyte(c.ef, p.ef, 2) | (__builtin_amdgcn_alignbyte(c.ef, p.ef, 1) << 1)) &
-                          0x80808080u;
-  return must23 ^ (t1 & t2 & c.t3);
+  const uint32_t must23 =
+      or_and(__builtin_amdgcn_alignbyte(c.ef, p.ef, 2), __builtin_amdgcn_alignbyte(c.ef, p.ef, 1) << 1, 0x80808080u);
+  return and_xor(t12, c.t3, must23);
 }
 
 // Strict UTF-8 check of one frame's payload bytes [s, fe) by G lanes (lane g
@@ -204,7 +218,7 @@ __device__ __forceinline__ uint64_t utf8_stream_frames(uint32_t R0, uint32_t nf,
       const Utf8Pre q1 = utf8_pre(v.x), q2 = utf8_pre(v.y), q3 = utf8_pre(v.z);
       const uint32_t e0 = utf8_dword_errors(q1, q_last), e1 = utf8_dword_errors(q2, q1),
                      e2 = utf8_dword_errors(q3, q2), e3 = utf8_dword_errors(q4, q3);
-      if (e0 | e1 | e2 | e3) {  // which frames: the first and the last error byte's
+      if (or3(e0, e1, e2) | e3) {  // which frames: the first and the last error byte's
         const uint64_t lo = (uint64_t)e0 | ((uint64_t)e1 << 32), hi = (uint64_t)e2 | ((uint64_t)e3 << 32);
         const int bf = lo ? (int)(__builtin_ctzll(lo) >> 3) : 8 + (int)(__builtin_ctzll(hi) >> 3);
         const int bl = hi ? 15 - (int)(__builtin_clzll(hi) >> 3) : 7 - (int)(__builtin_clzll(lo) >> 3);

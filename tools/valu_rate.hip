@@ -45,6 +45,15 @@ OP_LOOP(k_bitop3, "v_bitop3_b32 %0, %0, %1, %2 bitop3:0xe4")
 OP_LOOP(k_or3, "v_or3_b32 %0, %0, %1, %2")
 OP_LOOP(k_add, "v_add_u32 %0, %0, %1")
 OP_LOOP(k_bfi, "v_bfi_b32 %0, %0, %1, %2")
+OP_LOOP(k_and64, "v_and_b32_e64 %0, %0, %1")
+OP_LOOP(k_lshl64, "v_lshlrev_b32_e64 %0, 3, %0")
+OP_LOOP(k_lshr, "v_lshrrev_b32 %0, 3, %0")
+OP_LOOP(k_lshlor, "v_lshl_or_b32 %0, %0, 4, %1")
+OP_LOOP(k_andor, "v_and_or_b32 %0, %0, %1, %2")
+OP_LOOP(k_xor, "v_xor_b32 %0, %0, %1")
+OP_LOOP(k_bitop3b, "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x6a")
+OP_LOOP(k_alignbit, "v_alignbit_b32 %0, %0, %1, 4")
+OP_LOOP(k_perm2, "v_perm_b32 %0, %1, %0, %2")
 
 int main(int argc, char** argv) {
   const int waves = argc > 1 ? atoi(argv[1]) : 8;
@@ -68,7 +77,10 @@ int main(int argc, char** argv) {
     void (*fn)(unsigned*, unsigned long long*, unsigned, unsigned);
   } ks[] = {{"v_and_b32", k_and},         {"v_lshlrev_b32", k_lshl}, {"v_perm_b32", k_perm},
             {"v_alignbyte_b32", k_alignbyte}, {"v_bitop3_b32", k_bitop3}, {"v_or3_b32", k_or3},
-            {"v_add_u32", k_add},         {"v_bfi_b32", k_bfi}};
+            {"v_add_u32", k_add},         {"v_bfi_b32", k_bfi},   {"v_and_b32_e64", k_and64},
+            {"v_lshlrev_b32_e64", k_lshl64}, {"v_lshrrev_b32", k_lshr}, {"v_lshl_or_b32", k_lshlor},
+            {"v_and_or_b32", k_andor},    {"v_xor_b32", k_xor},   {"v_bitop3_b32_0x6a", k_bitop3b},
+            {"v_alignbit_b32", k_alignbit}, {"v_perm_b32_b", k_perm2}};
   printf("{\"cus\": %d, \"waves_per_simd\": %d, \"ghz_assumed\": %.3f, \"simd_cycles_per_wave_instr\": {", cus, waves,
          ghz);
   for (size_t k = 0; k < sizeof ks / sizeof ks[0]; ++k) {
