@@ -626,7 +626,8 @@ def e2e_host_decode_legs(torch, batch, frames, n, L, reps=3):
     payloads (rudp_encode_varlen_host)."""
     import numpy as np
     out = {}
-    d = batch.unpack_batch(frames, "rudp7", utf8=True)  # first call: slots, pinned staging, warm
+    d = batch.unpack_batch(frames, "rudp7", utf8=True)  # first calls: slots, pinned outputs, warm
+    d = batch.unpack_batch(frames, "rudp7", utf8=True)
     t0 = time.perf_counter()
     for _ in range(reps):
         d = batch.unpack_batch(frames, "rudp7", utf8=True)
@@ -638,7 +639,17 @@ def e2e_host_decode_legs(torch, batch, frames, n, L, reps=3):
                 "decode + strict UTF-8 kernel, D2H of seq/ack/flags/ok/csum/valid on three streams), "
                 "outputs into pinned arrays from torch's caching host allocator"}
     del d
-    # 1M one-character datagrams: packed frames + offsets in pinned host memory
+    out.update(e2e_host_varlen_leg(torch, batch, reps))
+    return out
+
+
+def e2e_host_varlen_leg(torch, batch, reps=3):
+    """1M one-character rudp5 datagrams packed back to back in pinned host memory
+    (a recvmmsg / sendmmsg batch): decode + UTF-8 through rudp_decode_varlen_host
+    and encode from packed payloads through rudp_encode_varlen_host, by the Python
+    entries."""
+    import numpy as np
+    out = {}
     m = 1 << 20
     pin = lambda k, dt: torch.empty(k, dtype=dt, pin_memory=True).numpy()  # noqa: E731
     rng = np.random.default_rng(0x5EED0004)
@@ -654,12 +665,18 @@ def e2e_host_decode_legs(torch, batch, frames, n, L, reps=3):
     enc = batch.pack_batch_varlen((seq, ack, flg), pay, lens, "rudp5", want_csum=True)
     fr, fo, cs = pin(enc.frames.size, torch.uint8), pin(m + 1, torch.int64), pin(m, torch.uint16)
     fr[:], fo[:], cs[:] = enc.frames, enc.frame_off, enc.csum
+    # two untimed calls of each first: the per-packet outputs come from torch's
+    # caching pinned allocator, whose first blocks of a size are fresh hipHostMallocs
+    # (a call allocates its outputs while the previous call's result is alive)
+    for _ in range(2):
+        enc = batch.pack_batch_varlen((seq, ack, flg), pay, lens, "rudp5", want_csum=True, out=fr)
     te = []
     for _ in range(reps):
         t0 = time.perf_counter()
         enc = batch.pack_batch_varlen((seq, ack, flg), pay, lens, "rudp5", want_csum=True, out=fr)
         te.append(time.perf_counter() - t0)
-    dv = batch.unpack_batch_varlen(fr, fo, "rudp5", csum=cs, utf8=True)
+    for _ in range(2):
+        dv = batch.unpack_batch_varlen(fr, fo, "rudp5", csum=cs, utf8=True)
     td = []
     for _ in range(reps):
         t0 = time.perf_counter()
@@ -681,7 +698,7 @@ def e2e_host_decode_legs(torch, batch, frames, n, L, reps=3):
                 "(6 B frames + 8 B offsets + 2 B sideband checksum per datagram up, 10 B of fields down); "
                 "pack_batch_varlen(numpy, out=pinned) = rudp_encode_varlen_host (10 B up, 6 B frame + 8 B "
                 "offset + 2 B checksum down); per-packet outputs from torch's caching pinned allocator "
-                "(decode_reuse_ms: into the previous result's arrays, reuse=); medians of 3 calls"}
+                "(decode_reuse_ms: into the previous result's arrays, reuse=); medians of 3 calls after 2 untimed ones"}
     return out
 
 
