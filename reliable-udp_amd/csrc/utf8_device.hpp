@@ -65,17 +65,14 @@ __device__ __forceinline__ uint32_t group_or(uint32_t bits, uint32_t G) { return
 // bytewise, so looking up the bytes and then shifting the results by one byte
 // equals shifting the bytes and looking them up): t12 = the "byte before"
 // tables of its high and low nibbles, ANDed (they only ever meet ANDed), t3 =
-// the "this byte" table of its high nibble, and ef = 0x80 per byte >= 0xE0
-// (a 3- or 4-byte lead), | 0x40 if >= 0xF0 (a 4-byte lead).  A table has 16
+// the "this byte" table of its high nibble, and ef = 0x40 per byte >= 0xE0
+// (a 3- or 4-byte lead), | 0x80 if >= 0xF0 (a 4-byte lead).  A table has 16
 // entries: v_perm_b32 looks up the nibble's bits 0-2 in 8 bytes, and a blend
 // by bit 3 (a mask of 0xFF per byte whose nibble is 8-15) picks the half; one
 // perm where a half is constant.
 struct Utf8Pre {
   uint32_t t12, t3, ef;
 };
-// Every byte of y replaced by 0xFF if its bit 7 is set, else 0: v_perm_b32's
-// selectors 8-11 replicate the sign bits of bytes 1, 3, 5, 7 of {y, y << 8}.
-__device__ __forceinline__ uint32_t sign_bytes(uint32_t y) { return __builtin_amdgcn_perm(y, y << 8, 0x0B090A08u); }
 // v_bitop3_b32 (gfx950; truth table indexed by s0 s1 s2 as bits 2 1 0): it
 // issues faster than v_bfi_b32 / v_or3_b32 (profiles/r05/sweeps/valu_issue_rates.json)
 __device__ __forceinline__ uint32_t blend(uint32_t m, uint32_t a, uint32_t b) {
@@ -90,23 +87,45 @@ __device__ __forceinline__ uint32_t and_xor(uint32_t a, uint32_t b, uint32_t c) 
 __device__ __forceinline__ uint32_t or3(uint32_t a, uint32_t b, uint32_t c) {
   return __builtin_amdgcn_bitop3_b32(a, b, c, 0xFE);  // a | b | c
 }
-__device__ __forceinline__ Utf8Pre utf8_pre(uint32_t x) {
-  const uint32_t sel_lo = x & 0x07070707u, m_lo = sign_bytes(x << 4);  // bit 3 of each byte
-  const uint32_t sel_hi = (x >> 4) & 0x07070707u, m_hi = sign_bytes(x);  // bit 7
-  // table bits: 0 too short, 1 too long, 2 overlong 3, 3 too large, 4 surrogate,
-  // 5 overlong 2, 6 too large 1000 / overlong 4, 7 two continuations
+// A 64-bit left shift of a dword pair: one v_lshlrev_b64 issues at the cost
+// of one 32-bit left shift (valu_issue_rates.json), so two dwords' shifted
+// copies cost one; the compiler would split it into a shift and a v_alignbit.
+template <int K>
+__device__ __forceinline__ uint64_t shl64(uint64_t x) {
+  uint64_t r;
+  asm("v_lshlrev_b64 %0, %1, %2" : "=v"(r) : "i"(K), "v"(x));
+  return r;
+}
+// The table inputs of dword x given x << 4, x << 12 and x << 8 (only bits 15
+// and 31 of each are read: the sign bits of bytes 1 and 3 that v_perm_b32's
+// selectors 8-11 replicate, so a pair's high dword may carry the low dword's
+// bits below them).
+__device__ __forceinline__ Utf8Pre utf8_pre_from(uint32_t x, uint32_t x4, uint32_t x12, uint32_t x8) {
+  const uint32_t sel_lo = x & 0x07070707u, m_lo = __builtin_amdgcn_perm(x4, x12, 0x0B090A08u);  // bit 3 of each byte
+  const uint32_t sel_hi = (x >> 4) & 0x07070707u, m_hi = __builtin_amdgcn_perm(x, x8, 0x0B090A08u);  // bit 7
+  // table bits (bits 6 and 7 of Keiser & Lemire's tables swapped): 0 too short,
+  // 1 too long, 2 overlong 3, 3 too large, 4 surrogate, 5 overlong 2,
+  // 6 two continuations, 7 too large 1000 / overlong 4
   Utf8Pre p;
   // as the byte before, its high nibble: 0-7 all 0x02 (too long), 8-15 from the second half
-  const uint32_t t1 = blend(m_hi, __builtin_amdgcn_perm(0x49150121u, 0x80808080u, sel_hi), 0x02020202u);
+  const uint32_t t1 = blend(m_hi, __builtin_amdgcn_perm(0x89150121u, 0x40404040u, sel_hi), 0x02020202u);
   // as the byte before, its low nibble: all 16 entries
   const uint32_t t2 = blend(m_lo, __builtin_amdgcn_perm(0xCBCBDBCBu, 0xCBCBCBCBu, sel_lo),
-                            __builtin_amdgcn_perm(0xCBCBCB8Bu, 0x8383A3E7u, sel_lo));
+                            __builtin_amdgcn_perm(0xCBCBCB4Bu, 0x434363E7u, sel_lo));
   p.t12 = t1 & t2;
   // as this byte, its high nibble: 0-7 and 12-15 all 0x01 (too short)
-  p.t3 = blend(m_hi, __builtin_amdgcn_perm(0x01010101u, 0xBABAAEE6u, sel_hi), 0x01010101u);
-  // leads: nibble 14 -> 0x80, 15 -> 0xC0 (selectors 6, 7: bytes 2, 3 of the first operand)
-  p.ef = m_hi & __builtin_amdgcn_perm(0xC0800000u, 0u, sel_hi);
+  p.t3 = blend(m_hi, __builtin_amdgcn_perm(0x01010101u, 0x7A7A6EE6u, sel_hi), 0x01010101u);
+  // leads: nibble 14 -> 0x40, 15 -> 0xC0 (selectors 6, 7: bytes 2, 3 of the first operand)
+  p.ef = m_hi & __builtin_amdgcn_perm(0xC0400000u, 0u, sel_hi);
   return p;
+}
+__device__ __forceinline__ Utf8Pre utf8_pre(uint32_t x) { return utf8_pre_from(x, x << 4, x << 12, x << 8); }
+// Two consecutive dwords (x0 before x1) with one 64-bit shift per amount.
+__device__ __forceinline__ void utf8_pre2(uint32_t x0, uint32_t x1, Utf8Pre& p0, Utf8Pre& p1) {
+  const uint64_t x = ((uint64_t)x1 << 32) | x0;
+  const uint64_t x4 = shl64<4>(x), x12 = shl64<12>(x), x8 = shl64<8>(x);
+  p0 = utf8_pre_from(x0, (uint32_t)x4, (uint32_t)x12, (uint32_t)x8);
+  p1 = utf8_pre_from(x1, (uint32_t)(x4 >> 32), (uint32_t)(x12 >> 32), (uint32_t)(x8 >> 32));
 }
 
 // Error bits of the four bytes of a dword (`c`: utf8_pre of it) given the four
@@ -118,9 +137,10 @@ __device__ __forceinline__ Utf8Pre utf8_pre(uint32_t x) {
 // predecessors.
 __device__ __forceinline__ uint32_t utf8_dword_errors(const Utf8Pre& c, const Utf8Pre& p) {
   const uint32_t t12 = __builtin_amdgcn_alignbyte(c.t12, p.t12, 3);  // byte i: the byte before's tables
-  // a continuation is owed from 2 bytes after a 3/4-byte lead and 3 after a 4-byte lead
+  // a continuation is owed from 2 bytes after a 3/4-byte lead (bit 6 two bytes
+  // back) and 3 after a 4-byte lead (bit 7 three bytes back, moved to bit 6)
   const uint32_t must23 =
-      or_and(__builtin_amdgcn_alignbyte(c.ef, p.ef, 2), __builtin_amdgcn_alignbyte(c.ef, p.ef, 1) << 1, 0x80808080u);
+      or_and(__builtin_amdgcn_alignbyte(c.ef, p.ef, 2), __builtin_amdgcn_alignbyte(c.ef, p.ef, 1) >> 1, 0x40404040u);
   return and_xor(t12, c.t3, must23);
 }
 
@@ -166,8 +186,10 @@ __device__ __forceinline__ uint32_t utf8_check_frame(uint64_t s, uint64_t fe, ui
         have_q = false;
         continue;
       }
-      const Utf8Pre q0 = have_q ? q_last : utf8_pre(prev), q1 = utf8_pre(v.x), q2 = utf8_pre(v.y),
-                    q3 = utf8_pre(v.z), q4 = utf8_pre(v.w);
+      const Utf8Pre q0 = have_q ? q_last : utf8_pre(prev);
+      Utf8Pre q1, q2, q3, q4;
+      utf8_pre2(v.x, v.y, q1, q2);
+      utf8_pre2(v.z, v.w, q3, q4);
       uint32_t err = utf8_dword_errors(q1, q0) | utf8_dword_errors(q2, q1) | utf8_dword_errors(q3, q2) |
                      utf8_dword_errors(q4, q3);
       if (c == c_hi && hi_b >= 16)  // the payload ends with this chunk: nothing may still be expected
@@ -212,10 +234,12 @@ __device__ __forceinline__ uint64_t utf8_stream_frames(uint32_t R0, uint32_t nf,
   auto body = [&](uint32_t c, u32x4 v) {
     // the chunk's last dword is the next one's "bytes before" either way: its
     // inputs once, ahead of the branch (not again inside it)
-    const Utf8Pre q4 = utf8_pre(v.w);
+    Utf8Pre q3, q4;
+    utf8_pre2(v.z, v.w, q3, q4);
     // ASCII with no lead byte just before: nothing to check
     if (high_bits(v) || (prev & (prev << 1) & 0x80808000u)) {
-      const Utf8Pre q1 = utf8_pre(v.x), q2 = utf8_pre(v.y), q3 = utf8_pre(v.z);
+      Utf8Pre q1, q2;
+      utf8_pre2(v.x, v.y, q1, q2);
       const uint32_t e0 = utf8_dword_errors(q1, q_last), e1 = utf8_dword_errors(q2, q1),
                      e2 = utf8_dword_errors(q3, q2), e3 = utf8_dword_errors(q4, q3);
       if (or3(e0, e1, e2) | e3) {  // which frames: the first and the last error byte's

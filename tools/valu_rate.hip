@@ -37,6 +37,31 @@
     }                                                                                      \
   }
 
+#define OP_LOOP64(NAME, ASM)                                                              \
+  __global__ void __launch_bounds__(256) NAME(unsigned* out, unsigned long long* cyc, unsigned iters, unsigned s) { \
+    unsigned long long a0 = threadIdx.x, a1 = a0 * 3u, a2 = a0 * 5u, a3 = a0 * 7u, a4 = a0 * 11u, \
+                       a5 = a0 * 13u, a6 = a0 * 17u, a7 = a0 * 19u;                        \
+    const unsigned long long b = s * 0x0101010101010101ull;                                \
+    const unsigned long long t0 = clock64(), r0 = wall_clock64();                          \
+    for (unsigned i = 0; i < iters; ++i) {                                                 \
+      asm volatile(ASM : "+v"(a0) : "v"(b));                                               \
+      asm volatile(ASM : "+v"(a1) : "v"(b));                                               \
+      asm volatile(ASM : "+v"(a2) : "v"(b));                                               \
+      asm volatile(ASM : "+v"(a3) : "v"(b));                                               \
+      asm volatile(ASM : "+v"(a4) : "v"(b));                                               \
+      asm volatile(ASM : "+v"(a5) : "v"(b));                                               \
+      asm volatile(ASM : "+v"(a6) : "v"(b));                                               \
+      asm volatile(ASM : "+v"(a7) : "v"(b));                                               \
+    }                                                                                      \
+    const unsigned long long t1 = clock64(), r1 = wall_clock64();                          \
+    out[blockIdx.x * blockDim.x + threadIdx.x] = (unsigned)(a0 ^ a1 ^ a2 ^ a3 ^ a4 ^ a5 ^ a6 ^ a7); \
+    if ((threadIdx.x & 63u) == 0) {                                                        \
+      const unsigned w = (blockIdx.x * blockDim.x + threadIdx.x) >> 6;                     \
+      cyc[2 * w] = t1 - t0;                                                                \
+      cyc[2 * w + 1] = r1 - r0;                                                            \
+    }                                                                                      \
+  }
+
 OP_LOOP(k_and, "v_and_b32 %0, %0, %1")
 OP_LOOP(k_lshl, "v_lshlrev_b32 %0, 3, %0")
 OP_LOOP(k_perm, "v_perm_b32 %0, %0, %1, %2")
@@ -54,6 +79,12 @@ OP_LOOP(k_xor, "v_xor_b32 %0, %0, %1")
 OP_LOOP(k_bitop3b, "v_bitop3_b32 %0, %0, %1, %2 bitop3:0x6a")
 OP_LOOP(k_alignbit, "v_alignbit_b32 %0, %0, %1, 4")
 OP_LOOP(k_perm2, "v_perm_b32 %0, %1, %0, %2")
+OP_LOOP64(k_lshl64b, "v_lshlrev_b64 %0, 4, %0")
+OP_LOOP64(k_lshr64b, "v_lshrrev_b64 %0, 4, %0")
+OP_LOOP64(k_lshladd64, "v_lshl_add_u64 %0, %0, 4, %1")
+OP_LOOP(k_pklshl, "v_pk_lshlrev_b16 %0, 4, %0")
+OP_LOOP(k_pkadd, "v_pk_add_u16 %0, %0, %1")
+OP_LOOP(k_bfe, "v_bfe_u32 %0, %0, 4, 3")
 
 int main(int argc, char** argv) {
   const int waves = argc > 1 ? atoi(argv[1]) : 8;
@@ -80,7 +111,9 @@ int main(int argc, char** argv) {
             {"v_add_u32", k_add},         {"v_bfi_b32", k_bfi},   {"v_and_b32_e64", k_and64},
             {"v_lshlrev_b32_e64", k_lshl64}, {"v_lshrrev_b32", k_lshr}, {"v_lshl_or_b32", k_lshlor},
             {"v_and_or_b32", k_andor},    {"v_xor_b32", k_xor},   {"v_bitop3_b32_0x6a", k_bitop3b},
-            {"v_alignbit_b32", k_alignbit}, {"v_perm_b32_b", k_perm2}};
+            {"v_alignbit_b32", k_alignbit}, {"v_perm_b32_b", k_perm2}, {"v_lshlrev_b64", k_lshl64b},
+            {"v_lshrrev_b64", k_lshr64b}, {"v_lshl_add_u64", k_lshladd64}, {"v_pk_lshlrev_b16", k_pklshl},
+            {"v_pk_add_u16", k_pkadd},    {"v_bfe_u32", k_bfe}};
   printf("{\"cus\": %d, \"waves_per_simd\": %d, \"ghz_assumed\": %.3f, \"simd_cycles_per_wave_instr\": {", cus, waves,
          ghz);
   for (size_t k = 0; k < sizeof ks / sizeof ks[0]; ++k) {
