@@ -96,13 +96,20 @@ __device__ __forceinline__ uint64_t shl64(uint64_t x) {
   asm("v_lshlrev_b64 %0, %1, %2" : "=v"(r) : "i"(K), "v"(x));
   return r;
 }
-// The table inputs of dword x given x << 4, x << 12 and x << 8 (only bits 15
-// and 31 of each are read: the sign bits of bytes 1 and 3 that v_perm_b32's
-// selectors 8-11 replicate, so a pair's high dword may carry the low dword's
-// bits below them).
-__device__ __forceinline__ Utf8Pre utf8_pre_from(uint32_t x, uint32_t x4, uint32_t x12, uint32_t x8) {
+template <int K>
+__device__ __forceinline__ uint64_t shr64(uint64_t x) {
+  uint64_t r;
+  asm("v_lshrrev_b64 %0, %1, %2" : "=v"(r) : "i"(K), "v"(x));
+  return r;
+}
+// The table inputs of dword x given x << 4, x << 12, x << 8 and x >> 4 (of the
+// left shifts only bits 15 and 31 are read: the sign bits of bytes 1 and 3
+// that v_perm_b32's selectors 8-11 replicate, so a pair's high dword may carry
+// the low dword's bits below them; of x >> 4 only bits 0-2 of each byte, so a
+// pair's low dword may carry the high dword's bits in bits 28-31).
+__device__ __forceinline__ Utf8Pre utf8_pre_from(uint32_t x, uint32_t x4, uint32_t x12, uint32_t x8, uint32_t xr4) {
   const uint32_t sel_lo = x & 0x07070707u, m_lo = __builtin_amdgcn_perm(x4, x12, 0x0B090A08u);  // bit 3 of each byte
-  const uint32_t sel_hi = (x >> 4) & 0x07070707u, m_hi = __builtin_amdgcn_perm(x, x8, 0x0B090A08u);  // bit 7
+  const uint32_t sel_hi = xr4 & 0x07070707u, m_hi = __builtin_amdgcn_perm(x, x8, 0x0B090A08u);  // bit 7
   // table bits (bits 6 and 7 of Keiser & Lemire's tables swapped): 0 too short,
   // 1 too long, 2 overlong 3, 3 too large, 4 surrogate, 5 overlong 2,
   // 6 two continuations, 7 too large 1000 / overlong 4
@@ -119,13 +126,13 @@ __device__ __forceinline__ Utf8Pre utf8_pre_from(uint32_t x, uint32_t x4, uint32
   p.ef = m_hi & __builtin_amdgcn_perm(0xC0400000u, 0u, sel_hi);
   return p;
 }
-__device__ __forceinline__ Utf8Pre utf8_pre(uint32_t x) { return utf8_pre_from(x, x << 4, x << 12, x << 8); }
+__device__ __forceinline__ Utf8Pre utf8_pre(uint32_t x) { return utf8_pre_from(x, x << 4, x << 12, x << 8, x >> 4); }
 // Two consecutive dwords (x0 before x1) with one 64-bit shift per amount.
 __device__ __forceinline__ void utf8_pre2(uint32_t x0, uint32_t x1, Utf8Pre& p0, Utf8Pre& p1) {
   const uint64_t x = ((uint64_t)x1 << 32) | x0;
-  const uint64_t x4 = shl64<4>(x), x12 = shl64<12>(x), x8 = shl64<8>(x);
-  p0 = utf8_pre_from(x0, (uint32_t)x4, (uint32_t)x12, (uint32_t)x8);
-  p1 = utf8_pre_from(x1, (uint32_t)(x4 >> 32), (uint32_t)(x12 >> 32), (uint32_t)(x8 >> 32));
+  const uint64_t x4 = shl64<4>(x), x12 = shl64<12>(x), x8 = shl64<8>(x), xr4 = shr64<4>(x);
+  p0 = utf8_pre_from(x0, (uint32_t)x4, (uint32_t)x12, (uint32_t)x8, (uint32_t)xr4);
+  p1 = utf8_pre_from(x1, (uint32_t)(x4 >> 32), (uint32_t)(x12 >> 32), (uint32_t)(x8 >> 32), (uint32_t)(xr4 >> 32));
 }
 
 // Error bits of the four bytes of a dword (`c`: utf8_pre of it) given the four
