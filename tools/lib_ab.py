@@ -30,14 +30,14 @@ def main():
     ap.add_argument("--libs", required=True)
     ap.add_argument("--L", default="1472,1024,64")
     ap.add_argument("--reps", type=int, default=11)
-    ap.add_argument("--op", default="encode", choices=["encode", "decode", "varlen", "vdecode", "u8text", "u8ascii"],
+    ap.add_argument("--op", default="encode", choices=["encode", "decode", "varlen", "vdecode", "u8text", "u8ascii", "u8val", "u8valtext"],
                     help="decode: verify-only fixed-length rudp_decode of the encoded frames; varlen: "
                          "rudp_encode_varlen_checked of packed payloads, --L lengths or 'ragged' "
                          "(uniform in [0, 2944]); a 'u' suffix (1472u) times the unchecked rudp_encode_varlen; "
                          "vdecode: rudp_decode_varlen_checked (no status word) of such frames, rudp5 with the "
                          "sideband checksums below 16-B payloads, else rudp7; u8text: rudp_decode_utf8 of "
                          "frames whose payload is valid multi-byte UTF-8 text (1-4 byte characters); u8ascii: "
-                         "rudp_decode_utf8 of the ASCII synthetic frames")
+                         "rudp_decode_utf8 of the ASCII synthetic frames; u8val / u8valtext: rudp_validate_utf8 (the check alone) of the ASCII / text frames")
     args = ap.parse_args()
     _native.lib()  # torch's HIP runtime first
     libs = {}
@@ -66,6 +66,10 @@ def main():
                                                  ctypes.c_uint64, ctypes.c_void_p] + [ctypes.c_void_p] * 6 + \
                                                 [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         h.rudp_decode_varlen_checked.restype = ctypes.c_int
+        if hasattr(h, "rudp_validate_utf8"):
+            h.rudp_validate_utf8.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64,
+                                             ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
+            h.rudp_validate_utf8.restype = ctypes.c_int
         libs[name] = h
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream().cuda_stream
@@ -82,7 +86,7 @@ def main():
         sets = []
         for _ in range(nsets):
             tab, pay = batch.synth_batch(n, L, 0x5EED0004, device=dev)
-            if args.op == "u8text":
+            if args.op in ("u8text", "u8valtext"):
                 text = ("é中😀aßЖ€𝄞" * (L // 8 + 8)).encode()[:L]
                 while True:
                     try:
@@ -104,6 +108,8 @@ def main():
         def call(h, fr, b):
             if args.op == "encode":
                 return h.rudp_encode(ctypes.byref(b), fr.data_ptr(), None, 7, 0, stream)
+            if args.op in ("u8val", "u8valtext"):
+                return h.rudp_validate_utf8(fr.data_ptr(), None, L + 7, n, 7, valid.data_ptr(), 0, stream)
             if args.op in ("u8text", "u8ascii"):
                 return h.rudp_decode_utf8(fr.data_ptr(), None, L + 7, n, None, *[t.data_ptr() for t in outs], None,
                                           valid.data_ptr(), 7, 0, stream)
