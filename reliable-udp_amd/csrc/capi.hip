@@ -585,6 +585,9 @@ int rudp_decode_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_nul
                    reinterpret_cast<uintptr_t>(d_csum_out_or_null) | reinterpret_cast<uintptr_t>(d_valid_or_null)) &
                   3u) == 0) ? 1u : 0u;
   a.xcd = (tuning().tile_xcd && frame_len >= 128u) ? 1u : 0u;
+#if RUDP_TOOLS
+  a.trace = tuning().encode_trace.load();  // decode tile timeline (tools/decode_timeline.py)
+#endif
   a.frames = d_frames;
   a.csum_in = d_csum_in_or_null;
   a.seq = d_seq;

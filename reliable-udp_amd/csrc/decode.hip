@@ -180,6 +180,22 @@ __global__ void __launch_bounds__(kBlock) decode_verify_kernel(DecodeArgs a) {
   }
 }
 
+#if RUDP_TOOLS
+// Diagnostics: a decode tile's timeline (100 MHz wall clock), XCD and CU, as
+// 6 u64 at trace[6 * block]: {start, staged, summed, end, XCC, CU}.  Thread 0
+// records each stamp, so "end" is thread 0's end (outputs of the other waves
+// may still be in flight).
+__device__ __forceinline__ void decode_trace_record(const DecodeArgs& a, uint32_t block, uint64_t t_start,
+                                                    uint64_t t_staged, uint64_t t_summed) {
+  if (!a.trace || threadIdx.x != 0) return;
+  const uint64_t xcc = __builtin_amdgcn_s_getreg((3 << 11) | (0 << 6) | 20);  // XCC_ID[3:0]
+  u32x4* rec = reinterpret_cast<u32x4*>(a.trace + 6ull * block);
+  rec[0] = make_u32x4(t_start, t_staged);
+  rec[1] = make_u32x4(t_summed, (uint64_t)wall_clock64());
+  rec[2] = make_u32x4(xcc, (uint64_t)__smid());
+}
+#endif
+
 // Decode through LDS, verify-only or with payload copy-out: the mirror of the
 // encode tile kernel.  A workgroup owns T = 256/G frames; T is a multiple of
 // 16, so the tile's frames start 16-byte aligned.  Phase 1 streams them into
@@ -206,6 +222,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
   const uint32_t Tv = left < T ? (uint32_t)left : T;
   const uint32_t F = a.F;
   const uint32_t L = F - H;
+#if RUDP_TOOLS
+  const uint64_t t_start = a.trace ? (uint64_t)wall_clock64() : 0ull;
+  uint64_t t_staged = 0, t_summed = 0;
+#endif
   const uint64_t total = a.n * (uint64_t)F;
   const uint64_t base = p0 * (uint64_t)F;  // 16-byte aligned: T % 16 == 0
   const uint32_t nbytes = Tv * F;
@@ -236,6 +256,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
     }
   }
   __syncthreads();
+#if RUDP_TOOLS
+  if (a.trace && tid == 0) t_staged = (uint64_t)wall_clock64();
+#endif
   const uint32_t* dw = reinterpret_cast<const uint32_t*>(lds);
   // the leader's header window, read now so its LDS round trip overlaps the sums
   u32x4 hdr = make_u32x4(0ull, 0ull);
@@ -283,6 +306,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
   }
   sum = group_sum(sum, G);
   if (U8) hib = group_or_rows(hib, G);
+#if RUDP_TOOLS
+  if (a.trace && tid == 0) t_summed = (uint64_t)wall_clock64();
+#endif
   uint32_t u8bad = 0;
   if (U8 && __any((hib & 0x80808080u) != 0)) {  // the byte checks, for waves whose frames hold a high bit
     if (G >= 2u) {
@@ -322,6 +348,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
       finish_packet<H, true>(a, p, sum, seq, ack, flags, H == 5 ? want_cs : inband);
       if (U8) a.valid[p] = u8bad ? 0 : 1;
     }
+#if RUDP_TOOLS
+    decode_trace_record(a, blockIdx.x, t_start, t_staged, t_summed);
+#endif
     return;
   }
   // Outputs staged in LDS after the tile (seq, ack, csum u16 [T]; flags, ok
@@ -381,6 +410,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
       if (U8) a.valid[p0 + i] = s_valid[i];
     }
   }
+#if RUDP_TOOLS
+  decode_trace_record(a, blockIdx.x, t_start, t_staged, t_summed);
+#endif
 }
 
 // Any frame length: one wave per packet, byte-granular.  Frames shorter

@@ -76,6 +76,9 @@ struct DecodeArgs {
   uint32_t align64;         // tile kernel: wave loads/stores start on 64-B sector boundaries
   uint32_t stage_out;       // tile kernel: outputs staged in LDS, written as dwords (pointers 4-B aligned)
   uint32_t xcd;             // tile kernel: XCD-contiguous tile order (xcd_tile)
+#if RUDP_TOOLS
+  uint64_t* trace;          // diagnostics (rudpx_encode_trace): per tile {start, staged, summed, end, XCC, CU}
+#endif
 };
 
 struct SynthArgs {
