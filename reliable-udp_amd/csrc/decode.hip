@@ -226,6 +226,11 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
   const uint64_t t_start = a.trace ? (uint64_t)wall_clock64() : 0ull;
   uint64_t t_staged = 0, t_summed = 0;
 #endif
+  // Issue priority (U8): every phase at 1 but the byte checks of a wave whose
+  // frames hold a high bit, at 0, so the few instructions of the CU's other
+  // tiles' staging and sums are not held behind a long check, which wins
+  // issue by age otherwise; ASCII tiles keep one priority throughout.
+  if (U8) __builtin_amdgcn_s_setprio(1);
   const uint64_t total = a.n * (uint64_t)F;
   const uint64_t base = p0 * (uint64_t)F;  // 16-byte aligned: T % 16 == 0
   const uint32_t nbytes = Tv * F;
@@ -311,6 +316,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
 #endif
   uint32_t u8bad = 0;
   if (U8 && __any((hib & 0x80808080u) != 0)) {  // the byte checks, for waves whose frames hold a high bit
+    __builtin_amdgcn_s_setprio(0);
     if (G >= 2u) {
       // the wave's 64 / G frames are contiguous in the tile: one stream over them, every
       // lane a contiguous run of chunks (utf8_stream_frames), frames ORed over the wave
@@ -337,6 +343,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
                                  [&](uint64_t x) { return x ? dw[(x >> 2) - 1u] : 0u; });
       u8bad = group_or(u8bad, G);
     }
+    __builtin_amdgcn_s_setprio(1);
   }
   if (!a.stage_out) {
     if (g == 0 && q < Tv) {
