@@ -16,6 +16,7 @@ the oracle restatement (oracle/codec_np).
 import ctypes
 
 import numpy as np
+import torch
 import pytest
 
 from conftest import small_lengths, split_by_lengths
@@ -230,6 +231,22 @@ def test_varlen_host_decode_reuse(cuda, golden_varlen):
         assert np.array_equal(getattr(d2, k), v), k
     with pytest.raises(ValueError, match="reuse"):
         batch.unpack_batch_varlen(flat, off, 7, reuse=d1)  # utf8 choice differs
+
+
+def test_host_entry_outputs_are_pinned(cuda, golden_varlen):
+    """The host entries' per-packet outputs are page-locked (the D2H runs at the
+    link's rate): unpack_batch_varlen / pack_batch_varlen / unpack_batch on numpy."""
+    g = golden_varlen
+    flat = g["frames7"]
+    off = np.concatenate([[0], np.cumsum(g["lengths"].astype(np.int64) + 7)]).astype(np.int64)
+    d = batch.unpack_batch_varlen(flat, off, 7, utf8=True)
+    for name in ("seq", "ack", "flags", "ok", "csum", "valid"):
+        assert torch.from_numpy(getattr(d, name)).is_pinned(), name
+    n = len(g["lengths"])
+    enc = batch.pack_batch_varlen((d.seq, d.ack, d.flags), np.zeros(int(g["lengths"].sum()), np.uint8),
+                                  g["lengths"].astype(np.int32), 7, want_csum=True)
+    assert torch.from_numpy(enc.frame_off).is_pinned() and torch.from_numpy(enc.csum).is_pinned()
+    assert enc.frame_off.shape == (n + 1,)
 
 
 def test_varlen_host_decode_empty(cuda):
