@@ -243,8 +243,12 @@ __device__ __forceinline__ uint64_t utf8_stream_frames(uint32_t R0, uint32_t nf,
     // inputs once, ahead of the branch (not again inside it)
     Utf8Pre q3, q4;
     utf8_pre2(v.z, v.w, q3, q4);
-    // ASCII with no lead byte just before: nothing to check
-    if (high_bits(v) || (prev & (prev << 1) & 0x80808000u)) {
+    // ASCII with no lead byte (11xxxxxx) in the three bytes just before:
+    // nothing to check.  One test: the high bits of the chunk, OR bit 6 of
+    // those bytes where bit 7 is set too (a right shift, the cheap one).
+    const uint32_t hb = or_and(or3(v.x, v.y, v.z), v.w, 0x80808080u);
+    const uint32_t lead = __builtin_amdgcn_bitop3_b32(prev >> 1, prev, 0x40404000u, 0x80);  // and3
+    if (hb | lead) {
       Utf8Pre q1, q2;
       utf8_pre2(v.x, v.y, q1, q2);
       const uint32_t e0 = utf8_dword_errors(q1, q_last), e1 = utf8_dword_errors(q2, q1),
