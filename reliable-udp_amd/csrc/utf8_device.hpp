@@ -188,8 +188,10 @@ __device__ __forceinline__ uint32_t utf8_check_frame(uint64_t s, uint64_t fe, ui
         prev = inner ? pd : pd & (uint32_t)byte_mask(lo_b + 4, 4);
       }
       last = v.w;
-      // ASCII, and no lead byte (11xxxxxx) just before: nothing to check
-      if (!high_bits(v) && !(prev & (prev << 1) & 0x80808000u)) {
+      // ASCII, and no lead byte (11xxxxxx) just before: nothing to check (one
+      // test, as in utf8_stream_frames)
+      if (!(or_and(or3(v.x, v.y, v.z), v.w, 0x80808080u) |
+            __builtin_amdgcn_bitop3_b32(prev >> 1, prev, 0x40404000u, 0x80))) {
         have_q = false;
         continue;
       }
