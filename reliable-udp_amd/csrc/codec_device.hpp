@@ -127,6 +127,20 @@ __device__ __forceinline__ uint32_t le16_acc(uint32_t x, uint32_t acc) {
   const rudp_us2 one = {1, 1};
   return __builtin_amdgcn_udot2(__builtin_bit_cast(rudp_us2, x), one, acc, false);
 }
+// Byte sums by position parity with v_dot4_u32_u8: bytes 0 and 2 (even) or 1
+// and 3 (odd) of x added to acc in one instruction.
+__device__ __forceinline__ uint32_t even_bytes_acc(uint32_t x, uint32_t acc) {
+  return __builtin_amdgcn_udot4(x, 0x00010001u, acc, false);
+}
+__device__ __forceinline__ uint32_t odd_bytes_acc(uint32_t x, uint32_t acc) {
+  return __builtin_amdgcn_udot4(x, 0x01000100u, acc, false);
+}
+__device__ __forceinline__ uint32_t even_bytes(u32x4 w) {
+  return even_bytes_acc(w.w, even_bytes_acc(w.z, 0u)) + even_bytes_acc(w.y, even_bytes_acc(w.x, 0u));
+}
+__device__ __forceinline__ uint32_t odd_bytes(u32x4 w) {
+  return odd_bytes_acc(w.w, odd_bytes_acc(w.z, 0u)) + odd_bytes_acc(w.y, odd_bytes_acc(w.x, 0u));
+}
 __device__ __forceinline__ uint32_t le16_sum(u32x4 v) {
   return le16_acc(v.w, le16_acc(v.z, 0u)) + le16_acc(v.y, le16_acc(v.x, 0u));
 }

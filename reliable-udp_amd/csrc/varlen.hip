@@ -260,10 +260,8 @@ __host__ __device__ inline uint32_t vt_pay_off(uint32_t T, uint32_t cap, uint32_
 // of 8.
 // Even/odd byte sums of a 16-B chunk, packed e | o << 16 (each at most 2040).
 __device__ __forceinline__ uint32_t eo_sum(uint64_t lo, uint64_t hi) {
-  constexpr uint64_t M = 0x00FF00FF00FF00FFull;
-  const uint64_t ev = (lo & M) + (hi & M), od = ((lo >> 8) & M) + ((hi >> 8) & M);
-  const uint32_t e2 = (uint32_t)ev + (uint32_t)(ev >> 32), o2 = (uint32_t)od + (uint32_t)(od >> 32);
-  return ((e2 & 0xFFFFu) + (e2 >> 16)) | (((o2 & 0xFFFFu) + (o2 >> 16)) << 16);
+  const u32x4 w = make_u32x4(lo, hi);  // (each at most 8 * 255: packs into 16 bits)
+  return even_bytes(w) | (odd_bytes(w) << 16);
 }
 template <int CTRL>
 __device__ __forceinline__ uint32_t dpp_u32(uint32_t x) {
@@ -1101,11 +1099,8 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
       auto add = [&](u32x4 w, uint32_t c) {
         if (c == c0 || c == c1) w = keep_bytes(w, (int)ps - (int)(c << 4), (int)fe - (int)(c << 4));
         if (U8) hib |= w.x | w.y | w.z | w.w;
-        const uint32_t e = (w.x & 0x00FF00FFu) + (w.y & 0x00FF00FFu) + (w.z & 0x00FF00FFu) + (w.w & 0x00FF00FFu);
-        const uint32_t o = ((w.x >> 8) & 0x00FF00FFu) + ((w.y >> 8) & 0x00FF00FFu) +
-                           ((w.z >> 8) & 0x00FF00FFu) + ((w.w >> 8) & 0x00FF00FFu);
-        even_sum += (e & 0xFFFFu) + (e >> 16);
-        odd_sum += (o & 0xFFFFu) + (o >> 16);
+        even_sum = even_bytes_acc(w.w, even_bytes_acc(w.z, even_bytes_acc(w.y, even_bytes_acc(w.x, even_sum))));
+        odd_sum = odd_bytes_acc(w.w, odd_bytes_acc(w.z, odd_bytes_acc(w.y, odd_bytes_acc(w.x, odd_sum))));
       };
       if (R4) {
         for (uint32_t c = c0 + g2; c <= c1; c += 4u * G2) {
