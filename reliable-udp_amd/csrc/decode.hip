@@ -128,8 +128,7 @@ __global__ void __launch_bounds__(kBlock) decode_verify_kernel(DecodeArgs a) {
   uint32_t even_sum = 0, odd_sum = 0;  // byte sums at even / odd global offsets
   u32x4 first = {0u, 0u, 0u, 0u};
   for (uint32_t i0 = g; i0 < nchunks; i0 += 8u * G) {
-    // per round: at most 32 dwords, so the packed 2 x 16-bit lanes cannot overflow
-    uint32_t even = 0, odd = 0;
+    uint32_t even = 0, odd = 0;  // (v_dot4_u32_u8 byte sums, codec_device.hpp)
     u32x4 v[8];
 #pragma unroll
     for (int u = 0; u < 8; ++u) {
@@ -148,13 +147,12 @@ __global__ void __launch_bounds__(kBlock) decode_verify_kernel(DecodeArgs a) {
           const uint64_t l = lo64(w) & byte_mask(lo, hi), h = hi64(w) & byte_mask(lo - 8, hi - 8);
           w = make_u32x4(l, h);
         }
-        even += (w.x & 0x00FF00FFu) + (w.y & 0x00FF00FFu) + (w.z & 0x00FF00FFu) + (w.w & 0x00FF00FFu);
-        odd += ((w.x >> 8) & 0x00FF00FFu) + ((w.y >> 8) & 0x00FF00FFu) +
-               ((w.z >> 8) & 0x00FF00FFu) + ((w.w >> 8) & 0x00FF00FFu);
+        even += even_bytes(w);
+        odd += odd_bytes(w);
       }
     }
-    even_sum += (even & 0xFFFFu) + (even >> 16);
-    odd_sum += (odd & 0xFFFFu) + (odd >> 16);
+    even_sum += even;
+    odd_sum += odd;
   }
   // frame position parity = parity(x + p): even-offset bytes are high bytes iff p is even
   uint32_t sum = (p & 1u) ? (even_sum + (odd_sum << 8)) : ((even_sum << 8) + odd_sum);

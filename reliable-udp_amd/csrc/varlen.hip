@@ -2042,8 +2042,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
           v &= (uint32_t)byte_mask(lo, hi < 4 ? hi : 4);
         }
         if (U8) hib |= v;
-        ev += (v & 0xFFu) + ((v >> 16) & 0xFFu);
-        od += ((v >> 8) & 0xFFu) + (v >> 24);
+        ev = even_bytes_acc(v, ev);
+        od = odd_bytes_acc(v, od);
       }
     }
     if (U8) {
