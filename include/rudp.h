@@ -36,10 +36,24 @@
  *    set while it enqueues (calls on one stream serialize on the host, as
  *    they do on the GPU) and the next call on that stream reuses it (stream
  *    order keeps them safe).  Nothing is held per host thread, so short-lived
- *    threads leave nothing behind; at most 64 streams per device keep a set
- *    (a 65th takes the least recently used one after a device synchronize),
- *    and a temporary grown past 64 MiB is freed when its call ends.  Under
- *    stream capture the temporaries are allocated and freed inside the graph.
+ *    threads leave nothing behind; at most 64 streams per device keep a set.
+ *    Once a device has 64, every call records an event behind its work as
+ *    it ends, and a call on a 65th stream takes the least recently used set
+ *    that has one, its own stream waiting for that event
+ *    (hipStreamWaitEvent: stream order, no host wait, no device
+ *    synchronize); with none, the call uses temporaries allocated and freed
+ *    in stream order.  A temporary grown past 64 MiB is freed when its call
+ *    ends.  Under stream capture the temporaries are allocated and freed
+ *    inside the graph.  While another thread holds a GLOBAL-mode stream
+ *    capture (hipStreamCaptureModeGlobal), the HIP runtime refuses
+ *    stream-ordered allocations and cross-stream event waits made outside
+ *    the capture: a call that needs either -- one on a stream without a set
+ *    once the device has 64, or whose temporaries must grow -- fails with
+ *    RUDP_EHIP_BASE - hipError and a message naming the capture, having
+ *    enqueued nothing; the capture is unaffected, and the call succeeds if
+ *    repeated after the capture ends.  Calls on streams that already hold
+ *    a large-enough set, and captures in thread-local or relaxed mode, are
+ *    not affected.
  *    Every launch choice is fixed at its
  *    measured default; librudp.so exports exactly the functions below.  (The
  *    diagnostics build of the same sources, librudp_tools.so, adds non-ABI

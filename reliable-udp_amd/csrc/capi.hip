@@ -20,7 +20,7 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
                   const uint16_t* d_csum_in, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
                   uint8_t* d_ok, uint16_t* d_csum_out, uint8_t* d_payload_out, int layout,
                   int device, void* hip_stream, bool checked = false, uint32_t* status_out = nullptr,
-                  uint64_t frames_lim = 0, uint8_t* d_valid = nullptr);
+                  uint64_t frames_lim = 0, uint8_t* d_valid = nullptr, bool fixed_stride = false);
 namespace {
 
 thread_local std::string g_last_error;
@@ -198,6 +198,8 @@ struct Pipeline {
   hipStream_t h2d = nullptr, comp = nullptr, d2h = nullptr;
   hipEvent_t in_ready[kMaxSlots], out_ready[kMaxSlots], slot_free[kMaxSlots];
   void* dbuf[kMaxSlots] = {};
+  uint32_t* d_status = nullptr;  // a call's device status, ORed over its chunks
+  uint32_t* h_status = nullptr;  // (pinned) its copy after the call
   size_t bytes = 0;
   int slots = 0;
 };
@@ -222,6 +224,8 @@ int pipeline_reserve(Pipeline* pp, int slots, size_t bytes) {
       RUDP_HIP(hipEventCreateWithFlags(&pp->out_ready[i], hipEventDisableTiming));
       RUDP_HIP(hipEventCreateWithFlags(&pp->slot_free[i], hipEventDisableTiming));
     }
+    RUDP_HIP(hipMalloc(reinterpret_cast<void**>(&pp->d_status), 256));
+    RUDP_HIP(hipHostMalloc(reinterpret_cast<void**>(&pp->h_status), 256, hipHostMallocDefault));
     pp->init = true;
   }
   if (pp->bytes >= bytes && pp->slots >= slots) return 0;
@@ -391,7 +395,7 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
                   const uint16_t* d_csum_in, uint16_t* d_seq, uint16_t* d_ack, uint8_t* d_flags,
                   uint8_t* d_ok, uint16_t* d_csum_out, uint8_t* d_payload_out, int layout,
                   int device, void* hip_stream, bool checked, uint32_t* status_out, uint64_t frames_lim,
-                  uint8_t* d_valid) {
+                  uint8_t* d_valid, bool fixed_stride) {
   if (layout != RUDP_LAYOUT_RUDP5 && layout != RUDP_LAYOUT_RUDP7)
     return fail(RUDP_EINVAL, "unsupported layout %d (use 5 or 7)", layout);
   if (d_payload_out)
@@ -414,6 +418,19 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
   a.csum_out = d_csum_out;
   a.valid = d_valid;
   a.n = n;
+  if (fixed_stride) {
+    // Fixed-length frames of len_hint bytes that miss the fixed-length decode
+    // tile: no offsets in memory (VarlenArgs::stride), the frames pointer
+    // moved back to a 16-B boundary, every frame inside [0, n F).
+    const uint64_t fmis = reinterpret_cast<uintptr_t>(d_frames) & 15u;
+    a.frames = const_cast<unsigned char*>(d_frames) - fmis;
+    a.frame_off = nullptr;
+    a.fo_base = fmis;
+    a.stride = len_hint;
+    checked = true;
+    frames_lim = fmis + n * (uint64_t)len_hint;
+    status_out = nullptr;
+  }
   // Lanes per frame from the caller's typical frame length (0 = unknown:
   // tiny frames).  Two or more 16-byte chunks per lane, G in [2, 16].
   const uint32_t chunks = len_hint / 16u + 1u;
@@ -481,7 +498,7 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
   const uint64_t S = (uint64_t)tuning().varlen_decode_span_bytes & ~15ull;
   const uint64_t span_cap = (S + 2u * (uint64_t)len_hint + 64u + 15u) & ~15ull;
   const uint64_t nt = S ? frames_lim / S + 1u : 0u;
-  const bool span = checked && tuning().varlen_decode_span && a.glog != kNoVec && !a.small_fpt &&
+  const bool span = checked && d_frame_off && tuning().varlen_decode_span && a.glog != kNoVec && !a.small_fpt &&
                     len_hint >= 256u && S >= 4096u && n < 0xFFFFFFFFull && nt < 0x7FFFFFFFull &&
                     decode_span_fits(span_cap) && (reinterpret_cast<uintptr_t>(d_frames) & 15u) == 0;
   std::optional<ScratchCall> call;
@@ -503,10 +520,67 @@ int decode_varlen(const uint8_t* d_frames, const uint64_t* d_frame_off, uint32_t
   return 0;
 }
 
-// Adds a chunk's base to the frame offsets its encode wrote from 0.
-__global__ void __launch_bounds__(256) add_base_kernel(uint64_t* off, uint64_t n1, uint64_t base) {
+// Fixed-length batches the fixed-length tile does not take (payloads not a
+// multiple of 16 B -- the reference's one-character datagrams,
+// utils/reliableUDP.py:11, :60 -- payloads over 4 KiB, unaligned views): the
+// varlen tile kernels with implicit offsets (VarlenArgs::stride, frame p at
+// p F, payload p at p L): no scan and no offsets in memory, one launch.
+// Payloads under 16 B take the small-frame tile (frames built in an LDS image
+// of the tile's output run), 16 B to 6 KiB the MTU tile, longer ones the
+// per-packet vector kernel.
+int encode_stride(const rudp_batch* in, uint8_t* d_frames, uint16_t* d_csum, int layout, hipStream_t s) {
+  const uint32_t L = in->payload_len, H = (uint32_t)layout;
+  const uint64_t fmis = reinterpret_cast<uintptr_t>(d_frames) & 15u;
+  const uint64_t pmis = reinterpret_cast<uintptr_t>(in->payload) & 15u;
+  VarlenArgs a{};
+  a.payload = in->payload ? in->payload - pmis : nullptr;
+  a.seq_in = in->seq;
+  a.ack_in = in->ack;
+  a.flags_in = in->flags;
+  a.frames = d_frames - fmis;
+  a.frame_off = nullptr;
+  a.csum = d_csum;
+  a.n = in->n;
+  a.fo_base = fmis;
+  a.stride = (uint64_t)L + H;
+  a.po_delta = pmis - fmis;
+  const uint32_t chunks = L / 16u + 1u;
+  uint32_t lg = 0;
+  while (lg < 4 && (4u << lg) <= chunks) ++lg;
+  a.glog = tuning().varlen_vec ? lg : kNoVec;
+  if (tuning().varlen_vec && tuning().varlen_tile) varlen_tile_geometry(L, &a.tile_T, &a.tile_glog, &a.tile_cap);
+  a.align64 = tuning().out_align64 == 1 ? 1u : 0u;
+  {
+    const int early = tuning().encode_early_table;
+    a.early_table = (early == 1 || (early < 0 && L >= 128u)) ? 1u : 0u;
+    const int vhc = tuning().varlen_hchunk;
+    a.vhc = (uint32_t)(vhc < 0 ? 0 : vhc > 2 ? 2 : vhc);
+  }
+  a.early_fo = tuning().varlen_early_fo ? 1u : 0u;
+  a.xcd = tuning().tile_xcd ? 1u : 0u;
+  a.tile_sums = tuning().varlen_tile_sums == 2 ? 2u : 0u;
+  const int small_hint = tuning().varlen_small;
+  if (small_hint > 0 && L < (uint32_t)small_hint && tuning().varlen_vec) {
+    a.small_fpt = L <= 4u ? 4u : 2u;  // (the varlen small-frame tile's measured choice)
+    const uint64_t T = (uint64_t)256u * a.small_fpt;
+    const uint64_t hint = L ? L : 1u;
+    a.small_cap = (uint32_t)((T * hint * 5u / 4u + 256u + 15u) & ~15ull);
+    return launch_encode_stride_small(a, layout, s);
+  }
+  return launch_encode_varlen(a, layout, s);
+}
+
+// Adds a chunk's base to the frame offsets its encode wrote from 0, and ORs
+// the chunk's device status into the call's (the chunks' kernels run in
+// stream order on one stream, so a plain read-modify-write by one thread).
+__global__ void __launch_bounds__(256) add_base_kernel(uint64_t* off, uint64_t n1, uint64_t base, const uint32_t* st,
+                                                      uint32_t* acc) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  if (i < n1) off[i] += base;
+  if (i < n1 && base) off[i] += base;
+  if (i == 0) {
+    const uint32_t v = *st;
+    if (v) *acc |= v;
+  }
 }
 
 }  // namespace rudp
@@ -535,6 +609,11 @@ int rudp_encode(const rudp_batch* in, uint8_t* d_frames, uint16_t* d_csum_or_nul
   if (rc || in->n == 0) return rc;
   DeviceScope dev_scope;
   if ((rc = dev_scope.set(device))) return rc;
+  if (!encode_tile_ok(in->payload_len, in->payload, d_frames)) {
+    rc = encode_stride(in, d_frames, d_csum_or_null, layout, (hipStream_t)hip_stream);
+    if (rc) return hip_fail((hipError_t)rc, "fixed-stride encode launch");
+    return 0;
+  }
   // Batches over `encode_launch_packets` go out as several launches on the
   // stream, each over a contiguous slice (a multiple of every tile size).
   const int lp = tuning().encode_launch_packets;
@@ -549,7 +628,7 @@ int rudp_encode(const rudp_batch* in, uint8_t* d_frames, uint16_t* d_csum_or_nul
     sub.payload = in->payload ? in->payload + p0 * in->payload_len : nullptr;
     EncodeTileArgs a = make_encode_args(&sub, d_frames + p0 * F, d_csum_or_null ? d_csum_or_null + p0 : nullptr,
                                         layout);
-    rc = launch_encode(a, layout, a.T != 0, (hipStream_t)hip_stream);
+    rc = launch_encode(a, layout, (hipStream_t)hip_stream);
     if (rc) return hip_fail((hipError_t)rc, "encode launch");
   }
   return 0;
@@ -577,6 +656,22 @@ int rudp_decode_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_nul
   if (rc || n == 0) return rc;
   DeviceScope dev_scope;
   if ((rc = dev_scope.set(device))) return rc;
+  uint8_t* pay_out = frame_len > (uint32_t)layout ? d_payload_out_or_null : nullptr;
+  if (!decode_vec_ok(frame_len, layout, d_frames, pay_out)) {
+    // Frames the fixed-length tiles do not take (payloads not a multiple of
+    // 16 B -- the reference's 6-9 B datagrams -- short frames, unaligned
+    // views): the varlen decode tiles with implicit offsets, strict UTF-8 in
+    // the same pass; a payload copy-out is one more launch over the frames.
+    rc = decode_varlen(d_frames, nullptr, frame_len, n, d_csum_in_or_null, d_seq, d_ack, d_flags, d_ok,
+                       d_csum_out_or_null, nullptr, layout, device, hip_stream, false, nullptr, 0, d_valid_or_null,
+                       true);
+    if (rc) return rc;
+    if (pay_out) {
+      rc = launch_copy_payloads(d_frames, frame_len, (uint32_t)layout, n, pay_out, (hipStream_t)hip_stream);
+      if (rc) return hip_fail((hipError_t)rc, "payload copy-out launch");
+    }
+    return 0;
+  }
   DecodeArgs a{};
   a.align64 = tuning().out_align64 == 1 ? 1u : 0u;
   a.stage_out = (tuning().decode_stage_out &&
@@ -595,13 +690,11 @@ int rudp_decode_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_nul
   a.flags = d_flags;
   a.ok = d_ok;
   a.csum_out = d_csum_out_or_null;
-  a.payload_out = frame_len > (uint32_t)layout ? d_payload_out_or_null : nullptr;
+  a.payload_out = pay_out;
   a.n = n;
   a.F = frame_len;
-  const bool vec = decode_vec_ok(frame_len, layout, d_frames, a.payload_out);
-  DecodePath path = DecodePath::kBytes;
-  a.glog = 0;
-  if (vec) {
+  DecodePath path;
+  {
     const uint32_t lg = decode_group_log2(frame_len - (uint32_t)layout);
     path = a.payload_out ? DecodePath::kCopy : DecodePath::kVerify;
     // the verify kernel reads the header from the group's first two lanes
@@ -623,8 +716,8 @@ int rudp_decode_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_nul
       a.glog = (uint32_t)forced;
   }
   // The tile kernels check each payload's UTF-8 in the same pass; the other
-  // forms (frames past a 64 KiB tile, copy-out by register windows, any other
-  // shape) leave it to the validation kernels, a second read of the frames.
+  // forms (frames past a 64 KiB tile, copy-out by register windows) leave it
+  // to the validation kernels, a second read of the frames.
   const bool fused = path == DecodePath::kCopyTile || path == DecodePath::kVerifyTile;
   a.valid = fused ? d_valid_or_null : nullptr;
   rc = launch_decode(a, layout, path, (hipStream_t)hip_stream);
@@ -1182,11 +1275,9 @@ int rudp_encode_varlen_host(const rudp_batch* h_in, uint64_t payload_bytes, uint
                                        layout, device, s);
     if (r) return r;
     const uint64_t fbase = pbase + p0 * H;
-    if (fbase) {
-      hipLaunchKernelGGL(add_base_kernel, dim3((uint32_t)((m + 256u) / 256u)), dim3(256), 0, s,
-                         (uint64_t*)(base + o_off), m + 1, fbase);
-      RUDP_HIP(hipGetLastError());
-    }
+    hipLaunchKernelGGL(add_base_kernel, dim3(fbase ? (uint32_t)((m + 256u) / 256u) : 1u), dim3(256), 0, s,
+                       (uint64_t*)(base + o_off), m + 1, fbase, (const uint32_t*)(base + o_st), pp->d_status);
+    RUDP_HIP(hipGetLastError());
     return 0;
   };
   auto d2h = [&](char* base, uint64_t p0, uint64_t m, hipStream_t s) -> int {
@@ -1198,7 +1289,17 @@ int rudp_encode_varlen_host(const rudp_batch* h_in, uint64_t payload_bytes, uint
     if (h_csum_or_null) RUDP_HIP(hipMemcpyAsync(h_csum_or_null + p0, base + o_cs, m * 2, hipMemcpyDeviceToHost, s));
     return 0;
   };
-  return run_pipeline_planned(pp, n, plan, h2d, kern, d2h);
+  // The device's own checks of every chunk (RUDP_ST_*, the checked encode's
+  // status) are read back, not assumed from the host's pre-pass.
+  *pp->h_status = 0;
+  RUDP_HIP(hipMemsetAsync(pp->d_status, 0, sizeof(uint32_t), pp->comp));
+  rc = run_pipeline_planned(pp, n, plan, h2d, kern, d2h);
+  if (rc) return rc;
+  RUDP_HIP(hipMemcpyAsync(pp->h_status, pp->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost, pp->comp));
+  RUDP_HIP(hipStreamSynchronize(pp->comp));
+  if (*pp->h_status)
+    return fail(RUDP_EINVAL, "rudp_encode_varlen_host: the device rejected the batch (status 0x%x)", *pp->h_status);
+  return 0;
 }
 
 // Packed frames in host memory (a recvmmsg batch): chunks of consecutive
@@ -1256,9 +1357,19 @@ int rudp_decode_varlen_host(const uint8_t* h_frames, uint64_t frames_bytes, cons
         a1 = b1 > b0 ? b1 : b0;
         return (int64_t)m;
       }
-      if (m == 1)
+      if (m == 1) {
+        // A frame the checked rule rejects (its offsets out of order, or past
+        // the buffer) is decoded from no bytes at all: nothing is staged, and
+        // the device marks it RUDP_OK_BAD_OFFSETS as rudp_decode_varlen_utf8
+        // would.  Only a valid frame larger than a slot is refused.
+        const uint64_t f0 = h_frame_off[p0], f1 = h_frame_off[p0 + 1];
+        if (f0 > f1 || f1 > frames_bytes) {
+          a0 = a1 = 0;
+          return 1;
+        }
         return fail(RUDP_ENOTSUP, "rudp_decode_varlen_host: frame %llu spans %llu bytes, over the %zu-byte staging slot",
                     (unsigned long long)p0, (unsigned long long)(b1 - b0), (size_t)bmax);
+      }
       m /= 2;
     }
   };

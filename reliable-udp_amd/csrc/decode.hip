@@ -14,7 +14,9 @@
 // through LDS.  With payload_out, the tile's payloads stream out as one
 // contiguous run.  Every frame byte leaves HBM once.  Frames too large for an
 // LDS tile take decode_verify_kernel (aligned chunks, parity-weighted sums) or
-// decode_vec_kernel (register windows); any other shape the byte kernel.
+// decode_vec_kernel (register windows).  Any other shape (payloads not a
+// multiple of 16 B, unaligned views) decodes through the varlen tiles with
+// implicit offsets (capi.hip rudp_decode_utf8, VarlenArgs::stride).
 #include "codec_device.hpp"
 #include "internal.hpp"
 #include "utf8_device.hpp"
@@ -420,48 +422,6 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
 #endif
 }
 
-// Any frame length: one wave per packet, byte-granular.  Frames shorter
-// than the header report RUDP_OK_SHORT with the fields that are present,
-// truncated the way utils/packet.py:31 slices a short bit string.
-template <int H>
-__global__ void __launch_bounds__(kBlock) decode_bytes_kernel(DecodeArgs a) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t p = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-  if (p >= a.n) return;  // wave-uniform
-  const uint32_t F = a.F;
-  const unsigned char* fr = a.frames + p * (uint64_t)F;
-  if (F < (uint32_t)H) {
-    if (lane == 0) {
-      uint32_t b[7] = {0, 0, 0, 0, 0, 0, 0};
-      for (uint32_t i = 0; i < F; ++i) b[i] = fr[i];
-      // A field cut short keeps only its present bytes (bit-string slice).
-      const uint32_t seq = F >= 2 ? (b[0] << 8) | b[1] : b[0];
-      const uint32_t ack = F >= 4 ? (b[2] << 8) | b[3] : b[2];
-      a.seq[p] = (uint16_t)seq;
-      a.ack[p] = (uint16_t)ack;
-      a.flags[p] = (uint8_t)b[4];
-      a.ok[p] = 2;
-      if (a.csum_out) a.csum_out[p] = 0;
-    }
-    return;
-  }
-  const uint32_t L = F - H;
-  uint32_t sum = 0;
-  for (uint32_t j = lane; j < L; j += 64) {
-    const uint32_t b = fr[H + j];
-    sum += (j & 1u) ? (b << 8) : b;
-    if (a.payload_out) a.payload_out[p * (uint64_t)L + j] = (unsigned char)b;
-  }
-  for (int m = 32; m > 0; m >>= 1) sum += __shfl_xor(sum, m, 64);
-  if (lane == 0) {
-    const uint32_t seq = ((uint32_t)fr[0] << 8) | fr[1];
-    const uint32_t ack = ((uint32_t)fr[2] << 8) | fr[3];
-    const uint32_t flags = fr[4];
-    const uint32_t inband = (H == 7) ? (((uint32_t)fr[5] << 8) | fr[6]) : 0u;
-    finish_packet<H>(a, p, sum, seq, ack, flags, inband);
-  }
-}
-
 template <int H, bool COPY, bool U8>
 static int launch_decode_tile(const DecodeArgs& args, size_t lds, uint64_t blocks, hipStream_t stream) {
   if (lds > 65536) {
@@ -481,7 +441,7 @@ static int launch_decode_tile_u8(const DecodeArgs& args, size_t lds, uint64_t bl
 
 int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream_t stream) {
   if (args.n == 0) return 0;
-  if (path != DecodePath::kBytes) {
+  {
     const uint32_t per_block = kBlock >> args.glog;
     const uint64_t blocks = (args.n + per_block - 1) / per_block;
     if (path == DecodePath::kCopyTile || path == DecodePath::kVerifyTile) {
@@ -513,12 +473,6 @@ int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream
     } else {
       hipLaunchKernelGGL(decode_vec_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
     }
-  } else {
-    const uint64_t blocks = (args.n + (kBlock / 64) - 1) / (kBlock / 64);
-    if (layout == 7)
-      hipLaunchKernelGGL(decode_bytes_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
-    else
-      hipLaunchKernelGGL(decode_bytes_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
   }
   return (int)hipGetLastError();
 }

@@ -143,7 +143,9 @@ static ScratchSet* lock_set(int device, hipStream_t stream) {
         std::sort(order.begin(), order.end(),
                   [](const ScratchSet* a, const ScratchSet* b) { return a->last_use < b->last_use; });
         for (ScratchSet* s : order) {
-          if (!s->done_valid || !s->mu.try_lock()) continue;
+          // (done_valid is read only under the set's own lock, which its
+          // writer, ~ScratchCall, holds)
+          if (!s->mu.try_lock()) continue;
           // the new stream waits, in stream order, for everything enqueued on
           // these buffers (no host wait, no query: neither is allowed while
           // another thread holds a global-mode graph capture)

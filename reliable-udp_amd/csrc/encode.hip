@@ -5,7 +5,7 @@
 //   (:43-57) -> set_payload (:60-65) -> to_byte (:76-81)
 // plus the build-defined RFC 1071 checksum.
 //
-// Fast kernel (payload_len % 16 == 0): one workgroup per TILE of T packets
+// Payloads that are a multiple of 16 B (and 16-B aligned buffers): one workgroup per TILE of T packets
 // (a power of two, 4..256; 16 at L >= 512).  The frame stride L+H is odd, so
 // for T < 16 a tile's output range starts and ends mid-chunk; the two shared
 // chunks are written bytewise by their owners.
@@ -321,33 +321,6 @@ __global__ void __launch_bounds__(BLOCK) encode_tile_kernel(EncodeTileArgs a) {
 #endif
 }
 
-// Any payload length / alignment: one wave per packet, byte-granular.
-// Same arithmetic as the tile kernel; used for reference-sized frames
-// (1-char payloads, utils/reliableUDP.py:11) and ragged shapes.
-template <int H>
-__global__ void __launch_bounds__(kBlock) encode_bytes_kernel(EncodeTileArgs a) {
-  const uint32_t lane = threadIdx.x & 63u;
-  const uint64_t p = (uint64_t)blockIdx.x * (kBlock / 64) + (threadIdx.x >> 6);
-  if (p >= a.n) return;  // wave-uniform
-  const uint32_t L = a.L;
-  const uint64_t F = (uint64_t)L + H;
-  const unsigned char* src = a.payload + p * (uint64_t)L;
-  unsigned char* dst = a.frames + p * F;
-  uint32_t sum = 0;
-  for (uint32_t j = lane; j < L; j += 64) {
-    const uint32_t b = src[j];
-    sum += (j & 1u) ? (b << 8) : b;
-    dst[H + j] = (unsigned char)b;
-  }
-  for (int m = 32; m > 0; m >>= 1) sum += __shfl_xor(sum, m, 64);
-  const uint32_t s = a.seq[p], k = a.ack[p], f = a.flags[p];
-  const uint32_t c = packet_csum(sum, s, k, f);
-  const uint64_t h = pack_header<H>(s, k, f, c);
-  if (lane < (uint32_t)H) dst[lane] = (unsigned char)(h >> (8 * lane));
-  if (lane == 0 && a.csum) a.csum[p] = (uint16_t)c;
-}
-
-
 template <int H, bool NTL, bool NTS, int P1, int BLOCK = kBlock, bool DMA = false>
 int launch_tile(const EncodeTileArgs& args, hipStream_t stream) {
   const uint64_t blocks = args.num_tiles;
@@ -424,16 +397,9 @@ int launch_tile_policy(const EncodeTileArgs& args, hipStream_t stream) {
 #endif
 
 
-int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStream_t stream) {
+int launch_encode(const EncodeTileArgs& args, int layout, hipStream_t stream) {
   if (args.n == 0) return 0;
-  if (tile_path)
-    return layout == 7 ? launch_tile_policy<7>(args, stream) : launch_tile_policy<5>(args, stream);
-  const uint64_t blocks = (args.n + (kBlock / 64) - 1) / (kBlock / 64);
-  if (layout == 7)
-    hipLaunchKernelGGL(encode_bytes_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
-  else
-    hipLaunchKernelGGL(encode_bytes_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
-  return (int)hipGetLastError();
+  return layout == 7 ? launch_tile_policy<7>(args, stream) : launch_tile_policy<5>(args, stream);
 }
 
 }  // namespace rudp

@@ -171,6 +171,15 @@ struct VarlenArgs {
   uint32_t map_bal;               // encode tile: chunk map built by output units, not by frames
   uint32_t dec_nt;                // decode tile: threads per workgroup (256, or 128: two-wave tiles)
   uint32_t dec_r4;                // decode tile: payload chunks read four at a time
+  // Fixed-stride batches through these kernels (frame_off == null): frame p
+  // starts at fo_base + p * stride, and a packed payload at that offset - p * H
+  // + po_delta (mod 2^64); len[] is stride - H for every packet.  The launcher
+  // moves `frames` / `payload` back to a 16-B boundary and puts the distance
+  // into fo_base / po_delta, so any caller alignment takes the tile kernels.
+  // No offsets are read or written.
+  uint64_t fo_base;
+  uint64_t stride;
+  uint64_t po_delta;
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -206,7 +215,7 @@ constexpr uint32_t kTileMaxPayload = 4096;
 // keeps every per-packet word sum exact in 32 bits (32768 words x 0xFFFF).
 constexpr uint32_t kMaxPayload = 65535;
 
-enum class DecodePath { kBytes, kCopy, kCopyTile, kVerify, kVerifyTile };
+enum class DecodePath { kCopy, kCopyTile, kVerify, kVerifyTile };
 
 // Launch choices, each at its measured default.  In librudp.so they are
 // compile-time constants.  In the tools build each is an atomic int set by
@@ -401,7 +410,7 @@ inline const Tuning& tuning() {
 void encode_tile_geometry(uint32_t L, uint32_t* T, uint32_t* glog);
 uint32_t decode_group_log2(uint32_t L);
 
-int launch_encode(const EncodeTileArgs& args, int layout, bool tile_path, hipStream_t stream);
+int launch_encode(const EncodeTileArgs& args, int layout, hipStream_t stream);
 int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream_t stream);
 int launch_synth(const SynthArgs& args, hipStream_t stream);
 void varlen_tile_geometry(uint32_t len_hint, uint32_t* T, uint32_t* glog, uint32_t* cap);
@@ -479,6 +488,14 @@ void scan_block_bases(uint64_t* sums, uint64_t nb, uint64_t* d_frame_off, uint64
 // two passes, then one kernel per tile of kBlock * fpt packets that writes the
 // tile's offsets and assembles its frames in LDS.
 int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int layout, hipStream_t stream);
+// The same tile kernel for a fixed-stride batch (args.frame_off == null): every
+// tile's base is known, so it is one launch and no scan (varlen.hip).
+int launch_encode_stride_small(const VarlenArgs& args, int layout, hipStream_t stream);
+// Payload copy-out of fixed-stride frames that miss the fixed-length decode
+// tile (payloads not a multiple of 16 B, unaligned views): payload i =
+// frames[i F + H, (i + 1) F) to out[i L, (i + 1) L), L = F - H (varlen.hip).
+int launch_copy_payloads(const unsigned char* frames, uint32_t F, uint32_t H, uint64_t n, unsigned char* out,
+                         hipStream_t stream);
 // Span starts for the byte-tiled varlen encode: rec[k] (k = 0 .. count) holds
 // p, the first packet whose packed payload starts at or after k * bytes, and
 // fo = frame_off[p], so a tile has its packet range and frame run from two

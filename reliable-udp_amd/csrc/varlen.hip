@@ -35,6 +35,21 @@ constexpr uint32_t kVarLanes = 8;
 // Uniform (a kernel argument), so this is one scalar load per wave.
 __device__ __forceinline__ bool call_failed(const uint32_t* status) { return status && *status; }
 
+// A batch's offsets: the frame_off array, or a fixed stride (frame_off null;
+// VarlenArgs::stride).  Uniform per launch, so each is one scalar branch.
+__device__ __forceinline__ uint64_t fo_at(const VarlenArgs& a, uint64_t p) {
+  return a.frame_off ? a.frame_off[p] : a.fo_base + p * a.stride;
+}
+template <int H>
+__device__ __forceinline__ uint32_t len_at(const VarlenArgs& a, uint64_t p) {
+  return a.frame_off ? a.len[p] : (uint32_t)a.stride - (uint32_t)H;
+}
+// Payload offset of packet p, whose frame starts at fo.
+template <int H>
+__device__ __forceinline__ uint64_t po_at(const VarlenArgs& a, uint64_t p, uint64_t fo) {
+  return a.payload_off ? a.payload_off[p] : fo - p * (uint64_t)H + a.po_delta;
+}
+
 #if RUDP_TOOLS
 struct FrameLen {
   const uint32_t* len;
@@ -52,9 +67,9 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_kernel(VarlenArgs a) {
   uint32_t sum = 0;
   uint64_t fo = 0;
   if (valid) {
-    const uint32_t L = a.len[p];
-    fo = a.frame_off[p];
-    const uint64_t po = a.payload_off ? a.payload_off[p] : fo - p * (uint64_t)H;
+    const uint32_t L = len_at<H>(a, p);
+    fo = fo_at(a, p);
+    const uint64_t po = po_at<H>(a, p, fo);
     for (uint32_t j = g; j < L; j += kVarLanes) {
       const uint32_t b = a.payload[po + j];
       sum += (j & 1u) ? (b << 8) : b;  // LE u16 word sum (payload at an odd frame offset)
@@ -131,9 +146,9 @@ template <int H>
 __device__ __forceinline__ void encode_varlen_packet(const VarlenArgs& a, uint64_t p, bool valid, uint32_t g,
                                                      uint32_t glog, uint64_t fo_in = ~0ull) {
   const uint32_t G = 1u << glog;
-  const uint32_t L = valid ? a.len[p] : 0u;
-  const uint64_t fo = valid ? (fo_in != ~0ull ? fo_in : a.frame_off[p]) : 0;
-  const uint64_t po = valid ? (a.payload_off ? a.payload_off[p] : fo - p * (uint64_t)H) : 0;
+  const uint32_t L = valid ? len_at<H>(a, p) : 0u;
+  const uint64_t fo = valid ? (fo_in != ~0ull ? fo_in : fo_at(a, p)) : 0;
+  const uint64_t po = valid ? po_at<H>(a, p, fo) : 0;
   const uint64_t pend = po + L;
   const uint32_t F = L + H;
   const uint64_t x_lo = fo >> 4;
@@ -351,8 +366,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     p0 = (uint64_t)(a.xcd ? xcd_tile(b, ptiles) : b) * a.tile_T;
     T = a.tile_T;
     Tv = Tall = a.n - p0 < a.tile_T ? (uint32_t)(a.n - p0) : a.tile_T;
-    fo0 = a.frame_off[p0];
-    fo_end = a.frame_off[p0 + Tv];
+    fo0 = fo_at(a, p0);
+    fo_end = fo_at(a, p0 + Tv);
     glog = a.tile_glog;
   }
   const uint32_t G = 1u << glog, q = tid >> glog, g = tid & (G - 1u);
@@ -365,8 +380,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     t_flags = a.flags_in[p0 + q];
   }
   if (call_failed(a.status)) return;
-  const uint64_t po0 = fo0 - p0 * (uint64_t)H;
-  const uint64_t po_end = fo_end - (p0 + Tv) * (uint64_t)H;
+  const uint64_t po0 = fo0 - p0 * (uint64_t)H + a.po_delta;
+  const uint64_t po_end = fo_end - (p0 + Tv) * (uint64_t)H + a.po_delta;
   const uint64_t A = po0 & ~15ull;
   const uint64_t run = ((po_end + 15u) & ~15ull) - A;
   if (Tall > T || run > cap) {  // uniform over the workgroup
@@ -382,8 +397,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     // payload stream so their round trip overlaps it (early_fo).
     uint32_t fo_r0 = 0, fo_r1 = 0;
     if (a.early_fo) {
-      if (tid <= Tv) fo_r0 = (uint32_t)(a.frame_off[p0 + tid] - fo0);
-      if (tid + kBlock <= Tv) fo_r1 = (uint32_t)(a.frame_off[p0 + tid + kBlock] - fo0);
+      if (tid <= Tv) fo_r0 = (uint32_t)(fo_at(a, p0 + tid) - fo0);
+      if (tid + kBlock <= Tv) fo_r1 = (uint32_t)(fo_at(a, p0 + tid + kBlock) - fo0);
     }
     const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + A);
     u32x4* dst = reinterpret_cast<u32x4*>(lds_pay + kVTGuard);
@@ -413,7 +428,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
       if (tid <= Tv) lds_fo[tid] = fo_r0;
       if (tid + kBlock <= Tv) lds_fo[tid + kBlock] = fo_r1;
     } else {
-      for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = (uint32_t)(a.frame_off[p0 + i] - fo0);
+      for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = (uint32_t)(fo_at(a, p0 + i) - fo0);
     }
   }
   __syncthreads();
@@ -718,7 +733,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
 // Byte limit of a decode's frames: the caller's buffer size for checked
 // calls, else (unchecked callers) the last offset.
 __device__ __forceinline__ uint64_t frames_limit(const VarlenArgs& a) {
-  return a.lim_checked ? a.frames_lim : a.frame_off[a.n];
+  return a.lim_checked ? a.frames_lim : fo_at(a, a.n);
 }
 
 // A frame whose offsets are invalid: no byte of it is read.
@@ -744,8 +759,8 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_kernel(VarlenArgs a) {
   uint64_t fo = 0;
   bool bad = false;
   if (valid) {
-    fo = a.frame_off[p];
-    const uint64_t fe = a.frame_off[p + 1];
+    fo = fo_at(a, p);
+    const uint64_t fe = fo_at(a, p + 1);
     bad = fo > fe || fe > frames_limit(a);
     F = bad ? 0u : fe - fo;
     for (uint64_t j = (uint64_t)H + g; j < F; j += kVarLanes) {
@@ -844,8 +859,8 @@ __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_
   const uint32_t tid = threadIdx.x;
   const uint32_t G = 1u << glog;
   const uint64_t total = frames_limit(a);
-  uint64_t fstart = valid ? a.frame_off[p] : 0;
-  uint64_t fend = valid ? a.frame_off[p + 1] : 0;
+  uint64_t fstart = valid ? fo_at(a, p) : 0;
+  uint64_t fend = valid ? fo_at(a, p + 1) : 0;
   const bool bad = valid && (fstart > fend || fend > total);
   if (bad) fstart = fend = 0;  // nothing of it is read
   const uint64_t c_lo = fstart >> 4;
@@ -969,7 +984,7 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
-  const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
+  const uint64_t fo0 = fo_at(a, p0), fo_end = fo_at(a, p0 + Tv);
   // Block sums for every tile (tile_sums 2), or (1) for a tile of uneven frames:
   // every wave reads the tile's T + 1 <= 64 offsets itself (the same lines as
   // wave 0's early ones), so the choice is the same in all four without a
@@ -984,7 +999,7 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   const bool adapt = RUDP_TOOLS && a.tile_sums == 1u && Tv == 16u;  // (16-frame tiles: MTU-scale hints)
   uint32_t len_adapt = 0;
   if (adapt && (tid & 63u) < 16u) {
-    const uint64_t d = a.frame_off[p0 + (tid & 63u) + 1u] - a.frame_off[p0 + (tid & 63u)];
+    const uint64_t d = fo_at(a, p0 + (tid & 63u) + 1u) - fo_at(a, p0 + (tid & 63u));
     len_adapt = d < 0xFFFFFFFFull ? (uint32_t)d : 0xFFFFFFFFu;
   }
   const uint64_t total = frames_limit(a);
@@ -1006,7 +1021,7 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   auto rel = [&](uint64_t o) { return o - A <= span_end ? (uint32_t)(o - A) : 0xFFFFFFFFu; };
   {
     // T = 256 / G <= 128 frames: one offset per lane, loaded before the run (early_fo)
-    const uint32_t fo_r = a.early_fo && tid <= Tv ? rel(a.frame_off[p0 + tid]) : 0u;
+    const uint32_t fo_r = a.early_fo && tid <= Tv ? rel(fo_at(a, p0 + tid)) : 0u;
     const uint32_t nvec = (uint32_t)(run >> 4);
     u32x4* dst = reinterpret_cast<u32x4*>(img);
     constexpr uint32_t P = 8;
@@ -1052,7 +1067,7 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
     if (a.early_fo) {
       if (tid <= Tv) lds_fo[tid] = fo_r;
     } else {
-      for (uint32_t i = tid; i <= Tv; i += NT) lds_fo[i] = rel(a.frame_off[p0 + i]);
+      for (uint32_t i = tid; i <= Tv; i += NT) lds_fo[i] = rel(fo_at(a, p0 + i));
     }
   }
   __syncthreads();
@@ -1645,13 +1660,15 @@ __host__ __device__ inline uint32_t small_out_cap(uint32_t T, uint32_t cap, uint
 // is 0 and its payload run is the whole payload buffer, whose size the call
 // states, so the run loads before the scan; the block scan's total then gives
 // frame_off[n] and the checks pass 1 would have made.  One launch per call.
+// FIXED (a fixed-stride batch, frame_off null): tile t's base is fo_at(t T),
+// every length is stride - H; no scan, no offsets written, one launch.
 constexpr uint64_t kSmallFusedTiles = 2048;
-enum SmallMode { kSmallBases = 0, kSmallFused = 1, kSmallSingle = 2 };
+enum SmallMode { kSmallBases = 0, kSmallFused = 1, kSmallSingle = 2, kSmallFixed = 3 };
 
 template <int H, uint32_t FPT, int MODE>
 __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs a, const uint64_t* sums,
                                                                      uint64_t nb, ScanCheck chk) {
-  constexpr bool FUSED = MODE == kSmallFused, SINGLE = MODE == kSmallSingle;
+  constexpr bool FUSED = MODE == kSmallFused, SINGLE = MODE == kSmallSingle, FIXED = MODE == kSmallFixed;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   constexpr uint32_t T = kBlock * FPT;
   const uint32_t tid = threadIdx.x;
@@ -1681,7 +1698,7 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
     const uint32_t q = j * kBlock + tid;
     lv[j] = sq[j] = ak[j] = fl[j] = 0;
     if (q < Tv) {
-      lv[j] = a.len[p0 + q];
+      lv[j] = FIXED ? (uint32_t)a.stride - (uint32_t)H : a.len[p0 + q];
       sq[j] = a.seq_in[p0 + q];
       ak[j] = a.ack_in[p0 + q];
       fl[j] = a.flags_in[p0 + q];
@@ -1731,6 +1748,9 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
   } else if (SINGLE) {
     fo0 = 0;
     fo_end = 0;  // from the scan below
+  } else if (FIXED) {
+    fo0 = fo_at(a, p0);
+    fo_end = fo_at(a, p0 + Tv);
   } else {
     fo0 = sums[tile];
     fo_end = p0 + T < a.n ? sums[tile + 1] : a.frame_off[a.n];
@@ -1739,8 +1759,8 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
 #if RUDP_TOOLS
   const uint64_t t_base = a.trace ? (uint64_t)wall_clock64() : 0ull;
 #endif
-  const uint64_t po0 = fo0 - p0 * (uint64_t)H;
-  const uint64_t po_end = SINGLE ? chk.payload_bytes : fo_end - (p0 + Tv) * (uint64_t)H;
+  const uint64_t po0 = fo0 - p0 * (uint64_t)H + a.po_delta;
+  const uint64_t po_end = SINGLE ? chk.payload_bytes : fo_end - (p0 + Tv) * (uint64_t)H + a.po_delta;
   const uint64_t A = po0 & ~15ull, OA = fo0 & ~15ull;
   const uint64_t prun = ((po_end + 15u) & ~15ull) - A;
   uint64_t orun = ((fo_end + 15u) & ~15ull) - OA;
@@ -1782,7 +1802,7 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
       mine += q < Tv ? s_len[q] + (uint32_t)H : 0u;
     }
     uint32_t total = 0;  // (at most 256 * FPT * 65542)
-    uint32_t run = block_exclusive_scan32(mine, &total, s_wave32);
+    uint32_t run = FIXED ? tid * FPT * (uint32_t)a.stride : block_exclusive_scan32(mine, &total, s_wave32);
 #pragma unroll
     for (uint32_t i = 0; i < FPT; ++i) {
       const uint32_t q = tid * FPT + i;
@@ -1808,7 +1828,7 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
   }
   __syncthreads();
 #pragma unroll
-  for (uint32_t j = 0; j < FPT; ++j) {
+  for (uint32_t j = 0; j < FPT && !FIXED; ++j) {
     const uint32_t q = j * kBlock + tid;
     if (q < Tv) const_cast<uint64_t*>(a.frame_off)[p0 + q] = fo0 + s_off[q];
   }
@@ -1918,6 +1938,111 @@ int launch_small_any(const VarlenArgs& args, const uint64_t* sums, uint64_t nb, 
                              : launch_small_fpt<H, 4>(args, sums, nb, chk, fused, stream);
 }
 
+template <int H, uint32_t FPT>
+int launch_stride_small_fpt(const VarlenArgs& args, hipStream_t stream) {
+  constexpr uint32_t T = kBlock * FPT;
+  const size_t lds = small_lds_off_out(T, args.small_cap) + small_out_cap(T, args.small_cap, H) + 32u;
+  const void* fn = reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT, kSmallFixed>);
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  const uint64_t nb = (args.n + T - 1) / T;
+  hipLaunchKernelGGL((encode_varlen_small_kernel<H, FPT, kSmallFixed>), dim3((uint32_t)nb), dim3(kBlock), lds, stream,
+                     args, nullptr, nb, ScanCheck{});
+  return (int)hipGetLastError();
+}
+
+int launch_encode_stride_small(const VarlenArgs& args, int layout, hipStream_t stream) {
+  if (args.n == 0) return 0;
+  if (args.small_fpt == 2)
+    return layout == 7 ? launch_stride_small_fpt<7, 2>(args, stream) : launch_stride_small_fpt<5, 2>(args, stream);
+  return layout == 7 ? launch_stride_small_fpt<7, 4>(args, stream) : launch_stride_small_fpt<5, 4>(args, stream);
+}
+
+// Copy-out of fixed-stride frames that miss the fixed-length decode tile
+// (launch_copy_payloads): a workgroup stages the run of its T frames in LDS
+// from the aligned-down start (bytes before the caller's first frame are
+// staged, never written) and writes the run [p0 L, (p0 + T) L) of `out` as
+// aligned 16-B chunks, each gathered from the payloads it covers -- one
+// byte-shifted LDS window per payload, one or two per chunk at L >= 16 -- the
+// two chunks shared with the neighbour tiles bytewise.
+constexpr uint32_t kCopyRun = 32768;  // frame bytes a tile stages (at least one frame)
+__global__ void __launch_bounds__(kBlock) copy_payloads_kernel(const unsigned char* frames, uint64_t fo_base,
+                                                                uint32_t F, uint32_t H, uint64_t n, uint32_t T,
+                                                                unsigned char* out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
+  unsigned char* img = lds + kVTGuard;  // the run, a guard before and after it
+  const uint32_t tid = threadIdx.x;
+  const uint64_t p0 = (uint64_t)(xcd_tile(blockIdx.x, gridDim.x)) * T;
+  const uint32_t Tv = n - p0 < T ? (uint32_t)(n - p0) : T;
+  const uint32_t L = F - H;
+  const uint64_t fo0 = fo_base + p0 * F, fo_end = fo0 + (uint64_t)Tv * F;
+  const uint64_t A = fo0 & ~15ull;
+  const uint32_t nvec = (uint32_t)((((fo_end + 15u) & ~15ull) - A) >> 4);
+  u32x4* dst = reinterpret_cast<u32x4*>(img);
+  for (uint32_t v0 = tid; v0 < nvec; v0 += 4u * kBlock) {
+    u32x4 r[4];
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u)
+      if (v0 + u * kBlock < nvec) r[u] = load16_guarded(frames, A + 16ull * (v0 + u * kBlock), fo_end);
+#pragma unroll
+    for (uint32_t u = 0; u < 4; ++u)
+      if (v0 + u * kBlock < nvec) dst[v0 + u * kBlock] = r[u];
+  }
+  __syncthreads();
+  const uint32_t* lds_dw = reinterpret_cast<const uint32_t*>(lds);
+  const uint32_t d0 = kVTGuard + (uint32_t)(fo0 - A) + H;  // LDS offset of the tile's first payload byte
+  unsigned char* o = out + p0 * (uint64_t)L;     // the tile's output run [0, nb)
+  const uint32_t nb = Tv * L;
+  const uint32_t lead = (uint32_t)(-(uintptr_t)o) & 15u;  // bytes before its first aligned chunk
+  const uint32_t nch = nb > lead ? (nb - lead + 15u) / 16u + 1u : 1u;  // chunk 0 is the head [0, lead)
+  for (uint32_t c = tid; c < nch; c += kBlock) {
+    // chunk c covers run bytes [x, x + 16) of which [b_lo, b_hi) are owned
+    const int x = c == 0 ? (int)lead - 16 : (int)lead + 16 * (int)(c - 1u);
+    const int b_lo = x < 0 ? -x : 0;
+    const int b_hi = x + 16 <= (int)nb ? 16 : (int)nb - x;
+    if (b_hi <= b_lo) continue;
+    uint64_t lo = 0, hi = 0;
+    uint32_t y = (uint32_t)(x + b_lo);
+    uint32_t q = y / L, j = y - q * L;
+    for (int b = b_lo; b < b_hi;) {
+      const int take = (int)(L - j) < b_hi - b ? (int)(L - j) : b_hi - b;
+      // chunk byte b is payload q's byte j, at LDS offset d0 + q F + j
+      const u32x4 w = window16_dw(lds_dw, d0 + q * F + j - (uint32_t)b);  // (>= kVTGuard - 15)
+      lo |= lo64(w) & byte_mask(b, b + take);
+      hi |= hi64(w) & byte_mask(b - 8, b + take - 8);
+      b += take;
+      ++q;
+      j = 0;
+    }
+    if (b_lo == 0 && b_hi == 16) {
+      __builtin_nontemporal_store(make_u32x4(lo, hi), reinterpret_cast<u32x4*>(o + x));
+    } else {
+      for (int b = b_lo; b < b_hi; ++b) o[x + b] = (unsigned char)(b < 8 ? lo >> (8 * b) : hi >> (8 * (b - 8)));
+    }
+  }
+}
+
+int launch_copy_payloads(const unsigned char* frames, uint32_t F, uint32_t H, uint64_t n, unsigned char* out,
+                         hipStream_t stream) {
+  if (n == 0 || F <= H) return 0;
+  const uint64_t fmis = reinterpret_cast<uintptr_t>(frames) & 15u;
+  uint32_t T = kCopyRun / F;
+  if (T < 1u) T = 1u;
+  if (T > 4096u) T = 4096u;
+  const size_t lds = 2u * kVTGuard + (((size_t)T * F + 31u) & ~size_t(15));
+  if (lds > 65536) {
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&copy_payloads_kernel),
+                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e != hipSuccess) return (int)e;
+  }
+  const uint64_t blocks = (n + T - 1) / T;
+  hipLaunchKernelGGL(copy_payloads_kernel, dim3((uint32_t)blocks), dim3(kBlock), lds, stream, frames - fmis, fmis, F,
+                     H, n, T, out);
+  return (int)hipGetLastError();
+}
+
 int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int layout, hipStream_t stream) {
   if (args.n == 0) return 0;
   const uint32_t fpt = args.small_fpt;
@@ -1949,7 +2074,7 @@ int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int
 // outside its staged run; rare).
 template <int H, bool U8>
 __device__ __forceinline__ void decode_varlen_frame_lane(const VarlenArgs& a, uint64_t p) {
-  const uint64_t fo = a.frame_off[p], fe = a.frame_off[p + 1];
+  const uint64_t fo = fo_at(a, p), fe = fo_at(a, p + 1);
   if (fo > fe || fe > frames_limit(a)) {
     decode_varlen_reject(a, p);
     return;
@@ -1981,7 +2106,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
   unsigned char* img = lds + ((4u * (T + 1u) + 15u) & ~15u);            // the run, then a guard
   const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint32_t Tv = a.n - p0 < T ? (uint32_t)(a.n - p0) : T;
-  const uint64_t fo0 = a.frame_off[p0], fo_end = a.frame_off[p0 + Tv];
+  const uint64_t fo0 = fo_at(a, p0), fo_end = fo_at(a, p0 + Tv);
   const uint64_t total = frames_limit(a);
   const uint64_t A = fo0 & ~15ull;
   const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
@@ -1998,7 +2123,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
 #pragma unroll
     for (uint32_t j = 0; j < FPT; ++j) {
       const uint32_t q = j * kBlock + tid;
-      const uint64_t o = q <= Tv ? a.frame_off[p0 + q] : A;
+      const uint64_t o = q <= Tv ? fo_at(a, p0 + q) : A;
       fo_r[j] = o - A <= fo_end - A ? (uint32_t)(o - A) : 0xFFFFFFFFu;  // outside [A, fo_end]
     }
     if (tid == 0) fo_last = (uint32_t)(fo_end - A);

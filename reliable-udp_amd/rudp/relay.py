@@ -220,8 +220,8 @@ class Relay(threading.Thread):
             except OSError as e:
                 if not self.stop_event.is_set():  # (a socket closed under a stopping relay is expected)
                     self.errors.append(e)         # anything else: kept for the caller, the relay goes on
-            except BaseException as e:  # noqa: BLE001 -- recorded; the slot is still given back
-                self.errors.append(e)
+            except Exception as e:  # noqa: BLE001 -- recorded; the slot is still given back
+                self.errors.append(e)   # (KeyboardInterrupt / SystemExit propagate after the finally)
             finally:
                 if slot is not None:
                     rx.release(slot)

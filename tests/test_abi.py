@@ -181,6 +181,10 @@ def test_product_code_object_ships_only_measured_forms():
     losing = [k for k in prod if "decode_span_index_kernel" in k or "decode_varlen_span_kernel" in k
               or re.search(r"decode_varlen_tile_kernelILi[57]ELb[01]ELj(128ELb0|256ELb1)E", k)]
     assert not losing, losing
+    # fixed-length batches that miss the fixed tiles take the varlen tiles with
+    # implicit offsets (round 6): the one-wave-per-packet byte kernels are gone
+    assert not [k for k in prod if "encode_bytes_kernel" in k or "decode_bytes_kernel" in k]
+    assert any("copy_payloads_kernel" in k for k in prod)
     tools = _code_object_kernels(_native.TOOLS_LIB_PATH)
     assert any("decode_varlen_span_kernel" in k for k in tools)
     assert any(re.search(r"decode_varlen_tile_kernelILi7ELb0ELj128ELb0E", k) for k in tools)

@@ -95,7 +95,10 @@ def test_roundtrip_vs_oracle(cuda, L):
             assert np.array_equal(host(d.payload), pay)
 
 
-def test_misaligned_buffers_take_byte_path(cuda):
+def test_misaligned_buffers_take_stride_tiles(cuda):
+    """1024-B payloads in views at odd byte offsets miss the fixed-length tiles
+    only through their alignment: the varlen tiles with implicit offsets frame
+    and decode them (tests/test_gpu_stride.py covers every shape)."""
     import torch
     n, L = 1000, 1024
     seq, ack, flags, pay = synth.synth(77, 0, n, L, ascii=False)
