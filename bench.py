@@ -587,6 +587,9 @@ def legs(torch, batch, device, steps):
     # the proxy-role caller's batch sizes (recvmmsg batches of <= 1024, proxy.py:126-154) and a
     # large socket batch: per-call cost of the sync-free entries back to back, and the latency of
     # one call waited for (launch + kernels + one synchronize)
+    # fixed-length payloads off the 16-B grid (the reference's 1-char datagrams; 1000 B),
+    # against the varlen path on the same bytes
+    out.update(fixed_stride_legs(torch, batch, device, steps))
     out["small_batch_calls"] = small_batch_calls(torch, batch, device)
     # socket boundary: 1M one-character frames sendmmsg'd over loopback, recvmmsg'd into a
     # pinned ring and decoded on the GPU per received batch (rudp.netio)
@@ -613,6 +616,155 @@ def legs(torch, batch, device, steps):
     del w, a, b
     torch.cuda.empty_cache()
     return out
+
+
+def fixed_stride_legs(torch, batch, device, steps, rounds=5):
+    """Fixed-length batches that miss the fixed-length tiles (payloads not a multiple
+    of 16 B), against the varlen path on the same bytes: 1M one-character rudp5
+    datagrams -- the reference's own traffic, utils/reliableUDP.py:11, :60, framed by
+    utils/packet.py:60-65 + :80-81 -- encoded (pack_batch on [N, 1] payloads) and
+    decoded with get_payload()'s strict UTF-8 (unpack_batch(utf8=True),
+    utils/packet.py:73), and 1M x 1000 B rudp7 encoded.  Both forms through the raw
+    C ABI with preallocated outputs (rudp_encode / rudp_decode_utf8 against
+    rudp_encode_varlen_checked / rudp_decode_varlen_utf8: at ~10 us per call the
+    Python entries' allocations would be the clock), and through the Python entries;
+    rounds of the forms interleaved, medians.  The fixed frames are compared with
+    the varlen frames (pinned by the reference goldens) outside the clock."""
+    import ctypes
+    from rudp import _native
+    lib = _native.lib()
+    sp = torch.cuda.current_stream().cuda_stream
+    di = device.index or 0
+    out = {}
+    n = 1 << 20
+    for L, layout in ((1, "rudp5"), (1000, "rudp7")):
+        H = batch.layout_header_len(layout)
+        F = L + H
+        tab, pay = batch.synth_batch(n, L, SEEDS[1472], device=device)
+        lens = torch.full((n,), L, dtype=torch.int32, device=device)
+        flat = pay.view(-1)
+        want_cs = H == 5
+        fr, cs = batch.pack_batch(tab, pay, layout, want_csum=want_cs)
+        v = batch.pack_batch_varlen(tab, flat, lens, layout, want_csum=want_cs, check=False)
+        v.check()
+        same = torch.equal(fr.view(-1), v.frames) and (
+            cs is None or torch.equal(cs.view(torch.int16), v.csum.view(torch.int16)))
+        rb = _native.RudpBatch(n=n, payload_len=L, reserved=0, seq=tab.seq.data_ptr(), ack=tab.ack.data_ptr(),
+                               flags=tab.flags.data_ptr(), payload=flat.data_ptr(), len=None, payload_off=None)
+        rv = _native.RudpBatch(n=n, payload_len=L, reserved=0, seq=tab.seq.data_ptr(), ack=tab.ack.data_ptr(),
+                               flags=tab.flags.data_ptr(), payload=flat.data_ptr(), len=lens.data_ptr(),
+                               payload_off=None)
+        vf, vo = torch.empty_like(v.frames), torch.empty_like(v.frame_off)
+        vc = torch.empty((n,), dtype=torch.uint16, device=device) if want_cs else None
+        st = torch.empty((1,), dtype=torch.int32, device=device)
+        fns = {
+            "encode_fixed_abi": lambda i: lib.rudp_encode(ctypes.byref(rb), fr.data_ptr(),
+                                                          cs.data_ptr() if want_cs else None, H, di, sp),
+            "encode_varlen_abi": lambda i: lib.rudp_encode_varlen_checked(
+                ctypes.byref(rv), flat.numel(), vf.data_ptr(), vf.numel(), vo.data_ptr(),
+                vc.data_ptr() if want_cs else None, st.data_ptr(), H, di, sp),
+            "encode_fixed_python": lambda i: batch.pack_batch(tab, pay, layout, out=fr, csum_out=cs,
+                                                              want_csum=want_cs),
+            "encode_varlen_python": lambda i: batch.pack_batch_varlen(tab, flat, lens, layout, want_csum=want_cs,
+                                                                      check=False, reuse=v),
+        }
+        if L == 1:
+            o = [torch.empty((n,), dtype=dt, device=device) for dt in
+                 (torch.uint16, torch.uint16, torch.uint8, torch.uint8, torch.uint16, torch.uint8)]
+            ov = [torch.empty_like(t) for t in o]
+            fns["decode_utf8_fixed_abi"] = lambda i: lib.rudp_decode_utf8(
+                fr.data_ptr(), None, F, n, cs.data_ptr(), *[t.data_ptr() for t in o[:5]], None, o[5].data_ptr(),
+                H, di, sp)
+            fns["decode_utf8_varlen_abi"] = lambda i: lib.rudp_decode_varlen_utf8(
+                v.frames.data_ptr(), v.frames.numel(), v.frame_off.data_ptr(), F, n, v.csum.data_ptr(),
+                *[t.data_ptr() for t in ov], None, H, di, sp)
+            fns["decode_utf8_fixed_python"] = lambda i: batch.unpack_batch(fr, layout, csum=cs, utf8=True)
+        per = {k: [] for k in fns}
+        for r in range(rounds):
+            for k, fn in fns.items():
+                per[k].append(time_loop(torch, fn, steps, 2 if r == 0 else 1) / steps)
+        ms = {k: sorted(x)[len(x) // 2] for k, x in per.items()}
+        if int(st.item()):
+            raise RuntimeError("the raw varlen encode rejected the bench batch")
+        same = same and torch.equal(vf, v.frames)
+        enc_bytes = n * algorithmic_bytes_encode(L)  # read L + 5, write L + 7 (frame + csum, or rudp7 frame)
+        out[f"encode_1Mx{L}_fixed"] = {
+            "ms": ms["encode_fixed_abi"], "vs_varlen_same_bytes": ms["encode_fixed_abi"] / ms["encode_varlen_abi"],
+            "roofline_frac": enc_bytes / (ms["encode_fixed_abi"] / 1e3) / 1e9 / HBM_PEAK_GBS,
+            "Mpkt_s": n / ms["encode_fixed_abi"] / 1e3, "layout": layout,
+            "frames_equal_varlen_path": bool(same), "ms_by_form": ms if L != 1 else
+            {k: x for k, x in ms.items() if k.startswith("encode")}}
+        if L == 1:
+            valid_ok = bool((o[5] == 1).all()) and bool((o[3] == 1).all()) and torch.equal(
+                o[0].view(torch.int16), tab.seq.view(torch.int16))
+            dec_bytes = n * (F + 2 + 6 + 2 + 1)  # read frame + sideband csum; write seq/ack/flags/ok, csum, valid
+            out["decode_utf8_1Mx1_fixed"] = {
+                "ms": ms["decode_utf8_fixed_abi"],
+                "vs_varlen_same_bytes": ms["decode_utf8_fixed_abi"] / ms["decode_utf8_varlen_abi"],
+                "roofline_frac": dec_bytes / (ms["decode_utf8_fixed_abi"] / 1e3) / 1e9 / HBM_PEAK_GBS,
+                "Mpkt_s": n / ms["decode_utf8_fixed_abi"] / 1e3, "layout": layout,
+                "all_valid_verified_fields_equal": valid_ok,
+                "ms_by_form": {k: x for k, x in ms.items() if k.startswith("decode")}}
+        del tab, pay, lens, flat, fr, cs, v, vf, vo, vc
+    out["note"] = ("fixed-length payloads of 1 and 1000 B (not multiples of 16): the varlen tile kernels with "
+                   "implicit offsets (one launch, no scan), against rudp_encode_varlen_checked / "
+                   "rudp_decode_varlen_utf8 on the same bytes; *_abi: raw C-ABI calls with preallocated "
+                   "outputs (the ratio is theirs), *_python: the Python entries; medians of 5 interleaved "
+                   "rounds; 1-char batches are 7-27 MB, resident in the Infinity Cache for both forms")
+    torch.cuda.empty_cache()
+    return out
+
+
+def baseline_summary(line):
+    """A compact digest of the BASELINE-config legs (C2, C3, C4, C5 on
+    one GPU) and the decode legs, appended as the LAST key of the JSON line so a
+    reader that keeps only the line's tail still sees each one with its ms,
+    roofline fraction and reference-digest result."""
+    lg = line.get("legs") or {}
+
+    def pick(key, ms="ms", frac="roofline_frac", chk=None, extra=()):
+        d = lg.get(key)
+        if not isinstance(d, dict):
+            return None
+        r = {"ms": round(d[ms], 4) if d.get(ms) is not None else None,
+             "frac": round(d[frac], 3) if d.get(frac) is not None else None}
+        if chk:
+            r["digests"] = d.get(chk)
+        for k in extra:
+            if k in d:
+                r[k] = round(d[k], 3) if isinstance(d[k], float) else d[k]
+        return r
+    out = {
+        "headline_C4_encode_1Mx1472": {"ms": round(line["roofline"]["kernel_ms_per_launch"], 4),
+                                       "frac": round(line["roofline"]["frac"], 3),
+                                       "matches_reference": line["config"].get("matches_reference")},
+        "C2_encode_1Mx1024": pick("encode_1Mx1024", chk="chunks_matching_reference_digests"),
+        "C3_encode_1Mx64": pick("encode_1Mx64", chk="chunks_matching_reference_digests",
+                                extra=("frac_of_copy_same_bytes",)),
+        "C4_roundtrip_1Mx1472": pick("roundtrip_1Mx1472", chk="chunks_matching_reference_digests",
+                                     extra=("decode_fields_equal_inputs",)),
+        "C5_encode_16Mx1472_1gpu": pick("encode_16Mx1472_C5_1gpu", chk="chunks_matching_reference_digests"),
+        "decode_verify_1Mx1472": pick("decode_verify_1Mx1472"),
+        "decode_utf8_ascii_1Mx1472": pick("decode_utf8_1Mx1472", extra=("all_valid_and_verified",)),
+        "decode_utf8_multibyte_text_1Mx1472": pick("decode_utf8_1Mx1472_multibyte_text",
+                                                   extra=("all_valid_and_verified",)),
+        "encode_1Mx1_fixed": pick("encode_1Mx1_fixed", extra=("vs_varlen_same_bytes", "frames_equal_varlen_path")),
+        "decode_utf8_1Mx1_fixed": pick("decode_utf8_1Mx1_fixed",
+                                       extra=("vs_varlen_same_bytes", "all_valid_verified_fields_equal")),
+        "encode_1Mx1000_fixed": pick("encode_1Mx1000_fixed",
+                                     extra=("vs_varlen_same_bytes", "frames_equal_varlen_path")),
+        "varlen_ragged_encode_ms": round(lg["varlen_1M_ragged_0_2944"]["encode_ms"], 4)
+        if "varlen_1M_ragged_0_2944" in lg else None,
+        "varlen_ragged_decode_frac": round(lg["varlen_1M_ragged_0_2944"]["decode_roofline_frac"], 3)
+        if "varlen_1M_ragged_0_2944" in lg else None,
+    }
+    c5 = lg.get("c5_16Mx1472_strong")
+    if c5:
+        out["C5_strong"] = {"ms": round(c5["ms"], 4), "GiB_s": round(c5["GiB_s"], 1), "n_gpus": c5["n_gpus"],
+                            "per_gpu_frac": round(c5["per_gpu_roofline_frac"], 3),
+                            "digests": f"{c5['chunks_matching_reference_digests']}/16"
+                            if c5["packets_total"] == C5_PACKETS else c5["chunks_matching_reference_digests"]}
+    return {k: v for k, v in out.items() if v is not None}
 
 
 def e2e_host_decode_legs(torch, batch, frames, n, L, reps=3):
@@ -950,6 +1102,25 @@ def read_pmc_traffic(L, n):
     return d.get("hbm_bytes_per_launch"), str(path.relative_to(REPO))
 
 
+def launch_ranks(n: int, argv, dry_run: bool = False) -> int:
+    """`python -m torch.distributed.run --nproc-per-node n` over this script with
+    the same arguments, rendezvous on 127.0.0.1 at a free port, as a child process
+    whose stdout is ours (rank 0's JSON line passes straight through)."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", str(Path(__file__).resolve()), *argv]
+    if dry_run:
+        print(json.dumps({"launch": cmd}), flush=True)
+        return 0
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")  # dmabuf IPC for RCCL on this host driver
+    return subprocess.run(cmd, env=env).returncode
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -974,11 +1145,19 @@ def main():
     ap.add_argument("--c5-packets", type=int, default=0,
                     help="testing only: packets of the C5 strong leg (default 16M)")
     ap.add_argument("--relay-peer", metavar="DIR", help=argparse.SUPPRESS)  # relay_leg's child process
+    ap.add_argument("--print-launch", action="store_true",
+                    help="testing only: with --gpus N > 1 and no launcher, print the rank launcher's "
+                         "command instead of running it")
     args = ap.parse_args()
     if args.relay_peer:
         relay_peer(args.relay_peer)
         return
 
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # no launcher around us: start torch.distributed.run as a CHILD process
+        # (before anything touches the GPU; never exec) with this command line,
+        # one rank per GPU, and hand back its exit status -- rank 0 prints the line
+        sys.exit(launch_ranks(args.gpus, sys.argv[1:], args.print_launch))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
@@ -1109,6 +1288,7 @@ def main():
             if ceiling:
                 line["roofline"]["measured_copy_ceiling_GBs"] = ceiling
                 line["roofline"]["frac_of_copy_ceiling"] = achieved / ceiling
+        line["baseline_legs"] = baseline_summary(line)  # last: visible in any tail of the line
         print(json.dumps(line), flush=True)
     if distributed:
         dist.destroy_process_group()

@@ -124,3 +124,29 @@ def test_c5_multirank_processes_match_reference(digests, world):
                 seen.append(first // chunk + k)
                 assert h == want["frames"][first // chunk + k], (layout, first, k)
         assert seen == list(range(16)), seen
+
+
+def test_bench_launches_its_own_ranks():
+    """`python3 bench.py --gpus 2 --share-device` with no launcher around it starts
+    torch.distributed.run itself, as a child process (never an exec), and relays
+    rank 0's one line: 2 ranks, bit-exact, and the C5 strong leg's chunks against
+    the reference digests (2 of the 16 chunks at --c5-packets 2^21)."""
+    import json
+    import subprocess
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    repo = Path(__file__).resolve().parent.parent
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK")}
+    r = subprocess.run([sys.executable, str(repo / "bench.py"), "--gpus", "2", "--share-device", "--steps", "3",
+                        "--warmup", "1", "--packets", str(1 << 18), "--c5-packets", str(1 << 21),
+                        "--no-cpu-baseline"], capture_output=True, text=True, env=env, timeout=110)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [ln for ln in r.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, r.stdout[-2000:]
+    line = json.loads(lines[0])
+    assert line["n_gpus"] == 2 and len(line["config"]["devices"]) == 2
+    c5 = line["legs"]["c5_16Mx1472_strong"]
+    assert c5["n_gpus"] == 2 and c5["ranks_bit_exact_vs_reference"] == 2
+    assert c5["chunks_matching_reference_digests"] == 2
+    assert list(line)[-1] == "baseline_legs" and line["baseline_legs"]["C5_strong"]["digests"] == 2
