@@ -35,19 +35,32 @@ constexpr uint32_t kVarLanes = 8;
 // Uniform (a kernel argument), so this is one scalar load per wave.
 __device__ __forceinline__ bool call_failed(const uint32_t* status) { return status && *status; }
 
-// A batch's offsets: the frame_off array, or a fixed stride (frame_off null;
-// VarlenArgs::stride).  Uniform per launch, so each is one scalar branch.
+// A batch's offsets: the frame_off array, or (FX) a fixed stride
+// (VarlenArgs::stride, frame_off null).  A template argument, not a branch:
+// the varlen kernels compile exactly as they did without the fixed-stride
+// form (a runtime choice in the encode tile cost 1M x 1472 B 0.539 -> 0.570
+// ms and ragged lengths 0.603 -> 0.690 in an A/B against the round-5 build,
+// profiles/r06/sweeps/stride_template.json), and the FX instantiations read
+// no offsets at all.
+template <bool FX>
 __device__ __forceinline__ uint64_t fo_at(const VarlenArgs& a, uint64_t p) {
-  return a.frame_off ? a.frame_off[p] : a.fo_base + p * a.stride;
+  if (FX) return a.fo_base + p * a.stride;
+  return a.frame_off[p];
 }
-template <int H>
+template <int H, bool FX>
 __device__ __forceinline__ uint32_t len_at(const VarlenArgs& a, uint64_t p) {
-  return a.frame_off ? a.len[p] : (uint32_t)a.stride - (uint32_t)H;
+  if (FX) return (uint32_t)a.stride - (uint32_t)H;
+  return a.len[p];
 }
 // Payload offset of packet p, whose frame starts at fo.
-template <int H>
+template <int H, bool FX>
 __device__ __forceinline__ uint64_t po_at(const VarlenArgs& a, uint64_t p, uint64_t fo) {
-  return a.payload_off ? a.payload_off[p] : fo - p * (uint64_t)H + a.po_delta;
+  if (FX) return fo - p * (uint64_t)H + a.po_delta;
+  return a.payload_off ? a.payload_off[p] : fo - p * (uint64_t)H;
+}
+// The byte-granular kernels (the diagnostics build's varlen_vec = 0 form) choose at run time.
+__device__ __forceinline__ uint64_t fo_rt(const VarlenArgs& a, uint64_t p) {
+  return a.frame_off ? fo_at<false>(a, p) : fo_at<true>(a, p);
 }
 
 #if RUDP_TOOLS
@@ -67,9 +80,9 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_kernel(VarlenArgs a) {
   uint32_t sum = 0;
   uint64_t fo = 0;
   if (valid) {
-    const uint32_t L = len_at<H>(a, p);
-    fo = fo_at(a, p);
-    const uint64_t po = po_at<H>(a, p, fo);
+    const uint32_t L = a.frame_off ? len_at<H, false>(a, p) : len_at<H, true>(a, p);
+    fo = fo_rt(a, p);
+    const uint64_t po = a.frame_off ? po_at<H, false>(a, p, fo) : po_at<H, true>(a, p, fo);
     for (uint32_t j = g; j < L; j += kVarLanes) {
       const uint32_t b = a.payload[po + j];
       sum += (j & 1u) ? (b << 8) : b;  // LE u16 word sum (payload at an odd frame offset)
@@ -142,13 +155,13 @@ __device__ __forceinline__ void store_owned(unsigned char* dst, int b_lo, int b_
 // written after the shfl reduction.
 // G = 2^glog lanes (g = 0..G-1, one aligned group of a wave) encode packet p.
 // fo_in: the frame's offset when the caller already has it (~0: read frame_off).
-template <int H>
+template <int H, bool FX = false>
 __device__ __forceinline__ void encode_varlen_packet(const VarlenArgs& a, uint64_t p, bool valid, uint32_t g,
                                                      uint32_t glog, uint64_t fo_in = ~0ull) {
   const uint32_t G = 1u << glog;
-  const uint32_t L = valid ? len_at<H>(a, p) : 0u;
-  const uint64_t fo = valid ? (fo_in != ~0ull ? fo_in : fo_at(a, p)) : 0;
-  const uint64_t po = valid ? po_at<H>(a, p, fo) : 0;
+  const uint32_t L = valid ? len_at<H, FX>(a, p) : 0u;
+  const uint64_t fo = valid ? (fo_in != ~0ull ? fo_in : fo_at<FX>(a, p)) : 0;
+  const uint64_t po = valid ? po_at<H, FX>(a, p, fo) : 0;
   const uint64_t pend = po + L;
   const uint32_t F = L + H;
   const uint64_t x_lo = fo >> 4;
@@ -228,13 +241,13 @@ __device__ __forceinline__ void encode_varlen_packet(const VarlenArgs& a, uint64
   }
 }
 
-template <int H>
+template <int H, bool FX = false>
 __global__ void __launch_bounds__(kBlock) encode_varlen_vec_kernel(VarlenArgs a) {
   if (call_failed(a.status)) return;
   const uint32_t tid = threadIdx.x;
   const uint32_t glog = a.glog;
   const uint64_t p = (uint64_t)blockIdx.x * (kBlock >> glog) + (tid >> glog);
-  encode_varlen_packet<H>(a, p, p < a.n, tid & ((1u << glog) - 1u), glog);
+  encode_varlen_packet<H, FX>(a, p, p < a.n, tid & ((1u << glog) - 1u), glog);
 }
 
 // LDS layout of the varlen encode tile: header words u64[T], tile-relative
@@ -315,7 +328,7 @@ __device__ __forceinline__ uint32_t octet_sum(uint32_t x) {
 // of S payload bytes instead, their lanes per packet from their count.  The
 // grid covers both forms; a tile learns its packets from the scan's records.
 // W: minimum waves per SIMD the register allocation must allow (1 = none).
-template <int H, int W>
+template <int H, int W, bool FX = false>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))) encode_varlen_tile_kernel(VarlenArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const uint32_t Tl = a.tile_Tl, cap = a.tile_cap;
@@ -366,8 +379,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     p0 = (uint64_t)(a.xcd ? xcd_tile(b, ptiles) : b) * a.tile_T;
     T = a.tile_T;
     Tv = Tall = a.n - p0 < a.tile_T ? (uint32_t)(a.n - p0) : a.tile_T;
-    fo0 = fo_at(a, p0);
-    fo_end = fo_at(a, p0 + Tv);
+    fo0 = fo_at<FX>(a, p0);
+    fo_end = fo_at<FX>(a, p0 + Tv);
     glog = a.tile_glog;
   }
   const uint32_t G = 1u << glog, q = tid >> glog, g = tid & (G - 1u);
@@ -380,13 +393,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     t_flags = a.flags_in[p0 + q];
   }
   if (call_failed(a.status)) return;
-  const uint64_t po0 = fo0 - p0 * (uint64_t)H + a.po_delta;
-  const uint64_t po_end = fo_end - (p0 + Tv) * (uint64_t)H + a.po_delta;
+  const uint64_t po0 = fo0 - p0 * (uint64_t)H + (FX ? a.po_delta : 0ull);
+  const uint64_t po_end = fo_end - (p0 + Tv) * (uint64_t)H + (FX ? a.po_delta : 0ull);
   const uint64_t A = po0 & ~15ull;
   const uint64_t run = ((po_end + 15u) & ~15ull) - A;
   if (Tall > T || run > cap) {  // uniform over the workgroup
     for (uint32_t q0 = 0; q0 < Tall; q0 += kBlock >> glog)  // (byte tiles may hold more than T packets)
-      encode_varlen_packet<H>(a, p0 + q0 + q, q0 + q < Tall, g, glog);
+      encode_varlen_packet<H, FX>(a, p0 + q0 + q, q0 + q < Tall, g, glog);
     return;
   }
   const bool early_tab = a.early_table;
@@ -397,8 +410,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
     // payload stream so their round trip overlaps it (early_fo).
     uint32_t fo_r0 = 0, fo_r1 = 0;
     if (a.early_fo) {
-      if (tid <= Tv) fo_r0 = (uint32_t)(fo_at(a, p0 + tid) - fo0);
-      if (tid + kBlock <= Tv) fo_r1 = (uint32_t)(fo_at(a, p0 + tid + kBlock) - fo0);
+      if (tid <= Tv) fo_r0 = (uint32_t)(fo_at<FX>(a, p0 + tid) - fo0);
+      if (tid + kBlock <= Tv) fo_r1 = (uint32_t)(fo_at<FX>(a, p0 + tid + kBlock) - fo0);
     }
     const u32x4* src = reinterpret_cast<const u32x4*>(a.payload + A);
     u32x4* dst = reinterpret_cast<u32x4*>(lds_pay + kVTGuard);
@@ -428,7 +441,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
       if (tid <= Tv) lds_fo[tid] = fo_r0;
       if (tid + kBlock <= Tv) lds_fo[tid + kBlock] = fo_r1;
     } else {
-      for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = (uint32_t)(fo_at(a, p0 + i) - fo0);
+      for (uint32_t i = tid; i <= Tv; i += kBlock) lds_fo[i] = (uint32_t)(fo_at<FX>(a, p0 + i) - fo0);
     }
   }
   __syncthreads();
@@ -732,8 +745,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(W))
 
 // Byte limit of a decode's frames: the caller's buffer size for checked
 // calls, else (unchecked callers) the last offset.
+template <bool FX = false>
 __device__ __forceinline__ uint64_t frames_limit(const VarlenArgs& a) {
-  return a.lim_checked ? a.frames_lim : fo_at(a, a.n);
+  return a.lim_checked ? a.frames_lim : fo_at<FX>(a, a.n);
 }
 
 // A frame whose offsets are invalid: no byte of it is read.
@@ -759,9 +773,9 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_kernel(VarlenArgs a) {
   uint64_t fo = 0;
   bool bad = false;
   if (valid) {
-    fo = fo_at(a, p);
-    const uint64_t fe = fo_at(a, p + 1);
-    bad = fo > fe || fe > frames_limit(a);
+    fo = fo_rt(a, p);
+    const uint64_t fe = fo_rt(a, p + 1);
+    bad = fo > fe || fe > (a.lim_checked ? a.frames_lim : fo_rt(a, a.n));
     F = bad ? 0u : fe - fo;
     for (uint64_t j = (uint64_t)H + g; j < F; j += kVarLanes) {
       const uint32_t b = a.frames[fo + j];
@@ -853,14 +867,14 @@ __device__ __forceinline__ void decode_varlen_finish(const VarlenArgs& a, uint64
 // U8: the payload's strict UTF-8 check in the same pass: the (masked) payload
 // words' high bits are OR'ed as they are summed, and only a frame that holds
 // one runs the byte checks (utf8_check_frame, its chunks again, from L2).
-template <int H, bool U8, int PL = 0>
+template <int H, bool U8, int PL = 0, bool FX = false>
 __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_t p, bool valid, uint32_t g,
                                                     uint32_t glog) {
   const uint32_t tid = threadIdx.x;
   const uint32_t G = 1u << glog;
-  const uint64_t total = frames_limit(a);
-  uint64_t fstart = valid ? fo_at(a, p) : 0;
-  uint64_t fend = valid ? fo_at(a, p + 1) : 0;
+  const uint64_t total = frames_limit<FX>(a);
+  uint64_t fstart = valid ? fo_at<FX>(a, p) : 0;
+  uint64_t fend = valid ? fo_at<FX>(a, p + 1) : 0;
   const bool bad = valid && (fstart > fend || fend > total);
   if (bad) fstart = fend = 0;  // nothing of it is read
   const uint64_t c_lo = fstart >> 4;
@@ -933,11 +947,11 @@ __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_
                           funnel32(first, next, (uint32_t)(fstart & 15u)));
 }
 
-template <int H, bool U8>
+template <int H, bool U8, bool FX = false>
 __global__ void __launch_bounds__(kBlock) decode_varlen_vec_kernel(VarlenArgs a) {
   const uint32_t glog = a.glog;
   const uint64_t p = (uint64_t)blockIdx.x * (kBlock >> glog) + (threadIdx.x >> glog);
-  decode_varlen_frame<H, U8>(a, p, p < a.n, threadIdx.x & ((1u << glog) - 1u), glog);
+  decode_varlen_frame<H, U8, 0, FX>(a, p, p < a.n, threadIdx.x & ((1u << glog) - 1u), glog);
 }
 
 // Varlen decode through an LDS tile (the fixed-length decode tile's shape):
@@ -973,7 +987,7 @@ __device__ __forceinline__ uint32_t octet_or(uint32_t x) {
 // R4: a lane reads its payload chunks four at a time (one LDS wait per four
 // instead of one per chunk: the longest frame's chain of LDS round trips is
 // what a wave of ragged lengths waits for).
-template <int H, bool U8, uint32_t NT = kBlock, bool R4 = false>
+template <int H, bool U8, uint32_t NT = kBlock, bool R4 = false, bool FX = false>
 __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const uint32_t tid = threadIdx.x;
@@ -984,7 +998,7 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint64_t left = a.n - p0;
   const uint32_t Tv = left < T ? (uint32_t)left : T;
-  const uint64_t fo0 = fo_at(a, p0), fo_end = fo_at(a, p0 + Tv);
+  const uint64_t fo0 = fo_at<FX>(a, p0), fo_end = fo_at<FX>(a, p0 + Tv);
   // Block sums for every tile (tile_sums 2), or (1) for a tile of uneven frames:
   // every wave reads the tile's T + 1 <= 64 offsets itself (the same lines as
   // wave 0's early ones), so the choice is the same in all four without a
@@ -999,14 +1013,14 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   const bool adapt = RUDP_TOOLS && a.tile_sums == 1u && Tv == 16u;  // (16-frame tiles: MTU-scale hints)
   uint32_t len_adapt = 0;
   if (adapt && (tid & 63u) < 16u) {
-    const uint64_t d = fo_at(a, p0 + (tid & 63u) + 1u) - fo_at(a, p0 + (tid & 63u));
+    const uint64_t d = fo_at<FX>(a, p0 + (tid & 63u) + 1u) - fo_at<FX>(a, p0 + (tid & 63u));
     len_adapt = d < 0xFFFFFFFFull ? (uint32_t)d : 0xFFFFFFFFu;
   }
-  const uint64_t total = frames_limit(a);
+  const uint64_t total = frames_limit<FX>(a);
   const uint64_t A = fo0 & ~15ull;
   const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
   if (fo0 > fo_end || fo_end > total || run > a.tile_cap) {  // uniform over the workgroup
-    decode_varlen_frame<H, U8, 6>(a, p0 + q, q < Tv, g, glog);
+    decode_varlen_frame<H, U8, 6, FX>(a, p0 + q, q < Tv, g, glog);
     return;
   }
   // The block words: tile_sums 2, a region of their own after the run's budget;
@@ -1021,7 +1035,7 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
   auto rel = [&](uint64_t o) { return o - A <= span_end ? (uint32_t)(o - A) : 0xFFFFFFFFu; };
   {
     // T = 256 / G <= 128 frames: one offset per lane, loaded before the run (early_fo)
-    const uint32_t fo_r = a.early_fo && tid <= Tv ? rel(fo_at(a, p0 + tid)) : 0u;
+    const uint32_t fo_r = a.early_fo && tid <= Tv ? rel(fo_at<FX>(a, p0 + tid)) : 0u;
     const uint32_t nvec = (uint32_t)(run >> 4);
     u32x4* dst = reinterpret_cast<u32x4*>(img);
     constexpr uint32_t P = 8;
@@ -1067,7 +1081,7 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
     if (a.early_fo) {
       if (tid <= Tv) lds_fo[tid] = fo_r;
     } else {
-      for (uint32_t i = tid; i <= Tv; i += NT) lds_fo[i] = rel(fo_at(a, p0 + i));
+      for (uint32_t i = tid; i <= Tv; i += NT) lds_fo[i] = rel(fo_at<FX>(a, p0 + i));
     }
   }
   __syncthreads();
@@ -1080,7 +1094,7 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
     // rule asks) but reach past the staged bytes, so it decodes from HBM, where
     // the rule is applied to its true offsets.  Uniform over the frame's lanes.
     if (fs > fe || fe > (uint32_t)span_end) {
-      decode_varlen_frame<H, U8, 6>(a, p0 + q, true, g2, glog2);
+      decode_varlen_frame<H, U8, 6, FX>(a, p0 + q, true, g2, glog2);
       return;
     }
     // the leader's header window, read now so its LDS round trip overlaps the sums
@@ -1242,7 +1256,7 @@ __global__ void __launch_bounds__(kBlock) decode_varlen_span_kernel(VarlenArgs a
   uint64_t* lds_lex = reinterpret_cast<uint64_t*>(lds_whc + 4);                                // [256]
   uint16_t* lds_lhc = reinterpret_cast<uint16_t*>(lds_lex + kBlock);                           // [256]
   unsigned char* img = lds + dsp_img_off();
-  const uint64_t total = frames_limit(a);
+  const uint64_t total = frames_limit<false>(a);
 #if RUDP_TOOLS
   if (a.diag & 64u) {  // ablation: the loads only
     const uint32_t nvec = (uint32_t)(run >> 4);
@@ -1749,8 +1763,8 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
     fo0 = 0;
     fo_end = 0;  // from the scan below
   } else if (FIXED) {
-    fo0 = fo_at(a, p0);
-    fo_end = fo_at(a, p0 + Tv);
+    fo0 = fo_at<true>(a, p0);
+    fo_end = fo_at<true>(a, p0 + Tv);
   } else {
     fo0 = sums[tile];
     fo_end = p0 + T < a.n ? sums[tile + 1] : a.frame_off[a.n];
@@ -1759,8 +1773,8 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
 #if RUDP_TOOLS
   const uint64_t t_base = a.trace ? (uint64_t)wall_clock64() : 0ull;
 #endif
-  const uint64_t po0 = fo0 - p0 * (uint64_t)H + a.po_delta;
-  const uint64_t po_end = SINGLE ? chk.payload_bytes : fo_end - (p0 + Tv) * (uint64_t)H + a.po_delta;
+  const uint64_t po0 = fo0 - p0 * (uint64_t)H + (FIXED ? a.po_delta : 0ull);
+  const uint64_t po_end = SINGLE ? chk.payload_bytes : fo_end - (p0 + Tv) * (uint64_t)H + (FIXED ? a.po_delta : 0ull);
   const uint64_t A = po0 & ~15ull, OA = fo0 & ~15ull;
   const uint64_t prun = ((po_end + 15u) & ~15ull) - A;
   uint64_t orun = ((fo_end + 15u) & ~15ull) - OA;
@@ -1836,7 +1850,7 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
 #pragma unroll
     for (uint32_t j = 0; j < FPT; ++j) {
       const uint32_t q = j * kBlock + tid;
-      encode_varlen_packet<H>(a, p0 + q, q < Tv, 0u, 0u, q < Tv ? fo0 + s_off[q] : 0ull);
+      encode_varlen_packet<H, FIXED>(a, p0 + q, q < Tv, 0u, 0u, q < Tv ? fo0 + s_off[q] : 0ull);
     }
     return;
   }
@@ -2072,10 +2086,10 @@ int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int
 // One frame by one lane, straight from HBM, byte by byte: the checked rule
 // on its true offsets (the small-frame tile's frames whose offsets fall
 // outside its staged run; rare).
-template <int H, bool U8>
+template <int H, bool U8, bool FX>
 __device__ __forceinline__ void decode_varlen_frame_lane(const VarlenArgs& a, uint64_t p) {
-  const uint64_t fo = fo_at(a, p), fe = fo_at(a, p + 1);
-  if (fo > fe || fe > frames_limit(a)) {
+  const uint64_t fo = fo_at<FX>(a, p), fe = fo_at<FX>(a, p + 1);
+  if (fo > fe || fe > frames_limit<FX>(a)) {
     decode_varlen_reject(a, p);
     return;
   }
@@ -2097,7 +2111,7 @@ __device__ __forceinline__ void decode_varlen_frame_lane(const VarlenArgs& a, ui
   decode_varlen_finish<H>(a, p, F, sum, h);
 }
 
-template <int H, uint32_t FPT, bool U8>
+template <int H, uint32_t FPT, bool U8, bool FX>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))) decode_varlen_small_kernel(VarlenArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   constexpr uint32_t T = kBlock * FPT;
@@ -2106,15 +2120,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
   unsigned char* img = lds + ((4u * (T + 1u) + 15u) & ~15u);            // the run, then a guard
   const uint64_t p0 = (uint64_t)(a.xcd ? xcd_tile(blockIdx.x, gridDim.x) : blockIdx.x) * T;
   const uint32_t Tv = a.n - p0 < T ? (uint32_t)(a.n - p0) : T;
-  const uint64_t fo0 = fo_at(a, p0), fo_end = fo_at(a, p0 + Tv);
-  const uint64_t total = frames_limit(a);
+  const uint64_t fo0 = fo_at<FX>(a, p0), fo_end = fo_at<FX>(a, p0 + Tv);
+  const uint64_t total = frames_limit<FX>(a);
   const uint64_t A = fo0 & ~15ull;
   const uint64_t run = ((fo_end + 15u) & ~15ull) - A;
   if (fo0 > fo_end || fo_end > total || run > a.small_cap) {  // uniform: per-frame path, two lanes each
 #pragma unroll
     for (uint32_t j = 0; j < 2u * FPT; ++j) {  // (the header comes from the pair's two first chunks)
       const uint32_t q = j * (kBlock / 2u) + (tid >> 1);
-      decode_varlen_frame<H, U8, U8 ? 4 : 0>(a, p0 + q, q < Tv, tid & 1u, 1u);
+      decode_varlen_frame<H, U8, U8 ? 4 : 0, FX>(a, p0 + q, q < Tv, tid & 1u, 1u);
     }
     return;
   }
@@ -2123,7 +2137,7 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
 #pragma unroll
     for (uint32_t j = 0; j < FPT; ++j) {
       const uint32_t q = j * kBlock + tid;
-      const uint64_t o = q <= Tv ? fo_at(a, p0 + q) : A;
+      const uint64_t o = q <= Tv ? fo_at<FX>(a, p0 + q) : A;
       fo_r[j] = o - A <= fo_end - A ? (uint32_t)(o - A) : 0xFFFFFFFFu;  // outside [A, fo_end]
     }
     if (tid == 0) fo_last = (uint32_t)(fo_end - A);
@@ -2181,35 +2195,37 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(5))
   }
 #pragma unroll 1
   for (uint32_t j = 0; j < FPT; ++j)  // one lane per such frame, straight from HBM (rare)
-    if (fallback & (1u << j)) decode_varlen_frame_lane<H, U8>(a, p0 + j * kBlock + tid);
+    if (fallback & (1u << j)) decode_varlen_frame_lane<H, U8, FX>(a, p0 + j * kBlock + tid);
 }
 
-template <int H, uint32_t FPT, bool U8>
+template <int H, uint32_t FPT, bool U8, bool FX>
 int launch_decode_small_fpt(const VarlenArgs& args, hipStream_t stream) {
   constexpr uint32_t T = kBlock * FPT;
   const size_t lds = ((4u * (T + 1u) + 15u) & ~15u) + (size_t)args.small_cap + 32u;
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_varlen_small_kernel<H, FPT, U8>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_varlen_small_kernel<H, FPT, U8, FX>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
   const uint64_t blocks = (args.n + T - 1) / T;
-  hipLaunchKernelGGL((decode_varlen_small_kernel<H, FPT, U8>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream,
+  hipLaunchKernelGGL((decode_varlen_small_kernel<H, FPT, U8, FX>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream,
                      args);
   return (int)hipGetLastError();
 }
 
-template <int H, bool U8>
+template <int H, bool U8, bool FX>
 int launch_decode_small(const VarlenArgs& args, hipStream_t stream) {
 #if RUDP_TOOLS  // 4 frames per thread is the measured choice; 1, 2 and 8 for sweeps
-  switch (args.small_fpt) {
-    case 1: return launch_decode_small_fpt<H, 1, U8>(args, stream);
-    case 2: return launch_decode_small_fpt<H, 2, U8>(args, stream);
-    case 8: return launch_decode_small_fpt<H, 8, U8>(args, stream);
-    default: break;
+  if constexpr (!FX) {
+    switch (args.small_fpt) {
+      case 1: return launch_decode_small_fpt<H, 1, U8, FX>(args, stream);
+      case 2: return launch_decode_small_fpt<H, 2, U8, FX>(args, stream);
+      case 8: return launch_decode_small_fpt<H, 8, U8, FX>(args, stream);
+      default: break;
+    }
   }
 #endif
-  return launch_decode_small_fpt<H, 4, U8>(args, stream);
+  return launch_decode_small_fpt<H, 4, U8, FX>(args, stream);
 }
 
 // Dynamic LDS of one varlen encode tile whose arrays hold Tl packets.
@@ -2297,18 +2313,18 @@ bool varlen_btile_ok(uint32_t tile_T, uint32_t* bt_slots, uint32_t min_slots, ui
   return spans * 20u <= packet_tiles * 21u;
 }
 
-template <int H, int W>
+template <int H, int W, bool FX>
 int launch_varlen_tile_w(const VarlenArgs& args, size_t lds, uint64_t blocks, hipStream_t stream) {
   if (lds > 65536) {
-    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_varlen_tile_kernel<H, W>),
+    hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&encode_varlen_tile_kernel<H, W, FX>),
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL((encode_varlen_tile_kernel<H, W>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
+  hipLaunchKernelGGL((encode_varlen_tile_kernel<H, W, FX>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
   return (int)hipGetLastError();
 }
 
-template <int H>
+template <int H, bool FX>
 int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
   VarlenArgs args = in;
   uint64_t blocks = (args.n + args.tile_T - 1) / args.tile_T;
@@ -2331,11 +2347,12 @@ int launch_varlen_tile(const VarlenArgs& in, hipStream_t stream) {
   int w = tuning().varlen_waves;
   if (w < 0) w = vt_waves<H>(lds);
 #if RUDP_TOOLS
-  if (w == 8) return launch_varlen_tile_w<H, 8>(args, lds, blocks, stream);
+  if constexpr (!FX)
+    if (w == 8) return launch_varlen_tile_w<H, 8, FX>(args, lds, blocks, stream);
 #endif
-  return w == 6 ? launch_varlen_tile_w<H, 6>(args, lds, blocks, stream)
-       : w == 7 ? launch_varlen_tile_w<H, 7>(args, lds, blocks, stream)
-                : launch_varlen_tile_w<H, 1>(args, lds, blocks, stream);
+  return w == 6 ? launch_varlen_tile_w<H, 6, FX>(args, lds, blocks, stream)
+       : w == 7 ? launch_varlen_tile_w<H, 7, FX>(args, lds, blocks, stream)
+                : launch_varlen_tile_w<H, 1, FX>(args, lds, blocks, stream);
 }
 
 void varlen_tile_geometry(uint32_t len_hint, uint32_t* T, uint32_t* glog, uint32_t* cap) {
@@ -2367,17 +2384,21 @@ void varlen_tile_geometry(uint32_t len_hint, uint32_t* T, uint32_t* glog, uint32
 
 int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream) {
   if (args.n == 0) return 0;
+  const bool fx = args.frame_off == nullptr;  // a fixed-stride batch (VarlenArgs::stride)
   if (args.tile_T && !args.payload_off && ((reinterpret_cast<uintptr_t>(args.frames) |
-                                            reinterpret_cast<uintptr_t>(args.payload)) & 15u) == 0)
-    return layout == 7 ? launch_varlen_tile<7>(args, stream) : launch_varlen_tile<5>(args, stream);
+                                            reinterpret_cast<uintptr_t>(args.payload)) & 15u) == 0) {
+    if (fx) return layout == 7 ? launch_varlen_tile<7, true>(args, stream) : launch_varlen_tile<5, true>(args, stream);
+    return layout == 7 ? launch_varlen_tile<7, false>(args, stream) : launch_varlen_tile<5, false>(args, stream);
+  }
   if (args.glog != kNoVec && ((reinterpret_cast<uintptr_t>(args.frames) |
                               reinterpret_cast<uintptr_t>(args.payload)) & 15u) == 0) {
     const uint64_t blocks = (args.n + (kBlock >> args.glog) - 1) / (kBlock >> args.glog);
-    if (layout == 7)
-      hipLaunchKernelGGL(encode_varlen_vec_kernel<7>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
-    else
-      hipLaunchKernelGGL(encode_varlen_vec_kernel<5>, dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
-    return (int)hipGetLastError();
+    const void* fn = layout == 7 ? (fx ? reinterpret_cast<const void*>(&encode_varlen_vec_kernel<7, true>)
+                                       : reinterpret_cast<const void*>(&encode_varlen_vec_kernel<7, false>))
+                                 : (fx ? reinterpret_cast<const void*>(&encode_varlen_vec_kernel<5, true>)
+                                       : reinterpret_cast<const void*>(&encode_varlen_vec_kernel<5, false>));
+    void* kargs[] = {const_cast<VarlenArgs*>(&args)};
+    return (int)hipLaunchKernel(fn, dim3((uint32_t)blocks), dim3(kBlock), kargs, 0, stream);
   }
   const uint64_t blocks = (args.n * kVarLanes + kBlock - 1) / kBlock;
   if (layout == 7)
@@ -2390,10 +2411,10 @@ int launch_encode_varlen(const VarlenArgs& args, int layout, hipStream_t stream)
 // Every varlen decode form validates the payload's UTF-8 in the same pass when
 // args.valid is set (U8): the reference's receive decodes every payload
 // (utils/reliableUDP.py:121, get_payload's strict decode at utils/packet.py:73).
-template <int H, bool U8>
+template <int H, bool U8, bool FX>
 static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
 #if RUDP_TOOLS  // byte spans (measured slower; the diagnostics build only)
-  if (args.span_rec) {  // byte spans: the index pass, then one workgroup per span (or per T frames)
+  if (!FX && args.span_rec) {  // byte spans: the index pass, then one workgroup per span (or per T frames)
     const uint32_t nt = (uint32_t)args.span_count;
     const uint64_t idx_threads = args.n + 2u + nt;
     hipLaunchKernelGGL(decode_span_index_kernel, dim3((uint32_t)((idx_threads + kBlock - 1) / kBlock)), dim3(kBlock),
@@ -2408,7 +2429,7 @@ static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
   }
 #endif
   if (args.small_fpt && args.glog != kNoVec && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0)
-    return launch_decode_small<H, U8>(args, stream);
+    return launch_decode_small<H, U8, FX>(args, stream);
   if (args.glog != kNoVec && args.tile_cap && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0) {
     const uint32_t T = kBlock >> args.glog;
     const size_t lds = dvt_lds_bytes(T, args.tile_cap, args.tile_sums == 2u);
@@ -2418,6 +2439,7 @@ static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
       // spills and was slower at every size (1M x 1479 B 0.265 -> 0.306 ms;
       // profiles/r01/sweeps/varlen_decode_waves.json).
 #if RUDP_TOOLS  // chunks read four at a time and two-wave tiles: measured slower
+      if constexpr (!FX) {
       if (args.dec_r4) {
         hipLaunchKernelGGL((decode_varlen_tile_kernel<H, U8, kBlock, true>), dim3((uint32_t)blocks), dim3(kBlock),
                            lds, stream, args);
@@ -2429,14 +2451,16 @@ static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
                            args);
         return (int)hipGetLastError();
       }
+      }
 #endif
-      hipLaunchKernelGGL((decode_varlen_tile_kernel<H, U8>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
+      hipLaunchKernelGGL((decode_varlen_tile_kernel<H, U8, kBlock, false, FX>), dim3((uint32_t)blocks), dim3(kBlock),
+                         lds, stream, args);
       return (int)hipGetLastError();
     }
   }
   if (args.glog != kNoVec && (reinterpret_cast<uintptr_t>(args.frames) & 15u) == 0) {
     const uint64_t blocks = (args.n + (kBlock >> args.glog) - 1) / (kBlock >> args.glog);
-    hipLaunchKernelGGL((decode_varlen_vec_kernel<H, U8>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
+    hipLaunchKernelGGL((decode_varlen_vec_kernel<H, U8, FX>), dim3((uint32_t)blocks), dim3(kBlock), 0, stream, args);
     return (int)hipGetLastError();
   }
   const uint64_t blocks = (args.n * kVarLanes + kBlock - 1) / kBlock;
@@ -2450,9 +2474,18 @@ bool decode_span_fits(uint64_t cap) { return cap < 65536u && dsp_lds_bytes((uint
 
 int launch_decode_varlen(const VarlenArgs& args, int layout, hipStream_t stream) {
   if (args.n == 0) return 0;
+  if (args.frame_off == nullptr) {  // a fixed-stride batch (VarlenArgs::stride)
+    if (args.valid)
+      return layout == 7 ? launch_decode_varlen_t<7, true, true>(args, stream)
+                         : launch_decode_varlen_t<5, true, true>(args, stream);
+    return layout == 7 ? launch_decode_varlen_t<7, false, true>(args, stream)
+                       : launch_decode_varlen_t<5, false, true>(args, stream);
+  }
   if (args.valid)
-    return layout == 7 ? launch_decode_varlen_t<7, true>(args, stream) : launch_decode_varlen_t<5, true>(args, stream);
-  return layout == 7 ? launch_decode_varlen_t<7, false>(args, stream) : launch_decode_varlen_t<5, false>(args, stream);
+    return layout == 7 ? launch_decode_varlen_t<7, true, false>(args, stream)
+                       : launch_decode_varlen_t<5, true, false>(args, stream);
+  return layout == 7 ? launch_decode_varlen_t<7, false, false>(args, stream)
+                     : launch_decode_varlen_t<5, false, false>(args, stream);
 }
 
 int launch_validate_utf8(const Utf8Args& args, hipStream_t stream) {

@@ -81,8 +81,8 @@ def _check_decode(got, frames, H, csum_in=None, utf8=True):
 def test_stride_goldens(cuda, golden_small, layout):
     """Every golden length that is not a multiple of 16 (0, 1, 2, 3, 15, 17, 31,
     100): frames equal the reference's to_byte(), the reference-framed batches
-    decode to the fields the reference read back, with valid = 1 (the goldens'
-    payloads come through the str API: ASCII) and the payloads copied out."""
+    decode to the fields the reference read back, with Python's strict-decoder
+    answer for each (full-range payloads) and the payloads copied out."""
     for L in small_lengths(golden_small):
         if L % 16 == 0 and L:
             continue
@@ -97,7 +97,8 @@ def test_stride_goldens(cuda, golden_small, layout):
         assert np.array_equal(host(d.seq), ref[:, 0]) and np.array_equal(host(d.ack), ref[:, 1]), L
         assert np.array_equal(host(d.flags), ref[:, 2]), L
         assert np.array_equal(host(d.payload), full[:, layout:]), L
-        assert (host(d.valid) == 1).all(), L
+        off = np.arange(full.shape[0] + 1, dtype=np.int64) * full.shape[1]
+        assert np.array_equal(host(d.valid), codec_np.utf8_valid(full.reshape(-1), off, layout)), L
         assert (host(d.ok) == (1 if layout == 7 else 3)).all(), L
 
 
