@@ -47,6 +47,21 @@ int hip_fail(hipError_t e, const char* what) {
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
+// Host memory the device can store to at the same address (pinned by
+// hipHostMalloc / hipHostRegister, e.g. torch's pinned allocator): the *_host
+// decode's kernels then write their per-frame outputs straight into the
+// caller's arrays over PCIe, with no device copy and no D2H copy per chunk.
+// Null is "nothing to write" and counts as visible; pageable memory is not.
+bool device_writable_host(const void* p) {
+  if (!p) return true;
+  hipPointerAttribute_t attr{};
+  if (hipPointerGetAttributes(&attr, p) != hipSuccess) {
+    (void)hipGetLastError();  // (pageable memory: the query's error is not the caller's)
+    return false;
+  }
+  return attr.type == hipMemoryTypeHost && attr.devicePointer == p;
+}
+
 uint64_t mix64(uint64_t z) {
   z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
   z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
@@ -570,13 +585,14 @@ int encode_stride(const rudp_batch* in, uint8_t* d_frames, uint16_t* d_csum, int
   return launch_encode_varlen(a, layout, s);
 }
 
-// Adds a chunk's base to the frame offsets its encode wrote from 0, and ORs
-// the chunk's device status into the call's (the chunks' kernels run in
+// Adds a chunk's base to the frame offsets its encode wrote from 0 -- in
+// place, or into the caller's pinned host array (`out`, no D2H copy) -- and
+// ORs the chunk's device status into the call's (the chunks' kernels run in
 // stream order on one stream, so a plain read-modify-write by one thread).
-__global__ void __launch_bounds__(256) add_base_kernel(uint64_t* off, uint64_t n1, uint64_t base, const uint32_t* st,
-                                                      uint32_t* acc) {
+__global__ void __launch_bounds__(256) add_base_kernel(uint64_t* off, uint64_t* out, uint64_t n1, uint64_t base,
+                                                      const uint32_t* st, uint32_t* acc) {
   const uint64_t i = (uint64_t)blockIdx.x * 256u + threadIdx.x;
-  if (i < n1 && base) off[i] += base;
+  if (i < n1 && (base || out != off)) out[i] = off[i] + base;
   if (i == 0) {
     const uint32_t v = *st;
     if (v) *acc |= v;
@@ -1235,6 +1251,14 @@ int rudp_encode_varlen_host(const rudp_batch* h_in, uint64_t payload_bytes, uint
   DeviceScope dev_scope;
   int rc = dev_scope.set(device);
   if (rc) return rc;
+  // Pinned offset / checksum arrays: for chunks that take the small-frame tile
+  // (its checksums leave as coalesced stores) the kernels store them directly,
+  // two D2H copies per chunk fewer; the frames always come back by one copy.
+  const bool pinned_out = tuning().host_direct_out && device_writable_host(h_frame_off) &&
+                          device_writable_host(h_csum_or_null);
+  auto direct_chunk = [&](uint64_t pb, uint64_t m) {
+    return pinned_out && tuning().varlen_small > 0 && pb / m < (uint64_t)tuning().varlen_small;
+  };
   const size_t o_pay = 0, o_fr = up256(bmax), o_len = o_fr + up256(bmax + cn * H + 64u),
                o_seq = o_len + up256(cn * 4), o_ack = o_seq + up256(cn * 2), o_fl = o_ack + up256(cn * 2),
                o_cs = o_fl + up256(cn), o_off = o_cs + up256(cn * 2), o_st = o_off + up256((cn + 1) * 8),
@@ -1270,19 +1294,25 @@ int rudp_encode_varlen_host(const rudp_batch* h_in, uint64_t payload_bytes, uint
     sub.flags = (const uint8_t*)(base + o_fl);
     sub.payload = (const uint8_t*)(base + o_pay);
     sub.len = (const uint32_t*)(base + o_len);
+    const bool direct = direct_chunk(pb, m);
+    uint16_t* cs = h_csum_or_null ? (direct ? h_csum_or_null + p0 : (uint16_t*)(base + o_cs)) : nullptr;
     int r = rudp_encode_varlen_checked(&sub, pb, (uint8_t*)(base + o_fr), pb + m * H + 64u, (uint64_t*)(base + o_off),
-                                       h_csum_or_null ? (uint16_t*)(base + o_cs) : nullptr, (uint32_t*)(base + o_st),
-                                       layout, device, s);
+                                       cs, (uint32_t*)(base + o_st), layout, device, s);
     if (r) return r;
     const uint64_t fbase = pbase + p0 * H;
-    hipLaunchKernelGGL(add_base_kernel, dim3(fbase ? (uint32_t)((m + 256u) / 256u) : 1u), dim3(256), 0, s,
-                       (uint64_t*)(base + o_off), m + 1, fbase, (const uint32_t*)(base + o_st), pp->d_status);
+    // offsets [p0, p0 + m): the chunk's last entry is the next chunk's first
+    const uint64_t last = start[k] == n ? m + 1 : m;
+    uint64_t* off = (uint64_t*)(base + o_off);
+    hipLaunchKernelGGL(add_base_kernel, dim3(fbase || direct ? (uint32_t)((m + 256u) / 256u) : 1u), dim3(256), 0, s,
+                       off, direct ? h_frame_off + p0 : off, direct ? last : m + 1, fbase,
+                       (const uint32_t*)(base + o_st), pp->d_status);
     RUDP_HIP(hipGetLastError());
     return 0;
   };
   auto d2h = [&](char* base, uint64_t p0, uint64_t m, hipStream_t s) -> int {
     const uint64_t fb = pay[k - 1] + m * H;
     RUDP_HIP(hipMemcpyAsync(h_frames + pbase + p0 * H, base + o_fr, fb, hipMemcpyDeviceToHost, s));
+    if (direct_chunk(pay[k - 1], m)) return 0;  // offsets and checksums stored by the kernels
     // offsets [p0, p0 + m): the chunk's last entry is the next chunk's first
     const uint64_t last = start[k] == n ? m + 1 : m;
     RUDP_HIP(hipMemcpyAsync(h_frame_off + p0, base + o_off, last * 8, hipMemcpyDeviceToHost, s));
@@ -1330,6 +1360,16 @@ int rudp_decode_varlen_host(const uint8_t* h_frames, uint64_t frames_bytes, cons
   if (rc) return rc;
   const uint64_t hint = len_hint ? len_hint : (frames_bytes / n ? frames_bytes / n : 1u);
   const uint64_t bmax = stage_bytes();  // frame bytes a slot holds
+  // Pinned output arrays: the small-frame decode tile (the reference's 6-9 B
+  // datagrams; its per-frame outputs leave as lane-strided, coalesced stores)
+  // writes the fields into them directly: six D2H copies per chunk fewer.
+  // Pageable arrays, and MTU frames (whose fields a group leader stores one at
+  // a time: 2-B PCIe writes), take the slot and the copies.
+  const bool direct = tuning().host_direct_out && tuning().varlen_small > 0 &&
+                      hint < (uint64_t)tuning().varlen_small + (uint64_t)layout && device_writable_host(h_seq) &&
+                      device_writable_host(h_ack) &&
+                      device_writable_host(h_flags) && device_writable_host(h_ok) &&
+                      device_writable_host(h_csum_out_or_null) && device_writable_host(h_valid_or_null);
   // frames per chunk: 3/4 of a slot's bytes at the hint (room for ragged
   // lengths), at least host_min_chunks chunks for a batch over 4 MiB
   uint64_t cn = chunk_packets(n, hint * 4u / 3u + 1u);
@@ -1380,16 +1420,22 @@ int rudp_decode_varlen_host(const uint8_t* h_frames, uint64_t frames_bytes, cons
       RUDP_HIP(hipMemcpyAsync(base + o_ci, h_csum_in_or_null + p0, m * 2, hipMemcpyHostToDevice, s));
     return 0;
   };
-  auto kern = [&](char* base, uint64_t, uint64_t m, hipStream_t s) -> int {
+  auto kern = [&](char* base, uint64_t p0, uint64_t m, hipStream_t s) -> int {
     // frame bytes at offset x (a0 <= x < a1) sit at base + (x - a0)
     const uint8_t* frames = reinterpret_cast<const uint8_t*>(base + o_fr) - a0;
-    return decode_varlen(frames, (const uint64_t*)(base + o_off), (uint32_t)(hint < 0xFFFFFFFFull ? hint : 0xFFFFFFFFu),
-                         m, h_csum_in_or_null ? (const uint16_t*)(base + o_ci) : nullptr, (uint16_t*)(base + o_seq),
+    const uint32_t h32 = (uint32_t)(hint < 0xFFFFFFFFull ? hint : 0xFFFFFFFFu);
+    const uint16_t* ci = h_csum_in_or_null ? (const uint16_t*)(base + o_ci) : nullptr;
+    if (direct)
+      return decode_varlen(frames, (const uint64_t*)(base + o_off), h32, m, ci, h_seq + p0, h_ack + p0, h_flags + p0,
+                           h_ok + p0, h_csum_out_or_null ? h_csum_out_or_null + p0 : nullptr, nullptr, layout, device,
+                           s, true, nullptr, frames_bytes, h_valid_or_null ? h_valid_or_null + p0 : nullptr);
+    return decode_varlen(frames, (const uint64_t*)(base + o_off), h32, m, ci, (uint16_t*)(base + o_seq),
                          (uint16_t*)(base + o_ack), (uint8_t*)(base + o_fl), (uint8_t*)(base + o_ok),
                          h_csum_out_or_null ? (uint16_t*)(base + o_co) : nullptr, nullptr, layout, device, s, true,
                          nullptr, frames_bytes, h_valid_or_null ? (uint8_t*)(base + o_va) : nullptr);
   };
   auto d2h = [&](char* base, uint64_t p0, uint64_t m, hipStream_t s) -> int {
+    if (direct) return 0;  // the kernel wrote them
     RUDP_HIP(hipMemcpyAsync(h_seq + p0, base + o_seq, m * 2, hipMemcpyDeviceToHost, s));
     RUDP_HIP(hipMemcpyAsync(h_ack + p0, base + o_ack, m * 2, hipMemcpyDeviceToHost, s));
     RUDP_HIP(hipMemcpyAsync(h_flags + p0, base + o_fl, m, hipMemcpyDeviceToHost, s));

@@ -394,6 +394,9 @@ struct Tuning {
   RUDP_KNOB(host_slots, 3)     // *_host pipeline: device staging slots (2..8)
   RUDP_KNOB(host_stage_mb, 128)  // *_host pipeline: MiB per slot (1M x 1472 B pinned: 33 ms at 128 vs 94 ms at 32)
   RUDP_KNOB(host_min_chunks, 4)  // *_host pipeline: batches over 4 MiB go as at least this many chunks (copy overlap)
+  // *_host varlen decode: kernels store the per-frame outputs straight into the
+  // caller's pinned arrays (1), or into the slot and D2H copies (0).
+  RUDP_KNOB(host_direct_out, 1)
 
 };
 #undef RUDP_KNOB

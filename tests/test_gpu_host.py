@@ -305,3 +305,74 @@ def test_varlen_host_encode_rejects(cuda):
                                                  None, 7, 0) == _native.EINVAL
     assert b"sum" in _native.lib().rudp_last_error()
     assert not fr.any()
+
+
+def test_varlen_host_decode_wide_descending_pair(cuda):
+    """a descending pair whose offsets lie far apart inside a buffer
+    larger than a staging slot (here 2.5 MiB -> 7 with 1-MiB slots) is rejected
+    as the device-resident checked decode rejects it (ok = 4), not refused with
+    RUDP_ENOTSUP; only a VALID frame over a slot is refused."""
+    rng = np.random.default_rng(8)
+    H = 7
+    nb = 3 << 20
+    flat = rng.integers(0x20, 0x7F, nb).astype(np.uint8)
+    hi = 5 * (1 << 19)  # 2.5 MiB
+    off = np.array([0, 7, 14, nb + 5, hi, hi + 7, hi + 14, 7, 14, 21], np.int64)
+    with _Knobs(stage_mb=1, slots=2):
+        d = batch.unpack_batch_varlen(flat, off, H, utf8=True, check=False)
+        got, want = _host_fields(d), _device_varlen(cuda, flat, off, H)
+    for k in want:
+        assert np.array_equal(got[k], want[k]), k
+    assert got["ok"][2] == 4 and got["ok"][3] == 4 and got["ok"][6] == 4
+    assert got["ok"][4] != 4 and got["ok"][7] != 4
+
+
+@pytest.mark.parametrize("direct", [1, 0])
+def test_varlen_host_one_char_outputs_direct_or_copied(cuda, direct):
+    """1-char datagrams through the host entries with the per-frame outputs
+    stored by the kernels straight into the pinned arrays (knob 73 = 1, the
+    product's form) or copied back from the slot (0), and through the raw C
+    ABI into PAGEABLE numpy arrays (always copied): every form equals the
+    device-resident decode / the oracle's frames, across many chunks."""
+    rng = np.random.default_rng(73 + direct)
+    n, H = 200003, 5
+    lens = np.ones(n, np.int32)
+    seq, ack = rng.integers(0, 1 << 16, n).astype(np.uint16), rng.integers(0, 1 << 16, n).astype(np.uint16)
+    flags = rng.choice(np.array([0, 0x80, 0x20, 0xA0, 0x40, 0x60], np.uint8), n)
+    pay = rng.integers(0x20, 0x80, n).astype(np.uint8)
+    pay[::1001] = 0xC3  # a lone lead byte: invalid UTF-8
+    want_fr, want_off, want_cs = _oracle_varlen(seq, ack, flags, lens, pay, H)
+    with _Knobs(stage_mb=1, slots=3) as lib:
+        lib.rudpx_tune(73, direct)
+        try:
+            r = batch.pack_batch_varlen((seq, ack, flags), pay, lens, H, want_csum=True)
+            assert np.array_equal(r.frames, want_fr) and np.array_equal(r.frame_off, want_off)
+            assert np.array_equal(r.csum, want_cs)
+            d = batch.unpack_batch_varlen(want_fr, want_off, H, csum=want_cs, utf8=True)
+            got = _host_fields(d)
+            # pageable outputs through the raw entry (the copy path whatever the knob)
+            pg = {k: np.full(n, 0xAB, dt) for k, dt in (("seq", np.uint16), ("ack", np.uint16), ("flags", np.uint8),
+                                                        ("ok", np.uint8), ("csum", np.uint16), ("valid", np.uint8))}
+            st = np.zeros(1, np.uint32)
+            rc = lib.rudp_decode_varlen_host(want_fr.ctypes.data, want_fr.size, want_off.ctypes.data, 0, n,
+                                             want_cs.ctypes.data, *[pg[k].ctypes.data for k in
+                                                                    ("seq", "ack", "flags", "ok", "csum", "valid")],
+                                             st.ctypes.data, H, 0)
+            assert rc == 0
+            fo = np.zeros(n + 1, np.uint64)
+            cs = np.zeros(n, np.uint16)
+            fr = np.zeros(want_fr.size, np.uint8)
+            b = _native.RudpBatch(n=n, payload_len=1, reserved=0, seq=seq.ctypes.data, ack=ack.ctypes.data,
+                                  flags=flags.ctypes.data, payload=pay.ctypes.data, len=lens.ctypes.data,
+                                  payload_off=None)
+            assert lib.rudp_encode_varlen_host(ctypes.byref(b), pay.size, fr.ctypes.data, fr.size, fo.ctypes.data,
+                                               cs.ctypes.data, H, 0) == 0
+        finally:
+            lib.rudpx_tune(73, 1)
+    want = _device_varlen(cuda, want_fr, want_off, H, want_cs)
+    for k in want:
+        assert np.array_equal(got[k], want[k]), (k, direct)
+        assert np.array_equal(pg[k], want[k]), (k, direct)
+    assert (got["ok"] == 1).all() and got["valid"].sum() == n - len(range(0, n, 1001))
+    assert np.array_equal(fr, want_fr) and np.array_equal(fo.astype(np.int64), want_off)
+    assert np.array_equal(cs, want_cs)
