@@ -1677,12 +1677,16 @@ __host__ __device__ inline uint32_t small_out_cap(uint32_t T, uint32_t cap, uint
 // FIXED (a fixed-stride batch, frame_off null): tile t's base is fo_at(t T),
 // every length is stride - H; no scan, no offsets written, one launch.
 constexpr uint64_t kSmallFusedTiles = 2048;
-enum SmallMode { kSmallBases = 0, kSmallFused = 1, kSmallSingle = 2, kSmallFixed = 3 };
+// FUSED_NIB: FUSED with pass 1's 4-bit length codes (VarlenArgs::len_nib) in
+// place of len[] (a code of 15 reads len[] for that packet): len[] leaves HBM
+// once per call instead of twice.
+enum SmallMode { kSmallBases = 0, kSmallFused = 1, kSmallSingle = 2, kSmallFixed = 3, kSmallFusedNib = 4 };
 
 template <int H, uint32_t FPT, int MODE>
 __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs a, const uint64_t* sums,
                                                                      uint64_t nb, ScanCheck chk) {
-  constexpr bool FUSED = MODE == kSmallFused, SINGLE = MODE == kSmallSingle, FIXED = MODE == kSmallFixed;
+  constexpr bool FUSED = MODE == kSmallFused || MODE == kSmallFusedNib, SINGLE = MODE == kSmallSingle,
+                 FIXED = MODE == kSmallFixed, NIB = MODE == kSmallFusedNib;
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   constexpr uint32_t T = kBlock * FPT;
   const uint32_t tid = threadIdx.x;
@@ -1712,10 +1716,19 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
     const uint32_t q = j * kBlock + tid;
     lv[j] = sq[j] = ak[j] = fl[j] = 0;
     if (q < Tv) {
-      lv[j] = FIXED ? (uint32_t)a.stride - (uint32_t)H : a.len[p0 + q];
+      lv[j] = FIXED ? (uint32_t)a.stride - (uint32_t)H : NIB ? 0u : a.len[p0 + q];
       sq[j] = a.seq_in[p0 + q];
       ak[j] = a.ack_in[p0 + q];
       fl[j] = a.flags_in[p0 + q];
+    }
+  }
+  if (NIB) {
+    const uint32_t code = a.len_nib[tile * kBlock + tid];
+#pragma unroll
+    for (uint32_t j = 0; j < FPT; ++j) {
+      const uint32_t q = j * kBlock + tid;
+      const uint32_t c = (code >> (4u * j)) & 15u;
+      lv[j] = q < Tv ? (c < 15u ? c : a.len[p0 + q]) : 0u;
     }
   }
   if (FUSED) {
@@ -1920,8 +1933,9 @@ int launch_small_fpt(const VarlenArgs& args, const uint64_t* sums, uint64_t nb, 
                      bool fused, hipStream_t stream) {
   constexpr uint32_t T = kBlock * FPT;
   const size_t lds = small_lds_off_out(T, args.small_cap) + small_out_cap(T, args.small_cap, H) + 32u;
-  const int mode = sums == nullptr ? kSmallSingle : fused ? kSmallFused : kSmallBases;
+  const int mode = sums == nullptr ? kSmallSingle : fused ? (args.len_nib ? kSmallFusedNib : kSmallFused) : kSmallBases;
   const void* fn = mode == kSmallSingle ? reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT, kSmallSingle>)
+                 : mode == kSmallFusedNib ? reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT, kSmallFusedNib>)
                  : mode == kSmallFused  ? reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT, kSmallFused>)
                                         : reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT, kSmallBases>);
   if (lds > 65536) {
@@ -1931,6 +1945,9 @@ int launch_small_fpt(const VarlenArgs& args, const uint64_t* sums, uint64_t nb, 
   if (mode == kSmallSingle)
     hipLaunchKernelGGL((encode_varlen_small_kernel<H, FPT, kSmallSingle>), dim3(1), dim3(kBlock), lds, stream,
                        args, sums, nb, chk);
+  else if (mode == kSmallFusedNib)
+    hipLaunchKernelGGL((encode_varlen_small_kernel<H, FPT, kSmallFusedNib>), dim3((uint32_t)nb), dim3(kBlock), lds,
+                       stream, args, sums, nb, chk);
   else if (mode == kSmallFused)
     hipLaunchKernelGGL((encode_varlen_small_kernel<H, FPT, kSmallFused>), dim3((uint32_t)nb), dim3(kBlock), lds,
                        stream, args, sums, nb, chk);
@@ -2072,10 +2089,17 @@ int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int
   // pass 1, then either the framing kernel finds its own base (two launches)
   // or pass 2 runs between them (three)
   const bool fused = tuning().varlen_small_fused && nb <= kSmallFusedTiles;
-  scan_block_sums(args.len, args.n, (uint32_t)layout, fpt, sums, chk, stream);
+  VarlenArgs a = args;
+  if (fused && tuning().varlen_small_nib && fpt <= 4u) {
+    void* nib = nullptr;  // (the records' slot: the MTU tile's, never used by a small-frame call)
+    e = stream_scratch(&nib, nb * kBlock * sizeof(uint16_t), stream, kScratchRecords);
+    if (e != hipSuccess) return (int)e;
+    a.len_nib = static_cast<const uint16_t*>(nib);
+  }
+  scan_block_sums(args.len, args.n, (uint32_t)layout, fpt, sums, chk, stream, 0u, 0u, const_cast<uint16_t*>(a.len_nib));
   if (!fused) scan_block_bases(sums, nb, const_cast<uint64_t*>(args.frame_off), args.n, (uint32_t)layout, chk, stream);
-  return layout == 7 ? launch_small_any<7>(args, sums, nb, chk, fused, stream)
-                     : launch_small_any<5>(args, sums, nb, chk, fused, stream);
+  return layout == 7 ? launch_small_any<7>(a, sums, nb, chk, fused, stream)
+                     : launch_small_any<5>(a, sums, nb, chk, fused, stream);
 }
 
 // Small-frame decode: a tile of T = 256 * FPT consecutive frames (the

@@ -818,9 +818,11 @@ def test_small_frame_tiles_vs_oracle(cuda, fpt):
         for layout in (5, 7):
             want, off, cs = codec_np.encode_varlen(seq, ack, flags, pays, layout)
             results = []
-            # the small-frame kernels (own tile bases, then after the pass-2 launch), then the vector kernels
-            for small, fused in ((16, 1), (16, 0), (0, 1)):
-                old = (lib.rudpx_tune(46, small), lib.rudpx_tune(47, fpt), lib.rudpx_tune(50, fused))
+            # the small-frame kernels (own tile bases: lengths from pass 1's 4-bit codes, code 15
+            # reading len[] again, or from len[]; then after the pass-2 launch), then the vector kernels
+            for small, fused, nib in ((16, 1, 1), (16, 1, 0), (16, 0, 1), (0, 1, 1)):
+                old = (lib.rudpx_tune(46, small), lib.rudpx_tune(47, fpt), lib.rudpx_tune(50, fused),
+                       lib.rudpx_tune(74, nib))
                 try:
                     r = batch.pack_batch_varlen((dev(seq, cuda), dev(ack, cuda), dev(flags, cuda)), dev(pay, cuda),
                                                 dev(lens, cuda), layout, want_csum=True, check=False).check()
@@ -837,14 +839,15 @@ def test_small_frame_tiles_vs_oracle(cuda, fpt):
                     lib.rudpx_tune(46, old[0])
                     lib.rudpx_tune(47, old[1])
                     lib.rudpx_tune(50, old[2])
-                ctx = (fpt, n, layout, small, fused)
+                    lib.rudpx_tune(74, old[3])
+                ctx = (fpt, n, layout, small, fused, nib)
                 assert np.array_equal(host(r.frames), want), ctx
                 assert np.array_equal(host(r.frame_off), off) and np.array_equal(host(r.csum), cs), ctx
                 exp = codec_np.decode_varlen(want, off, layout, cs if layout == 5 else None)
                 for g, e in zip((d.seq, d.ack, d.flags, d.ok, d.csum), exp):
                     assert np.array_equal(host(g), e), ctx
                 results.append(host(r.frames))
-            assert np.array_equal(results[0], results[1]) and np.array_equal(results[0], results[2])
+            assert all(np.array_equal(results[0], x) for x in results[1:])
 
 
 @pytest.mark.parametrize("dist", ["ragged", "equal", "bursty", "tiny_runs", "zeros", "jumbo", "threshold"])

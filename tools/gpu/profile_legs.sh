@@ -25,10 +25,13 @@ declare -A LEG=(
   [venc1c]="--op encode_varlen --L 1 --layout rudp5 --steps 80"
   [vdec1c]="--op decode_varlen --L 1 --layout rudp5 --steps 80"
   [vdecu8_1c]="--op decode_varlen --utf8 --L 1 --layout rudp5 --steps 80"
+  [senc1c]="--op encode --L 1 --layout rudp5 --steps 80"
+  [sdecu8_1c]="--op decode --utf8 --L 1 --layout rudp5 --steps 80"
+  [senc1000]="--op encode --L 1000 --steps 40"
 )
 legs=("$@")
 [ ${#legs[@]} -eq 0 ] && legs=(enc1472 enc1024 enc64 dec1472 decu8_1472 decu8text enc16M venc1472 vdec1472 vdecu8_1472 \
-                               vencrag vdecrag vdecu8rag utf8 dedup venc1c vdec1c vdecu8_1c)
+                               vencrag vdecrag vdecu8rag utf8 dedup venc1c vdec1c vdecu8_1c senc1c sdecu8_1c senc1000)
 for leg in "${legs[@]}"; do
   bash tools/gpu/run.sh trace ${P}_${leg}_kt $R ${LEG[$leg]}
   bash tools/gpu/run.sh pmc ${P}_${leg} $R ${LEG[$leg]} --steps 10
