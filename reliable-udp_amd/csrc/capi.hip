@@ -853,6 +853,7 @@ static int encode_varlen(const rudp_batch* in, uint8_t* d_frames, uint64_t* d_fr
     const uint64_t T = (uint64_t)256u * a.small_fpt;
     const uint64_t hint = in->payload_len ? in->payload_len : 1u;
     a.small_cap = (uint32_t)((T * hint * 5u / 4u + 256u + 15u) & ~15ull);
+    a.len_code_base = in->payload_len;  // (pass 1's length codes count from the hint)
 #if RUDP_TOOLS
     a.trace = tuning().encode_trace.load();
 #endif

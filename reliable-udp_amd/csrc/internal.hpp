@@ -180,9 +180,11 @@ struct VarlenArgs {
   uint64_t fo_base;
   uint64_t stride;
   uint64_t po_delta;
-  // Small-frame encode after a pass 1 (varlen_small_nib): the lengths as 4-bit
-  // codes, one u16 per thread of each tile (15: read len[]); null: len[] only.
-  const uint16_t* len_nib;
+  // Small-frame encode after a pass 1 (varlen_small_nib): each thread's fpt
+  // lengths as 8/fpt-bit offsets from len_code_base in one byte per thread of
+  // each tile (all ones: read len[]); null: len[] only.
+  const uint8_t* len_code;
+  uint32_t len_code_base;
 };
 constexpr uint32_t kNoVec = 0xFFFFFFFFu;
 
@@ -355,8 +357,9 @@ struct Tuning {
   RUDP_KNOB(varlen_small_fpt, 0)  // 0: 4 for hints up to 4 B, 2 above (profiles/r02/sweeps/small.json)
   RUDP_KNOB(varlen_small_fused, 1)  // the framing kernel finds its own base (no pass-2 launch)
   RUDP_KNOB(varlen_small_single, 1)  // a checked call that is one small-frame tile: one launch, no pass 1
-  // Small-frame encode: pass 1 leaves the lengths as 4-bit codes for the framing
-  // kernel (1), which then reads 0.5 B per packet instead of len[]'s 4 (0: len[]).
+  // Small-frame encode: pass 1 leaves the lengths as 2-bit (4 packets a thread)
+  // or 4-bit (2) codes for the framing kernel (1), which then reads 0.25-0.5 B
+  // per packet instead of len[]'s 4 (0: len[]).
   RUDP_KNOB(varlen_small_nib, 1)
   // Checked varlen decode by byte spans: a workgroup decodes the frames that
   // start in one span of varlen_decode_span_bytes, its lanes over the bytes
@@ -491,7 +494,7 @@ struct ScanCheck {
 // bits), then the exclusive block bases in place, frame_off[n] and the status.
 void scan_block_sums(const uint32_t* d_len, uint64_t n, uint32_t H, uint32_t items, uint64_t* sums,
                      const ScanCheck& chk, hipStream_t stream, uint32_t over_T = 0, uint32_t over_cap = 0,
-                     uint16_t* nib = nullptr);
+                     uint8_t* codes = nullptr, uint32_t code_base = 0);
 void scan_block_bases(uint64_t* sums, uint64_t nb, uint64_t* d_frame_off, uint64_t n, uint32_t H,
                       const ScanCheck& chk, hipStream_t stream, uint32_t* ctl = nullptr, uint32_t min_over = 0);
 // Small-frame varlen encode of packed payloads (varlen.hip): the scan's first

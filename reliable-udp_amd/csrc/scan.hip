@@ -32,15 +32,17 @@ constexpr uint32_t kScanBlockItems = kBlock * kScanItems;  // 2048 per block
 // consecutive packets -- over_T consecutive lanes of one load -- whose length
 // sum + 30 (a bound on their 16-B aligned payload run) exceeds over_cap are
 // counted into bits 44-55 of the sum (at most 2048 tiles per block).
-// With nib (ITEMS <= 4, the small-frame encode's pass): every thread also
-// stores its ITEMS lengths as 4-bit codes in one u16, nib[block * kBlock +
-// thread] (code 15: 15 or more, read len[] again), so the framing kernel, which
-// takes the same packets per thread, reads 2 B per 4 packets instead of 16.
+// With codes (ITEMS 2 or 4, the small-frame encode's pass): every thread also
+// stores its ITEMS lengths in one byte, codes[block * kBlock + thread], as
+// 8 / ITEMS-bit offsets from code_base (the all-ones code: any other length,
+// read len[] again), so the framing kernel, which takes the same packets per
+// thread, reads 1 B per ITEMS packets instead of 4 B per packet.
 template <uint32_t ITEMS>
 __global__ void __launch_bounds__(kBlock) scan_block_sums_kernel(const uint32_t* len, uint64_t n,
                                                                  uint32_t H, uint64_t* sums,
                                                                  ScanCheck chk, uint32_t over_T,
-                                                                 uint32_t over_cap, uint16_t* nib) {
+                                                                 uint32_t over_cap, uint8_t* codes,
+                                                                 uint32_t code_base) {
   __shared__ uint64_t s_wave[kBlock / 64];
   __shared__ uint32_t s_bits, s_over;
   if (threadIdx.x == 0) s_bits = s_over = 0;
@@ -51,7 +53,11 @@ __global__ void __launch_bounds__(kBlock) scan_block_sums_kernel(const uint32_t*
   for (uint32_t j = 0; j < ITEMS; ++j) {
     const uint64_t i = base + j * kBlock + threadIdx.x;
     const uint32_t l = i < n ? len[i] : 0u;
-    if (ITEMS <= 4) code |= (l < 15u ? l : 15u) << (4u * j);
+    if (ITEMS == 2 || ITEMS == 4) {
+      constexpr uint32_t B = 8u / ITEMS, M = (1u << B) - 1u;
+      const uint32_t c = l - code_base;  // (below the base: wraps high, the escape)
+      code |= (c < M ? c : M) << (B * j);
+    }
     if (i < n) {
       acc += (uint64_t)l + H;
       if (chk.status) {
@@ -69,7 +75,7 @@ __global__ void __launch_bounds__(kBlock) scan_block_sums_kernel(const uint32_t*
       over += (uint32_t)__popcll(__ballot(o));
     }
   }
-  if (ITEMS <= 4 && nib) nib[(uint64_t)blockIdx.x * kBlock + threadIdx.x] = (uint16_t)code;
+  if ((ITEMS == 2 || ITEMS == 4) && codes) codes[(uint64_t)blockIdx.x * kBlock + threadIdx.x] = (uint8_t)code;
   acc = wave_sum64(acc);
   __syncthreads();  // s_bits, s_over initialised
   if (bits) atomicOr(&s_bits, bits);
@@ -221,15 +227,19 @@ __global__ void __launch_bounds__(kBlock) scan_apply_kernel(const uint32_t* len,
 }
 
 void scan_block_sums(const uint32_t* d_len, uint64_t n, uint32_t H, uint32_t items, uint64_t* sums,
-                     const ScanCheck& chk, hipStream_t stream, uint32_t over_T, uint32_t over_cap, uint16_t* nib) {
+                     const ScanCheck& chk, hipStream_t stream, uint32_t over_T, uint32_t over_cap, uint8_t* codes,
+                     uint32_t code_base) {
   const uint64_t nb = (n + kBlock * items - 1) / (kBlock * items);
   const dim3 grid((uint32_t)nb), block(kBlock);
   switch (items) {
-    case 1: hipLaunchKernelGGL(scan_block_sums_kernel<1>, grid, block, 0, stream, d_len, n, H, sums, chk, 0u, 0u, nib); break;
-    case 2: hipLaunchKernelGGL(scan_block_sums_kernel<2>, grid, block, 0, stream, d_len, n, H, sums, chk, 0u, 0u, nib); break;
-    case 4: hipLaunchKernelGGL(scan_block_sums_kernel<4>, grid, block, 0, stream, d_len, n, H, sums, chk, 0u, 0u, nib); break;
+    case 1: hipLaunchKernelGGL(scan_block_sums_kernel<1>, grid, block, 0, stream, d_len, n, H, sums, chk, 0u, 0u,
+                               nullptr, 0u); break;
+    case 2: hipLaunchKernelGGL(scan_block_sums_kernel<2>, grid, block, 0, stream, d_len, n, H, sums, chk, 0u, 0u,
+                               codes, code_base); break;
+    case 4: hipLaunchKernelGGL(scan_block_sums_kernel<4>, grid, block, 0, stream, d_len, n, H, sums, chk, 0u, 0u,
+                               codes, code_base); break;
     default: hipLaunchKernelGGL(scan_block_sums_kernel<8>, grid, block, 0, stream, d_len, n, H, sums, chk, over_T,
-                                over_cap, nullptr);
+                                over_cap, nullptr, 0u);
   }
 }
 

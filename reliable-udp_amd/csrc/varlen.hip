@@ -1677,9 +1677,10 @@ __host__ __device__ inline uint32_t small_out_cap(uint32_t T, uint32_t cap, uint
 // FIXED (a fixed-stride batch, frame_off null): tile t's base is fo_at(t T),
 // every length is stride - H; no scan, no offsets written, one launch.
 constexpr uint64_t kSmallFusedTiles = 2048;
-// FUSED_NIB: FUSED with pass 1's 4-bit length codes (VarlenArgs::len_nib) in
-// place of len[] (a code of 15 reads len[] for that packet): len[] leaves HBM
-// once per call instead of twice.
+// FUSED_NIB: FUSED with pass 1's length codes (VarlenArgs::len_code: 2 bits a
+// packet at 4 packets a thread, 4 at 2, offsets from the call's length hint;
+// the all-ones code reads len[] for that packet): len[] leaves HBM once per
+// call instead of twice.
 enum SmallMode { kSmallBases = 0, kSmallFused = 1, kSmallSingle = 2, kSmallFixed = 3, kSmallFusedNib = 4 };
 
 template <int H, uint32_t FPT, int MODE>
@@ -1723,12 +1724,13 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
     }
   }
   if (NIB) {
-    const uint32_t code = a.len_nib[tile * kBlock + tid];
+    constexpr uint32_t B = 8u / FPT, M = (1u << B) - 1u;
+    const uint32_t code = a.len_code[tile * kBlock + tid];
 #pragma unroll
     for (uint32_t j = 0; j < FPT; ++j) {
       const uint32_t q = j * kBlock + tid;
-      const uint32_t c = (code >> (4u * j)) & 15u;
-      lv[j] = q < Tv ? (c < 15u ? c : a.len[p0 + q]) : 0u;
+      const uint32_t c = (code >> (B * j)) & M;
+      lv[j] = q < Tv ? (c < M ? a.len_code_base + c : a.len[p0 + q]) : 0u;
     }
   }
   if (FUSED) {
@@ -1933,7 +1935,7 @@ int launch_small_fpt(const VarlenArgs& args, const uint64_t* sums, uint64_t nb, 
                      bool fused, hipStream_t stream) {
   constexpr uint32_t T = kBlock * FPT;
   const size_t lds = small_lds_off_out(T, args.small_cap) + small_out_cap(T, args.small_cap, H) + 32u;
-  const int mode = sums == nullptr ? kSmallSingle : fused ? (args.len_nib ? kSmallFusedNib : kSmallFused) : kSmallBases;
+  const int mode = sums == nullptr ? kSmallSingle : fused ? (args.len_code ? kSmallFusedNib : kSmallFused) : kSmallBases;
   const void* fn = mode == kSmallSingle ? reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT, kSmallSingle>)
                  : mode == kSmallFusedNib ? reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT, kSmallFusedNib>)
                  : mode == kSmallFused  ? reinterpret_cast<const void*>(&encode_varlen_small_kernel<H, FPT, kSmallFused>)
@@ -2090,13 +2092,18 @@ int launch_encode_varlen_small(const VarlenArgs& args, const ScanCheck& chk, int
   // or pass 2 runs between them (three)
   const bool fused = tuning().varlen_small_fused && nb <= kSmallFusedTiles;
   VarlenArgs a = args;
-  if (fused && tuning().varlen_small_nib && fpt <= 4u) {
-    void* nib = nullptr;  // (the records' slot: the MTU tile's, never used by a small-frame call)
-    e = stream_scratch(&nib, nb * kBlock * sizeof(uint16_t), stream, kScratchRecords);
+  if (fused && tuning().varlen_small_nib && (fpt == 2u || fpt == 4u)) {
+    void* codes = nullptr;  // (the records' slot: the MTU tile's, never used by a small-frame call)
+    e = stream_scratch(&codes, nb * kBlock, stream, kScratchRecords);
     if (e != hipSuccess) return (int)e;
-    a.len_nib = static_cast<const uint16_t*>(nib);
+    a.len_code = static_cast<const uint8_t*>(codes);
+    // codes are offsets from the caller's length hint: 2-bit codes (4 packets a
+    // thread) cover hint .. hint + 2, 4-bit ones hint - 7 .. hint + 7
+    const uint32_t h = args.len_code_base;
+    a.len_code_base = fpt == 4u ? h : (h > 7u ? h - 7u : 0u);
   }
-  scan_block_sums(args.len, args.n, (uint32_t)layout, fpt, sums, chk, stream, 0u, 0u, const_cast<uint16_t*>(a.len_nib));
+  scan_block_sums(args.len, args.n, (uint32_t)layout, fpt, sums, chk, stream, 0u, 0u, const_cast<uint8_t*>(a.len_code),
+                  a.len_code_base);
   if (!fused) scan_block_bases(sums, nb, const_cast<uint64_t*>(args.frame_off), args.n, (uint32_t)layout, chk, stream);
   return layout == 7 ? launch_small_any<7>(a, sums, nb, chk, fused, stream)
                      : launch_small_any<5>(a, sums, nb, chk, fused, stream);

@@ -38,14 +38,14 @@ LEGS = {
     "dedup": ("proxy_dedup_1M_window500", "dedup_small_kernel", 1 << 20, 1, 15),
     # (round 6: pass 1 also leaves 4-bit length codes, the framing kernel's mode 4; the setup's
     # fixed-length encode of the same payloads is mode 3 and stays out of the sums)
-    "venc1c": ("encode_varlen_small_1Mx1char", "scan_block_sums_kernel<4u>,encode_varlen_small_kernel<5, 4u, 4>",
+    "venc1c": ("encode_varlen_small_1Mx1char", "scan_block_sums_kernel<4u>|encode_varlen_small_kernel<5, 4u, 4>",
                1 << 20, 1, 26),
     # fixed-length batches off the 16-B grid (round 6): the varlen tiles with implicit offsets.
     # encode 2L + 10 (run_kernel frames rudp5 without the sideband checksum: read L + 5, write L + 5);
     # rudp7 2L + 12; decode + UTF-8 read F = 6,
     # write seq/ack/flags/ok/csum/valid 9
-    "senc1c": ("encode_fixed_1Mx1char", "encode_varlen_small_kernel<5, 4u, 3>", 1 << 20, 1, 12),
-    "sdecu8_1c": ("decode_utf8_fixed_1Mx1char", "decode_varlen_small_kernel<5, 4u, true, true>", 1 << 20, 1, 15),
+    "senc1c": ("encode_fixed_1Mx1char", "encode_varlen_small_kernel<5, 4u, 3>|", 1 << 20, 1, 12),
+    "sdecu8_1c": ("decode_utf8_fixed_1Mx1char", "decode_varlen_small_kernel<5, 4u, true, true>|", 1 << 20, 1, 15),
     "senc1000": ("encode_fixed_1Mx1000", "encode_varlen_tile_kernel", 1 << 20, 1000, 2012),
     "vdec1c": ("decode_varlen_small_1Mx1char", "decode_varlen_small_kernel", 1 << 20, 1, 24),
     "vdecu8_1c": ("decode_varlen_utf8_small_1Mx1char", "decode_varlen_small_kernel", 1 << 20, 1, 25),

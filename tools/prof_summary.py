@@ -85,7 +85,8 @@ def main():
     out_dir = REPO / "profiles" / args.round
     out_dir.mkdir(parents=True, exist_ok=True)
     shutil.copy(_one(args.kt, "kernel_stats.csv"), out_dir / f"{args.tag}_kernel_stats.csv")
-    names = [k for k in args.kernel.split(",") if k]
+    # (a "|"-separated list when a kernel's template arguments hold commas)
+    names = [k for k in args.kernel.split("|" if "|" in args.kernel else ",") if k]
     stats = [kernel_stats(args.kt, k) for k in names]
     avg_ns = sum(st["avg_ns"] for st in stats)
     alg = args.n * args.alg_bytes_per_unit
