@@ -1723,16 +1723,8 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
       fl[j] = a.flags_in[p0 + q];
     }
   }
-  if (NIB) {
-    constexpr uint32_t B = 8u / FPT, M = (1u << B) - 1u;
-    const uint32_t code = a.len_code[tile * kBlock + tid];
-#pragma unroll
-    for (uint32_t j = 0; j < FPT; ++j) {
-      const uint32_t q = j * kBlock + tid;
-      const uint32_t c = (code >> (B * j)) & M;
-      lv[j] = q < Tv ? (c < M ? a.len_code_base + c : a.len[p0 + q]) : 0u;
-    }
-  }
+  uint32_t code = 0;
+  if (NIB) code = a.len_code[tile * kBlock + tid];  // (decoded after the base's round trip)
   if (FUSED) {
     __shared__ uint64_t s_pre[kBlock / 64], s_all[kBlock / 64];
     __shared__ uint32_t s_bits;
@@ -1788,6 +1780,15 @@ __global__ void __launch_bounds__(kBlock) encode_varlen_small_kernel(VarlenArgs 
 #if RUDP_TOOLS
   const uint64_t t_base = a.trace ? (uint64_t)wall_clock64() : 0ull;
 #endif
+  if (NIB) {  // the lengths from pass 1's codes (an all-ones code: len[] for that packet)
+    constexpr uint32_t B = 8u / FPT, M = (1u << B) - 1u;
+#pragma unroll
+    for (uint32_t j = 0; j < FPT; ++j) {
+      const uint32_t q = j * kBlock + tid;
+      const uint32_t c = (code >> (B * j)) & M;
+      lv[j] = q < Tv ? (c < M ? a.len_code_base + c : a.len[p0 + q]) : 0u;
+    }
+  }
   const uint64_t po0 = fo0 - p0 * (uint64_t)H + (FIXED ? a.po_delta : 0ull);
   const uint64_t po_end = SINGLE ? chk.payload_bytes : fo_end - (p0 + Tv) * (uint64_t)H + (FIXED ? a.po_delta : 0ull);
   const uint64_t A = po0 & ~15ull, OA = fo0 & ~15ull;
