@@ -34,6 +34,9 @@ def main():
     ap.add_argument("--reps", type=int, default=7)
     ap.add_argument("--chunks", default="1,2,4,8,16")
     ap.add_argument("--slots", default="3")
+    ap.add_argument("--direct", default="1",
+                    help="knob 73 values: 1 = the kernels store the per-frame outputs into the pinned arrays, "
+                         "0 = slot + D2H copies")
     args = ap.parse_args()
     lib = _native.lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
@@ -78,18 +81,21 @@ def main():
             torch.cuda.synchronize()
         return f
 
-    variants = [(c, s) for s in map(int, args.slots.split(",")) for c in map(int, args.chunks.split(","))]
-    old_c, old_s = lib.rudpx_tune(71, 4), lib.rudpx_tune(8, 3)
+    variants = [(c, s, d) for d in map(int, args.direct.split(",")) for s in map(int, args.slots.split(","))
+                for c in map(int, args.chunks.split(","))]
+    old_c, old_s, old_d = lib.rudpx_tune(71, 4), lib.rudpx_tune(8, 3), lib.rudpx_tune(73, 1)
     lib.rudpx_tune(71, old_c)
     lib.rudpx_tune(8, old_s)
+    lib.rudpx_tune(73, old_d)
     jobs = {"copy_dec_16MBup_9MBdown": copies(16 << 20, 9 << 20), "copy_enc_10MBup_16MBdown": copies(10 << 20, 16 << 20)}
-    for c, s in variants:
+    for c, s, d in variants:
         for name, fn in (("dec", dec), ("enc", encf)):
-            def run(c=c, s=s, fn=fn):
+            def run(c=c, s=s, d=d, fn=fn):
                 lib.rudpx_tune(71, c)
                 lib.rudpx_tune(8, s)
+                lib.rudpx_tune(73, d)
                 fn()
-            jobs[f"{name}_chunks{c}_slots{s}"] = run
+            jobs[f"{name}_chunks{c}_slots{s}_direct{d}"] = run
     times = {k: [] for k in jobs}
     for f in jobs.values():
         f()
@@ -100,6 +106,7 @@ def main():
             times[k].append(time.perf_counter() - t0)
     lib.rudpx_tune(71, old_c)
     lib.rudpx_tune(8, old_s)
+    lib.rudpx_tune(73, old_d)
     out = {k: round(sorted(v)[len(v) // 2] * 1e3, 4) for k, v in times.items()}
     print(json.dumps({"ms_median": out, "reps": args.reps}, indent=1))
 
