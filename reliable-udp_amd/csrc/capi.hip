@@ -229,7 +229,7 @@ Pipeline* pipeline_for(int device) {
   return g_pipe[device];
 }
 
-int pipeline_reserve(Pipeline* pp, int slots, size_t bytes) {
+int pipeline_init(Pipeline* pp) {
   if (!pp->init) {
     RUDP_HIP(hipStreamCreateWithFlags(&pp->h2d, hipStreamNonBlocking));
     RUDP_HIP(hipStreamCreateWithFlags(&pp->comp, hipStreamNonBlocking));
@@ -243,6 +243,11 @@ int pipeline_reserve(Pipeline* pp, int slots, size_t bytes) {
     RUDP_HIP(hipHostMalloc(reinterpret_cast<void**>(&pp->h_status), 256, hipHostMallocDefault));
     pp->init = true;
   }
+  return 0;
+}
+
+int pipeline_reserve(Pipeline* pp, int slots, size_t bytes) {
+  if (int rc = pipeline_init(pp)) return rc;
   if (pp->bytes >= bytes && pp->slots >= slots) return 0;
   for (int i = 0; i < kMaxSlots; ++i) {
     if (pp->dbuf[i]) RUDP_HIP(hipFree(pp->dbuf[i]));
@@ -1252,6 +1257,34 @@ int rudp_encode_varlen_host(const rudp_batch* h_in, uint64_t payload_bytes, uint
   DeviceScope dev_scope;
   int rc = dev_scope.set(device);
   if (rc) return rc;
+  // Zero copy: packed payloads of small frames (mean under varlen_small bytes)
+  // in pinned host memory, every array pinned, payload and frames 16-B aligned:
+  // ONE checked encode over the whole batch whose kernels read the lengths,
+  // header table and payloads over PCIe and store frames, offsets and checksums
+  // back over it (the host pre-pass above has checked the batch; the device's
+  // own status is read back as well).
+  if (tuning().host_zero_copy && tuning().varlen_small > 0 && total / n < (uint64_t)tuning().varlen_small &&
+      h_in->payload && aligned16(h_in->payload) && aligned16(h_frames) && device_writable_host(h_in->payload) &&
+      device_writable_host(h_in->len) && device_writable_host(h_in->seq) && device_writable_host(h_in->ack) &&
+      device_writable_host(h_in->flags) && device_writable_host(h_frames) && device_writable_host(h_frame_off) &&
+      device_writable_host(h_csum_or_null)) {
+    Pipeline* pp = pipeline_for(device);
+    std::lock_guard<std::mutex> lk(pp->mu);
+    if ((rc = pipeline_init(pp))) return rc;
+    rudp_batch b = *h_in;
+    b.payload_len = (uint32_t)(total / n);  // the batch's mean: picks the tiles and the length codes
+    rc = rudp_encode_varlen_checked(&b, total, h_frames, frames_cap, h_frame_off, h_csum_or_null, pp->d_status, layout,
+                                    device, pp->comp);
+    if (!rc) {
+      RUDP_HIP(hipMemcpyAsync(pp->h_status, pp->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost, pp->comp));
+    }
+    const hipError_t e = hipStreamSynchronize(pp->comp);
+    if (rc) return rc;
+    if (e != hipSuccess) return hip_fail(e, "zero-copy varlen encode");
+    if (*pp->h_status)
+      return fail(RUDP_EINVAL, "rudp_encode_varlen_host: the device rejected the batch (status 0x%x)", *pp->h_status);
+    return 0;
+  }
   // Pinned offset / checksum arrays: for chunks that take the small-frame tile
   // (its checksums leave as coalesced stores) the kernels store them directly,
   // two D2H copies per chunk fewer; the frames always come back by one copy.
@@ -1361,13 +1394,35 @@ int rudp_decode_varlen_host(const uint8_t* h_frames, uint64_t frames_bytes, cons
   if (rc) return rc;
   const uint64_t hint = len_hint ? len_hint : (frames_bytes / n ? frames_bytes / n : 1u);
   const uint64_t bmax = stage_bytes();  // frame bytes a slot holds
+  const bool small = tuning().varlen_small > 0 && hint < (uint64_t)tuning().varlen_small + (uint64_t)layout;
+  // Zero copy: a batch of small frames whose every array is pinned host memory
+  // (a recvmmsg ring, torch's pinned allocator) decodes in ONE launch of the
+  // small-frame tile that reads the frames, offsets and sideband checksums over
+  // PCIe and stores the fields back over it -- no staging slot, no chunks, no
+  // copies.  The kernel applies the checked rule to every frame's offsets
+  // itself, so the result is rudp_decode_varlen_utf8's.
+  if (tuning().host_zero_copy && small && aligned16(h_frames) && device_writable_host(h_frames) &&
+      device_writable_host(h_frame_off) && device_writable_host(h_csum_in_or_null) && device_writable_host(h_seq) &&
+      device_writable_host(h_ack) && device_writable_host(h_flags) && device_writable_host(h_ok) &&
+      device_writable_host(h_csum_out_or_null) && device_writable_host(h_valid_or_null)) {
+    Pipeline* pp = pipeline_for(device);
+    std::lock_guard<std::mutex> lk(pp->mu);
+    if ((rc = pipeline_init(pp))) return rc;
+    rc = decode_varlen(h_frames, h_frame_off, (uint32_t)(hint < 0xFFFFFFFFull ? hint : 0xFFFFFFFFu), n,
+                       h_csum_in_or_null, h_seq, h_ack, h_flags, h_ok, h_csum_out_or_null, nullptr, layout, device,
+                       pp->comp, true, nullptr, frames_bytes, h_valid_or_null);
+    const hipError_t e = hipStreamSynchronize(pp->comp);
+    if (rc) return rc;
+    if (e != hipSuccess) return hip_fail(e, "zero-copy varlen decode");
+    if (h_status_or_null && memchr(h_ok, RUDP_OK_BAD_OFFSETS, n)) *h_status_or_null = RUDP_ST_OFFSETS;
+    return 0;
+  }
   // Pinned output arrays: the small-frame decode tile (the reference's 6-9 B
   // datagrams; its per-frame outputs leave as lane-strided, coalesced stores)
   // writes the fields into them directly: six D2H copies per chunk fewer.
   // Pageable arrays, and MTU frames (whose fields a group leader stores one at
   // a time: 2-B PCIe writes), take the slot and the copies.
-  const bool direct = tuning().host_direct_out && tuning().varlen_small > 0 &&
-                      hint < (uint64_t)tuning().varlen_small + (uint64_t)layout && device_writable_host(h_seq) &&
+  const bool direct = tuning().host_direct_out && small && device_writable_host(h_seq) &&
                       device_writable_host(h_ack) &&
                       device_writable_host(h_flags) && device_writable_host(h_ok) &&
                       device_writable_host(h_csum_out_or_null) && device_writable_host(h_valid_or_null);

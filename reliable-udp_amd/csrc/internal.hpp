@@ -406,6 +406,10 @@ struct Tuning {
   // *_host varlen decode: kernels store the per-frame outputs straight into the
   // caller's pinned arrays (1), or into the slot and D2H copies (0).
   RUDP_KNOB(host_direct_out, 1)
+  // *_host varlen calls of small frames whose arrays are all pinned (and the
+  // frame / payload buffers 16-B aligned): one launch that reads and writes
+  // host memory over PCIe, no staging (1), or the slot pipeline (0).
+  RUDP_KNOB(host_zero_copy, 1)
 
 };
 #undef RUDP_KNOB

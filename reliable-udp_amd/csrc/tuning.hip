@@ -280,7 +280,8 @@ RUDP_API int rudpx_copy_vpt(const void* src, void* dst, uint64_t n16, int vpt, i
 // 64: a checked small-frame encode of one tile in one launch (no pass 1);
 // 71: *_host pipeline: least chunks for a batch over 4 MiB (copy / kernel overlap).
 // 73: *_host varlen decode: per-frame outputs stored by the kernels into pinned host arrays (1) or copied (0).
-// 74: small-frame varlen encode: pass 1's 4-bit length codes for the framing kernel (1) or len[] again (0).
+// 74: small-frame varlen encode: pass 1's length codes for the framing kernel (1) or len[] again (0).
+// 75: *_host varlen calls of small frames in pinned memory: one zero-copy launch (1) or the slot pipeline (0).
 // (72: a first-round stagger of half the fused decode tiles' workgroups (s_sleep),
 // 0.539 -> 0.540-0.543 ms on multi-byte text, ASCII 0.229 -> 0.231-0.233: removed;
 // profiles/r05/sweeps/utf8_decode_stagger.json.)
@@ -339,7 +340,8 @@ RUDP_API int rudpx_tune(int key, int value) {
             : key == 70 ? &t.dedup_small_fpt
             : key == 71 ? &t.host_min_chunks
             : key == 73 ? &t.host_direct_out
-            : key == 74 ? &t.varlen_small_nib : nullptr;
+            : key == 74 ? &t.varlen_small_nib
+            : key == 75 ? &t.host_zero_copy : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }

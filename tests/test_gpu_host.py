@@ -376,3 +376,48 @@ def test_varlen_host_one_char_outputs_direct_or_copied(cuda, direct):
     assert (got["ok"] == 1).all() and got["valid"].sum() == n - len(range(0, n, 1001))
     assert np.array_equal(fr, want_fr) and np.array_equal(fo.astype(np.int64), want_off)
     assert np.array_equal(cs, want_cs)
+
+
+def _pinned(a):
+    t = torch.empty(a.shape, dtype={np.uint8: torch.uint8, np.uint16: torch.uint16, np.int32: torch.int32,
+                                    np.int64: torch.int64}[a.dtype.type], pin_memory=True)
+    out = t.numpy()
+    out[...] = a
+    return out
+
+
+@pytest.mark.parametrize("zero_copy", [1, 0])
+def test_varlen_host_zero_copy_pinned_batches(cuda, zero_copy):
+    """A recvmmsg / sendmmsg batch of 1-char datagrams whose every array is
+    pinned host memory: one launch that reads and writes the host arrays over
+    PCIe (knob 75 = 1, the product's form) or the slot pipeline (0).  Frames,
+    offsets and checksums equal the oracle's; the decode's fields equal the
+    device-resident decode of the same bytes, rejected offsets included."""
+    rng = np.random.default_rng(75 + zero_copy)
+    n, H = 300007, 5
+    lens = rng.integers(0, 5, n).astype(np.int32)  # 0-4 B payloads (UTF-8 characters), mean ~2
+    seq, ack = rng.integers(0, 1 << 16, n).astype(np.uint16), rng.integers(0, 1 << 16, n).astype(np.uint16)
+    flags = rng.integers(0, 256, n).astype(np.uint8)
+    pay = rng.integers(0, 256, int(lens.sum())).astype(np.uint8)
+    want_fr, want_off, want_cs = _oracle_varlen(seq, ack, flags, lens, pay, H)
+    p_seq, p_ack, p_flags, p_pay, p_lens = (_pinned(a) for a in (seq, ack, flags, pay, lens))
+    p_fr = _pinned(np.zeros(want_fr.size + 64, np.uint8))[:want_fr.size]
+    off = want_off.copy()
+    off[1000] = off[999] - 1  # one decreasing pair: frames 999 and 1000 rejected
+    off[5000] = want_fr.size + 9  # past the buffer
+    p_off = _pinned(off)
+    with _Knobs() as lib:
+        old = lib.rudpx_tune(75, zero_copy)
+        try:
+            r = batch.pack_batch_varlen((p_seq, p_ack, p_flags), p_pay, p_lens, H, want_csum=True, out=p_fr)
+            assert np.array_equal(r.frames, want_fr) and np.array_equal(r.frame_off, want_off)
+            assert np.array_equal(r.csum, want_cs)
+            d = batch.unpack_batch_varlen(r.frames, p_off, H, csum=_pinned(want_cs), utf8=True, check=False)
+            got = _host_fields(d)
+        finally:
+            lib.rudpx_tune(75, old)
+    want = _device_varlen(cuda, want_fr, off, H, want_cs)
+    for k in want:
+        assert np.array_equal(got[k], want[k]), (k, zero_copy)
+    assert got["ok"][999] == 4 and got["ok"][1000] == 4 and got["ok"][4999] == 4 and got["ok"][5000] == 4
+    assert (np.delete(got["ok"], [999, 1000, 4999, 5000]) == 1).all()

@@ -37,6 +37,9 @@ def main():
     ap.add_argument("--direct", default="1",
                     help="knob 73 values: 1 = the kernels store the per-frame outputs into the pinned arrays, "
                          "0 = slot + D2H copies")
+    ap.add_argument("--zero-copy", default="0",
+                    help="knob 75 values: 1 = one launch reading and writing the pinned arrays over PCIe "
+                         "(then chunks / slots / direct do not apply), 0 = the slot pipeline")
     args = ap.parse_args()
     lib = _native.lib()
     lib.rudpx_tune.argtypes = [ctypes.c_int, ctypes.c_int]
@@ -81,21 +84,25 @@ def main():
             torch.cuda.synchronize()
         return f
 
-    variants = [(c, s, d) for d in map(int, args.direct.split(",")) for s in map(int, args.slots.split(","))
+    variants = [(c, s, d, 0) for d in map(int, args.direct.split(",")) for s in map(int, args.slots.split(","))
                 for c in map(int, args.chunks.split(","))]
-    old_c, old_s, old_d = lib.rudpx_tune(71, 4), lib.rudpx_tune(8, 3), lib.rudpx_tune(73, 1)
+    if "1" in args.zero_copy.split(","):
+        variants.append((4, 3, 1, 1))
+    old_c, old_s, old_d, old_z = lib.rudpx_tune(71, 4), lib.rudpx_tune(8, 3), lib.rudpx_tune(73, 1), lib.rudpx_tune(75, 0)
     lib.rudpx_tune(71, old_c)
     lib.rudpx_tune(8, old_s)
     lib.rudpx_tune(73, old_d)
+    lib.rudpx_tune(75, old_z)
     jobs = {"copy_dec_16MBup_9MBdown": copies(16 << 20, 9 << 20), "copy_enc_10MBup_16MBdown": copies(10 << 20, 16 << 20)}
-    for c, s, d in variants:
+    for c, s, d, z in variants:
         for name, fn in (("dec", dec), ("enc", encf)):
-            def run(c=c, s=s, d=d, fn=fn):
+            def run(c=c, s=s, d=d, z=z, fn=fn):
                 lib.rudpx_tune(71, c)
                 lib.rudpx_tune(8, s)
                 lib.rudpx_tune(73, d)
+                lib.rudpx_tune(75, z)
                 fn()
-            jobs[f"{name}_chunks{c}_slots{s}_direct{d}"] = run
+            jobs[f"{name}_zero_copy" if z else f"{name}_chunks{c}_slots{s}_direct{d}"] = run
     times = {k: [] for k in jobs}
     for f in jobs.values():
         f()
@@ -107,6 +114,7 @@ def main():
     lib.rudpx_tune(71, old_c)
     lib.rudpx_tune(8, old_s)
     lib.rudpx_tune(73, old_d)
+    lib.rudpx_tune(75, old_z)
     out = {k: round(sorted(v)[len(v) // 2] * 1e3, 4) for k, v in times.items()}
     print(json.dumps({"ms_median": out, "reps": args.reps}, indent=1))
 
