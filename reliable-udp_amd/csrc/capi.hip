@@ -703,6 +703,7 @@ int rudp_decode_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_nul
   a.xcd = (tuning().tile_xcd && frame_len >= 128u) ? 1u : 0u;
 #if RUDP_TOOLS
   a.trace = tuning().encode_trace.load();  // decode tile timeline (tools/decode_timeline.py)
+  a.u8_always = tuning().utf8_always ? 1u : 0u;
 #endif
   a.frames = d_frames;
   a.csum_in = d_csum_in_or_null;
@@ -733,7 +734,7 @@ int rudp_decode_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_nul
         (1u << forced) <= (frame_len - (uint32_t)layout) / 16u)
       a.glog = (uint32_t)forced;
     if ((path == DecodePath::kVerifyTile || path == DecodePath::kCopyTile) && forced >= 0 &&
-        forced <= 4 && (size_t)(256u >> forced) * frame_len + 48 <= 65536)
+        forced <= (RUDP_TOOLS ? 5 : 4) && (size_t)(256u >> forced) * frame_len + 48 <= 65536)
       a.glog = (uint32_t)forced;
   }
   // The tile kernels check each payload's UTF-8 in the same pass; the other

@@ -331,9 +331,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      uint64_t bits = nf ? utf8_stream_frames(wq0 * F, nf, F, H, tid & 63u, [&](uint32_t c) { return tile[c]; },
-                                              [&](uint32_t i) { return dw[i]; })
-                         : 0ull;
+      auto chunk = [&](uint32_t c) { return tile[c]; };
+      auto dword = [&](uint32_t i) { return dw[i]; };
+#if RUDP_TOOLS
+      uint64_t bits = 0;
+      if (nf && a.u8_always && __all((hib & 0x80808080u) != 0 || q >= Tv))
+        bits = utf8_stream_frames<true>(wq0 * F, nf, F, H, tid & 63u, chunk, dword);
+      else if (nf)
+        bits = utf8_stream_frames(wq0 * F, nf, F, H, tid & 63u, chunk, dword);
+#else
+      uint64_t bits = nf ? utf8_stream_frames(wq0 * F, nf, F, H, tid & 63u, chunk, dword) : 0ull;
+#endif
       const uint32_t lo = group_or_rows((uint32_t)bits, 64u), hi = group_or_rows((uint32_t)(bits >> 32), 64u);
       const uint32_t b = q - wq0 + 1u;  // this frame's bit
       u8bad = ((b < 32u ? lo >> b : hi >> (b - 32u)) & 1u);

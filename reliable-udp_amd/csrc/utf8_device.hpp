@@ -230,7 +230,8 @@ __device__ __forceinline__ uint32_t utf8_check_frame(uint64_t s, uint64_t fe, ui
 // name every frame it finds invalid.  Returns them as bit (frame + 1) of a
 // u64 (bit 0: frame -1); the caller ORs it over the wave.  `chunk(c)`
 // returns aligned chunk c, `dw(i)` the LDS dword i.
-template <class Chunk, class Dword>
+// ALWAYS (diagnostics build): no per-chunk ASCII test, every chunk checked.
+template <bool ALWAYS = false, class Chunk, class Dword>
 __device__ __forceinline__ uint64_t utf8_stream_frames(uint32_t R0, uint32_t nf, uint32_t F, uint32_t H,
                                                        uint32_t lane, Chunk chunk, Dword dw) {
   const uint32_t R1 = R0 + nf * F;
@@ -248,8 +249,8 @@ __device__ __forceinline__ uint64_t utf8_stream_frames(uint32_t R0, uint32_t nf,
     // ASCII with no lead byte (11xxxxxx) in the three bytes just before:
     // nothing to check.  One test: the high bits of the chunk, OR bit 6 of
     // those bytes where bit 7 is set too (a right shift, the cheap one).
-    const uint32_t hb = or_and(or3(v.x, v.y, v.z), v.w, 0x80808080u);
-    const uint32_t lead = __builtin_amdgcn_bitop3_b32(prev >> 1, prev, 0x40404000u, 0x80);  // and3
+    const uint32_t hb = ALWAYS ? 1u : or_and(or3(v.x, v.y, v.z), v.w, 0x80808080u);
+    const uint32_t lead = ALWAYS ? 0u : __builtin_amdgcn_bitop3_b32(prev >> 1, prev, 0x40404000u, 0x80);  // and3
     if (hb | lead) {
       Utf8Pre q1, q2;
       utf8_pre2(v.x, v.y, q1, q2);
