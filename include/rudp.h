@@ -143,9 +143,13 @@ typedef struct rudp_batch {
  * utils/packet.py:13-16, :43-57, :60-65, :76-81.
  * d_frames: n*(payload_len+layout) bytes.  d_csum_or_null: n u16 (rudp5
  * sideband; for rudp7 it receives a copy of the in-band value).
- * Fast path when payload_len % 16 == 0, payload_len <= 4096 and both
- * d_frames and payload are 16-byte aligned; any other shape runs a
- * byte-granular kernel with identical results.
+ * The fixed-length tile takes payload_len % 16 == 0, payload_len <= 4096
+ * and 16-byte aligned d_frames and payload; any other shape (the reference's
+ * 1-4 B datagrams, any length, unaligned views) runs the variable-length tile
+ * kernels with implicit offsets (one launch, no offset array) with identical
+ * results.  An unaligned buffer is read from the 16-byte boundary at or below
+ * its first byte to the one at or above its last (the same aligned 16-byte
+ * blocks, hence pages); nothing outside d_frames / d_csum is written.
  */
 RUDP_API int rudp_encode(const rudp_batch* in, uint8_t* d_frames, uint16_t* d_csum_or_null,
                 int layout, int device, void* hip_stream);
@@ -166,6 +170,10 @@ RUDP_API int rudp_encode(const rudp_batch* in, uint8_t* d_frames, uint16_t* d_cs
  * payloads copied out aligned; NULL = zero-copy (view at frame offset layout).
  * Frames shorter than the header get d_ok = RUDP_OK_SHORT and the fields
  * that are present (truncated as utils/packet.py:31 slices them), 0 otherwise.
+ * Fixed-length frames whose payload is not a multiple of 16 bytes, or whose
+ * buffers are not 16-byte aligned, decode through the variable-length tiles
+ * with implicit offsets (a payload copy-out is one more launch), with the
+ * same results; buffers are read as rudp_encode reads them.
  */
 RUDP_API int rudp_decode(const uint8_t* d_frames, const uint64_t* d_frame_off_or_null,
                 uint32_t frame_len, uint64_t n, const uint16_t* d_csum_in_or_null,
