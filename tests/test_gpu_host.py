@@ -403,8 +403,10 @@ def test_varlen_host_zero_copy_pinned_batches(cuda, zero_copy):
     p_seq, p_ack, p_flags, p_pay, p_lens = (_pinned(a) for a in (seq, ack, flags, pay, lens))
     p_fr = _pinned(np.zeros(want_fr.size + 64, np.uint8))[:want_fr.size]
     off = want_off.copy()
-    off[1000] = off[999] - 1  # one decreasing pair: frames 999 and 1000 rejected
-    off[5000] = want_fr.size + 9  # past the buffer
+    # One decreasing pair: frame 999 is rejected; frame 1000 then starts a byte
+    # early, is read and fails its checksum (RUDP_OK_BAD_CSUM).
+    off[1000] = off[999] - 1
+    off[5000] = want_fr.size + 9  # past the buffer: frames 4999 and 5000 rejected
     p_off = _pinned(off)
     with _Knobs() as lib:
         old = lib.rudpx_tune(75, zero_copy)
@@ -419,5 +421,5 @@ def test_varlen_host_zero_copy_pinned_batches(cuda, zero_copy):
     want = _device_varlen(cuda, want_fr, off, H, want_cs)
     for k in want:
         assert np.array_equal(got[k], want[k]), (k, zero_copy)
-    assert got["ok"][999] == 4 and got["ok"][1000] == 4 and got["ok"][4999] == 4 and got["ok"][5000] == 4
+    assert got["ok"][999] == 4 and got["ok"][1000] == 0 and got["ok"][4999] == 4 and got["ok"][5000] == 4
     assert (np.delete(got["ok"], [999, 1000, 4999, 5000]) == 1).all()
