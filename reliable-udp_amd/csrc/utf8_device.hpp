@@ -63,15 +63,24 @@ __device__ __forceinline__ uint32_t group_or(uint32_t bits, uint32_t G) { return
 // the dword's own check and the next one's (which needs the bytes before it).
 // The nibble tables are looked up on the dword's OWN bytes (a table is
 // bytewise, so looking up the bytes and then shifting the results by one byte
-// equals shifting the bytes and looking them up): t12 = the "byte before"
-// tables of its high and low nibbles, ANDed (they only ever meet ANDed), t3 =
-// the "this byte" table of its high nibble, and ef = 0x40 per byte >= 0xE0
-// (a 3- or 4-byte lead), | 0x80 if >= 0xF0 (a 4-byte lead).  A table has 16
-// entries: v_perm_b32 looks up the nibble's bits 0-2 in 8 bytes, and a blend
-// by bit 3 (a mask of 0xFF per byte whose nibble is 8-15) picks the half; one
-// perm where a half is constant.
+// equals shifting the bytes and looking them up): t1 = the "byte before" table
+// of its high nibble, t12 = t1 ANDed with the "byte before" table of its low
+// nibble (they only ever meet ANDed), t3 = the "this byte" table of its high
+// nibble.  A 16-entry table is v_perm_b32 on the nibble's bits 0-2 over 8
+// bytes and a blend by bit 3 (a mask of 0xFF per byte whose nibble is 8-15).
+// The high-nibble tables need no blend: their selector is bits 4-6 for a byte
+// >= 0x80 and a constant entry for an ASCII byte, one v_bitop3_b32 over the
+// byte's sign mask -- entry 0 (a continuation's) as the byte before, entry 7
+// (0xF_'s, "too short" only) as this byte.  A continuation's "byte before"
+// entry, "two continuations", then also stands for an ASCII byte before (Keiser
+// & Lemire's "too long"): the error it misses, a continuation after ASCII that
+// a lead 2-3 bytes back still owes, is the lead's own "too short" one or two
+// bytes earlier in the same payload.  That frees the "too long" bit: in t1 it
+// marks a 3- or 4-byte lead (E_, F_) and bit 3 ("too large", F_ only) a 4-byte
+// lead, which give the continuations owed 2 and 3 bytes on with no table of
+// their own (utf8_dword_errors).
 struct Utf8Pre {
-  uint32_t t12, t3, ef;
+  uint32_t t12, t3, t1;
 };
 // v_bitop3_b32 (gfx950; truth table indexed by s0 s1 s2 as bits 2 1 0): it
 // issues faster than v_bfi_b32 / v_or3_b32 (profiles/r05/sweeps/valu_issue_rates.json)
@@ -109,21 +118,21 @@ __device__ __forceinline__ uint64_t shr64(uint64_t x) {
 // pair's low dword may carry the high dword's bits in bits 28-31).
 __device__ __forceinline__ Utf8Pre utf8_pre_from(uint32_t x, uint32_t x4, uint32_t x12, uint32_t x8, uint32_t xr4) {
   const uint32_t sel_lo = x & 0x07070707u, m_lo = __builtin_amdgcn_perm(x4, x12, 0x0B090A08u);  // bit 3 of each byte
-  const uint32_t sel_hi = xr4 & 0x07070707u, m_hi = __builtin_amdgcn_perm(x, x8, 0x0B090A08u);  // bit 7
-  // table bits (bits 6 and 7 of Keiser & Lemire's tables swapped): 0 too short,
-  // 1 too long, 2 overlong 3, 3 too large, 4 surrogate, 5 overlong 2,
-  // 6 two continuations, 7 too large 1000 / overlong 4
+  const uint32_t m_hi = __builtin_amdgcn_perm(x, x8, 0x0B090A08u);                              // bit 7
+  const uint32_t sel_c = __builtin_amdgcn_bitop3_b32(m_hi, xr4, 0x07070707u, 0x80);  // m & hi: ASCII -> 0
+  const uint32_t sel_s = __builtin_amdgcn_bitop3_b32(m_hi, xr4, 0x07070707u, 0x8A);  // 7 & (hi | ~m): ASCII -> 7
+  // table bits: 0 too short, 1 (t1) a 3/4-byte lead, 2 overlong 3, 3 too large
+  // (t1: a 4-byte lead), 4 surrogate, 5 overlong 2, 6 two continuations (or
+  // one after ASCII), 7 too large 1000 / overlong 4
   Utf8Pre p;
-  // as the byte before, its high nibble: 0-7 all 0x02 (too long), 8-15 from the second half
-  const uint32_t t1 = blend(m_hi, __builtin_amdgcn_perm(0x89150121u, 0x40404040u, sel_hi), 0x02020202u);
+  // as the byte before, its high nibble: entries 8-B (and ASCII) 0x40, C 0x21, D 0x01, E 0x17, F 0x8B
+  p.t1 = __builtin_amdgcn_perm(0x8B170121u, 0x40404040u, sel_c);
   // as the byte before, its low nibble: all 16 entries
   const uint32_t t2 = blend(m_lo, __builtin_amdgcn_perm(0xCBCBDBCBu, 0xCBCBCBCBu, sel_lo),
                             __builtin_amdgcn_perm(0xCBCBCB4Bu, 0x434363E7u, sel_lo));
-  p.t12 = t1 & t2;
-  // as this byte, its high nibble: 0-7 and 12-15 all 0x01 (too short)
-  p.t3 = blend(m_hi, __builtin_amdgcn_perm(0x01010101u, 0x7A7A6EE6u, sel_hi), 0x01010101u);
-  // leads: nibble 14 -> 0x40, 15 -> 0xC0 (selectors 6, 7: bytes 2, 3 of the first operand)
-  p.ef = m_hi & __builtin_amdgcn_perm(0xC0400000u, 0u, sel_hi);
+  p.t12 = p.t1 & t2;
+  // as this byte, its high nibble: 8-B the continuation classes, C-F (and ASCII) 0x01 (too short)
+  p.t3 = __builtin_amdgcn_perm(0x01010101u, 0x78786CE4u, sel_s);
   return p;
 }
 __device__ __forceinline__ Utf8Pre utf8_pre(uint32_t x) { return utf8_pre_from(x, x << 4, x << 12, x << 8, x >> 4); }
@@ -144,10 +153,11 @@ __device__ __forceinline__ void utf8_pre2(uint32_t x0, uint32_t x1, Utf8Pre& p0,
 // predecessors.
 __device__ __forceinline__ uint32_t utf8_dword_errors(const Utf8Pre& c, const Utf8Pre& p) {
   const uint32_t t12 = __builtin_amdgcn_alignbyte(c.t12, p.t12, 3);  // byte i: the byte before's tables
-  // a continuation is owed from 2 bytes after a 3/4-byte lead (bit 6 two bytes
-  // back) and 3 after a 4-byte lead (bit 7 three bytes back, moved to bit 6)
+  // a continuation is owed from 2 bytes after a 3/4-byte lead (t1 bit 1 two
+  // bytes back) and 3 after a 4-byte lead (t1 bit 3 three bytes back), both
+  // moved to bit 6 by one funnel shift of the dword pair each
   const uint32_t must23 =
-      or_and(__builtin_amdgcn_alignbyte(c.ef, p.ef, 2), __builtin_amdgcn_alignbyte(c.ef, p.ef, 1) >> 1, 0x40404040u);
+      or_and(__builtin_amdgcn_alignbit(c.t1, p.t1, 11), __builtin_amdgcn_alignbit(c.t1, p.t1, 5), 0x40404040u);
   return and_xor(t12, c.t3, must23);
 }
 
