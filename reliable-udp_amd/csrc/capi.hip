@@ -703,7 +703,6 @@ int rudp_decode_utf8(const uint8_t* d_frames, const uint64_t* d_frame_off_or_nul
   a.xcd = (tuning().tile_xcd && frame_len >= 128u) ? 1u : 0u;
 #if RUDP_TOOLS
   a.trace = tuning().encode_trace.load();  // decode tile timeline (tools/decode_timeline.py)
-  a.u8_always = tuning().utf8_always ? 1u : 0u;
 #endif
   a.frames = d_frames;
   a.csum_in = d_csum_in_or_null;

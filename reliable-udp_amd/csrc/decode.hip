@@ -317,7 +317,13 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
   uint32_t u8bad = 0;
   if (U8 && __any((hib & 0x80808080u) != 0)) {  // the byte checks, for waves whose frames hold a high bit
     __builtin_amdgcn_s_setprio(0);
-    if (G >= 2u) {
+    if (G == 16u) {
+      // 16 lanes a frame (payloads of 1 KiB and more): each payload over the
+      // windows the sums read, the bytes before a window handed on by DPP
+      if ((hib & 0x80808080u) && q < Tv)  // hib and q are the row's (the frame's)
+        u8bad = utf8_check_windows_row16(V, g, [&](uint32_t v) { return window16_dw(dw, q * F + H + 16u * v); });
+      u8bad = group_or_rows(u8bad, 16u) ? 1u : 0u;
+    } else if (G >= 2u) {
       // the wave's 64 / G frames are contiguous in the tile: one stream over them, every
       // lane a contiguous run of chunks (utf8_stream_frames), frames ORed over the wave
       const uint32_t fpw = 64u >> glog, wq0 = (tid >> 6) * fpw;
@@ -331,17 +337,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
       __builtin_amdgcn_wave_barrier();
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      auto chunk = [&](uint32_t c) { return tile[c]; };
-      auto dword = [&](uint32_t i) { return dw[i]; };
-#if RUDP_TOOLS
-      uint64_t bits = 0;
-      if (nf && a.u8_always && __all((hib & 0x80808080u) != 0 || q >= Tv))
-        bits = utf8_stream_frames<true>(wq0 * F, nf, F, H, tid & 63u, chunk, dword);
-      else if (nf)
-        bits = utf8_stream_frames(wq0 * F, nf, F, H, tid & 63u, chunk, dword);
-#else
-      uint64_t bits = nf ? utf8_stream_frames(wq0 * F, nf, F, H, tid & 63u, chunk, dword) : 0ull;
-#endif
+      uint64_t bits = nf ? utf8_stream_frames(wq0 * F, nf, F, H, tid & 63u, [&](uint32_t c) { return tile[c]; },
+                                              [&](uint32_t i) { return dw[i]; })
+                         : 0ull;
       const uint32_t lo = group_or_rows((uint32_t)bits, 64u), hi = group_or_rows((uint32_t)(bits >> 32), 64u);
       const uint32_t b = q - wq0 + 1u;  // this frame's bit
       u8bad = ((b < 32u ? lo >> b : hi >> (b - 32u)) & 1u);

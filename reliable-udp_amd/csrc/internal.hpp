@@ -78,8 +78,6 @@ struct DecodeArgs {
   uint32_t xcd;             // tile kernel: XCD-contiguous tile order (xcd_tile)
 #if RUDP_TOOLS
   uint64_t* trace;          // diagnostics (rudpx_encode_trace): per tile {start, staged, summed, end, XCC, CU}
-  uint32_t u8_always;       // diagnostics (rudpx_tune 76): waves whose every frame holds a high bit check
-                            // every chunk (no per-chunk ASCII test)
 #endif
 };
 
@@ -412,9 +410,6 @@ struct Tuning {
   // frame / payload buffers 16-B aligned): one launch that reads and writes
   // host memory over PCIe, no staging (1), or the slot pipeline (0).
   RUDP_KNOB(host_zero_copy, 1)
-#if RUDP_TOOLS
-  RUDP_KNOB(utf8_always, 0)  // fused UTF-8 decode tile: waves of all-high-bit frames skip the per-chunk ASCII test
-#endif
 
 };
 #undef RUDP_KNOB

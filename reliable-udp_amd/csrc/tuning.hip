@@ -341,8 +341,7 @@ RUDP_API int rudpx_tune(int key, int value) {
             : key == 71 ? &t.host_min_chunks
             : key == 73 ? &t.host_direct_out
             : key == 74 ? &t.varlen_small_nib
-            : key == 75 ? &t.host_zero_copy
-            : key == 76 ? &t.utf8_always : nullptr;
+            : key == 75 ? &t.host_zero_copy : nullptr;
   if (!slot) return -22;
   return slot->exchange(value);
 }

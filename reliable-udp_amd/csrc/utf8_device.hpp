@@ -161,6 +161,59 @@ __device__ __forceinline__ uint32_t utf8_dword_errors(const Utf8Pre& c, const Ut
   return and_xor(t12, c.t3, must23);
 }
 
+// Strict UTF-8 of one payload of V 16-byte windows by the 16 lanes of a DPP
+// row (lane g: windows g, g + 16, ...; `win(v)` returns window v, payload
+// byte 16v on), the windows the decode tile's sums read.  A window's bytes
+// before are window v - 1's last dword: lane g - 1's this round, lane 15's the
+// round before for lane 0 -- one row_ror:1 of the last dword's table inputs
+// serves both.  Rounds go in pairs, so the carry alternates registers instead
+// of being copied back.
+// Bytes before the payload and after it count as 0, so a sequence cut by its
+// end fails on the zero dword the lane holding window V - 1 checks last.
+// Returns nonzero if this lane saw an invalid byte; the caller ORs it over
+// the row.  Every lane of the row must run it.
+template <class Window>
+__device__ __forceinline__ uint32_t utf8_check_windows_row16(uint32_t V, uint32_t g, Window win) {
+  const Utf8Pre zero = utf8_pre(0u);
+  uint32_t c12 = zero.t12, c1 = zero.t1;  // lane 0's bytes before: the payload starts after zeros
+  Utf8Pre last = zero;
+  uint32_t err = 0;
+  // in = 0: a window past the payload's end (a clamped re-read), judged but not counted
+  auto step = [&](const u32x4& w, bool in) {
+    Utf8Pre p1, p2, p3, p4;
+    utf8_pre2(w.x, w.y, p1, p2);
+    utf8_pre2(w.z, w.w, p3, p4);
+    const uint32_t r12 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p4.t12, 0x121, 0xF, 0xF, false);  // row_ror:1
+    const uint32_t r1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p4.t1, 0x121, 0xF, 0xF, false);
+    Utf8Pre p0;
+    p0.t12 = g ? r12 : c12;
+    p0.t1 = g ? r1 : c1;
+    c12 = r12;
+    c1 = r1;
+    const uint32_t e = or3(utf8_dword_errors(p1, p0), utf8_dword_errors(p2, p1), utf8_dword_errors(p3, p2)) |
+                       utf8_dword_errors(p4, p3);
+    err |= in ? e : 0u;
+    last = p4;
+  };
+  // Rounds of 16 windows, every lane in each (a lane's window is in range
+  // whenever its predecessor's is, so what it reads across the row was computed
+  // that round; the lane holding window V - 1 is never past the end later).
+  const uint32_t rounds = (V + 15u) >> 4;
+  uint32_t j = 0;
+  for (; j + 2u <= rounds; j += 2u) {  // the first of a pair is always in range (16 (j + 1) < V)
+    const uint32_t v = g + 16u * j, v1 = v + 16u;
+    const u32x4 w0 = win(v), w1 = win(v1 < V ? v1 : V - 1u);
+    step(w0, true);
+    step(w1, v1 < V);
+  }
+  if (j < rounds) {
+    const uint32_t v = g + 16u * j;
+    step(win(v < V ? v : V - 1u), v < V);
+  }
+  if (V && g == ((V - 1u) & 15u)) err |= utf8_dword_errors(zero, last);  // nothing may still be expected
+  return err;
+}
+
 // Strict UTF-8 check of one frame's payload bytes [s, fe) by G lanes (lane g
 // takes aligned chunk pairs from c_lo + 2g, every 2G): `chunk(c)` returns aligned chunk c
 // and `prev(x)` the dword of bytes x-4 .. x-1 (x a multiple of 16; only bytes
@@ -240,8 +293,7 @@ __device__ __forceinline__ uint32_t utf8_check_frame(uint64_t s, uint64_t fe, ui
 // name every frame it finds invalid.  Returns them as bit (frame + 1) of a
 // u64 (bit 0: frame -1); the caller ORs it over the wave.  `chunk(c)`
 // returns aligned chunk c, `dw(i)` the LDS dword i.
-// ALWAYS (diagnostics build): no per-chunk ASCII test, every chunk checked.
-template <bool ALWAYS = false, class Chunk, class Dword>
+template <class Chunk, class Dword>
 __device__ __forceinline__ uint64_t utf8_stream_frames(uint32_t R0, uint32_t nf, uint32_t F, uint32_t H,
                                                        uint32_t lane, Chunk chunk, Dword dw) {
   const uint32_t R1 = R0 + nf * F;
@@ -259,8 +311,8 @@ __device__ __forceinline__ uint64_t utf8_stream_frames(uint32_t R0, uint32_t nf,
     // ASCII with no lead byte (11xxxxxx) in the three bytes just before:
     // nothing to check.  One test: the high bits of the chunk, OR bit 6 of
     // those bytes where bit 7 is set too (a right shift, the cheap one).
-    const uint32_t hb = ALWAYS ? 1u : or_and(or3(v.x, v.y, v.z), v.w, 0x80808080u);
-    const uint32_t lead = ALWAYS ? 0u : __builtin_amdgcn_bitop3_b32(prev >> 1, prev, 0x40404000u, 0x80);  // and3
+    const uint32_t hb = or_and(or3(v.x, v.y, v.z), v.w, 0x80808080u);
+    const uint32_t lead = __builtin_amdgcn_bitop3_b32(prev >> 1, prev, 0x40404000u, 0x80);  // and3
     if (hb | lead) {
       Utf8Pre q1, q2;
       utf8_pre2(v.x, v.y, q1, q2);

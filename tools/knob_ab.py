@@ -5,7 +5,8 @@ For every shape, each knob value's launches run in rotation (median of
 output is compared byte for byte with the first value's.
 
 shapes: encode:L (fixed-length, 1M x L, rotating sets below 1 GiB), decode:L, u8:L (decode + UTF-8),
-u8text:L (the same on valid multi-byte text), varlen:L
+u8text:L (the same on valid multi-byte text), u8mix:L (mostly-ASCII text with a few
+multi-byte characters in every payload), varlen:L
 (packed, equal lengths), ragged (lengths uniform in [0, 2944]), decode:L,
 vdec:L (varlen decode, equal lengths; vdec:L+u with the UTF-8 check), rdec (varlen
 decode, ragged ASCII lengths; rdec:+u; rdec:sort sorts each run of 16 lengths,
@@ -35,7 +36,7 @@ from rudp import _native, batch  # noqa: E402
 def make_shape(spec, dev):
     n = 1 << 20
     kind, _, arg = spec.partition(":")
-    if kind in ("encode", "decode", "u8", "u8text"):
+    if kind in ("encode", "decode", "u8", "u8text", "u8mix"):
         L = int(arg)
         nsets = max(1, min(8, math.ceil((1 << 30) / (n * (2 * L + 12)))))
         sets = []
@@ -44,6 +45,9 @@ def make_shape(spec, dev):
             if kind == "u8text":  # valid multi-byte text in every payload (bench decode_utf8_*_multibyte_text)
                 from run_kernel import text_payloads
                 pay = text_payloads(n, L, dev)
+            elif kind == "u8mix":  # mostly-ASCII text, a few multi-byte characters in every payload
+                from run_kernel import mixed_text_payloads
+                pay = mixed_text_payloads(n, L, dev)
             fr, _ = batch.pack_batch(tab, pay, 7)
             sets.append((tab, pay, fr))
         cur = [0]

@@ -38,6 +38,22 @@ def text_payloads(n, L, dev):
     return torch.frombuffer(bytearray(text), dtype=torch.uint8).to(dev).expand(n, L).contiguous()
 
 
+def mixed_text_payloads(n, L, dev):
+    """n copies of one L-byte payload of mostly-ASCII text with a few multi-byte characters
+    (about one 16-B chunk in two holds a high bit): every frame holds a high bit, most chunks
+    do not."""
+    text = ("Reliable UDP delivers each datagram in order; the proxy drops some \u2014 caf\u00e9. "
+            * (L // 40 + 2)).encode()[:L]
+    while True:
+        try:
+            text.decode()
+            break
+        except UnicodeDecodeError:
+            text = text[:-1]
+    text += b"x" * (L - len(text))
+    return torch.frombuffer(bytearray(text), dtype=torch.uint8).to(dev).expand(n, L).contiguous()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--op", choices=["encode", "decode", "decode_copy", "roundtrip", "encode_varlen",
