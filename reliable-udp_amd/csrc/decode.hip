@@ -208,7 +208,11 @@ __device__ __forceinline__ void decode_trace_record(const DecodeArgs& a, uint32_
 // reference decodes every payload, utils/reliableUDP.py:121 ->
 // utils/packet.py:73): the windows' high bits are OR'ed as they are summed,
 // and only a frame with a high bit runs the byte checks over its LDS chunks.
-template <int H, bool COPY, bool U8>
+// FUSE (U8, 16 lanes a frame, payloads of 1 KiB and more; launch_decode_tile_u8
+// picks it): a payload whose first windows hold a high bit has its sums and
+// its UTF-8 check in one pass.  Its own instantiation, so the other shapes run
+// the code they were measured with.
+template <int H, bool COPY, bool U8, bool FUSE = false>
 __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 ? 8 : 1))) decode_tile_kernel(DecodeArgs a) {
   extern __shared__ __attribute__((aligned(16))) unsigned char lds[];
   const uint32_t tid = threadIdx.x;
@@ -268,10 +272,19 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
   // the leader's header window, read now so its LDS round trip overlaps the sums
   u32x4 hdr = make_u32x4(0ull, 0ull);
   if (g == 0 && q < Tv) hdr = window16_dw(dw, q * F);
-  uint32_t sum = 0, hib = 0;
+  uint32_t sum = 0, hib = 0, u8bad = 0;
   const uint64_t p = p0 + q;
   const uint32_t V = L >> 4;
-  if (q < Tv) {
+  // FUSE: a payload whose first windows hold a high bit has its windows read
+  // once for its sums and its UTF-8 check (`fused`, wave-uniform)
+  bool fused = false;
+  if (FUSE) {
+    if (q < Tv) {
+      const uint32_t pay = q * F + H;
+      u8bad = utf8_check_windows_row16<true>(V, g, [&](uint32_t v) { return window16_dw(dw, pay + 16u * v); }, sum,
+                                             &hib, &fused);
+    }
+  } else if (q < Tv) {
     const uint32_t pay = q * F + H;  // LDS byte offset of the payload
     for (uint32_t v = g; v < V; v += G) {
       const u32x4 w = window16_dw(dw, pay + 16u * v);
@@ -314,14 +327,17 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
 #if RUDP_TOOLS
   if (a.trace && tid == 0) t_summed = (uint64_t)wall_clock64();
 #endif
-  uint32_t u8bad = 0;
-  if (U8 && __any((hib & 0x80808080u) != 0)) {  // the byte checks, for waves whose frames hold a high bit
+  if (fused) {
+    u8bad = group_or_rows(u8bad, 16u) ? 1u : 0u;
+  } else if (U8 && __any((hib & 0x80808080u) != 0)) {  // the byte checks, for waves whose frames hold a high bit
     __builtin_amdgcn_s_setprio(0);
     if (G == 16u) {
-      // 16 lanes a frame (payloads of 1 KiB and more): each payload over the
-      // windows the sums read, the bytes before a window handed on by DPP
-      if ((hib & 0x80808080u) && q < Tv)  // hib and q are the row's (the frame's)
-        u8bad = utf8_check_windows_row16(V, g, [&](uint32_t v) { return window16_dw(dw, q * F + H + 16u * v); });
+      // each payload over the windows the sums read, the bytes before a window handed on by DPP
+      if ((hib & 0x80808080u) && q < Tv) {  // hib and q are the row's (the frame's)
+        uint32_t unused = 0;
+        u8bad = utf8_check_windows_row16<false>(V, g, [&](uint32_t v) { return window16_dw(dw, q * F + H + 16u * v); },
+                                                unused);
+      }
       u8bad = group_or_rows(u8bad, 16u) ? 1u : 0u;
     } else if (G >= 2u) {
       // the wave's 64 / G frames are contiguous in the tile: one stream over them, every
@@ -428,21 +444,27 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
 #endif
 }
 
-template <int H, bool COPY, bool U8>
+template <int H, bool COPY, bool U8, bool FUSE = false>
 static int launch_decode_tile(const DecodeArgs& args, size_t lds, uint64_t blocks, hipStream_t stream) {
   if (lds > 65536) {
-    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_tile_kernel<H, COPY, U8>),
+    const hipError_t e = hipFuncSetAttribute(reinterpret_cast<const void*>(&decode_tile_kernel<H, COPY, U8, FUSE>),
                                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return (int)e;
   }
-  hipLaunchKernelGGL((decode_tile_kernel<H, COPY, U8>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream, args);
+  hipLaunchKernelGGL((decode_tile_kernel<H, COPY, U8, FUSE>), dim3((uint32_t)blocks), dim3(kBlock), lds, stream,
+                     args);
   return (int)hipGetLastError();
 }
 
 template <int H, bool COPY>
 static int launch_decode_tile_u8(const DecodeArgs& args, size_t lds, uint64_t blocks, hipStream_t stream) {
-  return args.valid ? launch_decode_tile<H, COPY, true>(args, lds, blocks, stream)
-                    : launch_decode_tile<H, COPY, false>(args, lds, blocks, stream);
+  if (!args.valid) return launch_decode_tile<H, COPY, false>(args, lds, blocks, stream);
+  // one pass for the sums and the check at 16 lanes a frame from 1 KiB payloads on
+  // (at 512 B the ASCII frames' high-bit test costs more than the second read
+  // saves: profiles/r06/sweeps/utf8_fused_ab.json)
+  if (args.glog == 4u && (args.F - (uint32_t)H) / 16u >= 64u)
+    return launch_decode_tile<H, COPY, true, true>(args, lds, blocks, stream);
+  return launch_decode_tile<H, COPY, true>(args, lds, blocks, stream);
 }
 
 int launch_decode(const DecodeArgs& args, int layout, DecodePath path, hipStream_t stream) {

@@ -136,6 +136,9 @@ __device__ __forceinline__ Utf8Pre utf8_pre_from(uint32_t x, uint32_t x4, uint32
   return p;
 }
 __device__ __forceinline__ Utf8Pre utf8_pre(uint32_t x) { return utf8_pre_from(x, x << 4, x << 12, x << 8, x >> 4); }
+// utf8_pre(0), spelled out (the 64-bit shifts are asm, which the compiler does
+// not fold): the inputs of any ASCII dword as the bytes before another
+__device__ __forceinline__ Utf8Pre utf8_pre_zero() { return Utf8Pre{0x40404040u, 0x01010101u, 0x40404040u}; }
 // Two consecutive dwords (x0 before x1) with one 64-bit shift per amount.
 __device__ __forceinline__ void utf8_pre2(uint32_t x0, uint32_t x1, Utf8Pre& p0, Utf8Pre& p1) {
   const uint64_t x = ((uint64_t)x1 << 32) | x0;
@@ -161,25 +164,32 @@ __device__ __forceinline__ uint32_t utf8_dword_errors(const Utf8Pre& c, const Ut
   return and_xor(t12, c.t3, must23);
 }
 
-// Strict UTF-8 of one payload of V 16-byte windows by the 16 lanes of a DPP
-// row (lane g: windows g, g + 16, ...; `win(v)` returns window v, payload
-// byte 16v on), the windows the decode tile's sums read.  A window's bytes
-// before are window v - 1's last dword: lane g - 1's this round, lane 15's the
-// round before for lane 0 -- one row_ror:1 of the last dword's table inputs
-// serves both.  Rounds go in pairs, so the carry alternates registers instead
-// of being copied back.
-// Bytes before the payload and after it count as 0, so a sequence cut by its
-// end fails on the zero dword the lane holding window V - 1 checks last.
-// Returns nonzero if this lane saw an invalid byte; the caller ORs it over
-// the row.  Every lane of the row must run it.
-template <class Window>
-__device__ __forceinline__ uint32_t utf8_check_windows_row16(uint32_t V, uint32_t g, Window win) {
-  const Utf8Pre zero = utf8_pre(0u);
-  uint32_t c12 = zero.t12, c1 = zero.t1;  // lane 0's bytes before: the payload starts after zeros
+// One payload of V 16-byte windows by the 16 lanes of a DPP row (lane g:
+// windows g, g + 16, ...; `win(v)` returns window v, payload byte 16v on): its
+// strict UTF-8 check and, with SUM, its LE u16 word sum (added to `sum`) in
+// the same pass, so every window is read from LDS once.  With SUM (V >= 17)
+// the first round pair is summed and tested: if no window of the wave holds a
+// high bit, the rest is the plain sums loop (ASCII waves pay one test) and any
+// high bit it meets goes to *hib for the caller's own check (*checked stays
+// false); else the check runs from that pair to the end (*checked = true).  A
+// window's bytes before are window v - 1's last dword: lane g - 1's this
+// round, lane 15's the round before for lane 0 -- one row_ror:1 of the last
+// dword's table inputs serves both.  Rounds go in pairs, so the carry
+// alternates registers instead of being copied back.  Bytes before the payload
+// and after it count as 0, so a sequence cut by its end fails on the zero
+// dword the lane holding window V - 1 checks last.  Returns nonzero if this
+// lane saw an invalid byte; the caller ORs it over the row.  Every lane of the
+// row must run it; with SUM it sets the issue priority to 0 while it checks
+// (1 after).
+template <bool SUM, class Window>
+__device__ __forceinline__ uint32_t utf8_check_windows_row16(uint32_t V, uint32_t g, Window win, uint32_t& sum,
+                                                             uint32_t* hib = nullptr, bool* checked = nullptr) {
+  const Utf8Pre zero = utf8_pre_zero();
+  uint32_t c12 = zero.t12, c1 = zero.t1;  // lane 0's bytes before: zeros (or ASCII)
   Utf8Pre last = zero;
   uint32_t err = 0;
-  // in = 0: a window past the payload's end (a clamped re-read), judged but not counted
-  auto step = [&](const u32x4& w, bool in) {
+  // in = 0: a window past the payload's end (stale or a clamped re-read), judged but not counted
+  auto check = [&](const u32x4& w, bool in) {
     Utf8Pre p1, p2, p3, p4;
     utf8_pre2(w.x, w.y, p1, p2);
     utf8_pre2(w.z, w.w, p3, p4);
@@ -200,17 +210,43 @@ __device__ __forceinline__ uint32_t utf8_check_windows_row16(uint32_t V, uint32_
   // that round; the lane holding window V - 1 is never past the end later).
   const uint32_t rounds = (V + 15u) >> 4;
   uint32_t j = 0;
+  if (SUM) {
+    // the first round pair summed and tested for high bits: none in the wave,
+    // and the rest is the plain sums loop, any high bit it meets left to the
+    // caller's check (*hib); else the check starts with that pair
+    auto hbits = [](const u32x4& w) { return or3(w.x, w.y, w.z) | w.w; };
+    const uint32_t v1 = g + 16u;
+    const u32x4 w0 = win(g), w1 = win(v1 < V ? v1 : V - 1u);
+    sum += le16_sum(w0) + (v1 < V ? le16_sum(w1) : 0u);
+    if (!__any(((hbits(w0) | (v1 < V ? hbits(w1) : 0u)) & 0x80808080u) != 0u)) {
+      for (uint32_t v = g + 32u; v < V; v += 16u) {
+        const u32x4 w = win(v);
+        sum += le16_sum(w);
+        *hib |= hbits(w);
+      }
+      return 0u;
+    }
+    __builtin_amdgcn_s_setprio(0);
+    *checked = true;
+    check(w0, true);
+    check(w1, v1 < V);
+    j = 2u;
+  }
   for (; j + 2u <= rounds; j += 2u) {  // the first of a pair is always in range (16 (j + 1) < V)
     const uint32_t v = g + 16u * j, v1 = v + 16u;
     const u32x4 w0 = win(v), w1 = win(v1 < V ? v1 : V - 1u);
-    step(w0, true);
-    step(w1, v1 < V);
+    if (SUM) sum += le16_sum(w0) + (v1 < V ? le16_sum(w1) : 0u);
+    check(w0, true);
+    check(w1, v1 < V);
   }
   if (j < rounds) {
     const uint32_t v = g + 16u * j;
-    step(win(v < V ? v : V - 1u), v < V);
+    const u32x4 w = win(v < V ? v : V - 1u);
+    if (SUM) sum += v < V ? le16_sum(w) : 0u;
+    check(w, v < V);
   }
   if (V && g == ((V - 1u) & 15u)) err |= utf8_dword_errors(zero, last);  // nothing may still be expected
+  if (SUM) __builtin_amdgcn_s_setprio(1);
   return err;
 }
 

@@ -484,3 +484,51 @@ def test_fixed_fused_sequences_across_frame_edges(cuda, L, H):
     for copy in (False, True):
         got = batch.unpack_batch(dev(fr, cuda), H, copy_payload=copy, utf8=True)
         assert np.array_equal(host(got.valid), want), copy
+
+
+@pytest.mark.parametrize("L", [1024, 1472, 2048])
+@pytest.mark.parametrize("H", [5, 7])
+def test_fused_tile_high_bits_after_an_ascii_start(cuda, L, H):
+    """The 16-lane decode tile sums a payload's first 512 B (two window rounds)
+    and tests them for high bits: with one, the sums and the UTF-8 check share
+    one pass over the windows; with none, the plain sums loop finishes the
+    payload and a high bit it meets sends the wave to the separate window check.
+    Frames with an ASCII start of every length around that edge, then valid
+    multi-byte text, a corrupted byte, a truncated sequence or more ASCII, in
+    every mix within a wave: checksums verify, fields equal the encode's inputs
+    and valid equals Python's strict decoder."""
+    import torch
+    rng = np.random.default_rng(L * 10 + H)
+    text = ("é中😀aßЖ€𝄞" * 400).encode()
+    bodies = []
+    for prefix in (0, 1, 15, 16, 100, 495, 496, 500, 511, 512, 513, 527, 528, 700, L - 17, L - 4, L - 1, L):
+        for kind in range(5):
+            tail = text[:L - prefix]
+            b = bytearray(b"a" * prefix + tail)
+            if kind == 1 and len(tail):  # a corrupted byte in the tail
+                b[prefix + int(rng.integers(0, len(tail)))] = int(rng.choice([0x80, 0xC0, 0xED, 0xF5, 0xFF]))
+            elif kind == 2 and prefix < L:  # a lead byte as the payload's last
+                b[-1] = 0xE4
+            elif kind == 3:  # all ASCII
+                b = bytearray(b"a" * L)
+            elif kind == 4 and prefix < L:  # one 2-byte character at the very end
+                b[-2:] = "é".encode()
+            bodies.append(bytes(b[:L]))
+    n = len(bodies)
+    order = rng.permutation(n)  # every mix of kinds within a wave's 4 frames
+    pay = np.frombuffer(b"".join(bodies[i] for i in order), np.uint8).reshape(n, L)
+    seq = rng.integers(0, 1 << 16, n).astype(np.uint16)
+    ack = rng.integers(0, 1 << 16, n).astype(np.uint16)
+    flags = rng.integers(0, 256, n).astype(np.uint8)
+    fr, cs = batch.pack_batch((dev(seq, cuda), dev(ack, cuda), dev(flags, cuda)), dev(pay, cuda), H, want_csum=True)
+    off = np.arange(n + 1, dtype=np.int64) * (L + H)
+    want = codec_np.utf8_valid(host(fr).reshape(-1), off, H)
+    assert 0.1 < want.mean() < 0.9
+    for copy in (False, True):
+        d = batch.unpack_batch(fr, H, csum=cs if H == 5 else None, copy_payload=copy, utf8=True)
+        assert np.array_equal(host(d.valid), want), copy
+        assert (host(d.ok) == 1).all(), copy
+        assert np.array_equal(host(d.seq), seq) and np.array_equal(host(d.ack), ack)
+        assert np.array_equal(host(d.flags), flags)
+        if copy:
+            assert torch.equal(d.payload, dev(pay, cuda))
