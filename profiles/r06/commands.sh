@@ -1,0 +1,10 @@
+# Round-6 profiles (from the repo root, under gpurun), then on the build host:
+#   python3 tools/leg_summaries.py --prefix p6a --round r06 <legs>; ... --prefix p6b ...
+bash tools/gpu/profile_legs.sh p6a enc1472 enc1024 enc64 dec1472 decu8_1472 decu8text enc16M venc1472 vdec1472 vdecu8_1472
+bash tools/gpu/profile_legs.sh p6b vencrag vdecrag vdecu8rag utf8 dedup venc1c vdec1c vdecu8_1c senc1c sdecu8_1c senc1000
+bash tools/gpu/run.sh pmcsq p6text tools/run_kernel.py --op decode --utf8 --text --L 1472 --steps 10
+bash tools/gpu/run.sh pmcvalu p6text tools/run_kernel.py --op decode --utf8 --text --L 1472 --steps 60
+bash tools/gpu/run.sh pmcsq p6ascii tools/run_kernel.py --op decode --utf8 --L 1472 --steps 10
+bash tools/gpu/run.sh bench r06c
+# python3 tools/clock_spread.py gpurun_out/p6text_valu/run_counter_collection.csv --kernel decode_tile_kernel \
+#   --json profiles/r06/utf8_text_clock_spread.json
