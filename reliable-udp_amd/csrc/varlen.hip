@@ -1156,8 +1156,21 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
       if (__any((hib & 0x80808080u) != 0)) {
         if (hib & 0x80808080u) {
           const uint32_t* idw = reinterpret_cast<const uint32_t*>(img);  // kVTGuard bytes before it
-          u8bad = utf8_check_frame(ps, fe, g2, G2, [&](uint64_t c) { return img16[c]; },
-                                   [&](uint64_t x) { return idw[(int64_t)(x >> 2) - 1]; });
+          if (G2 == 16u) {
+            // 16 lanes a frame: over payload-aligned windows, the bytes before a
+            // window handed across the DPP row (utf8_device.hpp); the last window
+            // masked to the payload (the run's budget has 32 B past its end)
+            const uint32_t L = fe - ps, V = (L + 15u) >> 4;
+            uint32_t unused = 0;
+            u8bad = utf8_check_windows_row16<false>(V, g2, [&](uint32_t v) {
+              u32x4 w = window16_dw(idw, ps + 16u * v);
+              if (16u * v + 16u > L) w = keep_bytes(w, 0, (int)(L - 16u * v));
+              return w;
+            }, unused);
+          } else {
+            u8bad = utf8_check_frame(ps, fe, g2, G2, [&](uint64_t c) { return img16[c]; },
+                                     [&](uint64_t x) { return idw[(int64_t)(x >> 2) - 1]; });
+          }
         }
         u8bad = group_or(u8bad, G2);
       }

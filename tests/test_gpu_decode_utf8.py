@@ -532,3 +532,44 @@ def test_fused_tile_high_bits_after_an_ascii_start(cuda, L, H):
         assert np.array_equal(host(d.flags), flags)
         if copy:
             assert torch.equal(d.payload, dev(pay, cuda))
+
+
+@pytest.mark.parametrize("H", [5, 7])
+def test_varlen_tile_windows_text_of_any_length(cuda, H):
+    """Packed frames at hints of 769-1536 B take the varlen decode tile at 16
+    lanes a frame, which checks each payload over payload-aligned windows (the
+    last one masked to the payload) with the bytes before a window handed
+    across the DPP row.  Text payloads of every length (0-3000 B: whole
+    windows and every remainder), with a corrupted byte, a truncated last
+    character or a lead byte at the very end; the answer equals Python's
+    strict decoder at hints 1000 and 1472 and the fields agree with the
+    checksum-only decode."""
+    rng = np.random.default_rng(1600 + H)
+    text = ("é中😀aßЖ€𝄞" * 600).encode()
+    rows = []
+    for k in range(3000):
+        L = int(rng.integers(0, 3001)) if k % 3 else int(rng.integers(1400, 1560))
+        body = bytearray(text[:L].decode("utf-8", "ignore").encode())
+        body += b"q" * (L - len(body))
+        kind = k % 5
+        if kind == 1 and L:
+            body[int(rng.integers(0, L))] = int(rng.choice([0x80, 0xBF, 0xC1, 0xE0, 0xED, 0xF4, 0xF5, 0xFF]))
+        elif kind == 2 and L >= 2:
+            body[-1] = 0xF0
+        elif kind == 3 and L >= 3:
+            body[-3:] = "€".encode()[:2] + b"q"  # a 3-byte character cut to 2, then ASCII
+        rows.append(bytes(body))
+    hdr = b"\x12\x34\x56\x78\x40" + (b"\x00\x00" if H == 7 else b"")
+    frames = [hdr + r for r in rows]
+    flat = np.frombuffer(b"".join(frames), np.uint8)
+    off = np.zeros(len(frames) + 1, np.int64)
+    off[1:] = np.cumsum([len(f) for f in frames])
+    want = codec_np.utf8_valid(flat, off, H)
+    assert 0.2 < want.mean() < 0.9
+    d_flat, d_off = dev(flat, cuda), dev(off, cuda)
+    for hint in (1000, 1472):
+        g = _varlen_decode(d_flat, flat.size, d_off, len(frames), hint, H, True)
+        assert np.array_equal(g["valid"], want), hint
+        plain = _varlen_decode(d_flat, flat.size, d_off, len(frames), hint, H, False)
+        for k in plain:
+            assert np.array_equal(g[k], plain[k]), (hint, k)

@@ -30,7 +30,8 @@ def main():
     ap.add_argument("--libs", required=True)
     ap.add_argument("--L", default="1472,1024,64")
     ap.add_argument("--reps", type=int, default=11)
-    ap.add_argument("--op", default="encode", choices=["encode", "decode", "varlen", "vdecode", "u8text", "u8ascii", "u8val", "u8valtext"],
+    ap.add_argument("--op", default="encode", choices=["encode", "decode", "varlen", "vdecode", "vu8", "u8text", "u8ascii",
+                                                       "u8val", "u8valtext"],
                     help="decode: verify-only fixed-length rudp_decode of the encoded frames; varlen: "
                          "rudp_encode_varlen_checked of packed payloads, --L lengths or 'ragged' "
                          "(uniform in [0, 2944]); a 'u' suffix (1472u) times the unchecked rudp_encode_varlen; "
@@ -66,6 +67,11 @@ def main():
                                                  ctypes.c_uint64, ctypes.c_void_p] + [ctypes.c_void_p] * 6 + \
                                                 [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
         h.rudp_decode_varlen_checked.restype = ctypes.c_int
+        if hasattr(h, "rudp_decode_varlen_utf8"):
+            h.rudp_decode_varlen_utf8.argtypes = [ctypes.c_void_p, ctypes.c_uint64, ctypes.c_void_p, ctypes.c_uint32,
+                                                  ctypes.c_uint64] + [ctypes.c_void_p] * 8 + \
+                                                 [ctypes.c_int, ctypes.c_int, ctypes.c_void_p]
+            h.rudp_decode_varlen_utf8.restype = ctypes.c_int
         if hasattr(h, "rudp_validate_utf8"):
             h.rudp_validate_utf8.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_uint32, ctypes.c_uint64,
                                              ctypes.c_int, ctypes.c_void_p, ctypes.c_int, ctypes.c_void_p]
@@ -74,9 +80,10 @@ def main():
     dev = torch.device("cuda", 0)
     stream = torch.cuda.current_stream().cuda_stream
     out = {}
-    if args.op in ("varlen", "vdecode"):
+    if args.op in ("varlen", "vdecode", "vu8"):
         for spec in args.L.split(","):
-            out[spec] = (varlen_ab if args.op == "varlen" else vdecode_ab)(libs, spec, args.reps, dev, stream)
+            fn = varlen_ab if args.op == "varlen" else vdecode_ab if args.op == "vdecode" else vu8_ab
+            out[spec] = fn(libs, spec, args.reps, dev, stream)
             print(spec, out[spec], file=sys.stderr, flush=True)
         print(json.dumps(out, indent=1))
         return
@@ -239,6 +246,69 @@ def vdecode_ab(libs, spec, reps, dev, stream):
             e.synchronize()
             times[name].append(s.elapsed_time(e) / 10)
     return {"ms": {k: statistics.median(v) for k, v in times.items()}, "exact": exact, "layout": layout}
+
+
+def text_flat(lens, dev):
+    """Packed payloads of valid multi-byte text: payload i is the longest
+    character-aligned prefix of one text of at most lens[i] bytes, padded with
+    ASCII to lens[i]."""
+    t = ("é中😀aßЖ€𝄞" * 400).encode()
+    vl = torch.tensor([len(t[:k].decode("utf-8", "ignore").encode()) for k in range(int(lens.max().item()) + 1)],
+                      dtype=torch.int64, device=dev)
+    tt = torch.frombuffer(bytearray(t), dtype=torch.uint8).to(dev)
+    l64 = lens.to(torch.int64)
+    starts = torch.cumsum(l64, 0) - l64
+    total = int(l64.sum().item())
+    pos = torch.arange(total, device=dev, dtype=torch.int64) - torch.repeat_interleave(starts, l64)
+    keep = torch.repeat_interleave(vl[l64], l64)
+    return torch.where(pos < keep, tt[pos.clamp(max=tt.numel() - 1)], torch.full_like(pos, 0x78).to(torch.uint8))
+
+
+def vu8_ab(libs, spec, reps, dev, stream):
+    n = 1 << 20
+    g = torch.Generator(device=dev).manual_seed(0x5EED0004)
+    text = spec.endswith("t")
+    spec = spec.rstrip("t")
+    if spec == "ragged":
+        lens = torch.randint(0, 2945, (n,), dtype=torch.int32, device=dev, generator=g)
+        hint = 1472
+    else:
+        hint = int(spec)
+        lens = torch.full((n,), hint, dtype=torch.int32, device=dev)
+    tab, _ = batch.synth_batch(n, 0, 0x5EED0004, device=dev)
+    if text:
+        pay = text_flat(lens, dev)
+    else:
+        pay = torch.randint(0x20, 0x7F, (int(lens.sum().item()),), dtype=torch.uint8, device=dev, generator=g)
+    enc = batch.pack_batch_varlen(tab, pay, lens, 7)
+    outs = [torch.empty((n,), dtype=dt, device=dev) for dt in (torch.uint16, torch.uint16, torch.uint8, torch.uint8,
+                                                                 torch.uint16, torch.uint8)]
+
+    def call(h):
+        return h.rudp_decode_varlen_utf8(enc.frames.data_ptr(), enc.frames.numel(), enc.frame_off.data_ptr(),
+                                         hint + 7, n, None, *[t.data_ptr() for t in outs], None, 7, 0, stream)
+    ref, exact = None, {}
+    for name, h in libs.items():
+        for t in outs:
+            t.zero_()
+        assert call(h) == 0
+        got = torch.cat([t.view(torch.uint8) for t in outs])
+        ref = got if ref is None else ref
+        exact[name] = bool(torch.equal(got, ref))
+    all_valid = bool((outs[5] == 1).all().item()) and bool((outs[3] == 1).all().item())
+    times = {k: [] for k in libs}
+    for _ in range(reps):
+        for name, h in libs.items():
+            for _ in range(2):
+                call(h)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            for _ in range(10):
+                call(h)
+            e.record()
+            e.synchronize()
+            times[name].append(s.elapsed_time(e) / 10)
+    return {"ms": {k: statistics.median(v) for k, v in times.items()}, "exact": exact, "all_valid_verified": all_valid}
 
 
 if __name__ == "__main__":
