@@ -536,6 +536,27 @@ def legs(torch, batch, device, steps):
         "ms_by_form": tm,
         "note": "Python entry, sync-free (offset scan and device-side checks included); medians of "
                 "7 interleaved rounds beside the eager-check and raw C-ABI forms"}
+    # packed frames of valid multi-byte text (the fixed-length text leg's payload):
+    # decode + get_payload()'s strict UTF-8 in the varlen tile, every payload checked
+    text = ("é中😀aßЖ€𝄞" * 200).encode()[:1472]
+    while True:
+        try:
+            text.decode()
+            break
+        except UnicodeDecodeError:
+            text = text[:-1]
+    text += b"x" * (1472 - len(text))
+    flatt = torch.frombuffer(bytearray(text), dtype=torch.uint8).to(device).repeat(n1)
+    enct = batch.pack_batch_varlen(tabm, flatt, lensm, "rudp7")
+    dt0 = batch.unpack_batch_varlen(enct.frames, enct.frame_off, "rudp7", utf8=True)
+    ms_vt = time_loop(torch, lambda i: batch.unpack_batch_varlen(enct.frames, enct.frame_off, "rudp7", check=False,
+                                                                  utf8=True, reuse=dt0), steps, 3) / steps
+    dt0.check()
+    out["varlen_decode_utf8_text_1Mx1472"] = {
+        "ms": ms_vt, "roofline_frac": n1 * (1479 + 8 + 9) / (ms_vt / 1e3) / 1e9 / HBM_PEAK_GBS,
+        "all_valid_and_verified": bool((dt0.valid == 1).all()) and bool((dt0.ok == 1).all()),
+        "note": "packed rudp7 frames of valid multi-byte text through unpack_batch_varlen(utf8=True), sync-free"}
+    del flatt, enct, dt0
     # ragged MTU-range lengths: uniform in [0, 2944] (mean 1472), packed; the tile
     # kernel takes byte tiles for this batch (the scan counts its overflowing
     # packet tiles), against the equal-length 1472-B leg above
@@ -748,6 +769,8 @@ def baseline_summary(line):
         "decode_utf8_ascii_1Mx1472": pick("decode_utf8_1Mx1472", extra=("all_valid_and_verified",)),
         "decode_utf8_multibyte_text_1Mx1472": pick("decode_utf8_1Mx1472_multibyte_text",
                                                    extra=("all_valid_and_verified",)),
+        "varlen_decode_utf8_text_1Mx1472": pick("varlen_decode_utf8_text_1Mx1472",
+                                                extra=("all_valid_and_verified",)),
         "encode_1Mx1_fixed": pick("encode_1Mx1_fixed", extra=("vs_varlen_same_bytes", "frames_equal_varlen_path")),
         "decode_utf8_1Mx1_fixed": pick("decode_utf8_1Mx1_fixed",
                                        extra=("vs_varlen_same_bytes", "all_valid_verified_fields_equal")),

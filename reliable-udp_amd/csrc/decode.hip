@@ -281,8 +281,9 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
   if (FUSE) {
     if (q < Tv) {
       const uint32_t pay = q * F + H;
-      u8bad = utf8_check_windows_row16<true>(V, g, [&](uint32_t v) { return window16_dw(dw, pay + 16u * v); }, sum,
-                                             &hib, &fused);
+      u8bad = utf8_check_windows_row16<true, false>(  // (V >= 64)
+          V, g, [&](uint32_t v) { return window16_dw(dw, pay + 16u * v); },
+          [&](const u32x4& w, bool in) { sum += in ? le16_sum(w) : 0u; }, &hib, &fused);
     }
   } else if (q < Tv) {
     const uint32_t pay = q * F + H;  // LDS byte offset of the payload
@@ -334,9 +335,8 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
     if (G == 16u) {
       // each payload over the windows the sums read, the bytes before a window handed on by DPP
       if ((hib & 0x80808080u) && q < Tv) {  // hib and q are the row's (the frame's)
-        uint32_t unused = 0;
-        u8bad = utf8_check_windows_row16<false>(V, g, [&](uint32_t v) { return window16_dw(dw, q * F + H + 16u * v); },
-                                                unused);
+        u8bad = utf8_check_windows_row16<false>(
+            V, g, [&](uint32_t v) { return window16_dw(dw, q * F + H + 16u * v); }, [](const u32x4&, bool) {});
       }
       u8bad = group_or_rows(u8bad, 16u) ? 1u : 0u;
     } else if (G >= 2u) {

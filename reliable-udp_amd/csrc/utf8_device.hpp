@@ -166,8 +166,9 @@ __device__ __forceinline__ uint32_t utf8_dword_errors(const Utf8Pre& c, const Ut
 
 // One payload of V 16-byte windows by the 16 lanes of a DPP row (lane g:
 // windows g, g + 16, ...; `win(v)` returns window v, payload byte 16v on): its
-// strict UTF-8 check and, with SUM, its LE u16 word sum (added to `sum`) in
-// the same pass, so every window is read from LDS once.  With SUM (V >= 17)
+// strict UTF-8 check and, with SUM, the caller's sums (`acc(w, in)` for
+// every window, `in` = 0 for one past the end) in the same pass, so every
+// window is read from LDS once.  With SUM
 // the first round pair is summed and tested: if no window of the wave holds a
 // high bit, the rest is the plain sums loop (ASCII waves pay one test) and any
 // high bit it meets goes to *hib for the caller's own check (*checked stays
@@ -181,8 +182,10 @@ __device__ __forceinline__ uint32_t utf8_dword_errors(const Utf8Pre& c, const Ut
 // lane saw an invalid byte; the caller ORs it over the row.  Every lane of the
 // row must run it; with SUM it sets the issue priority to 0 while it checks
 // (1 after).
-template <bool SUM, class Window>
-__device__ __forceinline__ uint32_t utf8_check_windows_row16(uint32_t V, uint32_t g, Window win, uint32_t& sum,
+// SHORT: V may be under 17 (the varlen tiles' short payloads); without it the
+// first round pair is taken to be whole.
+template <bool SUM, bool SHORT = true, class Window, class Acc>
+__device__ __forceinline__ uint32_t utf8_check_windows_row16(uint32_t V, uint32_t g, Window win, Acc acc,
                                                              uint32_t* hib = nullptr, bool* checked = nullptr) {
   const Utf8Pre zero = utf8_pre_zero();
   uint32_t c12 = zero.t12, c1 = zero.t1;  // lane 0's bytes before: zeros (or ASCII)
@@ -215,34 +218,40 @@ __device__ __forceinline__ uint32_t utf8_check_windows_row16(uint32_t V, uint32_
     // and the rest is the plain sums loop, any high bit it meets left to the
     // caller's check (*hib); else the check starts with that pair
     auto hbits = [](const u32x4& w) { return or3(w.x, w.y, w.z) | w.w; };
+    if (SHORT && V == 0u) return 0u;
     const uint32_t v1 = g + 16u;
-    const u32x4 w0 = win(g), w1 = win(v1 < V ? v1 : V - 1u);
-    sum += le16_sum(w0) + (v1 < V ? le16_sum(w1) : 0u);
-    if (!__any(((hbits(w0) | (v1 < V ? hbits(w1) : 0u)) & 0x80808080u) != 0u)) {
+    const bool in0 = !SHORT || g < V, in1 = !SHORT || v1 < V;
+    const u32x4 w0 = win(in0 ? g : V - 1u), w1 = win(in1 ? v1 : V - 1u);
+    acc(w0, in0);
+    acc(w1, in1);
+    if (!__any((((in0 ? hbits(w0) : 0u) | (in1 ? hbits(w1) : 0u)) & 0x80808080u) != 0u)) {
       for (uint32_t v = g + 32u; v < V; v += 16u) {
         const u32x4 w = win(v);
-        sum += le16_sum(w);
+        acc(w, true);
         *hib |= hbits(w);
       }
       return 0u;
     }
     __builtin_amdgcn_s_setprio(0);
     *checked = true;
-    check(w0, true);
-    check(w1, v1 < V);
+    check(w0, in0);
+    check(w1, in1);
     j = 2u;
   }
   for (; j + 2u <= rounds; j += 2u) {  // the first of a pair is always in range (16 (j + 1) < V)
     const uint32_t v = g + 16u * j, v1 = v + 16u;
     const u32x4 w0 = win(v), w1 = win(v1 < V ? v1 : V - 1u);
-    if (SUM) sum += le16_sum(w0) + (v1 < V ? le16_sum(w1) : 0u);
+    if (SUM) {
+      acc(w0, true);
+      acc(w1, v1 < V);
+    }
     check(w0, true);
     check(w1, v1 < V);
   }
   if (j < rounds) {
     const uint32_t v = g + 16u * j;
     const u32x4 w = win(v < V ? v : V - 1u);
-    if (SUM) sum += v < V ? le16_sum(w) : 0u;
+    if (SUM) acc(w, v < V);
     check(w, v < V);
   }
   if (V && g == ((V - 1u) & 15u)) err |= utf8_dword_errors(zero, last);  // nothing may still be expected
