@@ -340,25 +340,15 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
       }
       u8bad = group_or_rows(u8bad, 16u) ? 1u : 0u;
     } else if (G >= 2u) {
-      // the wave's 64 / G frames are contiguous in the tile: one stream over them, every
-      // lane a contiguous run of chunks (utf8_stream_frames), frames ORed over the wave
-      const uint32_t fpw = 64u >> glog, wq0 = (tid >> 6) * fpw;
-      const uint32_t nf = Tv > wq0 ? (Tv - wq0 < fpw ? Tv - wq0 : fpw) : 0u;
-      // this wave's frames' header bytes read as 0 in the stream: zeroed in LDS
-      // (its leaders read their headers above; LDS keeps one wave's accesses
-      // in order, and no other wave reads these bytes but as discarded window
-      // edges)
-      if (q < Tv)
-        for (uint32_t b = g; b < (uint32_t)H; b += G) lds[q * F + b] = 0;
-      __builtin_amdgcn_wave_barrier();
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-      uint64_t bits = nf ? utf8_stream_frames(wq0 * F, nf, F, H, tid & 63u, [&](uint32_t c) { return tile[c]; },
-                                              [&](uint32_t i) { return dw[i]; })
-                         : 0ull;
-      const uint32_t lo = group_or_rows((uint32_t)bits, 64u), hi = group_or_rows((uint32_t)(bits >> 32), 64u);
-      const uint32_t b = q - wq0 + 1u;  // this frame's bit
-      u8bad = ((b < 32u ? lo >> b : hi >> (b - 32u)) & 1u);
+      // 2-8 lanes a frame: the same window check in lane groups (DPP within the rows)
+      if ((hib & 0x80808080u) && q < Tv) {  // hib and q are the group's (the frame's)
+        auto win = [&](uint32_t v) { return window16_dw(dw, q * F + H + 16u * v); };
+        auto none = [](const u32x4&, bool) {};
+        u8bad = G == 8u   ? utf8_check_windows_rows<false, true, 8>(V, g, win, none)
+                : G == 4u ? utf8_check_windows_rows<false, true, 4>(V, g, win, none)
+                          : utf8_check_windows_rows<false, true, 2>(V, g, win, none);
+      }
+      u8bad = group_or_rows(u8bad, G) ? 1u : 0u;
     } else {
       if ((hib & 0x80808080u) && q < Tv)
         u8bad = utf8_check_frame(q * F + H, q * F + F, g, G, [&](uint64_t c) { return tile[c]; },

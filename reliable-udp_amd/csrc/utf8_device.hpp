@@ -164,29 +164,31 @@ __device__ __forceinline__ uint32_t utf8_dword_errors(const Utf8Pre& c, const Ut
   return and_xor(t12, c.t3, must23);
 }
 
-// One payload of V 16-byte windows by the 16 lanes of a DPP row (lane g:
-// windows g, g + 16, ...; `win(v)` returns window v, payload byte 16v on): its
-// strict UTF-8 check and, with SUM, the caller's sums (`acc(w, in)` for
+// One payload of V 16-byte windows by the GL lanes of a lane group (GL a
+// power of two, 2..16, the groups aligned within the 16-lane DPP rows; lane
+// g: windows g, g + GL, ...; `win(v)` returns window v, payload byte 16v on):
+// its strict UTF-8 check and, with SUM, the caller's sums (`acc(w, in)` for
 // every window, `in` = 0 for one past the end) in the same pass, so every
-// window is read from LDS once.  With SUM
-// the first round pair is summed and tested: if no window of the wave holds a
-// high bit, the rest is the plain sums loop (ASCII waves pay one test) and any
-// high bit it meets goes to *hib for the caller's own check (*checked stays
-// false); else the check runs from that pair to the end (*checked = true).  A
-// window's bytes before are window v - 1's last dword: lane g - 1's this
-// round, lane 15's the round before for lane 0 -- one row_ror:1 of the last
-// dword's table inputs serves both.  Rounds go in pairs, so the carry
-// alternates registers instead of being copied back.  Bytes before the payload
-// and after it count as 0, so a sequence cut by its end fails on the zero
-// dword the lane holding window V - 1 checks last.  Returns nonzero if this
-// lane saw an invalid byte; the caller ORs it over the row.  Every lane of the
-// row must run it; with SUM it sets the issue priority to 0 while it checks
-// (1 after).
-// SHORT: V may be under 17 (the varlen tiles' short payloads); without it the
-// first round pair is taken to be whole.
-template <bool SUM, bool SHORT = true, class Window, class Acc>
-__device__ __forceinline__ uint32_t utf8_check_windows_row16(uint32_t V, uint32_t g, Window win, Acc acc,
-                                                             uint32_t* hib = nullptr, bool* checked = nullptr) {
+// window is read from LDS once.  With SUM the first round pair is summed and
+// tested: if no window of the wave holds a high bit, the rest is the plain
+// sums loop (ASCII waves pay one test) and any high bit it meets goes to *hib
+// for the caller's own check (*checked stays false); else the check runs from
+// that pair to the end (*checked = true).  A window's bytes before are window
+// v - 1's last dword: lane g - 1's this round, lane GL - 1's the round before
+// for lane 0 -- at GL = 16 one row_ror:1 of the last dword's table inputs
+// serves both, below it a row_shr:1 and a row_ror:(17 - GL).  Rounds go in
+// pairs, so the carry alternates registers instead of being copied back.
+// Bytes before the payload and after it count as 0, so a sequence cut by its
+// end fails on the zero dword the lane holding window V - 1 checks last.
+// Returns nonzero if this lane saw an invalid byte; the caller ORs it over the
+// group.  Every lane of the group must run it; with SUM it sets the issue
+// priority to 0 while it checks (1 after).
+// SHORT: V may be under 2 GL + 1 (the varlen tiles' short payloads); without
+// it the first round pair is taken to be whole.
+template <bool SUM, bool SHORT = true, uint32_t GL = 16, class Window, class Acc>
+__device__ __forceinline__ uint32_t utf8_check_windows_rows(uint32_t V, uint32_t g, Window win, Acc acc,
+                                                            uint32_t* hib = nullptr, bool* checked = nullptr) {
+  static_assert(GL >= 2 && GL <= 16 && (GL & (GL - 1)) == 0, "lane groups of 2-16 lanes");
   const Utf8Pre zero = utf8_pre_zero();
   uint32_t c12 = zero.t12, c1 = zero.t1;  // lane 0's bytes before: zeros (or ASCII)
   Utf8Pre last = zero;
@@ -196,22 +198,36 @@ __device__ __forceinline__ uint32_t utf8_check_windows_row16(uint32_t V, uint32_
     Utf8Pre p1, p2, p3, p4;
     utf8_pre2(w.x, w.y, p1, p2);
     utf8_pre2(w.z, w.w, p3, p4);
-    const uint32_t r12 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p4.t12, 0x121, 0xF, 0xF, false);  // row_ror:1
-    const uint32_t r1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p4.t1, 0x121, 0xF, 0xF, false);
     Utf8Pre p0;
-    p0.t12 = g ? r12 : c12;
-    p0.t1 = g ? r1 : c1;
-    c12 = r12;
-    c1 = r1;
+    if constexpr (GL == 16) {
+      const uint32_t r12 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p4.t12, 0x121, 0xF, 0xF, false);  // row_ror:1
+      const uint32_t r1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p4.t1, 0x121, 0xF, 0xF, false);
+      p0.t12 = g ? r12 : c12;
+      p0.t1 = g ? r1 : c1;
+      c12 = r12;
+      c1 = r1;
+    } else {
+      // (every DPP read with the whole group active: a lane the read names must
+      // not be masked off by the select that follows)
+      constexpr int kRor = 0x120 + (17 - (int)GL);  // lane g = 0 <- lane GL - 1 of its group
+      const uint32_t s12 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p4.t12, 0x111, 0xF, 0xF, false);  // row_shr:1
+      const uint32_t s1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p4.t1, 0x111, 0xF, 0xF, false);
+      const uint32_t r12 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p4.t12, kRor, 0xF, 0xF, false);
+      const uint32_t r1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p4.t1, kRor, 0xF, 0xF, false);
+      p0.t12 = g ? s12 : c12;
+      p0.t1 = g ? s1 : c1;
+      c12 = r12;
+      c1 = r1;
+    }
     const uint32_t e = or3(utf8_dword_errors(p1, p0), utf8_dword_errors(p2, p1), utf8_dword_errors(p3, p2)) |
                        utf8_dword_errors(p4, p3);
     err |= in ? e : 0u;
     last = p4;
   };
-  // Rounds of 16 windows, every lane in each (a lane's window is in range
-  // whenever its predecessor's is, so what it reads across the row was computed
-  // that round; the lane holding window V - 1 is never past the end later).
-  const uint32_t rounds = (V + 15u) >> 4;
+  // Rounds of GL windows, every lane in each (a lane's window is in range
+  // whenever its predecessor's is, so what it reads across the group was
+  // computed that round; the lane holding window V - 1 is never past the end later).
+  const uint32_t rounds = (V + GL - 1u) / GL;
   uint32_t j = 0;
   if (SUM) {
     // the first round pair summed and tested for high bits: none in the wave,
@@ -219,13 +235,13 @@ __device__ __forceinline__ uint32_t utf8_check_windows_row16(uint32_t V, uint32_
     // caller's check (*hib); else the check starts with that pair
     auto hbits = [](const u32x4& w) { return or3(w.x, w.y, w.z) | w.w; };
     if (SHORT && V == 0u) return 0u;
-    const uint32_t v1 = g + 16u;
+    const uint32_t v1 = g + GL;
     const bool in0 = !SHORT || g < V, in1 = !SHORT || v1 < V;
     const u32x4 w0 = win(in0 ? g : V - 1u), w1 = win(in1 ? v1 : V - 1u);
     acc(w0, in0);
     acc(w1, in1);
     if (!__any((((in0 ? hbits(w0) : 0u) | (in1 ? hbits(w1) : 0u)) & 0x80808080u) != 0u)) {
-      for (uint32_t v = g + 32u; v < V; v += 16u) {
+      for (uint32_t v = g + 2u * GL; v < V; v += GL) {
         const u32x4 w = win(v);
         acc(w, true);
         *hib |= hbits(w);
@@ -238,8 +254,8 @@ __device__ __forceinline__ uint32_t utf8_check_windows_row16(uint32_t V, uint32_
     check(w1, in1);
     j = 2u;
   }
-  for (; j + 2u <= rounds; j += 2u) {  // the first of a pair is always in range (16 (j + 1) < V)
-    const uint32_t v = g + 16u * j, v1 = v + 16u;
+  for (; j + 2u <= rounds; j += 2u) {  // the first of a pair is always in range (GL (j + 1) < V)
+    const uint32_t v = g + GL * j, v1 = v + GL;
     const u32x4 w0 = win(v), w1 = win(v1 < V ? v1 : V - 1u);
     if (SUM) {
       acc(w0, true);
@@ -249,14 +265,20 @@ __device__ __forceinline__ uint32_t utf8_check_windows_row16(uint32_t V, uint32_
     check(w1, v1 < V);
   }
   if (j < rounds) {
-    const uint32_t v = g + 16u * j;
+    const uint32_t v = g + GL * j;
     const u32x4 w = win(v < V ? v : V - 1u);
     if (SUM) acc(w, v < V);
     check(w, v < V);
   }
-  if (V && g == ((V - 1u) & 15u)) err |= utf8_dword_errors(zero, last);  // nothing may still be expected
+  if (V && g == ((V - 1u) & (GL - 1u))) err |= utf8_dword_errors(zero, last);  // nothing may still be expected
   if (SUM) __builtin_amdgcn_s_setprio(1);
   return err;
+}
+// The 16-lane form (the tiles' MTU shapes).
+template <bool SUM, bool SHORT = true, class Window, class Acc>
+__device__ __forceinline__ uint32_t utf8_check_windows_row16(uint32_t V, uint32_t g, Window win, Acc acc,
+                                                             uint32_t* hib = nullptr, bool* checked = nullptr) {
+  return utf8_check_windows_rows<SUM, SHORT, 16>(V, g, win, acc, hib, checked);
 }
 
 // Strict UTF-8 check of one frame's payload bytes [s, fe) by G lanes (lane g
@@ -297,7 +319,7 @@ __device__ __forceinline__ uint32_t utf8_check_frame(uint64_t s, uint64_t fe, ui
       }
       last = v.w;
       // ASCII, and no lead byte (11xxxxxx) just before: nothing to check (one
-      // test, as in utf8_stream_frames)
+      // test: the chunk's high bits, OR bit 6 of the bytes before where bit 7 is set too)
       if (!(or_and(or3(v.x, v.y, v.z), v.w, 0x80808080u) |
             __builtin_amdgcn_bitop3_b32(prev >> 1, prev, 0x40404000u, 0x80))) {
         have_q = false;
@@ -317,81 +339,6 @@ __device__ __forceinline__ uint32_t utf8_check_frame(uint64_t s, uint64_t fe, ui
     }
   }
   return bad;
-}
-
-// Strict UTF-8 of `nf` back-to-back fixed-length frames (F bytes each, the
-// first H a header) staged in LDS from byte R0 on, judged by the 64 lanes of
-// one wave as ONE stream (the fixed-length decode tile: a wave's frames are
-// contiguous): lane l takes a contiguous run of the aligned 16-B chunks that
-// cover [R0, R1 = R0 + nf F] plus the chunk holding byte R1, so no lane walks
-// a frame's edges or pairs its chunks.  The caller has zeroed the frames'
-// header bytes in LDS (the wave's own frames; its leaders read their headers
-// before): a payload can then neither borrow a lead byte from the header
-// before it nor leave a sequence open into the next frame (the 0 there fails
-// as "too short", as the byte after a payload does in utf8_check_frame).
-// Bytes at and past R1 (the next wave's frames) read as 0; bytes before R0
-// (the frame before, another wave's) are judged but their errors, like those
-// at a header byte, belong to the frame before -- here frame -1, ignored --
-// and the H zeros of frame 0's header cut any sequence from them.  Errors are
-// looked up only in a chunk that has some (valid text: never): a chunk spans
-// at most two frames' bytes (F >= H + 16), so its first and last error bytes
-// name every frame it finds invalid.  Returns them as bit (frame + 1) of a
-// u64 (bit 0: frame -1); the caller ORs it over the wave.  `chunk(c)`
-// returns aligned chunk c, `dw(i)` the LDS dword i.
-template <class Chunk, class Dword>
-__device__ __forceinline__ uint64_t utf8_stream_frames(uint32_t R0, uint32_t nf, uint32_t F, uint32_t H,
-                                                       uint32_t lane, Chunk chunk, Dword dw) {
-  const uint32_t R1 = R0 + nf * F;
-  const uint32_t cA = R0 >> 4, cEnd = R1 >> 4, N = cEnd - cA + 1u;
-  const uint32_t k0 = lane * N / 64u, k1 = (lane + 1u) * N / 64u;
-  if (k0 >= k1) return 0ull;
-  uint32_t prev = cA + k0 > 0 ? dw(((cA + k0) << 2) - 1u) : 0u;
-  Utf8Pre q_last = utf8_pre(prev);
-  uint64_t bits = 0;
-  auto body = [&](uint32_t c, u32x4 v) {
-    // the chunk's last dword is the next one's "bytes before" either way: its
-    // inputs once, ahead of the branch (not again inside it)
-    Utf8Pre q3, q4;
-    utf8_pre2(v.z, v.w, q3, q4);
-    // ASCII with no lead byte (11xxxxxx) in the three bytes just before:
-    // nothing to check.  One test: the high bits of the chunk, OR bit 6 of
-    // those bytes where bit 7 is set too (a right shift, the cheap one).
-    const uint32_t hb = or_and(or3(v.x, v.y, v.z), v.w, 0x80808080u);
-    const uint32_t lead = __builtin_amdgcn_bitop3_b32(prev >> 1, prev, 0x40404000u, 0x80);  // and3
-    if (hb | lead) {
-      Utf8Pre q1, q2;
-      utf8_pre2(v.x, v.y, q1, q2);
-      const uint32_t e0 = utf8_dword_errors(q1, q_last), e1 = utf8_dword_errors(q2, q1),
-                     e2 = utf8_dword_errors(q3, q2), e3 = utf8_dword_errors(q4, q3);
-      if (or3(e0, e1, e2) | e3) {  // which frames: the first and the last error byte's
-        const uint64_t lo = (uint64_t)e0 | ((uint64_t)e1 << 32), hi = (uint64_t)e2 | ((uint64_t)e3 << 32);
-        const int bf = lo ? (int)(__builtin_ctzll(lo) >> 3) : 8 + (int)(__builtin_ctzll(hi) >> 3);
-        const int bl = hi ? 15 - (int)(__builtin_clzll(hi) >> 3) : 7 - (int)(__builtin_clzll(lo) >> 3);
-        // byte x of the stream (relative to R0) belongs to frame floor((x - H) / F)
-        const int x0 = (int)(c << 4) - (int)R0 - (int)H;
-        const int f0 = x0 + bf >= 0 ? (x0 + bf) / (int)F : -1, f1 = x0 + bl >= 0 ? (x0 + bl) / (int)F : -1;
-        bits |= (1ull << (f0 + 1)) | (1ull << (f1 + 1));
-      }
-    }
-    q_last = q4;
-    prev = v.w;
-  };
-  // two chunks an iteration: the loop-carried inputs rotate through registers
-  // once per pair instead of being copied back after every chunk
-  uint32_t k = k0;
-  for (; k + 2u < k1; k += 2u) {
-    const u32x4 v0 = chunk(cA + k), v1 = chunk(cA + k + 1u);
-    body(cA + k, v0);
-    body(cA + k + 1u, v1);
-  }
-  if (k + 1u < k1) body(cA + k, chunk(cA + k));
-  // the lane's last chunk; the next wave's bytes read as 0 (only in the chunk
-  // holding R1, the last of the last lane's run)
-  const uint32_t cl = cA + k1 - 1u;
-  u32x4 v = chunk(cl);
-  if (cl == cEnd) v = keep_bytes(v, 0, (int)(R1 & 15u));
-  body(cl, v);
-  return bits;
 }
 
 // Lane g of `lanes` judges a contiguous slice of the payload bytes [s, s + len)

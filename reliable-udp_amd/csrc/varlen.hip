@@ -987,7 +987,7 @@ __device__ __forceinline__ uint32_t octet_or(uint32_t x) {
 // R4: a lane reads its payload chunks four at a time (one LDS wait per four
 // instead of one per chunk: the longest frame's chain of LDS round trips is
 // what a wave of ragged lengths waits for).
-// FUSE (U8, 16 lanes a frame, chunk sums; launch_decode_varlen_t picks it): a
+// FUSE (U8, 2-16 lanes a frame, chunk sums; launch_decode_varlen_t picks it): a
 // frame's payload chunks are summed and UTF-8 checked in one pass when the
 // first two chunk rounds of the wave hold a high bit.  Its own instantiation,
 // so the other forms keep the code they were measured with.
@@ -1115,21 +1115,23 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
       // bit, UTF-8 checked in the same pass (utf8_device.hpp: the bytes before
       // a chunk handed across the DPP row; bytes outside the payload are 0)
       const uint32_t c0 = ps >> 4, c1 = (fe - 1u) >> 4;
-      u8bad_f = utf8_check_windows_row16<true>(
-          c1 - c0 + 1u, g2,
-          [&](uint32_t v) {
-            const uint32_t c = c0 + v;
-            u32x4 w = img16[c];
-            if (c == c0 || c == c1) w = keep_bytes(w, (int)ps - (int)(c << 4), (int)fe - (int)(c << 4));
-            return w;
-          },
-          [&](const u32x4& w, bool in) {
-            const uint32_t e = even_bytes_acc(w.w, even_bytes_acc(w.z, even_bytes_acc(w.y, even_bytes_acc(w.x, 0u))));
-            const uint32_t o = odd_bytes_acc(w.w, odd_bytes_acc(w.z, odd_bytes_acc(w.y, odd_bytes_acc(w.x, 0u))));
-            even_sum += in ? e : 0u;
-            odd_sum += in ? o : 0u;
-          },
-          &hib, &fused);
+      auto chunk = [&](uint32_t v) {
+        const uint32_t c = c0 + v;
+        u32x4 w = img16[c];
+        if (c == c0 || c == c1) w = keep_bytes(w, (int)ps - (int)(c << 4), (int)fe - (int)(c << 4));
+        return w;
+      };
+      auto sums = [&](const u32x4& w, bool in) {
+        const uint32_t e = even_bytes_acc(w.w, even_bytes_acc(w.z, even_bytes_acc(w.y, even_bytes_acc(w.x, 0u))));
+        const uint32_t o = odd_bytes_acc(w.w, odd_bytes_acc(w.z, odd_bytes_acc(w.y, odd_bytes_acc(w.x, 0u))));
+        even_sum += in ? e : 0u;
+        odd_sum += in ? o : 0u;
+      };
+      const uint32_t nc = c1 - c0 + 1u;
+      u8bad_f = G2 == 16u ? utf8_check_windows_rows<true, true, 16>(nc, g2, chunk, sums, &hib, &fused)
+                : G2 == 8u ? utf8_check_windows_rows<true, true, 8>(nc, g2, chunk, sums, &hib, &fused)
+                : G2 == 4u ? utf8_check_windows_rows<true, true, 4>(nc, g2, chunk, sums, &hib, &fused)
+                           : utf8_check_windows_rows<true, true, 2>(nc, g2, chunk, sums, &hib, &fused);
     } else if (blk && fe > ps) {
       // the 16 chunks of the blocks holding the payload's first and last bytes
       // (each masked to the payload), then the block words between
@@ -1185,16 +1187,21 @@ __global__ void __launch_bounds__(NT) decode_varlen_tile_kernel(VarlenArgs a) {
       } else if (__any((hib & 0x80808080u) != 0)) {
         if (hib & 0x80808080u) {
           const uint32_t* idw = reinterpret_cast<const uint32_t*>(img);  // kVTGuard bytes before it
-          if (G2 == 16u) {
-            // 16 lanes a frame: over payload-aligned windows, the bytes before a
-            // window handed across the DPP row (utf8_device.hpp); the last window
-            // masked to the payload (the run's budget has 32 B past its end)
+          if (G2 >= 2u && G2 <= 16u) {
+            // 2-16 lanes a frame: over payload-aligned windows, the bytes before a
+            // window handed across the lane group by DPP (utf8_device.hpp); the
+            // last window masked to the payload (the run's budget has 32 B past its end)
             const uint32_t L = fe - ps, V = (L + 15u) >> 4;
-            u8bad = utf8_check_windows_row16<false>(V, g2, [&](uint32_t v) {
+            auto win = [&](uint32_t v) {
               u32x4 w = window16_dw(idw, ps + 16u * v);
               if (16u * v + 16u > L) w = keep_bytes(w, 0, (int)(L - 16u * v));
               return w;
-            }, [](const u32x4&, bool) {});
+            };
+            auto none = [](const u32x4&, bool) {};
+            u8bad = G2 == 16u  ? utf8_check_windows_rows<false, true, 16>(V, g2, win, none)
+                    : G2 == 8u ? utf8_check_windows_rows<false, true, 8>(V, g2, win, none)
+                    : G2 == 4u ? utf8_check_windows_rows<false, true, 4>(V, g2, win, none)
+                               : utf8_check_windows_rows<false, true, 2>(V, g2, win, none);
           } else {
             u8bad = utf8_check_frame(ps, fe, g2, G2, [&](uint64_t c) { return img16[c]; },
                                      [&](uint64_t x) { return idw[(int64_t)(x >> 2) - 1]; });
@@ -2526,9 +2533,9 @@ static int launch_decode_varlen_t(const VarlenArgs& args, hipStream_t stream) {
       }
       }
 #endif
-      // 16 lanes a frame with the UTF-8 check: sums and check in one pass
+      // 2-16 lanes a frame with the UTF-8 check: sums and check in one pass
       // (profiles/r06/sweeps/varlen_utf8_fused_ab.json)
-      if (U8 && args.glog == 4u && args.tile_sums != 2u)
+      if (U8 && args.glog >= 1u && args.glog <= 4u && args.tile_sums != 2u)
         hipLaunchKernelGGL((decode_varlen_tile_kernel<H, U8, kBlock, false, FX, true>), dim3((uint32_t)blocks),
                            dim3(kBlock), lds, stream, args);
       else
