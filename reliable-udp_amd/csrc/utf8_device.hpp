@@ -281,6 +281,46 @@ __device__ __forceinline__ uint32_t utf8_check_windows_row16(uint32_t V, uint32_
   return utf8_check_windows_rows<SUM, SHORT, 16>(V, g, win, acc, hib, checked);
 }
 
+// Strict UTF-8 of one payload of L bytes by a lane group of GL lanes, with
+// nothing else to do on its bytes (the validation kernels): `win(v)` returns
+// the payload-aligned window v (any LDS alignment; the last one is masked
+// here).  The first round pair is tested for high bits (utf8_check_windows_rows
+// with SUM and no sums): with one in the wave the check runs from there;
+// without, the rest is read for high bits alone, and a frame that shows one
+// is checked over all its windows.  Nonzero if this lane saw an invalid byte;
+// every lane of the group must run it.
+template <uint32_t GL, class Window>
+__device__ __forceinline__ uint32_t utf8_check_payload_rows(uint32_t L, uint32_t g, Window raw) {
+  const uint32_t V = (L + 15u) >> 4;
+  auto win = [&](uint32_t v) {
+    u32x4 w = raw(v);
+    if (16u * v + 16u > L) w = keep_bytes(w, 0, (int)(L - 16u * v));
+    return w;
+  };
+  auto none = [](const u32x4&, bool) {};
+  uint32_t hib = 0;
+  bool checked = false;
+  uint32_t bad = utf8_check_windows_rows<true, true, GL>(V, g, win, none, &hib, &checked);
+  if (!checked) {
+    hib = group_or_rows(hib, GL);
+    if (__any((hib & 0x80808080u) != 0u) && (hib & 0x80808080u)) {
+      __builtin_amdgcn_s_setprio(0);
+      bad = utf8_check_windows_rows<false, true, GL>(V, g, win, none);
+      __builtin_amdgcn_s_setprio(1);
+    }
+  }
+  return bad;
+}
+// The same at a run-time group size: 2-16 lanes (`ok` false for any other G,
+// which the caller checks its own way).
+template <class Window>
+__device__ __forceinline__ uint32_t utf8_check_payload_group(uint32_t L, uint32_t g, uint32_t G, Window raw) {
+  return G == 16u  ? utf8_check_payload_rows<16>(L, g, raw)
+         : G == 8u ? utf8_check_payload_rows<8>(L, g, raw)
+         : G == 4u ? utf8_check_payload_rows<4>(L, g, raw)
+                   : utf8_check_payload_rows<2>(L, g, raw);
+}
+
 // Strict UTF-8 check of one frame's payload bytes [s, fe) by G lanes (lane g
 // takes aligned chunk pairs from c_lo + 2g, every 2G): `chunk(c)` returns aligned chunk c
 // and `prev(x)` the dword of bytes x-4 .. x-1 (x a multiple of 16; only bytes

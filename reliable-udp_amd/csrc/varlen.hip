@@ -1621,9 +1621,12 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_tile_kernel(Utf8Args a) 
   uint32_t bad = 0;
   if (q < Tv) {
     const uint32_t* dw = reinterpret_cast<const uint32_t*>(lds + 16);
-    bad = utf8_check_frame(q * F + H, q * F + F, g, G,  // payload bytes [s, fe) of the tile
-                           [&](uint64_t c) { return tile[c]; },
-                           [&](uint64_t x) { return dw[(x >> 2) - 1u]; });  // x = 0 reads the guard
+    if (G >= 2u && G <= 16u)  // over payload-aligned windows, the bytes before handed on by DPP
+      bad = utf8_check_payload_group(F - H, g, G, [&](uint32_t v) { return window16_dw(dw, q * F + H + 16u * v); });
+    else
+      bad = utf8_check_frame(q * F + H, q * F + F, g, G,  // payload bytes [s, fe) of the tile
+                             [&](uint64_t c) { return tile[c]; },
+                             [&](uint64_t x) { return dw[(x >> 2) - 1u]; });  // x = 0 reads the guard
   }
   for (uint32_t m = G >> 1; m > 0; m >>= 1) bad |= __shfl_xor(bad, (int)m, 64);
   if (g == 0 && q < Tv) a.valid[p0 + q] = bad ? 0 : 1;
@@ -1674,9 +1677,14 @@ __global__ void __launch_bounds__(kBlock) validate_utf8_vtile_kernel(Utf8Args a)
     __syncthreads();
     if (q < Tv) {
       const uint32_t* dw = reinterpret_cast<const uint32_t*>(lds + img_off);
-      bad = utf8_check_frame((uint64_t)lds_fo[q] + a.H, lds_fo[q + 1], g, G,
-                             [&](uint64_t c) { return img[c]; },
-                             [&](uint64_t x) { return dw[(x >> 2) - 1u]; });  // x = 0 reads the guard
+      const uint32_t ps = lds_fo[q] + a.H, fe = lds_fo[q + 1];
+      if (G >= 2u && G <= 16u)  // over payload-aligned windows, the bytes before handed on by DPP
+        bad = utf8_check_payload_group(fe > ps ? fe - ps : 0u, g, G,
+                                       [&](uint32_t v) { return window16_dw(dw, ps + 16u * v); });
+      else
+        bad = utf8_check_frame((uint64_t)ps, fe, g, G,
+                               [&](uint64_t c) { return img[c]; },
+                               [&](uint64_t x) { return dw[(x >> 2) - 1u]; });  // x = 0 reads the guard
     }
   }
   for (uint32_t m = G >> 1; m > 0; m >>= 1) bad |= __shfl_xor(bad, (int)m, 64);

@@ -532,6 +532,7 @@ def test_fused_tile_high_bits_after_an_ascii_start(cuda, L, H):
         assert np.array_equal(host(d.flags), flags)
         if copy:
             assert torch.equal(d.payload, dev(pay, cuda))
+    assert np.array_equal(host(batch.validate_utf8(fr, H)), want)
 
 
 @pytest.mark.parametrize("H", [5, 7])
@@ -573,3 +574,4 @@ def test_varlen_tile_windows_text_of_any_length(cuda, H):
         plain = _varlen_decode(d_flat, flat.size, d_off, len(frames), hint, H, False)
         for k in plain:
             assert np.array_equal(g[k], plain[k]), (hint, k)
+    assert np.array_equal(host(batch.validate_utf8(d_flat, H, frame_off=d_off)), want)
