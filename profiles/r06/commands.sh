@@ -8,3 +8,8 @@ bash tools/gpu/run.sh pmcsq p6ascii tools/run_kernel.py --op decode --utf8 --L 1
 bash tools/gpu/run.sh bench r06c
 # python3 tools/clock_spread.py gpurun_out/p6text_valu/run_counter_collection.csv --kernel decode_tile_kernel \
 #   --json profiles/r06/utf8_text_clock_spread.json
+# after the last UTF-8 kernel changes:
+bash tools/gpu/profile_legs.sh p6c decu8_1472 decu8text vdecu8_1472 vdecu8rag utf8
+bash tools/gpu/run.sh pmcsq p6ctext tools/run_kernel.py --op decode --utf8 --text --L 1472 --steps 10
+bash tools/gpu/run.sh pmcvalu p6ctext tools/run_kernel.py --op decode --utf8 --text --L 1472 --steps 60
+bash tools/gpu/run.sh bench r06e
