@@ -159,3 +159,68 @@ def test_random_text_with_corruption():
             b[rng.integers(0, len(b))] = rng.integers(0, 256)
         rows.append(bytes(b))
     check(rows)
+
+
+def window_rows_valid(payloads: list[bytes], GL: int) -> np.ndarray:
+    """utf8_check_windows_rows's round structure emulated over equal-length
+    payloads: lane g of a GL-lane group takes 16-B windows g, g + GL, ...; a
+    window's bytes before are lane g - 1's last dword of the same round, or
+    for lane 0 the carry (lane GL - 1's of the round before); a window past
+    the end is a re-read of window V - 1 whose errors do not count; the lane
+    holding window V - 1 checks a zero dword after it."""
+    L = len(payloads[0])
+    assert all(len(p) == L for p in payloads)
+    n = len(payloads)
+    V = (L + 15) // 16
+    if V == 0:
+        return np.ones(n, bool)
+    buf = np.zeros((n, V * 16), np.uint8)
+    for i, p in enumerate(payloads):
+        buf[i, :L] = np.frombuffer(p, np.uint8)
+    dw = buf.view("<u4").astype(np.uint64).reshape(n, V, 4)
+    zero = tuple(np.full(n, x, np.uint64) for x in (0x40404040, 0x01010101, 0x40404040))
+    carry = zero
+    last = [zero] * GL
+    err = np.zeros((GL, n), np.uint64)
+    for r in range((V + GL - 1) // GL):
+        p4s = []
+        for g in range(GL):
+            v = g + GL * r
+            w = dw[:, min(v, V - 1)]
+            ps = [pre(w[:, k]) for k in range(4)]
+            p0 = p4s[g - 1] if g else carry
+            e = dword_errors(ps[0], p0) | dword_errors(ps[1], ps[0]) | dword_errors(ps[2], ps[1]) | \
+                dword_errors(ps[3], ps[2])
+            if v < V:
+                err[g] |= e
+            last[g] = ps[3]
+            p4s.append(ps[3])
+        carry = p4s[GL - 1]
+    gl = (V - 1) % GL
+    err[gl] |= dword_errors(zero, last[gl])
+    return (err == 0).all(axis=0)
+
+
+def test_window_rounds_and_carries_every_group_size():
+    """The lane-group window check's rounds, carries, clamped re-reads and end
+    check (csrc/utf8_device.hpp utf8_check_windows_rows) give CPython's answer
+    for payloads of every length up to 300 B in groups of 2, 4, 8 and 16
+    lanes: multi-byte text, corrupted at a random byte, cut mid-character,
+    or ASCII."""
+    rng = np.random.default_rng(11)
+    text = ("é中😀aßЖ€𝄞" * 60).encode()
+    for L in list(range(1, 70)) + list(range(70, 301, 7)):
+        rows = []
+        for k in range(48):
+            b = bytearray(text[:L].decode("utf-8", "ignore").encode())
+            b += b"q" * (L - len(b))
+            if k % 4 == 1:
+                b[rng.integers(0, L)] = int(rng.integers(0x80, 0x100))
+            elif k % 4 == 2:
+                b[-1] = 0xE2
+            elif k % 4 == 3:
+                b = bytearray(b"x" * L)
+            rows.append(bytes(b))
+        want = np.array([cpython_valid(r) for r in rows])
+        for GL in (2, 4, 8, 16):
+            assert np.array_equal(window_rows_valid(rows, GL), want), (L, GL)
