@@ -349,11 +349,10 @@ __global__ void __launch_bounds__(kBlock) __attribute__((amdgpu_waves_per_eu(U8 
                           : utf8_check_windows_rows<false, true, 2>(V, g, win, none);
       }
       u8bad = group_or_rows(u8bad, G) ? 1u : 0u;
-    } else {
+    } else {  // one lane a frame (payloads of 16-63 B): its windows in turn
       if ((hib & 0x80808080u) && q < Tv)
-        u8bad = utf8_check_frame(q * F + H, q * F + F, g, G, [&](uint64_t c) { return tile[c]; },
-                                 [&](uint64_t x) { return x ? dw[(x >> 2) - 1u] : 0u; });
-      u8bad = group_or(u8bad, G);
+        u8bad = utf8_check_windows_rows<false, true, 1>(
+            V, g, [&](uint32_t v) { return window16_dw(dw, q * F + H + 16u * v); }, [](const u32x4&, bool) {});
     }
     __builtin_amdgcn_s_setprio(1);
   }

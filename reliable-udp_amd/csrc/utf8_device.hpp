@@ -165,7 +165,7 @@ __device__ __forceinline__ uint32_t utf8_dword_errors(const Utf8Pre& c, const Ut
 }
 
 // One payload of V 16-byte windows by the GL lanes of a lane group (GL a
-// power of two, 2..16, the groups aligned within the 16-lane DPP rows; lane
+// power of two, 1..16, the groups aligned within the 16-lane DPP rows; lane
 // g: windows g, g + GL, ...; `win(v)` returns window v, payload byte 16v on):
 // its strict UTF-8 check and, with SUM, the caller's sums (`acc(w, in)` for
 // every window, `in` = 0 for one past the end) in the same pass, so every
@@ -188,7 +188,7 @@ __device__ __forceinline__ uint32_t utf8_dword_errors(const Utf8Pre& c, const Ut
 template <bool SUM, bool SHORT = true, uint32_t GL = 16, class Window, class Acc>
 __device__ __forceinline__ uint32_t utf8_check_windows_rows(uint32_t V, uint32_t g, Window win, Acc acc,
                                                             uint32_t* hib = nullptr, bool* checked = nullptr) {
-  static_assert(GL >= 2 && GL <= 16 && (GL & (GL - 1)) == 0, "lane groups of 2-16 lanes");
+  static_assert(GL >= 1 && GL <= 16 && (GL & (GL - 1)) == 0, "lane groups of 1-16 lanes");
   const Utf8Pre zero = utf8_pre_zero();
   uint32_t c12 = zero.t12, c1 = zero.t1;  // lane 0's bytes before: zeros (or ASCII)
   Utf8Pre last = zero;
@@ -199,7 +199,12 @@ __device__ __forceinline__ uint32_t utf8_check_windows_rows(uint32_t V, uint32_t
     utf8_pre2(w.x, w.y, p1, p2);
     utf8_pre2(w.z, w.w, p3, p4);
     Utf8Pre p0;
-    if constexpr (GL == 16) {
+    if constexpr (GL == 1) {  // one lane a frame: the lane's own previous window
+      p0.t12 = c12;
+      p0.t1 = c1;
+      c12 = p4.t12;
+      c1 = p4.t1;
+    } else if constexpr (GL == 16) {
       const uint32_t r12 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p4.t12, 0x121, 0xF, 0xF, false);  // row_ror:1
       const uint32_t r1 = (uint32_t)__builtin_amdgcn_mov_dpp((int)p4.t1, 0x121, 0xF, 0xF, false);
       p0.t12 = g ? r12 : c12;

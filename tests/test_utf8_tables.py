@@ -204,7 +204,7 @@ def window_rows_valid(payloads: list[bytes], GL: int) -> np.ndarray:
 def test_window_rounds_and_carries_every_group_size():
     """The lane-group window check's rounds, carries, clamped re-reads and end
     check (csrc/utf8_device.hpp utf8_check_windows_rows) give CPython's answer
-    for payloads of every length up to 300 B in groups of 2, 4, 8 and 16
+    for payloads of every length up to 300 B in groups of 1, 2, 4, 8 and 16
     lanes: multi-byte text, corrupted at a random byte, cut mid-character,
     or ASCII."""
     rng = np.random.default_rng(11)
@@ -222,5 +222,5 @@ def test_window_rounds_and_carries_every_group_size():
                 b = bytearray(b"x" * L)
             rows.append(bytes(b))
         want = np.array([cpython_valid(r) for r in rows])
-        for GL in (2, 4, 8, 16):
+        for GL in (1, 2, 4, 8, 16):
             assert np.array_equal(window_rows_valid(rows, GL), want), (L, GL)
