@@ -866,7 +866,8 @@ __device__ __forceinline__ void decode_varlen_finish(const VarlenArgs& a, uint64
 // same answer.
 // U8: the payload's strict UTF-8 check in the same pass: the (masked) payload
 // words' high bits are OR'ed as they are summed, and only a frame that holds
-// one runs the byte checks (utf8_check_frame, its chunks again, from L2).
+// one runs the byte checks (its chunks again, from L2, in lane groups:
+// utf8_check_windows_rows).
 template <int H, bool U8, int PL = 0, bool FX = false>
 __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_t p, bool valid, uint32_t g,
                                                     uint32_t glog) {
@@ -923,11 +924,32 @@ __device__ __forceinline__ void decode_varlen_frame(const VarlenArgs& a, uint64_
   if (U8) hib = group_or_rows(hib, G);
   uint32_t u8bad = 0;
   if (U8 && __any((hib & 0x80808080u) != 0)) {  // the byte checks, for frames with a high bit
-    if ((hib & 0x80808080u) && valid && !bad)
-      u8bad = utf8_check_frame(ps, fend, g, G, [&](uint64_t c) { return load16_guarded(a.frames, c << 4, total); },
-                               [&](uint64_t x) {
-                                 return x >= 4 ? *reinterpret_cast<const uint32_t*>(a.frames + x - 4) : 0u;
-                               });
+    if ((hib & 0x80808080u) && valid && !bad && fend > ps) {
+      if (PL == 0 && G >= 2u && G <= 16u) {
+        // the payload's aligned chunks again (from L2), the edge ones masked to
+        // it, in lane groups: the bytes before a chunk handed on by DPP (the
+        // vector kernel's form; the tiles' over-budget frames keep the
+        // chunk-pair check, so the tile kernels' code stays as measured)
+        const uint64_t c0 = ps >> 4, c1 = (fend - 1u) >> 4;
+        auto chunk = [&](uint32_t v) {
+          const uint64_t cb = (c0 + v) << 4;
+          u32x4 w = load16_guarded(a.frames, cb, total);
+          if (v == 0u || c0 + v == c1) w = keep_bytes(w, (int)((int64_t)ps - (int64_t)cb), (int)((int64_t)fend - (int64_t)cb));
+          return w;
+        };
+        auto none = [](const u32x4&, bool) {};
+        const uint32_t nc = (uint32_t)(c1 - c0 + 1u);
+        u8bad = G == 16u  ? utf8_check_windows_rows<false, true, 16>(nc, g, chunk, none)
+                : G == 8u ? utf8_check_windows_rows<false, true, 8>(nc, g, chunk, none)
+                : G == 4u ? utf8_check_windows_rows<false, true, 4>(nc, g, chunk, none)
+                          : utf8_check_windows_rows<false, true, 2>(nc, g, chunk, none);
+      } else {
+        u8bad = utf8_check_frame(ps, fend, g, G, [&](uint64_t c) { return load16_guarded(a.frames, c << 4, total); },
+                                 [&](uint64_t x) {
+                                   return x >= 4 ? *reinterpret_cast<const uint32_t*>(a.frames + x - 4) : 0u;
+                                 });
+      }
+    }
     u8bad = group_or(u8bad, G);
   }
   const int src = (int)((tid & 63u) + 1u);
