@@ -1221,6 +1221,45 @@ int rudp_encode_varlen_host(const rudp_batch* h_in, uint64_t payload_bytes, uint
     return fail(RUDP_EINVAL, "rudp_encode_varlen_host: NULL buffer for a non-empty batch");
   if (n > 0x7FFFFFFFull) return fail(RUDP_EINVAL, "rudp_encode_varlen_host: at most 2^31-1 packets per call");
   const uint64_t H = (uint64_t)layout;
+  // Zero copy: packed payloads of small frames (mean under varlen_small bytes)
+  // in pinned host memory, every array pinned, payload and frames 16-B aligned:
+  // ONE checked encode over the whole batch whose kernels read the lengths,
+  // header table and payloads over PCIe and store frames, offsets and checksums
+  // back over it.  No host pass over the lengths: the device's own checks
+  // (lengths, their sum against payload_bytes, the frames' capacity) come back
+  // as its status word, with the messages the host checks give.
+  if (tuning().host_zero_copy && tuning().varlen_small > 0 && payload_bytes / n < (uint64_t)tuning().varlen_small &&
+      h_in->payload && aligned16(h_in->payload) && aligned16(h_frames) && device_writable_host(h_in->payload) &&
+      device_writable_host(h_in->len) && device_writable_host(h_in->seq) && device_writable_host(h_in->ack) &&
+      device_writable_host(h_in->flags) && device_writable_host(h_frames) && device_writable_host(h_frame_off) &&
+      device_writable_host(h_csum_or_null)) {
+    DeviceScope dev_scope;
+    int rc = dev_scope.set(device);
+    if (rc) return rc;
+    Pipeline* pp = pipeline_for(device);
+    std::lock_guard<std::mutex> lk(pp->mu);
+    if ((rc = pipeline_init(pp))) return rc;
+    rudp_batch b = *h_in;
+    b.payload_len = (uint32_t)(payload_bytes / n);  // the batch's mean: picks the tiles and the length codes
+    rc = rudp_encode_varlen_checked(&b, payload_bytes, h_frames, frames_cap, h_frame_off, h_csum_or_null,
+                                    pp->d_status, layout, device, pp->comp);
+    if (!rc) {
+      RUDP_HIP(hipMemcpyAsync(pp->h_status, pp->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost, pp->comp));
+    }
+    const hipError_t e = hipStreamSynchronize(pp->comp);
+    if (rc) return rc;
+    if (e != hipSuccess) return hip_fail(e, "zero-copy varlen encode");
+    const uint32_t st = *pp->h_status;
+    if (st & RUDP_ST_LEN) return fail(RUDP_EINVAL, "lengths must lie in [0, 65535]");
+    if (st & RUDP_ST_PAYLOAD)
+      return fail(RUDP_EINVAL, "packed payloads: sum(lengths) must equal payload.numel() (%llu)",
+                  (unsigned long long)payload_bytes);
+    if (st & RUDP_ST_FRAMES_CAP)
+      return fail(RUDP_EINVAL, "out is too small for the frames (sum(lengths) + N * header bytes > %llu)",
+                  (unsigned long long)frames_cap);
+    if (st) return fail(RUDP_EINVAL, "rudp_encode_varlen_host: the device rejected the batch (status 0x%x)", st);
+    return 0;
+  }
   const uint64_t bmax = stage_bytes();
   const uint64_t hint = h_in->payload_len ? h_in->payload_len : 1u;
   uint64_t cn = chunk_packets(n, 2u * hint + H + 13u);
@@ -1257,34 +1296,6 @@ int rudp_encode_varlen_host(const rudp_batch* h_in, uint64_t payload_bytes, uint
   DeviceScope dev_scope;
   int rc = dev_scope.set(device);
   if (rc) return rc;
-  // Zero copy: packed payloads of small frames (mean under varlen_small bytes)
-  // in pinned host memory, every array pinned, payload and frames 16-B aligned:
-  // ONE checked encode over the whole batch whose kernels read the lengths,
-  // header table and payloads over PCIe and store frames, offsets and checksums
-  // back over it (the host pre-pass above has checked the batch; the device's
-  // own status is read back as well).
-  if (tuning().host_zero_copy && tuning().varlen_small > 0 && total / n < (uint64_t)tuning().varlen_small &&
-      h_in->payload && aligned16(h_in->payload) && aligned16(h_frames) && device_writable_host(h_in->payload) &&
-      device_writable_host(h_in->len) && device_writable_host(h_in->seq) && device_writable_host(h_in->ack) &&
-      device_writable_host(h_in->flags) && device_writable_host(h_frames) && device_writable_host(h_frame_off) &&
-      device_writable_host(h_csum_or_null)) {
-    Pipeline* pp = pipeline_for(device);
-    std::lock_guard<std::mutex> lk(pp->mu);
-    if ((rc = pipeline_init(pp))) return rc;
-    rudp_batch b = *h_in;
-    b.payload_len = (uint32_t)(total / n);  // the batch's mean: picks the tiles and the length codes
-    rc = rudp_encode_varlen_checked(&b, total, h_frames, frames_cap, h_frame_off, h_csum_or_null, pp->d_status, layout,
-                                    device, pp->comp);
-    if (!rc) {
-      RUDP_HIP(hipMemcpyAsync(pp->h_status, pp->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost, pp->comp));
-    }
-    const hipError_t e = hipStreamSynchronize(pp->comp);
-    if (rc) return rc;
-    if (e != hipSuccess) return hip_fail(e, "zero-copy varlen encode");
-    if (*pp->h_status)
-      return fail(RUDP_EINVAL, "rudp_encode_varlen_host: the device rejected the batch (status 0x%x)", *pp->h_status);
-    return 0;
-  }
   // Pinned offset / checksum arrays: for chunks that take the small-frame tile
   // (its checksums leave as coalesced stores) the kernels store them directly,
   // two D2H copies per chunk fewer; the frames always come back by one copy.

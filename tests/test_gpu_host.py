@@ -423,3 +423,40 @@ def test_varlen_host_zero_copy_pinned_batches(cuda, zero_copy):
         assert np.array_equal(got[k], want[k]), (k, zero_copy)
     assert got["ok"][999] == 4 and got["ok"][1000] == 0 and got["ok"][4999] == 4 and got["ok"][5000] == 4
     assert (np.delete(got["ok"], [999, 1000, 4999, 5000]) == 1).all()
+
+
+def test_varlen_host_zero_copy_rejects(cuda):
+    """The zero-copy encode makes no host pass over the lengths: the device's
+    checked encode judges the batch and its status comes back as the host
+    checks' ValueErrors (a length over 65535, a sum that is not the payload's
+    size, a frame buffer too small), with no frame byte written."""
+    n, H = 100003, 5
+    z16, z8 = _pinned(np.zeros(n, np.uint16)), _pinned(np.zeros(n, np.uint8))
+    tab = (z16, z16, z8)
+    cases = []
+    big = np.ones(n, np.int32)
+    big[n // 2] = 70000
+    cases.append(("65535", big, int(big.sum()), int(big.sum()) + n * H))
+    ones = np.ones(n, np.int32)
+    cases.append(("sum", ones, n + 5, n + 5 + n * H))
+    cases.append(("sum", ones, n - 5, n - 5 + n * H))
+    cases.append(("too small", ones, n, n + n * H - 16))
+    with _Knobs() as lib:
+        old = lib.rudpx_tune(75, 1)
+        try:
+            for msg, lens, pb, cap in cases:
+                out = _pinned(np.full(cap + 64, 0xAB, np.uint8))[:cap]
+                with pytest.raises(ValueError, match=msg):
+                    batch.pack_batch_varlen(tab, _pinned(np.zeros(pb + 16, np.uint8))[:pb], _pinned(lens), H,
+                                            want_csum=True, out=out)
+                assert (out == 0xAB).all(), msg
+            # and a good batch through the same arrays after the refusals
+            pay = _pinned(np.arange(n, dtype=np.uint8))
+            out = _pinned(np.zeros(n + n * H + 64, np.uint8))[:n + n * H]
+            r = batch.pack_batch_varlen(tab, pay, _pinned(ones), H, want_csum=True, out=out)
+        finally:
+            lib.rudpx_tune(75, old)
+    want_fr, want_off, want_cs = _oracle_varlen(np.zeros(n, np.uint16), np.zeros(n, np.uint16), np.zeros(n, np.uint8),
+                                                ones, np.arange(n, dtype=np.uint8), H)
+    assert np.array_equal(r.frames, want_fr) and np.array_equal(r.frame_off, want_off)
+    assert np.array_equal(r.csum, want_cs)
