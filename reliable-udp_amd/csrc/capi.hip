@@ -1419,13 +1419,18 @@ int rudp_decode_varlen_host(const uint8_t* h_frames, uint64_t frames_bytes, cons
     Pipeline* pp = pipeline_for(device);
     std::lock_guard<std::mutex> lk(pp->mu);
     if ((rc = pipeline_init(pp))) return rc;
+    // (the rejected-offsets status from the kernels' own flag word, 4 bytes
+    // back, not a host scan of ok[]: 1 MiB of pinned memory per 1M frames)
+    if (h_status_or_null) RUDP_HIP(hipMemsetAsync(pp->d_status, 0, sizeof(uint32_t), pp->comp));
     rc = decode_varlen(h_frames, h_frame_off, (uint32_t)(hint < 0xFFFFFFFFull ? hint : 0xFFFFFFFFu), n,
                        h_csum_in_or_null, h_seq, h_ack, h_flags, h_ok, h_csum_out_or_null, nullptr, layout, device,
-                       pp->comp, true, nullptr, frames_bytes, h_valid_or_null);
+                       pp->comp, true, h_status_or_null ? pp->d_status : nullptr, frames_bytes, h_valid_or_null);
+    if (!rc && h_status_or_null)
+      RUDP_HIP(hipMemcpyAsync(pp->h_status, pp->d_status, sizeof(uint32_t), hipMemcpyDeviceToHost, pp->comp));
     const hipError_t e = hipStreamSynchronize(pp->comp);
     if (rc) return rc;
     if (e != hipSuccess) return hip_fail(e, "zero-copy varlen decode");
-    if (h_status_or_null && memchr(h_ok, RUDP_OK_BAD_OFFSETS, n)) *h_status_or_null = RUDP_ST_OFFSETS;
+    if (h_status_or_null) *h_status_or_null = *pp->h_status & RUDP_ST_OFFSETS;
     return 0;
   }
   // Pinned output arrays: the small-frame decode tile (the reference's 6-9 B

@@ -416,6 +416,10 @@ def test_varlen_host_zero_copy_pinned_batches(cuda, zero_copy):
             assert np.array_equal(r.csum, want_cs)
             d = batch.unpack_batch_varlen(r.frames, p_off, H, csum=_pinned(want_cs), utf8=True, check=False)
             got = _host_fields(d)
+            assert int(np.asarray(d.status)[0]) == 8  # RUDP_ST_OFFSETS: rejected frames in the batch
+            clean = batch.unpack_batch_varlen(r.frames, _pinned(want_off), H, csum=_pinned(want_cs), utf8=True,
+                                              check=False)
+            assert int(np.asarray(clean.status)[0]) == 0 and (clean.ok == 1).all()
         finally:
             lib.rudpx_tune(75, old)
     want = _device_varlen(cuda, want_fr, off, H, want_cs)
