@@ -13,3 +13,7 @@ bash tools/gpu/profile_legs.sh p6c decu8_1472 decu8text vdecu8_1472 vdecu8rag ut
 bash tools/gpu/run.sh pmcsq p6ctext tools/run_kernel.py --op decode --utf8 --text --L 1472 --steps 10
 bash tools/gpu/run.sh pmcvalu p6ctext tools/run_kernel.py --op decode --utf8 --text --L 1472 --steps 60
 bash tools/gpu/run.sh bench r06e
+# host zero-copy A/Bs (old library via RUDP_LIB, alternating processes):
+#   python -u tools/e2e_varlen_leg.py --reps 9   -> profiles/r06/sweeps/host_zero_copy_*_ab.json
+# round end on the final tree:
+bash tools/gpu/run.sh tests && bash tools/gpu/run.sh smoke && bash tools/gpu/run.sh bench r06g
