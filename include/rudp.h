@@ -397,8 +397,12 @@ RUDP_API int rudp_udp_send_batch_to(int fd, const uint8_t* h_frames, const uint6
  *   h_frame_off receives n + 1 offsets (the exclusive scan of len[i] +
  *   layout).  Every length (<= 65535), sum(len) == payload_bytes (the size
  *   of h_in->payload) and frames_cap (>= sum(len) + n * layout) are checked
- *   before any work is enqueued: a bad batch returns RUDP_EINVAL and writes
- *   nothing.
+ *   before any frame byte is written: a bad batch returns RUDP_EINVAL and
+ *   h_frames and h_csum_or_null are untouched.  The host checks the lengths
+ *   before it enqueues any work, except for a batch of small frames (mean
+ *   payload under 16 B) whose every array is pinned: that one runs as one
+ *   checked device encode over PCIe, whose first pass makes the same checks
+ *   (h_frame_off is then left unspecified on a bad batch).
  */
 RUDP_API int rudp_encode_host(const rudp_batch* h_in, uint8_t* h_frames, uint16_t* h_csum_or_null,
                      int layout, int device);

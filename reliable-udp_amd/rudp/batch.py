@@ -570,7 +570,7 @@ class HostVarlenFrames(NamedTuple):
     """Result of ``pack_batch_varlen`` on numpy arrays (host memory, staged
     through the GPU by rudp_encode_varlen_host): frames (u8, back to back),
     frame_off (int64 [N + 1]), csum (u16 [N] or None), status (always 0: the
-    batch was checked before any work, and a bad one raised)."""
+    batch was checked before any frame byte was written, and a bad one raised)."""
     frames: Any
     frame_off: Any
     csum: Any
@@ -595,7 +595,7 @@ def _pack_varlen_host(tab: HeaderTable, payload, lengths, H, payload_off, want_c
         if a.shape[0] != n:
             raise ValueError(f"{name} has {a.shape[0]} entries for {n} packets")
     # (the lengths, their sum against the payload and the capacity are checked by the
-    # C entry before any work: a bad batch raises ValueError and nothing is written)
+    # C entry before any frame byte is written: a bad batch raises ValueError)
     if out is not None:
         if not isinstance(out, np.ndarray) or out.dtype != np.uint8 or out.ndim != 1 \
                 or not out.flags["C_CONTIGUOUS"] or not out.flags["WRITEABLE"]:
@@ -640,8 +640,8 @@ def pack_batch_varlen(headers, payload, lengths, layout: Union[str, int] = "rudp
 
     numpy arrays (packed payloads in host memory, a send buffer): staged
     through GPU ``device`` by rudp_encode_varlen_host, synchronously; the
-    lengths are checked before any work (ValueError) and the result is a
-    ``HostVarlenFrames`` of numpy arrays.
+    lengths are checked before any frame byte is written (ValueError) and the
+    result is a ``HostVarlenFrames`` of numpy arrays.
     """
     H = layout_header_len(layout)
     tab = _as_table(headers)
